@@ -1,0 +1,186 @@
+"""Generate golden fixtures by running the REFERENCE (/root/reference) on CPU.
+
+Run in the build container only (the reference never travels to the GPU box):
+
+    python tests/golden/make_golden.py [case ...]
+
+Each case writes ``tests/golden/<case>.npz`` holding
+* the inputs: net config, weights (``p:<state_dict key>``), optional lattice size;
+* the reference's outputs: skeleton (V0, E0) for skeleton cases, per-step
+  (idx, V, E) counts and SHA-256 of (vertices, edges int64, cache) after every
+  ``subpoly_`` call, the final surface vertices, ``faces_with_indices`` and
+  float ``faces``.
+
+Rules: argsort forced stable; the tinycudann stub is the
+oracle's encoding (oracle/encoding.py); weights come from numpy PCG64
+(tropical/synthetic.py) or from a short CPU fit of the oracle net to an
+analytic SDF (weights are stored, so the fit itself needs no determinism).
+"""
+from __future__ import annotations
+
+import hashlib
+import importlib.util
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+sys.path.insert(0, REPO)
+
+_spec = importlib.util.spec_from_file_location(
+    "_synthetic", os.path.join(REPO, "tropical-nerf.pytorch_amd", "tropical", "synthetic.py"))
+syn = importlib.util.module_from_spec(_spec)
+_spec.loader.exec_module(syn)
+
+FULL_MAX_TRI = 20_000
+SMALL = dict(num_layers=3, num_hidden=16, levels=4, r_min=2, r_max=32, T=19)
+LARGE = dict(num_layers=3, num_hidden=16, levels=4, r_min=8, r_max=128, T=19)
+
+
+def sha(*arrays) -> str:
+    h = hashlib.sha256()
+    for a in arrays:
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()
+
+
+def fit_sdf(cfg, fn, seed, iters=1000, batch=4096):
+    """Fit the oracle net to an analytic SDF on CPU (stand-in pretrained net)."""
+    from oracle.subdivide import RefNet, load_params
+    net = RefNet(**cfg)
+    load_params(net, syn.random_params(net.enc.module.params.numel(), net.num_nodes, seed, 1e-4))
+    opt = torch.optim.Adam(net.parameters(), lr=1e-2)
+    sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, iters)
+    g = torch.Generator().manual_seed(seed)
+    for it in range(iters):
+        x = torch.rand(batch, 3, generator=g) * 2.0 - 1.0
+        loss = (net.sdf(x)[:, 0] - torch.tanh(fn(x))).abs().mean()
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        sched.step()
+    print(f"  fit loss {loss.item():.5f}")
+    return {k: v.detach().numpy().copy() for k, v in net.state_dict().items()}
+
+
+def sphere(x):
+    return x.norm(dim=-1) - 0.6
+
+
+def torus(x):
+    q = torch.stack([torch.sqrt(x[:, 0] ** 2 + x[:, 1] ** 2) - 0.5, x[:, 2]], -1)
+    return q.norm(dim=-1) - 0.2
+
+
+CASES = {
+    # name: (kind, cfg, weights, extra)
+    "synth24": ("lattice", None, ("rand", 1, 0.1), 24),
+    "synth32": ("lattice", None, ("rand", 2, 0.1), 32),
+    "synth32u": ("lattice", None, ("rand_uncentered", 0, 0.1), 32),
+    "small_sphere": ("subpoly", SMALL, ("fit", sphere, 7), None),
+    "small_torus": ("subpoly", SMALL, ("fit", torus, 11), None),
+    "small_rand": ("subpoly", SMALL, ("rand", 5, 0.05), None),
+}
+
+
+def build_params(cfg, spec, net):
+    if spec[0] == "rand_uncentered":
+        return syn.random_params(net.enc.module.params.numel(), net.num_nodes, spec[1], spec[2])
+    if spec[0] == "rand":
+        p = syn.random_params(net.enc.module.params.numel(), net.num_nodes, spec[1], spec[2])
+
+        def col(x):
+            net.load_state_dict({k: torch.from_numpy(v) for k, v in p.items()})
+            with torch.no_grad():
+                return net(torch.from_numpy(x), gather=True)[1][-1][:, 0].numpy()
+        return syn.center_sdf_bias(p, col, spec[1])
+    return fit_sdf(cfg, spec[1], spec[2])
+
+
+def run_case(name):
+    sp, model = __import__("ref_loader").import_reference()
+    kind, cfg, wspec, n = CASES[name]
+    if kind == "lattice":
+        cfg = syn.net_config_for_lattice(n)
+    net = model.Net(**cfg)
+    params = build_params(cfg, wspec, net)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()})
+    out = {"case": name, "kind": kind, "cfg_keys": np.array(list(cfg.keys())),
+           "cfg_vals": np.array(list(cfg.values()), dtype=np.int64),
+           "marks": net.enc.marks.numpy()}
+    for k, v in params.items():
+        out["p:" + k] = v
+
+    steps = []
+    orig = sp.subpoly_
+
+    def wrapped(vertices, edges, net_, l, h, eps, outputs_=None, **kw):
+        v, e, o = orig(vertices, edges, net_, l, h, eps, outputs_, **kw)
+        steps.append((l * net_.num_hidden + h, v.shape[0], e.shape[0],
+                      sha(v.numpy(), e.numpy().astype(np.int64), o.numpy())))
+        return v, e, o
+
+    sp.subpoly_ = wrapped
+    t0 = time.time()
+    with torch.no_grad():
+        if kind == "lattice":
+            V = torch.from_numpy(syn.lattice_vertices(net.enc.marks.numpy()))
+            E = torch.from_numpy(syn.lattice_edges(n))
+            out["lattice_n"] = n
+            o = None
+            for l in range(net.num_layers - 1):
+                for h in range(net.num_hidden):
+                    V, E, o = sp.subpoly_(V, E, net, l, h, 1e-4, o, force=True)
+            V, E, o = sp.subpoly_(V, E, net, net.num_layers - 2, net.num_hidden, 1e-4, o,
+                                  force=True)
+            out["pre_VE"] = np.array([V.shape[0], E.shape[0]])
+            Vs, Es, used = sp.extract_skeleton(V, E, net, 1e-4, o)
+            out["surf_V"] = Vs.numpy()
+            out["surf_E"] = Es.numpy()
+            faces, fwi = sp.extract_faces(Vs, Es, net, o[used], 1e-4)
+        else:
+            for m in net.modules():
+                if isinstance(m, sys.modules["tropical"].TropicalHashGrid):
+                    V0, E0 = m.skeleton(net)
+                    break
+            out["skel_V"] = V0.numpy()
+            out["skel_E"] = E0.numpy()
+            faces, Vs, fwi = sp.subpoly(net, 3, 1.2, 1e-4, force=True)
+            out["surf_V"] = Vs.numpy()
+    sp.subpoly_ = orig
+    faces = np.asarray(faces, dtype=np.float32)
+    tri = np.asarray(fwi, dtype=np.int64)
+    surf = out.pop("surf_V")
+    out["n_surf"] = np.array([surf.shape[0], tri.shape[0]])
+    out["sha_surf"] = sha(surf)
+    out["sha_tri"] = sha(tri)
+    out["sha_faces"] = sha(faces)
+    if tri.shape[0] <= FULL_MAX_TRI:   # small enough to commit in full
+        out["surf_V"], out["tri"], out["faces"] = surf, tri, faces
+    if "surf_E" in out:
+        out["sha_surf_E"] = sha(out.pop("surf_E").astype(np.int64))
+    if "skel_E" in out and out["skel_E"].shape[0] > 200_000:
+        out["sha_skel"] = sha(out.pop("skel_V"), out.pop("skel_E").astype(np.int64))
+    out["step_idx"] = np.array([s[0] for s in steps])
+    out["step_V"] = np.array([s[1] for s in steps])
+    out["step_E"] = np.array([s[2] for s in steps])
+    out["step_sha"] = np.array([s[3] for s in steps])
+    out["ref_seconds"] = time.time() - t0
+    path = os.path.join(HERE, f"{name}.npz")
+    np.savez_compressed(path, **out)
+    print(f"{name}: V_surf={out['n_surf'][0]} tris={out['n_surf'][1]} "
+          f"steps={len(steps)} {out['ref_seconds']:.1f}s -> {os.path.getsize(path)/1e3:.0f} kB")
+
+
+if __name__ == "__main__":
+    if os.environ.get("GOLDEN_TRACE"):
+        import faulthandler
+        faulthandler.dump_traceback_later(int(os.environ["GOLDEN_TRACE"]), exit=True)
+    names = sys.argv[1:] or list(CASES)
+    for nm in names:
+        run_case(nm)
