@@ -1,0 +1,169 @@
+/*
+ * tropical_hip.h -- C ABI of the MI355X (gfx950) polyhedral-complex
+ * extraction library (libtropical_hip.so).
+ *
+ * Every pointer named d_* is DEVICE memory on the engine's / caller's current
+ * HIP device; `stream` is a hipStream_t passed as void* (0 = null stream).
+ * No torch types cross this boundary.  All functions return 0 on success and
+ * -1 on failure; tnp_last_error() then describes the failure (thread-local).
+ *
+ * The reference (seonghunn/tropical-nerf.pytorch) is pure Python/PyTorch and
+ * has no FFI of its own; each entry point below names the reference
+ * function (file:line under tropical/) whose semantics it implements.  The
+ * Python host package (tropical-nerf.pytorch_amd/tropical) binds these with
+ * ctypes behind the reference's own call surface.
+ */
+#ifndef TROPICAL_HIP_H
+#define TROPICAL_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TNP_MAX_LEVELS 8
+#define TNP_ABI_VERSION 1
+
+/* Piecewise-trilinear SDF net: hash-grid encoding (tcnn Grid/Hash, 2
+ * features/level, tropical.py:32-40) + ReLU MLP (model.py:38-50).
+ * weights: fc.0.weight (H x 2L, row-major), fc.0.bias (H), fc.1.weight,
+ * fc.1.bias, ..., fc.last.weight (2 x H), fc.last.bias (2), packed in that
+ * order.  table: the flat `enc.module.params` (tcnn layout
+ * params[(offset_l + index) * 2 + f]). */
+typedef struct tnp_net {
+  int32_t n_levels;   /* L  (2 or 4 are instantiated) */
+  int32_t n_features; /* F  (must be 2) */
+  int32_t num_layers; /* 3 */
+  int32_t num_hidden; /* 16 */
+  int32_t n_marks;    /* len(TropicalHashGrid.marks) */
+  float eps;          /* Net.eps (model.py:20) */
+  float scales[TNP_MAX_LEVELS];    /* fp32 exp2(l*log2 b)*N_min - 1 */
+  int32_t res[TNP_MAX_LEVELS];     /* ceil(scale)+1 */
+  uint32_t sizes[TNP_MAX_LEVELS];  /* min(next_mult(res^3,8), 2^T) */
+  uint32_t offsets[TNP_MAX_LEVELS];
+  int32_t dense[TNP_MAX_LEVELS];   /* res^3 <= size */
+  const float* d_table;
+  const float* d_weights;
+  const float* d_marks;
+} tnp_net;
+
+/* Per-step counters (the roofline model's inputs). */
+typedef struct tnp_step_stats {
+  int32_t idx;
+  int64_t V_in, E_in, S, H, X, V_out, E_out;
+  int64_t A;      /* augmented region rows the reference would build */
+  int64_t P;      /* candidate in-region pairs the reference would build */
+  int64_t pair_tests; /* member pairs this implementation tested */
+  int32_t override_applied;
+  uint64_t next_active; /* planes > idx a kept edge would split (pruning steps) */
+} tnp_step_stats;
+
+const char* tnp_last_error(void);
+int tnp_abi_version(void);
+int tnp_device_count(int* n);
+
+/* ---- stateless net ops -------------------------------------------------- */
+
+/* Net.forward(x, gather=True)[1] concatenated (model.py:52-76): pre-
+ * activations of every hidden neuron + (o1 - o0), written PLANE-MAJOR
+ * d_pre[p * ld + i], p < K = (num_layers-1)*num_hidden + 1.  Bitwise equal
+ * to the PyTorch-CPU reference (sequential-fma MLP, non-fused encoding). */
+int tnp_forward(const tnp_net* net, const float* d_xyz, int64_t n,
+                float* d_pre, int64_t ld, float* d_out2, void* stream);
+/* d_out2 (nullable): the raw last-layer outputs [n][2] (Net.forward(x)
+ * without gather).  d_pre may be null. */
+
+/* TropicalHashGrid.forward(x) (tropical.py:46-47): x in [0,1]^3 (already
+ * preprocessed), out [n][2L] fp32 (level-major, tcnn column order). */
+int tnp_encode(const tnp_net* net, const float* d_x01, int64_t n, float* d_out,
+               void* stream);
+
+/* Net.forward(x, gather=True, group=8) (model.py:67-70): rows come in groups
+ * of 8 box corners sharing one activation pattern. */
+int tnp_forward_grouped(const tnp_net* net, const float* d_xyz, int64_t n,
+                        float* d_pre, int64_t ld, float* d_out2, void* stream);
+
+/* Net.region(v, output, eps) (model.py:90-103 + tropical.py:227-236):
+ * d_m[n x (3+K)] int64 {grid mask 0/1, plane sign -1/0/1}, d_off[n x 3]
+ * int64 offsets.  d_pre is plane-major with leading dimension ld. */
+int tnp_region(const tnp_net* net, const float* d_xyz, const float* d_pre,
+               int64_t ld, int64_t n, float eps, int64_t* d_m, int64_t* d_off,
+               void* stream);
+
+/* Net.sdf (model.py:84-88) and its input gradient (Net.normal,
+ * model.py:105-123).  d_grad may be null. */
+int tnp_sdf_grad(const tnp_net* net, const float* d_xyz, int64_t n,
+                 float* d_sdf, float* d_grad, void* stream);
+
+/* ---- stateful extraction engine ---------------------------------------- */
+
+typedef struct tnp_engine tnp_engine;
+
+int tnp_engine_create(tnp_engine** out, int device);
+void tnp_engine_destroy(tnp_engine* eng);
+int tnp_engine_set_net(tnp_engine* eng, const tnp_net* net);
+
+/* Load a complex: vertices V x 3 fp32, edges E x 2 int64 (device).  d_pre:
+ * optional cached outputs_ (V x K fp32, row-major as the reference keeps
+ * them); null computes them (subpoly.py:92-93).  keep_all_planes=1 keeps
+ * every cached column through compaction (needed to hand outputs_ back);
+ * 0 keeps only the columns later steps read. */
+int tnp_engine_load(tnp_engine* eng, const float* d_xyz, int64_t V,
+                    const int64_t* d_edges, int64_t E, const float* d_pre,
+                    int keep_all_planes, void* stream);
+
+/* TropicalHashGrid.skeleton(net, unit) with PRUNING_MODE="distance"
+ * (tropical.py:158-225) computed on the device and loaded as the complex;
+ * falls back to get_hypercube(3, size) (subpoly.py:51-52, 731-750). */
+int tnp_engine_skeleton(tnp_engine* eng, int unit, float size, void* stream,
+                        int64_t* V, int64_t* E);
+
+/* Load the full lattice over the marks restricted to the x-slab of mark
+ * indices [x0, x1] (x0=0, x1=n_marks-1: the whole N^3 lattice) in the
+ * layout of TropicalHashGrid._skeleton(..., pruning=False)
+ * (tropical.py:103-109) with vertex ids (i-x0)*N^2 + j*N + k. */
+int tnp_engine_lattice(tnp_engine* eng, int x0, int x1, int keep_all_planes,
+                       void* stream, int64_t* V, int64_t* E);
+
+/* Bit p (p >= from) set iff some edge has endpoints with non-zero opposite
+ * eps-signs on plane p, i.e. subpoly_ at idx=p would split (subpoly.py:104-110). */
+int tnp_engine_active_planes(tnp_engine* eng, int from, uint64_t* mask,
+                             void* stream);
+
+/* subpoly_ phase 1 (subpoly.py:98-117, 180-189): sign test, order-preserving
+ * split compaction, new vertices, their forward pass and the LOCAL
+ * failover-override predicate.  Writes S (local split count) and fail. */
+int tnp_engine_split(tnp_engine* eng, int idx, void* stream, int64_t* S,
+                     int32_t* fail);
+
+/* subpoly_ phase 2 (subpoly.py:189-279): apply the override if `override`
+ * (the GLOBAL predicate), connecting edges, pruning (prune=1) and vertex
+ * compaction.  Must follow tnp_engine_split on the same idx. */
+int tnp_engine_finish(tnp_engine* eng, int idx, int prune, int override,
+                      void* stream, tnp_step_stats* stats);
+
+int tnp_engine_sizes(tnp_engine* eng, int64_t* V, int64_t* E);
+
+/* Copy the complex out: d_xyz V x 3, d_edges E x 2 int64, d_pre V x K
+ * row-major (requires keep_all_planes, else may be null). */
+int tnp_engine_export(tnp_engine* eng, float* d_xyz, int64_t* d_edges,
+                      float* d_pre, void* stream);
+
+/* extract_skeleton (subpoly.py:556-581) applied in place; writes the
+ * surface sizes (0/0 when fewer than 3 surface vertices). */
+int tnp_engine_surface(tnp_engine* eng, void* stream, int64_t* V, int64_t* E);
+
+/* extract_faces (subpoly.py:584-728, geometry.py:483-556) on the current
+ * (surface) complex: n_tri = rows of faces_with_indices, n_faces = rows of
+ * the float faces (they differ only when a vertex sits exactly at the
+ * origin, which the reference's norm>0 mask drops).  Read both with
+ * tnp_engine_faces_export (d_tri n_tri x 3 int64, d_faces n_faces x 3 x 3). */
+int tnp_engine_faces(tnp_engine* eng, void* stream, int64_t* n_tri, int64_t* n_faces);
+int tnp_engine_faces_export(tnp_engine* eng, int64_t* d_tri, float* d_faces,
+                            void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TROPICAL_HIP_H */

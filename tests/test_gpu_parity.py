@@ -1,0 +1,181 @@
+"""GPU parity: the HIP path against the reference's golden fixtures and the
+oracle (bit-exact integer outputs and vertices; the north-star tolerance for
+vertex coordinates is 1e-5 abs, but the design target -- and what these
+tests require -- is bitwise equality, see DESIGN.md "Bitwise contract")."""
+import numpy as np
+import pytest
+import torch
+
+from golden_io import cases, load, sha
+from helpers import engine_steps, oracle_net, product_net
+
+pytestmark = pytest.mark.gpu
+
+VERTEX_TOL = 1e-5  # north_star: vertex coords within 1e-5 abs
+
+
+def _rand_points(n, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.rand(n, 3, generator=g) * 2 - 1
+
+
+@pytest.mark.parametrize("name", ["small_sphere", "synth32", "small_rand"])
+def test_forward_bitwise(cuda, name):
+    d = load(name)
+    net, ref = product_net(d, cuda), oracle_net(d)
+    x = _rand_points(20000, 1)
+    # include exact lattice points (grid-plane ties) and the box corners
+    mk = torch.as_tensor(d["marks"])
+    lat = torch.stack(torch.meshgrid(mk[::3], mk[::5], mk[::7], indexing="ij"), -1).reshape(-1, 3) * 2 - 1
+    x = torch.cat([x, lat, torch.tensor([[-1.0, -1, -1], [1, 1, 1]])])
+    with torch.no_grad():
+        want = torch.cat(ref(x, gather=True)[1], -1)
+        out_ref = ref(x)
+    out, pre = net(x.to(cuda), gather=True)
+    got = torch.cat(pre, -1).cpu()
+    assert torch.equal(got, want), f"max |diff| {(got - want).abs().max()}"
+    assert torch.equal(out.cpu(), out_ref)
+
+
+@pytest.mark.parametrize("n", [1, 2, 5, 15, 16, 17, 64])
+def test_forward_small_batches_bitwise(cuda, n):
+    """A call's row count selects the reference's MKL summation schedule
+    (1 row; 2..15 rows for the 2-output layer): the HIP MLP follows it."""
+    d = load("small_sphere")
+    net, ref = product_net(d, cuda), oracle_net(d)
+    x = _rand_points(n * 37, 7)
+    for c in x.split(n):
+        with torch.no_grad():
+            want = torch.cat(ref(c, gather=True)[1], -1)
+        got = torch.cat(net(c.to(cuda), gather=True)[1], -1).cpu()
+        assert torch.equal(got, want)
+
+
+def test_encoding_bitwise(cuda):
+    d = load("synth32u")
+    net, ref = product_net(d, cuda), oracle_net(d)
+    x = (_rand_points(5000, 2) + 1) / 2
+    got = net.enc(x.to(cuda)).cpu()
+    with torch.no_grad():
+        want = ref.enc(x)
+    assert torch.equal(got, want)
+
+
+@pytest.mark.parametrize("name", ["small_sphere", "synth24"])
+def test_region_and_sdf(cuda, name):
+    d = load(name)
+    net, ref = product_net(d, cuda), oracle_net(d)
+    x = _rand_points(4000, 3)
+    mk = torch.as_tensor(d["marks"])
+    x[:500, 0] = mk[torch.arange(500) % len(mk)] * 2 - 1  # on grid planes
+    m, off, _ = net.region(x.to(cuda))
+    with torch.no_grad():
+        m_ref, off_ref, _ = ref.region(x)
+        sdf_ref = ref.sdf(x)
+    assert torch.equal(m.cpu(), m_ref)
+    assert torch.equal(off.cpu(), off_ref)
+    assert (net.sdf(x.to(cuda)).cpu() - sdf_ref).abs().max() < 1e-5
+    J = net.normal(x[:64].to(cuda)).cpu()
+    J_ref = ref.normal(x[:64].clone())
+    assert (J - J_ref).abs().max() < 1e-3 * max(1.0, J_ref.abs().max().item())
+
+
+@pytest.mark.parametrize("name", cases("lattice"))
+def test_lattice_steps_bitwise(cuda, name):
+    """Every one of the 33 subpoly_ steps on the full lattice, hashed
+    against the reference's (vertices, edges, cache) after each call."""
+    from tropical._engine import engine_for
+    d = load(name)
+    net = product_net(d, cuda)
+    eng = engine_for(net)
+    eng.lattice(keep_all=True)
+    got = engine_steps(eng)
+    for i, (g, V, E, s) in enumerate(zip(got, d["step_V"], d["step_E"], d["step_sha"])):
+        assert (g[0], g[1]) == (V, E), f"step {i}: V/E {g[:2]} != {(V, E)}"
+        assert g[2] == s, f"step {i}: state hash differs"
+    _check_surface_faces(eng, d)
+
+
+def _check_surface_faces(eng, d):
+    sV, sE = eng.surface()
+    assert sV == int(d["n_surf"][0])
+    if sV == 0:
+        return
+    v, e, _ = eng.export()
+    tri, fc = eng.faces()
+    if "sha_surf_E" in d:
+        assert sha(e.cpu().numpy()) == str(d["sha_surf_E"])
+    if "surf_V" in d:
+        assert np.abs(v.cpu().numpy() - d["surf_V"]).max() <= VERTEX_TOL
+        assert tri.shape[0] == d["tri"].shape[0]
+        np.testing.assert_array_equal(tri.cpu().numpy(), d["tri"])
+        np.testing.assert_array_equal(fc.cpu().numpy(), d["faces"])
+    assert sha(v.cpu().numpy()) == str(d["sha_surf"])
+    assert tri.shape[0] == int(d["n_surf"][1])
+    assert sha(tri.cpu().numpy()) == str(d["sha_tri"])
+    assert sha(fc.cpu().numpy()) == str(d["sha_faces"])
+
+
+@pytest.mark.parametrize("name", cases("subpoly"))
+def test_skeleton_bitwise(cuda, name):
+    from tropical._engine import engine_for
+    d = load(name)
+    net = product_net(d, cuda)
+    eng = engine_for(net)
+    V, E = eng.skeleton(128, 1.2)
+    v, e, _ = eng.export()
+    if "skel_V" in d:
+        np.testing.assert_array_equal(v.cpu().numpy(), d["skel_V"])
+        np.testing.assert_array_equal(e.cpu().numpy(), d["skel_E"])
+    else:
+        assert sha(v.cpu().numpy(), e.cpu().numpy()) == str(d["sha_skel"])
+
+
+@pytest.mark.parametrize("name", cases("subpoly"))
+def test_subpoly_steps_bitwise(cuda, name):
+    from tropical._engine import engine_for
+    d = load(name)
+    net = product_net(d, cuda)
+    eng = engine_for(net)
+    eng.skeleton(128, 1.2)
+    v0, e0, _ = eng.export()
+    eng.load(v0, e0, keep_all=True)
+    got = engine_steps(eng)
+    for i, (g, V, E, s) in enumerate(zip(got, d["step_V"], d["step_E"], d["step_sha"])):
+        assert (g[0], g[1]) == (V, E), f"step {i}: V/E {g[:2]} != {(V, E)}"
+        assert g[2] == s, f"step {i}: state hash differs"
+    _check_surface_faces(eng, d)
+
+
+@pytest.mark.parametrize("name", cases("subpoly"))
+def test_subpoly_dropin(cuda, name, capsys):
+    """The drop-in call surface: subpoly(net, 3, 1.2, force=True)."""
+    import tropical.subpoly as sp
+    d = load(name)
+    net = product_net(d, cuda)
+    stats = []
+    faces, verts, fwi = sp.subpoly(net, 3, 1.2, force=True, stats=stats)
+    out = capsys.readouterr().out
+    assert "# of vertices and edges = " in out and " faces, " in out
+    assert verts.shape[0] == int(d["n_surf"][0])
+    assert sha(verts.cpu().numpy()) == str(d["sha_surf"])
+    assert sha(np.asarray(fwi, dtype=np.int64)) == str(d["sha_tri"])
+    assert sha(np.asarray(faces, dtype=np.float32)) == str(d["sha_faces"])
+    assert sum(s["S"] for s in stats) > 0
+
+
+def test_subpoly_step_dropin(cuda):
+    """subpoly_(vertices, edges, net, l, h, eps, outputs_) one call at a time
+    reproduces the reference's per-step states."""
+    import tropical.subpoly as sp
+    from tropical.synthetic import lattice_edges, lattice_vertices
+    d = load("synth24")
+    net = product_net(d, cuda)
+    n = int(d["lattice_n"])
+    V = torch.from_numpy(lattice_vertices(d["marks"])).to(cuda)
+    E = torch.from_numpy(lattice_edges(n)).to(cuda)
+    o = None
+    for step, idx in enumerate(d["step_idx"][:12]):
+        l, h = divmod(int(idx), net.num_hidden)
+        V, E, o = sp.subpoly_(V, E, net, l, h, 1e-4, o, force=True)
+        assert sha(V.cpu().numpy(), E.cpu().numpy(), o.cpu().numpy()) == str(d["step_sha"][step])

@@ -1,0 +1,114 @@
+// Shared device utilities for the gfx950 (CDNA4) extraction kernels.
+// Wave size is 64 on CDNA; every wave idiom below is written for 64 lanes.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define TNP_BLOCK 256
+#define TNP_WAVES (TNP_BLOCK / 64)
+
+#define TNP_CHECK(expr)                                                        \
+  do {                                                                         \
+    hipError_t _e = (expr);                                                    \
+    if (_e != hipSuccess) {                                                    \
+      tnp_set_error("%s:%d %s: %s", __FILE__, __LINE__, #expr,                 \
+                    hipGetErrorString(_e));                                    \
+      return -1;                                                               \
+    }                                                                          \
+  } while (0)
+
+// Host-side error slot (engine.cpp); printf-style.
+void tnp_set_error(const char* fmt, ...);
+
+static inline unsigned tnp_grid(int64_t n, int per_block = TNP_BLOCK) {
+  int64_t g = (n + per_block - 1) / per_block;
+  return (unsigned)(g < 1 ? 1 : g);
+}
+
+namespace tnp {
+
+__device__ __forceinline__ int lane() { return threadIdx.x & 63; }
+__device__ __forceinline__ int wave() { return threadIdx.x >> 6; }
+
+// rank of this lane among the lanes of its wave whose bit is set in `mask`
+__device__ __forceinline__ int mbcnt(uint64_t mask) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                   __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
+}
+
+// inclusive wave scan
+template <typename T>
+__device__ __forceinline__ T wave_scan_incl(T v) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    T n = __shfl_up(v, o, 64);
+    if (lane() >= o) v += n;
+  }
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ uint64_t wave_or(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Block-wide exclusive rank of a 0/1 flag (order = thread order). Returns
+// the rank; `total` receives the block count. `lds` needs TNP_WAVES ints.
+// Contains two barriers: every thread of the block must call it.
+__device__ __forceinline__ int block_rank(bool f, int* lds, int& total) {
+  uint64_t b = __ballot(f);
+  int r = mbcnt(b);
+  if (lane() == 0) lds[wave()] = __popcll(b);
+  __syncthreads();
+  int off = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < TNP_WAVES; ++i) {
+    int c = lds[i];
+    off += (i < wave()) ? c : 0;
+    tot += c;
+  }
+  __syncthreads();
+  total = tot;
+  return off + r;
+}
+
+// Block-wide exclusive scan of an int64 value (thread order).
+__device__ __forceinline__ int64_t block_scan_excl(int64_t v, int64_t* lds, int64_t& total) {
+  int64_t inc = wave_scan_incl(v);
+  if (lane() == 63) lds[wave()] = inc;
+  __syncthreads();
+  int64_t off = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < TNP_WAVES; ++i) {
+    int64_t c = lds[i];
+    off += (i < wave()) ? c : 0;
+    tot += c;
+  }
+  __syncthreads();
+  total = tot;
+  return off + inc - v;
+}
+
+// ---------------------------------------------------------------------------
+// Packed per-vertex grid word (cell offsets + on-grid-plane flags).
+//   bits  0..15  offset x + 2      bits 48..50 zero flag per dim (on a mark)
+//   bits 16..31  offset y + 2
+//   bits 32..47  offset z + 2
+// offset = searchsorted(marks, x + eps) - 1 in [-1, M-1] (tropical.py:230-231)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int grid_off(uint64_t g, int d) {
+  return (int)((g >> (16 * d)) & 0xFFFF) - 2;
+}
+__device__ __forceinline__ bool grid_zero(uint64_t g, int d) {
+  return (g >> (48 + d)) & 1;
+}
+
+}  // namespace tnp

@@ -1,0 +1,947 @@
+// Host side of the extraction engine: device-resident complex, buffer
+// management and the per-step launch sequence (C ABI in
+// include/tropical_hip.h).  One engine = one device = one HIP stream per
+// call; all scratch is stream-ordered (hipMallocAsync) and reused across
+// steps.  Host syncs per active step: split count, hit count, cell entries,
+// pair count, final sizes (each one pinned readback of the counter block).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <utility>
+
+#include "../../include/tropical_hip.h"
+#include "common.h"
+#include "kernels.h"
+#include "step.h"
+
+static thread_local std::string g_err;
+
+void tnp_set_error(const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+}
+
+extern "C" const char* tnp_last_error(void) { return g_err.c_str(); }
+extern "C" int tnp_abi_version(void) { return TNP_ABI_VERSION; }
+extern "C" int tnp_device_count(int* n) {
+  TNP_CHECK(hipGetDeviceCount(n));
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// small utility kernels (layout conversion)
+// ---------------------------------------------------------------------------
+namespace {
+
+__global__ void k_i64_to_i32(const int64_t* __restrict__ in, int32_t* __restrict__ out, int64_t n) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (int32_t)in[i];
+}
+__global__ void k_i32_to_i64(const int32_t* __restrict__ in, int64_t* __restrict__ out, int64_t n) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = in[i];
+}
+// row-major [n][K] <-> plane-major [K][ld]
+__global__ void k_rows_to_planes(const float* __restrict__ in, int64_t n, int K, float* __restrict__ out,
+                                 int64_t ld) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  for (int p = 0; p < K; ++p) out[(int64_t)p * ld + i] = in[i * K + p];
+}
+__global__ void k_planes_to_rows(const float* __restrict__ in, int64_t ld, int64_t n, int K,
+                                 float* __restrict__ out) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  for (int p = 0; p < K; ++p) out[i * K + p] = in[(int64_t)p * ld + i];
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// buffers
+// ---------------------------------------------------------------------------
+struct Buf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+static int buf_ensure(Buf& b, size_t bytes, hipStream_t s, bool keep = false) {
+  if (bytes <= b.bytes && b.p) return 0;
+  size_t nb = std::max(bytes, b.bytes + b.bytes / 2);
+  nb = std::max<size_t>(nb, 256);
+  void* p = nullptr;
+  TNP_CHECK(hipMallocAsync(&p, nb, s));
+  if (keep && b.p && b.bytes) TNP_CHECK(hipMemcpyAsync(p, b.p, b.bytes, hipMemcpyDeviceToDevice, s));
+  if (b.p) TNP_CHECK(hipFreeAsync(b.p, s));
+  b.p = p;
+  b.bytes = nb;
+  return 0;
+}
+static void buf_free(Buf& b, hipStream_t s) {
+  if (b.p) (void)hipFreeAsync(b.p, s);
+  b.p = nullptr;
+  b.bytes = 0;
+}
+
+template <typename T>
+static T* P(Buf& b) { return static_cast<T*>(b.p); }
+
+struct VSet {
+  Buf xyz, pre, pos, zero, grid;
+  int64_t cap = 0;  // rows; pre leading dimension == cap
+};
+
+struct tnp_engine {
+  int device = 0;
+  NetDev net{};
+  int K = 0;
+  bool has_net = false;
+  VSet cur, alt;
+  Buf edges, edges_alt;
+  int64_t V = 0, E = 0;
+  int keep_all = 0;
+  int valid_from = 0;  // pre planes [valid_from, K) are valid for every vertex
+  // step scratch
+  Buf blk, blkoff, scan_scr, sa, sb, stage, shared, members, cellcnt, cellcur, celloff, ent_v,
+      ent_c, paircnt, paircur, pairoff, pair_hi, pair_lo, used, nid, ctr;
+  int64_t* h_ctr = nullptr;  // pinned mirror of ctr
+  // pending split
+  int pend_idx = -1;
+  int64_t pend_S = 0;
+  // faces output
+  Buf tri, faces;
+  int64_t n_tri = 0, n_faces = 0;
+  Buf fscr[12];
+  Buf fscr2[32];
+};
+
+static int read_ctr(tnp_engine* e, hipStream_t s) {
+  TNP_CHECK(hipMemcpyAsync(e->h_ctr, e->ctr.p, CTR_N * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  TNP_CHECK(hipStreamSynchronize(s));
+  return 0;
+}
+
+static int scan_counts(tnp_engine* e, const int32_t* in, int64_t* out, int64_t n, int slot,
+                       hipStream_t s) {
+  if (buf_ensure(e->scan_scr, scan_scratch_bytes(n), s)) return -1;
+  return scan_i32_to_i64(in, out, n, P<int64_t>(e->ctr) + slot, e->scan_scr.p, e->scan_scr.bytes, s);
+}
+
+// grow a vertex set to `rows` keeping [0, keep_rows)
+static int vset_ensure(tnp_engine* e, VSet& v, int64_t rows, int64_t keep_rows, hipStream_t s) {
+  if (rows <= v.cap) return 0;
+  int64_t nc = std::max<int64_t>(rows, v.cap + v.cap / 2);
+  nc = (nc + 255) / 256 * 256;
+  VSet n;
+  n.cap = nc;
+  if (buf_ensure(n.xyz, nc * 3 * sizeof(float), s)) return -1;
+  if (buf_ensure(n.pre, (size_t)nc * e->K * sizeof(float), s)) return -1;
+  if (buf_ensure(n.pos, nc * sizeof(uint64_t), s)) return -1;
+  if (buf_ensure(n.zero, nc * sizeof(uint64_t), s)) return -1;
+  if (buf_ensure(n.grid, nc * sizeof(uint64_t), s)) return -1;
+  if (keep_rows > 0 && v.cap > 0) {
+    TNP_CHECK(hipMemcpyAsync(n.xyz.p, v.xyz.p, keep_rows * 3 * sizeof(float), hipMemcpyDeviceToDevice, s));
+    TNP_CHECK(hipMemcpy2DAsync(n.pre.p, nc * sizeof(float), v.pre.p, v.cap * sizeof(float),
+                               keep_rows * sizeof(float), e->K, hipMemcpyDeviceToDevice, s));
+    TNP_CHECK(hipMemcpyAsync(n.pos.p, v.pos.p, keep_rows * 8, hipMemcpyDeviceToDevice, s));
+    TNP_CHECK(hipMemcpyAsync(n.zero.p, v.zero.p, keep_rows * 8, hipMemcpyDeviceToDevice, s));
+    TNP_CHECK(hipMemcpyAsync(n.grid.p, v.grid.p, keep_rows * 8, hipMemcpyDeviceToDevice, s));
+  }
+  buf_free(v.xyz, s);
+  buf_free(v.pre, s);
+  buf_free(v.pos, s);
+  buf_free(v.zero, s);
+  buf_free(v.grid, s);
+  v = n;
+  return 0;
+}
+
+static int keys_for(tnp_engine* e, VSet& v, int64_t from, int64_t n, hipStream_t s) {
+  return launch_keys(e->net, P<float>(v.xyz) + 3 * from, P<float>(v.pre) + from, v.cap, n, e->K,
+                     P<uint64_t>(v.pos) + from, P<uint64_t>(v.zero) + from,
+                     P<uint64_t>(v.grid) + from, s);
+}
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+extern "C" int tnp_engine_create(tnp_engine** out, int device) {
+  TNP_CHECK(hipSetDevice(device));
+  tnp_engine* e = new tnp_engine();
+  e->device = device;
+  if (hipHostMalloc((void**)&e->h_ctr, CTR_N * sizeof(int64_t), hipHostMallocDefault) != hipSuccess) {
+    delete e;
+    tnp_set_error("hipHostMalloc failed");
+    return -1;
+  }
+  *out = e;
+  return 0;
+}
+
+extern "C" void tnp_engine_destroy(tnp_engine* e) {
+  if (!e) return;
+  (void)hipSetDevice(e->device);
+  (void)hipDeviceSynchronize();
+  hipStream_t s = 0;
+  VSet* sets[2] = {&e->cur, &e->alt};
+  for (VSet* v : sets) {
+    buf_free(v->xyz, s); buf_free(v->pre, s); buf_free(v->pos, s); buf_free(v->zero, s); buf_free(v->grid, s);
+  }
+  Buf* bufs[] = {&e->edges, &e->edges_alt, &e->blk, &e->blkoff, &e->scan_scr, &e->sa, &e->sb,
+                 &e->stage, &e->shared, &e->members, &e->cellcnt, &e->cellcur, &e->celloff,
+                 &e->ent_v, &e->ent_c, &e->paircnt, &e->paircur, &e->pairoff, &e->pair_hi,
+                 &e->pair_lo, &e->used, &e->nid, &e->ctr, &e->tri, &e->faces};
+  for (Buf* b : bufs) buf_free(*b, s);
+  for (Buf& b : e->fscr) buf_free(b, s);
+  for (Buf& b : e->fscr2) buf_free(b, s);
+  (void)hipDeviceSynchronize();
+  if (e->h_ctr) (void)hipHostFree(e->h_ctr);
+  delete e;
+}
+
+static NetDev to_dev(const tnp_net* n) {
+  NetDev d{};
+  for (int l = 0; l < TNP_MAX_LEVELS; ++l) {
+    d.scales[l] = n->scales[l];
+    d.res[l] = n->res[l];
+    d.sizes[l] = n->sizes[l];
+    d.offsets[l] = n->offsets[l];
+    d.dense[l] = n->dense[l];
+  }
+  d.table = n->d_table;
+  d.weights = n->d_weights;
+  d.marks = n->d_marks;
+  d.n_levels = n->n_levels;
+  d.num_layers = n->num_layers;
+  d.num_hidden = n->num_hidden;
+  d.n_marks = n->n_marks;
+  d.eps = n->eps;
+  return d;
+}
+
+static int check_net(const tnp_net* n) {
+  if (!n) { tnp_set_error("null net"); return -1; }
+  if (n->n_features != 2) { tnp_set_error("n_features must be 2"); return -1; }
+  NetDev d = to_dev(n);
+  if (!net_supported(d)) {
+    tnp_set_error("net shape (levels=%d, layers=%d, hidden=%d) not instantiated", n->n_levels,
+                  n->num_layers, n->num_hidden);
+    return -1;
+  }
+  if (net_K(d) > 64) { tnp_set_error("more than 64 planes"); return -1; }
+  return 0;
+}
+
+extern "C" int tnp_engine_set_net(tnp_engine* e, const tnp_net* n) {
+  if (check_net(n)) return -1;
+  e->net = to_dev(n);
+  e->K = net_K(e->net);
+  e->has_net = true;
+  return 0;
+}
+
+extern "C" int tnp_forward(const tnp_net* n, const float* xyz, int64_t N, float* pre, int64_t ld,
+                           float* out2, void* stream) {
+  if (check_net(n)) return -1;
+  return launch_forward(to_dev(n), xyz, N, pre, ld, 1, (hipStream_t)stream, out2);
+}
+extern "C" int tnp_encode(const tnp_net* n, const float* x01, int64_t N, float* out, void* stream) {
+  if (check_net(n)) return -1;
+  return launch_encode(to_dev(n), x01, N, out, (hipStream_t)stream);
+}
+extern "C" int tnp_forward_grouped(const tnp_net* n, const float* xyz, int64_t N, float* pre,
+                                   int64_t ld, float* out2, void* stream) {
+  if (check_net(n)) return -1;
+  return launch_forward(to_dev(n), xyz, N, pre, ld, 8, (hipStream_t)stream, out2);
+}
+extern "C" int tnp_region(const tnp_net* n, const float* xyz, const float* pre, int64_t ld,
+                          int64_t N, float eps, int64_t* m, int64_t* off, void* stream) {
+  if (check_net(n)) return -1;
+  return launch_region(to_dev(n), xyz, pre, ld, N, eps, m, off, (hipStream_t)stream);
+}
+extern "C" int tnp_sdf_grad(const tnp_net* n, const float* xyz, int64_t N, float* sdf, float* grad,
+                            void* stream) {
+  if (check_net(n)) return -1;
+  return launch_sdf_grad(to_dev(n), xyz, N, sdf, grad, (hipStream_t)stream);
+}
+
+static int set_edges_i64(tnp_engine* e, const int64_t* d_edges, int64_t E, hipStream_t s) {
+  if (buf_ensure(e->edges, std::max<int64_t>(E, 1) * 2 * sizeof(int32_t), s)) return -1;
+  if (E > 0)
+    hipLaunchKernelGGL(k_i64_to_i32, dim3(tnp_grid(2 * E)), dim3(TNP_BLOCK), 0, s, d_edges,
+                       P<int32_t>(e->edges), 2 * E);
+  TNP_CHECK(hipGetLastError());
+  e->E = E;
+  return 0;
+}
+
+extern "C" int tnp_engine_load(tnp_engine* e, const float* d_xyz, int64_t V, const int64_t* d_edges,
+                               int64_t E, const float* d_pre, int keep_all, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (!e->has_net) { tnp_set_error("engine has no net"); return -1; }
+  TNP_CHECK(hipSetDevice(e->device));
+  if (buf_ensure(e->ctr, CTR_N * sizeof(int64_t), s)) return -1;
+  if (vset_ensure(e, e->cur, std::max<int64_t>(V, 1), 0, s)) return -1;
+  if (V > 0)
+    TNP_CHECK(hipMemcpyAsync(e->cur.xyz.p, d_xyz, V * 3 * sizeof(float), hipMemcpyDeviceToDevice, s));
+  if (set_edges_i64(e, d_edges, E, s)) return -1;
+  if (d_pre) {
+    if (V > 0)
+      hipLaunchKernelGGL(k_rows_to_planes, dim3(tnp_grid(V)), dim3(TNP_BLOCK), 0, s, d_pre, V, e->K,
+                         P<float>(e->cur.pre), e->cur.cap);
+    TNP_CHECK(hipGetLastError());
+  } else if (launch_forward(e->net, P<float>(e->cur.xyz), V, P<float>(e->cur.pre), e->cur.cap, 1, s)) {
+    return -1;
+  }
+  if (keys_for(e, e->cur, 0, V, s)) return -1;
+  e->V = V;
+  e->keep_all = keep_all;
+  e->valid_from = 0;
+  e->pend_idx = -1;
+  return 0;
+}
+
+extern "C" int tnp_engine_sizes(tnp_engine* e, int64_t* V, int64_t* E) {
+  *V = e->V;
+  *E = e->E;
+  return 0;
+}
+
+extern "C" int tnp_engine_active_planes(tnp_engine* e, int from, uint64_t* mask, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  TNP_CHECK(hipSetDevice(e->device));
+  if (buf_ensure(e->ctr, CTR_N * sizeof(int64_t), s)) return -1;
+  TNP_CHECK(hipMemsetAsync(P<int64_t>(e->ctr) + CTR_ACTIVE, 0, sizeof(int64_t), s));
+  if (launch_active_planes(P<int32_t>(e->edges), e->E, from, e->K - 1, P<uint64_t>(e->cur.pos),
+                           P<uint64_t>(e->cur.zero), P<int64_t>(e->ctr), s))
+    return -1;
+  if (read_ctr(e, s)) return -1;
+  *mask = (uint64_t)e->h_ctr[CTR_ACTIVE];
+  return 0;
+}
+
+extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S_out, int32_t* fail) {
+  hipStream_t s = (hipStream_t)stream;
+  TNP_CHECK(hipSetDevice(e->device));
+  if (idx < e->valid_from || idx >= e->K) {
+    tnp_set_error("plane %d not cached (valid from %d)", idx, e->valid_from);
+    return -1;
+  }
+  const float eps = e->net.eps;
+  const float* col = P<float>(e->cur.pre) + (int64_t)idx * e->cur.cap;
+  TNP_CHECK(hipMemsetAsync(e->ctr.p, 0, CTR_N * sizeof(int64_t), s));
+  int64_t tiles = step_tiles(e->E);
+  if (buf_ensure(e->blk, (tiles + 1) * sizeof(int32_t), s)) return -1;
+  if (buf_ensure(e->blkoff, (tiles + 1) * sizeof(int64_t), s)) return -1;
+  int64_t S = 0;
+  if (e->E > 0) {
+    if (launch_split_count(P<int32_t>(e->edges), e->E, col, eps, P<int32_t>(e->blk), s)) return -1;
+    if (scan_counts(e, P<int32_t>(e->blk), P<int64_t>(e->blkoff), tiles, CTR_S, s)) return -1;
+    if (read_ctr(e, s)) return -1;
+    S = e->h_ctr[CTR_S];
+  }
+  *fail = 0;
+  if (S > 0) {
+    if (buf_ensure(e->sa, S * sizeof(int32_t), s)) return -1;
+    if (buf_ensure(e->sb, S * sizeof(int32_t), s)) return -1;
+    if (launch_split_emit(P<int32_t>(e->edges), e->E, col, eps, P<int64_t>(e->blkoff), e->V,
+                          P<int32_t>(e->sa), P<int32_t>(e->sb), s))
+      return -1;
+    if (vset_ensure(e, e->cur, e->V + S, e->V, s)) return -1;
+    col = P<float>(e->cur.pre) + (int64_t)idx * e->cur.cap;  // may have moved
+    if (launch_new_vertices(P<int32_t>(e->sa), P<int32_t>(e->sb), S, col, eps, P<float>(e->cur.xyz),
+                            e->V, s))
+      return -1;
+    if (buf_ensure(e->stage, (size_t)S * e->K * sizeof(float), s)) return -1;
+    if (buf_ensure(e->shared, S * sizeof(uint64_t), s)) return -1;
+    if (launch_forward(e->net, P<float>(e->cur.xyz) + 3 * e->V, S, P<float>(e->stage), S, 1, s))
+      return -1;
+    if (launch_fail_check(P<int32_t>(e->sa), P<int32_t>(e->sb), S, idx, P<uint64_t>(e->cur.zero),
+                          P<float>(e->stage), eps, P<uint64_t>(e->shared), P<int64_t>(e->ctr), s))
+      return -1;
+    // grid words of the new vertices (coordinates are final)
+    if (launch_keys(e->net, P<float>(e->cur.xyz) + 3 * e->V, P<float>(e->stage), S, S, 0,
+                    P<uint64_t>(e->cur.pos) + e->V, P<uint64_t>(e->cur.zero) + e->V,
+                    P<uint64_t>(e->cur.grid) + e->V, s))
+      return -1;
+    if (read_ctr(e, s)) return -1;
+    *fail = e->h_ctr[CTR_FAIL] ? 1 : 0;
+  }
+  *S_out = S;
+  e->pend_idx = idx;
+  e->pend_S = S;
+  return 0;
+}
+
+extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override_, void* stream,
+                                 tnp_step_stats* st) {
+  hipStream_t s = (hipStream_t)stream;
+  TNP_CHECK(hipSetDevice(e->device));
+  if (e->pend_idx != idx) { tnp_set_error("finish(%d) without split(%d)", idx, idx); return -1; }
+  e->pend_idx = -1;
+  const float eps = e->net.eps;
+  const int K = e->K;
+  const int64_t V = e->V, E = e->E, S = e->pend_S;
+  const int64_t NV = V + S;
+  VSet& c = e->cur;
+  const float* col = P<float>(c.pre) + (int64_t)idx * c.cap;
+  int64_t* ctr = P<int64_t>(e->ctr);
+  uint64_t* pos = P<uint64_t>(c.pos);
+  uint64_t* zero = P<uint64_t>(c.zero);
+  uint64_t* grid = P<uint64_t>(c.grid);
+
+  // 1. override + keys of the new vertices
+  if (launch_finalize_new(S, K, override_, P<uint64_t>(e->shared), P<float>(e->stage), eps,
+                          P<float>(c.pre), c.cap, e->valid_from, V, pos, zero, s))
+    return -1;
+
+  // 2. members = new vertices ++ hit vertices (ascending)
+  int64_t vt = step_tiles(V);
+  if (buf_ensure(e->blk, (vt + 1) * sizeof(int32_t), s)) return -1;
+  if (buf_ensure(e->blkoff, (vt + 1) * sizeof(int64_t), s)) return -1;
+  if (buf_ensure(e->members, std::max<int64_t>(NV, 1) * sizeof(int32_t), s)) return -1;
+  if (V > 0) {
+    if (launch_hit_count(col, V, eps, P<int32_t>(e->blk), s)) return -1;
+    if (scan_counts(e, P<int32_t>(e->blk), P<int64_t>(e->blkoff), vt, CTR_H, s)) return -1;
+  }
+  if (launch_hit_emit(col, V, eps, P<int64_t>(e->blkoff), P<int32_t>(e->members), S, s)) return -1;
+
+  // 3. bucket members by grid cell (dense cell grid over the marks)
+  const int NC = e->net.n_marks + 2;
+  const int64_t ncell = (int64_t)NC * NC * NC;
+  if (buf_ensure(e->cellcnt, ncell * sizeof(int32_t), s)) return -1;
+  if (buf_ensure(e->cellcur, ncell * sizeof(int32_t), s)) return -1;
+  if (buf_ensure(e->celloff, ncell * sizeof(int64_t), s)) return -1;
+  TNP_CHECK(hipMemsetAsync(e->cellcnt.p, 0, ncell * sizeof(int32_t), s));
+  TNP_CHECK(hipMemsetAsync(e->cellcur.p, 0, ncell * sizeof(int32_t), s));
+  if (read_ctr(e, s)) return -1;
+  const int64_t H = V > 0 ? e->h_ctr[CTR_H] : 0;
+  const int64_t M = S + H;
+  if (launch_cell_count(P<int32_t>(e->members), M, grid, zero, idx, NC, P<int32_t>(e->cellcnt), ctr, s))
+    return -1;
+  if (scan_counts(e, P<int32_t>(e->cellcnt), P<int64_t>(e->celloff), ncell, CTR_T, s)) return -1;
+  if (read_ctr(e, s)) return -1;
+  if (e->h_ctr[CTR_K0]) {
+    // the reference builds torch.cartesian_prod() of zero tensors (subpoly.py:317)
+    tnp_set_error("meshgrid expects a non-empty TensorList (a region row without zeros, plane %d)", idx);
+    return -1;
+  }
+  const int64_t T = e->h_ctr[CTR_T];
+  if (buf_ensure(e->ent_v, std::max<int64_t>(T, 1) * sizeof(int32_t), s)) return -1;
+  if (buf_ensure(e->ent_c, std::max<int64_t>(T, 1) * sizeof(int32_t), s)) return -1;
+  if (launch_cell_scatter(P<int32_t>(e->members), M, grid, NC, P<int64_t>(e->celloff),
+                          P<int32_t>(e->cellcur), P<int32_t>(e->ent_v), P<int32_t>(e->ent_c), s))
+    return -1;
+
+  // 4. connecting edges, bucketed by their smaller endpoint
+  if (buf_ensure(e->paircnt, std::max<int64_t>(NV, 1) * sizeof(int32_t), s)) return -1;
+  if (buf_ensure(e->paircur, std::max<int64_t>(NV, 1) * sizeof(int32_t), s)) return -1;
+  if (buf_ensure(e->pairoff, std::max<int64_t>(NV, 1) * sizeof(int64_t), s)) return -1;
+  TNP_CHECK(hipMemsetAsync(e->paircnt.p, 0, NV * sizeof(int32_t), s));
+  TNP_CHECK(hipMemsetAsync(e->paircur.p, 0, NV * sizeof(int32_t), s));
+  if (launch_pairs(false, P<int32_t>(e->ent_v), P<int32_t>(e->ent_c), T, P<int64_t>(e->celloff),
+                   P<int32_t>(e->cellcnt), NC, idx, pos, zero, grid, P<int32_t>(e->paircnt),
+                   nullptr, nullptr, nullptr, ctr, s))
+    return -1;
+  if (scan_counts(e, P<int32_t>(e->paircnt), P<int64_t>(e->pairoff), NV, CTR_X, s)) return -1;
+  if (read_ctr(e, s)) return -1;
+  if (e->h_ctr[CTR_COMPAT] == 0) {
+    // every region has a single member: extract_every_valid_edge cats an
+    // empty list (subpoly.py:505-513)
+    tnp_set_error("torch.cat(): expected a non-empty list of Tensors (no region with two vertices, plane %d)", idx);
+    return -1;
+  }
+  const int64_t X = e->h_ctr[CTR_X];
+  if (buf_ensure(e->pair_hi, std::max<int64_t>(X, 1) * sizeof(int32_t), s)) return -1;
+  if (buf_ensure(e->pair_lo, std::max<int64_t>(X, 1) * sizeof(int32_t), s)) return -1;
+  if (launch_pairs(true, P<int32_t>(e->ent_v), P<int32_t>(e->ent_c), T, P<int64_t>(e->celloff),
+                   P<int32_t>(e->cellcnt), NC, idx, pos, zero, grid, P<int32_t>(e->paircnt),
+                   P<int64_t>(e->pairoff), P<int32_t>(e->paircur), P<int32_t>(e->pair_hi), ctr, s))
+    return -1;
+  if (launch_pair_sort(P<int64_t>(e->pairoff), P<int32_t>(e->paircnt), NV, P<int32_t>(e->pair_hi),
+                       P<int32_t>(e->pair_lo), s))
+    return -1;
+
+  // 5. pruning over [edges; e_new; c_new] + vertex compaction
+  const int64_t N = E + S + X;
+  int64_t nt = step_tiles(N);
+  if (buf_ensure(e->blk, (nt + 1) * sizeof(int32_t), s)) return -1;
+  if (buf_ensure(e->blkoff, (nt + 1) * sizeof(int64_t), s)) return -1;
+  if (buf_ensure(e->edges_alt, std::max<int64_t>(N, 1) * 2 * sizeof(int32_t), s)) return -1;
+  TNP_CHECK(hipMemsetAsync(ctr + CTR_ACTIVE, 0, sizeof(int64_t), s));
+  const int32_t* eg = P<int32_t>(e->edges);
+  int64_t V2 = NV, E2 = N;
+  int next_valid = e->valid_from;
+  if (prune) {
+    if (buf_ensure(e->used, std::max<int64_t>(NV, 1) * sizeof(int32_t), s)) return -1;
+    if (buf_ensure(e->nid, std::max<int64_t>(NV, 1) * sizeof(int64_t), s)) return -1;
+    TNP_CHECK(hipMemsetAsync(e->used.p, 0, NV * sizeof(int32_t), s));
+    if (launch_prune(false, eg, E, P<int32_t>(e->sb), S, V, P<int32_t>(e->pair_lo),
+                     P<int32_t>(e->pair_hi), X, idx, 1, K - 1, pos, zero, P<int32_t>(e->blk),
+                     nullptr, nullptr, nullptr, ctr, s))
+      return -1;
+    if (scan_counts(e, P<int32_t>(e->blk), P<int64_t>(e->blkoff), nt, CTR_E, s)) return -1;
+    if (launch_prune(true, eg, E, P<int32_t>(e->sb), S, V, P<int32_t>(e->pair_lo),
+                     P<int32_t>(e->pair_hi), X, idx, 1, K - 1, pos, zero, nullptr,
+                     P<int64_t>(e->blkoff), P<int32_t>(e->edges_alt), P<int32_t>(e->used), ctr, s))
+      return -1;
+    if (scan_counts(e, P<int32_t>(e->used), P<int64_t>(e->nid), NV, CTR_V, s)) return -1;
+    next_valid = e->keep_all ? 0 : std::min(idx + 1, K - 1);
+    if (vset_ensure(e, e->alt, NV, 0, s)) return -1;
+    VSet& a = e->alt;
+    if (launch_gather_vertices(P<int32_t>(e->used), P<int64_t>(e->nid), NV, K, next_valid,
+                               P<float>(c.xyz), P<float>(c.pre), c.cap, pos, zero, grid,
+                               P<float>(a.xyz), P<float>(a.pre), a.cap, P<uint64_t>(a.pos),
+                               P<uint64_t>(a.zero), P<uint64_t>(a.grid), s))
+      return -1;
+    if (read_ctr(e, s)) return -1;
+    E2 = e->h_ctr[CTR_E];
+    V2 = e->h_ctr[CTR_V];
+    if (launch_remap_edges(P<int32_t>(e->edges_alt), E2, P<int64_t>(e->nid), s)) return -1;
+    std::swap(e->cur, e->alt);
+  } else {
+    if (launch_prune(true, eg, E, P<int32_t>(e->sb), S, V, P<int32_t>(e->pair_lo),
+                     P<int32_t>(e->pair_hi), X, idx, 0, K - 1, pos, zero, nullptr, nullptr,
+                     P<int32_t>(e->edges_alt), nullptr, ctr, s))
+      return -1;
+    if (read_ctr(e, s)) return -1;
+  }
+  std::swap(e->edges, e->edges_alt);
+  e->V = V2;
+  e->E = E2;
+  e->valid_from = next_valid;
+  if (st) {
+    st->idx = idx;
+    st->V_in = V;
+    st->E_in = E;
+    st->S = S;
+    st->H = H;
+    st->X = X;
+    st->V_out = V2;
+    st->E_out = E2;
+    st->A = e->h_ctr[CTR_A];
+    st->P = e->h_ctr[CTR_P];
+    st->pair_tests = e->h_ctr[CTR_TESTS];
+    st->override_applied = override_;
+    st->next_active = (uint64_t)e->h_ctr[CTR_ACTIVE];
+  }
+  return 0;
+}
+
+extern "C" int tnp_engine_export(tnp_engine* e, float* d_xyz, int64_t* d_edges, float* d_pre,
+                                 void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  TNP_CHECK(hipSetDevice(e->device));
+  if (d_xyz && e->V > 0)
+    TNP_CHECK(hipMemcpyAsync(d_xyz, e->cur.xyz.p, e->V * 3 * sizeof(float), hipMemcpyDeviceToDevice, s));
+  if (d_edges && e->E > 0)
+    hipLaunchKernelGGL(k_i32_to_i64, dim3(tnp_grid(2 * e->E)), dim3(TNP_BLOCK), 0, s,
+                       P<int32_t>(e->edges), d_edges, 2 * e->E);
+  if (d_pre && e->V > 0) {
+    if (e->valid_from != 0) {
+      tnp_set_error("cached planes below %d were dropped (load with keep_all_planes=1)", e->valid_from);
+      return -1;
+    }
+    hipLaunchKernelGGL(k_planes_to_rows, dim3(tnp_grid(e->V)), dim3(TNP_BLOCK), 0, s,
+                       P<float>(e->cur.pre), e->cur.cap, e->V, e->K, d_pre);
+  }
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+
+// extract_skeleton (subpoly.py:556-581)
+extern "C" int tnp_engine_surface(tnp_engine* e, void* stream, int64_t* V_out, int64_t* E_out) {
+  hipStream_t s = (hipStream_t)stream;
+  TNP_CHECK(hipSetDevice(e->device));
+  const int64_t V = e->V, E = e->E;
+  VSet& c = e->cur;
+  const float* col = P<float>(c.pre) + (int64_t)(e->K - 1) * c.cap;
+  if (buf_ensure(e->used, std::max<int64_t>(V, 1) * sizeof(int32_t), s)) return -1;
+  if (buf_ensure(e->paircnt, std::max<int64_t>(V, 1) * sizeof(int32_t), s)) return -1;
+  if (buf_ensure(e->nid, std::max<int64_t>(V, 1) * sizeof(int64_t), s)) return -1;
+  TNP_CHECK(hipMemsetAsync(e->ctr.p, 0, CTR_N * sizeof(int64_t), s));
+  int32_t* on = P<int32_t>(e->paircnt);
+  if (launch_surface_flags(P<float>(c.xyz), col, V, e->net.eps, on, s)) return -1;
+  if (scan_counts(e, on, P<int64_t>(e->nid), V, CTR_AUX, s)) return -1;
+  if (read_ctr(e, s)) return -1;
+  if (e->h_ctr[CTR_AUX] < 3) {
+    e->V = 0;
+    e->E = 0;
+    *V_out = 0;
+    *E_out = 0;
+    return 0;
+  }
+  int64_t nt = step_tiles(E);
+  if (buf_ensure(e->blk, (nt + 1) * sizeof(int32_t), s)) return -1;
+  if (buf_ensure(e->blkoff, (nt + 1) * sizeof(int64_t), s)) return -1;
+  if (buf_ensure(e->edges_alt, std::max<int64_t>(E, 1) * 2 * sizeof(int32_t), s)) return -1;
+  TNP_CHECK(hipMemsetAsync(e->used.p, 0, V * sizeof(int32_t), s));
+  if (launch_surface_edges(P<int32_t>(e->edges), E, on, P<int32_t>(e->blk), nullptr, 0, nullptr,
+                           nullptr, s))
+    return -1;
+  if (scan_counts(e, P<int32_t>(e->blk), P<int64_t>(e->blkoff), nt, CTR_E, s)) return -1;
+  if (launch_surface_edges(P<int32_t>(e->edges), E, on, nullptr, P<int64_t>(e->blkoff), 1,
+                           P<int32_t>(e->edges_alt), P<int32_t>(e->used), s))
+    return -1;
+  if (scan_counts(e, P<int32_t>(e->used), P<int64_t>(e->nid), V, CTR_V, s)) return -1;
+  if (vset_ensure(e, e->alt, V, 0, s)) return -1;
+  VSet& a = e->alt;
+  int keep_from = e->valid_from;
+  if (launch_gather_vertices(P<int32_t>(e->used), P<int64_t>(e->nid), V, e->K, keep_from,
+                             P<float>(c.xyz), P<float>(c.pre), c.cap, P<uint64_t>(c.pos),
+                             P<uint64_t>(c.zero), P<uint64_t>(c.grid), P<float>(a.xyz),
+                             P<float>(a.pre), a.cap, P<uint64_t>(a.pos), P<uint64_t>(a.zero),
+                             P<uint64_t>(a.grid), s))
+    return -1;
+  if (read_ctr(e, s)) return -1;
+  int64_t E2 = e->h_ctr[CTR_E], V2 = e->h_ctr[CTR_V];
+  if (launch_remap_edges(P<int32_t>(e->edges_alt), E2, P<int64_t>(e->nid), s)) return -1;
+  std::swap(e->cur, e->alt);
+  std::swap(e->edges, e->edges_alt);
+  e->V = V2;
+  e->E = E2;
+  *V_out = V2;
+  *E_out = E2;
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// full lattice over the marks, x-slab [x0, x1] (tropical.py:103-109 layout:
+// x-edges, then y, then z, each (hi, lo), meshgrid-ij order)
+// ---------------------------------------------------------------------------
+namespace {
+__global__ void k_lattice_vertices(const float* __restrict__ marks, int N, int x0, int nx,
+                                   float* __restrict__ xyz) {
+  int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t nv = (int64_t)nx * N * N;
+  if (v >= nv) return;
+  int k = (int)(v % N), j = (int)((v / N) % N), i = (int)(v / ((int64_t)N * N)) + x0;
+  // preprocess_inverse: x * 2 - 1 (model.py:81-82)
+  xyz[3 * v + 0] = __fsub_rn(__fmul_rn(marks[i], 2.0f), 1.0f);
+  xyz[3 * v + 1] = __fsub_rn(__fmul_rn(marks[j], 2.0f), 1.0f);
+  xyz[3 * v + 2] = __fsub_rn(__fmul_rn(marks[k], 2.0f), 1.0f);
+}
+__global__ void k_lattice_edges(int N, int nx, int32_t* __restrict__ edges) {
+  const int64_t NN = (int64_t)N * N;
+  const int64_t ex = (int64_t)(nx - 1) * NN;
+  const int64_t ey = (int64_t)nx * (N - 1) * N;
+  const int64_t ez = (int64_t)nx * N * (N - 1);
+  int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t lo, hi;
+  if (e < ex) {
+    lo = e;
+    hi = e + NN;
+  } else if (e < ex + ey) {
+    int64_t r = e - ex;  // shape (nx, N-1, N)
+    int64_t k = r % N, j = (r / N) % (N - 1), i = r / ((int64_t)(N - 1) * N);
+    lo = i * NN + j * N + k;
+    hi = lo + N;
+  } else if (e < ex + ey + ez) {
+    int64_t r = e - ex - ey;  // shape (nx, N, N-1)
+    int64_t k = r % (N - 1), j = (r / (N - 1)) % N, i = r / ((int64_t)N * (N - 1));
+    lo = i * NN + j * N + k;
+    hi = lo + 1;
+  } else {
+    return;
+  }
+  edges[2 * e] = (int32_t)hi;
+  edges[2 * e + 1] = (int32_t)lo;
+}
+}  // namespace
+
+extern "C" int tnp_engine_lattice(tnp_engine* e, int x0, int x1, int keep_all, void* stream,
+                                  int64_t* V_out, int64_t* E_out) {
+  hipStream_t s = (hipStream_t)stream;
+  if (!e->has_net) { tnp_set_error("engine has no net"); return -1; }
+  TNP_CHECK(hipSetDevice(e->device));
+  const int N = e->net.n_marks;
+  if (x0 < 0 || x1 >= N || x1 < x0) { tnp_set_error("bad slab [%d, %d] of %d marks", x0, x1, N); return -1; }
+  const int nx = x1 - x0 + 1;
+  const int64_t V = (int64_t)nx * N * N;
+  const int64_t E = (int64_t)(nx - 1) * N * N + 2LL * nx * (N - 1) * N;
+  if (V >= (1LL << 31) || E >= (1LL << 31)) { tnp_set_error("lattice too large for int32 ids"); return -1; }
+  if (buf_ensure(e->ctr, CTR_N * sizeof(int64_t), s)) return -1;
+  if (vset_ensure(e, e->cur, V, 0, s)) return -1;
+  if (buf_ensure(e->edges, std::max<int64_t>(E, 1) * 2 * sizeof(int32_t), s)) return -1;
+  hipLaunchKernelGGL(k_lattice_vertices, dim3(tnp_grid(V)), dim3(TNP_BLOCK), 0, s, e->net.marks, N,
+                     x0, nx, P<float>(e->cur.xyz));
+  hipLaunchKernelGGL(k_lattice_edges, dim3(tnp_grid(E)), dim3(TNP_BLOCK), 0, s, N, nx,
+                     P<int32_t>(e->edges));
+  TNP_CHECK(hipGetLastError());
+  if (launch_forward(e->net, P<float>(e->cur.xyz), V, P<float>(e->cur.pre), e->cur.cap, 1, s)) return -1;
+  if (keys_for(e, e->cur, 0, V, s)) return -1;
+  e->V = V;
+  e->E = E;
+  e->keep_all = keep_all;
+  e->valid_from = 0;
+  e->pend_idx = -1;
+  *V_out = V;
+  *E_out = E;
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// skeleton (tropical.py:158-225) + hypercube fallback (subpoly.py:51-52)
+// ---------------------------------------------------------------------------
+#include <vector>
+
+#include "skeleton.h"
+
+static int load_hypercube(tnp_engine* e, float size, hipStream_t s) {
+  float x[2] = {-size, size};
+  std::vector<float> v;
+  for (int i = 0; i < 2; ++i)
+    for (int j = 0; j < 2; ++j)
+      for (int k = 0; k < 2; ++k) {
+        v.push_back(x[i]);
+        v.push_back(x[j]);
+        v.push_back(x[k]);
+      }
+  std::vector<int32_t> ed;
+  for (int i = 0; i < 8; ++i)
+    for (int j = i + 1; j < 8; ++j) {
+      int neg = 0;
+      for (int d = 0; d < 3; ++d) neg += (v[3 * i + d] * v[3 * j + d] < 0.f);
+      if (neg == 1) {
+        ed.push_back(i);
+        ed.push_back(j);
+      }
+    }
+  if (vset_ensure(e, e->cur, 8, 0, s)) return -1;
+  if (buf_ensure(e->edges, ed.size() * sizeof(int32_t), s)) return -1;
+  TNP_CHECK(hipMemcpyAsync(e->cur.xyz.p, v.data(), v.size() * sizeof(float), hipMemcpyHostToDevice, s));
+  TNP_CHECK(hipMemcpyAsync(e->edges.p, ed.data(), ed.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
+  TNP_CHECK(hipStreamSynchronize(s));  // host vectors go out of scope
+  e->V = 8;
+  e->E = (int64_t)ed.size() / 2;
+  return 0;
+}
+
+extern "C" int tnp_engine_skeleton(tnp_engine* e, int unit, float size, void* stream, int64_t* V_out,
+                                   int64_t* E_out) {
+  hipStream_t s = (hipStream_t)stream;
+  if (!e->has_net) { tnp_set_error("engine has no net"); return -1; }
+  if (unit < 2) { tnp_set_error("unit must be >= 2"); return -1; }
+  TNP_CHECK(hipSetDevice(e->device));
+  const int L = e->net.n_marks;
+  if ((int64_t)L * L * L >= (1LL << 31)) { tnp_set_error("too many marks for int32 ids"); return -1; }
+  std::vector<float> mk(L);
+  TNP_CHECK(hipMemcpyAsync(mk.data(), e->net.marks, L * sizeof(float), hipMemcpyDeviceToHost, s));
+  TNP_CHECK(hipStreamSynchronize(s));
+  float dmax = -INFINITY;  // torch.diff(marks).max().item()
+  for (int i = 0; i + 1 < L; ++i) dmax = std::max(dmax, mk[i + 1] - mk[i]);
+  if (buf_ensure(e->ctr, CTR_N * sizeof(int64_t), s)) return -1;
+  const int64_t LLL = (int64_t)L * L * L;
+  if (buf_ensure(e->used, LLL * sizeof(int32_t), s)) return -1;
+  if (buf_ensure(e->nid, LLL * sizeof(int64_t), s)) return -1;
+  TNP_CHECK(hipMemsetAsync(e->used.p, 0, LLL * sizeof(int32_t), s));
+  int64_t tile_pts = (int64_t)std::min(unit, L) * std::min(unit, L) * std::min(unit, L);
+  if (buf_ensure(e->stage, tile_pts * sizeof(float), s)) return -1;
+  if (buf_ensure(e->shared, 16, s)) return -1;
+  unsigned int* gmax = P<unsigned int>(e->shared);
+  int64_t total = 0;
+  for (int i0 = 0; i0 < L; i0 += unit - 1)
+    for (int j0 = 0; j0 < L; j0 += unit - 1)
+      for (int k0 = 0; k0 < L; k0 += unit - 1) {
+        int n0 = std::min(L, i0 + unit) - i0, n1 = std::min(L, j0 + unit) - j0,
+            n2 = std::min(L, k0 + unit) - k0;
+        TNP_CHECK(hipMemsetAsync(gmax, 0, sizeof(unsigned int), s));
+        if (launch_skel_eval(e->net, i0, j0, k0, n0, n1, n2, P<float>(e->stage), gmax, s)) return -1;
+        int64_t N = skel_candidates(n0, n1, n2);
+        int64_t nt = skel_tiles(N);
+        if (buf_ensure(e->blk, (nt + 1) * sizeof(int32_t), s)) return -1;
+        if (buf_ensure(e->blkoff, (nt + 1) * sizeof(int64_t), s)) return -1;
+        if (launch_skel_edges(false, i0, j0, k0, n0, n1, n2, L, P<float>(e->stage), dmax, gmax,
+                              P<int32_t>(e->blk), nullptr, 0, nullptr, nullptr, s))
+          return -1;
+        if (scan_counts(e, P<int32_t>(e->blk), P<int64_t>(e->blkoff), nt, CTR_AUX, s)) return -1;
+        if (read_ctr(e, s)) return -1;
+        int64_t cnt = e->h_ctr[CTR_AUX];
+        if (cnt > 0) {
+          if (buf_ensure(e->edges_alt, (total + cnt) * 2 * sizeof(int32_t), s, true)) return -1;
+          if (launch_skel_edges(true, i0, j0, k0, n0, n1, n2, L, P<float>(e->stage), dmax, gmax,
+                                nullptr, P<int64_t>(e->blkoff), total, P<int32_t>(e->edges_alt),
+                                P<int32_t>(e->used), s))
+            return -1;
+        }
+        total += cnt;
+      }
+  e->pend_idx = -1;
+  e->valid_from = 0;
+  if (total == 0) {
+    if (load_hypercube(e, size, s)) return -1;
+  } else {
+    if (scan_counts(e, P<int32_t>(e->used), P<int64_t>(e->nid), LLL, CTR_V, s)) return -1;
+    if (read_ctr(e, s)) return -1;
+    int64_t V = e->h_ctr[CTR_V];
+    if (vset_ensure(e, e->cur, V, 0, s)) return -1;
+    if (launch_skel_vertices(P<int32_t>(e->used), P<int64_t>(e->nid), LLL, L, e->net.marks,
+                             P<float>(e->cur.xyz), s))
+      return -1;
+    if (launch_remap_i32(P<int32_t>(e->edges_alt), 2 * total, P<int64_t>(e->nid), s)) return -1;
+    std::swap(e->edges, e->edges_alt);
+    e->V = V;
+    e->E = total;
+  }
+  if (launch_forward(e->net, P<float>(e->cur.xyz), e->V, P<float>(e->cur.pre), e->cur.cap, 1, s)) return -1;
+  if (keys_for(e, e->cur, 0, e->V, s)) return -1;
+  e->keep_all = 0;
+  *V_out = e->V;
+  *E_out = e->E;
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// extract_faces (subpoly.py:584-728) on the current complex
+// ---------------------------------------------------------------------------
+#include "faces.h"
+
+enum { FS_TABLE, FS_CNT, FS_KC, FS_KF, FS_MEMOFF, FS_RID, FS_MEM, FS_CUR, FS_ROFF, FS_RCNT,
+       FS_BCNT, FS_BOFF, FS_BCUR, FS_ROWS, FS_KEEP, FS_KOFF, FS_FROW, FS_MEAN, FS_NRM, FS_SDF,
+       FS_KEY, FS_ORDV, FS_CALL, FS_CNZ, FS_HIST, FS_BASE, FS_N };
+
+extern "C" int tnp_engine_faces(tnp_engine* e, void* stream, int64_t* n_tri, int64_t* n_faces) {
+  hipStream_t s = (hipStream_t)stream;
+  TNP_CHECK(hipSetDevice(e->device));
+  static_assert(FS_N <= 32, "face scratch slots");
+  Buf* fs = e->fscr2;
+  const int64_t V = e->V;
+  const int K = e->K;
+  e->n_tri = e->n_faces = 0;
+  *n_tri = *n_faces = 0;
+  if (V == 0) return 0;
+  if (e->net.n_marks + 2 >= 1024 || K - 1 > 34) {
+    tnp_set_error("faces: region key needs n_marks+2 < 1024 and <= 34 planes");
+    return -1;
+  }
+  const uint64_t pmask = (K - 1 >= 64) ? ~0ull : ((1ull << (K - 1)) - 1ull);
+  int64_t* ctr = P<int64_t>(e->ctr);
+  const uint64_t* pos = P<uint64_t>(e->cur.pos);
+  const uint64_t* zero = P<uint64_t>(e->cur.zero);
+  const uint64_t* grid = P<uint64_t>(e->cur.grid);
+  const float* xyz = P<float>(e->cur.xyz);
+  TNP_CHECK(hipMemsetAsync(ctr, 0, CTR_N * sizeof(int64_t), s));
+  // F1: augmented-row count and region hash table
+  if (launch_face_count(V, grid, pos, zero, pmask, ctr + CTR_AUX - 1, s)) return -1;
+  if (read_ctr(e, s)) return -1;
+  const int64_t A = e->h_ctr[CTR_AUX - 1];
+  if (e->h_ctr[CTR_AUX] > 30) { tnp_set_error("faces: a vertex lies on %lld planes", (long long)e->h_ctr[CTR_AUX]); return -1; }
+  int64_t cap = 1024;
+  while (cap < 2 * A) cap <<= 1;
+  if (buf_ensure(fs[FS_TABLE], cap * 8, s) || buf_ensure(fs[FS_CNT], cap * 4, s) ||
+      buf_ensure(fs[FS_KC], cap * 4, s) || buf_ensure(fs[FS_KF], cap * 4, s) ||
+      buf_ensure(fs[FS_MEMOFF], cap * 8, s) || buf_ensure(fs[FS_RID], cap * 8, s) ||
+      buf_ensure(fs[FS_CUR], cap * 4, s))
+    return -1;
+  TNP_CHECK(hipMemsetAsync(fs[FS_TABLE].p, 0xFF, cap * 8, s));
+  TNP_CHECK(hipMemsetAsync(fs[FS_CNT].p, 0, cap * 4, s));
+  TNP_CHECK(hipMemsetAsync(fs[FS_CUR].p, 0, cap * 4, s));
+  if (launch_face_insert(V, grid, pos, zero, pmask, P<uint64_t>(fs[FS_TABLE]), (uint64_t)cap - 1,
+                         P<int32_t>(fs[FS_CNT]), s))
+    return -1;
+  if (launch_keep_counts(P<int32_t>(fs[FS_CNT]), cap, P<int32_t>(fs[FS_KC]), P<int32_t>(fs[FS_KF]), s)) return -1;
+  if (scan_counts(e, P<int32_t>(fs[FS_KC]), P<int64_t>(fs[FS_MEMOFF]), cap, CTR_T, s)) return -1;
+  if (scan_counts(e, P<int32_t>(fs[FS_KF]), P<int64_t>(fs[FS_RID]), cap, CTR_X, s)) return -1;
+  if (read_ctr(e, s)) return -1;
+  const int64_t Mtot = e->h_ctr[CTR_T], R = e->h_ctr[CTR_X];
+  if (R == 0) return 0;
+  // F2: member lists (k, v)-sorted
+  if (buf_ensure(fs[FS_MEM], Mtot * 8, s) || buf_ensure(fs[FS_ROFF], R * 8, s) ||
+      buf_ensure(fs[FS_RCNT], R * 4, s))
+    return -1;
+  if (launch_face_scatter(V, grid, pos, zero, pmask, P<uint64_t>(fs[FS_TABLE]), (uint64_t)cap - 1,
+                          P<int32_t>(fs[FS_CNT]), P<int64_t>(fs[FS_MEMOFF]), P<int32_t>(fs[FS_CUR]),
+                          P<uint64_t>(fs[FS_MEM]), s))
+    return -1;
+  if (launch_region_finalize(cap, P<int32_t>(fs[FS_KF]), P<int64_t>(fs[FS_RID]), P<int32_t>(fs[FS_CNT]),
+                             P<int64_t>(fs[FS_MEMOFF]), P<uint64_t>(fs[FS_MEM]), P<int64_t>(fs[FS_ROFF]),
+                             P<int32_t>(fs[FS_RCNT]), s))
+    return -1;
+  // F3: lexicographic row order + unique
+  if (buf_ensure(fs[FS_BCNT], V * 4, s) || buf_ensure(fs[FS_BOFF], V * 8, s) ||
+      buf_ensure(fs[FS_BCUR], V * 4, s) || buf_ensure(fs[FS_ROWS], R * 4, s) ||
+      buf_ensure(fs[FS_KEEP], R * 4, s) || buf_ensure(fs[FS_KOFF], R * 8, s))
+    return -1;
+  TNP_CHECK(hipMemsetAsync(fs[FS_BCNT].p, 0, V * 4, s));
+  TNP_CHECK(hipMemsetAsync(fs[FS_BCUR].p, 0, V * 4, s));
+  const uint64_t* mem = P<uint64_t>(fs[FS_MEM]);
+  const int64_t* roff = P<int64_t>(fs[FS_ROFF]);
+  const int32_t* rcnt = P<int32_t>(fs[FS_RCNT]);
+  if (launch_row_buckets(R, V, mem, roff, rcnt, P<int32_t>(fs[FS_BCNT]), nullptr, nullptr, nullptr, nullptr, 0, s))
+    return -1;
+  if (scan_counts(e, P<int32_t>(fs[FS_BCNT]), P<int64_t>(fs[FS_BOFF]), V, CTR_AUX, s)) return -1;
+  if (launch_row_buckets(R, V, mem, roff, rcnt, nullptr, P<int64_t>(fs[FS_BOFF]), P<int32_t>(fs[FS_BCUR]),
+                         P<int32_t>(fs[FS_ROWS]), nullptr, 1, s))
+    return -1;
+  if (launch_row_buckets(R, V, mem, roff, rcnt, P<int32_t>(fs[FS_BCNT]), P<int64_t>(fs[FS_BOFF]), nullptr,
+                         P<int32_t>(fs[FS_ROWS]), P<int32_t>(fs[FS_KEEP]), 2, s))
+    return -1;
+  if (scan_counts(e, P<int32_t>(fs[FS_KEEP]), P<int64_t>(fs[FS_KOFF]), R, CTR_E, s)) return -1;
+  if (read_ctr(e, s)) return -1;
+  const int64_t F = e->h_ctr[CTR_E];
+  if (buf_ensure(fs[FS_FROW], F * 4, s) || buf_ensure(fs[FS_MEAN], F * 12, s) ||
+      buf_ensure(fs[FS_NRM], F * 12, s) || buf_ensure(fs[FS_SDF], F * 4, s) ||
+      buf_ensure(fs[FS_KEY], Mtot * 8, s) || buf_ensure(fs[FS_ORDV], Mtot * 4, s) ||
+      buf_ensure(fs[FS_CALL], F * 4, s) || buf_ensure(fs[FS_CNZ], F * 4, s))
+    return -1;
+  if (launch_compact_rows(R, P<int32_t>(fs[FS_KEEP]), P<int64_t>(fs[FS_KOFF]), P<int32_t>(fs[FS_ROWS]),
+                          P<int32_t>(fs[FS_FROW]), s))
+    return -1;
+  const int32_t* frow = P<int32_t>(fs[FS_FROW]);
+  // F4: normals at the row means, angular order
+  if (launch_row_mean(F, frow, mem, roff, rcnt, xyz, P<float>(fs[FS_MEAN]), s)) return -1;
+  if (launch_sdf_grad(e->net, P<float>(fs[FS_MEAN]), F, P<float>(fs[FS_SDF]), P<float>(fs[FS_NRM]), s)) return -1;
+  if (launch_row_order(F, frow, mem, roff, rcnt, xyz, P<float>(fs[FS_NRM]), F == 3 ? 1 : 0,
+                       P<uint64_t>(fs[FS_KEY]), P<int32_t>(fs[FS_ORDV]), P<int32_t>(fs[FS_CALL]),
+                       P<int32_t>(fs[FS_CNZ]), s))
+    return -1;
+  TNP_CHECK(hipMemsetAsync(ctr + CTR_TRI, 0, 2 * sizeof(int64_t), s));
+  if (launch_max_i32(P<int32_t>(fs[FS_CALL]), F, ctr + CTR_TRI, s)) return -1;
+  if (launch_max_i32(P<int32_t>(fs[FS_CNZ]), F, ctr + CTR_FACES, s)) return -1;
+  if (read_ctr(e, s)) return -1;
+  // F5: fan triangles, fan-position-major
+  const int64_t nb = fan_blocks(F);
+  for (int floats = 0; floats < 2; ++floats) {
+    const int32_t* cnt = P<int32_t>(fs[floats ? FS_CNZ : FS_CALL]);
+    int T = (int)e->h_ctr[floats ? CTR_FACES : CTR_TRI] - 2;
+    if (T <= 0) continue;
+    if (buf_ensure(fs[FS_HIST], (int64_t)T * nb * 4, s) || buf_ensure(fs[FS_BASE], (int64_t)T * nb * 8, s))
+      return -1;
+    if (launch_fan_hist(F, cnt, T, P<int32_t>(fs[FS_HIST]), s)) return -1;
+    if (scan_counts(e, P<int32_t>(fs[FS_HIST]), P<int64_t>(fs[FS_BASE]), (int64_t)T * nb, CTR_AUX, s)) return -1;
+    if (read_ctr(e, s)) return -1;
+    int64_t n = e->h_ctr[CTR_AUX];
+    if (floats) {
+      if (buf_ensure(e->faces, std::max<int64_t>(n, 1) * 9 * sizeof(float), s)) return -1;
+      e->n_faces = n;
+    } else {
+      if (buf_ensure(e->tri, std::max<int64_t>(n, 1) * 3 * sizeof(int64_t), s)) return -1;
+      e->n_tri = n;
+    }
+    if (launch_fan_emit(F, frow, P<int32_t>(fs[FS_ORDV]), roff, rcnt, cnt, T, P<int64_t>(fs[FS_BASE]), floats,
+                        xyz, P<int64_t>(e->tri), P<float>(e->faces), s))
+      return -1;
+  }
+  TNP_CHECK(hipStreamSynchronize(s));
+  *n_tri = e->n_tri;
+  *n_faces = e->n_faces;
+  return 0;
+}
+
+extern "C" int tnp_engine_faces_export(tnp_engine* e, int64_t* d_tri, float* d_faces, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  TNP_CHECK(hipSetDevice(e->device));
+  if (d_tri && e->n_tri > 0)
+    TNP_CHECK(hipMemcpyAsync(d_tri, e->tri.p, e->n_tri * 3 * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
+  if (d_faces && e->n_faces > 0)
+    TNP_CHECK(hipMemcpyAsync(d_faces, e->faces.p, e->n_faces * 9 * sizeof(float), hipMemcpyDeviceToDevice, s));
+  return 0;
+}

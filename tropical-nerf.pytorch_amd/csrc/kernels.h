@@ -1,0 +1,45 @@
+// Internal launcher interface between engine.cpp and the .hip kernel files.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/tropical_hip.h"
+
+// Net descriptor passed BY VALUE as a kernel argument (lives in SGPRs /
+// the kernarg segment; every field is wave-uniform).
+struct NetDev {
+  float scales[TNP_MAX_LEVELS];
+  int32_t res[TNP_MAX_LEVELS];
+  uint32_t sizes[TNP_MAX_LEVELS];
+  uint32_t offsets[TNP_MAX_LEVELS];
+  int32_t dense[TNP_MAX_LEVELS];
+  const float* table;
+  const float* weights;
+  const float* marks;
+  int32_t n_levels, num_layers, num_hidden, n_marks;
+  float eps;
+};
+
+static inline int net_K(const NetDev& n) { return (n.num_layers - 1) * n.num_hidden + 1; }
+int net_supported(const NetDev& n);  // 1 if an instantiation exists
+
+// ---- net.hip ----
+// pre plane-major [K][ld]; rows [0, n)
+int launch_forward(const NetDev& net, const float* xyz, int64_t n, float* pre,
+                   int64_t ld, int group, hipStream_t s, float* out2 = nullptr);
+int launch_encode(const NetDev& net, const float* x01, int64_t n, float* out, hipStream_t s);
+// pre plane-major; writes int64 m[n][3+K] and off[n][3] (Net.region)
+int launch_region(const NetDev& net, const float* xyz, const float* pre, int64_t ld,
+                  int64_t n, float eps, int64_t* m, int64_t* off, hipStream_t s);
+int launch_sdf_grad(const NetDev& net, const float* xyz, int64_t n, float* sdf,
+                    float* grad, hipStream_t s);
+// packed keys from pre (planes [0,K)) + grid word from coordinates
+int launch_keys(const NetDev& net, const float* xyz, const float* pre, int64_t ld,
+                int64_t n, int K, uint64_t* pos, uint64_t* zero, uint64_t* grid,
+                hipStream_t s);
+
+// ---- scan.hip ----
+// exclusive scan of int32 counts into int64 offsets; *total (device) = sum
+int scan_i32_to_i64(const int32_t* in, int64_t* out, int64_t n, int64_t* total,
+                    void* scratch, size_t scratch_bytes, hipStream_t s);
+size_t scan_scratch_bytes(int64_t n);

@@ -1,0 +1,224 @@
+// Fused hash-grid encoding + ReLU MLP forward for gfx950, plus the eps-sign
+// region vector, packed sign keys and the analytic SDF input gradient.
+//
+// Reference semantics:
+//   Net.forward(x, gather=True)   tropical/stanford/model.py:52-76
+//   TropicalHashGrid.forward      tropical/tropical.py:46-47 -> tcnn Grid/Hash
+//   Net.region / grid region      model.py:90-103, tropical.py:227-236
+//   Net.sdf / Net.normal          model.py:84-88, 105-123
+//
+// Bitwise contract with the PyTorch-CPU path (oracle/encoding.py,
+// oracle/subdivide.py): the encoding uses the same non-fused op order, and
+// every Linear layer is acc=0; acc=fma(x_k, W_jk, acc) for k ascending, then
+// acc + b_j -- which is what x86 MKL sgemm (torch.nn.Linear on CPU) computes
+// for these shapes (verified bitwise, tests/test_oracle_golden.py).  This
+// file MUST be compiled with -ffp-contract=off; explicit __f*_rn intrinsics
+// pin every rounding anyway.
+//
+// Roofline: one new vertex costs ~200 B of table gathers (L2/MALL resident:
+// 70 kB-5 MB tables) + 12 B coords in + 4K B pre-activations out and
+// ~2 kflop -- bandwidth-bound on the K*4 B store.  The MLP (8->16->16->2) is
+// too narrow for MFMA tiles and its sequential-fma order is part of the
+// parity contract, so it runs on VALU with weights broadcast from LDS.
+#include "common.h"
+#include "kernels.h"
+#include "net_device.h"
+
+using namespace tnpnet;
+
+namespace {
+
+// GROUPED: rows come in groups of 8 consecutive lanes (box corners); a
+// hidden unit is active for the whole group iff corner 0 or corner 7 has a
+// pre-activation > eps (model.py:67-70), else ReLU.
+template <int LV, int H, int NL, bool GROUPED>
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_forward(NetDev net, const float* __restrict__ xyz, int64_t n, float* __restrict__ pre,
+          int64_t ld, float* __restrict__ out2) {
+  constexpr int IN = 2 * LV;
+  constexpr int NW = H * IN + H + (NL - 2) * (H * H + H) + 2 * H + 2;
+  __shared__ float w[NW];
+  for (int i = threadIdx.x; i < NW; i += blockDim.x) w[i] = net.weights[i];
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = i < n;
+  float x[3] = {0.f, 0.f, 0.f};
+  if (live) load_point(xyz, i, x);
+  float h[H > IN ? H : IN];
+  float a[H];
+  encode<LV>(net, x, h);
+  const float* W = w;
+  int p = 0;
+  const int mh = lin_mode(n, false), mo = lin_mode(n, true);
+#pragma unroll
+  for (int layer = 0; layer < NL - 1; ++layer) {
+    if (layer == 0) {
+      linear_mode<IN, H>(W, W + H * IN, h, a, mh);
+      W += H * IN + H;
+    } else {
+      linear_mode<H, H>(W, W + H * H, h, a, mh);
+      W += H * H + H;
+    }
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+      if (live && pre) pre[(int64_t)(p + j) * ld + i] = a[j];
+      if (GROUPED) {
+        const int base = (threadIdx.x & 63) & ~7;
+        float a_first = __shfl(a[j], base, 64);
+        float a_last = __shfl(a[j], base + 7, 64);
+        bool on = (a_first > net.eps) || (a_last > net.eps);
+        h[j] = __fmul_rn(a[j], on ? 1.0f : 0.0f);
+      } else {
+        h[j] = fmaxf(a[j], 0.0f);
+      }
+    }
+    p += H;
+  }
+  float o[2];
+  linear_mode<H, 2>(W, W + 2 * H, h, o, mo);
+  if (live && pre) pre[(int64_t)p * ld + i] = __fsub_rn(o[1], o[0]);
+  if (live && out2) {
+    out2[2 * i] = o[0];
+    out2[2 * i + 1] = o[1];
+  }
+}
+
+// TropicalHashGrid.forward: raw encoding of x already in [0,1]^3 -> [n][2L]
+template <int LV>
+__global__ void k_encode(NetDev net, const float* __restrict__ x01, int64_t n, float* __restrict__ out) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float x[3] = {x01[3 * i], x01[3 * i + 1], x01[3 * i + 2]};
+  float f[2 * LV];
+  encode<LV>(net, x, f);
+#pragma unroll
+  for (int k = 0; k < 2 * LV; ++k) out[i * 2 * LV + k] = f[k];
+}
+
+__global__ void k_region(NetDev net, const float* __restrict__ xyz,
+                         const float* __restrict__ pre, int64_t ld, int64_t n, int K,
+                         float eps, int64_t* __restrict__ m, int64_t* __restrict__ off) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float x[3];
+  load_point(xyz, i, x);
+  uint64_t g = grid_word(net.marks, net.n_marks, eps, x);
+  const int C = 3 + K;
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    m[i * C + d] = tnp::grid_zero(g, d) ? 0 : 1;
+    off[i * 3 + d] = tnp::grid_off(g, d);
+  }
+  for (int p = 0; p < K; ++p) {
+    float v = pre[(int64_t)p * ld + i];
+    m[i * C + 3 + p] = (fabsf(v) <= eps) ? 0 : (v > 0.f ? 1 : -1);
+  }
+}
+
+__global__ void k_keys(NetDev net, const float* __restrict__ xyz, const float* __restrict__ pre,
+                       int64_t ld, int64_t n, int K, uint64_t* __restrict__ pos,
+                       uint64_t* __restrict__ zero, uint64_t* __restrict__ grid) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float x[3];
+  load_point(xyz, i, x);
+  grid[i] = grid_word(net.marks, net.n_marks, net.eps, x);
+  uint64_t ps = 0, zs = 0;
+  for (int p = 0; p < K; ++p) {
+    float v = pre[(int64_t)p * ld + i];
+    ps |= (uint64_t)(v > net.eps) << p;  // sign +1 ((output>0)*2-1 with |.|<=eps -> 0)
+    zs |= (uint64_t)(fabsf(v) <= net.eps) << p;
+  }
+  pos[i] = ps;
+  zero[i] = zs;
+}
+
+// SDF = tanh(o1 - o0) and its input gradient (Net.sdf / Net.normal).
+template <int LV, int H, int NL>
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_sdf_grad(NetDev net, const float* __restrict__ xyz, int64_t n, float* __restrict__ sdf,
+           float* __restrict__ grad) {
+  static_assert(NL == 3, "gradient kernel instantiated for 3-layer nets");
+  constexpr int NW = NetShape<LV, H, NL>::NW;
+  __shared__ float w[NW];
+  for (int i = threadIdx.x; i < NW; i += blockDim.x) w[i] = net.weights[i];
+  __syncthreads();
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float x[3];
+  load_point(xyz, i, x);
+  float g[3];
+  float y = sdf_grad<LV, H>(net, w, x, grad ? g : nullptr);
+  sdf[i] = y;
+  if (grad)
+    for (int d = 0; d < 3; ++d) grad[3 * i + d] = g[d];
+}
+
+}  // namespace
+
+#define TNP_DISPATCH(LV, BODY)                                      \
+  switch (LV) {                                                     \
+    case 2: { constexpr int L_ = 2; BODY; break; }                  \
+    case 4: { constexpr int L_ = 4; BODY; break; }                  \
+    default: tnp_set_error("n_levels=%d not instantiated", LV); return -1; \
+  }
+
+int net_supported(const NetDev& n) {
+  return (n.n_levels == 2 || n.n_levels == 4) && n.num_hidden == 16 && n.num_layers == 3;
+}
+
+int launch_forward(const NetDev& net, const float* xyz, int64_t n, float* pre, int64_t ld,
+                   int group, hipStream_t s, float* out2) {
+  if (n <= 0) return 0;
+  if (!net_supported(net)) { tnp_set_error("unsupported net shape"); return -1; }
+  if (group != 1 && (group != 8 || n % 8)) { tnp_set_error("group must be 1 or 8 (n%%8==0)"); return -1; }
+  TNP_DISPATCH(net.n_levels, {
+    if (group == 8)
+      hipLaunchKernelGGL((k_forward<L_, 16, 3, true>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s,
+                         net, xyz, n, pre, ld, out2);
+    else
+      hipLaunchKernelGGL((k_forward<L_, 16, 3, false>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s,
+                         net, xyz, n, pre, ld, out2);
+  });
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int launch_region(const NetDev& net, const float* xyz, const float* pre, int64_t ld, int64_t n,
+                  float eps, int64_t* m, int64_t* off, hipStream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_region, dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net, xyz, pre, ld, n,
+                     net_K(net), eps, m, off);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int launch_keys(const NetDev& net, const float* xyz, const float* pre, int64_t ld, int64_t n,
+                int K, uint64_t* pos, uint64_t* zero, uint64_t* grid, hipStream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_keys, dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net, xyz, pre, ld, n, K,
+                     pos, zero, grid);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int launch_sdf_grad(const NetDev& net, const float* xyz, int64_t n, float* sdf, float* grad,
+                    hipStream_t s) {
+  if (n <= 0) return 0;
+  if (!net_supported(net)) { tnp_set_error("unsupported net shape"); return -1; }
+  TNP_DISPATCH(net.n_levels, {
+    hipLaunchKernelGGL((k_sdf_grad<L_, 16, 3>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net,
+                       xyz, n, sdf, grad);
+  });
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int launch_encode(const NetDev& net, const float* x01, int64_t n, float* out, hipStream_t s) {
+  if (n <= 0) return 0;
+  TNP_DISPATCH(net.n_levels, {
+    hipLaunchKernelGGL((k_encode<L_>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net, x01, n, out);
+  });
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}

@@ -1,0 +1,247 @@
+// Device-side building blocks of the net evaluation, shared by net.hip
+// (forward / region / keys / gradient kernels) and skeleton.hip.
+// Bitwise contract: see net.hip.
+#pragma once
+#include "common.h"
+#include "kernels.h"
+
+namespace tnpnet {
+
+constexpr uint32_t P1 = 2654435761u;
+constexpr uint32_t P2 = 805459861u;
+
+template <int LV>
+__device__ __forceinline__ void encode(const NetDev& net, const float x[3], float* feat) {
+#pragma unroll
+  for (int l = 0; l < LV; ++l) {
+    const float s = net.scales[l];
+    float t[3];
+    uint32_t g[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      float pos = __fadd_rn(__fmul_rn(x[d], s), 0.5f);
+      float fl = floorf(pos);
+      t[d] = __fsub_rn(pos, fl);
+      g[d] = (uint32_t)(int)fl;
+    }
+    const uint32_t res = (uint32_t)net.res[l];
+    const uint32_t size = net.sizes[l];
+    const bool dense = net.dense[l] != 0;
+    const float2* tab = reinterpret_cast<const float2*>(net.table) + net.offsets[l];
+    float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      float w = 1.0f;
+      uint32_t gc[3];
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        if ((c >> d) & 1) {
+          w = __fmul_rn(w, t[d]);
+          gc[d] = g[d] + 1u;
+        } else {
+          w = __fmul_rn(w, __fsub_rn(1.0f, t[d]));
+          gc[d] = g[d];
+        }
+      }
+      uint32_t idx = dense ? (gc[0] + gc[1] * res + gc[2] * (res * res))
+                           : (gc[0] ^ (gc[1] * P1) ^ (gc[2] * P2));
+      idx %= size;
+      float2 v = tab[idx];
+      a0 = __fadd_rn(a0, __fmul_rn(w, v.x));
+      a1 = __fadd_rn(a1, __fmul_rn(w, v.y));
+    }
+    feat[2 * l] = a0;
+    feat[2 * l + 1] = a1;
+  }
+}
+
+__device__ __forceinline__ void load_point(const float* xyz, int64_t i, float x[3]) {
+  // Net.preprocess: (x + 1) / 2   (model.py:78-79)
+#pragma unroll
+  for (int d = 0; d < 3; ++d) x[d] = __fdiv_rn(__fadd_rn(xyz[3 * i + d], 1.0f), 2.0f);
+}
+
+template <int IN, int OUT>
+__device__ __forceinline__ void linear(const float* __restrict__ W, const float* __restrict__ b,
+                                       const float* in, float* out) {
+#pragma unroll
+  for (int j = 0; j < OUT; ++j) {
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k < IN; ++k) acc = __fmaf_rn(in[k], W[j * IN + k], acc);
+    out[j] = __fadd_rn(acc, b[j]);
+  }
+}
+
+// lower_bound over the sorted marks: torch.searchsorted(marks, v) (left)
+__device__ __forceinline__ int search_left(const float* marks, int M, float v) {
+  int lo = 0, hi = M;
+  while (lo < hi) {
+    int mid = (lo + hi) >> 1;
+    if (marks[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ uint64_t grid_word(const float* marks, int M, float eps,
+                                              const float x[3]) {
+  uint64_t g = 0;
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    int off = search_left(marks, M, __fadd_rn(x[d], eps)) - 1;
+    float mk = marks[off < 0 ? off + M : off];
+    bool zero = !(fabsf(__fsub_rn(mk, x[d])) > eps);
+    g |= (uint64_t)(uint32_t)(off + 2) << (16 * d);
+    g |= (uint64_t)(zero ? 1 : 0) << (48 + d);
+  }
+  return g;
+}
+
+
+// SDF = tanh(o1 - o0) and d SDF / d x (input gradient through ReLU masks and
+// the trilinear encoding; floor() has zero gradient so the cell on the right
+// is used on grid lines, as autograd through tcnn does).  w: packed weights.
+template <int LV, int H>
+__device__ __forceinline__ float sdf_grad(const NetDev& net, const float* w, const float x[3],
+                                          float* grad) {
+  constexpr int IN = 2 * LV;
+  float f[IN], a1[H], h1[H], a2[H], h2[H], o[2];
+  encode<LV>(net, x, f);
+  const float* W0 = w;
+  const float* W1 = W0 + H * IN + H;
+  const float* W2 = W1 + H * H + H;
+  linear<IN, H>(W0, W0 + H * IN, f, a1);
+#pragma unroll
+  for (int j = 0; j < H; ++j) h1[j] = fmaxf(a1[j], 0.f);
+  linear<H, H>(W1, W1 + H * H, h1, a2);
+#pragma unroll
+  for (int j = 0; j < H; ++j) h2[j] = fmaxf(a2[j], 0.f);
+  linear<H, 2>(W2, W2 + 2 * H, h2, o);
+  float y = tanhf(o[1] - o[0]);
+  if (grad == nullptr) return y;
+  float gz = 1.f - y * y;
+  float d2[H], d1[H], df[IN];
+#pragma unroll
+  for (int j = 0; j < H; ++j) {
+    float v = gz * W2[H + j] - gz * W2[j];
+    d2[j] = a2[j] > 0.f ? v : 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < H; ++k) {
+    float v = 0.f;
+#pragma unroll
+    for (int j = 0; j < H; ++j) v += d2[j] * W1[j * H + k];
+    d1[k] = a1[k] > 0.f ? v : 0.f;
+  }
+#pragma unroll
+  for (int m = 0; m < IN; ++m) {
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < H; ++k) v += d1[k] * W0[k * IN + m];
+    df[m] = v;
+  }
+  float gx[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+  for (int l = 0; l < LV; ++l) {
+    const float s = net.scales[l];
+    float t[3];
+    uint32_t g[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      float pos = x[d] * s + 0.5f;
+      float fl = floorf(pos);
+      t[d] = pos - fl;
+      g[d] = (uint32_t)(int)fl;
+    }
+    const uint32_t res = (uint32_t)net.res[l];
+    const float2* tab = reinterpret_cast<const float2*>(net.table) + net.offsets[l];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      float fc[3];
+      uint32_t gc[3];
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        bool up = (c >> d) & 1;
+        fc[d] = up ? t[d] : 1.f - t[d];
+        gc[d] = g[d] + (up ? 1u : 0u);
+      }
+      uint32_t idx = net.dense[l] ? (gc[0] + gc[1] * res + gc[2] * (res * res))
+                                  : (gc[0] ^ (gc[1] * P1) ^ (gc[2] * P2));
+      idx %= net.sizes[l];
+      float2 v = tab[idx];
+      float dv = v.x * df[2 * l] + v.y * df[2 * l + 1];
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        float sg = ((c >> d) & 1) ? 1.f : -1.f;
+        gx[d] += sg * fc[(d + 1) % 3] * fc[(d + 2) % 3] * dv * s;
+      }
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < 3; ++d) grad[d] = gx[d] * 0.5f;  // d/dx of (x+1)/2
+  return y;
+}
+
+// Batch-size-dependent summation schedules of x86 MKL sgemm (what
+// torch.nn.Linear computes on CPU in the reference), reverse-engineered
+// bitwise (oracle/subdivide.py::linear_seqfma, tools/mkl_order_probe.py):
+//   SEQ   acc = 0; acc = fma(x_k, W_jk, acc); acc + b_j
+//   ONE   (a 1-row call) lanes {0, fma(x1,W_j1,x0*W_j0), x2*W_j2, ...},
+//         halving fold, + b_j; the 2-output layer adds x0*W_j0 after the
+//         fold of {0, x1*W_j1, x2*W_j2, ...}
+//   FOLD  (2-output layer, 2..15 rows) halving fold of x_k*W_jk, + b_j
+enum LinMode { LIN_SEQ = 0, LIN_ONE = 1, LIN_FOLD = 2 };
+
+template <int IN>
+__device__ __forceinline__ float fold_lanes(float* l) {
+#pragma unroll
+  for (int h = IN / 2; h >= 1; h /= 2) {
+#pragma unroll
+    for (int i = 0; i < h; ++i) l[i] = __fadd_rn(l[i], l[i + h]);
+  }
+  return l[0];
+}
+
+template <int IN, int OUT>
+__device__ __forceinline__ void linear_mode(const float* __restrict__ W, const float* __restrict__ b,
+                                            const float* in, float* out, int mode) {
+  if (mode == LIN_SEQ) {
+    linear<IN, OUT>(W, b, in, out);
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < OUT; ++j) {
+    float l[IN];
+#pragma unroll
+    for (int k = 0; k < IN; ++k) l[k] = __fmul_rn(in[k], W[j * IN + k]);
+    float r;
+    if (mode == LIN_FOLD) {
+      r = fold_lanes<IN>(l);
+    } else if (OUT == 2) {
+      float p0 = l[0];
+      l[0] = 0.f;
+      r = __fadd_rn(p0, fold_lanes<IN>(l));
+    } else {
+      l[1] = __fmaf_rn(in[1], W[j * IN + 1], l[0]);
+      l[0] = 0.f;
+      r = fold_lanes<IN>(l);
+    }
+    out[j] = __fadd_rn(r, b[j]);
+  }
+}
+
+// per-layer mode for a call on n rows (hidden layers: OUT = H, last: OUT = 2)
+__device__ __forceinline__ int lin_mode(int64_t n, bool last) {
+  if (n == 1) return LIN_ONE;
+  if (last && n <= 15) return LIN_FOLD;
+  return LIN_SEQ;
+}
+
+template <int LV, int H, int NL>
+struct NetShape {
+  static constexpr int IN = 2 * LV;
+  static constexpr int NW = H * IN + H + (NL - 2) * (H * H + H) + 2 * H + 2;
+};
+
+}  // namespace tnpnet

@@ -1,0 +1,224 @@
+// TropicalHashGrid.skeleton(net, unit=128) with PRUNING_MODE="distance"
+// (tropical/tropical.py:113-225) on the device.
+//
+// Per reference tile (starts range(0, L, unit-1), 1-mark overlap):
+//   skel_eval   : |sdf| at every tile lattice point + tile max |grad sdf|
+//   skel_edges  : axis edges (hi, lo) with both |sdf| <= sqrt(3)*2*dmax*gmax,
+//                 x then y then z, meshgrid-ij order (count -> scan -> emit)
+// then squeeze: used global ids p2v(i,j,k) -> dense ranks (sorted unique),
+// vertices = marks[v2p(id)]*2-1 with the reference's float32 v2p division.
+// Duplicate edges on tile overlaps are kept, as in the reference.
+#include "common.h"
+#include "kernels.h"
+#include "net_device.h"
+#include "skeleton.h"
+
+using namespace tnpnet;
+
+namespace {
+
+constexpr int IPT = 8;
+constexpr int TILE = TNP_BLOCK * IPT;
+
+template <int LV, int H>
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_skel_eval(NetDev net, int i0, int j0, int k0, int n0, int n1, int n2,
+            float* __restrict__ dist, unsigned int* __restrict__ gmax_bits) {
+  constexpr int NW = NetShape<LV, H, 3>::NW;
+  __shared__ float w[NW];
+  for (int i = threadIdx.x; i < NW; i += blockDim.x) w[i] = net.weights[i];
+  __syncthreads();
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t n = (int64_t)n0 * n1 * n2;
+  float gn = 0.f;
+  if (t < n) {
+    int k = (int)(t % n2), j = (int)((t / n2) % n1), i = (int)(t / ((int64_t)n1 * n2));
+    int ix[3] = {i0 + i, j0 + j, k0 + k};
+    float x[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      // vertex = marks*2-1 (preprocess_inverse), then preprocess (x+1)/2
+      float v = __fsub_rn(__fmul_rn(net.marks[ix[d]], 2.0f), 1.0f);
+      x[d] = __fdiv_rn(__fadd_rn(v, 1.0f), 2.0f);
+    }
+    float g[3];
+    float y = sdf_grad<LV, H>(net, w, x, g);
+    dist[t] = fabsf(y);
+    gn = sqrtf(g[0] * g[0] + g[1] * g[1] + g[2] * g[2]);
+  }
+  // non-negative floats order like their bit patterns
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) gn = fmaxf(gn, __shfl_xor(gn, o, 64));
+  if (tnp::lane() == 0) atomicMax(gmax_bits, __float_as_uint(gn));
+}
+
+struct TileGeom {
+  int i0, j0, k0, n0, n1, n2, L;
+  int64_t nx, ny, nz;
+};
+
+__device__ __forceinline__ bool skel_edge(const TileGeom& g, const float* dist, float thr, int64_t c,
+                                          int& hi, int& lo) {
+  int a0, a1, a2, b0, b1, b2;  // lo (a) and hi (b) local coords
+  if (c < g.nx) {              // shape (n0-1, n1, n2)
+    a2 = (int)(c % g.n2); a1 = (int)((c / g.n2) % g.n1); a0 = (int)(c / ((int64_t)g.n1 * g.n2));
+    b0 = a0 + 1; b1 = a1; b2 = a2;
+  } else if (c < g.nx + g.ny) {  // shape (n0, n1-1, n2)
+    int64_t r = c - g.nx;
+    a2 = (int)(r % g.n2); a1 = (int)((r / g.n2) % (g.n1 - 1)); a0 = (int)(r / ((int64_t)(g.n1 - 1) * g.n2));
+    b0 = a0; b1 = a1 + 1; b2 = a2;
+  } else {                       // shape (n0, n1, n2-1)
+    int64_t r = c - g.nx - g.ny;
+    a2 = (int)(r % (g.n2 - 1)); a1 = (int)((r / (g.n2 - 1)) % g.n1); a0 = (int)(r / ((int64_t)g.n1 * (g.n2 - 1)));
+    b0 = a0; b1 = a1; b2 = a2 + 1;
+  }
+  float da = dist[((int64_t)a0 * g.n1 + a1) * g.n2 + a2];
+  float db = dist[((int64_t)b0 * g.n1 + b1) * g.n2 + b2];
+  const int64_t LL = (int64_t)g.L * g.L;
+  lo = (int)((g.i0 + a0) * LL + (int64_t)(g.j0 + a1) * g.L + (g.k0 + a2));
+  hi = (int)((g.i0 + b0) * LL + (int64_t)(g.j0 + b1) * g.L + (g.k0 + b2));
+  return (db <= thr) && (da <= thr);
+}
+
+__device__ __forceinline__ float skel_threshold(float dmax, const unsigned int* gmax_bits) {
+  // sqrt(tensor(3.0)) * 2 * len_max * max_grad, left to right in fp32
+  float t = __fmul_rn(sqrtf(3.0f), 2.0f);
+  t = __fmul_rn(t, dmax);
+  return __fmul_rn(t, __uint_as_float(*gmax_bits));
+}
+
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_skel_count(TileGeom g, const float* __restrict__ dist, float dmax,
+             const unsigned int* __restrict__ gmax_bits, int32_t* __restrict__ blk) {
+  __shared__ int lds[TNP_WAVES];
+  const float thr = skel_threshold(dmax, gmax_bits);
+  const int64_t N = g.nx + g.ny + g.nz;
+  int64_t base = (int64_t)blockIdx.x * TILE;
+  int c = 0;
+  for (int k = 0; k < IPT; ++k) {
+    int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
+    int hi, lo;
+    if (i < N) c += skel_edge(g, dist, thr, i, hi, lo);
+  }
+  c = tnp::wave_sum(c);
+  if (tnp::lane() == 0) lds[tnp::wave()] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+    for (int w = 0; w < TNP_WAVES; ++w) t += lds[w];
+    blk[blockIdx.x] = t;
+  }
+}
+
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_skel_emit(TileGeom g, const float* __restrict__ dist, float dmax,
+            const unsigned int* __restrict__ gmax_bits, const int64_t* __restrict__ blkoff,
+            int64_t out_base, int32_t* __restrict__ out, int32_t* __restrict__ used) {
+  __shared__ int lds[TNP_WAVES];
+  const float thr = skel_threshold(dmax, gmax_bits);
+  const int64_t N = g.nx + g.ny + g.nz;
+  int64_t base = (int64_t)blockIdx.x * TILE;
+  int64_t run = out_base + blkoff[blockIdx.x];
+  for (int k = 0; k < IPT; ++k) {
+    int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
+    int hi = 0, lo = 0;
+    bool f = (i < N) && skel_edge(g, dist, thr, i, hi, lo);
+    int tot;
+    int r = tnp::block_rank(f, lds, tot);
+    if (f) {
+      out[2 * (run + r)] = hi;
+      out[2 * (run + r) + 1] = lo;
+      used[hi] = 1;
+      used[lo] = 1;
+    }
+    run += tot;
+  }
+}
+
+__global__ void k_skel_vertices(const int32_t* __restrict__ used, const int64_t* __restrict__ nid,
+                                int64_t n, int L, const float* __restrict__ marks,
+                                float* __restrict__ xyz) {
+  int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= n || !used[v]) return;
+  int64_t r = v;
+  int p[3];
+  const int64_t Lp[3] = {(int64_t)L * L, (int64_t)L, 1};
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    // v_idx.div(L**i).floor().long(): int64 -> float32 true division
+    float q = floorf(__fdiv_rn((float)r, (float)Lp[d]));
+    int64_t qi = (int64_t)q;
+    p[d] = (int)qi;
+    r -= qi * Lp[d];
+  }
+  int64_t o = nid[v];
+#pragma unroll
+  for (int d = 0; d < 3; ++d) xyz[3 * o + d] = __fsub_rn(__fmul_rn(marks[p[d]], 2.0f), 1.0f);
+}
+
+__global__ void k_remap(int32_t* __restrict__ e, int64_t n, const int64_t* __restrict__ nid) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) e[i] = (int32_t)nid[e[i]];
+}
+
+}  // namespace
+
+int launch_skel_eval(const NetDev& net, int i0, int j0, int k0, int n0, int n1, int n2,
+                     float* dist, unsigned int* gmax_bits, hipStream_t s) {
+  int64_t n = (int64_t)n0 * n1 * n2;
+  if (n <= 0) return 0;
+  if (!net_supported(net)) { tnp_set_error("unsupported net shape"); return -1; }
+  if (net.n_levels == 4)
+    hipLaunchKernelGGL((k_skel_eval<4, 16>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net, i0, j0,
+                       k0, n0, n1, n2, dist, gmax_bits);
+  else
+    hipLaunchKernelGGL((k_skel_eval<2, 16>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net, i0, j0,
+                       k0, n0, n1, n2, dist, gmax_bits);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int64_t skel_candidates(int n0, int n1, int n2) {
+  return (int64_t)(n0 - 1) * n1 * n2 + (int64_t)n0 * (n1 - 1) * n2 + (int64_t)n0 * n1 * (n2 - 1);
+}
+
+int64_t skel_tiles(int64_t n) { return (n + TILE - 1) / TILE; }
+
+static TileGeom geom(int i0, int j0, int k0, int n0, int n1, int n2, int L) {
+  TileGeom g{i0, j0, k0, n0, n1, n2, L, (int64_t)(n0 - 1) * n1 * n2,
+             (int64_t)n0 * (n1 - 1) * n2, (int64_t)n0 * n1 * (n2 - 1)};
+  return g;
+}
+
+int launch_skel_edges(bool emit, int i0, int j0, int k0, int n0, int n1, int n2, int L,
+                      const float* dist, float dmax, const unsigned int* gmax_bits, int32_t* blk,
+                      const int64_t* blkoff, int64_t out_base, int32_t* out, int32_t* used,
+                      hipStream_t s) {
+  TileGeom g = geom(i0, j0, k0, n0, n1, n2, L);
+  int64_t N = g.nx + g.ny + g.nz;
+  if (N <= 0) return 0;
+  if (emit)
+    hipLaunchKernelGGL(k_skel_emit, dim3((unsigned)skel_tiles(N)), dim3(TNP_BLOCK), 0, s, g, dist, dmax,
+                       gmax_bits, blkoff, out_base, out, used);
+  else
+    hipLaunchKernelGGL(k_skel_count, dim3((unsigned)skel_tiles(N)), dim3(TNP_BLOCK), 0, s, g, dist,
+                       dmax, gmax_bits, blk);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int launch_skel_vertices(const int32_t* used, const int64_t* nid, int64_t n, int L,
+                         const float* marks, float* xyz, hipStream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_skel_vertices, dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, used, nid, n, L, marks,
+                     xyz);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int launch_remap_i32(int32_t* e, int64_t n, const int64_t* nid, hipStream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_remap, dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, e, n, nid);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}

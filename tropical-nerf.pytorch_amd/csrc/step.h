@@ -1,0 +1,74 @@
+// Internal: step-kernel launchers (step.hip) and device counter slots.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+// slots of the engine's int64 device counter block (one pinned readback)
+enum {
+  CTR_S = 0,        // split count (scan total)
+  CTR_H = 1,        // hit vertices
+  CTR_T = 2,        // cell entries
+  CTR_X = 3,        // connecting edges
+  CTR_E = 4,        // kept edges
+  CTR_V = 5,        // kept vertices
+  CTR_A = 6,        // augmented rows (reference regions_to_vertices size)
+  CTR_P = 7,        // candidate pairs (reference extract_every_valid_edge size)
+  CTR_COMPAT = 8,   // member pairs sharing >= 1 region
+  CTR_TESTS = 9,    // member pairs tested
+  CTR_FAIL = 10,    // local failover-override predicate
+  CTR_K0 = 11,      // some member row has no zero (reference raises)
+  CTR_ACTIVE = 12,  // next-active plane mask (u64 bits)
+  CTR_TRI = 13,
+  CTR_FACES = 14,
+  CTR_AUX = 15,
+  CTR_N = 16
+};
+
+int64_t step_tiles(int64_t n);
+int launch_split_count(const int32_t* edges, int64_t E, const float* col, float eps, int32_t* blk,
+                       hipStream_t s);
+int launch_split_emit(int32_t* edges, int64_t E, const float* col, float eps, const int64_t* blkoff,
+                      int64_t V, int32_t* sa, int32_t* sb, hipStream_t s);
+int launch_new_vertices(const int32_t* sa, const int32_t* sb, int64_t S, const float* col,
+                        float eps, float* xyz, int64_t V, hipStream_t s);
+int launch_fail_check(const int32_t* sa, const int32_t* sb, int64_t S, int idx,
+                      const uint64_t* zero, const float* stage, float eps, uint64_t* shared,
+                      int64_t* ctr, hipStream_t s);
+int launch_finalize_new(int64_t S, int K, int override_, const uint64_t* shared, float* stage,
+                        float eps, float* pre, int64_t ld, int keep_from, int64_t V, uint64_t* pos,
+                        uint64_t* zero, hipStream_t s);
+int launch_hit_count(const float* col, int64_t V, float eps, int32_t* blk, hipStream_t s);
+int launch_hit_emit(const float* col, int64_t V, float eps, const int64_t* blkoff,
+                    int32_t* members, int64_t S, hipStream_t s);
+int launch_cell_count(const int32_t* members, int64_t M, const uint64_t* grid, const uint64_t* zero,
+                      int idx, int NC, int32_t* cellcnt, int64_t* ctr, hipStream_t s);
+int launch_cell_scatter(const int32_t* members, int64_t M, const uint64_t* grid, int NC,
+                        const int64_t* celloff, int32_t* cellcur, int32_t* ent_v, int32_t* ent_c,
+                        hipStream_t s);
+int launch_pairs(bool emit, const int32_t* ent_v, const int32_t* ent_c, int64_t T,
+                 const int64_t* celloff, const int32_t* cellcnt, int NC, int idx,
+                 const uint64_t* pos, const uint64_t* zero, const uint64_t* grid,
+                 int32_t* paircnt, const int64_t* pairoff, int32_t* paircur, int32_t* pair_hi,
+                 int64_t* ctr, hipStream_t s);
+int launch_pair_sort(const int64_t* pairoff, const int32_t* paircnt, int64_t NV, int32_t* pair_hi,
+                     int32_t* pair_lo, hipStream_t s);
+int launch_prune(bool emit, const int32_t* edges, int64_t E, const int32_t* sb, int64_t S,
+                 int64_t V, const int32_t* c_lo, const int32_t* c_hi, int64_t X, int idx,
+                 int prune, int last_plane, const uint64_t* pos, const uint64_t* zero,
+                 int32_t* blk, const int64_t* blkoff, int32_t* out, int32_t* used, int64_t* ctr,
+                 hipStream_t s);
+int launch_gather_vertices(const int32_t* used, const int64_t* nid, int64_t NV, int K,
+                           int keep_from, const float* xyz, const float* pre, int64_t ld,
+                           const uint64_t* pos, const uint64_t* zero, const uint64_t* grid,
+                           float* xyz2, float* pre2, int64_t ld2, uint64_t* pos2, uint64_t* zero2,
+                           uint64_t* grid2, hipStream_t s);
+int launch_remap_edges(int32_t* edges, int64_t E, const int64_t* nid, hipStream_t s);
+int launch_active_planes(const int32_t* edges, int64_t E, int from, int last_plane,
+                         const uint64_t* pos, const uint64_t* zero, int64_t* ctr, hipStream_t s);
+
+// ---- surface.hip ----
+int launch_surface_flags(const float* xyz, const float* col, int64_t V, float eps, int32_t* on,
+                         hipStream_t s);
+int launch_surface_edges(const int32_t* edges, int64_t E, const int32_t* on, int32_t* blk,
+                         const int64_t* blkoff, int emit, int32_t* out, int32_t* used,
+                         hipStream_t s);

@@ -1,0 +1,660 @@
+// One hyperplane step of the subdivision (tropical/subpoly.py:90-279, flat
+// branch) as gfx950 kernels.  Launch order per active step (engine.cpp):
+//
+//   split_count -> scan -> split_emit            order-preserving split
+//   new_vertices -> forward(stage) -> fail_check   coords, MLP, override test
+//   [host: S, global override flag]
+//   finalize_new                                 override + packed keys
+//   hit_count -> scan -> hit_emit                 old vertices on the plane
+//   cell_count -> scan -> cell_scatter            members bucketed by grid cell
+//   pair_count -> scan -> pair_emit -> pair_sort  connecting edges c_new
+//   prune_count -> scan -> prune_emit             future-key pruning
+//   scan(used) -> gather_vertices, remap_edges    vertex compaction
+//
+// Layouts: xyz fp32 [V][3]; pre fp32 plane-major [K][ld]; packed keys per
+// vertex: pos/zero u64 (bit p = plane p), grid u64 (common.h); edges int32
+// [E][2].  Everything that fixes an output ORDER is a scan in input order
+// (the reference's masked_scatter_ / sorted unique semantics); atomics only
+// produce counts and bucket membership, and every bucket is sorted before
+// it is emitted, so results are deterministic and bitwise reproducible.
+#include "common.h"
+#include "kernels.h"
+#include "step.h"
+
+namespace {
+
+constexpr int IPT = 8;                  // items per thread per tile
+constexpr int TILE = TNP_BLOCK * IPT;   // tile of a compaction pass
+
+// ---------------------------------------------------------------------------
+// split test: subpoly.py:102-105
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool split_test(const float* __restrict__ col, const int32_t* e,
+                                           float eps) {
+  float d0 = col[e[0]], d1 = col[e[1]];
+  return (__fmul_rn(d0, d1) < 0.f) && (fabsf(d0) > eps) && (fabsf(d1) > eps);
+}
+
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_split_count(const int32_t* __restrict__ edges, int64_t E, const float* __restrict__ col,
+              float eps, int32_t* __restrict__ blk) {
+  __shared__ int lds[TNP_WAVES];
+  int64_t base = (int64_t)blockIdx.x * TILE;
+  int c = 0;
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
+    if (i < E) c += split_test(col, edges + 2 * i, eps);
+  }
+  c = tnp::wave_sum(c);
+  if (tnp::lane() == 0) lds[tnp::wave()] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+    for (int w = 0; w < TNP_WAVES; ++w) t += lds[w];
+    blk[blockIdx.x] = t;
+  }
+}
+
+// new vertex r gets id V + r in edge order (masked_scatter_, subpoly.py:211)
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_split_emit(int32_t* __restrict__ edges, int64_t E, const float* __restrict__ col, float eps,
+             const int64_t* __restrict__ blkoff, int64_t V, int32_t* __restrict__ sa,
+             int32_t* __restrict__ sb) {
+  __shared__ int lds[TNP_WAVES];
+  int64_t base = (int64_t)blockIdx.x * TILE;
+  int64_t run = blkoff[blockIdx.x];
+  for (int k = 0; k < IPT; ++k) {
+    int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
+    bool f = (i < E) && split_test(col, edges + 2 * i, eps);
+    int tot;
+    int r = tnp::block_rank(f, lds, tot);
+    if (f) {
+      int64_t id = run + r;
+      sa[id] = edges[2 * i];
+      sb[id] = edges[2 * i + 1];
+      edges[2 * i + 1] = (int32_t)(V + id);
+    }
+    run += tot;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// new vertices: subpoly.py:113-117, 180
+//   d = d/eps; w = |d0| / |d1 - d0|; v = e0*(1-w) + e1*w
+// ---------------------------------------------------------------------------
+__global__ void k_new_vertices(const int32_t* __restrict__ sa, const int32_t* __restrict__ sb,
+                               int64_t S, const float* __restrict__ col, float eps,
+                               float* __restrict__ xyz, int64_t V) {
+  int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= S) return;
+  int a = sa[r], b = sb[r];
+  float d0 = __fdiv_rn(col[a], eps), d1 = __fdiv_rn(col[b], eps);
+  float w = __fdiv_rn(fabsf(d0), fabsf(__fsub_rn(d1, d0)));
+  float om = __fsub_rn(1.0f, w);
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    float e0 = xyz[3 * (int64_t)a + d], e1 = xyz[3 * (int64_t)b + d];
+    xyz[3 * (V + r) + d] = __fadd_rn(__fmul_rn(e0, om), __fmul_rn(e1, w));
+  }
+}
+
+// shared planes (subpoly_debug.py:35-42): planes j < idx where both
+// endpoints are eps-zero, plus the current plane idx.  Any new vertex off one
+// of its shared planes by more than eps -> global override flag.
+__global__ void k_fail_check(const int32_t* __restrict__ sa, const int32_t* __restrict__ sb,
+                             int64_t S, int idx, const uint64_t* __restrict__ zero,
+                             const float* __restrict__ stage, float eps,
+                             uint64_t* __restrict__ shared, int64_t* __restrict__ ctr) {
+  int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool bad = false;
+  if (r < S) {
+    uint64_t below = (idx >= 64) ? ~0ull : ((1ull << idx) - 1ull);
+    uint64_t m = (zero[sa[r]] & zero[sb[r]] & below) | (1ull << idx);
+    shared[r] = m;
+    for (uint64_t t = m; t; t &= t - 1) {
+      int p = __builtin_ctzll(t);
+      bad |= fabsf(stage[(int64_t)p * S + r]) > eps;
+    }
+  }
+  if (__ballot(bad) && tnp::lane() == 0) atomicOr((unsigned long long*)&ctr[CTR_FAIL], 1ull);
+}
+
+// override (masked_fill_ on the shared planes, subpoly_debug.py:48), packed
+// keys of the final pre-activations, live planes copied into the cache.
+__global__ void k_finalize_new(int64_t S, int K, int override_, const uint64_t* __restrict__ shared,
+                               float* __restrict__ stage, float eps, float* __restrict__ pre,
+                               int64_t ld, int keep_from, int64_t V, uint64_t* __restrict__ pos,
+                               uint64_t* __restrict__ zero) {
+  int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= S) return;
+  uint64_t m = override_ ? shared[r] : 0ull;
+  uint64_t ps = 0, zs = 0;
+  for (int p = 0; p < K; ++p) {
+    float v = stage[(int64_t)p * S + r];
+    if ((m >> p) & 1) v = 0.f;
+    ps |= (uint64_t)(v > eps) << p;   // sign +1  (pos & zero == 0)
+    zs |= (uint64_t)(fabsf(v) <= eps) << p;
+    if (p >= keep_from) pre[(int64_t)p * ld + V + r] = v;
+  }
+  pos[V + r] = ps;
+  zero[V + r] = zs;
+}
+
+// ---------------------------------------------------------------------------
+// hit vertices: |outputs_[:, idx]| < eps (subpoly.py:233), ascending order
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_hit_count(const float* __restrict__ col, int64_t V, float eps, int32_t* __restrict__ blk) {
+  __shared__ int lds[TNP_WAVES];
+  int64_t base = (int64_t)blockIdx.x * TILE;
+  int c = 0;
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
+    if (i < V) c += fabsf(col[i]) < eps;
+  }
+  c = tnp::wave_sum(c);
+  if (tnp::lane() == 0) lds[tnp::wave()] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+    for (int w = 0; w < TNP_WAVES; ++w) t += lds[w];
+    blk[blockIdx.x] = t;
+  }
+}
+
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_hit_emit(const float* __restrict__ col, int64_t V, float eps, const int64_t* __restrict__ blkoff,
+           int32_t* __restrict__ members, int64_t S) {
+  __shared__ int lds[TNP_WAVES];
+  int64_t base = (int64_t)blockIdx.x * TILE;
+  int64_t run = blkoff[blockIdx.x];
+  for (int k = 0; k < IPT; ++k) {
+    int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
+    bool f = (i < V) && (fabsf(col[i]) < eps);
+    int tot;
+    int r = tnp::block_rank(f, lds, tot);
+    if (f) members[S + run + r] = (int32_t)i;
+    run += tot;
+  }
+}
+
+__global__ void k_new_members(int32_t* __restrict__ members, int64_t S, int64_t V) {
+  int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < S) members[r] = (int32_t)(V + r);
+}
+
+// ---------------------------------------------------------------------------
+// grid cells spanned by a member: per dim {off-1, off} on a mark else {off}
+// (the grid part of regions_to_vertices' augmentation, subpoly.py:327-332)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void cell_span(uint64_t g, int lo[3], int n[3]) {
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    int o = tnp::grid_off(g, d);
+    bool z = tnp::grid_zero(g, d);
+    lo[d] = z ? o - 1 : o;
+    n[d] = z ? 2 : 1;
+  }
+}
+
+__device__ __forceinline__ int64_t cell_id(int cx, int cy, int cz, int NC) {
+  return ((int64_t)(cx + 2) * NC + (cy + 2)) * NC + (cz + 2);
+}
+
+__global__ void k_cell_count(const int32_t* __restrict__ members, int64_t M,
+                             const uint64_t* __restrict__ grid, const uint64_t* __restrict__ zero,
+                             int idx, int NC, int32_t* __restrict__ cellcnt,
+                             int64_t* __restrict__ ctr) {
+  int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t aug = 0;
+  bool k0 = false;
+  if (m < M) {
+    int v = members[m];
+    uint64_t g = grid[v];
+    int lo[3], n[3];
+    cell_span(g, lo, n);
+    for (int i = 0; i < n[0]; ++i)
+      for (int j = 0; j < n[1]; ++j)
+        for (int k = 0; k < n[2]; ++k)
+          atomicAdd(&cellcnt[cell_id(lo[0] + i, lo[1] + j, lo[2] + k, NC)], 1);
+    uint64_t below = (idx >= 64) ? ~0ull : ((1ull << idx) - 1ull);
+    int kz = __popcll(zero[v] & below) + (n[0] - 1) + (n[1] - 1) + (n[2] - 1);
+    aug = 1ll << kz;
+    k0 = kz == 0;
+  }
+  aug = tnp::wave_sum(aug);
+  if (tnp::lane() == 0) atomicAdd((unsigned long long*)&ctr[CTR_A], (unsigned long long)aug);
+  if (__ballot(k0) && tnp::lane() == 0) atomicOr((unsigned long long*)&ctr[CTR_K0], 1ull);
+}
+
+__global__ void k_cell_scatter(const int32_t* __restrict__ members, int64_t M,
+                               const uint64_t* __restrict__ grid, int NC,
+                               const int64_t* __restrict__ celloff, int32_t* __restrict__ cellcur,
+                               int32_t* __restrict__ ent_v, int32_t* __restrict__ ent_c) {
+  int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= M) return;
+  int v = members[m];
+  int lo[3], n[3];
+  cell_span(grid[v], lo, n);
+  for (int i = 0; i < n[0]; ++i)
+    for (int j = 0; j < n[1]; ++j)
+      for (int k = 0; k < n[2]; ++k) {
+        int64_t c = cell_id(lo[0] + i, lo[1] + j, lo[2] + k, NC);
+        int64_t p = celloff[c] + atomicAdd(&cellcur[c], 1);
+        ent_v[p] = v;
+        ent_c[p] = (int32_t)c;
+      }
+}
+
+// ---------------------------------------------------------------------------
+// connecting-edge pair test (subpoly.py:484-535 in closed form).
+// Two members share an augmented region iff, per coordinate, their augmented
+// value sets intersect: grid dim d -> [lo, off] intervals overlap; plane
+// j < idx -> not (both non-zero with opposite signs).  The reference keeps
+// the pair iff they share >= 1 zero plane (grid zeros only with equal
+// offsets).  Each pair is emitted once, in the canonical cell
+// (per-dim max of the two interval lows).
+// ---------------------------------------------------------------------------
+struct PairTest {
+  bool emit;
+  bool compat;
+  int64_t regions;  // shared regions (for the reference's candidate count P)
+};
+
+__device__ __forceinline__ PairTest pair_test(int u, int v, int64_t cell, int NC, uint64_t below,
+                                              const uint64_t* __restrict__ pos,
+                                              const uint64_t* __restrict__ zero,
+                                              const uint64_t* __restrict__ grid) {
+  PairTest t{false, false, 0};
+  uint64_t gu = grid[u], gv = grid[v];
+  int cz = (int)(cell % NC) - 2;
+  int cy = (int)((cell / NC) % NC) - 2;
+  int cx = (int)(cell / ((int64_t)NC * NC)) - 2;
+  int cc[3] = {cx, cy, cz};
+  int64_t reg = 1;
+  bool grid_share = false;
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    int ou = tnp::grid_off(gu, d), ov = tnp::grid_off(gv, d);
+    bool zu = tnp::grid_zero(gu, d), zv = tnp::grid_zero(gv, d);
+    int lu = zu ? ou - 1 : ou, lv = zv ? ov - 1 : ov;
+    int lo = lu > lv ? lu : lv;
+    int hi = ou < ov ? ou : ov;
+    if (cc[d] != lo) return t;  // not the canonical cell (or no overlap)
+    reg *= (hi - lo + 1);
+    grid_share |= zu && zv && (ou == ov);
+  }
+  uint64_t pu = pos[u], pv = pos[v], zu = zero[u], zv = zero[v];
+  if (((pu ^ pv) & ~zu & ~zv & below) != 0) return t;
+  t.compat = true;
+  t.regions = reg << __popcll(zu & zv & below);
+  t.emit = grid_share || ((zu & zv & below) != 0);
+  return t;
+}
+
+template <bool EMIT>
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_pairs(const int32_t* __restrict__ ent_v, const int32_t* __restrict__ ent_c, int64_t T,
+        const int64_t* __restrict__ celloff, const int32_t* __restrict__ cellcnt, int NC, int idx,
+        const uint64_t* __restrict__ pos, const uint64_t* __restrict__ zero,
+        const uint64_t* __restrict__ grid, int32_t* __restrict__ paircnt,
+        const int64_t* __restrict__ pairoff, int32_t* __restrict__ paircur,
+        int32_t* __restrict__ pair_hi, int64_t* __restrict__ ctr) {
+  int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t n_compat = 0, n_reg = 0, n_test = 0;
+  if (e < T) {
+    int u = ent_v[e];
+    int64_t c = ent_c[e];
+    int64_t start = celloff[c], end = start + cellcnt[c];
+    uint64_t below = (idx >= 64) ? ~0ull : ((1ull << idx) - 1ull);
+    for (int64_t q = e + 1; q < end; ++q) {
+      int v = ent_v[q];
+      PairTest t = pair_test(u, v, c, NC, below, pos, zero, grid);
+      n_test++;
+      if (!t.compat) continue;
+      n_compat++;
+      n_reg += t.regions;
+      if (!t.emit) continue;
+      int lo = u < v ? u : v, hi = u < v ? v : u;
+      if (EMIT) {
+        int64_t p = pairoff[lo] + atomicAdd(&paircur[lo], 1);
+        pair_hi[p] = hi;
+      } else {
+        atomicAdd(&paircnt[lo], 1);
+      }
+    }
+    (void)start;
+  }
+  if (!EMIT) {
+    n_compat = tnp::wave_sum(n_compat);
+    n_reg = tnp::wave_sum(n_reg);
+    n_test = tnp::wave_sum(n_test);
+    if (tnp::lane() == 0) {
+      atomicAdd((unsigned long long*)&ctr[CTR_COMPAT], (unsigned long long)n_compat);
+      atomicAdd((unsigned long long*)&ctr[CTR_P], (unsigned long long)n_reg);
+      atomicAdd((unsigned long long*)&ctr[CTR_TESTS], (unsigned long long)n_test);
+    }
+  }
+}
+
+// sort each lo-bucket by hi (shell sort; buckets are small, but degenerate
+// regions can make a few large ones) and record lo per pair
+__global__ void k_pair_sort(const int64_t* __restrict__ pairoff, const int32_t* __restrict__ paircnt,
+                            int64_t NV, int32_t* __restrict__ pair_hi, int32_t* __restrict__ pair_lo) {
+  int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= NV) return;
+  int n = paircnt[v];
+  if (n == 0) return;
+  int32_t* a = pair_hi + pairoff[v];
+  int gap = 1;
+  while (gap < n / 3) gap = 3 * gap + 1;
+  for (; gap > 0; gap /= 3) {
+    for (int i = gap; i < n; ++i) {
+      int32_t x = a[i];
+      int j = i;
+      while (j >= gap && a[j - gap] > x) {
+        a[j] = a[j - gap];
+        j -= gap;
+      }
+      a[j] = x;
+    }
+  }
+  int32_t* lo = pair_lo + pairoff[v];
+  for (int i = 0; i < n; ++i) lo[i] = (int32_t)v;
+}
+
+// ---------------------------------------------------------------------------
+// pruning: keep an edge iff its endpoints' future sign keys (planes >= idx)
+// differ (subpoly.py:252-265).  The candidate list is the concatenation
+// [edges (split ones already rewired); e_new; c_new].
+// ---------------------------------------------------------------------------
+struct EdgeSrc {
+  const int32_t* edges;  int64_t E;
+  const int32_t* sb;     int64_t S;  int64_t V;
+  const int32_t* c_lo;   const int32_t* c_hi; int64_t X;
+};
+
+__device__ __forceinline__ void fetch_edge(const EdgeSrc& s, int64_t i, int& a, int& b) {
+  if (i < s.E) {
+    a = s.edges[2 * i];
+    b = s.edges[2 * i + 1];
+  } else if (i < s.E + s.S) {
+    int64_t r = i - s.E;
+    a = s.sb[r];
+    b = (int)(s.V + r);
+  } else {
+    int64_t x = i - s.E - s.S;
+    a = s.c_lo[x];
+    b = s.c_hi[x];
+  }
+}
+
+__device__ __forceinline__ bool keep_edge(int a, int b, uint64_t fmask, const uint64_t* pos,
+                                          const uint64_t* zero) {
+  return ((pos[a] ^ pos[b]) & fmask) != 0 || ((zero[a] ^ zero[b]) & fmask) != 0;
+}
+
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_prune_count(EdgeSrc src, int64_t N, uint64_t fmask, const uint64_t* __restrict__ pos,
+              const uint64_t* __restrict__ zero, int32_t* __restrict__ blk) {
+  __shared__ int lds[TNP_WAVES];
+  int64_t base = (int64_t)blockIdx.x * TILE;
+  int c = 0;
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
+    if (i < N) {
+      int a, b;
+      fetch_edge(src, i, a, b);
+      c += keep_edge(a, b, fmask, pos, zero);
+    }
+  }
+  c = tnp::wave_sum(c);
+  if (tnp::lane() == 0) lds[tnp::wave()] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+    for (int w = 0; w < TNP_WAVES; ++w) t += lds[w];
+    blk[blockIdx.x] = t;
+  }
+}
+
+// emits kept edges in order, flags used vertices and ORs the next-active
+// plane mask: planes > idx on which a kept edge has non-zero opposite signs
+// (exactly the split test of that future step, subpoly.py:104-105).
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_prune_emit(EdgeSrc src, int64_t N, uint64_t fmask, uint64_t amask,
+             const uint64_t* __restrict__ pos, const uint64_t* __restrict__ zero,
+             const int64_t* __restrict__ blkoff, int prune, int32_t* __restrict__ out,
+             int32_t* __restrict__ used, int64_t* __restrict__ ctr) {
+  __shared__ int lds[TNP_WAVES];
+  int64_t base = (int64_t)blockIdx.x * TILE;
+  int64_t run = prune ? blkoff[blockIdx.x] : base;
+  uint64_t act = 0;
+  for (int k = 0; k < IPT; ++k) {
+    int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
+    int a = 0, b = 0;
+    bool f = false;
+    if (i < N) {
+      fetch_edge(src, i, a, b);
+      f = !prune || keep_edge(a, b, fmask, pos, zero);
+    }
+    if (prune) {
+      int tot;
+      int r = tnp::block_rank(f, lds, tot);
+      if (f) {
+        out[2 * (run + r)] = a;
+        out[2 * (run + r) + 1] = b;
+      }
+      run += tot;
+    } else if (f) {
+      out[2 * i] = a;
+      out[2 * i + 1] = b;
+    }
+    if (f) {
+      if (used) {
+        used[a] = 1;
+        used[b] = 1;
+      }
+      uint64_t za = zero[a], zb = zero[b];
+      act |= (pos[a] ^ pos[b]) & ~za & ~zb & amask;
+    }
+  }
+  act = tnp::wave_or(act);
+  if (tnp::lane() == 0 && act) atomicOr((unsigned long long*)&ctr[CTR_ACTIVE], act);
+}
+
+__global__ void k_gather_vertices(const int32_t* __restrict__ used, const int64_t* __restrict__ nid,
+                                  int64_t NV, int K, int keep_from,
+                                  const float* __restrict__ xyz, const float* __restrict__ pre,
+                                  int64_t ld, const uint64_t* __restrict__ pos,
+                                  const uint64_t* __restrict__ zero, const uint64_t* __restrict__ grid,
+                                  float* __restrict__ xyz2, float* __restrict__ pre2, int64_t ld2,
+                                  uint64_t* __restrict__ pos2, uint64_t* __restrict__ zero2,
+                                  uint64_t* __restrict__ grid2) {
+  int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= NV || !used[v]) return;
+  int64_t n = nid[v];
+#pragma unroll
+  for (int d = 0; d < 3; ++d) xyz2[3 * n + d] = xyz[3 * v + d];
+  for (int p = keep_from; p < K; ++p) pre2[(int64_t)p * ld2 + n] = pre[(int64_t)p * ld + v];
+  pos2[n] = pos[v];
+  zero2[n] = zero[v];
+  grid2[n] = grid[v];
+}
+
+__global__ void k_remap_edges(int32_t* __restrict__ edges, int64_t E, const int64_t* __restrict__ nid) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 2 * E) return;
+  edges[i] = (int32_t)nid[edges[i]];
+}
+
+// initial next-active mask for an arbitrary edge set
+__global__ void k_active_planes(const int32_t* __restrict__ edges, int64_t E, uint64_t amask,
+                                const uint64_t* __restrict__ pos, const uint64_t* __restrict__ zero,
+                                int64_t* __restrict__ ctr) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t act = 0;
+  if (i < E) {
+    int a = edges[2 * i], b = edges[2 * i + 1];
+    act = (pos[a] ^ pos[b]) & ~zero[a] & ~zero[b] & amask;
+  }
+  act = tnp::wave_or(act);
+  if (tnp::lane() == 0 && act) atomicOr((unsigned long long*)&ctr[CTR_ACTIVE], act);
+}
+
+}  // namespace
+
+// ----------------------------------------------------------------------------
+// launchers
+// ----------------------------------------------------------------------------
+int64_t step_tiles(int64_t n) { return (n + TILE - 1) / TILE; }
+
+int launch_split_count(const int32_t* edges, int64_t E, const float* col, float eps, int32_t* blk,
+                       hipStream_t s) {
+  hipLaunchKernelGGL(k_split_count, dim3((unsigned)step_tiles(E)), dim3(TNP_BLOCK), 0, s, edges,
+                     E, col, eps, blk);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_split_emit(int32_t* edges, int64_t E, const float* col, float eps, const int64_t* blkoff,
+                      int64_t V, int32_t* sa, int32_t* sb, hipStream_t s) {
+  hipLaunchKernelGGL(k_split_emit, dim3((unsigned)step_tiles(E)), dim3(TNP_BLOCK), 0, s, edges, E,
+                     col, eps, blkoff, V, sa, sb);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_new_vertices(const int32_t* sa, const int32_t* sb, int64_t S, const float* col,
+                        float eps, float* xyz, int64_t V, hipStream_t s) {
+  if (S <= 0) return 0;
+  hipLaunchKernelGGL(k_new_vertices, dim3(tnp_grid(S)), dim3(TNP_BLOCK), 0, s, sa, sb, S, col, eps,
+                     xyz, V);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_fail_check(const int32_t* sa, const int32_t* sb, int64_t S, int idx,
+                      const uint64_t* zero, const float* stage, float eps, uint64_t* shared,
+                      int64_t* ctr, hipStream_t s) {
+  if (S <= 0) return 0;
+  hipLaunchKernelGGL(k_fail_check, dim3(tnp_grid(S)), dim3(TNP_BLOCK), 0, s, sa, sb, S, idx, zero,
+                     stage, eps, shared, ctr);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_finalize_new(int64_t S, int K, int override_, const uint64_t* shared, float* stage,
+                        float eps, float* pre, int64_t ld, int keep_from, int64_t V, uint64_t* pos,
+                        uint64_t* zero, hipStream_t s) {
+  if (S <= 0) return 0;
+  hipLaunchKernelGGL(k_finalize_new, dim3(tnp_grid(S)), dim3(TNP_BLOCK), 0, s, S, K, override_,
+                     shared, stage, eps, pre, ld, keep_from, V, pos, zero);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_hit_count(const float* col, int64_t V, float eps, int32_t* blk, hipStream_t s) {
+  hipLaunchKernelGGL(k_hit_count, dim3((unsigned)step_tiles(V)), dim3(TNP_BLOCK), 0, s, col, V,
+                     eps, blk);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_hit_emit(const float* col, int64_t V, float eps, const int64_t* blkoff,
+                    int32_t* members, int64_t S, hipStream_t s) {
+  hipLaunchKernelGGL(k_hit_emit, dim3((unsigned)step_tiles(V)), dim3(TNP_BLOCK), 0, s, col, V, eps,
+                     blkoff, members, S);
+  if (S > 0)
+    hipLaunchKernelGGL(k_new_members, dim3(tnp_grid(S)), dim3(TNP_BLOCK), 0, s, members, S, V);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_cell_count(const int32_t* members, int64_t M, const uint64_t* grid, const uint64_t* zero,
+                      int idx, int NC, int32_t* cellcnt, int64_t* ctr, hipStream_t s) {
+  if (M <= 0) return 0;
+  hipLaunchKernelGGL(k_cell_count, dim3(tnp_grid(M)), dim3(TNP_BLOCK), 0, s, members, M, grid,
+                     zero, idx, NC, cellcnt, ctr);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_cell_scatter(const int32_t* members, int64_t M, const uint64_t* grid, int NC,
+                        const int64_t* celloff, int32_t* cellcur, int32_t* ent_v, int32_t* ent_c,
+                        hipStream_t s) {
+  if (M <= 0) return 0;
+  hipLaunchKernelGGL(k_cell_scatter, dim3(tnp_grid(M)), dim3(TNP_BLOCK), 0, s, members, M, grid,
+                     NC, celloff, cellcur, ent_v, ent_c);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_pairs(bool emit, const int32_t* ent_v, const int32_t* ent_c, int64_t T,
+                 const int64_t* celloff, const int32_t* cellcnt, int NC, int idx,
+                 const uint64_t* pos, const uint64_t* zero, const uint64_t* grid,
+                 int32_t* paircnt, const int64_t* pairoff, int32_t* paircur, int32_t* pair_hi,
+                 int64_t* ctr, hipStream_t s) {
+  if (T <= 0) return 0;
+  if (emit)
+    hipLaunchKernelGGL(k_pairs<true>, dim3(tnp_grid(T)), dim3(TNP_BLOCK), 0, s, ent_v, ent_c, T,
+                       celloff, cellcnt, NC, idx, pos, zero, grid, paircnt, pairoff, paircur,
+                       pair_hi, ctr);
+  else
+    hipLaunchKernelGGL(k_pairs<false>, dim3(tnp_grid(T)), dim3(TNP_BLOCK), 0, s, ent_v, ent_c, T,
+                       celloff, cellcnt, NC, idx, pos, zero, grid, paircnt, pairoff, paircur,
+                       pair_hi, ctr);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_pair_sort(const int64_t* pairoff, const int32_t* paircnt, int64_t NV, int32_t* pair_hi,
+                     int32_t* pair_lo, hipStream_t s) {
+  if (NV <= 0) return 0;
+  hipLaunchKernelGGL(k_pair_sort, dim3(tnp_grid(NV)), dim3(TNP_BLOCK), 0, s, pairoff, paircnt, NV,
+                     pair_hi, pair_lo);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_prune(bool emit, const int32_t* edges, int64_t E, const int32_t* sb, int64_t S,
+                 int64_t V, const int32_t* c_lo, const int32_t* c_hi, int64_t X, int idx,
+                 int prune, int last_plane, const uint64_t* pos, const uint64_t* zero,
+                 int32_t* blk, const int64_t* blkoff, int32_t* out, int32_t* used, int64_t* ctr,
+                 hipStream_t s) {
+  EdgeSrc src{edges, E, sb, S, V, c_lo, c_hi, X};
+  int64_t N = E + S + X;
+  if (N <= 0) return 0;
+  uint64_t fmask = (idx >= 64) ? 0ull : (~0ull << idx);
+  if (last_plane < 63) fmask &= (1ull << (last_plane + 1)) - 1ull;
+  uint64_t amask = (idx + 1 >= 64) ? 0ull : (~0ull << (idx + 1));
+  if (last_plane < 63) amask &= (1ull << (last_plane + 1)) - 1ull;
+  if (!emit)
+    hipLaunchKernelGGL(k_prune_count, dim3((unsigned)step_tiles(N)), dim3(TNP_BLOCK), 0, s, src, N,
+                       fmask, pos, zero, blk);
+  else
+    hipLaunchKernelGGL(k_prune_emit, dim3((unsigned)step_tiles(N)), dim3(TNP_BLOCK), 0, s, src, N,
+                       fmask, amask, pos, zero, blkoff, prune, out, used, ctr);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_gather_vertices(const int32_t* used, const int64_t* nid, int64_t NV, int K,
+                           int keep_from, const float* xyz, const float* pre, int64_t ld,
+                           const uint64_t* pos, const uint64_t* zero, const uint64_t* grid,
+                           float* xyz2, float* pre2, int64_t ld2, uint64_t* pos2, uint64_t* zero2,
+                           uint64_t* grid2, hipStream_t s) {
+  if (NV <= 0) return 0;
+  hipLaunchKernelGGL(k_gather_vertices, dim3(tnp_grid(NV)), dim3(TNP_BLOCK), 0, s, used, nid, NV,
+                     K, keep_from, xyz, pre, ld, pos, zero, grid, xyz2, pre2, ld2, pos2, zero2,
+                     grid2);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_remap_edges(int32_t* edges, int64_t E, const int64_t* nid, hipStream_t s) {
+  if (E <= 0) return 0;
+  hipLaunchKernelGGL(k_remap_edges, dim3(tnp_grid(2 * E)), dim3(TNP_BLOCK), 0, s, edges, E, nid);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_active_planes(const int32_t* edges, int64_t E, int from, int last_plane,
+                         const uint64_t* pos, const uint64_t* zero, int64_t* ctr, hipStream_t s) {
+  if (E <= 0) return 0;
+  uint64_t amask = (from >= 64) ? 0ull : (~0ull << from);
+  if (last_plane < 63) amask &= (1ull << (last_plane + 1)) - 1ull;
+  hipLaunchKernelGGL(k_active_planes, dim3(tnp_grid(E)), dim3(TNP_BLOCK), 0, s, edges, E, amask,
+                     pos, zero, ctr);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}

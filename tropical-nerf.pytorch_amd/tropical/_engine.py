@@ -1,0 +1,163 @@
+"""Python handle on the device-resident extraction engine (tnp_engine_*).
+
+The engine keeps the polyhedral complex (vertices, edges, the plane-major
+pre-activation cache and packed eps-sign keys) in HBM across all hyperplane
+steps; Python only sequences the steps and reads back the sizes the next
+allocation needs.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import weakref
+
+import numpy as np
+import torch
+
+from . import _hip
+
+
+class Engine:
+    def __init__(self, device: torch.device):
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise RuntimeError("Engine needs a ROCm GPU device")
+        h = C.c_void_p()
+        idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        self.device = torch.device("cuda", idx)
+        with torch.cuda.device(idx):
+            _hip.check(_hip.lib().tnp_engine_create(C.byref(h), idx), "tnp_engine_create")
+        self.h = h
+        self._keep = None
+        self.K = None
+        self._fin = weakref.finalize(self, _hip.lib().tnp_engine_destroy, h)
+
+    @property
+    def _s(self):
+        return C.c_void_p(_hip.stream_ptr(self.device))
+
+    def set_net(self, net):
+        s, keep = net.tnp_desc()
+        self._keep = (s, keep)  # the engine reads these device buffers later
+        self.K = net.K
+        self.num_hidden = net.num_hidden
+        self.num_layers = net.num_layers
+        _hip.check(_hip.lib().tnp_engine_set_net(self.h, C.byref(s)), "tnp_engine_set_net")
+        return self
+
+    # -- complex I/O ---------------------------------------------------------
+    def load(self, vertices: torch.Tensor, edges: torch.Tensor, pre: torch.Tensor = None,
+             keep_all: bool = False):
+        v = vertices.detach().to(self.device, torch.float32).contiguous()
+        e = edges.detach().to(self.device, torch.int64).contiguous()
+        p = None if pre is None else pre.detach().to(self.device, torch.float32).contiguous()
+        _hip.check(_hip.lib().tnp_engine_load(self.h, _hip.ptr(v), v.shape[0], _hip.ptr(e),
+                                              e.shape[0], _hip.ptr(p), int(keep_all), self._s),
+                   "tnp_engine_load")
+        return v.shape[0], e.shape[0]
+
+    def lattice(self, x0: int = 0, x1: int = -1, keep_all: bool = False):
+        n_marks = int(self._keep[0].n_marks)
+        x1 = n_marks - 1 if x1 < 0 else x1
+        V, E = C.c_int64(), C.c_int64()
+        _hip.check(_hip.lib().tnp_engine_lattice(self.h, x0, x1, int(keep_all), self._s,
+                                                 C.byref(V), C.byref(E)), "tnp_engine_lattice")
+        return V.value, E.value
+
+    def skeleton(self, unit: int = 128, size: float = None):
+        V, E = C.c_int64(), C.c_int64()
+        _hip.check(_hip.lib().tnp_engine_skeleton(self.h, unit, float(size or 0.0), self._s,
+                                                  C.byref(V), C.byref(E)), "tnp_engine_skeleton")
+        return V.value, E.value
+
+    def sizes(self):
+        V, E = C.c_int64(), C.c_int64()
+        _hip.check(_hip.lib().tnp_engine_sizes(self.h, C.byref(V), C.byref(E)), "tnp_engine_sizes")
+        return V.value, E.value
+
+    def export(self, pre: bool = False):
+        V, E = self.sizes()
+        verts = torch.empty(V, 3, device=self.device)
+        edges = torch.empty(E, 2, dtype=torch.int64, device=self.device)
+        cache = torch.empty(V, self.K, device=self.device) if pre else None
+        _hip.check(_hip.lib().tnp_engine_export(self.h, _hip.ptr(verts), _hip.ptr(edges),
+                                                _hip.ptr(cache), self._s), "tnp_engine_export")
+        return verts, edges, cache
+
+    # -- steps ---------------------------------------------------------------
+    def active_planes(self, start: int = 0) -> int:
+        m = C.c_uint64()
+        _hip.check(_hip.lib().tnp_engine_active_planes(self.h, start, C.byref(m), self._s),
+                   "tnp_engine_active_planes")
+        return m.value
+
+    def split(self, idx: int):
+        S, fail = C.c_int64(), C.c_int32()
+        _hip.check(_hip.lib().tnp_engine_split(self.h, idx, self._s, C.byref(S), C.byref(fail)),
+                   "tnp_engine_split")
+        return S.value, bool(fail.value)
+
+    def finish(self, idx: int, prune: bool, override: bool) -> dict:
+        st = _hip.TnpStepStats()
+        _hip.check(_hip.lib().tnp_engine_finish(self.h, idx, int(prune), int(override), self._s,
+                                                C.byref(st)), "tnp_engine_finish")
+        return st.as_dict()
+
+    def surface(self):
+        V, E = C.c_int64(), C.c_int64()
+        _hip.check(_hip.lib().tnp_engine_surface(self.h, self._s, C.byref(V), C.byref(E)),
+                   "tnp_engine_surface")
+        return V.value, E.value
+
+    def faces(self):
+        nt, nf = C.c_int64(), C.c_int64()
+        _hip.check(_hip.lib().tnp_engine_faces(self.h, self._s, C.byref(nt), C.byref(nf)),
+                   "tnp_engine_faces")
+        tri = torch.empty(nt.value, 3, dtype=torch.int64, device=self.device)
+        fc = torch.empty(nf.value, 3, 3, device=self.device)
+        _hip.check(_hip.lib().tnp_engine_faces_export(self.h, _hip.ptr(tri), _hip.ptr(fc), self._s),
+                   "tnp_engine_faces_export")
+        return tri, fc
+
+    # -- the hot loop (subpoly.py:58-69) -------------------------------------
+    def run_steps(self, stats: list = None, allreduce=None):
+        """All hyperplane steps with empty steps skipped (they have no side
+        effects, subpoly.py:110).  ``allreduce(vec, op)`` (multi-GPU) makes
+        the split count, the override predicate and the active mask global."""
+        K, H = self.K, self.num_hidden
+        mask = self.active_planes(0)
+        if allreduce is not None:
+            mask = int(allreduce(np.array([mask], dtype=np.uint64), "or")[0])
+        for idx in range(K):
+            if not (mask >> idx) & 1:
+                continue
+            S, fail = self.split(idx)
+            if allreduce is not None:
+                g = allreduce(np.array([S, int(fail)], dtype=np.int64), "max")
+                S_glob, fail = int(g[0]), bool(g[1])
+            else:
+                S_glob = S
+            if S_glob == 0:
+                continue
+            prune = idx < K - 1  # h == num_hidden (final step) never prunes
+            st = self.finish(idx, prune, fail)
+            if stats is not None:
+                stats.append(st)
+            if prune:
+                m2 = st["next_active"]
+                if allreduce is not None:
+                    m2 = int(allreduce(np.array([m2], dtype=np.uint64), "or")[0])
+                mask = (mask & ((1 << (idx + 1)) - 1)) | m2
+        return stats
+
+
+_ENGINES = {}
+
+
+def engine_for(net) -> Engine:
+    dev = net.device()
+    key = (dev.index if dev.index is not None else torch.cuda.current_device())
+    eng = _ENGINES.get(key)
+    if eng is None:
+        eng = Engine(torch.device("cuda", key))
+        _ENGINES[key] = eng
+    return eng.set_net(net)

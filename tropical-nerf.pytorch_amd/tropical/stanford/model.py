@@ -1,0 +1,136 @@
+"""Net: the piecewise-trilinear SDF network of the reference
+(tropical/stanford/model.py:18-135), MI355X-native.
+
+Same constructor, attributes (``enc``, ``fc``, ``num_layers``,
+``num_hidden``, ``num_nodes``, ``eps``, ``scale``), state_dict keys
+(``enc.module.params``, ``fc.{i}.weight``, ``fc.{i}.bias``) and methods
+(``forward(x, gather, group)``, ``preprocess``, ``preprocess_inverse``,
+``sdf``, ``region``, ``normal``).  Every evaluation is a fused HIP kernel
+(encoding + MLP, csrc/net.hip) on the net's ROCm device; the forward is
+bitwise equal to the reference's PyTorch-CPU evaluation.  Training
+(autograd through the hash grid) is out of scope for this build
+(DESIGN.md), so these ops are inference-only.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+import torch.nn as nn
+from torch import Tensor
+
+from .. import _hip
+from ..tropical import TropicalHashGrid
+
+
+class Net(nn.Module):
+    def __init__(self, num_layers: int = 3, num_hidden: int = 16, levels: int = 4,
+                 r_min: int = 2, r_max: int = 32, T: int = 19, eps: float = 1e-4):
+        super().__init__()
+        self.num_layers = num_layers
+        self.num_hidden = num_hidden
+        self.eps = eps
+        self.scale = 1
+        self.enc = TropicalHashGrid(1.0, 3, levels, 2, T, r_min, r_max, eps)
+        self.num_nodes = [levels * 2] + [num_hidden] * (num_layers - 1) + [2]
+        self.fc = nn.ModuleList(nn.Linear(a, b) for a, b in
+                                zip(self.num_nodes[:-1], self.num_nodes[1:]))
+
+    @property
+    def K(self) -> int:
+        return (self.num_layers - 1) * self.num_hidden + 1
+
+    def device(self):
+        return next(self.parameters()).device
+
+    # -- C ABI descriptor ----------------------------------------------------
+    def tnp_desc(self):
+        """(tnp_net struct, keep-alive tensors) for the current parameters."""
+        dev = self.device()
+        if dev.type != "cuda":
+            raise RuntimeError("Net: move the net to a ROCm GPU (.cuda()); the tropical HIP "
+                               "path has no CPU fallback")
+        s = _hip.TnpNet()
+        self.enc.tnp_fields(s)
+        s.num_layers, s.num_hidden, s.eps = self.num_layers, self.num_hidden, float(self.eps)
+        table = self.enc.module.params.detach().float().contiguous()
+        w = torch.cat([t.detach().float().reshape(-1) for lin in self.fc
+                       for t in (lin.weight, lin.bias)]).contiguous()
+        marks = self.enc.marks.to(dev).contiguous()
+        s.d_table, s.d_weights, s.d_marks = table.data_ptr(), w.data_ptr(), marks.data_ptr()
+        return s, (table, w, marks)
+
+    # -- evaluation ----------------------------------------------------------
+    def _forward_planes(self, x: Tensor, group: int = 1, want_out: bool = False):
+        _hip.require_cuda(x, "Net.forward")
+        s, keep = self.tnp_desc()
+        x = x.detach().float().contiguous()
+        n = x.shape[0]
+        pre = torch.empty(self.K, n, device=x.device)
+        out2 = torch.empty(n, 2, device=x.device) if want_out else None
+        fn = _hip.lib().tnp_forward_grouped if group == 8 else _hip.lib().tnp_forward
+        if group not in (1, 8):
+            raise NotImplementedError("group must be 1 or 8 (box corners)")
+        _hip.check(fn(ctypes.byref(s), _hip.ptr(x), n, _hip.ptr(pre), n, _hip.ptr(out2),
+                      ctypes.c_void_p(_hip.stream_ptr(x.device))), "tnp_forward")
+        del keep
+        return pre, out2
+
+    def forward(self, x, gather: bool = False, group: int = 1):
+        pre, out = self._forward_planes(x, group, want_out=True)
+        if not gather:
+            return out
+        H = self.num_hidden
+        cols = pre.t()
+        inputs = [cols[:, i * H:(i + 1) * H] for i in range(self.num_layers - 1)]
+        inputs.append(cols[:, -1:])
+        return out, inputs
+
+    def preprocess(self, x):
+        return (x + self.scale) / (self.scale * 2)
+
+    def preprocess_inverse(self, x):
+        return x * (self.scale * 2) - self.scale
+
+    def sdf(self, x):
+        _hip.require_cuda(x, "Net.sdf")
+        s, keep = self.tnp_desc()
+        x = x.detach().float().contiguous()
+        y = torch.empty(x.shape[0], device=x.device)
+        _hip.check(_hip.lib().tnp_sdf_grad(ctypes.byref(s), _hip.ptr(x), x.shape[0], _hip.ptr(y),
+                                           None, ctypes.c_void_p(_hip.stream_ptr(x.device))),
+                   "tnp_sdf_grad")
+        return y.unsqueeze(-1)
+
+    def region(self, vertices: Tensor, output: Tensor = None, eps=None):
+        eps = self.eps if eps is None else eps
+        _hip.require_cuda(vertices, "Net.region")
+        v = vertices.detach().float().contiguous()
+        if output is None:
+            planes, _ = self._forward_planes(v)
+            output = planes.t()
+        else:
+            planes = output.detach().float().t().contiguous()
+        s, keep = self.tnp_desc()
+        n = v.shape[0]
+        m = torch.empty(n, 3 + self.K, dtype=torch.int64, device=v.device)
+        off = torch.empty(n, 3, dtype=torch.int64, device=v.device)
+        _hip.check(_hip.lib().tnp_region(ctypes.byref(s), _hip.ptr(v), _hip.ptr(planes), n, n,
+                                         float(eps), _hip.ptr(m), _hip.ptr(off),
+                                         ctypes.c_void_p(_hip.stream_ptr(v.device))), "tnp_region")
+        return m, off, output
+
+    def normal(self, vertices: Tensor, l: int = None, h: int = None, create_graph=False,
+               return_y=False) -> Tensor:
+        if l is not None and h is not None and h != self.num_hidden:
+            raise NotImplementedError("Net.normal: per-neuron gradients (the reference's "
+                                      "l/h branch references an undefined global)")
+        _hip.require_cuda(vertices, "Net.normal")
+        s, keep = self.tnp_desc()
+        x = vertices.detach().float().contiguous()
+        y = torch.empty(x.shape[0], device=x.device)
+        J = torch.empty(x.shape[0], 3, device=x.device)
+        _hip.check(_hip.lib().tnp_sdf_grad(ctypes.byref(s), _hip.ptr(x), x.shape[0], _hip.ptr(y),
+                                           _hip.ptr(J), ctypes.c_void_p(_hip.stream_ptr(x.device))),
+                   "tnp_sdf_grad")
+        return (J, y.unsqueeze(-1)) if return_y else J

@@ -1,0 +1,137 @@
+"""Drop-in for the reference's ``tropical.subpoly`` (tropical/subpoly.py).
+
+``subpoly(net, d, size, eps, force)`` keeps the reference's signature, stdout
+line and return types; the whole extraction -- skeleton, every hyperplane
+step, surface and faces -- runs in the device-resident HIP engine
+(csrc/*.hip through include/tropical_hip.h).  Empty steps are skipped
+without a launch: the engine knows from the packed eps-sign keys which
+future planes split an edge (subpoly.py:104-110 has no side effects when
+nothing splits).
+"""
+from __future__ import annotations
+
+from typing import List
+
+import numpy as np
+import torch
+from torch import Tensor
+
+from ._engine import engine_for
+
+
+def _check_eps(net, eps):
+    if eps is not None and float(eps) != float(net.eps):
+        raise NotImplementedError(
+            f"eps={eps} differs from net.eps={net.eps}; the reference mixes both "
+            "(subpoly_ uses eps, Net.region uses net.eps) -- construct Net(eps=...) instead")
+
+
+def _faces_to_numpy(tri: Tensor, faces: Tensor):
+    if tri.shape[0] == 0:
+        return [], []
+    return faces.cpu().numpy(), tri.cpu().numpy()
+
+
+@torch.no_grad()
+def subpoly(net, d: int, size: float, eps: float = 1e-4, force: bool = False,
+            stats: list = None) -> List:
+    """Skeleton -> all hyperplane steps -> surface -> faces (subpoly.py:23-86).
+
+    Returns ``(faces float np F x 3 x 3, vertices V x 3 on net.device(),
+    faces_with_indices int64 np F x 3)``; ``stats`` (optional list) receives
+    one counter dict per active step."""
+    _check_eps(net, eps)
+    if d != 3:
+        raise NotImplementedError("d must be 3 (the reference's hash grid is 3-D)")
+    if not force:
+        from .curve import subpoly_curve
+        return subpoly_curve(net, size, stats=stats)
+    eng = engine_for(net)
+    eng.skeleton(unit=128, size=size)
+    eng.run_steps(stats)
+    return _finish(eng, net)
+
+
+def _finish(eng, net):
+    nV, nE = eng.sizes()
+    print()
+    print(f"# of vertices and edges = {nV}/{nE} => ", end="")
+    sV, sE = eng.surface()
+    print(f"{sV}/{sE}", end=", ")
+    if sV == 0:
+        print("0 faces", end=", ")
+        return [], torch.zeros(0, dtype=torch.int64, device=eng.device), []
+    verts, _, _ = eng.export()
+    tri, fc = eng.faces()
+    faces, fwi = _faces_to_numpy(tri, fc)
+    print(f"{len(faces)} faces", end=", ")
+    return faces, verts, fwi
+
+
+@torch.no_grad()
+def subpoly_lattice(net, x0: int = 0, x1: int = -1, stats: list = None, faces: bool = True):
+    """The hot loop on the full lattice of the marks (no skeleton pruning):
+    the north-star synthetic workload."""
+    eng = engine_for(net)
+    eng.lattice(x0, x1)
+    eng.run_steps(stats)
+    if not faces:
+        return eng
+    return _finish(eng, net)
+
+
+def subpoly_(vertices, edges, net, l, h, eps, outputs_=None, pruning=True, strict=True,
+             force=False):
+    """One hyperplane step (subpoly.py:90-279), flat branch.
+
+    Deviation: the caller's ``edges`` tensor is not rewritten in place (the
+    reference's masked_scatter_ side effect at subpoly.py:211); the returned
+    edges are identical."""
+    _check_eps(net, eps)
+    if not force:
+        raise NotImplementedError("subpoly_ curve branch: use subpoly(..., force=False)")
+    eng = engine_for(net)
+    eng.load(vertices, edges, outputs_, keep_all=True)
+    idx = l * net.num_hidden + h
+    S, fail = eng.split(idx)
+    if S == 0:
+        v, e, o = eng.export(pre=True)
+        return v, e, o
+    eng.finish(idx, bool(h < net.num_hidden and pruning), fail)
+    return eng.export(pre=True)
+
+
+def extract_skeleton(vertices, edges, net, eps, outputs=None):
+    """subpoly.py:556-581; returns (vertices, edges, v_idx)."""
+    _check_eps(net, eps)
+    on = (outputs[:, -1].abs() < eps) if outputs is not None else (net.sdf(vertices)[:, 0].abs() < eps)
+    v = net.preprocess(vertices)
+    on[(v > 1).sum(dim=-1) > 0] = False
+    on[(v < 0).sum(dim=-1) > 0] = False
+    if 3 > on.sum():
+        return torch.Tensor([]).to(edges), torch.Tensor([]).to(edges), None
+    edges = edges[on[edges].sum(dim=-1) == 2]
+    v_idx, r_idx = edges.view(-1).unique(return_inverse=True)
+    return vertices[v_idx], r_idx.view(-1, 2), v_idx
+
+
+def extract_faces(vertices, edges, net, outputs=None, eps=None):
+    """subpoly.py:584-652 on the device engine."""
+    _check_eps(net, eps)
+    if vertices.shape[0] == 0:
+        return [], []
+    eng = engine_for(net)
+    eng.load(vertices, edges, outputs, keep_all=True)
+    tri, fc = eng.faces()
+    return _faces_to_numpy(tri, fc)
+
+
+def get_hypercube(d, size):
+    """subpoly.py:731-750."""
+    x = torch.Tensor([-size, size])
+    vertices = torch.stack(torch.meshgrid(x, x, x, indexing="ij"), dim=-1).view(-1, 3)
+    pairs = [[i, j] for i in range(8) for j in range(i + 1, 8)
+             if int((vertices[i] * vertices[j] < 0).sum()) == 1]
+    faces = [[0, 3, 5, 1], [0, 2, 8, 4], [3, 4, 10, 7],
+             [1, 2, 9, 6], [8, 9, 11, 10], [7, 11, 6, 5]]
+    return vertices, torch.LongTensor(pairs), faces
