@@ -1,0 +1,251 @@
+#!/usr/bin/env python3
+"""Benchmark: edges subdivided / second on the north-star synthetic workload.
+
+One "step" = one full pass of the hot path (tropical.subpoly's hyperplane
+loop, subpoly.py:58-69) over one synthetic input: load the initial lattice
+and its cached pre-activations (one forward over every lattice vertex), then
+every hyperplane step (split, new-vertex forward, failover override,
+connecting edges, pruning, compaction), all in HBM on the HIP engine.
+
+Workload: synthetic random-weight trilinear net,
+Net(num_layers=3, num_hidden=16, levels=2, r_min=G-1, r_max=G-1, T=19)
+(G marks per axis; hash table U(-0.1,0.1), nn.Linear-bound MLP, numpy PCG64
+seed 0), initial edges = the full G^3 lattice.  G = 128 at one GPU; at N GPUs
+the lattice grows to round(128 * N^(1/3)) marks per axis and is cut into N
+x-slabs (weak scaling, one process per GPU, RCCL only for the per-step
+8-byte agreements).  value = edges subdivided by all ranks (each split
+counted once) / max-over-ranks wall time.
+
+Run: python bench.py [--gpus N --steps K --warmup W]  (torchrun for N > 1)
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "tropical-nerf.pytorch_amd")
+for _p in (ROOT, PKG, os.path.join(ROOT, "tests")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def synthetic_params(G: int, seed: int = 0, amp: float = 0.1):
+    from tropical.synthetic import net_config_for_lattice, random_params
+    from tropical.tropical import level_meta
+    cfg = net_config_for_lattice(G)
+    b = np.exp2(np.log2((cfg["r_max"] * 1.0) / cfg["r_min"]) / (cfg["levels"] - 1))
+    n_params = level_meta(cfg["levels"], cfg["r_min"], b, cfg["T"])[-1] * 2
+    nodes = [cfg["levels"] * 2] + [cfg["num_hidden"]] * (cfg["num_layers"] - 1) + [2]
+    return cfg, random_params(n_params, nodes, seed, amp)
+
+
+def make_net(G, device, seed=0):
+    from tropical.stanford.model import Net
+    cfg, p = synthetic_params(G, seed)
+    net = Net(**cfg)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in p.items()})
+    return net.to(device)
+
+
+def slab(G: int, rank: int, world: int):
+    """Marks [x0, x1] of this rank's x-slab (cells split evenly)."""
+    cuts = [round(r * (G - 1) / world) for r in range(world + 1)]
+    return cuts[rank], cuts[rank + 1]
+
+
+def algorithmic_bytes(st: dict, K: int) -> int:
+    """SURVEY §8d per-step traffic model B_s (bytes the step must move)."""
+    E_in, S, V_in = st["E_in"], st["S"], st["V_in"]
+    C = 3 + K
+    b = 16 * E_in
+    if S > 0:
+        b += (184 * S + math.ceil(2 * C / 8) * V_in + 8 * (E_in + 2 * S + st["X"])
+              + 8 * st["E_out"] + 2 * (12 + 4 * K) * st["V_out"] + 56 * st["A"] + 34 * st["P"])
+    return b
+
+
+class Collective:
+    """Per-step agreements between slab ranks (the reference's global
+    decisions, subpoly.py:110 and subpoly_debug.py:43-49)."""
+
+    def __init__(self, device):
+        import torch.distributed as dist
+        self.dist = dist
+        self.device = device
+
+    def __call__(self, vec: np.ndarray, op: str):
+        t = torch.tensor(vec.astype(np.int64).view(np.int64), device=self.device)
+        if op == "or":
+            # OR of 64-bit masks: gather and OR on the host (RCCL has no BOR)
+            out = [torch.empty_like(t) for _ in range(self.dist.get_world_size())]
+            self.dist.all_gather(out, t)
+            acc = np.zeros_like(vec)
+            for o in out:
+                acc |= o.cpu().numpy().view(vec.dtype)
+            return acc
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return t.cpu().numpy()
+
+
+def cpu_baseline(sample_marks: int, seed: int, threads: int):
+    """The oracle (PyTorch-CPU restatement of the reference, same op sequence)
+    on a bounded sample: the same synthetic generator at sample_marks^3."""
+    import oracle.subdivide as od
+    from tropical.synthetic import lattice_edges, lattice_vertices
+    torch.set_num_threads(threads)
+    cfg, p = synthetic_params(sample_marks, seed)
+    ref = od.load_params(od.RefNet(**cfg), p)
+    V = torch.from_numpy(lattice_vertices(ref.enc.marks.numpy()))
+    E = torch.from_numpy(lattice_edges(sample_marks))
+    stats = {}
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        V, E, c = od.run_steps(V, E, ref, 1e-4, None, stats)
+    dt = time.perf_counter() - t0
+    S = sum(s["S"] for s in stats["steps"])
+    with torch.no_grad():
+        Vs, Es, used = od.extract_surface(V, E, ref, 1e-4, c)
+    return S / dt, S, dt, Vs
+
+
+def chamfer(a: np.ndarray, b: np.ndarray) -> float:
+    """chamfer_distance.py:39-48 formula (mean NN L2 both ways / 2)."""
+    if len(a) == 0 or len(b) == 0:
+        return 0.0 if len(a) == len(b) else float("inf")
+    from scipy.spatial import cKDTree
+    d1, _ = cKDTree(b).query(a)
+    d2, _ = cKDTree(a).query(b)
+    return float((d1.mean() + d2.mean()) / 2)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--marks", type=int, default=128, help="marks per axis per GPU (weak scaling)")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--cpu-sample-marks", type=int, default=int(os.environ.get("TNP_CPU_SAMPLE", 40)))
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    coll = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+        coll = Collective(dev)
+
+    from tropical._engine import engine_for
+    G = args.marks if world == 1 else int(round(args.marks * world ** (1.0 / 3.0)))
+    net = make_net(G, dev, args.seed)
+    x0, x1 = slab(G, rank, world)
+    eng = engine_for(net)
+    eng.set_dup_plane(x1 if rank < world - 1 else -1)
+
+    def one_pass():
+        stats = []
+        eng.lattice(x0, x1)
+        eng.run_steps(stats, coll)
+        return stats
+
+    def barrier():
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize(dev)
+
+    for _ in range(args.warmup):
+        one_pass()
+    eng.kernel_timer(True)
+    barrier()
+    t0 = time.perf_counter()
+    all_stats = []
+    for _ in range(args.steps):
+        all_stats.append(one_pass())
+    barrier()
+    dt = time.perf_counter() - t0
+    ktime = eng.kernel_timer(False)
+
+    splits = sum(s["S"] - s["S_dup"] for st in all_stats for s in st)
+    bytes_alg = sum(algorithmic_bytes(s, net.K) for st in all_stats for s in st)
+    vec = torch.tensor([dt, float(splits), float(bytes_alg)], device=dev, dtype=torch.float64)
+    if world > 1:
+        mx = vec.clone()
+        torch.distributed.all_reduce(mx[:1], op=torch.distributed.ReduceOp.MAX)
+        torch.distributed.all_reduce(vec[1:], op=torch.distributed.ReduceOp.SUM)
+        vec[0] = mx[0]
+    dt_max, splits_tot, bytes_tot = vec.tolist()
+
+    if rank == 0:
+        per_pass = splits_tot / args.steps
+        value = splits_tot / dt_max
+        st0 = all_stats[0]
+        # dominant kernel: HIP events around each launch inside the engine
+        dom = max(ktime, key=lambda k: ktime[k]["ms"]) if ktime else None
+        roof = None
+        if dom:
+            kt = ktime[dom]
+            avg_ms = kt["ms"] / max(kt["launches"], 1)
+            alg = kt["bytes"] / max(kt["launches"], 1)
+            ach = alg / (avg_ms * 1e-3) / 1e9
+            roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                    "avg_launch_us": round(avg_ms * 1e3, 2), "launches": kt["launches"],
+                    "alg_bytes_per_launch": int(alg)}
+        loop_gbs = bytes_tot / dt_max / 1e9
+        out = {
+            "metric": "edges subdivided/sec", "value": round(value, 1), "unit": "edges/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(dt_max / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": f"synthetic random-weight trilinear net, {G}^3 initial lattice "
+                                   f"({'x-slab per GPU' if world > 1 else 'one GPU'}), flat path, all "
+                                   f"{net.K} hyperplane steps", "marks_per_axis": G,
+                       "lattice_vertices": G ** 3, "edges_subdivided_per_pass": int(per_pass),
+                       "seed": args.seed, "table_amp": 0.1, "parallelism": f"xslab{world}"},
+            "roofline": roof,
+            "loop_model_bytes_per_pass": int(bytes_tot / args.steps),
+            "loop_model_gbs": round(loop_gbs, 1),
+            "kernel_ms_per_pass": {k: round(v["ms"] / args.steps, 3) for k, v in
+                                   sorted(ktime.items(), key=lambda kv: -kv[1]["ms"])},
+            "active_steps": len(st0),
+        }
+        if not args.no_cpu and world == 1:
+            thr = max(1, min(16, len(os.sched_getaffinity(0))))
+            cps, S_cpu, t_cpu, Vs_cpu = cpu_baseline(args.cpu_sample_marks, args.seed, thr)
+            out["cpu_baseline"] = {
+                "value": round(cps, 1), "unit": "edges/s", "cores": thr, "kind": "port",
+                "sample": f"oracle (PyTorch-CPU restatement of the reference) on the same generator at "
+                          f"{args.cpu_sample_marks}^3: {S_cpu} splits in {t_cpu:.1f}s"}
+            # Chamfer-L2 of our surface vs the reference path's on that sample
+            small = make_net(args.cpu_sample_marks, dev, args.seed)
+            e2 = engine_for(small)
+            e2.lattice()
+            e2.run_steps()
+            e2.surface()
+            vs, _, _ = e2.export()
+            out["chamfer_l2_vs_ref"] = chamfer(vs.cpu().numpy(), Vs_cpu.numpy())
+            out["gpu_over_cpu"] = round(value / cps, 1)
+            engine_for(net)  # restore
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -57,6 +57,7 @@ typedef struct tnp_step_stats {
   int64_t pair_tests; /* member pairs this implementation tested */
   int32_t override_applied;
   uint64_t next_active; /* planes > idx a kept edge would split (pruning steps) */
+  int64_t S_dup;        /* splits on the shared slab boundary plane (multi-GPU) */
 } tnp_step_stats;
 
 const char* tnp_last_error(void);
@@ -162,6 +163,29 @@ int tnp_engine_surface(tnp_engine* eng, void* stream, int64_t* V, int64_t* E);
 int tnp_engine_faces(tnp_engine* eng, void* stream, int64_t* n_tri, int64_t* n_faces);
 int tnp_engine_faces_export(tnp_engine* eng, int64_t* d_tri, float* d_faces,
                             void* stream);
+
+/* Multi-GPU x-slabs: count splits of edges lying in mark plane x = mark
+ * (the plane this slab shares with its upper neighbour; -1 = none), so the
+ * global split count can subtract the replicated boundary work. */
+int tnp_engine_set_dup_plane(tnp_engine* eng, int mark);
+
+/* HIP-event timing of every engine kernel launch (on=1 clears and starts;
+ * on=0 stops, synchronizes and aggregates per kernel name); read the
+ * aggregates with tnp_engine_kernel_stat (ms, launches, modelled
+ * algorithmic bytes). */
+int tnp_engine_kernel_timer(tnp_engine* eng, int on, void* stream, int32_t* n_kernels);
+int tnp_engine_kernel_stat(tnp_engine* eng, int i, char* name, int cap, double* ms,
+                           int64_t* launches, double* bytes);
+
+/* Self-check of the fp32 primitives the bitwise contract relies on:
+ * out[8i..8i+7] = sqrt_rn(a), a/b (rn), fma(a,b,c), a*b, a+b, sqrtf(a),
+ * a/b (default), tanhf(a). */
+int tnp_debug_ops(const float* d_a, const float* d_b, const float* d_c, int64_t n,
+                  float* d_out, void* stream);
+
+/* Debug: padded angular scores (F x width fp32) of the last faces call. */
+int tnp_engine_faces_debug(tnp_engine* eng, float* d_scores, int64_t cap, int64_t* F,
+                           int64_t* width, void* stream);
 
 #ifdef __cplusplus
 }

@@ -12,6 +12,7 @@
 #include <cstring>
 #include <string>
 #include <utility>
+#include <vector>
 
 #include "../../include/tropical_hip.h"
 #include "common.h"
@@ -99,8 +100,20 @@ struct VSet {
   int64_t cap = 0;  // rows; pre leading dimension == cap
 };
 
+struct KRec {
+  const char* name;
+  double bytes;
+  hipEvent_t a, b;
+};
+
 struct tnp_engine {
   int device = 0;
+  int dup_mark = -1;
+  bool kt_on = false;
+  std::vector<KRec> kt;
+  std::vector<std::string> kt_names;
+  std::vector<double> kt_ms, kt_bytes;
+  std::vector<int64_t> kt_n;
   NetDev net{};
   int K = 0;
   bool has_net = false;
@@ -115,10 +128,10 @@ struct tnp_engine {
   int64_t* h_ctr = nullptr;  // pinned mirror of ctr
   // pending split
   int pend_idx = -1;
-  int64_t pend_S = 0;
+  int64_t pend_S = 0, pend_dup = 0;
   // faces output
   Buf tri, faces;
-  int64_t n_tri = 0, n_faces = 0;
+  int64_t n_tri = 0, n_faces = 0, dbg_F = 0, dbg_W = 0;
   Buf fscr[12];
   Buf fscr2[32];
 };
@@ -129,10 +142,33 @@ static int read_ctr(tnp_engine* e, hipStream_t s) {
   return 0;
 }
 
+// ---- per-kernel HIP-event timer (bench.py's roofline leg) -----------------
+static int ktimer_begin(tnp_engine* e, const char* name, double bytes, hipStream_t s) {
+  if (!e->kt_on) return -1;
+  KRec r;
+  r.name = name;
+  r.bytes = bytes;
+  if (hipEventCreate(&r.a) != hipSuccess || hipEventCreate(&r.b) != hipSuccess) return -1;
+  (void)hipEventRecord(r.a, s);
+  e->kt.push_back(r);
+  return (int)e->kt.size() - 1;
+}
+static void ktimer_end(tnp_engine* e, int t, hipStream_t s) {
+  if (t >= 0) (void)hipEventRecord(e->kt[t].b, s);
+}
+#define TIMED(name, bytes, call)                                   \
+  do {                                                             \
+    int _t = ktimer_begin(e, name, (double)(bytes), s);            \
+    if (call) return -1;                                           \
+    ktimer_end(e, _t, s);                                          \
+  } while (0)
+
 static int scan_counts(tnp_engine* e, const int32_t* in, int64_t* out, int64_t n, int slot,
                        hipStream_t s) {
   if (buf_ensure(e->scan_scr, scan_scratch_bytes(n), s)) return -1;
-  return scan_i32_to_i64(in, out, n, P<int64_t>(e->ctr) + slot, e->scan_scr.p, e->scan_scr.bytes, s);
+  TIMED("scan", 16.0 * n,
+        scan_i32_to_i64(in, out, n, P<int64_t>(e->ctr) + slot, e->scan_scr.p, e->scan_scr.bytes, s));
+  return 0;
 }
 
 // grow a vertex set to `rows` keeping [0, keep_rows)
@@ -343,7 +379,7 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
   if (buf_ensure(e->blkoff, (tiles + 1) * sizeof(int64_t), s)) return -1;
   int64_t S = 0;
   if (e->E > 0) {
-    if (launch_split_count(P<int32_t>(e->edges), e->E, col, eps, P<int32_t>(e->blk), s)) return -1;
+    TIMED("split_count", 16.0 * e->E, launch_split_count(P<int32_t>(e->edges), e->E, col, eps, P<int32_t>(e->blk), s));
     if (scan_counts(e, P<int32_t>(e->blk), P<int64_t>(e->blkoff), tiles, CTR_S, s)) return -1;
     if (read_ctr(e, s)) return -1;
     S = e->h_ctr[CTR_S];
@@ -352,21 +388,22 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
   if (S > 0) {
     if (buf_ensure(e->sa, S * sizeof(int32_t), s)) return -1;
     if (buf_ensure(e->sb, S * sizeof(int32_t), s)) return -1;
-    if (launch_split_emit(P<int32_t>(e->edges), e->E, col, eps, P<int64_t>(e->blkoff), e->V,
-                          P<int32_t>(e->sa), P<int32_t>(e->sb), s))
-      return -1;
+    TIMED("split_emit", 16.0 * e->E + 12.0 * S,
+          launch_split_emit(P<int32_t>(e->edges), e->E, col, eps, P<int64_t>(e->blkoff), e->V,
+                            P<int32_t>(e->sa), P<int32_t>(e->sb), e->dup_mark,
+                            P<uint64_t>(e->cur.grid), P<int64_t>(e->ctr), s));
     if (vset_ensure(e, e->cur, e->V + S, e->V, s)) return -1;
     col = P<float>(e->cur.pre) + (int64_t)idx * e->cur.cap;  // may have moved
-    if (launch_new_vertices(P<int32_t>(e->sa), P<int32_t>(e->sb), S, col, eps, P<float>(e->cur.xyz),
-                            e->V, s))
-      return -1;
+    TIMED("new_vertices", 52.0 * S,
+          launch_new_vertices(P<int32_t>(e->sa), P<int32_t>(e->sb), S, col, eps, P<float>(e->cur.xyz),
+                              e->V, s));
     if (buf_ensure(e->stage, (size_t)S * e->K * sizeof(float), s)) return -1;
     if (buf_ensure(e->shared, S * sizeof(uint64_t), s)) return -1;
-    if (launch_forward(e->net, P<float>(e->cur.xyz) + 3 * e->V, S, P<float>(e->stage), S, 1, s))
-      return -1;
-    if (launch_fail_check(P<int32_t>(e->sa), P<int32_t>(e->sb), S, idx, P<uint64_t>(e->cur.zero),
-                          P<float>(e->stage), eps, P<uint64_t>(e->shared), P<int64_t>(e->ctr), s))
-      return -1;
+    TIMED("forward", (12.0 + 4.0 * e->K) * S,
+          launch_forward(e->net, P<float>(e->cur.xyz) + 3 * e->V, S, P<float>(e->stage), S, 1, s));
+    TIMED("fail_check", 40.0 * S,
+          launch_fail_check(P<int32_t>(e->sa), P<int32_t>(e->sb), S, idx, P<uint64_t>(e->cur.zero),
+                            P<float>(e->stage), eps, P<uint64_t>(e->shared), P<int64_t>(e->ctr), s));
     // grid words of the new vertices (coordinates are final)
     if (launch_keys(e->net, P<float>(e->cur.xyz) + 3 * e->V, P<float>(e->stage), S, S, 0,
                     P<uint64_t>(e->cur.pos) + e->V, P<uint64_t>(e->cur.zero) + e->V,
@@ -375,6 +412,7 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
     if (read_ctr(e, s)) return -1;
     *fail = e->h_ctr[CTR_FAIL] ? 1 : 0;
   }
+  e->pend_dup = S > 0 ? e->h_ctr[CTR_DUP] : 0;
   *S_out = S;
   e->pend_idx = idx;
   e->pend_S = S;
@@ -399,9 +437,9 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   uint64_t* grid = P<uint64_t>(c.grid);
 
   // 1. override + keys of the new vertices
-  if (launch_finalize_new(S, K, override_, P<uint64_t>(e->shared), P<float>(e->stage), eps,
-                          P<float>(c.pre), c.cap, e->valid_from, V, pos, zero, s))
-    return -1;
+  TIMED("finalize_new", (8.0 + 4.0 * K + 4.0 * (K - e->valid_from) + 16.0) * S,
+        launch_finalize_new(S, K, override_, P<uint64_t>(e->shared), P<float>(e->stage), eps,
+                            P<float>(c.pre), c.cap, e->valid_from, V, pos, zero, s));
 
   // 2. members = new vertices ++ hit vertices (ascending)
   int64_t vt = step_tiles(V);
@@ -409,10 +447,10 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   if (buf_ensure(e->blkoff, (vt + 1) * sizeof(int64_t), s)) return -1;
   if (buf_ensure(e->members, std::max<int64_t>(NV, 1) * sizeof(int32_t), s)) return -1;
   if (V > 0) {
-    if (launch_hit_count(col, V, eps, P<int32_t>(e->blk), s)) return -1;
+    TIMED("hit_count", 4.0 * V, launch_hit_count(col, V, eps, P<int32_t>(e->blk), s));
     if (scan_counts(e, P<int32_t>(e->blk), P<int64_t>(e->blkoff), vt, CTR_H, s)) return -1;
   }
-  if (launch_hit_emit(col, V, eps, P<int64_t>(e->blkoff), P<int32_t>(e->members), S, s)) return -1;
+  TIMED("hit_emit", 4.0 * V + 4.0 * S, launch_hit_emit(col, V, eps, P<int64_t>(e->blkoff), P<int32_t>(e->members), S, s));
 
   // 3. bucket members by grid cell (dense cell grid over the marks)
   const int NC = e->net.n_marks + 2;
@@ -425,8 +463,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   if (read_ctr(e, s)) return -1;
   const int64_t H = V > 0 ? e->h_ctr[CTR_H] : 0;
   const int64_t M = S + H;
-  if (launch_cell_count(P<int32_t>(e->members), M, grid, zero, idx, NC, P<int32_t>(e->cellcnt), ctr, s))
-    return -1;
+  TIMED("cell_count", 24.0 * M, launch_cell_count(P<int32_t>(e->members), M, grid, zero, idx, NC, P<int32_t>(e->cellcnt), ctr, s));
   if (scan_counts(e, P<int32_t>(e->cellcnt), P<int64_t>(e->celloff), ncell, CTR_T, s)) return -1;
   if (read_ctr(e, s)) return -1;
   if (e->h_ctr[CTR_K0]) {
@@ -437,9 +474,9 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   const int64_t T = e->h_ctr[CTR_T];
   if (buf_ensure(e->ent_v, std::max<int64_t>(T, 1) * sizeof(int32_t), s)) return -1;
   if (buf_ensure(e->ent_c, std::max<int64_t>(T, 1) * sizeof(int32_t), s)) return -1;
-  if (launch_cell_scatter(P<int32_t>(e->members), M, grid, NC, P<int64_t>(e->celloff),
-                          P<int32_t>(e->cellcur), P<int32_t>(e->ent_v), P<int32_t>(e->ent_c), s))
-    return -1;
+  TIMED("cell_scatter", 12.0 * M + 20.0 * T,
+        launch_cell_scatter(P<int32_t>(e->members), M, grid, NC, P<int64_t>(e->celloff),
+                            P<int32_t>(e->cellcur), P<int32_t>(e->ent_v), P<int32_t>(e->ent_c), s));
 
   // 4. connecting edges, bucketed by their smaller endpoint
   if (buf_ensure(e->paircnt, std::max<int64_t>(NV, 1) * sizeof(int32_t), s)) return -1;
@@ -447,10 +484,10 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   if (buf_ensure(e->pairoff, std::max<int64_t>(NV, 1) * sizeof(int64_t), s)) return -1;
   TNP_CHECK(hipMemsetAsync(e->paircnt.p, 0, NV * sizeof(int32_t), s));
   TNP_CHECK(hipMemsetAsync(e->paircur.p, 0, NV * sizeof(int32_t), s));
-  if (launch_pairs(false, P<int32_t>(e->ent_v), P<int32_t>(e->ent_c), T, P<int64_t>(e->celloff),
-                   P<int32_t>(e->cellcnt), NC, idx, pos, zero, grid, P<int32_t>(e->paircnt),
-                   nullptr, nullptr, nullptr, ctr, s))
-    return -1;
+  TIMED("pairs_count", 8.0 * T,
+        launch_pairs(false, P<int32_t>(e->ent_v), P<int32_t>(e->ent_c), T, P<int64_t>(e->celloff),
+                     P<int32_t>(e->cellcnt), NC, idx, pos, zero, grid, P<int32_t>(e->paircnt),
+                     nullptr, nullptr, nullptr, ctr, s));
   if (scan_counts(e, P<int32_t>(e->paircnt), P<int64_t>(e->pairoff), NV, CTR_X, s)) return -1;
   if (read_ctr(e, s)) return -1;
   if (e->h_ctr[CTR_COMPAT] == 0) {
@@ -462,13 +499,13 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   const int64_t X = e->h_ctr[CTR_X];
   if (buf_ensure(e->pair_hi, std::max<int64_t>(X, 1) * sizeof(int32_t), s)) return -1;
   if (buf_ensure(e->pair_lo, std::max<int64_t>(X, 1) * sizeof(int32_t), s)) return -1;
-  if (launch_pairs(true, P<int32_t>(e->ent_v), P<int32_t>(e->ent_c), T, P<int64_t>(e->celloff),
-                   P<int32_t>(e->cellcnt), NC, idx, pos, zero, grid, P<int32_t>(e->paircnt),
-                   P<int64_t>(e->pairoff), P<int32_t>(e->paircur), P<int32_t>(e->pair_hi), ctr, s))
-    return -1;
-  if (launch_pair_sort(P<int64_t>(e->pairoff), P<int32_t>(e->paircnt), NV, P<int32_t>(e->pair_hi),
-                       P<int32_t>(e->pair_lo), s))
-    return -1;
+  TIMED("pairs_emit", 8.0 * T + 4.0 * X,
+        launch_pairs(true, P<int32_t>(e->ent_v), P<int32_t>(e->ent_c), T, P<int64_t>(e->celloff),
+                     P<int32_t>(e->cellcnt), NC, idx, pos, zero, grid, P<int32_t>(e->paircnt),
+                     P<int64_t>(e->pairoff), P<int32_t>(e->paircur), P<int32_t>(e->pair_hi), ctr, s));
+  TIMED("pair_sort", 12.0 * NV + 12.0 * X,
+        launch_pair_sort(P<int64_t>(e->pairoff), P<int32_t>(e->paircnt), NV, P<int32_t>(e->pair_hi),
+                         P<int32_t>(e->pair_lo), s));
 
   // 5. pruning over [edges; e_new; c_new] + vertex compaction
   const int64_t N = E + S + X;
@@ -484,28 +521,28 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     if (buf_ensure(e->used, std::max<int64_t>(NV, 1) * sizeof(int32_t), s)) return -1;
     if (buf_ensure(e->nid, std::max<int64_t>(NV, 1) * sizeof(int64_t), s)) return -1;
     TNP_CHECK(hipMemsetAsync(e->used.p, 0, NV * sizeof(int32_t), s));
-    if (launch_prune(false, eg, E, P<int32_t>(e->sb), S, V, P<int32_t>(e->pair_lo),
-                     P<int32_t>(e->pair_hi), X, idx, 1, K - 1, pos, zero, P<int32_t>(e->blk),
-                     nullptr, nullptr, nullptr, ctr, s))
-      return -1;
+    TIMED("prune_count", 40.0 * N,
+          launch_prune(false, eg, E, P<int32_t>(e->sb), S, V, P<int32_t>(e->pair_lo),
+                       P<int32_t>(e->pair_hi), X, idx, 1, K - 1, pos, zero, P<int32_t>(e->blk),
+                       nullptr, nullptr, nullptr, ctr, s));
     if (scan_counts(e, P<int32_t>(e->blk), P<int64_t>(e->blkoff), nt, CTR_E, s)) return -1;
-    if (launch_prune(true, eg, E, P<int32_t>(e->sb), S, V, P<int32_t>(e->pair_lo),
-                     P<int32_t>(e->pair_hi), X, idx, 1, K - 1, pos, zero, nullptr,
-                     P<int64_t>(e->blkoff), P<int32_t>(e->edges_alt), P<int32_t>(e->used), ctr, s))
-      return -1;
+    TIMED("prune_emit", 40.0 * N,
+          launch_prune(true, eg, E, P<int32_t>(e->sb), S, V, P<int32_t>(e->pair_lo),
+                       P<int32_t>(e->pair_hi), X, idx, 1, K - 1, pos, zero, nullptr,
+                       P<int64_t>(e->blkoff), P<int32_t>(e->edges_alt), P<int32_t>(e->used), ctr, s));
     if (scan_counts(e, P<int32_t>(e->used), P<int64_t>(e->nid), NV, CTR_V, s)) return -1;
     next_valid = e->keep_all ? 0 : std::min(idx + 1, K - 1);
     if (vset_ensure(e, e->alt, NV, 0, s)) return -1;
     VSet& a = e->alt;
-    if (launch_gather_vertices(P<int32_t>(e->used), P<int64_t>(e->nid), NV, K, next_valid,
-                               P<float>(c.xyz), P<float>(c.pre), c.cap, pos, zero, grid,
-                               P<float>(a.xyz), P<float>(a.pre), a.cap, P<uint64_t>(a.pos),
-                               P<uint64_t>(a.zero), P<uint64_t>(a.grid), s))
-      return -1;
+    TIMED("gather_vertices", 4.0 * NV + 2.0 * (12 + 4.0 * (K - next_valid) + 24) * NV,
+          launch_gather_vertices(P<int32_t>(e->used), P<int64_t>(e->nid), NV, K, next_valid,
+                                 P<float>(c.xyz), P<float>(c.pre), c.cap, pos, zero, grid,
+                                 P<float>(a.xyz), P<float>(a.pre), a.cap, P<uint64_t>(a.pos),
+                                 P<uint64_t>(a.zero), P<uint64_t>(a.grid), s));
     if (read_ctr(e, s)) return -1;
     E2 = e->h_ctr[CTR_E];
     V2 = e->h_ctr[CTR_V];
-    if (launch_remap_edges(P<int32_t>(e->edges_alt), E2, P<int64_t>(e->nid), s)) return -1;
+    TIMED("remap_edges", 32.0 * E2, launch_remap_edges(P<int32_t>(e->edges_alt), E2, P<int64_t>(e->nid), s));
     std::swap(e->cur, e->alt);
   } else {
     if (launch_prune(true, eg, E, P<int32_t>(e->sb), S, V, P<int32_t>(e->pair_lo),
@@ -532,6 +569,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     st->pair_tests = e->h_ctr[CTR_TESTS];
     st->override_applied = override_;
     st->next_active = (uint64_t)e->h_ctr[CTR_ACTIVE];
+    st->S_dup = e->pend_dup;
   }
   return 0;
 }
@@ -848,10 +886,18 @@ extern "C" int tnp_engine_faces(tnp_engine* e, void* stream, int64_t* n_tri, int
                          P<int32_t>(fs[FS_CNT]), s))
     return -1;
   if (launch_keep_counts(P<int32_t>(fs[FS_CNT]), cap, P<int32_t>(fs[FS_KC]), P<int32_t>(fs[FS_KF]), s)) return -1;
+  // padded width of r_idx_as_tensor = the largest region over ALL regions
+  TNP_CHECK(hipMemsetAsync(ctr + CTR_COMPAT, 0, sizeof(int64_t), s));
+  if (launch_max_i32(P<int32_t>(fs[FS_CNT]), cap, ctr + CTR_COMPAT, s)) return -1;
   if (scan_counts(e, P<int32_t>(fs[FS_KC]), P<int64_t>(fs[FS_MEMOFF]), cap, CTR_T, s)) return -1;
   if (scan_counts(e, P<int32_t>(fs[FS_KF]), P<int64_t>(fs[FS_RID]), cap, CTR_X, s)) return -1;
   if (read_ctr(e, s)) return -1;
   const int64_t Mtot = e->h_ctr[CTR_T], R = e->h_ctr[CTR_X];
+  const int width = (int)e->h_ctr[CTR_COMPAT];
+  if (width > (1 << 16)) {
+    tnp_set_error("faces: a region with %d vertices (degenerate complex)", width);
+    return -1;
+  }
   if (R == 0) return 0;
   // F2: member lists (k, v)-sorted
   if (buf_ensure(fs[FS_MEM], Mtot * 8, s) || buf_ensure(fs[FS_ROFF], R * 8, s) ||
@@ -889,18 +935,20 @@ extern "C" int tnp_engine_faces(tnp_engine* e, void* stream, int64_t* n_tri, int
   const int64_t F = e->h_ctr[CTR_E];
   if (buf_ensure(fs[FS_FROW], F * 4, s) || buf_ensure(fs[FS_MEAN], F * 12, s) ||
       buf_ensure(fs[FS_NRM], F * 12, s) || buf_ensure(fs[FS_SDF], F * 4, s) ||
-      buf_ensure(fs[FS_KEY], Mtot * 8, s) || buf_ensure(fs[FS_ORDV], Mtot * 4, s) ||
+      buf_ensure(fs[FS_KEY], row_order_scratch(F, width), s) || buf_ensure(fs[FS_ORDV], Mtot * 4, s) ||
       buf_ensure(fs[FS_CALL], F * 4, s) || buf_ensure(fs[FS_CNZ], F * 4, s))
     return -1;
   if (launch_compact_rows(R, P<int32_t>(fs[FS_KEEP]), P<int64_t>(fs[FS_KOFF]), P<int32_t>(fs[FS_ROWS]),
                           P<int32_t>(fs[FS_FROW]), s))
     return -1;
   const int32_t* frow = P<int32_t>(fs[FS_FROW]);
+  e->dbg_F = F;
+  e->dbg_W = width;
   // F4: normals at the row means, angular order
-  if (launch_row_mean(F, frow, mem, roff, rcnt, xyz, P<float>(fs[FS_MEAN]), s)) return -1;
+  if (launch_row_mean(F, frow, mem, roff, rcnt, width, xyz, P<float>(fs[FS_MEAN]), s)) return -1;
   if (launch_sdf_grad(e->net, P<float>(fs[FS_MEAN]), F, P<float>(fs[FS_SDF]), P<float>(fs[FS_NRM]), s)) return -1;
-  if (launch_row_order(F, frow, mem, roff, rcnt, xyz, P<float>(fs[FS_NRM]), F == 3 ? 1 : 0,
-                       P<uint64_t>(fs[FS_KEY]), P<int32_t>(fs[FS_ORDV]), P<int32_t>(fs[FS_CALL]),
+  if (launch_row_order(F, frow, mem, roff, rcnt, width, xyz, P<float>(fs[FS_NRM]), F == 3 ? 1 : 0,
+                       fs[FS_KEY].p, P<int32_t>(fs[FS_ORDV]), P<int32_t>(fs[FS_CALL]),
                        P<int32_t>(fs[FS_CNZ]), s))
     return -1;
   TNP_CHECK(hipMemsetAsync(ctr + CTR_TRI, 0, 2 * sizeof(int64_t), s));
@@ -943,5 +991,74 @@ extern "C" int tnp_engine_faces_export(tnp_engine* e, int64_t* d_tri, float* d_f
     TNP_CHECK(hipMemcpyAsync(d_tri, e->tri.p, e->n_tri * 3 * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
   if (d_faces && e->n_faces > 0)
     TNP_CHECK(hipMemcpyAsync(d_faces, e->faces.p, e->n_faces * 9 * sizeof(float), hipMemcpyDeviceToDevice, s));
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// slab boundary + kernel timer controls
+// ---------------------------------------------------------------------------
+extern "C" int tnp_engine_set_dup_plane(tnp_engine* e, int mark) {
+  e->dup_mark = mark;
+  return 0;
+}
+
+extern "C" int tnp_engine_kernel_timer(tnp_engine* e, int on, void* stream, int32_t* n_kernels) {
+  hipStream_t s = (hipStream_t)stream;
+  TNP_CHECK(hipSetDevice(e->device));
+  *n_kernels = 0;
+  if (on) {
+    e->kt.clear();
+    e->kt_on = true;
+    return 0;
+  }
+  e->kt_on = false;
+  TNP_CHECK(hipStreamSynchronize(s));
+  e->kt_names.clear();
+  e->kt_ms.clear();
+  e->kt_bytes.clear();
+  e->kt_n.clear();
+  for (KRec& r : e->kt) {
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, r.a, r.b);
+    (void)hipEventDestroy(r.a);
+    (void)hipEventDestroy(r.b);
+    size_t i = 0;
+    for (; i < e->kt_names.size(); ++i)
+      if (e->kt_names[i] == r.name) break;
+    if (i == e->kt_names.size()) {
+      e->kt_names.push_back(r.name);
+      e->kt_ms.push_back(0);
+      e->kt_bytes.push_back(0);
+      e->kt_n.push_back(0);
+    }
+    e->kt_ms[i] += ms;
+    e->kt_bytes[i] += r.bytes;
+    e->kt_n[i] += 1;
+  }
+  e->kt.clear();
+  *n_kernels = (int32_t)e->kt_names.size();
+  return 0;
+}
+
+extern "C" int tnp_engine_kernel_stat(tnp_engine* e, int i, char* name, int cap, double* ms,
+                                      int64_t* launches, double* bytes) {
+  if (i < 0 || i >= (int)e->kt_names.size()) { tnp_set_error("kernel stat %d out of range", i); return -1; }
+  snprintf(name, cap, "%s", e->kt_names[i].c_str());
+  *ms = e->kt_ms[i];
+  *launches = e->kt_n[i];
+  *bytes = e->kt_bytes[i];
+  return 0;
+}
+
+// debugging aid: the padded angular scores of the last tnp_engine_faces call
+// (F x width fp32, final-row order); returns F and width
+extern "C" int tnp_engine_faces_debug(tnp_engine* e, float* d_scores, int64_t cap, int64_t* F, int64_t* width,
+                                      void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  *F = e->dbg_F;
+  *width = e->dbg_W;
+  int64_t n = e->dbg_F * e->dbg_W;
+  if (d_scores && n > 0 && n <= cap)
+    TNP_CHECK(hipMemcpyAsync(d_scores, e->fscr2[FS_KEY].p, n * sizeof(float), hipMemcpyDeviceToDevice, s));
   return 0;
 }

@@ -20,9 +20,10 @@ int launch_row_buckets(int64_t R, int64_t V, const uint64_t* mem, const int64_t*
 int launch_compact_rows(int64_t n, const int32_t* keep, const int64_t* koff, const int32_t* rows,
                         int32_t* out, hipStream_t s);
 int launch_row_mean(int64_t F, const int32_t* frow, const uint64_t* mem, const int64_t* roff,
-                    const int32_t* rcnt, const float* xyz, float* mean, hipStream_t s);
+                    const int32_t* rcnt, int M, const float* xyz, float* mean, hipStream_t s);
+size_t row_order_scratch(int64_t F, int M);
 int launch_row_order(int64_t F, const int32_t* frow, const uint64_t* mem, const int64_t* roff,
-                     const int32_t* rcnt, const float* xyz, const float* nrm, int quirk3, uint64_t* key,
+                     const int32_t* rcnt, int M, const float* xyz, const float* nrm, int quirk3, void* scratch,
                      int32_t* ordv, int32_t* cnt_all, int32_t* cnt_nz, hipStream_t s);
 int64_t fan_blocks(int64_t F);
 int launch_fan_hist(int64_t F, const int32_t* cnt, int T, int32_t* hist, hipStream_t s);

@@ -245,62 +245,131 @@ __global__ void k_compact_rows(int64_t n, const int32_t* __restrict__ keep, cons
   if (i < n && keep[i]) out[koff[i]] = rows[i];
 }
 
-// mean point of each final row (mean_points_with_valid: sum / #members)
+// ---------------------------------------------------------------------------
+// torch CPU float semantics the polygon sort depends on (pinned by probes in
+// tools/torch_cpu_semantics.py):
+//  * Tensor.sum over the padded row width M (dim=-2): ATen cascade row_sum
+//    with 4 interleaved lanes, tail into lane 0, lanes added in order
+//  * torch.cross (CPU): out0 = fma(a1, b2, -(a2*b1)) (gcc-contracted)
+//  * linalg.vector_norm: sqrt_rn(fma(z,z, fma(y,y, x*x)))
+//  * bmm of a 3-vector: (c0*n0 + c1*n1) + c2*n2, no fma
+//  * cosine_similarity: (a/max(|a|,1e-8)) * (b/max(|b|,1e-8)), summed in order
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int ceil_log2(int64_t x) {
+  if (x <= 2) return 1;
+  return 64 - __builtin_clzll((uint64_t)(x - 1));
+}
+
+// row_sum of coordinate d over positions [0, M) of a row whose first c
+// positions hold members (the rest are zero padding)
+__device__ float torch_row_sum(const uint64_t* mem, int64_t off, int c, int M, int d,
+                               const float* xyz) {
+  auto X = [&](int64_t p) -> float {
+    if (p >= c) return 0.f;
+    int v = (int)(uint32_t)mem[off + p];
+    return xyz[3 * (int64_t)v + d];
+  };
+  const int64_t size = M / 4;
+  float acc[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[j][k] = 0.f;
+  const int level_power = max(4, ceil_log2(size) / 4);
+  const int64_t level_step = 1ll << level_power;
+  const int64_t level_mask = level_step - 1;
+  int64_t i = 0;
+  for (; i + level_step <= size;) {
+    for (int64_t j = 0; j < level_step; ++j, ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc[0][k] = __fadd_rn(acc[0][k], X(i * 4 + k));
+    for (int j = 1; j < 4; ++j) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        acc[j][k] = __fadd_rn(acc[j][k], acc[j - 1][k]);
+        acc[j - 1][k] = 0.f;
+      }
+      if ((i & (level_mask << (j * level_power))) != 0) break;
+    }
+  }
+  for (; i < size; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[0][k] = __fadd_rn(acc[0][k], X(i * 4 + k));
+  for (int j = 1; j < 4; ++j)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[0][k] = __fadd_rn(acc[0][k], acc[j][k]);
+  for (int64_t p = size * 4; p < M; ++p) acc[0][0] = __fadd_rn(acc[0][0], X(p));
+  float r = acc[0][0];
+  r = __fadd_rn(r, acc[0][1]);
+  r = __fadd_rn(r, acc[0][2]);
+  r = __fadd_rn(r, acc[0][3]);
+  return r;
+}
+
+__device__ __forceinline__ bool nonzero3(const float* p) {
+  return p[0] != 0.f || p[1] != 0.f || p[2] != 0.f;
+}
+
+// mean_points_with_valid: points.sum(dim=1) / Z (subpoly.py:669-678)
 __global__ void k_row_mean(int64_t F, const int32_t* __restrict__ frow, const uint64_t* __restrict__ mem,
-                           const int64_t* __restrict__ roff, const int32_t* __restrict__ rcnt,
+                           const int64_t* __restrict__ roff, const int32_t* __restrict__ rcnt, int M,
                            const float* __restrict__ xyz, float* __restrict__ mean) {
   int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (f >= F) return;
   int r = frow[f];
   int c = rcnt[r];
-  float s[3] = {0.f, 0.f, 0.f};
-  for (int i = 0; i < c; ++i) {
-    int v = row_v(mem, roff[r], i);
 #pragma unroll
-    for (int d = 0; d < 3; ++d) s[d] += xyz[3 * (int64_t)v + d];
-  }
-#pragma unroll
-  for (int d = 0; d < 3; ++d) mean[3 * f + d] = s[d] / (float)c;
+  for (int d = 0; d < 3; ++d)
+    mean[3 * f + d] = __fdiv_rn(torch_row_sum(mem, roff[r], c, M, d, xyz), (float)c);
 }
 
-__device__ __forceinline__ void row_centroid(const uint64_t* mem, int64_t off, int c, const float* xyz,
-                                             float cen[3]) {
-  float s[3] = {0.f, 0.f, 0.f};
+// centroid of sort_polygon_vertices_batch: v.sum(dim=-2) / max(#{|v|>0}, 1)
+__device__ __forceinline__ void row_centroid(const uint64_t* mem, int64_t off, int c, int M,
+                                             const float* xyz, float cen[3]) {
   int k = 0;
   for (int i = 0; i < c; ++i) {
-    int v = row_v(mem, off, i);
-    float p[3] = {xyz[3 * (int64_t)v], xyz[3 * (int64_t)v + 1], xyz[3 * (int64_t)v + 2]};
-    s[0] += p[0];
-    s[1] += p[1];
-    s[2] += p[2];
-    k += (p[0] != 0.f || p[1] != 0.f || p[2] != 0.f);  // norm > 0
+    int v = (int)(uint32_t)mem[off + i];
+    k += nonzero3(xyz + 3 * (int64_t)v);
   }
   if (k == 0) k = 1;
 #pragma unroll
-  for (int d = 0; d < 3; ++d) cen[d] = s[d] / (float)k;
+  for (int d = 0; d < 3; ++d) cen[d] = __fdiv_rn(torch_row_sum(mem, off, c, M, d, xyz), (float)k);
 }
 
 __device__ __forceinline__ void cross3(const float a[3], const float b[3], float o[3]) {
-  o[0] = a[1] * b[2] - a[2] * b[1];
-  o[1] = a[2] * b[0] - a[0] * b[2];
-  o[2] = a[0] * b[1] - a[1] * b[0];
+  o[0] = __fmaf_rn(a[1], b[2], -__fmul_rn(a[2], b[1]));
+  o[1] = __fmaf_rn(a[2], b[0], -__fmul_rn(a[0], b[2]));
+  o[2] = __fmaf_rn(a[0], b[1], -__fmul_rn(a[1], b[0]));
 }
 
-// F.cosine_similarity: (x1/max(|x1|,eps)) . (x2/max(|x2|,eps)), eps=1e-8
+__device__ __forceinline__ float vnorm3(const float a[3]) {
+  // sqrtf, not __fsqrt_rn: on gfx950 only sqrtf is correctly rounded (tools/diag_ops.py)
+  return sqrtf(__fmaf_rn(a[2], a[2], __fmaf_rn(a[1], a[1], __fmul_rn(a[0], a[0]))));
+}
+
 __device__ __forceinline__ float cosine(const float a[3], const float b[3]) {
-  float na = fmaxf(sqrtf(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]), 1e-8f);
-  float nb = fmaxf(sqrtf(b[0] * b[0] + b[1] * b[1] + b[2] * b[2]), 1e-8f);
-  return (a[0] / na) * (b[0] / nb) + (a[1] / na) * (b[1] / nb) + (a[2] / na) * (b[2] / nb);
+  float na = fmaxf(vnorm3(a), 1e-8f), nb = fmaxf(vnorm3(b), 1e-8f);
+  float p0 = __fmul_rn(__fdiv_rn(a[0], na), __fdiv_rn(b[0], nb));
+  float p1 = __fmul_rn(__fdiv_rn(a[1], na), __fdiv_rn(b[1], nb));
+  float p2 = __fmul_rn(__fdiv_rn(a[2], na), __fdiv_rn(b[2], nb));
+  return __fadd_rn(__fadd_rn(p0, p1), p2);
 }
 
-// F4a: angular score of every member of every final row (no in-place
-// writes, so the exactly-3-rows quirk can read the other rows).  quirk3:
-// torch.cross without dim= picks dim 0 when there are exactly 3 rows
-// (geometry.py:500).  key = (descending score << 32) | position.
+__device__ __forceinline__ float dot3_bmm(const float c[3], const float n[3]) {
+  return __fadd_rn(__fadd_rn(__fmul_rn(c[0], n[0]), __fmul_rn(c[1], n[1])), __fmul_rn(c[2], n[2]));
+}
+
+// F4a: angular score of every entry of every final row's PADDED row (width
+// M = the largest region; pads are the zero point), exactly as
+// sort_polygon_vertices_batch evaluates it -- the pads matter because the
+// reference sorts them together with the members (an unstable sort, so
+// their positions steer how exact ties among members resolve).
+// quirk3: torch.cross without dim= picks dim 0 when there are exactly 3 rows
+// (geometry.py:500).
 __global__ void k_row_score(int64_t F, const int32_t* __restrict__ frow, const uint64_t* __restrict__ mem,
-                            const int64_t* __restrict__ roff, const int32_t* __restrict__ rcnt,
+                            const int64_t* __restrict__ roff, const int32_t* __restrict__ rcnt, int M,
                             const float* __restrict__ xyz, const float* __restrict__ nrm, int quirk3,
-                            uint64_t* __restrict__ key, int32_t* __restrict__ cnt_all,
+                            float* __restrict__ skey, int32_t* __restrict__ sidx, int32_t* __restrict__ cnt_all,
                             int32_t* __restrict__ cnt_nz) {
   int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (f >= F) return;
@@ -308,11 +377,11 @@ __global__ void k_row_score(int64_t F, const int32_t* __restrict__ frow, const u
   const int c = rcnt[r];
   const int64_t off = roff[r];
   float cen[3];
-  row_centroid(mem, off, c, xyz, cen);
+  row_centroid(mem, off, c, M, xyz, cen);
   const int v0 = row_v(mem, off, 0);
   float u0[3];
 #pragma unroll
-  for (int d = 0; d < 3; ++d) u0[d] = xyz[3 * (int64_t)v0 + d] - cen[d];
+  for (int d = 0; d < 3; ++d) u0[d] = __fsub_rn(xyz[3 * (int64_t)v0 + d], cen[d]);
   const float n[3] = {nrm[3 * f], nrm[3 * f + 1], nrm[3 * f + 2]};
   float U0[3][3], CEN[3][3];
   int RC[3] = {0, 0, 0};
@@ -322,61 +391,208 @@ __global__ void k_row_score(int64_t F, const int32_t* __restrict__ frow, const u
       int rq = frow[q];
       RC[q] = rcnt[rq];
       ROFF[q] = roff[rq];
-      row_centroid(mem, ROFF[q], RC[q], xyz, CEN[q]);
+      row_centroid(mem, ROFF[q], RC[q], M, xyz, CEN[q]);
       int bq = row_v(mem, ROFF[q], 0);
-      for (int d = 0; d < 3; ++d) U0[q][d] = xyz[3 * (int64_t)bq + d] - CEN[q][d];
+      for (int d = 0; d < 3; ++d) U0[q][d] = __fsub_rn(xyz[3 * (int64_t)bq + d], CEN[q][d]);
     }
   }
   int nz = 0;
-  for (int i = 0; i < c; ++i) {
-    int v = row_v(mem, off, i);
-    float p[3] = {xyz[3 * (int64_t)v], xyz[3 * (int64_t)v + 1], xyz[3 * (int64_t)v + 2]};
-    nz += (p[0] != 0.f || p[1] != 0.f || p[2] != 0.f);
-    float u[3] = {p[0] - cen[0], p[1] - cen[1], p[2] - cen[2]};
+  float* key = skey + f * (int64_t)M;
+  int32_t* idx = sidx + f * (int64_t)M;
+  for (int i = 0; i < M; ++i) {
+    float p[3] = {0.f, 0.f, 0.f};
+    if (i < c) {
+      int v = row_v(mem, off, i);
+      p[0] = xyz[3 * (int64_t)v];
+      p[1] = xyz[3 * (int64_t)v + 1];
+      p[2] = xyz[3 * (int64_t)v + 2];
+      nz += nonzero3(p);
+    }
+    float u[3] = {__fsub_rn(p[0], cen[0]), __fsub_rn(p[1], cen[1]), __fsub_rn(p[2], cen[2])};
     float dd = 0.f;
     if (!quirk3) {
       float cr[3];
       cross3(u0, u, cr);
-      dd = cr[0] * n[0] + cr[1] * n[1] + cr[2] * n[2];
+      dd = dot3_bmm(cr, n);
     } else {
       // D[q][m][c] = (a x b)[q] with a = (u_q[0][c])_q, b = (u_q[m][c])_q
+      float col[3];
       for (int cc = 0; cc < 3; ++cc) {
         float av[3], bv[3], o[3];
         for (int q = 0; q < 3; ++q) {
           av[q] = U0[q][cc];
-          if (i < RC[q]) {
-            int vq = row_v(mem, ROFF[q], i);
-            bv[q] = xyz[3 * (int64_t)vq + cc] - CEN[q][cc];
-          } else {
-            bv[q] = -CEN[q][cc];  // padding entry: the zero point minus the centroid
-          }
+          float pq = 0.f;
+          if (i < RC[q]) pq = xyz[3 * (int64_t)row_v(mem, ROFF[q], i) + cc];
+          bv[q] = __fsub_rn(pq, CEN[q][cc]);
         }
         cross3(av, bv, o);
-        dd += o[f] * n[cc];
+        col[cc] = o[f];
       }
+      dd = dot3_bmm(col, n);
     }
     float cs = cosine(u0, u);
-    float sc = cs * (dd >= 0.f ? 1.f : -1.f) + (dd < 0.f ? 2.f : 0.f);
-    uint32_t sb = __float_as_uint(sc);
-    sb = (sb & 0x80000000u) ? ~sb : (sb | 0x80000000u);  // ascending-orderable bits
-    key[off + i] = ((uint64_t)(~sb) << 32) | (uint64_t)(uint32_t)i;  // descending score
+    key[i] = __fadd_rn(__fmul_rn(cs, dd >= 0.f ? 1.f : -1.f), dd < 0.f ? 2.f : 0.f);
+    idx[i] = i;
   }
   cnt_all[f] = c;
   cnt_nz[f] = nz;
 }
 
-// F4b: sort each row's keys (descending score, then position) and write the
-// ordered vertex ids
+// ---- libstdc++ std::sort (introsort) with torch's KeyValueCompDesc ----------
+// torch.sort(descending=True, stable=False) on CPU (ATen SortingKernel) runs
+// std::sort over (value, index) pairs comparing values only; emulated step by
+// step so that exact ties land where the reference puts them.
+struct KV {
+  float k;
+  int32_t v;
+};
+
+__device__ __forceinline__ bool kv_less(const KV& a, const KV& b) {  // "comes first"
+  return (isnan(a.k) && !isnan(b.k)) || (a.k > b.k);
+}
+__device__ __forceinline__ void kv_swap(KV* a, KV* b) {
+  KV t = *a;
+  *a = *b;
+  *b = t;
+}
+__device__ void unguarded_linear_insert(KV* last) {
+  KV val = *last;
+  KV* next = last - 1;
+  while (kv_less(val, *next)) {
+    *last = *next;
+    last = next;
+    --next;
+  }
+  *last = val;
+}
+__device__ void insertion_sort(KV* first, KV* last) {
+  if (first == last) return;
+  for (KV* i = first + 1; i != last; ++i) {
+    if (kv_less(*i, *first)) {
+      KV val = *i;
+      for (KV* p = i; p != first; --p) *p = *(p - 1);
+      *first = val;
+    } else {
+      unguarded_linear_insert(i);
+    }
+  }
+}
+__device__ void move_median_to_first(KV* result, KV* a, KV* b, KV* c) {
+  if (kv_less(*a, *b)) {
+    if (kv_less(*b, *c)) kv_swap(result, b);
+    else if (kv_less(*a, *c)) kv_swap(result, c);
+    else kv_swap(result, a);
+  } else if (kv_less(*a, *c)) {
+    kv_swap(result, a);
+  } else if (kv_less(*b, *c)) {
+    kv_swap(result, c);
+  } else {
+    kv_swap(result, b);
+  }
+}
+__device__ KV* unguarded_partition(KV* first, KV* last, KV* pivot) {
+  while (true) {
+    while (kv_less(*first, *pivot)) ++first;
+    --last;
+    while (kv_less(*pivot, *last)) --last;
+    if (!(first < last)) return first;
+    kv_swap(first, last);
+    ++first;
+  }
+}
+__device__ void push_heap_(KV* first, int64_t hole, int64_t top, KV value) {
+  int64_t parent = (hole - 1) / 2;
+  while (hole > top && kv_less(first[parent], value)) {
+    first[hole] = first[parent];
+    hole = parent;
+    parent = (hole - 1) / 2;
+  }
+  first[hole] = value;
+}
+__device__ void adjust_heap(KV* first, int64_t hole, int64_t len, KV value) {
+  const int64_t top = hole;
+  int64_t child = hole;
+  while (child < (len - 1) / 2) {
+    child = 2 * (child + 1);
+    if (kv_less(first[child], first[child - 1])) child--;
+    first[hole] = first[child];
+    hole = child;
+  }
+  if ((len & 1) == 0 && child == (len - 2) / 2) {
+    child = 2 * (child + 1);
+    first[hole] = first[child - 1];
+    hole = child - 1;
+  }
+  push_heap_(first, hole, top, value);
+}
+__device__ void heap_sort(KV* first, KV* last) {  // std::__partial_sort(first, last, last)
+  int64_t len = last - first;
+  if (len >= 2) {
+    for (int64_t parent = (len - 2) / 2;; --parent) {
+      adjust_heap(first, parent, len, first[parent]);
+      if (parent == 0) break;
+    }
+  }
+  while (last - first > 1) {
+    --last;
+    KV value = *last;
+    *last = *first;
+    adjust_heap(first, 0, last - first, value);
+  }
+}
+__device__ void std_sort(KV* first, KV* last) {
+  const int64_t n = last - first;
+  if (n <= 1) return;
+  int depth0 = 2 * (63 - __builtin_clzll((uint64_t)n));
+  // introsort loop; sub-ranges are independent, so an explicit stack
+  // visits them in a different order with identical results
+  struct Rng { KV* f; KV* l; int d; };
+  Rng stack[64];
+  int sp = 0;
+  stack[sp++] = {first, last, depth0};
+  while (sp) {
+    Rng g = stack[--sp];
+    KV* f = g.f;
+    KV* l = g.l;
+    int depth = g.d;
+    while (l - f > 16) {
+      if (depth == 0) {
+        heap_sort(f, l);
+        l = f;
+        break;
+      }
+      --depth;
+      KV* mid = f + (l - f) / 2;
+      move_median_to_first(f, f + 1, mid, l - 1);
+      KV* cut = unguarded_partition(f + 1, l, f);
+      stack[sp++] = {cut, l, depth};
+      l = cut;
+    }
+  }
+  if (n > 16) {
+    insertion_sort(first, first + 16);
+    for (KV* i = first + 16; i != last; ++i) unguarded_linear_insert(i);
+  } else {
+    insertion_sort(first, last);
+  }
+}
+
+// F4b: sort each padded row and write the members' ids in sorted order
 __global__ void k_row_sort(int64_t F, const int32_t* __restrict__ frow, const uint64_t* __restrict__ mem,
-                           const int64_t* __restrict__ roff, const int32_t* __restrict__ rcnt,
-                           uint64_t* __restrict__ key, int32_t* __restrict__ ordv) {
+                           const int64_t* __restrict__ roff, const int32_t* __restrict__ rcnt, int M,
+                           KV* __restrict__ kv, const float* __restrict__ skey, const int32_t* __restrict__ sidx,
+                           int32_t* __restrict__ ordv) {
   int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (f >= F) return;
   const int r = frow[f];
   const int c = rcnt[r];
   const int64_t off = roff[r];
-  shell_sort(key + off, c);
-  for (int j = 0; j < c; ++j) ordv[off + j] = row_v(mem, off, (int)(uint32_t)key[off + j]);
+  KV* a = kv + f * (int64_t)M;
+  for (int i = 0; i < M; ++i) a[i] = KV{skey[f * (int64_t)M + i], sidx[f * (int64_t)M + i]};
+  std_sort(a, a + M);
+  int j = 0;
+  for (int i = 0; i < M; ++i)
+    if (a[i].v < c) ordv[off + j++] = row_v(mem, off, a[i].v);
 }
 
 // F5: per block of rows, how many rows have c >= t+3, t-major layout
@@ -499,19 +715,26 @@ int launch_compact_rows(int64_t n, const int32_t* keep, const int64_t* koff, con
   return 0;
 }
 int launch_row_mean(int64_t F, const int32_t* frow, const uint64_t* mem, const int64_t* roff,
-                    const int32_t* rcnt, const float* xyz, float* mean, hipStream_t s) {
+                    const int32_t* rcnt, int M, const float* xyz, float* mean, hipStream_t s) {
   if (F <= 0) return 0;
-  hipLaunchKernelGGL(k_row_mean, dim3(tnp_grid(F)), dim3(TNP_BLOCK), 0, s, F, frow, mem, roff, rcnt, xyz, mean);
+  hipLaunchKernelGGL(k_row_mean, dim3(tnp_grid(F)), dim3(TNP_BLOCK), 0, s, F, frow, mem, roff, rcnt, M, xyz,
+                     mean);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
+size_t row_order_scratch(int64_t F, int M) { return (size_t)F * M * (sizeof(float) + 4 + sizeof(KV)); }
+
 int launch_row_order(int64_t F, const int32_t* frow, const uint64_t* mem, const int64_t* roff,
-                     const int32_t* rcnt, const float* xyz, const float* nrm, int quirk3, uint64_t* key,
+                     const int32_t* rcnt, int M, const float* xyz, const float* nrm, int quirk3, void* scratch,
                      int32_t* ordv, int32_t* cnt_all, int32_t* cnt_nz, hipStream_t s) {
   if (F <= 0) return 0;
-  hipLaunchKernelGGL(k_row_score, dim3(tnp_grid(F)), dim3(TNP_BLOCK), 0, s, F, frow, mem, roff, rcnt, xyz, nrm,
-                     quirk3, key, cnt_all, cnt_nz);
-  hipLaunchKernelGGL(k_row_sort, dim3(tnp_grid(F)), dim3(TNP_BLOCK), 0, s, F, frow, mem, roff, rcnt, key, ordv);
+  float* skey = static_cast<float*>(scratch);
+  int32_t* sidx = reinterpret_cast<int32_t*>(skey + F * (int64_t)M);
+  KV* kv = reinterpret_cast<KV*>(sidx + F * (int64_t)M);
+  hipLaunchKernelGGL(k_row_score, dim3(tnp_grid(F)), dim3(TNP_BLOCK), 0, s, F, frow, mem, roff, rcnt, M, xyz,
+                     nrm, quirk3, skey, sidx, cnt_all, cnt_nz);
+  hipLaunchKernelGGL(k_row_sort, dim3(tnp_grid(F)), dim3(TNP_BLOCK), 0, s, F, frow, mem, roff, rcnt, M, kv, skey,
+                     sidx, ordv);
   TNP_CHECK(hipGetLastError());
   return 0;
 }

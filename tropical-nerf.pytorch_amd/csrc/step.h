@@ -21,14 +21,16 @@ enum {
   CTR_TRI = 13,
   CTR_FACES = 14,
   CTR_AUX = 15,
-  CTR_N = 16
+  CTR_DUP = 16,     // splits on the slab's shared boundary plane
+  CTR_N = 24
 };
 
 int64_t step_tiles(int64_t n);
 int launch_split_count(const int32_t* edges, int64_t E, const float* col, float eps, int32_t* blk,
                        hipStream_t s);
 int launch_split_emit(int32_t* edges, int64_t E, const float* col, float eps, const int64_t* blkoff,
-                      int64_t V, int32_t* sa, int32_t* sb, hipStream_t s);
+                      int64_t V, int32_t* sa, int32_t* sb, int dup_mark, const uint64_t* grid,
+                      int64_t* ctr, hipStream_t s);
 int launch_new_vertices(const int32_t* sa, const int32_t* sb, int64_t S, const float* col,
                         float eps, float* xyz, int64_t V, hipStream_t s);
 int launch_fail_check(const int32_t* sa, const int32_t* sb, int64_t S, int idx,

@@ -60,10 +60,12 @@ k_split_count(const int32_t* __restrict__ edges, int64_t E, const float* __restr
 __global__ void __launch_bounds__(TNP_BLOCK)
 k_split_emit(int32_t* __restrict__ edges, int64_t E, const float* __restrict__ col, float eps,
              const int64_t* __restrict__ blkoff, int64_t V, int32_t* __restrict__ sa,
-             int32_t* __restrict__ sb) {
+             int32_t* __restrict__ sb, int dup_mark, const uint64_t* __restrict__ grid,
+             int64_t* __restrict__ ctr) {
   __shared__ int lds[TNP_WAVES];
   int64_t base = (int64_t)blockIdx.x * TILE;
   int64_t run = blkoff[blockIdx.x];
+  int dup = 0;
   for (int k = 0; k < IPT; ++k) {
     int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
     bool f = (i < E) && split_test(col, edges + 2 * i, eps);
@@ -71,11 +73,23 @@ k_split_emit(int32_t* __restrict__ edges, int64_t E, const float* __restrict__ c
     int r = tnp::block_rank(f, lds, tot);
     if (f) {
       int64_t id = run + r;
-      sa[id] = edges[2 * i];
-      sb[id] = edges[2 * i + 1];
+      int a = edges[2 * i], b = edges[2 * i + 1];
+      sa[id] = a;
+      sb[id] = b;
       edges[2 * i + 1] = (int32_t)(V + id);
+      if (dup_mark >= 0) {
+        // edge lying in this slab's upper boundary mark plane (x = mark):
+        // the neighbouring slab splits the same edge, count it once
+        uint64_t ga = grid[a], gb = grid[b];
+        dup += tnp::grid_zero(ga, 0) && tnp::grid_zero(gb, 0) && tnp::grid_off(ga, 0) == dup_mark &&
+               tnp::grid_off(gb, 0) == dup_mark;
+      }
     }
     run += tot;
+  }
+  if (dup_mark >= 0) {
+    dup = tnp::wave_sum(dup);
+    if (tnp::lane() == 0 && dup) atomicAdd((unsigned long long*)&ctr[CTR_DUP], (unsigned long long)dup);
   }
 }
 
@@ -520,9 +534,10 @@ int launch_split_count(const int32_t* edges, int64_t E, const float* col, float 
   return 0;
 }
 int launch_split_emit(int32_t* edges, int64_t E, const float* col, float eps, const int64_t* blkoff,
-                      int64_t V, int32_t* sa, int32_t* sb, hipStream_t s) {
+                      int64_t V, int32_t* sa, int32_t* sb, int dup_mark, const uint64_t* grid,
+                      int64_t* ctr, hipStream_t s) {
   hipLaunchKernelGGL(k_split_emit, dim3((unsigned)step_tiles(E)), dim3(TNP_BLOCK), 0, s, edges, E,
-                     col, eps, blkoff, V, sa, sb);
+                     col, eps, blkoff, V, sa, sb, dup_mark, grid, ctr);
   TNP_CHECK(hipGetLastError());
   return 0;
 }

@@ -83,6 +83,24 @@ class Engine:
                                                 _hip.ptr(cache), self._s), "tnp_engine_export")
         return verts, edges, cache
 
+    def set_dup_plane(self, mark: int):
+        _hip.check(_hip.lib().tnp_engine_set_dup_plane(self.h, int(mark)), "tnp_engine_set_dup_plane")
+
+    def kernel_timer(self, on: bool):
+        """on=True: start HIP-event timing of every engine launch; on=False:
+        stop and return {kernel: {"ms", "launches", "bytes"}}."""
+        n = C.c_int32()
+        _hip.check(_hip.lib().tnp_engine_kernel_timer(self.h, int(on), self._s, C.byref(n)),
+                   "tnp_engine_kernel_timer")
+        out = {}
+        for i in range(n.value):
+            name = C.create_string_buffer(64)
+            ms, nl, by = C.c_double(), C.c_int64(), C.c_double()
+            _hip.check(_hip.lib().tnp_engine_kernel_stat(self.h, i, name, 64, C.byref(ms), C.byref(nl),
+                                                         C.byref(by)), "tnp_engine_kernel_stat")
+            out[name.value.decode()] = {"ms": ms.value, "launches": nl.value, "bytes": by.value}
+        return out
+
     # -- steps ---------------------------------------------------------------
     def active_planes(self, start: int = 0) -> int:
         m = C.c_uint64()

@@ -33,7 +33,7 @@ class TnpStepStats(C.Structure):
         ("V_in", C.c_int64), ("E_in", C.c_int64), ("S", C.c_int64), ("H", C.c_int64),
         ("X", C.c_int64), ("V_out", C.c_int64), ("E_out", C.c_int64),
         ("A", C.c_int64), ("P", C.c_int64), ("pair_tests", C.c_int64),
-        ("override_applied", C.c_int32), ("next_active", C.c_uint64),
+        ("override_applied", C.c_int32), ("next_active", C.c_uint64), ("S_dup", C.c_int64),
     ]
 
     def as_dict(self):
@@ -67,6 +67,12 @@ SIGNATURES = {
     "tnp_engine_surface": (C.c_int, [_VP, _VP, _P64, _P64]),
     "tnp_engine_faces": (C.c_int, [_VP, _VP, _P64, _P64]),
     "tnp_engine_faces_export": (C.c_int, [_VP, _VP, _VP, _VP]),
+    "tnp_engine_set_dup_plane": (C.c_int, [_VP, C.c_int]),
+    "tnp_debug_ops": (C.c_int, [_VP, _VP, _VP, C.c_int64, _VP, _VP]),
+    "tnp_engine_faces_debug": (C.c_int, [_VP, _VP, C.c_int64, _P64, _P64, _VP]),
+    "tnp_engine_kernel_timer": (C.c_int, [_VP, C.c_int, _VP, _P32]),
+    "tnp_engine_kernel_stat": (C.c_int, [_VP, C.c_int, C.c_char_p, C.c_int, C.POINTER(C.c_double),
+                                         _P64, C.POINTER(C.c_double)]),
 }
 
 _lib = None
