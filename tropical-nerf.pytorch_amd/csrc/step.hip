@@ -21,6 +21,8 @@
 #include "kernels.h"
 #include "step.h"
 
+#include <algorithm>
+
 namespace {
 
 constexpr int IPT = 8;                  // items per thread per tile
@@ -353,6 +355,17 @@ k_pairs(const int32_t* __restrict__ ent_v, const int32_t* __restrict__ ent_c, in
   }
 }
 
+// total member-pair tests of the cell buckets: sum_c n_c (n_c - 1) / 2
+__global__ void k_cell_pairs(const int32_t* __restrict__ cellcnt, int64_t n, int64_t* __restrict__ ctr) {
+  int64_t t = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t c = cellcnt[i];
+    t += c * (c - 1) / 2;
+  }
+  t = tnp::wave_sum(t);
+  if (tnp::lane() == 0 && t) atomicAdd((unsigned long long*)&ctr[CTR_AUX], (unsigned long long)t);
+}
+
 // sort each lo-bucket by hi (shell sort; buckets are small, but degenerate
 // regions can make a few large ones) and record lo per pair
 __global__ void k_pair_sort(const int64_t* __restrict__ pairoff, const int32_t* __restrict__ paircnt,
@@ -613,6 +626,12 @@ int launch_pairs(bool emit, const int32_t* ent_v, const int32_t* ent_c, int64_t 
     hipLaunchKernelGGL(k_pairs<false>, dim3(tnp_grid(T)), dim3(TNP_BLOCK), 0, s, ent_v, ent_c, T,
                        celloff, cellcnt, NC, idx, pos, zero, grid, paircnt, pairoff, paircur,
                        pair_hi, ctr);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_cell_pairs(const int32_t* cellcnt, int64_t n, int64_t* ctr, hipStream_t s) {
+  unsigned g = (unsigned)std::min<int64_t>(tnp_grid(n), 2048);
+  hipLaunchKernelGGL(k_cell_pairs, dim3(g), dim3(TNP_BLOCK), 0, s, cellcnt, n, ctr);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
