@@ -2,6 +2,7 @@
 # One GPU-box session: parity tests, then a short bench.  Stops at the first
 # step that ends in anything but success/test-failure (fault, abort, timeout).
 set -u
+export TMPDIR=/tmp
 mkdir -p gpurun_out
 run() {  # name timeout cmd...
   local name=$1 t=$2; shift 2
@@ -19,6 +20,9 @@ for step in "$@"; do
     bench) run bench 900 python bench.py --steps 3 --warmup 1 ;;
     benchfast) run bench 600 python bench.py --steps 3 --warmup 1 --no-cpu ;;
     smoke) run smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    stats) run step_stats 300 python tools/step_stats.py 128 6 ;;
+    pmcf) run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu ;;
+    pmcw) run pmc_write 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu ;;
     prof) run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu ;;
   esac
 done

@@ -6,7 +6,7 @@ from bench import make_net
 from tropical._engine import engine_for
 G = int(sys.argv[1]) if len(sys.argv) > 1 else 128
 dev = torch.device("cuda", 0)
-net = make_net(G, dev, 0)
+net = make_net(G, dev, int(sys.argv[2]) if len(sys.argv) > 2 else 6)
 eng = engine_for(net)
 eng.lattice()
 stats = []

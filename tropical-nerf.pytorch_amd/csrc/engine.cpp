@@ -126,7 +126,9 @@ struct tnp_engine {
   int valid_from = 0;  // pre planes [valid_from, K) are valid for every vertex
   // step scratch
   Buf blk, blkoff, scan_scr, sa, sb, stage, shared, members, cellcnt, cellcur, celloff, ent_v,
-      ent_c, paircnt, paircur, pairoff, pair_hi, pair_lo, used, nid, ctr;
+      ent_g, ent_p, ent_z, tcnt, toff, bcell, bstat, ckeys_a, ckeys_b, sort_scr, flags, used, nid,
+      ctr;
+  uint64_t* ckeys = nullptr;  // sorted connecting edges of the current step
   int64_t* h_ctr = nullptr;  // pinned mirror of ctr
   // pending split
   int pend_idx = -1;
@@ -236,8 +238,9 @@ extern "C" void tnp_engine_destroy(tnp_engine* e) {
   }
   Buf* bufs[] = {&e->edges, &e->edges_alt, &e->blk, &e->blkoff, &e->scan_scr, &e->sa, &e->sb,
                  &e->stage, &e->shared, &e->members, &e->cellcnt, &e->cellcur, &e->celloff,
-                 &e->ent_v, &e->ent_c, &e->paircnt, &e->paircur, &e->pairoff, &e->pair_hi,
-                 &e->pair_lo, &e->used, &e->nid, &e->ctr, &e->tri, &e->faces};
+                 &e->ent_v, &e->ent_g, &e->ent_p, &e->ent_z, &e->tcnt, &e->toff, &e->bcell,
+                 &e->bstat, &e->ckeys_a, &e->ckeys_b, &e->sort_scr, &e->flags, &e->used, &e->nid,
+                 &e->ctr, &e->tri, &e->faces};
   for (Buf* b : bufs) buf_free(*b, s);
   for (Buf& b : e->fscr) buf_free(b, s);
   for (Buf& b : e->fscr2) buf_free(b, s);
@@ -468,15 +471,19 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   const int64_t M = S + H;
   TIMED("cell_count", 24.0 * M, launch_cell_count(P<int32_t>(e->members), M, grid, zero, idx, NC, P<int32_t>(e->cellcnt), ctr, s));
   if (scan_counts(e, P<int32_t>(e->cellcnt), P<int64_t>(e->celloff), ncell, CTR_T, s)) return -1;
-  TNP_CHECK(hipMemsetAsync(ctr + CTR_AUX, 0, sizeof(int64_t), s));
-  if (launch_cell_pairs(P<int32_t>(e->cellcnt), ncell, ctr, s)) return -1;
+  // member pairs per cell -> flattened pair space offsets (total = tests)
+  if (buf_ensure(e->tcnt, ncell * sizeof(int32_t), s)) return -1;
+  if (buf_ensure(e->toff, ncell * sizeof(int64_t), s)) return -1;
+  if (launch_cell_tcnt(P<int32_t>(e->cellcnt), ncell, P<int32_t>(e->tcnt), ctr, s)) return -1;
+  if (scan_counts(e, P<int32_t>(e->tcnt), P<int64_t>(e->toff), ncell, CTR_TESTS, s)) return -1;
   if (read_ctr(e, s)) return -1;
-  if (e->h_ctr[CTR_AUX] > e->max_pair_tests) {
+  const int64_t TT = e->h_ctr[CTR_TESTS];
+  if (e->h_ctr[CTR_BIG] || TT > e->max_pair_tests) {
     // one linear region holding ~sqrt(2*tests) vertices: the reference would
     // materialise every in-region pair (subpoly.py:505-518) and run out of
     // memory long before; refuse instead of grinding for hours
     tnp_set_error("degenerate complex at plane %d: %lld in-cell vertex pairs exceed the limit %lld "
-                  "(TNP_MAX_PAIR_TESTS)", idx, (long long)e->h_ctr[CTR_AUX], (long long)e->max_pair_tests);
+                  "(TNP_MAX_PAIR_TESTS)", idx, (long long)TT, (long long)e->max_pair_tests);
     return -1;
   }
   if (e->h_ctr[CTR_K0]) {
@@ -486,39 +493,52 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   }
   const int64_t T = e->h_ctr[CTR_T];
   if (buf_ensure(e->ent_v, std::max<int64_t>(T, 1) * sizeof(int32_t), s)) return -1;
-  if (buf_ensure(e->ent_c, std::max<int64_t>(T, 1) * sizeof(int32_t), s)) return -1;
-  TIMED("cell_scatter", 12.0 * M + 20.0 * T,
-        launch_cell_scatter(P<int32_t>(e->members), M, grid, NC, P<int64_t>(e->celloff),
-                            P<int32_t>(e->cellcur), P<int32_t>(e->ent_v), P<int32_t>(e->ent_c), s));
+  if (buf_ensure(e->ent_g, std::max<int64_t>(T, 1) * sizeof(uint64_t), s)) return -1;
+  if (buf_ensure(e->ent_p, std::max<int64_t>(T, 1) * sizeof(uint64_t), s)) return -1;
+  if (buf_ensure(e->ent_z, std::max<int64_t>(T, 1) * sizeof(uint64_t), s)) return -1;
+  TIMED("cell_scatter", 28.0 * M + 32.0 * T,
+        launch_cell_scatter(P<int32_t>(e->members), M, grid, pos, zero, NC, P<int64_t>(e->celloff),
+                            P<int32_t>(e->cellcur), P<int32_t>(e->ent_v), P<uint64_t>(e->ent_g),
+                            P<uint64_t>(e->ent_p), P<uint64_t>(e->ent_z), s));
 
-  // 4. connecting edges, bucketed by their smaller endpoint
-  if (buf_ensure(e->paircnt, std::max<int64_t>(NV, 1) * sizeof(int32_t), s)) return -1;
-  if (buf_ensure(e->paircur, std::max<int64_t>(NV, 1) * sizeof(int32_t), s)) return -1;
-  if (buf_ensure(e->pairoff, std::max<int64_t>(NV, 1) * sizeof(int64_t), s)) return -1;
-  TNP_CHECK(hipMemsetAsync(e->paircnt.p, 0, NV * sizeof(int32_t), s));
-  TNP_CHECK(hipMemsetAsync(e->paircur.p, 0, NV * sizeof(int32_t), s));
-  TIMED("pairs_count", 8.0 * T,
-        launch_pairs(false, P<int32_t>(e->ent_v), P<int32_t>(e->ent_c), T, P<int64_t>(e->celloff),
-                     P<int32_t>(e->cellcnt), NC, idx, pos, zero, grid, P<int32_t>(e->paircnt),
-                     nullptr, nullptr, nullptr, ctr, s));
-  if (scan_counts(e, P<int32_t>(e->paircnt), P<int64_t>(e->pairoff), NV, CTR_X, s)) return -1;
-  if (read_ctr(e, s)) return -1;
+  // 4. connecting edges: test every in-cell member pair once, append the
+  //    emitted ones, radix-sort them (lexicographic c_new, subpoly.py:243-244)
+  int nb = 1;
+  while (nb < 31 && (1ll << nb) < NV) ++nb;
+  const int64_t nblk = connect_blocks(TT);
+  if (buf_ensure(e->bcell, std::max<int64_t>(nblk, 1) * sizeof(int32_t), s)) return -1;
+  if (buf_ensure(e->bstat, std::max<int64_t>(nblk, 1) * 2 * sizeof(int64_t), s)) return -1;
+  int64_t cap = std::max<int64_t>(e->ckeys_a.bytes / sizeof(uint64_t), std::min<int64_t>(TT, 4 * M + 1024));
+  cap = std::min<int64_t>(cap, std::max<int64_t>(TT, 1));
+  int64_t X = 0;
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    if (buf_ensure(e->ckeys_a, std::max<int64_t>(cap, 1) * sizeof(uint64_t), s)) return -1;
+    TNP_CHECK(hipMemsetAsync(ctr + CTR_X, 0, sizeof(int64_t), s));
+    TNP_CHECK(hipMemsetAsync(ctr + CTR_P, 0, 2 * sizeof(int64_t), s));  // CTR_P, CTR_COMPAT
+    TIMED("connect", 32.0 * TT + 8.0 * T,
+          launch_connect(P<int64_t>(e->toff), P<int32_t>(e->cellcnt), P<int64_t>(e->celloff), ncell,
+                         NC, TT, P<int32_t>(e->bcell), P<int32_t>(e->ent_v), P<uint64_t>(e->ent_g),
+                         P<uint64_t>(e->ent_p), P<uint64_t>(e->ent_z), idx, nb,
+                         P<uint64_t>(e->ckeys_a), cap, ctr, P<int64_t>(e->bstat), s));
+    if (read_ctr(e, s)) return -1;
+    X = e->h_ctr[CTR_X];
+    if (X <= cap) break;
+    cap = X;  // appended beyond the buffer: grow to the exact count and redo
+  }
   if (e->h_ctr[CTR_COMPAT] == 0) {
     // every region has a single member: extract_every_valid_edge cats an
     // empty list (subpoly.py:505-513)
     tnp_set_error("torch.cat(): expected a non-empty list of Tensors (no region with two vertices, plane %d)", idx);
     return -1;
   }
-  const int64_t X = e->h_ctr[CTR_X];
-  if (buf_ensure(e->pair_hi, std::max<int64_t>(X, 1) * sizeof(int32_t), s)) return -1;
-  if (buf_ensure(e->pair_lo, std::max<int64_t>(X, 1) * sizeof(int32_t), s)) return -1;
-  TIMED("pairs_emit", 8.0 * T + 4.0 * X,
-        launch_pairs(true, P<int32_t>(e->ent_v), P<int32_t>(e->ent_c), T, P<int64_t>(e->celloff),
-                     P<int32_t>(e->cellcnt), NC, idx, pos, zero, grid, P<int32_t>(e->paircnt),
-                     P<int64_t>(e->pairoff), P<int32_t>(e->paircur), P<int32_t>(e->pair_hi), ctr, s));
-  TIMED("pair_sort", 12.0 * NV + 12.0 * X,
-        launch_pair_sort(P<int64_t>(e->pairoff), P<int32_t>(e->paircnt), NV, P<int32_t>(e->pair_hi),
-                         P<int32_t>(e->pair_lo), s));
+  if (buf_ensure(e->ckeys_b, std::max<int64_t>(X, 1) * sizeof(uint64_t), s)) return -1;
+  {
+    size_t need = sort_scratch_bytes(X, 2 * nb);
+    if (buf_ensure(e->sort_scr, std::max<size_t>(need, 16), s)) return -1;
+    TIMED("pair_sort", 16.0 * X * ((2 * nb + 7) / 8),
+          sort_keys_u64(P<uint64_t>(e->ckeys_a), P<uint64_t>(e->ckeys_b), X, 2 * nb, e->sort_scr.p,
+                        e->sort_scr.bytes, &e->ckeys, s));
+  }
 
   // 5. pruning over [edges; e_new; c_new] + vertex compaction
   const int64_t N = E + S + X;
@@ -535,13 +555,11 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     if (buf_ensure(e->nid, std::max<int64_t>(NV, 1) * sizeof(int64_t), s)) return -1;
     TNP_CHECK(hipMemsetAsync(e->used.p, 0, NV * sizeof(int32_t), s));
     TIMED("prune_count", 40.0 * N,
-          launch_prune(false, eg, E, P<int32_t>(e->sb), S, V, P<int32_t>(e->pair_lo),
-                       P<int32_t>(e->pair_hi), X, idx, 1, K - 1, pos, zero, P<int32_t>(e->blk),
+          launch_prune(false, eg, E, P<int32_t>(e->sb), S, V, e->ckeys, nb, X, idx, 1, K - 1, pos, zero, P<int32_t>(e->blk),
                        nullptr, nullptr, nullptr, ctr, s));
     if (scan_counts(e, P<int32_t>(e->blk), P<int64_t>(e->blkoff), nt, CTR_E, s)) return -1;
     TIMED("prune_emit", 40.0 * N,
-          launch_prune(true, eg, E, P<int32_t>(e->sb), S, V, P<int32_t>(e->pair_lo),
-                       P<int32_t>(e->pair_hi), X, idx, 1, K - 1, pos, zero, nullptr,
+          launch_prune(true, eg, E, P<int32_t>(e->sb), S, V, e->ckeys, nb, X, idx, 1, K - 1, pos, zero, nullptr,
                        P<int64_t>(e->blkoff), P<int32_t>(e->edges_alt), P<int32_t>(e->used), ctr, s));
     if (scan_counts(e, P<int32_t>(e->used), P<int64_t>(e->nid), NV, CTR_V, s)) return -1;
     next_valid = e->keep_all ? 0 : std::min(idx + 1, K - 1);
@@ -558,8 +576,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     TIMED("remap_edges", 32.0 * E2, launch_remap_edges(P<int32_t>(e->edges_alt), E2, P<int64_t>(e->nid), s));
     std::swap(e->cur, e->alt);
   } else {
-    if (launch_prune(true, eg, E, P<int32_t>(e->sb), S, V, P<int32_t>(e->pair_lo),
-                     P<int32_t>(e->pair_hi), X, idx, 0, K - 1, pos, zero, nullptr, nullptr,
+    if (launch_prune(true, eg, E, P<int32_t>(e->sb), S, V, e->ckeys, nb, X, idx, 0, K - 1, pos, zero, nullptr, nullptr,
                      P<int32_t>(e->edges_alt), nullptr, ctr, s))
       return -1;
     if (read_ctr(e, s)) return -1;
@@ -616,10 +633,10 @@ extern "C" int tnp_engine_surface(tnp_engine* e, void* stream, int64_t* V_out, i
   VSet& c = e->cur;
   const float* col = P<float>(c.pre) + (int64_t)(e->K - 1) * c.cap;
   if (buf_ensure(e->used, std::max<int64_t>(V, 1) * sizeof(int32_t), s)) return -1;
-  if (buf_ensure(e->paircnt, std::max<int64_t>(V, 1) * sizeof(int32_t), s)) return -1;
+  if (buf_ensure(e->flags, std::max<int64_t>(V, 1) * sizeof(int32_t), s)) return -1;
   if (buf_ensure(e->nid, std::max<int64_t>(V, 1) * sizeof(int64_t), s)) return -1;
   TNP_CHECK(hipMemsetAsync(e->ctr.p, 0, CTR_N * sizeof(int64_t), s));
-  int32_t* on = P<int32_t>(e->paircnt);
+  int32_t* on = P<int32_t>(e->flags);
   if (launch_surface_flags(P<float>(c.xyz), col, V, e->net.eps, on, s)) return -1;
   if (scan_counts(e, on, P<int64_t>(e->nid), V, CTR_AUX, s)) return -1;
   if (read_ctr(e, s)) return -1;

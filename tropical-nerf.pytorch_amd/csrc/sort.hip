@@ -1,0 +1,29 @@
+// Ascending radix sort of packed u64 keys (connecting edges lo << nb | hi)
+// on their 2*nb significant bits: the lexicographic order of
+// c_new.sort(-1).unique(dim=0) (subpoly.py:243-244) -- the keys are already
+// unique, one per canonical cell.  rocPRIM's onesweep radix sort is the
+// primitive; only the significant bits are visited.
+#include <rocprim/device/device_radix_sort.hpp>
+
+#include "common.h"
+#include "step.h"
+
+size_t sort_scratch_bytes(int64_t n, int bits) {
+  size_t bytes = 0;
+  rocprim::double_buffer<uint64_t> db(nullptr, nullptr);
+  if (rocprim::radix_sort_keys(nullptr, bytes, db, (size_t)std::max<int64_t>(n, 1), 0u,
+                               (unsigned)bits) != hipSuccess)
+    return 0;
+  return bytes;
+}
+
+int sort_keys_u64(uint64_t* a, uint64_t* b, int64_t n, int bits, void* scratch, size_t scratch_bytes,
+                  uint64_t** out, hipStream_t s) {
+  *out = a;
+  if (n <= 1) return 0;
+  rocprim::double_buffer<uint64_t> db(a, b);
+  size_t bytes = scratch_bytes;
+  TNP_CHECK(rocprim::radix_sort_keys(scratch, bytes, db, (size_t)n, 0u, (unsigned)bits, s));
+  *out = db.current();
+  return 0;
+}

@@ -22,6 +22,7 @@ enum {
   CTR_FACES = 14,
   CTR_AUX = 15,
   CTR_DUP = 16,     // splits on the slab's shared boundary plane
+  CTR_BIG = 17,     // a cell with more than 65535 members
   CTR_N = 24
 };
 
@@ -44,19 +45,27 @@ int launch_hit_emit(const float* col, int64_t V, float eps, const int64_t* blkof
                     int32_t* members, int64_t S, hipStream_t s);
 int launch_cell_count(const int32_t* members, int64_t M, const uint64_t* grid, const uint64_t* zero,
                       int idx, int NC, int32_t* cellcnt, int64_t* ctr, hipStream_t s);
-int launch_cell_scatter(const int32_t* members, int64_t M, const uint64_t* grid, int NC,
-                        const int64_t* celloff, int32_t* cellcur, int32_t* ent_v, int32_t* ent_c,
-                        hipStream_t s);
-int launch_pairs(bool emit, const int32_t* ent_v, const int32_t* ent_c, int64_t T,
-                 const int64_t* celloff, const int32_t* cellcnt, int NC, int idx,
-                 const uint64_t* pos, const uint64_t* zero, const uint64_t* grid,
-                 int32_t* paircnt, const int64_t* pairoff, int32_t* paircur, int32_t* pair_hi,
-                 int64_t* ctr, hipStream_t s);
-int launch_cell_pairs(const int32_t* cellcnt, int64_t n, int64_t* ctr, hipStream_t s);
-int launch_pair_sort(const int64_t* pairoff, const int32_t* paircnt, int64_t NV, int32_t* pair_hi,
-                     int32_t* pair_lo, hipStream_t s);
+int launch_cell_scatter(const int32_t* members, int64_t M, const uint64_t* grid,
+                        const uint64_t* pos, const uint64_t* zero, int NC, const int64_t* celloff,
+                        int32_t* cellcur, int32_t* ent_v, uint64_t* ent_g, uint64_t* ent_p,
+                        uint64_t* ent_z, hipStream_t s);
+int launch_cell_tcnt(const int32_t* cellcnt, int64_t n, int32_t* tcnt, int64_t* ctr, hipStream_t s);
+int64_t connect_blocks(int64_t TT);
+// connecting-edge test over the flattened pair space; appends packed keys
+// (lo << nb | hi) to keys[0, cap) and counts them in ctr[CTR_X]
+int launch_connect(const int64_t* toff, const int32_t* cellcnt, const int64_t* celloff,
+                   int64_t ncell, int NC, int64_t TT, int32_t* bcell, const int32_t* ent_v,
+                   const uint64_t* ent_g, const uint64_t* ent_p, const uint64_t* ent_z, int idx,
+                   int nb, uint64_t* keys, int64_t cap, int64_t* ctr, int64_t* bstat,
+                   hipStream_t s);
+// ---- sort.hip ----
+// ascending LSD radix sort of n u64 keys on bits [0, bits); the sorted keys
+// end in *out (== a or b)
+size_t sort_scratch_bytes(int64_t n, int bits);
+int sort_keys_u64(uint64_t* a, uint64_t* b, int64_t n, int bits, void* scratch, size_t scratch_bytes,
+                  uint64_t** out, hipStream_t s);
 int launch_prune(bool emit, const int32_t* edges, int64_t E, const int32_t* sb, int64_t S,
-                 int64_t V, const int32_t* c_lo, const int32_t* c_hi, int64_t X, int idx,
+                 int64_t V, const uint64_t* ckeys, int nb, int64_t X, int idx,
                  int prune, int last_plane, const uint64_t* pos, const uint64_t* zero,
                  int32_t* blk, const int64_t* blkoff, int32_t* out, int32_t* used, int64_t* ctr,
                  hipStream_t s);

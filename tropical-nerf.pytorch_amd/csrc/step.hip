@@ -7,7 +7,7 @@
 //   finalize_new                                 override + packed keys
 //   hit_count -> scan -> hit_emit                 old vertices on the plane
 //   cell_count -> scan -> cell_scatter            members bucketed by grid cell
-//   pair_count -> scan -> pair_emit -> pair_sort  connecting edges c_new
+//   cell_tcnt -> scan -> connect -> radix sort    connecting edges c_new
 //   prune_count -> scan -> prune_emit             future-key pruning
 //   scan(used) -> gather_vertices, remap_edges    vertex compaction
 //
@@ -15,8 +15,9 @@
 // vertex: pos/zero u64 (bit p = plane p), grid u64 (common.h); edges int32
 // [E][2].  Everything that fixes an output ORDER is a scan in input order
 // (the reference's masked_scatter_ / sorted unique semantics); atomics only
-// produce counts and bucket membership, and every bucket is sorted before
-// it is emitted, so results are deterministic and bitwise reproducible.
+// produce counts, bucket membership and append slots, and every appended
+// set is sorted before it is used, so results are deterministic and
+// bitwise reproducible.
 #include "common.h"
 #include "kernels.h"
 #include "step.h"
@@ -245,22 +246,29 @@ __global__ void k_cell_count(const int32_t* __restrict__ members, int64_t M,
   if (__ballot(k0) && tnp::lane() == 0) atomicOr((unsigned long long*)&ctr[CTR_K0], 1ull);
 }
 
+// bucket every (member, spanned cell) entry; the member's packed keys are
+// copied entry-aligned so the pair test reads them contiguously per cell
 __global__ void k_cell_scatter(const int32_t* __restrict__ members, int64_t M,
-                               const uint64_t* __restrict__ grid, int NC,
+                               const uint64_t* __restrict__ grid, const uint64_t* __restrict__ pos,
+                               const uint64_t* __restrict__ zero, int NC,
                                const int64_t* __restrict__ celloff, int32_t* __restrict__ cellcur,
-                               int32_t* __restrict__ ent_v, int32_t* __restrict__ ent_c) {
+                               int32_t* __restrict__ ent_v, uint64_t* __restrict__ ent_g,
+                               uint64_t* __restrict__ ent_p, uint64_t* __restrict__ ent_z) {
   int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= M) return;
   int v = members[m];
+  uint64_t g = grid[v], ps = pos[v], zs = zero[v];
   int lo[3], n[3];
-  cell_span(grid[v], lo, n);
+  cell_span(g, lo, n);
   for (int i = 0; i < n[0]; ++i)
     for (int j = 0; j < n[1]; ++j)
       for (int k = 0; k < n[2]; ++k) {
         int64_t c = cell_id(lo[0] + i, lo[1] + j, lo[2] + k, NC);
         int64_t p = celloff[c] + atomicAdd(&cellcur[c], 1);
         ent_v[p] = v;
-        ent_c[p] = (int32_t)c;
+        ent_g[p] = g;
+        ent_p[p] = ps;
+        ent_z[p] = zs;
       }
 }
 
@@ -279,30 +287,23 @@ struct PairTest {
   int64_t regions;  // shared regions (for the reference's candidate count P)
 };
 
-__device__ __forceinline__ PairTest pair_test(int u, int v, int64_t cell, int NC, uint64_t below,
-                                              const uint64_t* __restrict__ pos,
-                                              const uint64_t* __restrict__ zero,
-                                              const uint64_t* __restrict__ grid) {
+__device__ __forceinline__ PairTest pair_test(const int cc[3], uint64_t below, uint64_t gu,
+                                              uint64_t pu, uint64_t zu, uint64_t gv, uint64_t pv,
+                                              uint64_t zv) {
   PairTest t{false, false, 0};
-  uint64_t gu = grid[u], gv = grid[v];
-  int cz = (int)(cell % NC) - 2;
-  int cy = (int)((cell / NC) % NC) - 2;
-  int cx = (int)(cell / ((int64_t)NC * NC)) - 2;
-  int cc[3] = {cx, cy, cz};
   int64_t reg = 1;
   bool grid_share = false;
 #pragma unroll
   for (int d = 0; d < 3; ++d) {
     int ou = tnp::grid_off(gu, d), ov = tnp::grid_off(gv, d);
-    bool zu = tnp::grid_zero(gu, d), zv = tnp::grid_zero(gv, d);
-    int lu = zu ? ou - 1 : ou, lv = zv ? ov - 1 : ov;
+    bool zdu = tnp::grid_zero(gu, d), zdv = tnp::grid_zero(gv, d);
+    int lu = zdu ? ou - 1 : ou, lv = zdv ? ov - 1 : ov;
     int lo = lu > lv ? lu : lv;
     int hi = ou < ov ? ou : ov;
     if (cc[d] != lo) return t;  // not the canonical cell (or no overlap)
     reg *= (hi - lo + 1);
-    grid_share |= zu && zv && (ou == ov);
+    grid_share |= zdu && zdv && (ou == ov);
   }
-  uint64_t pu = pos[u], pv = pos[v], zu = zero[u], zv = zero[v];
   if (((pu ^ pv) & ~zu & ~zv & below) != 0) return t;
   t.compat = true;
   t.regions = reg << __popcll(zu & zv & below);
@@ -310,88 +311,153 @@ __device__ __forceinline__ PairTest pair_test(int u, int v, int64_t cell, int NC
   return t;
 }
 
-template <bool EMIT>
-__global__ void __launch_bounds__(TNP_BLOCK)
-k_pairs(const int32_t* __restrict__ ent_v, const int32_t* __restrict__ ent_c, int64_t T,
-        const int64_t* __restrict__ celloff, const int32_t* __restrict__ cellcnt, int NC, int idx,
-        const uint64_t* __restrict__ pos, const uint64_t* __restrict__ zero,
-        const uint64_t* __restrict__ grid, int32_t* __restrict__ paircnt,
-        const int64_t* __restrict__ pairoff, int32_t* __restrict__ paircur,
-        int32_t* __restrict__ pair_hi, int64_t* __restrict__ ctr) {
-  int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  int64_t n_compat = 0, n_reg = 0, n_test = 0;
-  if (e < T) {
-    int u = ent_v[e];
-    int64_t c = ent_c[e];
-    int64_t start = celloff[c], end = start + cellcnt[c];
-    uint64_t below = (idx >= 64) ? ~0ull : ((1ull << idx) - 1ull);
-    for (int64_t q = e + 1; q < end; ++q) {
-      int v = ent_v[q];
-      PairTest t = pair_test(u, v, c, NC, below, pos, zero, grid);
-      n_test++;
-      if (!t.compat) continue;
-      n_compat++;
-      n_reg += t.regions;
-      if (!t.emit) continue;
-      int lo = u < v ? u : v, hi = u < v ? v : u;
-      if (EMIT) {
-        int64_t p = pairoff[lo] + atomicAdd(&paircur[lo], 1);
-        pair_hi[p] = hi;
-      } else {
-        atomicAdd(&paircnt[lo], 1);
-      }
-    }
-    (void)start;
-  }
-  if (!EMIT) {
-    n_compat = tnp::wave_sum(n_compat);
-    n_reg = tnp::wave_sum(n_reg);
-    n_test = tnp::wave_sum(n_test);
-    if (tnp::lane() == 0) {
-      atomicAdd((unsigned long long*)&ctr[CTR_COMPAT], (unsigned long long)n_compat);
-      atomicAdd((unsigned long long*)&ctr[CTR_P], (unsigned long long)n_reg);
-      atomicAdd((unsigned long long*)&ctr[CTR_TESTS], (unsigned long long)n_test);
-    }
-  }
-}
-
-// total member-pair tests of the cell buckets: sum_c n_c (n_c - 1) / 2
-__global__ void k_cell_pairs(const int32_t* __restrict__ cellcnt, int64_t n, int64_t* __restrict__ ctr) {
-  int64_t t = 0;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+// member pairs a cell tests: n (n - 1) / 2 (cells above 65535 members flag
+// CTR_BIG: one linear region that large is the degenerate case the host
+// refuses anyway)
+__global__ void k_cell_tcnt(const int32_t* __restrict__ cellcnt, int64_t n, int32_t* __restrict__ tcnt,
+                            int64_t* __restrict__ ctr) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool big = false;
+  if (i < n) {
     int64_t c = cellcnt[i];
-    t += c * (c - 1) / 2;
+    big = c > 65535;
+    tcnt[i] = big ? 0 : (int32_t)(c * (c - 1) / 2);
   }
-  t = tnp::wave_sum(t);
-  if (tnp::lane() == 0 && t) atomicAdd((unsigned long long*)&ctr[CTR_AUX], (unsigned long long)t);
+  if (__ballot(big) && tnp::lane() == 0) atomicOr((unsigned long long*)&ctr[CTR_BIG], 1ull);
 }
 
-// sort each lo-bucket by hi (shell sort; buckets are small, but degenerate
-// regions can make a few large ones) and record lo per pair
-__global__ void k_pair_sort(const int64_t* __restrict__ pairoff, const int32_t* __restrict__ paircnt,
-                            int64_t NV, int32_t* __restrict__ pair_hi, int32_t* __restrict__ pair_lo) {
-  int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (v >= NV) return;
-  int n = paircnt[v];
-  if (n == 0) return;
-  int32_t* a = pair_hi + pairoff[v];
-  int gap = 1;
-  while (gap < n / 3) gap = 3 * gap + 1;
-  for (; gap > 0; gap /= 3) {
-    for (int i = gap; i < n; ++i) {
-      int32_t x = a[i];
-      int j = i;
-      while (j >= gap && a[j - gap] > x) {
-        a[j] = a[j - gap];
-        j -= gap;
+// first index in [lo, hi) with a[i] > x (hi if none)
+__device__ __forceinline__ int64_t upper_bound_i64(const int64_t* __restrict__ a, int64_t lo,
+                                                   int64_t hi, int64_t x) {
+  while (lo < hi) {
+    int64_t mid = (lo + hi) >> 1;
+    if (a[mid] <= x) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+constexpr int CIPT = 8;                 // consecutive pair indices per thread
+constexpr int CCH = TNP_BLOCK * CIPT;   // pair indices per block
+
+// cell holding the first pair index of every connect block
+__global__ void k_block_cells(const int64_t* __restrict__ toff, int64_t ncell, int64_t nblk,
+                              int32_t* __restrict__ bcell) {
+  int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nblk) return;
+  bcell[b] = (int32_t)(upper_bound_i64(toff, 0, ncell, b * (int64_t)CCH) - 1);
+}
+
+__device__ __forceinline__ void cell_coords(int64_t cell, int NC, int cc[3]) {
+  cc[2] = (int)(cell % NC) - 2;
+  cc[1] = (int)((cell / NC) % NC) - 2;
+  cc[0] = (int)(cell / ((int64_t)NC * NC)) - 2;
+}
+
+// The flattened pair-index space of all cells (cell-major, then (i, j<i)
+// within the cell's member list) split evenly over threads: every thread
+// tests CIPT consecutive pairs, so a cell of 10^4 members costs the same per
+// thread as 10^4 cells of 2.  Member keys come from the entry-aligned copies
+// written by cell_scatter (contiguous per cell: L1/L2 hits).  Emitted pairs
+// are packed (lo << nb | hi) and appended block-contiguously through ONE
+// atomic per block; their order is restored by the radix sort that follows,
+// so the appended order never reaches the output.
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_connect(const int64_t* __restrict__ toff, const int32_t* __restrict__ cellcnt,
+          const int64_t* __restrict__ celloff, int64_t ncell, int NC, int64_t TT,
+          const int32_t* __restrict__ bcell, int64_t nblk, const int32_t* __restrict__ ent_v,
+          const uint64_t* __restrict__ ent_g, const uint64_t* __restrict__ ent_p,
+          const uint64_t* __restrict__ ent_z, int idx, int nb, uint64_t* __restrict__ keys,
+          int64_t cap, int64_t* __restrict__ ctr, int64_t* __restrict__ bstat) {
+  __shared__ int64_t lds[TNP_WAVES];
+  __shared__ int64_t s_base;
+  const int64_t b = blockIdx.x;
+  const int64_t p0 = b * (int64_t)CCH + (int64_t)threadIdx.x * CIPT;
+  const uint64_t below = (idx >= 64) ? ~0ull : ((1ull << idx) - 1ull);
+  uint64_t kk[CIPT];
+  int ne = 0;
+  int64_t n_compat = 0, n_reg = 0;
+  if (p0 < TT) {
+    const int64_t c_end = (b + 1 < nblk) ? (int64_t)bcell[b + 1] + 1 : ncell;
+    int64_t c = upper_bound_i64(toff, bcell[b], c_end, p0) - 1;
+    int64_t q = p0 - toff[c];
+    int64_t i = (int64_t)((1.0 + sqrt(1.0 + 8.0 * (double)q)) * 0.5);
+    while (i * (i - 1) / 2 > q) --i;
+    while ((i + 1) * i / 2 <= q) ++i;
+    int64_t j = q - i * (i - 1) / 2;
+    int n = cellcnt[c];
+    int64_t base = celloff[c];
+    int cc[3];
+    cell_coords(c, NC, cc);
+    int vu = ent_v[base + i];
+    uint64_t gu = ent_g[base + i], pu = ent_p[base + i], zu = ent_z[base + i];
+#pragma unroll
+    for (int k = 0; k < CIPT; ++k) {
+      const int64_t p = p0 + k;
+      if (p < TT) {
+        int64_t e = base + j;
+        PairTest t = pair_test(cc, below, gu, pu, zu, ent_g[e], ent_p[e], ent_z[e]);
+        if (t.compat) {
+          n_compat++;
+          n_reg += t.regions;
+          if (t.emit) {
+            uint32_t vv = (uint32_t)ent_v[e];
+            uint32_t lo = (uint32_t)vu < vv ? (uint32_t)vu : vv;
+            uint32_t hi = (uint32_t)vu < vv ? vv : (uint32_t)vu;
+            kk[ne++] = ((uint64_t)lo << nb) | hi;
+          }
+        }
+        if (++j == i) {
+          j = 0;
+          if (++i == n) {
+            if (p + 1 < TT && k + 1 < CIPT) {
+              c = upper_bound_i64(toff, c + 1, c_end, p + 1) - 1;
+              n = cellcnt[c];
+              base = celloff[c];
+              cell_coords(c, NC, cc);
+              i = 1;
+            }
+          }
+          if (k + 1 < CIPT && i < n) {
+            vu = ent_v[base + i];
+            gu = ent_g[base + i];
+            pu = ent_p[base + i];
+            zu = ent_z[base + i];
+          }
+        }
       }
-      a[j] = x;
     }
   }
-  int32_t* lo = pair_lo + pairoff[v];
-  for (int i = 0; i < n; ++i) lo[i] = (int32_t)v;
+  int64_t tot;
+  int64_t off = tnp::block_scan_excl((int64_t)ne, lds, tot);
+  if (threadIdx.x == 0) s_base = tot ? (int64_t)atomicAdd((unsigned long long*)&ctr[CTR_X], (unsigned long long)tot) : 0;
+  __syncthreads();
+  const int64_t w0 = s_base + off;
+  for (int k = 0; k < ne; ++k)
+    if (w0 + k < cap) keys[w0 + k] = kk[k];
+  int64_t tc = tnp::block_scan_excl(n_compat, lds, tot);
+  (void)tc;
+  if (threadIdx.x == 0) bstat[2 * b] = tot;
+  int64_t tr = tnp::block_scan_excl(n_reg, lds, tot);
+  (void)tr;
+  if (threadIdx.x == 0) bstat[2 * b + 1] = tot;
 }
 
+// per-block (compatible pairs, shared regions) -> ctr[CTR_COMPAT], ctr[CTR_P]
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_sum_bstat(const int64_t* __restrict__ bstat, int64_t nblk, int64_t* __restrict__ ctr) {
+  int64_t a = 0, r = 0;
+  for (int64_t i = threadIdx.x; i < nblk; i += blockDim.x) {
+    a += bstat[2 * i];
+    r += bstat[2 * i + 1];
+  }
+  a = tnp::wave_sum(a);
+  r = tnp::wave_sum(r);
+  if (tnp::lane() == 0) {
+    atomicAdd((unsigned long long*)&ctr[CTR_COMPAT], (unsigned long long)a);
+    atomicAdd((unsigned long long*)&ctr[CTR_P], (unsigned long long)r);
+  }
+}
 // ---------------------------------------------------------------------------
 // pruning: keep an edge iff its endpoints' future sign keys (planes >= idx)
 // differ (subpoly.py:252-265).  The candidate list is the concatenation
@@ -400,7 +466,7 @@ __global__ void k_pair_sort(const int64_t* __restrict__ pairoff, const int32_t* 
 struct EdgeSrc {
   const int32_t* edges;  int64_t E;
   const int32_t* sb;     int64_t S;  int64_t V;
-  const int32_t* c_lo;   const int32_t* c_hi; int64_t X;
+  const uint64_t* ckeys;  int nb;      int64_t X;   // packed (lo << nb | hi)
 };
 
 __device__ __forceinline__ void fetch_edge(const EdgeSrc& s, int64_t i, int& a, int& b) {
@@ -412,9 +478,9 @@ __device__ __forceinline__ void fetch_edge(const EdgeSrc& s, int64_t i, int& a, 
     a = s.sb[r];
     b = (int)(s.V + r);
   } else {
-    int64_t x = i - s.E - s.S;
-    a = s.c_lo[x];
-    b = s.c_hi[x];
+    uint64_t k = s.ckeys[i - s.E - s.S];
+    a = (int)(k >> s.nb);
+    b = (int)(k & ((1ull << s.nb) - 1ull));
   }
 }
 
@@ -603,52 +669,44 @@ int launch_cell_count(const int32_t* members, int64_t M, const uint64_t* grid, c
   TNP_CHECK(hipGetLastError());
   return 0;
 }
-int launch_cell_scatter(const int32_t* members, int64_t M, const uint64_t* grid, int NC,
-                        const int64_t* celloff, int32_t* cellcur, int32_t* ent_v, int32_t* ent_c,
-                        hipStream_t s) {
+int launch_cell_scatter(const int32_t* members, int64_t M, const uint64_t* grid,
+                        const uint64_t* pos, const uint64_t* zero, int NC, const int64_t* celloff,
+                        int32_t* cellcur, int32_t* ent_v, uint64_t* ent_g, uint64_t* ent_p,
+                        uint64_t* ent_z, hipStream_t s) {
   if (M <= 0) return 0;
   hipLaunchKernelGGL(k_cell_scatter, dim3(tnp_grid(M)), dim3(TNP_BLOCK), 0, s, members, M, grid,
-                     NC, celloff, cellcur, ent_v, ent_c);
+                     pos, zero, NC, celloff, cellcur, ent_v, ent_g, ent_p, ent_z);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
-int launch_pairs(bool emit, const int32_t* ent_v, const int32_t* ent_c, int64_t T,
-                 const int64_t* celloff, const int32_t* cellcnt, int NC, int idx,
-                 const uint64_t* pos, const uint64_t* zero, const uint64_t* grid,
-                 int32_t* paircnt, const int64_t* pairoff, int32_t* paircur, int32_t* pair_hi,
-                 int64_t* ctr, hipStream_t s) {
-  if (T <= 0) return 0;
-  if (emit)
-    hipLaunchKernelGGL(k_pairs<true>, dim3(tnp_grid(T)), dim3(TNP_BLOCK), 0, s, ent_v, ent_c, T,
-                       celloff, cellcnt, NC, idx, pos, zero, grid, paircnt, pairoff, paircur,
-                       pair_hi, ctr);
-  else
-    hipLaunchKernelGGL(k_pairs<false>, dim3(tnp_grid(T)), dim3(TNP_BLOCK), 0, s, ent_v, ent_c, T,
-                       celloff, cellcnt, NC, idx, pos, zero, grid, paircnt, pairoff, paircur,
-                       pair_hi, ctr);
+int launch_cell_tcnt(const int32_t* cellcnt, int64_t n, int32_t* tcnt, int64_t* ctr, hipStream_t s) {
+  hipLaunchKernelGGL(k_cell_tcnt, dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, cellcnt, n, tcnt, ctr);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
-int launch_cell_pairs(const int32_t* cellcnt, int64_t n, int64_t* ctr, hipStream_t s) {
-  unsigned g = (unsigned)std::min<int64_t>(tnp_grid(n), 2048);
-  hipLaunchKernelGGL(k_cell_pairs, dim3(g), dim3(TNP_BLOCK), 0, s, cellcnt, n, ctr);
-  TNP_CHECK(hipGetLastError());
-  return 0;
-}
-int launch_pair_sort(const int64_t* pairoff, const int32_t* paircnt, int64_t NV, int32_t* pair_hi,
-                     int32_t* pair_lo, hipStream_t s) {
-  if (NV <= 0) return 0;
-  hipLaunchKernelGGL(k_pair_sort, dim3(tnp_grid(NV)), dim3(TNP_BLOCK), 0, s, pairoff, paircnt, NV,
-                     pair_hi, pair_lo);
+int64_t connect_blocks(int64_t TT) { return (TT + CCH - 1) / CCH; }
+int launch_connect(const int64_t* toff, const int32_t* cellcnt, const int64_t* celloff,
+                   int64_t ncell, int NC, int64_t TT, int32_t* bcell, const int32_t* ent_v,
+                   const uint64_t* ent_g, const uint64_t* ent_p, const uint64_t* ent_z, int idx,
+                   int nb, uint64_t* keys, int64_t cap, int64_t* ctr, int64_t* bstat,
+                   hipStream_t s) {
+  if (TT <= 0) return 0;
+  int64_t nblk = connect_blocks(TT);
+  hipLaunchKernelGGL(k_block_cells, dim3(tnp_grid(nblk)), dim3(TNP_BLOCK), 0, s, toff, ncell, nblk,
+                     bcell);
+  hipLaunchKernelGGL(k_connect, dim3((unsigned)nblk), dim3(TNP_BLOCK), 0, s, toff, cellcnt, celloff,
+                     ncell, NC, TT, bcell, nblk, ent_v, ent_g, ent_p, ent_z, idx, nb, keys, cap,
+                     ctr, bstat);
+  hipLaunchKernelGGL(k_sum_bstat, dim3(1), dim3(TNP_BLOCK), 0, s, bstat, nblk, ctr);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
 int launch_prune(bool emit, const int32_t* edges, int64_t E, const int32_t* sb, int64_t S,
-                 int64_t V, const int32_t* c_lo, const int32_t* c_hi, int64_t X, int idx,
+                 int64_t V, const uint64_t* ckeys, int nb, int64_t X, int idx,
                  int prune, int last_plane, const uint64_t* pos, const uint64_t* zero,
                  int32_t* blk, const int64_t* blkoff, int32_t* out, int32_t* used, int64_t* ctr,
                  hipStream_t s) {
-  EdgeSrc src{edges, E, sb, S, V, c_lo, c_hi, X};
+  EdgeSrc src{edges, E, sb, S, V, ckeys, nb, X};
   int64_t N = E + S + X;
   if (N <= 0) return 0;
   uint64_t fmask = (idx >= 64) ? 0ull : (~0ull << idx);
