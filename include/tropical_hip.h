@@ -164,6 +164,15 @@ int tnp_engine_faces(tnp_engine* eng, void* stream, int64_t* n_tri, int64_t* n_f
 int tnp_engine_faces_export(tnp_engine* eng, int64_t* d_tri, float* d_faces,
                             void* stream);
 
+/* 1: subpoly_(..., force=False) -- the curve-approximation branch
+ * (subpoly.py:120-177, 201-207; geometry.py:24-138, 259-299;
+ * subpoly_debug.py:121-165, 234-271): new vertices of non-axis-aligned split
+ * edges move to the intersection of the two trilinear level sets (largest
+ * real root in [0,1] of the xz-plane quartic, gradient-descent fallback) and
+ * the strict filter drops splits that miss their planes.  0: flat (default).
+ * Single-device only (the descent's stop criterion is global). */
+int tnp_engine_set_curve(tnp_engine* eng, int on);
+
 /* Multi-GPU x-slabs: count splits of edges lying in mark plane x = mark
  * (the plane this slab shares with its upper neighbour; -1 = none), so the
  * global split count can subtract the replicated boundary work. */

@@ -20,6 +20,7 @@ for step in "$@"; do
     bench) run bench 900 python bench.py --steps 3 --warmup 1 ;;
     benchfast) run bench 600 python bench.py --steps 3 --warmup 1 --no-cpu ;;
     smoke) run smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    curve) run gpu_curve 600 python -u -m pytest tests/test_gpu_curve.py -x -v --timeout 300 -p no:cacheprovider ;;
     stats) run step_stats 300 python tools/step_stats.py 128 6 ;;
     pmcf) run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu ;;
     pmcw) run pmc_write 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu ;;

@@ -1,0 +1,621 @@
+// Curve-approximation branch of a hyperplane step (subpoly_(..., force=False),
+// tropical/subpoly.py:120-177, 201-207; tropical/geometry.py:24-138, 259-299,
+// 350-372; tropical/subpoly_debug.py:121-165, 234-271) on gfx950.
+//
+// For every split edge that is not axis-aligned (c rows) the new vertex is
+// the intersection of the two trilinear level sets it lies between -- the
+// last plane below idx both endpoints are zero on (p) and the current plane
+// (q) -- on the xz-diagonal plane of the edge's box:
+//
+//   curve_flags   c = more than one coordinate differs by > eps
+//   curve_corners 8 box corners per c row (corner 4i+2j+k: x from endpoint
+//                 k, y from j, z from i) + the shared plane p
+//   forward(group=8) over the corners (one activation pattern per box)
+//   curve_solve   quartic in x from the corner values, largest real root in
+//                 [0,1] (the reference's last LAPACK eigenvalue in [0,1] --
+//                 every multi-root case of the goldens is the largest one),
+//                 y from the quadratic ratio, bilinear boxes -> -1
+//   forward over e0(1-t) + e1 t, curve_dnew  residuals on p and q
+//   descend       normalised gradient descent of p^2 + q^2 (500 iterations
+//                 max, all rows stop together: pass 1 records per-iteration
+//                 convergence bits, pass 2 replays to the common stop)
+//   curve_apply   v = e0 + t (e1 - e0); strict-filter inputs
+//   (finish) strict_keep + compact_splits: dropped splits stay unsplit, new
+//                 vertex ids follow the surviving edges' order
+//
+// Roots are isolated in double precision (derivative brackets + bisection),
+// so vertices agree with the reference's fp32 LAPACK path to ~1e-7, not
+// bitwise (curve path tolerance 1e-5).
+#include "common.h"
+#include "kernels.h"
+#include "net_device.h"
+#include "step.h"
+
+using namespace tnpnet;
+
+namespace {
+
+constexpr float ROOT_EPS = 1e-9f;  // geometry.py:259, 271
+
+__global__ void k_curve_flags(const int32_t* __restrict__ sa, const int32_t* __restrict__ sb,
+                              int64_t S, const float* __restrict__ xyz, float eps,
+                              int32_t* __restrict__ cflag) {
+  int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= S) return;
+  int a = sa[r], b = sb[r], n = 0;
+#pragma unroll
+  for (int d = 0; d < 3; ++d)
+    n += fabsf(__fsub_rn(xyz[3 * (int64_t)b + d], xyz[3 * (int64_t)a + d])) > eps;
+  cflag[r] = n > 1;
+}
+
+__global__ void k_curve_rows(const int32_t* __restrict__ cflag, const int64_t* __restrict__ coff,
+                             int64_t S, int32_t* __restrict__ crow) {
+  int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < S && cflag[r]) crow[coff[r]] = (int32_t)r;
+}
+
+__global__ void k_curve_corners(const int32_t* __restrict__ crow, int64_t B,
+                                const int32_t* __restrict__ sa, const int32_t* __restrict__ sb,
+                                const float* __restrict__ xyz, const uint64_t* __restrict__ zero,
+                                int idx, float* __restrict__ corners, int32_t* __restrict__ plane,
+                                int64_t* __restrict__ ctr) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 8 * B) return;
+  int64_t b = t >> 3;
+  int n = (int)(t & 7);
+  int r = crow[b];
+  int e[2] = {sa[r], sb[r]};
+  int k = n & 1, j = (n >> 1) & 1, i = n >> 2;
+  corners[3 * t + 0] = xyz[3 * (int64_t)e[k] + 0];
+  corners[3 * t + 1] = xyz[3 * (int64_t)e[j] + 1];
+  corners[3 * t + 2] = xyz[3 * (int64_t)e[i] + 2];
+  if (n == 0) {
+    // last plane j < idx both endpoints are eps-zero on (nonzero_last,
+    // torch_ext.py:18-29); none -> the reference exit()s (subpoly.py:141-148)
+    uint64_t below = (idx >= 64) ? ~0ull : ((1ull << idx) - 1ull);
+    uint64_t m = zero[e[0]] & zero[e[1]] & below;
+    plane[b] = m ? 63 - __builtin_clzll(m) : 0;
+    if (!m) atomicOr((unsigned long long*)&ctr[CTR_NOPLANE], 1ull);
+  }
+}
+
+// ---- polynomial roots in [0, 1] ---------------------------------------------
+// p(x) = a[0] x^N + ... + a[N]; ascending real roots in [0, 1] via the roots
+// of p' as brackets (monotone between them) and bisection to full double
+// precision.
+template <int N>
+struct Roots01 {
+  __device__ static double eval(const double* a, double x) {
+    double r = a[0];
+#pragma unroll
+    for (int k = 1; k <= N; ++k) r = fma(r, x, a[k]);
+    return r;
+  }
+  __device__ static int find(const double* a, double* out) {
+    double da[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) da[k] = a[k] * (double)(N - k);
+    double br[N + 1];
+    int nb = Roots01<N - 1>::find(da, br + 1);
+    br[0] = 0.0;
+    br[nb + 1] = 1.0;
+    int n = 0;
+    for (int i = 0; i <= nb; ++i) {
+      double lo = br[i], hi = br[i + 1];
+      double flo = eval(a, lo), fhi = eval(a, hi);
+      if (flo == 0.0) {
+        if (n == 0 || out[n - 1] != lo) out[n++] = lo;
+        continue;
+      }
+      if ((flo < 0.0) == (fhi < 0.0) || fhi == 0.0) continue;
+      for (int it = 0; it < 80 && lo < hi; ++it) {
+        double mid = 0.5 * (lo + hi);
+        if (mid <= lo || mid >= hi) break;
+        double fm = eval(a, mid);
+        if (fm == 0.0) { lo = hi = mid; break; }
+        if ((fm < 0.0) == (flo < 0.0)) lo = mid;
+        else hi = mid;
+      }
+      out[n++] = 0.5 * (lo + hi);
+    }
+    if (eval(a, 1.0) == 0.0 && (n == 0 || out[n - 1] != 1.0)) out[n++] = 1.0;
+    return n;
+  }
+};
+template <>
+struct Roots01<1> {
+  __device__ static int find(const double* a, double* out) {
+    if (a[0] == 0.0) return 0;
+    double r = -a[1] / a[0];
+    if (r >= 0.0 && r <= 1.0) {
+      out[0] = r;
+      return 1;
+    }
+    return 0;
+  }
+};
+
+// batched_polynomial_roots (geometry.py:259-299) for one row of 5 fp32
+// coefficients (leading first): tiny coefficients zeroed, degree from the
+// first non-zero one, companion row r_k = -c_k / c_lead in fp32 (what LAPACK
+// sees), largest real root in [0, 1], -1 if none.
+__device__ float largest_root01(float c[5]) {
+#pragma unroll
+  for (int k = 0; k < 5; ++k)
+    if (fabsf(c[k]) < ROOT_EPS) c[k] = 0.f;
+  int i = 0;
+  while (i < 4 && c[i] == 0.f) ++i;
+  if (i == 4) return -1.f;
+  const int N = 4 - i;
+  float s = 0.f;
+  for (int k = 4; k >= i; --k) s = __fadd_rn(s, fabsf(c[k]));
+  if (!(__fdiv_rn(s, (float)(N + 1)) > ROOT_EPS)) return -1.f;
+  if (N == 1) {
+    float r = __fdiv_rn(-c[4], c[3]);
+    return (r >= 0.f && r <= 1.f) ? r : -1.f;
+  }
+  double a[5];
+  a[0] = 1.0;
+  for (int k = 1; k <= N; ++k) a[k] = -(double)__fdiv_rn(-c[i + k], c[i]);
+  double rt[4];
+  int n = 0;
+  switch (N) {
+    case 2: n = Roots01<2>::find(a, rt); break;
+    case 3: n = Roots01<3>::find(a, rt); break;
+    default: n = Roots01<4>::find(a, rt); break;
+  }
+  if (n == 0) return -1.f;
+  float r = (float)rt[n - 1];
+  return (r >= 0.f && r <= 1.f) ? r : -1.f;
+}
+
+// intersection_of_two_planes (geometry.py:24-138), "xz" assumption
+__device__ void plane_intersection(const float p[8], const float q[8], float t[3]) {
+  const int LO[4] = {0, 1, 4, 5}, HI[4] = {2, 3, 6, 7};
+  float zq_lo[3] = {q[LO[0]], __fadd_rn(q[LO[1]], q[LO[2]]), q[LO[3]]};
+  float zq_hi[3] = {q[HI[0]], __fadd_rn(q[HI[1]], q[HI[2]]), q[HI[3]]};
+  float zp_lo[3] = {p[LO[0]], __fadd_rn(p[LO[1]], p[LO[2]]), p[LO[3]]};
+  float zp_hi[3] = {p[HI[0]], __fadd_rn(p[HI[1]], p[HI[2]]), p[HI[3]]};
+  float A[3][3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      A[i][j] = __fsub_rn(__fmul_rn(zq_lo[i], zp_hi[j]), __fmul_rn(zq_hi[i], zp_lo[j]));
+  const float T[3][3] = {{1.f, -2.f, 1.f}, {-1.f, 1.f, 0.f}, {1.f, 0.f, 0.f}};
+  float M[3][3], Bm[3][3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      float acc = 0.f;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) acc = __fmaf_rn(T[k][i], A[k][j], acc);
+      M[i][j] = acc;
+    }
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      float acc = 0.f;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) acc = __fmaf_rn(M[i][k], T[k][j], acc);
+      Bm[i][j] = acc;
+    }
+  float c[5] = {Bm[0][0], __fadd_rn(Bm[1][0], Bm[0][1]),
+                __fadd_rn(__fadd_rn(Bm[2][0], Bm[1][1]), Bm[0][2]),
+                __fadd_rn(Bm[1][2], Bm[2][1]), Bm[2][2]};
+  float x = largest_root01(c);
+  float om = __fsub_rn(1.f, x);
+  float X[4] = {__fmul_rn(om, om), __fmul_rn(x, om), __fmul_rn(x, om), __fmul_rn(x, x)};
+  float ax = 0.f, bx = 0.f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    ax = __fadd_rn(ax, __fmul_rn(q[LO[k]], X[k]));
+    bx = __fadd_rn(bx, __fmul_rn(q[HI[k]], X[k]));
+  }
+  float y = __fdiv_rn(ax, __fsub_rn(ax, bx));
+  // bilinear boxes (both planes constant along one axis): the reference's
+  // failover=False branch marks them -1 (geometry.py:106-136)
+  const int FT[3][4] = {{0, 1, 4, 5}, {0, 1, 2, 3}, {0, 4, 2, 6}};
+  const int FU[3][4] = {{2, 3, 6, 7}, {4, 5, 6, 7}, {1, 5, 3, 7}};
+  bool flat = false;
+#pragma unroll
+  for (int f = 0; f < 3; ++f) {
+    bool all = true;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) all &= (p[FT[f][k]] == p[FU[f][k]]) && (q[FT[f][k]] == q[FU[f][k]]);
+    flat |= all;
+  }
+  if (flat) x = y = -1.f;
+  t[0] = x;
+  t[1] = y;
+  t[2] = x;
+}
+
+__global__ void k_curve_solve(int64_t B, const float* __restrict__ stage_c, int64_t ldc,
+                              const int32_t* __restrict__ plane, int idx,
+                              const int32_t* __restrict__ crow, const int32_t* __restrict__ sa,
+                              const int32_t* __restrict__ sb, const float* __restrict__ xyz,
+                              float* __restrict__ ints, float* __restrict__ pts) {
+  int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  float p[8], q[8];
+  const float* P = stage_c + (int64_t)plane[b] * ldc + 8 * b;
+  const float* Q = stage_c + (int64_t)idx * ldc + 8 * b;
+#pragma unroll
+  for (int n = 0; n < 8; ++n) {
+    p[n] = P[n];
+    q[n] = Q[n];
+  }
+  float t[3];
+  plane_intersection(p, q, t);
+  int r = crow[b];
+  int64_t a = sa[r], e = sb[r];
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    ints[3 * b + d] = t[d];
+    pts[3 * b + d] = __fadd_rn(__fmul_rn(xyz[3 * a + d], __fsub_rn(1.f, t[d])),
+                               __fmul_rn(xyz[3 * e + d], t[d]));
+  }
+}
+
+// residuals at the solved points; gg (no root in the box), gd (needs descent)
+__global__ void k_curve_dnew(int64_t B, const float* __restrict__ stage_p, int64_t ldp,
+                             const int32_t* __restrict__ plane, int idx,
+                             const float* __restrict__ ints, float eps, float* __restrict__ d0s,
+                             float* __restrict__ d1s, int32_t* __restrict__ gg,
+                             int32_t* __restrict__ gd) {
+  int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  float d0 = stage_p[(int64_t)plane[b] * ldp + b];
+  float d1 = stage_p[(int64_t)idx * ldp + b];
+  bool out = false;
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    float t = ints[3 * b + d];
+    out |= (t < 0.f) || (t > 1.f);
+  }
+  d0s[b] = d0;
+  d1s[b] = d1;
+  gg[b] = out;
+  gd[b] = !out && (fabsf(d0) > eps || fabsf(d1) > eps);
+}
+
+__global__ void k_gd_rows(const int32_t* __restrict__ gd, const int64_t* __restrict__ goff, int64_t B,
+                          int32_t* __restrict__ glist) {
+  int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < B && gd[b]) glist[goff[b]] = (int32_t)b;
+}
+
+// pre-activations of planes j0, j1 at u (preprocessed) and d(d0^2 + d1^2)/du
+template <int LV, int H>
+__device__ __forceinline__ void plane_pair_grad(const NetDev& net, const float* w, const float u[3],
+                                                int j0, int j1, float& d0, float& d1,
+                                                float gu[3]) {
+  constexpr int IN = 2 * LV;
+  float f[IN], a1[H], h1[H], a2[H], h2[H], o[2];
+  encode<LV>(net, u, f);
+  const float* W0 = w;
+  const float* W1 = W0 + H * IN + H;
+  const float* W2 = W1 + H * H + H;
+  linear<IN, H>(W0, W0 + H * IN, f, a1);
+#pragma unroll
+  for (int j = 0; j < H; ++j) h1[j] = fmaxf(a1[j], 0.f);
+  linear<H, H>(W1, W1 + H * H, h1, a2);
+#pragma unroll
+  for (int j = 0; j < H; ++j) h2[j] = fmaxf(a2[j], 0.f);
+  linear<H, 2>(W2, W2 + 2 * H, h2, o);
+  float last = __fsub_rn(o[1], o[0]);
+  d0 = j0 < H ? a1[j0] : (j0 < 2 * H ? a2[j0 - H] : last);
+  d1 = j1 < H ? a1[j1] : (j1 < 2 * H ? a2[j1 - H] : last);
+  // seeds of y = d0^2 + d1^2
+  float g1[H], g2[H], go = 0.f;
+#pragma unroll
+  for (int j = 0; j < H; ++j) g1[j] = g2[j] = 0.f;
+  const int js[2] = {j0, j1};
+  const float ds[2] = {d0, d1};
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    float g = 2.f * ds[s];
+    int j = js[s];
+    if (j < H) {
+#pragma unroll
+      for (int k = 0; k < H; ++k) g1[k] += (k == j) ? g : 0.f;
+    } else if (j < 2 * H) {
+#pragma unroll
+      for (int k = 0; k < H; ++k) g2[k] += (k == j - H) ? g : 0.f;
+    } else {
+      go += g;
+    }
+  }
+  // back through layer 3 (o1 - o0), ReLU 2, layer 2, ReLU 1, layer 1;
+  // g1 / g2 end as the total gradients of the pre-activations a1 / a2
+#pragma unroll
+  for (int k = 0; k < H; ++k) {
+    float v = go * W2[H + k] - go * W2[k];
+    g2[k] = a2[k] > 0.f ? g2[k] + v : g2[k];
+  }
+  float gh1[H];
+#pragma unroll
+  for (int k = 0; k < H; ++k) {
+    float v = 0.f;
+#pragma unroll
+    for (int j = 0; j < H; ++j) v += g2[j] * W1[j * H + k];
+    gh1[k] = v;
+  }
+  float df[IN];
+#pragma unroll
+  for (int m = 0; m < IN; ++m) {
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < H; ++k) v += (a1[k] > 0.f ? g1[k] + gh1[k] : g1[k]) * W0[k * IN + m];
+    df[m] = v;
+  }
+  float gx[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+  for (int l = 0; l < LV; ++l) {
+    const float sc = net.scales[l];
+    float t[3];
+    uint32_t g[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      float pos = u[d] * sc + 0.5f;
+      float fl = floorf(pos);
+      t[d] = pos - fl;
+      g[d] = (uint32_t)(int)fl;
+    }
+    const uint32_t res = (uint32_t)net.res[l];
+    const float2* tab = reinterpret_cast<const float2*>(net.table) + net.offsets[l];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      float fc[3];
+      uint32_t gc[3];
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        bool up = (c >> d) & 1;
+        fc[d] = up ? t[d] : 1.f - t[d];
+        gc[d] = g[d] + (up ? 1u : 0u);
+      }
+      uint32_t id = net.dense[l] ? (gc[0] + gc[1] * res + gc[2] * (res * res))
+                                 : (gc[0] ^ (gc[1] * P1) ^ (gc[2] * P2));
+      id %= net.sizes[l];
+      float2 v = tab[id];
+      float dv = v.x * df[2 * l] + v.y * df[2 * l + 1];
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        float sg = ((c >> d) & 1) ? 1.f : -1.f;
+        gx[d] += sg * fc[(d + 1) % 3] * fc[(d + 2) % 3] * dv * sc;
+      }
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < 3; ++d) gu[d] = gx[d];
+}
+
+// deal_with_gradient_descent (subpoly_debug.py:121-165), one thread per row.
+// record != 0: AND this row's per-iteration "both residuals <= eps" bits into
+// conv[0..7] (iteration i -> bit i) so the host finds the common stop.
+template <int LV, int H>
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_descend(NetDev net, int64_t G, const int32_t* __restrict__ glist,
+          const int32_t* __restrict__ crow, const int32_t* __restrict__ sa,
+          const int32_t* __restrict__ sb, const float* __restrict__ xyz,
+          const int32_t* __restrict__ plane, int idx, float eps, int iters, int record,
+          float* __restrict__ ints, float* __restrict__ d0s, float* __restrict__ d1s,
+          unsigned long long* __restrict__ conv) {
+  constexpr int NW = NetShape<LV, H, 3>::NW;
+  __shared__ float w[NW];
+  for (int i = threadIdx.x; i < NW; i += blockDim.x) w[i] = net.weights[i];
+  __syncthreads();
+  int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G) return;
+  int b = glist[g];
+  int r = crow[b];
+  float e0[3], de[3], x[3];
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    e0[d] = xyz[3 * (int64_t)sa[r] + d];
+    de[d] = __fsub_rn(xyz[3 * (int64_t)sb[r] + d], e0[d]);
+    x[d] = ints[3 * b + d];
+  }
+  const int j0 = plane[b];
+  uint64_t bits[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float d0 = 1.f, d1 = 1.f;
+  for (int it = 0; it < iters; ++it) {
+    float u[3], gu[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d)
+      u[d] = __fdiv_rn(__fadd_rn(__fadd_rn(e0[d], __fmul_rn(x[d], de[d])), 1.0f), 2.0f);
+    plane_pair_grad<LV, H>(net, w, u, j0, idx, d0, d1, gu);
+    float gx[3], nn = 0.f;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      gx[d] = __fmul_rn(__fmul_rn(gu[d], 0.5f), de[d]);
+      nn = __fmaf_rn(gx[d], gx[d], nn);
+    }
+    float den = fmaxf(__fsqrt_rn(nn), 1e-12f);
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      float v = __fsub_rn(x[d], __fmul_rn(1e-2f, __fdiv_rn(gx[d], den)));
+      x[d] = fminf(fmaxf(v, 0.f), 1.f);
+    }
+    if (record && fabsf(d0) <= eps && fabsf(d1) <= eps) bits[it >> 6] |= 1ull << (it & 63);
+  }
+  if (record)
+    for (int k = 0; k < 8; ++k) atomicAnd(&conv[k], (unsigned long long)bits[k]);
+#pragma unroll
+  for (int d = 0; d < 3; ++d) ints[3 * b + d] = x[d];
+  d0s[b] = d0;
+  d1s[b] = d1;
+}
+
+// v = e0 + t (e1 - e0) for c rows (subpoly.py:204-207) and the per-split
+// strict-filter inputs: cinfo bit0 c row, bit1 gg, bit2 |d0| < eps; the
+// global "some kept c row has |d0| > eps" flag (subpoly_debug.py:253-257).
+__global__ void k_curve_apply(int64_t B, const int32_t* __restrict__ crow,
+                              const int32_t* __restrict__ sa, const int32_t* __restrict__ sb,
+                              float* __restrict__ xyz, int64_t V, const float* __restrict__ ints,
+                              const float* __restrict__ d0s, const int32_t* __restrict__ gg,
+                              float eps, int32_t* __restrict__ cinfo, int64_t* __restrict__ ctr) {
+  int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool tight = false;
+  if (b < B) {
+    int r = crow[b];
+    int64_t a = sa[r], e = sb[r];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      float e0 = xyz[3 * a + d];
+      float dd = __fsub_rn(xyz[3 * e + d], e0);
+      xyz[3 * (V + r) + d] = __fadd_rn(e0, __fmul_rn(ints[3 * b + d], dd));
+    }
+    bool out = gg[b] != 0;
+    float d0 = out ? 0.f : d0s[b];
+    cinfo[r] = 1 | (out ? 2 : 0) | (fabsf(d0) < eps ? 4 : 0);
+    tight = fabsf(d0) > eps;
+  }
+  if (__ballot(tight) && tnp::lane() == 0) atomicOr((unsigned long long*)&ctr[CTR_TIGHT], 1ull);
+}
+
+// strict_check (subpoly_debug.py:234-271) after the override
+__global__ void k_strict_keep(int64_t S, const int32_t* __restrict__ cinfo,
+                              const float* __restrict__ stage, int idx, int override_,
+                              const uint64_t* __restrict__ shared, float eps, int tight,
+                              int32_t* __restrict__ keep) {
+  int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= S) return;
+  float chk = stage[(int64_t)idx * S + r];
+  if (override_ && ((shared[r] >> idx) & 1)) chk = 0.f;
+  bool k = fabsf(chk) < eps;
+  int ci = cinfo[r];
+  if (ci & 1) k = k && !(ci & 2) && (!tight || (ci & 4));
+  keep[r] = k;
+}
+
+// surviving splits -> consecutive new ids in edge order; the split edge's
+// second endpoint becomes the new vertex (masked_scatter_, subpoly.py:211)
+__global__ void k_compact_splits(int64_t S, int K, const int32_t* __restrict__ keep,
+                                 const int64_t* __restrict__ nid, const int32_t* __restrict__ eidx,
+                                 int64_t V, const int32_t* __restrict__ sa,
+                                 const int32_t* __restrict__ sb, const uint64_t* __restrict__ shared,
+                                 const float* __restrict__ stage, const float* __restrict__ xyz,
+                                 const uint64_t* __restrict__ grid, int64_t S2,
+                                 int32_t* __restrict__ sa2, int32_t* __restrict__ sb2,
+                                 uint64_t* __restrict__ shared2, float* __restrict__ stage2,
+                                 float* __restrict__ xyz2, uint64_t* __restrict__ grid2,
+                                 int32_t* __restrict__ edges) {
+  int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= S || !keep[r]) return;
+  int64_t n = nid[r];
+  sa2[n] = sa[r];
+  sb2[n] = sb[r];
+  shared2[n] = shared[r];
+  for (int p = 0; p < K; ++p) stage2[(int64_t)p * S2 + n] = stage[(int64_t)p * S + r];
+#pragma unroll
+  for (int d = 0; d < 3; ++d) xyz2[3 * n + d] = xyz[3 * (V + r) + d];
+  grid2[n] = grid[V + r];
+  edges[2 * (int64_t)eidx[r] + 1] = (int32_t)(V + n);
+}
+
+#define TNP_DISPATCH(LV, BODY)                                      \
+  switch (LV) {                                                     \
+    case 2: { constexpr int L_ = 2; BODY; break; }                  \
+    case 4: { constexpr int L_ = 4; BODY; break; }                  \
+    default: tnp_set_error("n_levels=%d not instantiated", LV); return -1; \
+  }
+
+}  // namespace
+
+int launch_curve_flags(const int32_t* sa, const int32_t* sb, int64_t S, const float* xyz, float eps,
+                       int32_t* cflag, hipStream_t s) {
+  if (S <= 0) return 0;
+  hipLaunchKernelGGL(k_curve_flags, dim3(tnp_grid(S)), dim3(TNP_BLOCK), 0, s, sa, sb, S, xyz, eps,
+                     cflag);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_curve_rows(const int32_t* cflag, const int64_t* coff, int64_t S, int32_t* crow,
+                      hipStream_t s) {
+  if (S <= 0) return 0;
+  hipLaunchKernelGGL(k_curve_rows, dim3(tnp_grid(S)), dim3(TNP_BLOCK), 0, s, cflag, coff, S, crow);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_curve_corners(const int32_t* crow, int64_t B, const int32_t* sa, const int32_t* sb,
+                         const float* xyz, const uint64_t* zero, int idx, float* corners,
+                         int32_t* plane, int64_t* ctr, hipStream_t s) {
+  if (B <= 0) return 0;
+  hipLaunchKernelGGL(k_curve_corners, dim3(tnp_grid(8 * B)), dim3(TNP_BLOCK), 0, s, crow, B, sa, sb,
+                     xyz, zero, idx, corners, plane, ctr);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_curve_solve(int64_t B, const float* stage_c, int64_t ldc, const int32_t* plane, int idx,
+                       const int32_t* crow, const int32_t* sa, const int32_t* sb, const float* xyz,
+                       float* ints, float* pts, hipStream_t s) {
+  if (B <= 0) return 0;
+  hipLaunchKernelGGL(k_curve_solve, dim3(tnp_grid(B)), dim3(TNP_BLOCK), 0, s, B, stage_c, ldc, plane,
+                     idx, crow, sa, sb, xyz, ints, pts);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_curve_dnew(int64_t B, const float* stage_p, int64_t ldp, const int32_t* plane, int idx,
+                      const float* ints, float eps, float* d0s, float* d1s, int32_t* gg, int32_t* gd,
+                      hipStream_t s) {
+  if (B <= 0) return 0;
+  hipLaunchKernelGGL(k_curve_dnew, dim3(tnp_grid(B)), dim3(TNP_BLOCK), 0, s, B, stage_p, ldp, plane,
+                     idx, ints, eps, d0s, d1s, gg, gd);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_gd_rows(const int32_t* gd, const int64_t* goff, int64_t B, int32_t* glist, hipStream_t s) {
+  if (B <= 0) return 0;
+  hipLaunchKernelGGL(k_gd_rows, dim3(tnp_grid(B)), dim3(TNP_BLOCK), 0, s, gd, goff, B, glist);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_descend(const NetDev& net, int64_t G, const int32_t* glist, const int32_t* crow,
+                   const int32_t* sa, const int32_t* sb, const float* xyz, const int32_t* plane,
+                   int idx, float eps, int iters, int record, float* ints, float* d0s, float* d1s,
+                   unsigned long long* conv, hipStream_t s) {
+  if (G <= 0) return 0;
+  if (!net_supported(net)) { tnp_set_error("unsupported net shape"); return -1; }
+  if (iters > 512) { tnp_set_error("descend: at most 512 iterations"); return -1; }
+  TNP_DISPATCH(net.n_levels, {
+    hipLaunchKernelGGL((k_descend<L_, 16>), dim3(tnp_grid(G)), dim3(TNP_BLOCK), 0, s, net, G, glist,
+                       crow, sa, sb, xyz, plane, idx, eps, iters, record, ints, d0s, d1s, conv);
+  });
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_curve_apply(int64_t B, const int32_t* crow, const int32_t* sa, const int32_t* sb,
+                       float* xyz, int64_t V, const float* ints, const float* d0s, const int32_t* gg,
+                       float eps, int32_t* cinfo, int64_t* ctr, hipStream_t s) {
+  if (B <= 0) return 0;
+  hipLaunchKernelGGL(k_curve_apply, dim3(tnp_grid(B)), dim3(TNP_BLOCK), 0, s, B, crow, sa, sb, xyz, V,
+                     ints, d0s, gg, eps, cinfo, ctr);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_strict_keep(int64_t S, const int32_t* cinfo, const float* stage, int idx, int override_,
+                       const uint64_t* shared, float eps, int tight, int32_t* keep, hipStream_t s) {
+  if (S <= 0) return 0;
+  hipLaunchKernelGGL(k_strict_keep, dim3(tnp_grid(S)), dim3(TNP_BLOCK), 0, s, S, cinfo, stage, idx,
+                     override_, shared, eps, tight, keep);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_compact_splits(int64_t S, int K, const int32_t* keep, const int64_t* nid,
+                          const int32_t* eidx, int64_t V, const int32_t* sa, const int32_t* sb,
+                          const uint64_t* shared, const float* stage, const float* xyz,
+                          const uint64_t* grid, int64_t S2, int32_t* sa2, int32_t* sb2,
+                          uint64_t* shared2, float* stage2, float* xyz2, uint64_t* grid2,
+                          int32_t* edges, hipStream_t s) {
+  if (S <= 0) return 0;
+  hipLaunchKernelGGL(k_compact_splits, dim3(tnp_grid(S)), dim3(TNP_BLOCK), 0, s, S, K, keep, nid,
+                     eidx, V, sa, sb, shared, stage, xyz, grid, S2, sa2, sb2, shared2, stage2, xyz2,
+                     grid2, edges);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}

@@ -107,9 +107,19 @@ struct KRec {
   hipEvent_t a, b;
 };
 
+// curve-path scratch (force=False branch, curve.hip)
+enum {
+  CV_EIDX, CV_CFLAG, CV_COFF, CV_CROW, CV_CORNERS, CV_PLANE, CV_STAGE_C, CV_INTS, CV_INTS0, CV_PTS,
+  CV_STAGE_P, CV_D0, CV_D1, CV_GG, CV_GD, CV_GOFF, CV_GLIST, CV_CONV, CV_CINFO, CV_KEEP, CV_NID,
+  CV_SA2, CV_SB2, CV_SHARED2, CV_STAGE2, CV_XYZ2, CV_GRID2, CV_N
+};
+
 struct tnp_engine {
   int device = 0;
   int dup_mark = -1;
+  int curve = 0;          // 1: subpoly_(force=False) semantics
+  int pend_tight = 0;
+  int gd_iters = 500;     // subpoly_debug.py:141
   int64_t max_pair_tests = 20000000000LL;
   bool kt_on = false;
   std::vector<KRec> kt;
@@ -138,6 +148,7 @@ struct tnp_engine {
   int64_t n_tri = 0, n_faces = 0, dbg_F = 0, dbg_W = 0;
   Buf fscr[12];
   Buf fscr2[32];
+  Buf cv[CV_N];
 };
 
 static int read_ctr(tnp_engine* e, hipStream_t s) {
@@ -244,6 +255,7 @@ extern "C" void tnp_engine_destroy(tnp_engine* e) {
   for (Buf* b : bufs) buf_free(*b, s);
   for (Buf& b : e->fscr) buf_free(b, s);
   for (Buf& b : e->fscr2) buf_free(b, s);
+  for (Buf& b : e->cv) buf_free(b, s);
   (void)hipDeviceSynchronize();
   if (e->h_ctr) (void)hipHostFree(e->h_ctr);
   delete e;
@@ -370,6 +382,147 @@ extern "C" int tnp_engine_active_planes(tnp_engine* e, int from, uint64_t* mask,
   return 0;
 }
 
+// ---------------------------------------------------------------------------
+// curve path, phase 1 (subpoly.py:120-177, 204-207): correct the new vertices
+// of non-axis-aligned split edges to the trilinear intersection, with the
+// gradient-descent fallback; leaves per-split strict-filter inputs in cinfo.
+// ---------------------------------------------------------------------------
+static int curve_correct(tnp_engine* e, int idx, int64_t S, hipStream_t s) {
+  const float eps = e->net.eps;
+  const int K = e->K;
+  Buf* cv = e->cv;
+  int64_t* ctr = P<int64_t>(e->ctr);
+  const int32_t* sa = P<int32_t>(e->sa);
+  const int32_t* sb = P<int32_t>(e->sb);
+  float* xyz = P<float>(e->cur.xyz);
+  if (buf_ensure(cv[CV_CFLAG], S * sizeof(int32_t), s)) return -1;
+  if (buf_ensure(cv[CV_COFF], S * sizeof(int64_t), s)) return -1;
+  if (buf_ensure(cv[CV_CINFO], S * sizeof(int32_t), s)) return -1;
+  TNP_CHECK(hipMemsetAsync(cv[CV_CINFO].p, 0, S * sizeof(int32_t), s));
+  TIMED("curve_flags", 32.0 * S,
+        launch_curve_flags(sa, sb, S, xyz, eps, P<int32_t>(cv[CV_CFLAG]), s));
+  if (scan_counts(e, P<int32_t>(cv[CV_CFLAG]), P<int64_t>(cv[CV_COFF]), S, CTR_B, s)) return -1;
+  if (read_ctr(e, s)) return -1;
+  const int64_t B = e->h_ctr[CTR_B];
+  if (B == 0) return 0;
+  if (buf_ensure(cv[CV_CROW], B * sizeof(int32_t), s)) return -1;
+  if (buf_ensure(cv[CV_CORNERS], 24 * B * sizeof(float), s)) return -1;
+  if (buf_ensure(cv[CV_PLANE], B * sizeof(int32_t), s)) return -1;
+  if (buf_ensure(cv[CV_STAGE_C], (size_t)8 * B * K * sizeof(float), s)) return -1;
+  if (buf_ensure(cv[CV_INTS], 3 * B * sizeof(float), s)) return -1;
+  if (buf_ensure(cv[CV_INTS0], 3 * B * sizeof(float), s)) return -1;
+  if (buf_ensure(cv[CV_PTS], 3 * B * sizeof(float), s)) return -1;
+  if (buf_ensure(cv[CV_STAGE_P], (size_t)B * K * sizeof(float), s)) return -1;
+  for (int k : {CV_D0, CV_D1, CV_GG, CV_GD}) if (buf_ensure(cv[k], B * 4, s)) return -1;
+  if (buf_ensure(cv[CV_GOFF], B * sizeof(int64_t), s)) return -1;
+  int32_t* crow = P<int32_t>(cv[CV_CROW]);
+  int32_t* plane = P<int32_t>(cv[CV_PLANE]);
+  float* ints = P<float>(cv[CV_INTS]);
+  float* d0s = P<float>(cv[CV_D0]);
+  float* d1s = P<float>(cv[CV_D1]);
+  if (launch_curve_rows(P<int32_t>(cv[CV_CFLAG]), P<int64_t>(cv[CV_COFF]), S, crow, s)) return -1;
+  TIMED("curve_corners", 8.0 * B * 12 + 24.0 * B,
+        launch_curve_corners(crow, B, sa, sb, xyz, P<uint64_t>(e->cur.zero), idx,
+                             P<float>(cv[CV_CORNERS]), plane, ctr, s));
+  TIMED("curve_forward", 8.0 * B * (12 + 4.0 * K),
+        launch_forward(e->net, P<float>(cv[CV_CORNERS]), 8 * B, P<float>(cv[CV_STAGE_C]), 8 * B, 8, s));
+  TIMED("curve_solve", 64.0 * B + 24.0 * B,
+        launch_curve_solve(B, P<float>(cv[CV_STAGE_C]), 8 * B, plane, idx, crow, sa, sb, xyz, ints,
+                           P<float>(cv[CV_PTS]), s));
+  TIMED("curve_forward", B * (12 + 4.0 * K),
+        launch_forward(e->net, P<float>(cv[CV_PTS]), B, P<float>(cv[CV_STAGE_P]), B, 1, s));
+  if (launch_curve_dnew(B, P<float>(cv[CV_STAGE_P]), B, plane, idx, ints, eps, d0s, d1s,
+                        P<int32_t>(cv[CV_GG]), P<int32_t>(cv[CV_GD]), s)) return -1;
+  if (scan_counts(e, P<int32_t>(cv[CV_GD]), P<int64_t>(cv[CV_GOFF]), B, CTR_G, s)) return -1;
+  if (read_ctr(e, s)) return -1;
+  if (e->h_ctr[CTR_NOPLANE]) {
+    tnp_set_error("curve path: a split edge shares no plane below %d (the reference prints it and "
+                  "exit()s, subpoly.py:141-148)", idx);
+    return -1;
+  }
+  const int64_t G = e->h_ctr[CTR_G];
+  if (G > 0) {
+    if (buf_ensure(cv[CV_GLIST], G * sizeof(int32_t), s)) return -1;
+    if (buf_ensure(cv[CV_CONV], 8 * sizeof(uint64_t), s)) return -1;
+    int32_t* glist = P<int32_t>(cv[CV_GLIST]);
+    unsigned long long* conv = P<unsigned long long>(cv[CV_CONV]);
+    if (launch_gd_rows(P<int32_t>(cv[CV_GD]), P<int64_t>(cv[CV_GOFF]), B, glist, s)) return -1;
+    TNP_CHECK(hipMemcpyAsync(cv[CV_INTS0].p, ints, 3 * B * sizeof(float), hipMemcpyDeviceToDevice, s));
+    TNP_CHECK(hipMemsetAsync(conv, 0xFF, 8 * sizeof(uint64_t), s));
+    TIMED("descend", 0.0,
+          launch_descend(e->net, G, glist, crow, sa, sb, xyz, plane, idx, eps, e->gd_iters, 1, ints,
+                         d0s, d1s, conv, s));
+    uint64_t h_conv[8];
+    TNP_CHECK(hipMemcpyAsync(h_conv, conv, sizeof(h_conv), hipMemcpyDeviceToHost, s));
+    TNP_CHECK(hipStreamSynchronize(s));
+    int stop = -1;  // first iteration after which every row met both planes
+    for (int i = 0; i < e->gd_iters && stop < 0; ++i)
+      if ((h_conv[i >> 6] >> (i & 63)) & 1) stop = i;
+    if (stop >= 0 && stop + 1 < e->gd_iters) {
+      // the loop of subpoly_debug.py:141 ends after iteration `stop`: replay
+      TNP_CHECK(hipMemcpyAsync(ints, cv[CV_INTS0].p, 3 * B * sizeof(float), hipMemcpyDeviceToDevice, s));
+      TIMED("descend", 0.0,
+            launch_descend(e->net, G, glist, crow, sa, sb, xyz, plane, idx, eps, stop + 1, 0, ints,
+                           d0s, d1s, conv, s));
+    }
+  }
+  TIMED("curve_apply", 60.0 * B,
+        launch_curve_apply(B, crow, sa, sb, xyz, e->V, ints, d0s, P<int32_t>(cv[CV_GG]), eps,
+                           P<int32_t>(cv[CV_CINFO]), ctr, s));
+  return 0;
+}
+
+// curve path, phase 2 (subpoly_debug.py:234-271): strict filter after the
+// override; surviving splits get consecutive ids in edge order and rewire
+// their edges (masked_scatter_ of the filtered mask, subpoly.py:201-212).
+static int curve_filter(tnp_engine* e, int idx, int override_, hipStream_t s, int64_t* S_out) {
+  const int64_t S = e->pend_S, V = e->V;
+  const int K = e->K;
+  Buf* cv = e->cv;
+  if (S == 0) { *S_out = 0; return 0; }
+  if (buf_ensure(cv[CV_KEEP], S * sizeof(int32_t), s)) return -1;
+  if (buf_ensure(cv[CV_NID], S * sizeof(int64_t), s)) return -1;
+  if (launch_strict_keep(S, P<int32_t>(cv[CV_CINFO]), P<float>(e->stage), idx, override_,
+                         P<uint64_t>(e->shared), e->net.eps, e->pend_tight, P<int32_t>(cv[CV_KEEP]), s))
+    return -1;
+  if (scan_counts(e, P<int32_t>(cv[CV_KEEP]), P<int64_t>(cv[CV_NID]), S, CTR_KEEP, s)) return -1;
+  if (read_ctr(e, s)) return -1;
+  const int64_t S2 = e->h_ctr[CTR_KEEP];
+  const int64_t n = std::max<int64_t>(S2, 1);
+  if (buf_ensure(cv[CV_SA2], n * sizeof(int32_t), s)) return -1;
+  if (buf_ensure(cv[CV_SB2], n * sizeof(int32_t), s)) return -1;
+  if (buf_ensure(cv[CV_SHARED2], n * sizeof(uint64_t), s)) return -1;
+  if (buf_ensure(cv[CV_STAGE2], (size_t)n * K * sizeof(float), s)) return -1;
+  if (buf_ensure(cv[CV_XYZ2], 3 * n * sizeof(float), s)) return -1;
+  if (buf_ensure(cv[CV_GRID2], n * sizeof(uint64_t), s)) return -1;
+  TIMED("compact_splits", (16.0 + 8.0 * K + 40.0) * S,
+        launch_compact_splits(S, K, P<int32_t>(cv[CV_KEEP]), P<int64_t>(cv[CV_NID]),
+                              P<int32_t>(cv[CV_EIDX]), V, P<int32_t>(e->sa), P<int32_t>(e->sb),
+                              P<uint64_t>(e->shared), P<float>(e->stage), P<float>(e->cur.xyz),
+                              P<uint64_t>(e->cur.grid), S2, P<int32_t>(cv[CV_SA2]),
+                              P<int32_t>(cv[CV_SB2]), P<uint64_t>(cv[CV_SHARED2]),
+                              P<float>(cv[CV_STAGE2]), P<float>(cv[CV_XYZ2]),
+                              P<uint64_t>(cv[CV_GRID2]), P<int32_t>(e->edges), s));
+  if (S2 > 0) {
+    TNP_CHECK(hipMemcpyAsync(P<float>(e->cur.xyz) + 3 * V, cv[CV_XYZ2].p, 3 * S2 * sizeof(float),
+                             hipMemcpyDeviceToDevice, s));
+    TNP_CHECK(hipMemcpyAsync(P<uint64_t>(e->cur.grid) + V, cv[CV_GRID2].p, S2 * sizeof(uint64_t),
+                             hipMemcpyDeviceToDevice, s));
+  }
+  std::swap(e->sa, cv[CV_SA2]);
+  std::swap(e->sb, cv[CV_SB2]);
+  std::swap(e->shared, cv[CV_SHARED2]);
+  std::swap(e->stage, cv[CV_STAGE2]);
+  e->pend_S = S2;
+  *S_out = S2;
+  return 0;
+}
+
+extern "C" int tnp_engine_set_curve(tnp_engine* e, int on) {
+  e->curve = on ? 1 : 0;
+  return 0;
+}
+
 extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S_out, int32_t* fail) {
   hipStream_t s = (hipStream_t)stream;
   TNP_CHECK(hipSetDevice(e->device));
@@ -394,15 +547,18 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
   if (S > 0) {
     if (buf_ensure(e->sa, S * sizeof(int32_t), s)) return -1;
     if (buf_ensure(e->sb, S * sizeof(int32_t), s)) return -1;
+    if (e->curve && buf_ensure(e->cv[CV_EIDX], S * sizeof(int32_t), s)) return -1;
     TIMED("split_emit", 16.0 * e->E + 12.0 * S,
           launch_split_emit(P<int32_t>(e->edges), e->E, col, eps, P<int64_t>(e->blkoff), e->V,
                             P<int32_t>(e->sa), P<int32_t>(e->sb), e->dup_mark,
-                            P<uint64_t>(e->cur.grid), P<int64_t>(e->ctr), s));
+                            P<uint64_t>(e->cur.grid), P<int64_t>(e->ctr),
+                            e->curve ? P<int32_t>(e->cv[CV_EIDX]) : nullptr, s));
     if (vset_ensure(e, e->cur, e->V + S, e->V, s)) return -1;
     col = P<float>(e->cur.pre) + (int64_t)idx * e->cur.cap;  // may have moved
     TIMED("new_vertices", 52.0 * S,
           launch_new_vertices(P<int32_t>(e->sa), P<int32_t>(e->sb), S, col, eps, P<float>(e->cur.xyz),
                               e->V, s));
+    if (e->curve && curve_correct(e, idx, S, s)) return -1;
     if (buf_ensure(e->stage, (size_t)S * e->K * sizeof(float), s)) return -1;
     if (buf_ensure(e->shared, S * sizeof(uint64_t), s)) return -1;
     TIMED("forward", (12.0 + 4.0 * e->K) * S,
@@ -419,6 +575,7 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
     *fail = e->h_ctr[CTR_FAIL] ? 1 : 0;
   }
   e->pend_dup = S > 0 ? e->h_ctr[CTR_DUP] : 0;
+  e->pend_tight = (S > 0 && e->curve) ? (int)e->h_ctr[CTR_TIGHT] : 0;
   *S_out = S;
   e->pend_idx = idx;
   e->pend_S = S;
@@ -433,7 +590,9 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   e->pend_idx = -1;
   const float eps = e->net.eps;
   const int K = e->K;
-  const int64_t V = e->V, E = e->E, S = e->pend_S;
+  int64_t S_kept = e->pend_S;
+  if (e->curve && curve_filter(e, idx, override_, s, &S_kept)) return -1;
+  const int64_t V = e->V, E = e->E, S = S_kept;
   const int64_t NV = V + S;
   VSet& c = e->cur;
   const float* col = P<float>(c.pre) + (int64_t)idx * c.cap;

@@ -23,15 +23,22 @@ enum {
   CTR_AUX = 15,
   CTR_DUP = 16,     // splits on the slab's shared boundary plane
   CTR_BIG = 17,     // a cell with more than 65535 members
+  CTR_B = 18,       // curve path: non-axis-aligned split edges
+  CTR_G = 19,       // curve path: rows needing gradient descent
+  CTR_NOPLANE = 20, // curve path: a c row with no shared plane below idx
+  CTR_TIGHT = 21,   // curve path: a kept c row misses its edge plane by > eps
+  CTR_KEEP = 22,    // curve path: splits surviving the strict filter
   CTR_N = 24
 };
 
 int64_t step_tiles(int64_t n);
 int launch_split_count(const int32_t* edges, int64_t E, const float* col, float eps, int32_t* blk,
                        hipStream_t s);
+// eidx != null (curve path): record each split's edge index instead of
+// rewiring the edge (the strict filter decides later which splits survive)
 int launch_split_emit(int32_t* edges, int64_t E, const float* col, float eps, const int64_t* blkoff,
                       int64_t V, int32_t* sa, int32_t* sb, int dup_mark, const uint64_t* grid,
-                      int64_t* ctr, hipStream_t s);
+                      int64_t* ctr, int32_t* eidx, hipStream_t s);
 int launch_new_vertices(const int32_t* sa, const int32_t* sb, int64_t S, const float* col,
                         float eps, float* xyz, int64_t V, hipStream_t s);
 int launch_fail_check(const int32_t* sa, const int32_t* sb, int64_t S, int idx,
@@ -84,3 +91,35 @@ int launch_surface_flags(const float* xyz, const float* col, int64_t V, float ep
 int launch_surface_edges(const int32_t* edges, int64_t E, const int32_t* on, int32_t* blk,
                          const int64_t* blkoff, int emit, int32_t* out, int32_t* used,
                          hipStream_t s);
+
+// ---- curve.hip (force=False branch) ----
+int launch_curve_flags(const int32_t* sa, const int32_t* sb, int64_t S, const float* xyz, float eps,
+                       int32_t* cflag, hipStream_t s);
+int launch_curve_rows(const int32_t* cflag, const int64_t* coff, int64_t S, int32_t* crow,
+                      hipStream_t s);
+int launch_curve_corners(const int32_t* crow, int64_t B, const int32_t* sa, const int32_t* sb,
+                         const float* xyz, const uint64_t* zero, int idx, float* corners,
+                         int32_t* plane, int64_t* ctr, hipStream_t s);
+int launch_curve_solve(int64_t B, const float* stage_c, int64_t ldc, const int32_t* plane, int idx,
+                       const int32_t* crow, const int32_t* sa, const int32_t* sb, const float* xyz,
+                       float* ints, float* pts, hipStream_t s);
+int launch_curve_dnew(int64_t B, const float* stage_p, int64_t ldp, const int32_t* plane, int idx,
+                      const float* ints, float eps, float* d0s, float* d1s, int32_t* gg, int32_t* gd,
+                      hipStream_t s);
+int launch_gd_rows(const int32_t* gd, const int64_t* goff, int64_t B, int32_t* glist, hipStream_t s);
+struct NetDev;
+int launch_descend(const NetDev& net, int64_t G, const int32_t* glist, const int32_t* crow,
+                   const int32_t* sa, const int32_t* sb, const float* xyz, const int32_t* plane,
+                   int idx, float eps, int iters, int record, float* ints, float* d0s, float* d1s,
+                   unsigned long long* conv, hipStream_t s);
+int launch_curve_apply(int64_t B, const int32_t* crow, const int32_t* sa, const int32_t* sb,
+                       float* xyz, int64_t V, const float* ints, const float* d0s, const int32_t* gg,
+                       float eps, int32_t* cinfo, int64_t* ctr, hipStream_t s);
+int launch_strict_keep(int64_t S, const int32_t* cinfo, const float* stage, int idx, int override_,
+                       const uint64_t* shared, float eps, int tight, int32_t* keep, hipStream_t s);
+int launch_compact_splits(int64_t S, int K, const int32_t* keep, const int64_t* nid,
+                          const int32_t* eidx, int64_t V, const int32_t* sa, const int32_t* sb,
+                          const uint64_t* shared, const float* stage, const float* xyz,
+                          const uint64_t* grid, int64_t S2, int32_t* sa2, int32_t* sb2,
+                          uint64_t* shared2, float* stage2, float* xyz2, uint64_t* grid2,
+                          int32_t* edges, hipStream_t s);

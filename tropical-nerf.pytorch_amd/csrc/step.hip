@@ -64,7 +64,7 @@ __global__ void __launch_bounds__(TNP_BLOCK)
 k_split_emit(int32_t* __restrict__ edges, int64_t E, const float* __restrict__ col, float eps,
              const int64_t* __restrict__ blkoff, int64_t V, int32_t* __restrict__ sa,
              int32_t* __restrict__ sb, int dup_mark, const uint64_t* __restrict__ grid,
-             int64_t* __restrict__ ctr) {
+             int64_t* __restrict__ ctr, int32_t* __restrict__ eidx) {
   __shared__ int lds[TNP_WAVES];
   int64_t base = (int64_t)blockIdx.x * TILE;
   int64_t run = blkoff[blockIdx.x];
@@ -79,7 +79,8 @@ k_split_emit(int32_t* __restrict__ edges, int64_t E, const float* __restrict__ c
       int a = edges[2 * i], b = edges[2 * i + 1];
       sa[id] = a;
       sb[id] = b;
-      edges[2 * i + 1] = (int32_t)(V + id);
+      if (eidx) eidx[id] = (int32_t)i;
+      else edges[2 * i + 1] = (int32_t)(V + id);
       if (dup_mark >= 0) {
         // edge lying in this slab's upper boundary mark plane (x = mark):
         // the neighbouring slab splits the same edge, count it once
@@ -614,9 +615,9 @@ int launch_split_count(const int32_t* edges, int64_t E, const float* col, float 
 }
 int launch_split_emit(int32_t* edges, int64_t E, const float* col, float eps, const int64_t* blkoff,
                       int64_t V, int32_t* sa, int32_t* sb, int dup_mark, const uint64_t* grid,
-                      int64_t* ctr, hipStream_t s) {
+                      int64_t* ctr, int32_t* eidx, hipStream_t s) {
   hipLaunchKernelGGL(k_split_emit, dim3((unsigned)step_tiles(E)), dim3(TNP_BLOCK), 0, s, edges, E,
-                     col, eps, blkoff, V, sa, sb, dup_mark, grid, ctr);
+                     col, eps, blkoff, V, sa, sb, dup_mark, grid, ctr, eidx);
   TNP_CHECK(hipGetLastError());
   return 0;
 }

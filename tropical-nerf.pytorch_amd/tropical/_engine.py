@@ -83,6 +83,12 @@ class Engine:
                                                 _hip.ptr(cache), self._s), "tnp_engine_export")
         return verts, edges, cache
 
+    def set_curve(self, on: bool):
+        """subpoly_(force=False) semantics for the following steps."""
+        _hip.check(_hip.lib().tnp_engine_set_curve(self.h, int(on)), "tnp_engine_set_curve")
+        self.curve = bool(on)
+        return self
+
     def set_dup_plane(self, mark: int):
         _hip.check(_hip.lib().tnp_engine_set_dup_plane(self.h, int(mark)), "tnp_engine_set_dup_plane")
 
@@ -142,6 +148,9 @@ class Engine:
         effects, subpoly.py:110).  ``allreduce(vec, op)`` (multi-GPU) makes
         the split count, the override predicate and the active mask global."""
         K, H = self.K, self.num_hidden
+        if allreduce is not None and getattr(self, "curve", False):
+            raise NotImplementedError("curve path (force=False) is single-device: the descent's "
+                                      "stop criterion is global (subpoly_debug.py:141)")
         mask = self.active_planes(0)
         if allreduce is not None:
             mask = int(allreduce(np.array([mask], dtype=np.uint64), "or")[0])
@@ -178,4 +187,4 @@ def engine_for(net) -> Engine:
     if eng is None:
         eng = Engine(torch.device("cuda", key))
         _ENGINES[key] = eng
-    return eng.set_net(net)
+    return eng.set_net(net).set_curve(False)

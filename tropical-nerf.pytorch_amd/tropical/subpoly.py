@@ -43,10 +43,7 @@ def subpoly(net, d: int, size: float, eps: float = 1e-4, force: bool = False,
     _check_eps(net, eps)
     if d != 3:
         raise NotImplementedError("d must be 3 (the reference's hash grid is 3-D)")
-    if not force:
-        from .curve import subpoly_curve
-        return subpoly_curve(net, size, stats=stats)
-    eng = engine_for(net)
+    eng = engine_for(net).set_curve(not force)
     eng.skeleton(unit=128, size=size)
     eng.run_steps(stats)
     return _finish(eng, net)
@@ -82,15 +79,16 @@ def subpoly_lattice(net, x0: int = 0, x1: int = -1, stats: list = None, faces: b
 
 def subpoly_(vertices, edges, net, l, h, eps, outputs_=None, pruning=True, strict=True,
              force=False):
-    """One hyperplane step (subpoly.py:90-279), flat branch.
+    """One hyperplane step (subpoly.py:90-279); ``force=False`` is the curve
+    branch (strict filter on, as the reference's default ``strict=True``).
 
     Deviation: the caller's ``edges`` tensor is not rewritten in place (the
     reference's masked_scatter_ side effect at subpoly.py:211); the returned
     edges are identical."""
     _check_eps(net, eps)
-    if not force:
-        raise NotImplementedError("subpoly_ curve branch: use subpoly(..., force=False)")
-    eng = engine_for(net)
+    if not force and not strict:
+        raise NotImplementedError("subpoly_(force=False, strict=False) is not on the extraction path")
+    eng = engine_for(net).set_curve(not force)
     eng.load(vertices, edges, outputs_, keep_all=True)
     idx = l * net.num_hidden + h
     S, fail = eng.split(idx)
