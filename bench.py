@@ -196,6 +196,7 @@ def main():
     x0, x1 = slab(G, rank, world)
     eng = engine_for(net)
     eng.set_dup_plane(x1 if rank < world - 1 else -1)
+    eng.set_shards(world)
 
     def one_pass():
         stats = []

@@ -178,6 +178,12 @@ int tnp_engine_set_curve(tnp_engine* eng, int on);
  * global split count can subtract the replicated boundary work. */
 int tnp_engine_set_dup_plane(tnp_engine* eng, int mark);
 
+/* world > 1: this engine holds one x-slab of a complex sharded over `world`
+ * devices.  A step the other shards split may leave this one without any
+ * connecting pair; the reference's empty-torch.cat error (subpoly.py:505-513)
+ * then only applies to the whole complex, not to a shard. */
+int tnp_engine_set_shards(tnp_engine* eng, int world);
+
 /* HIP-event timing of every engine kernel launch (on=1 clears and starts;
  * on=0 stops, synchronizes and aggregates per kernel name); read the
  * aggregates with tnp_engine_kernel_stat (ms, launches, modelled

@@ -118,6 +118,7 @@ struct tnp_engine {
   int device = 0;
   int dup_mark = -1;
   int curve = 0;          // 1: subpoly_(force=False) semantics
+  int shards = 1;         // >1: one x-slab of a sharded complex
   int pend_tight = 0;
   int gd_iters = 500;     // subpoly_debug.py:141
   int64_t max_pair_tests = 20000000000LL;
@@ -518,6 +519,11 @@ static int curve_filter(tnp_engine* e, int idx, int override_, hipStream_t s, in
   return 0;
 }
 
+extern "C" int tnp_engine_set_shards(tnp_engine* e, int world) {
+  e->shards = world < 1 ? 1 : world;
+  return 0;
+}
+
 extern "C" int tnp_engine_set_curve(tnp_engine* e, int on) {
   e->curve = on ? 1 : 0;
   return 0;
@@ -684,7 +690,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     if (X <= cap) break;
     cap = X;  // appended beyond the buffer: grow to the exact count and redo
   }
-  if (e->h_ctr[CTR_COMPAT] == 0) {
+  if (e->h_ctr[CTR_COMPAT] == 0 && e->shards <= 1) {
     // every region has a single member: extract_every_valid_edge cats an
     // empty list (subpoly.py:505-513)
     tnp_set_error("torch.cat(): expected a non-empty list of Tensors (no region with two vertices, plane %d)", idx);

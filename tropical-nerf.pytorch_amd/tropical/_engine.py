@@ -89,6 +89,10 @@ class Engine:
         self.curve = bool(on)
         return self
 
+    def set_shards(self, world: int):
+        _hip.check(_hip.lib().tnp_engine_set_shards(self.h, int(world)), "tnp_engine_set_shards")
+        return self
+
     def set_dup_plane(self, mark: int):
         _hip.check(_hip.lib().tnp_engine_set_dup_plane(self.h, int(mark)), "tnp_engine_set_dup_plane")
 

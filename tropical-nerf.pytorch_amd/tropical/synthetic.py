@@ -74,3 +74,21 @@ def lattice_vertices(marks: np.ndarray) -> np.ndarray:
     n = m.shape[0]
     g = np.stack(np.meshgrid(m, m, m, indexing="ij"), -1).reshape(-1, 3)
     return (g * np.float32(2) - np.float32(1)).astype(np.float32)
+
+
+def slab_lattice(marks: np.ndarray, x0: int, x1: int):
+    """The x-slab [x0, x1] (mark indices) of the full lattice, laid out as
+    tnp_engine_lattice does: vertex (i, j, k) -> id (i - x0) N^2 + j N + k;
+    x-edges, then y, then z, each (hi, lo) -- an order-preserving subsequence
+    of lattice_edges(N) restricted to the slab, so shards number and orient
+    every shared element exactly as the unsharded run does."""
+    m = np.asarray(marks, dtype=np.float32)
+    n = m.shape[0]
+    nx = x1 - x0 + 1
+    g = np.stack(np.meshgrid(m[x0:x1 + 1], m, m, indexing="ij"), -1).reshape(-1, 3)
+    verts = (g * np.float32(2) - np.float32(1)).astype(np.float32)
+    ids = np.arange(nx * n * n, dtype=np.int64).reshape(nx, n, n)
+    ex = np.stack([ids[1:, :, :].reshape(-1), ids[:-1, :, :].reshape(-1)], -1)
+    ey = np.stack([ids[:, 1:, :].reshape(-1), ids[:, :-1, :].reshape(-1)], -1)
+    ez = np.stack([ids[:, :, 1:].reshape(-1), ids[:, :, :-1].reshape(-1)], -1)
+    return verts, np.concatenate([ex, ey, ez], 0)
