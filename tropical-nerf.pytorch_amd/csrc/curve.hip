@@ -136,6 +136,191 @@ struct Roots01<1> {
   }
 };
 
+
+// ---- sgeev on a 2x2 real matrix, as x86 MKL computes it ---------------------
+// (torch.linalg.eigvals on the quadratics' companion matrices -- 98% of the
+// curve rows).  sgebal (permute + power-of-2 balance), slahqr's
+// Ahues-Kressner deflation test on H(2,1), slanv2's standardisation; fp32
+// with explicit roundings.  Reverse-engineered bitwise against torch on CPU
+// (tools/lapack2x2_probe.py: 20000 random companions + every quadratic row
+// of the golden nets).
+__device__ __forceinline__ float fsign(float a, float b) { return b >= 0.f ? fabsf(a) : -fabsf(a); }
+
+__device__ __forceinline__ float slapy2(float x, float y) {
+  x = fabsf(x);
+  y = fabsf(y);
+  float w = fmaxf(x, y), z = fminf(x, y);
+  if (z == 0.f || w > 3.4e38f) return w;
+  float r = __fdiv_rn(z, w);
+  return __fmul_rn(w, __fsqrt_rn(__fadd_rn(1.f, __fmul_rn(r, r))));
+}
+
+__device__ void slanv2(float a, float b, float c, float d, float wr[2], float wi[2]) {
+  const float EPS = 1.1920928955078125e-07f;  // slamch('P')
+  if (c == 0.f) {
+  } else if (b == 0.f) {
+    float t = d;
+    d = a;
+    a = t;
+    b = -c;
+    c = 0.f;
+  } else if (__fsub_rn(a, d) == 0.f && ((b > 0.f) != (c > 0.f))) {
+  } else {
+    float temp = __fsub_rn(a, d);
+    float p = __fmul_rn(0.5f, temp);
+    float bcmax = fmaxf(fabsf(b), fabsf(c));
+    float bcmis = __fmul_rn(__fmul_rn(fminf(fabsf(b), fabsf(c)), fsign(1.f, b)), fsign(1.f, c));
+    float scale = fmaxf(fabsf(p), bcmax);
+    float z = __fadd_rn(__fmul_rn(__fdiv_rn(p, scale), p), __fmul_rn(__fdiv_rn(bcmax, scale), bcmis));
+    if (z >= 4.f * EPS) {
+      z = __fadd_rn(p, fsign(__fmul_rn(__fsqrt_rn(scale), __fsqrt_rn(z)), p));
+      a = __fadd_rn(d, z);
+      d = __fsub_rn(d, __fmul_rn(__fdiv_rn(bcmax, z), bcmis));
+      b = __fsub_rn(b, c);
+      c = 0.f;
+    } else {
+      float sigma = __fadd_rn(b, c);
+      float tau = slapy2(sigma, temp);
+      float cs = __fsqrt_rn(__fmul_rn(0.5f, __fadd_rn(1.f, __fdiv_rn(fabsf(sigma), tau))));
+      float sn = __fmul_rn(-__fdiv_rn(p, __fmul_rn(tau, cs)), fsign(1.f, sigma));
+      float aa = __fadd_rn(__fmul_rn(a, cs), __fmul_rn(b, sn));
+      float bb = __fadd_rn(__fmul_rn(-a, sn), __fmul_rn(b, cs));
+      float cc = __fadd_rn(__fmul_rn(c, cs), __fmul_rn(d, sn));
+      float dd = __fadd_rn(__fmul_rn(-c, sn), __fmul_rn(d, cs));
+      a = __fadd_rn(__fmul_rn(aa, cs), __fmul_rn(cc, sn));
+      b = __fadd_rn(__fmul_rn(bb, cs), __fmul_rn(dd, sn));
+      c = __fadd_rn(__fmul_rn(-aa, sn), __fmul_rn(cc, cs));
+      d = __fadd_rn(__fmul_rn(-bb, sn), __fmul_rn(dd, cs));
+      temp = __fmul_rn(0.5f, __fadd_rn(a, d));
+      a = d = temp;
+      if (c != 0.f) {
+        if (b != 0.f) {
+          if ((b > 0.f) == (c > 0.f)) {
+            float sab = __fsqrt_rn(fabsf(b)), sac = __fsqrt_rn(fabsf(c));
+            p = fsign(__fmul_rn(sab, sac), c);
+            a = __fadd_rn(temp, p);
+            d = __fsub_rn(temp, p);
+            b = __fsub_rn(b, c);
+            c = 0.f;
+          }
+        } else {
+          b = -c;
+          c = 0.f;
+        }
+      }
+    }
+  }
+  wr[0] = a;
+  wr[1] = d;
+  if (c == 0.f) {
+    wi[0] = wi[1] = 0.f;
+  } else {
+    wi[0] = __fmul_rn(__fsqrt_rn(fabsf(b)), __fsqrt_rn(fabsf(c)));
+    wi[1] = -wi[0];
+  }
+}
+
+__device__ __forceinline__ float nrm2_2(float x, float y) {
+  double s = (double)x * (double)x + (double)y * (double)y;
+  return (float)sqrt(s);
+}
+
+__device__ void eig2x2(float A[2][2], float wr[2], float wi[2]) {
+  // sgebal: permutations isolating eigenvalues
+  int k = 0, l = 1;
+  bool done = false;
+  for (;;) {  // rows with zero off-diagonal (columns 0..l) pushed down
+    int found = -1;
+    for (int j = l; j >= 0; --j) {
+      bool z = true;
+      for (int i = 0; i <= l; ++i)
+        if (i != j && A[j][i] != 0.f) z = false;
+      if (z) { found = j; break; }
+    }
+    if (found < 0) break;
+    if (found != l) {
+      for (int r = 0; r < 2; ++r) { float t = A[r][found]; A[r][found] = A[r][l]; A[r][l] = t; }
+      for (int c = 0; c < 2; ++c) { float t = A[found][c]; A[found][c] = A[l][c]; A[l][c] = t; }
+    }
+    if (l == 0) { done = true; break; }
+    --l;
+  }
+  if (done) {
+    wr[0] = A[0][0]; wr[1] = A[1][1]; wi[0] = wi[1] = 0.f;
+    return;
+  }
+  for (;;) {  // columns with zero off-diagonal (rows k..l) pushed left
+    int found = -1;
+    for (int j = k; j <= l; ++j) {
+      bool z = true;
+      for (int i = k; i <= l; ++i)
+        if (i != j && A[i][j] != 0.f) z = false;
+      if (z) { found = j; break; }
+    }
+    if (found < 0) break;
+    if (found != k) {
+      for (int r = 0; r < 2; ++r) { float t = A[r][found]; A[r][found] = A[r][k]; A[r][k] = t; }
+      for (int c = 0; c < 2; ++c) { float t = A[found][c]; A[found][c] = A[k][c]; A[k][c] = t; }
+    }
+    ++k;
+  }
+  if (k >= l) {  // at most one row left unisolated
+    wr[0] = A[0][0]; wr[1] = A[1][1]; wi[0] = wi[1] = 0.f;
+    return;
+  }
+  // power-of-2 balancing of rows/columns k..l (= 0..1 here)
+  const float SAFMIN = 1.17549435e-38f, ULP = 1.1920928955078125e-07f;
+  const float SFMIN1 = SAFMIN / ULP, SFMAX1 = 1.f / SFMIN1;
+  const float SFMIN2 = SFMIN1 * 2.f, SFMAX2 = 1.f / SFMIN2;
+  float scale[2] = {1.f, 1.f};
+  for (int pass = 0; pass < 64; ++pass) {
+    bool noconv = false;
+    for (int i = 0; i < 2; ++i) {
+      float c = nrm2_2(A[0][i], A[1][i]);
+      float r = nrm2_2(A[i][0], A[i][1]);
+      float ca = fmaxf(fabsf(A[0][i]), fabsf(A[1][i]));
+      float ra = fmaxf(fabsf(A[i][0]), fabsf(A[i][1]));
+      if (c == 0.f || r == 0.f) continue;
+      float g = r / 2.f, f = 1.f, s = __fadd_rn(c, r);
+      while (!(c >= g || fmaxf(f, fmaxf(c, ca)) >= SFMAX2 || fminf(r, fminf(g, ra)) <= SFMIN2)) {
+        f *= 2.f; c *= 2.f; ca *= 2.f; r /= 2.f; g /= 2.f; ra /= 2.f;
+      }
+      g = c / 2.f;
+      while (!(g < r || fmaxf(r, ra) >= SFMAX2 || fminf(fminf(f, c), fminf(g, ca)) <= SFMIN2)) {
+        f /= 2.f; c /= 2.f; g /= 2.f; ca /= 2.f; r *= 2.f; ra *= 2.f;
+      }
+      if (__fadd_rn(c, r) >= __fmul_rn(0.95f, s)) continue;
+      if (f < 1.f && scale[i] < 1.f && f * scale[i] <= SFMIN1) continue;
+      if (f > 1.f && scale[i] > 1.f && scale[i] >= SFMAX1 / f) continue;
+      float gi = 1.f / f;
+      scale[i] *= f;
+      noconv = true;
+      A[i][0] *= gi; A[i][1] *= gi;
+      A[0][i] *= f; A[1][i] *= f;
+    }
+    if (!noconv) break;
+  }
+  // slahqr: H(2,1) negligible (Ahues & Kressner) -> two 1x1 blocks
+  const float SMLNUM = SAFMIN * (2.f / ULP);
+  float h21 = fabsf(A[1][0]);
+  bool defl = h21 <= SMLNUM;
+  if (!defl) {
+    float tst = __fadd_rn(fabsf(A[0][0]), fabsf(A[1][1]));
+    if (h21 <= __fmul_rn(ULP, tst)) {
+      float ab = fmaxf(h21, fabsf(A[0][1])), ba = fminf(h21, fabsf(A[0][1]));
+      float dd = fabsf(__fsub_rn(A[0][0], A[1][1]));
+      float aa = fmaxf(fabsf(A[1][1]), dd), bb = fminf(fabsf(A[1][1]), dd);
+      float s = __fadd_rn(aa, ab);
+      defl = __fmul_rn(ba, __fdiv_rn(ab, s)) <= fmaxf(SMLNUM, __fmul_rn(ULP, __fmul_rn(bb, __fdiv_rn(aa, s))));
+    }
+  }
+  if (defl) {
+    wr[0] = A[0][0]; wr[1] = A[1][1]; wi[0] = wi[1] = 0.f;
+    return;
+  }
+  slanv2(A[0][0], A[0][1], A[1][0], A[1][1], wr, wi);
+}
+
 // batched_polynomial_roots (geometry.py:259-299) for one row of 5 fp32
 // coefficients (leading first): tiny coefficients zeroed, degree from the
 // first non-zero one, companion row r_k = -c_k / c_lead in fp32 (what LAPACK
@@ -154,6 +339,17 @@ __device__ float largest_root01(float c[5]) {
   if (N == 1) {
     float r = __fdiv_rn(-c[4], c[3]);
     return (r >= 0.f && r <= 1.f) ? r : -1.f;
+  }
+  if (N == 2) {
+    // companion [[0, 1], [-c4/c2, -c3/c2]]; the LAST eigenvalue (LAPACK's
+    // order) that is real and in [0, 1]
+    float A[2][2] = {{0.f, 1.f}, {__fdiv_rn(-c[4], c[2]), __fdiv_rn(-c[3], c[2])}};
+    float wr[2], wi[2];
+    eig2x2(A, wr, wi);
+    float r = -1.f;
+    for (int k = 0; k < 2; ++k)
+      if (fabsf(wi[k]) <= ROOT_EPS && wr[k] >= 0.f && wr[k] <= 1.f) r = wr[k];
+    return r;
   }
   double a[5];
   a[0] = 1.0;
@@ -289,28 +485,47 @@ __global__ void k_gd_rows(const int32_t* __restrict__ gd, const int64_t* __restr
   if (b < B && gd[b]) glist[goff[b]] = (int32_t)b;
 }
 
+// x86 MKL's 1-row sgemm (1x16 @ 16x16, the gradient through layer 2 when
+// a single row descends): this summation tree with these fused products
+// (tools probe, bitwise against torch.mm on CPU)
+__device__ __forceinline__ float mm1_16(const float* x, const float* W, int ld, int k) {
+  auto pr = [&](int a, int b) {  // fma(x_a, w_a, x_b * w_b)
+    return __fmaf_rn(x[a], W[a * ld + k], __fmul_rn(x[b], W[b * ld + k]));
+  };
+  float v = __fadd_rn(__fadd_rn(pr(0, 2), pr(1, 3)), __fadd_rn(pr(4, 6), pr(5, 7)));
+  v = __fmaf_rn(x[14], W[14 * ld + k], v);
+  v = __fmaf_rn(x[12], W[12 * ld + k], v);
+  v = __fadd_rn(v, pr(13, 15));
+  return __fadd_rn(v, __fadd_rn(pr(8, 10), pr(9, 11)));
+}
+
 // pre-activations of planes j0, j1 at u (preprocessed) and d(d0^2 + d1^2)/du
+// exactly as torch autograd computes it on CPU for a G-row batch
+// (subpoly_debug.py:143-148): forward with MKL's G-row schedules, backward
+// through AddmmBackward (mm(grad, W): sequential fma; 1-row layer-2 tree),
+// threshold_backward, and the encoding's input gradient (oracle/encoding.py
+// _GridFn.backward op order).
 template <int LV, int H>
 __device__ __forceinline__ void plane_pair_grad(const NetDev& net, const float* w, const float u[3],
-                                                int j0, int j1, float& d0, float& d1,
-                                                float gu[3]) {
+                                                int j0, int j1, int mh, int mo, bool one_row,
+                                                float& d0, float& d1, float gu[3]) {
   constexpr int IN = 2 * LV;
   float f[IN], a1[H], h1[H], a2[H], h2[H], o[2];
   encode<LV>(net, u, f);
   const float* W0 = w;
   const float* W1 = W0 + H * IN + H;
   const float* W2 = W1 + H * H + H;
-  linear<IN, H>(W0, W0 + H * IN, f, a1);
+  linear_mode<IN, H>(W0, W0 + H * IN, f, a1, mh);
 #pragma unroll
   for (int j = 0; j < H; ++j) h1[j] = fmaxf(a1[j], 0.f);
-  linear<H, H>(W1, W1 + H * H, h1, a2);
+  linear_mode<H, H>(W1, W1 + H * H, h1, a2, mh);
 #pragma unroll
   for (int j = 0; j < H; ++j) h2[j] = fmaxf(a2[j], 0.f);
-  linear<H, 2>(W2, W2 + 2 * H, h2, o);
+  linear_mode<H, 2>(W2, W2 + 2 * H, h2, o, mo);
   float last = __fsub_rn(o[1], o[0]);
   d0 = j0 < H ? a1[j0] : (j0 < 2 * H ? a2[j0 - H] : last);
   d1 = j1 < H ? a1[j1] : (j1 < 2 * H ? a2[j1 - H] : last);
-  // seeds of y = d0^2 + d1^2
+  // seeds of y = d0^2 + d1^2 on the gathered pre-activations (2 d, exact)
   float g1[H], g2[H], go = 0.f;
 #pragma unroll
   for (int j = 0; j < H; ++j) g1[j] = g2[j] = 0.f;
@@ -318,41 +533,46 @@ __device__ __forceinline__ void plane_pair_grad(const NetDev& net, const float* 
   const float ds[2] = {d0, d1};
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    float g = 2.f * ds[s];
+    float g = __fmul_rn(2.f, ds[s]);
     int j = js[s];
-    if (j < H) {
 #pragma unroll
-      for (int k = 0; k < H; ++k) g1[k] += (k == j) ? g : 0.f;
-    } else if (j < 2 * H) {
-#pragma unroll
-      for (int k = 0; k < H; ++k) g2[k] += (k == j - H) ? g : 0.f;
-    } else {
-      go += g;
+    for (int k = 0; k < H; ++k) {
+      if (j == k) g1[k] = __fadd_rn(g1[k], g);
+      if (j == H + k) g2[k] = __fadd_rn(g2[k], g);
     }
+    if (j == 2 * H) go = __fadd_rn(go, g);
   }
-  // back through layer 3 (o1 - o0), ReLU 2, layer 2, ReLU 1, layer 1;
-  // g1 / g2 end as the total gradients of the pre-activations a1 / a2
+  // layer 3 (o1 - o0): mm([-go, go], W2), K = 2 sequential fma; ReLU 2
 #pragma unroll
   for (int k = 0; k < H; ++k) {
-    float v = go * W2[H + k] - go * W2[k];
-    g2[k] = a2[k] > 0.f ? g2[k] + v : g2[k];
+    float v = __fmaf_rn(go, W2[H + k], __fmul_rn(-go, W2[k]));
+    if (a2[k] > 0.f) g2[k] = __fadd_rn(g2[k], v);
   }
-  float gh1[H];
+  // layer 2: mm(g_a2, W1) ; ReLU 1
+  float ga1[H];
 #pragma unroll
   for (int k = 0; k < H; ++k) {
-    float v = 0.f;
+    float v;
+    if (one_row) {
+      v = mm1_16(g2, W1, H, k);
+    } else {
+      v = 0.f;
 #pragma unroll
-    for (int j = 0; j < H; ++j) v += g2[j] * W1[j * H + k];
-    gh1[k] = v;
+      for (int j = 0; j < H; ++j) v = __fmaf_rn(g2[j], W1[j * H + k], v);
+    }
+    ga1[k] = a1[k] > 0.f ? __fadd_rn(g1[k], v) : g1[k];
   }
+  // layer 1: mm(g_a1, W0), sequential fma
   float df[IN];
 #pragma unroll
   for (int m = 0; m < IN; ++m) {
     float v = 0.f;
 #pragma unroll
-    for (int k = 0; k < H; ++k) v += (a1[k] > 0.f ? g1[k] + gh1[k] : g1[k]) * W0[k * IN + m];
+    for (int k = 0; k < H; ++k) v = __fmaf_rn(ga1[k], W0[k * IN + m], v);
     df[m] = v;
   }
+  // encoding input gradient: per level, per corner, per dim
+  //   gx_d += (((sgn * f_e0) * f_e1) * dv) * scale,  dv = val . g_feat
   float gx[3] = {0.f, 0.f, 0.f};
 #pragma unroll
   for (int l = 0; l < LV; ++l) {
@@ -361,9 +581,9 @@ __device__ __forceinline__ void plane_pair_grad(const NetDev& net, const float* 
     uint32_t g[3];
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
-      float pos = u[d] * sc + 0.5f;
+      float pos = __fadd_rn(__fmul_rn(u[d], sc), 0.5f);
       float fl = floorf(pos);
-      t[d] = pos - fl;
+      t[d] = __fsub_rn(pos, fl);
       g[d] = (uint32_t)(int)fl;
     }
     const uint32_t res = (uint32_t)net.res[l];
@@ -375,18 +595,19 @@ __device__ __forceinline__ void plane_pair_grad(const NetDev& net, const float* 
 #pragma unroll
       for (int d = 0; d < 3; ++d) {
         bool up = (c >> d) & 1;
-        fc[d] = up ? t[d] : 1.f - t[d];
+        fc[d] = up ? t[d] : __fsub_rn(1.f, t[d]);
         gc[d] = g[d] + (up ? 1u : 0u);
       }
       uint32_t id = net.dense[l] ? (gc[0] + gc[1] * res + gc[2] * (res * res))
                                  : (gc[0] ^ (gc[1] * P1) ^ (gc[2] * P2));
       id %= net.sizes[l];
       float2 v = tab[id];
-      float dv = v.x * df[2 * l] + v.y * df[2 * l + 1];
+      float dv = __fadd_rn(__fmul_rn(v.x, df[2 * l]), __fmul_rn(v.y, df[2 * l + 1]));
 #pragma unroll
       for (int d = 0; d < 3; ++d) {
         float sg = ((c >> d) & 1) ? 1.f : -1.f;
-        gx[d] += sg * fc[(d + 1) % 3] * fc[(d + 2) % 3] * dv * sc;
+        float fa = fc[d == 0 ? 1 : 0], fb = fc[d == 2 ? 1 : 2];
+        gx[d] = __fadd_rn(gx[d], __fmul_rn(__fmul_rn(__fmul_rn(__fmul_rn(sg, fa), fb), dv), sc));
       }
     }
   }
@@ -421,6 +642,7 @@ k_descend(NetDev net, int64_t G, const int32_t* __restrict__ glist,
     x[d] = ints[3 * b + d];
   }
   const int j0 = plane[b];
+  const int mh = lin_mode(G, false), mo = lin_mode(G, true);
   uint64_t bits[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   float d0 = 1.f, d1 = 1.f;
   for (int it = 0; it < iters; ++it) {
@@ -428,7 +650,7 @@ k_descend(NetDev net, int64_t G, const int32_t* __restrict__ glist,
 #pragma unroll
     for (int d = 0; d < 3; ++d)
       u[d] = __fdiv_rn(__fadd_rn(__fadd_rn(e0[d], __fmul_rn(x[d], de[d])), 1.0f), 2.0f);
-    plane_pair_grad<LV, H>(net, w, u, j0, idx, d0, d1, gu);
+    plane_pair_grad<LV, H>(net, w, u, j0, idx, mh, mo, G == 1, d0, d1, gu);
     float gx[3], nn = 0.f;
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
