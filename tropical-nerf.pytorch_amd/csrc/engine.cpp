@@ -136,6 +136,7 @@ struct tnp_engine {
   int keep_all = 0;
   int valid_from = 0;  // pre planes [valid_from, K) are valid for every vertex
   // step scratch
+  Buf spcnt, spoff, part, ekey_a, ekey_b, eval_b, cellend, sort_scr2;
   Buf blk, blkoff, scan_scr, sa, sb, stage, shared, members, cellcnt, cellcur, celloff, ent_v,
       ent_g, ent_p, ent_z, tcnt, toff, bcell, bstat, ckeys_a, ckeys_b, sort_scr, flags, used, nid,
       ctr;
@@ -257,6 +258,9 @@ extern "C" void tnp_engine_destroy(tnp_engine* e) {
   for (Buf& b : e->fscr) buf_free(b, s);
   for (Buf& b : e->fscr2) buf_free(b, s);
   for (Buf& b : e->cv) buf_free(b, s);
+  for (Buf* b : {&e->spcnt, &e->spoff, &e->part, &e->ekey_a, &e->ekey_b, &e->eval_b, &e->cellend,
+                 &e->sort_scr2})
+    buf_free(*b, s);
   (void)hipDeviceSynchronize();
   if (e->h_ctr) (void)hipHostFree(e->h_ctr);
   delete e;
@@ -623,23 +627,59 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   }
   TIMED("hit_emit", 4.0 * V + 4.0 * S, launch_hit_emit(col, V, eps, P<int64_t>(e->blkoff), P<int32_t>(e->members), S, s));
 
-  // 3. bucket members by grid cell (dense cell grid over the marks)
+  // 3. bucket members by grid cell (dense cell grid over the marks): one
+  //    (cell, member) entry per spanned cell, radix-sorted by cell
   const int NC = e->net.n_marks + 2;
   const int64_t ncell = (int64_t)NC * NC * NC;
-  if (buf_ensure(e->cellcnt, ncell * sizeof(int32_t), s)) return -1;
-  if (buf_ensure(e->cellcur, ncell * sizeof(int32_t), s)) return -1;
-  if (buf_ensure(e->celloff, ncell * sizeof(int64_t), s)) return -1;
-  TNP_CHECK(hipMemsetAsync(e->cellcnt.p, 0, ncell * sizeof(int32_t), s));
-  TNP_CHECK(hipMemsetAsync(e->cellcur.p, 0, ncell * sizeof(int32_t), s));
   if (read_ctr(e, s)) return -1;
   const int64_t H = V > 0 ? e->h_ctr[CTR_H] : 0;
   const int64_t M = S + H;
-  TIMED("cell_count", 24.0 * M, launch_cell_count(P<int32_t>(e->members), M, grid, zero, idx, NC, P<int32_t>(e->cellcnt), ctr, s));
-  if (scan_counts(e, P<int32_t>(e->cellcnt), P<int64_t>(e->celloff), ncell, CTR_T, s)) return -1;
-  // member pairs per cell -> flattened pair space offsets (total = tests)
+  if (buf_ensure(e->spcnt, std::max<int64_t>(M, 1) * sizeof(int32_t), s)) return -1;
+  if (buf_ensure(e->spoff, std::max<int64_t>(M, 1) * sizeof(int64_t), s)) return -1;
+  if (buf_ensure(e->part, (int64_t)(tnp_grid(M) + 1) * sizeof(int64_t), s)) return -1;
+  TIMED("span_count", 28.0 * M,
+        launch_span_count(P<int32_t>(e->members), M, grid, zero, idx, P<int32_t>(e->spcnt),
+                          P<int64_t>(e->part), ctr, s));
+  if (scan_counts(e, P<int32_t>(e->spcnt), P<int64_t>(e->spoff), M, CTR_T, s)) return -1;
+  if (read_ctr(e, s)) return -1;
+  if (e->h_ctr[CTR_K0]) {
+    // the reference builds torch.cartesian_prod() of zero tensors (subpoly.py:317)
+    tnp_set_error("meshgrid expects a non-empty TensorList (a region row without zeros, plane %d)", idx);
+    return -1;
+  }
+  const int64_t T = e->h_ctr[CTR_T];
+  const int64_t T1 = std::max<int64_t>(T, 1);
+  if (buf_ensure(e->ekey_a, T1 * sizeof(uint32_t), s)) return -1;
+  if (buf_ensure(e->ekey_b, T1 * sizeof(uint32_t), s)) return -1;
+  if (buf_ensure(e->ent_v, T1 * sizeof(int32_t), s)) return -1;
+  if (buf_ensure(e->eval_b, T1 * sizeof(int32_t), s)) return -1;
+  TIMED("span_emit", 20.0 * M + 8.0 * T,
+        launch_span_emit(P<int32_t>(e->members), M, grid, NC, P<int64_t>(e->spoff),
+                         P<uint32_t>(e->ekey_a), P<int32_t>(e->ent_v), s));
+  int cbits = 1;
+  while (cbits < 32 && (1ll << cbits) < ncell) ++cbits;
+  uint32_t* skey = nullptr;
+  int32_t* sval = nullptr;
+  {
+    size_t need = sort_pairs_scratch_bytes(T, cbits);
+    if (buf_ensure(e->sort_scr2, std::max<size_t>(need, 16), s)) return -1;
+    TIMED("cell_sort", 16.0 * T * ((cbits + 7) / 8),
+          sort_pairs_u32(P<uint32_t>(e->ekey_a), P<uint32_t>(e->ekey_b), P<int32_t>(e->ent_v),
+                         P<int32_t>(e->eval_b), T, cbits, e->sort_scr2.p, e->sort_scr2.bytes, &skey,
+                         &sval, s));
+  }
+  if (buf_ensure(e->celloff, ncell * sizeof(int64_t), s)) return -1;
+  if (buf_ensure(e->cellend, ncell * sizeof(int64_t), s)) return -1;
+  if (buf_ensure(e->cellcnt, ncell * sizeof(int32_t), s)) return -1;
   if (buf_ensure(e->tcnt, ncell * sizeof(int32_t), s)) return -1;
   if (buf_ensure(e->toff, ncell * sizeof(int64_t), s)) return -1;
-  if (launch_cell_tcnt(P<int32_t>(e->cellcnt), ncell, P<int32_t>(e->tcnt), ctr, s)) return -1;
+  TNP_CHECK(hipMemsetAsync(e->celloff.p, 0, ncell * sizeof(int64_t), s));
+  TNP_CHECK(hipMemsetAsync(e->cellend.p, 0, ncell * sizeof(int64_t), s));
+  TIMED("cell_bounds", 12.0 * T,
+        launch_cell_bounds(skey, T, P<int64_t>(e->celloff), P<int64_t>(e->cellend), s));
+  // member pairs per cell -> flattened pair space offsets (total = tests)
+  if (launch_cell_counts(P<int64_t>(e->celloff), P<int64_t>(e->cellend), ncell, P<int32_t>(e->cellcnt),
+                         P<int32_t>(e->tcnt), ctr, s)) return -1;
   if (scan_counts(e, P<int32_t>(e->tcnt), P<int64_t>(e->toff), ncell, CTR_TESTS, s)) return -1;
   if (read_ctr(e, s)) return -1;
   const int64_t TT = e->h_ctr[CTR_TESTS];
@@ -651,20 +691,12 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
                   "(TNP_MAX_PAIR_TESTS)", idx, (long long)TT, (long long)e->max_pair_tests);
     return -1;
   }
-  if (e->h_ctr[CTR_K0]) {
-    // the reference builds torch.cartesian_prod() of zero tensors (subpoly.py:317)
-    tnp_set_error("meshgrid expects a non-empty TensorList (a region row without zeros, plane %d)", idx);
-    return -1;
-  }
-  const int64_t T = e->h_ctr[CTR_T];
-  if (buf_ensure(e->ent_v, std::max<int64_t>(T, 1) * sizeof(int32_t), s)) return -1;
-  if (buf_ensure(e->ent_g, std::max<int64_t>(T, 1) * sizeof(uint64_t), s)) return -1;
-  if (buf_ensure(e->ent_p, std::max<int64_t>(T, 1) * sizeof(uint64_t), s)) return -1;
-  if (buf_ensure(e->ent_z, std::max<int64_t>(T, 1) * sizeof(uint64_t), s)) return -1;
-  TIMED("cell_scatter", 28.0 * M + 32.0 * T,
-        launch_cell_scatter(P<int32_t>(e->members), M, grid, pos, zero, NC, P<int64_t>(e->celloff),
-                            P<int32_t>(e->cellcur), P<int32_t>(e->ent_v), P<uint64_t>(e->ent_g),
-                            P<uint64_t>(e->ent_p), P<uint64_t>(e->ent_z), s));
+  if (buf_ensure(e->ent_g, T1 * sizeof(uint64_t), s)) return -1;
+  if (buf_ensure(e->ent_p, T1 * sizeof(uint64_t), s)) return -1;
+  if (buf_ensure(e->ent_z, T1 * sizeof(uint64_t), s)) return -1;
+  TIMED("entry_keys", 52.0 * T,
+        launch_entry_keys(sval, T, grid, pos, zero, P<uint64_t>(e->ent_g), P<uint64_t>(e->ent_p),
+                          P<uint64_t>(e->ent_z), s));
 
   // 4. connecting edges: test every in-cell member pair once, append the
   //    emitted ones, radix-sort them (lexicographic c_new, subpoly.py:243-244)
@@ -682,7 +714,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     TNP_CHECK(hipMemsetAsync(ctr + CTR_P, 0, 2 * sizeof(int64_t), s));  // CTR_P, CTR_COMPAT
     TIMED("connect", 32.0 * TT + 8.0 * T,
           launch_connect(P<int64_t>(e->toff), P<int32_t>(e->cellcnt), P<int64_t>(e->celloff), ncell,
-                         NC, TT, P<int32_t>(e->bcell), P<int32_t>(e->ent_v), P<uint64_t>(e->ent_g),
+                         NC, TT, P<int32_t>(e->bcell), sval, P<uint64_t>(e->ent_g),
                          P<uint64_t>(e->ent_p), P<uint64_t>(e->ent_z), idx, nb,
                          P<uint64_t>(e->ckeys_a), cap, ctr, P<int64_t>(e->bstat), s));
     if (read_ctr(e, s)) return -1;

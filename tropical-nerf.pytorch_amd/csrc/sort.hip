@@ -1,4 +1,4 @@
-// Ascending radix sort of packed u64 keys (connecting edges lo << nb | hi)
+// Radix sorts: (1) cell bucketing of (cell, member) entries; (2) packed u64 keys (connecting edges lo << nb | hi)
 // on their 2*nb significant bits: the lexicographic order of
 // c_new.sort(-1).unique(dim=0) (subpoly.py:243-244) -- the keys are already
 // unique, one per canonical cell.  rocPRIM's onesweep radix sort is the
@@ -25,5 +25,29 @@ int sort_keys_u64(uint64_t* a, uint64_t* b, int64_t n, int bits, void* scratch, 
   size_t bytes = scratch_bytes;
   TNP_CHECK(rocprim::radix_sort_keys(scratch, bytes, db, (size_t)n, 0u, (unsigned)bits, s));
   *out = db.current();
+  return 0;
+}
+
+size_t sort_pairs_scratch_bytes(int64_t n, int bits) {
+  size_t bytes = 0;
+  rocprim::double_buffer<uint32_t> k(nullptr, nullptr);
+  rocprim::double_buffer<int32_t> v(nullptr, nullptr);
+  if (rocprim::radix_sort_pairs(nullptr, bytes, k, v, (size_t)std::max<int64_t>(n, 1), 0u,
+                                (unsigned)bits) != hipSuccess)
+    return 0;
+  return bytes;
+}
+
+int sort_pairs_u32(uint32_t* ka, uint32_t* kb, int32_t* va, int32_t* vb, int64_t n, int bits,
+                   void* scratch, size_t scratch_bytes, uint32_t** ko, int32_t** vo, hipStream_t s) {
+  *ko = ka;
+  *vo = va;
+  if (n <= 1) return 0;
+  rocprim::double_buffer<uint32_t> k(ka, kb);
+  rocprim::double_buffer<int32_t> v(va, vb);
+  size_t bytes = scratch_bytes;
+  TNP_CHECK(rocprim::radix_sort_pairs(scratch, bytes, k, v, (size_t)n, 0u, (unsigned)bits, s));
+  *ko = k.current();
+  *vo = v.current();
   return 0;
 }

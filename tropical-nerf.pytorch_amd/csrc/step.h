@@ -56,6 +56,18 @@ int launch_cell_scatter(const int32_t* members, int64_t M, const uint64_t* grid,
                         const uint64_t* pos, const uint64_t* zero, int NC, const int64_t* celloff,
                         int32_t* cellcur, int32_t* ent_v, uint64_t* ent_g, uint64_t* ent_p,
                         uint64_t* ent_z, hipStream_t s);
+// sort-based cell bucketing: span counts (+ A), (cell, member) entries,
+// segment bounds of the cell-sorted entries, per-cell counts, key copies
+int launch_span_count(const int32_t* members, int64_t M, const uint64_t* grid, const uint64_t* zero,
+                      int idx, int32_t* cnt, int64_t* part, int64_t* ctr, hipStream_t s);
+int launch_span_emit(const int32_t* members, int64_t M, const uint64_t* grid, int NC,
+                     const int64_t* eoff, uint32_t* ekey, int32_t* eval, hipStream_t s);
+int launch_cell_bounds(const uint32_t* key, int64_t T, int64_t* cstart, int64_t* cend, hipStream_t s);
+int launch_cell_counts(const int64_t* cstart, const int64_t* cend, int64_t n, int32_t* cellcnt,
+                       int32_t* tcnt, int64_t* ctr, hipStream_t s);
+int launch_entry_keys(const int32_t* ent_v, int64_t T, const uint64_t* grid, const uint64_t* pos,
+                      const uint64_t* zero, uint64_t* ent_g, uint64_t* ent_p, uint64_t* ent_z,
+                      hipStream_t s);
 int launch_cell_tcnt(const int32_t* cellcnt, int64_t n, int32_t* tcnt, int64_t* ctr, hipStream_t s);
 int64_t connect_blocks(int64_t TT);
 // connecting-edge test over the flattened pair space; appends packed keys
@@ -69,6 +81,11 @@ int launch_connect(const int64_t* toff, const int32_t* cellcnt, const int64_t* c
 // ascending LSD radix sort of n u64 keys on bits [0, bits); the sorted keys
 // end in *out (== a or b)
 size_t sort_scratch_bytes(int64_t n, int bits);
+size_t sort_pairs_scratch_bytes(int64_t n, int bits);
+// (u32 key, i32 value) pairs ascending by key bits [0, bits); stable; the
+// sorted arrays end in *ko / *vo (== the a or b buffers)
+int sort_pairs_u32(uint32_t* ka, uint32_t* kb, int32_t* va, int32_t* vb, int64_t n, int bits,
+                   void* scratch, size_t scratch_bytes, uint32_t** ko, int32_t** vo, hipStream_t s);
 int sort_keys_u64(uint64_t* a, uint64_t* b, int64_t n, int bits, void* scratch, size_t scratch_bytes,
                   uint64_t** out, hipStream_t s);
 int launch_prune(bool emit, const int32_t* edges, int64_t E, const int32_t* sb, int64_t S,

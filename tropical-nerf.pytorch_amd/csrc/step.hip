@@ -273,6 +273,106 @@ __global__ void k_cell_scatter(const int32_t* __restrict__ members, int64_t M,
       }
 }
 
+// ---- sort-based cell bucketing ---------------------------------------------
+// entries (cell, member) are generated per member in span order, radix-sorted
+// by cell; segment bounds give each cell's member list.  No per-entry
+// atomics (the atomic counting sort they replace serialised on the spatially
+// coherent members of a wave).
+__device__ __forceinline__ int span_cells(uint64_t g, int lo[3], int n[3]) {
+  cell_span(g, lo, n);
+  return n[0] * n[1] * n[2];
+}
+
+// entries per member; per-block sums of the reference's augmented rows (A)
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_span_count(const int32_t* __restrict__ members, int64_t M, const uint64_t* __restrict__ grid,
+             const uint64_t* __restrict__ zero, int idx, int32_t* __restrict__ cnt,
+             int64_t* __restrict__ part, int64_t* __restrict__ ctr) {
+  __shared__ int64_t lds[TNP_WAVES];
+  int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t aug = 0;
+  bool k0 = false;
+  if (m < M) {
+    int v = members[m];
+    int lo[3], n[3];
+    cnt[m] = span_cells(grid[v], lo, n);
+    uint64_t below = (idx >= 64) ? ~0ull : ((1ull << idx) - 1ull);
+    int kz = __popcll(zero[v] & below) + (n[0] - 1) + (n[1] - 1) + (n[2] - 1);
+    aug = 1ll << kz;
+    k0 = kz == 0;
+  }
+  if (__ballot(k0) && tnp::lane() == 0) atomicOr((unsigned long long*)&ctr[CTR_K0], 1ull);
+  int64_t tot;
+  tnp::block_scan_excl(aug, lds, tot);
+  if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_sum_parts(const int64_t* __restrict__ part, int64_t n, int64_t* __restrict__ ctr, int slot) {
+  int64_t a = 0;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) a += part[i];
+  a = tnp::wave_sum(a);
+  if (tnp::lane() == 0 && a) atomicAdd((unsigned long long*)&ctr[slot], (unsigned long long)a);
+}
+
+__global__ void k_span_emit(const int32_t* __restrict__ members, int64_t M,
+                            const uint64_t* __restrict__ grid, int NC,
+                            const int64_t* __restrict__ eoff, uint32_t* __restrict__ ekey,
+                            int32_t* __restrict__ eval) {
+  int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= M) return;
+  int v = members[m];
+  int lo[3], n[3];
+  cell_span(grid[v], lo, n);
+  int64_t p = eoff[m];
+  for (int i = 0; i < n[0]; ++i)
+    for (int j = 0; j < n[1]; ++j)
+      for (int k = 0; k < n[2]; ++k) {
+        ekey[p] = (uint32_t)cell_id(lo[0] + i, lo[1] + j, lo[2] + k, NC);
+        eval[p] = v;
+        ++p;
+      }
+}
+
+// segment [start, end) of every cell in the cell-sorted entries
+__global__ void k_cell_bounds(const uint32_t* __restrict__ key, int64_t T,
+                              int64_t* __restrict__ cstart, int64_t* __restrict__ cend) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= T) return;
+  uint32_t k = key[i];
+  if (i == 0 || key[i - 1] != k) cstart[k] = i;
+  if (i == T - 1 || key[i + 1] != k) cend[k] = i + 1;
+}
+
+// member count and member pairs n (n - 1) / 2 per cell (CTR_BIG: > 65535)
+__global__ void k_cell_counts(const int64_t* __restrict__ cstart, const int64_t* __restrict__ cend,
+                              int64_t n, int32_t* __restrict__ cellcnt, int32_t* __restrict__ tcnt,
+                              int64_t* __restrict__ ctr) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool big = false;
+  if (i < n) {
+    int64_t c = cend[i] - cstart[i];
+    big = c > 65535;
+    cellcnt[i] = (int32_t)c;
+    tcnt[i] = big ? 0 : (int32_t)(c * (c - 1) / 2);
+  }
+  if (__ballot(big) && tnp::lane() == 0) atomicOr((unsigned long long*)&ctr[CTR_BIG], 1ull);
+}
+
+// entry-aligned copies of the members' packed keys (read contiguously per
+// cell by the pair test)
+__global__ void k_entry_keys(const int32_t* __restrict__ ent_v, int64_t T,
+                             const uint64_t* __restrict__ grid, const uint64_t* __restrict__ pos,
+                             const uint64_t* __restrict__ zero, uint64_t* __restrict__ ent_g,
+                             uint64_t* __restrict__ ent_p, uint64_t* __restrict__ ent_z) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= T) return;
+  int v = ent_v[i];
+  ent_g[i] = grid[v];
+  ent_p[i] = pos[v];
+  ent_z[i] = zero[v];
+}
+
 // ---------------------------------------------------------------------------
 // connecting-edge pair test (subpoly.py:484-535 in closed form).
 // Two members share an augmented region iff, per coordinate, their augmented
@@ -677,6 +777,46 @@ int launch_cell_scatter(const int32_t* members, int64_t M, const uint64_t* grid,
   if (M <= 0) return 0;
   hipLaunchKernelGGL(k_cell_scatter, dim3(tnp_grid(M)), dim3(TNP_BLOCK), 0, s, members, M, grid,
                      pos, zero, NC, celloff, cellcur, ent_v, ent_g, ent_p, ent_z);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_span_count(const int32_t* members, int64_t M, const uint64_t* grid, const uint64_t* zero,
+                      int idx, int32_t* cnt, int64_t* part, int64_t* ctr, hipStream_t s) {
+  if (M <= 0) return 0;
+  hipLaunchKernelGGL(k_span_count, dim3(tnp_grid(M)), dim3(TNP_BLOCK), 0, s, members, M, grid, zero,
+                     idx, cnt, part, ctr);
+  hipLaunchKernelGGL(k_sum_parts, dim3(1), dim3(TNP_BLOCK), 0, s, part, (int64_t)tnp_grid(M), ctr,
+                     (int)CTR_A);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_span_emit(const int32_t* members, int64_t M, const uint64_t* grid, int NC,
+                     const int64_t* eoff, uint32_t* ekey, int32_t* eval, hipStream_t s) {
+  if (M <= 0) return 0;
+  hipLaunchKernelGGL(k_span_emit, dim3(tnp_grid(M)), dim3(TNP_BLOCK), 0, s, members, M, grid, NC,
+                     eoff, ekey, eval);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_cell_bounds(const uint32_t* key, int64_t T, int64_t* cstart, int64_t* cend, hipStream_t s) {
+  if (T <= 0) return 0;
+  hipLaunchKernelGGL(k_cell_bounds, dim3(tnp_grid(T)), dim3(TNP_BLOCK), 0, s, key, T, cstart, cend);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_cell_counts(const int64_t* cstart, const int64_t* cend, int64_t n, int32_t* cellcnt,
+                       int32_t* tcnt, int64_t* ctr, hipStream_t s) {
+  hipLaunchKernelGGL(k_cell_counts, dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, cstart, cend, n, cellcnt,
+                     tcnt, ctr);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_entry_keys(const int32_t* ent_v, int64_t T, const uint64_t* grid, const uint64_t* pos,
+                      const uint64_t* zero, uint64_t* ent_g, uint64_t* ent_p, uint64_t* ent_z,
+                      hipStream_t s) {
+  if (T <= 0) return 0;
+  hipLaunchKernelGGL(k_entry_keys, dim3(tnp_grid(T)), dim3(TNP_BLOCK), 0, s, ent_v, T, grid, pos, zero,
+                     ent_g, ent_p, ent_z);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
