@@ -134,12 +134,14 @@ int tnp_engine_active_planes(tnp_engine* eng, int from, uint64_t* mask,
 
 /* subpoly_ phase 1 (subpoly.py:98-117, 180-189): sign test, order-preserving
  * split compaction, new vertices, their forward pass and the LOCAL
- * failover-override predicate.  Writes S (local split count) and fail. */
+ * failover-override predicate.  Writes S (local split count) and fail
+ * (0/1; -1 = left on the device -- single-device flat engines skip that
+ * round trip; pass it on to tnp_engine_finish unchanged). */
 int tnp_engine_split(tnp_engine* eng, int idx, void* stream, int64_t* S,
                      int32_t* fail);
 
 /* subpoly_ phase 2 (subpoly.py:189-279): apply the override if `override`
- * (the GLOBAL predicate), connecting edges, pruning (prune=1) and vertex
+ * (the GLOBAL predicate; -1: the device-resident local one), connecting edges, pruning (prune=1) and vertex
  * compaction.  Must follow tnp_engine_split on the same idx. */
 int tnp_engine_finish(tnp_engine* eng, int idx, int prune, int override,
                       void* stream, tnp_step_stats* stats);

@@ -60,6 +60,18 @@ __device__ __forceinline__ uint64_t wave_or(uint64_t v) {
   return v;
 }
 
+// Sticky flag / bit-mask OR into a device counter word shared by the whole
+// grid.  Same-address atomics serialise in the memory-side atomic unit, so
+// the word is read first (agent scope: sees other XCDs' updates) and the
+// atomic only issued while it would still add a bit -- a mask saturates
+// after a few waves instead of costing one atomic per wave.
+__device__ __forceinline__ void or_sticky(int64_t* p, uint64_t bits) {
+  if (!bits) return;
+  uint64_t cur = __hip_atomic_load(reinterpret_cast<uint64_t*>(p), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+  if (bits & ~cur) atomicOr(reinterpret_cast<unsigned long long*>(p), (unsigned long long)bits);
+}
+
 // Block-wide exclusive rank of a 0/1 flag (order = thread order). Returns
 // the rank; `total` receives the block count. `lds` needs TNP_WAVES ints.
 // Contains two barriers: every thread of the block must call it.

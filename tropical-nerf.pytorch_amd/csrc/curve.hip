@@ -697,7 +697,7 @@ __global__ void k_curve_apply(int64_t B, const int32_t* __restrict__ crow,
     cinfo[r] = 1 | (out ? 2 : 0) | (fabsf(d0) < eps ? 4 : 0);
     tight = fabsf(d0) > eps;
   }
-  if (__ballot(tight) && tnp::lane() == 0) atomicOr((unsigned long long*)&ctr[CTR_TIGHT], 1ull);
+  if (__ballot(tight) && tnp::lane() == 0) tnp::or_sticky(&ctr[CTR_TIGHT], 1ull);
 }
 
 // strict_check (subpoly_debug.py:234-271) after the override

@@ -170,6 +170,10 @@ static int ktimer_begin(tnp_engine* e, const char* name, double bytes, hipStream
   e->kt.push_back(r);
   return (int)e->kt.size() - 1;
 }
+// modelled bytes of the last timed launch, when they depend on its result
+static void ktimer_set_bytes(tnp_engine* e, double bytes) {
+  if (e->kt_on && !e->kt.empty()) e->kt.back().bytes = bytes;
+}
 static void ktimer_end(tnp_engine* e, int t, hipStream_t s) {
   if (t >= 0) (void)hipEventRecord(e->kt[t].b, s);
 }
@@ -581,8 +585,14 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
                     P<uint64_t>(e->cur.pos) + e->V, P<uint64_t>(e->cur.zero) + e->V,
                     P<uint64_t>(e->cur.grid) + e->V, s))
       return -1;
-    if (read_ctr(e, s)) return -1;
-    *fail = e->h_ctr[CTR_FAIL] ? 1 : 0;
+    if (e->curve || e->shards > 1) {
+      // the host takes the global override decision (all-reduce) / the curve
+      // filter needs it: read it back
+      if (read_ctr(e, s)) return -1;
+      *fail = e->h_ctr[CTR_FAIL] ? 1 : 0;
+    } else {
+      *fail = -1;  // single device: the finish kernels read it in place
+    }
   }
   e->pend_dup = S > 0 ? e->h_ctr[CTR_DUP] : 0;
   e->pend_tight = (S > 0 && e->curve) ? (int)e->h_ctr[CTR_TIGHT] : 0;
@@ -614,7 +624,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   // 1. override + keys of the new vertices
   TIMED("finalize_new", (8.0 + 4.0 * K + 4.0 * (K - e->valid_from) + 16.0) * S,
         launch_finalize_new(S, K, override_, P<uint64_t>(e->shared), P<float>(e->stage), eps,
-                            P<float>(c.pre), c.cap, e->valid_from, V, pos, zero, s));
+                            P<float>(c.pre), c.cap, e->valid_from, V, pos, zero, ctr, s));
 
   // 2. members = new vertices ++ hit vertices (ascending)
   int64_t vt = step_tiles(V);
@@ -631,14 +641,13 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   //    (cell, member) entry per spanned cell, radix-sorted by cell
   const int NC = e->net.n_marks + 2;
   const int64_t ncell = (int64_t)NC * NC * NC;
-  if (read_ctr(e, s)) return -1;
-  const int64_t H = V > 0 ? e->h_ctr[CTR_H] : 0;
-  const int64_t M = S + H;
+  const int64_t M = S + V;  // capacity; the kernels read the hit count on the device
+  if (V == 0) TNP_CHECK(hipMemsetAsync(ctr + CTR_H, 0, sizeof(int64_t), s));
   if (buf_ensure(e->spcnt, std::max<int64_t>(M, 1) * sizeof(int32_t), s)) return -1;
   if (buf_ensure(e->spoff, std::max<int64_t>(M, 1) * sizeof(int64_t), s)) return -1;
   if (buf_ensure(e->part, (int64_t)(tnp_grid(M) + 1) * sizeof(int64_t), s)) return -1;
   TIMED("span_count", 28.0 * M,
-        launch_span_count(P<int32_t>(e->members), M, grid, zero, idx, P<int32_t>(e->spcnt),
+        launch_span_count(P<int32_t>(e->members), S, M, grid, zero, idx, P<int32_t>(e->spcnt),
                           P<int64_t>(e->part), ctr, s));
   if (scan_counts(e, P<int32_t>(e->spcnt), P<int64_t>(e->spoff), M, CTR_T, s)) return -1;
   if (read_ctr(e, s)) return -1;
@@ -647,6 +656,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     tnp_set_error("meshgrid expects a non-empty TensorList (a region row without zeros, plane %d)", idx);
     return -1;
   }
+  const int64_t H = e->h_ctr[CTR_H];
   const int64_t T = e->h_ctr[CTR_T];
   const int64_t T1 = std::max<int64_t>(T, 1);
   if (buf_ensure(e->ekey_a, T1 * sizeof(uint32_t), s)) return -1;
@@ -654,8 +664,8 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   if (buf_ensure(e->ent_v, T1 * sizeof(int32_t), s)) return -1;
   if (buf_ensure(e->eval_b, T1 * sizeof(int32_t), s)) return -1;
   TIMED("span_emit", 20.0 * M + 8.0 * T,
-        launch_span_emit(P<int32_t>(e->members), M, grid, NC, P<int64_t>(e->spoff),
-                         P<uint32_t>(e->ekey_a), P<int32_t>(e->ent_v), s));
+        launch_span_emit(P<int32_t>(e->members), S, M, grid, NC, P<int64_t>(e->spoff),
+                         P<uint32_t>(e->ekey_a), P<int32_t>(e->ent_v), ctr, s));
   int cbits = 1;
   while (cbits < 32 && (1ll << cbits) < ncell) ++cbits;
   uint32_t* skey = nullptr;
@@ -681,16 +691,6 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   if (launch_cell_counts(P<int64_t>(e->celloff), P<int64_t>(e->cellend), ncell, P<int32_t>(e->cellcnt),
                          P<int32_t>(e->tcnt), ctr, s)) return -1;
   if (scan_counts(e, P<int32_t>(e->tcnt), P<int64_t>(e->toff), ncell, CTR_TESTS, s)) return -1;
-  if (read_ctr(e, s)) return -1;
-  const int64_t TT = e->h_ctr[CTR_TESTS];
-  if (e->h_ctr[CTR_BIG] || TT > e->max_pair_tests) {
-    // one linear region holding ~sqrt(2*tests) vertices: the reference would
-    // materialise every in-region pair (subpoly.py:505-518) and run out of
-    // memory long before; refuse instead of grinding for hours
-    tnp_set_error("degenerate complex at plane %d: %lld in-cell vertex pairs exceed the limit %lld "
-                  "(TNP_MAX_PAIR_TESTS)", idx, (long long)TT, (long long)e->max_pair_tests);
-    return -1;
-  }
   if (buf_ensure(e->ent_g, T1 * sizeof(uint64_t), s)) return -1;
   if (buf_ensure(e->ent_p, T1 * sizeof(uint64_t), s)) return -1;
   if (buf_ensure(e->ent_z, T1 * sizeof(uint64_t), s)) return -1;
@@ -699,29 +699,53 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
                           P<uint64_t>(e->ent_z), s));
 
   // 4. connecting edges: test every in-cell member pair once, append the
-  //    emitted ones, radix-sort them (lexicographic c_new, subpoly.py:243-244)
+  //    emitted ones, radix-sort them (lexicographic c_new, subpoly.py:243-244).
+  //    The pair count stays on the device; the chunk table and the key buffer
+  //    keep their capacity across steps and grow (then redo) on overflow.
   int nb = 1;
   while (nb < 31 && (1ll << nb) < NV) ++nb;
-  const int64_t nblk = connect_blocks(TT);
-  if (buf_ensure(e->bcell, std::max<int64_t>(nblk, 1) * sizeof(int32_t), s)) return -1;
-  if (buf_ensure(e->bstat, std::max<int64_t>(nblk, 1) * 2 * sizeof(int64_t), s)) return -1;
-  int64_t cap = std::max<int64_t>(e->ckeys_a.bytes / sizeof(uint64_t), std::min<int64_t>(TT, 4 * M + 1024));
-  cap = std::min<int64_t>(cap, std::max<int64_t>(TT, 1));
-  int64_t X = 0;
-  for (int attempt = 0; attempt < 2; ++attempt) {
+  if (buf_ensure(e->bstat, 2 * connect_grid() * sizeof(int64_t), s)) return -1;
+  int64_t bcap = std::max<int64_t>(e->bcell.bytes / sizeof(int32_t), 4096);
+  int64_t cap = std::max<int64_t>(e->ckeys_a.bytes / sizeof(uint64_t), 4 * M + 1024);
+  int64_t X = 0, TT = 0;
+  bool chunks_ok = false;
+  for (int attempt = 0; attempt < 3; ++attempt) {
+    if (!chunks_ok) {
+      if (buf_ensure(e->bcell, bcap * sizeof(int32_t), s)) return -1;
+      TNP_CHECK(hipMemsetAsync(ctr + CTR_BOVF, 0, sizeof(int64_t), s));
+      if (launch_chunk_cells(P<int64_t>(e->toff), P<int32_t>(e->tcnt), ncell, P<int32_t>(e->bcell),
+                             bcap, ctr, s)) return -1;
+    }
     if (buf_ensure(e->ckeys_a, std::max<int64_t>(cap, 1) * sizeof(uint64_t), s)) return -1;
     TNP_CHECK(hipMemsetAsync(ctr + CTR_X, 0, sizeof(int64_t), s));
     TNP_CHECK(hipMemsetAsync(ctr + CTR_P, 0, 2 * sizeof(int64_t), s));  // CTR_P, CTR_COMPAT
-    TIMED("connect", 32.0 * TT + 8.0 * T,
+    TIMED("connect", 0.0,
           launch_connect(P<int64_t>(e->toff), P<int32_t>(e->cellcnt), P<int64_t>(e->celloff), ncell,
-                         NC, TT, P<int32_t>(e->bcell), sval, P<uint64_t>(e->ent_g),
+                         NC, e->max_pair_tests, P<int32_t>(e->bcell), sval, P<uint64_t>(e->ent_g),
                          P<uint64_t>(e->ent_p), P<uint64_t>(e->ent_z), idx, nb,
                          P<uint64_t>(e->ckeys_a), cap, ctr, P<int64_t>(e->bstat), s));
     if (read_ctr(e, s)) return -1;
+    TT = e->h_ctr[CTR_TESTS];
     X = e->h_ctr[CTR_X];
+    ktimer_set_bytes(e, 32.0 * TT + 8.0 * T);  // known only now
+    if (e->h_ctr[CTR_BIG] || TT > e->max_pair_tests) {
+      // one linear region holding ~sqrt(2*tests) vertices: the reference would
+      // materialise every in-region pair (subpoly.py:505-518) and run out of
+      // memory long before; refuse instead of grinding for hours
+      tnp_set_error("degenerate complex at plane %d: %lld in-cell vertex pairs exceed the limit %lld "
+                    "(TNP_MAX_PAIR_TESTS)", idx, (long long)TT, (long long)e->max_pair_tests);
+      return -1;
+    }
+    if (e->h_ctr[CTR_BOVF]) {  // chunk table too small: grow, remap, redo
+      bcap = connect_chunks(TT) + 1;
+      chunks_ok = false;
+      continue;
+    }
+    chunks_ok = true;
     if (X <= cap) break;
     cap = X;  // appended beyond the buffer: grow to the exact count and redo
   }
+  if (e->h_ctr[CTR_BOVF] || X > cap) { tnp_set_error("connect: capacity retry failed"); return -1; }
   if (e->h_ctr[CTR_COMPAT] == 0 && e->shards <= 1) {
     // every region has a single member: extract_every_valid_edge cats an
     // empty list (subpoly.py:505-513)
@@ -794,7 +818,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     st->A = e->h_ctr[CTR_A];
     st->P = e->h_ctr[CTR_P];
     st->pair_tests = e->h_ctr[CTR_TESTS];
-    st->override_applied = override_;
+    st->override_applied = override_ < 0 ? (e->h_ctr[CTR_FAIL] != 0) : override_;
     st->next_active = (uint64_t)e->h_ctr[CTR_ACTIVE];
     st->S_dup = e->pend_dup;
   }

@@ -28,6 +28,7 @@ enum {
   CTR_NOPLANE = 20, // curve path: a c row with no shared plane below idx
   CTR_TIGHT = 21,   // curve path: a kept c row misses its edge plane by > eps
   CTR_KEEP = 22,    // curve path: splits surviving the strict filter
+  CTR_BOVF = 23,    // pair-chunk table overflow
   CTR_N = 24
 };
 
@@ -46,22 +47,20 @@ int launch_fail_check(const int32_t* sa, const int32_t* sb, int64_t S, int idx,
                       int64_t* ctr, hipStream_t s);
 int launch_finalize_new(int64_t S, int K, int override_, const uint64_t* shared, float* stage,
                         float eps, float* pre, int64_t ld, int keep_from, int64_t V, uint64_t* pos,
-                        uint64_t* zero, hipStream_t s);
+                        uint64_t* zero, const int64_t* ctr, hipStream_t s);
 int launch_hit_count(const float* col, int64_t V, float eps, int32_t* blk, hipStream_t s);
 int launch_hit_emit(const float* col, int64_t V, float eps, const int64_t* blkoff,
                     int32_t* members, int64_t S, hipStream_t s);
-int launch_cell_count(const int32_t* members, int64_t M, const uint64_t* grid, const uint64_t* zero,
-                      int idx, int NC, int32_t* cellcnt, int64_t* ctr, hipStream_t s);
-int launch_cell_scatter(const int32_t* members, int64_t M, const uint64_t* grid,
-                        const uint64_t* pos, const uint64_t* zero, int NC, const int64_t* celloff,
-                        int32_t* cellcur, int32_t* ent_v, uint64_t* ent_g, uint64_t* ent_p,
-                        uint64_t* ent_z, hipStream_t s);
 // sort-based cell bucketing: span counts (+ A), (cell, member) entries,
 // segment bounds of the cell-sorted entries, per-cell counts, key copies
-int launch_span_count(const int32_t* members, int64_t M, const uint64_t* grid, const uint64_t* zero,
-                      int idx, int32_t* cnt, int64_t* part, int64_t* ctr, hipStream_t s);
-int launch_span_emit(const int32_t* members, int64_t M, const uint64_t* grid, int NC,
-                     const int64_t* eoff, uint32_t* ekey, int32_t* eval, hipStream_t s);
+// M = capacity (S + V); the live member count S + ctr[CTR_H] is read on
+// the device (no host round trip for the hit count)
+int launch_span_count(const int32_t* members, int64_t S, int64_t M, const uint64_t* grid,
+                      const uint64_t* zero, int idx, int32_t* cnt, int64_t* part, int64_t* ctr,
+                      hipStream_t s);
+int launch_span_emit(const int32_t* members, int64_t S, int64_t M, const uint64_t* grid, int NC,
+                     const int64_t* eoff, uint32_t* ekey, int32_t* eval, const int64_t* ctr,
+                     hipStream_t s);
 int launch_cell_bounds(const uint32_t* key, int64_t T, int64_t* cstart, int64_t* cend, hipStream_t s);
 int launch_cell_counts(const int64_t* cstart, const int64_t* cend, int64_t n, int32_t* cellcnt,
                        int32_t* tcnt, int64_t* ctr, hipStream_t s);
@@ -69,14 +68,20 @@ int launch_entry_keys(const int32_t* ent_v, int64_t T, const uint64_t* grid, con
                       const uint64_t* zero, uint64_t* ent_g, uint64_t* ent_p, uint64_t* ent_z,
                       hipStream_t s);
 int launch_cell_tcnt(const int32_t* cellcnt, int64_t n, int32_t* tcnt, int64_t* ctr, hipStream_t s);
-int64_t connect_blocks(int64_t TT);
-// connecting-edge test over the flattened pair space; appends packed keys
-// (lo << nb | hi) to keys[0, cap) and counts them in ctr[CTR_X]
+// connecting edges over the flattened pair space (cell-major, then (i, j<i));
+// the pair count is read on the device (ctr[CTR_TESTS]).  chunk_cells maps
+// pair chunks to cells (capacity cap chunks, overflow -> CTR_BOVF); connect
+// appends packed keys (lo << nb | hi) to keys[0, cap) and counts them in
+// ctr[CTR_X]; bstat needs 2 * connect_grid() slots.
+int64_t connect_chunks(int64_t TT);
+int64_t connect_grid();
+int launch_chunk_cells(const int64_t* toff, const int32_t* tcnt, int64_t ncell, int32_t* bcell,
+                       int64_t cap, int64_t* ctr, hipStream_t s);
 int launch_connect(const int64_t* toff, const int32_t* cellcnt, const int64_t* celloff,
-                   int64_t ncell, int NC, int64_t TT, int32_t* bcell, const int32_t* ent_v,
-                   const uint64_t* ent_g, const uint64_t* ent_p, const uint64_t* ent_z, int idx,
-                   int nb, uint64_t* keys, int64_t cap, int64_t* ctr, int64_t* bstat,
-                   hipStream_t s);
+                   int64_t ncell, int NC, int64_t max_tests, const int32_t* bcell,
+                   const int32_t* ent_v, const uint64_t* ent_g, const uint64_t* ent_p,
+                   const uint64_t* ent_z, int idx, int nb, uint64_t* keys, int64_t cap,
+                   int64_t* ctr, int64_t* bstat, hipStream_t s);
 // ---- sort.hip ----
 // ascending LSD radix sort of n u64 keys on bits [0, bits); the sorted keys
 // end in *out (== a or b)

@@ -91,9 +91,16 @@ k_split_emit(int32_t* __restrict__ edges, int64_t E, const float* __restrict__ c
     }
     run += tot;
   }
-  if (dup_mark >= 0) {
+  if (dup_mark >= 0) {  // one atomic per block
     dup = tnp::wave_sum(dup);
-    if (tnp::lane() == 0 && dup) atomicAdd((unsigned long long*)&ctr[CTR_DUP], (unsigned long long)dup);
+    __syncthreads();
+    if (tnp::lane() == 0) lds[tnp::wave()] = dup;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int t = 0;
+      for (int w = 0; w < TNP_WAVES; ++w) t += lds[w];
+      if (t) atomicAdd((unsigned long long*)&ctr[CTR_DUP], (unsigned long long)t);
+    }
   }
 }
 
@@ -135,18 +142,20 @@ __global__ void k_fail_check(const int32_t* __restrict__ sa, const int32_t* __re
       bad |= fabsf(stage[(int64_t)p * S + r]) > eps;
     }
   }
-  if (__ballot(bad) && tnp::lane() == 0) atomicOr((unsigned long long*)&ctr[CTR_FAIL], 1ull);
+  if (__ballot(bad) && tnp::lane() == 0) tnp::or_sticky(&ctr[CTR_FAIL], 1ull);
 }
 
 // override (masked_fill_ on the shared planes, subpoly_debug.py:48), packed
 // keys of the final pre-activations, live planes copied into the cache.
+// override_ < 0: the (single-device) predicate is still in ctr[CTR_FAIL]
 __global__ void k_finalize_new(int64_t S, int K, int override_, const uint64_t* __restrict__ shared,
                                float* __restrict__ stage, float eps, float* __restrict__ pre,
                                int64_t ld, int keep_from, int64_t V, uint64_t* __restrict__ pos,
-                               uint64_t* __restrict__ zero) {
+                               uint64_t* __restrict__ zero, const int64_t* __restrict__ ctr) {
   int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= S) return;
-  uint64_t m = override_ ? shared[r] : 0ull;
+  const bool ov = override_ < 0 ? ctr[CTR_FAIL] != 0 : override_ != 0;
+  uint64_t m = ov ? shared[r] : 0ull;
   uint64_t ps = 0, zs = 0;
   for (int p = 0; p < K; ++p) {
     float v = stage[(int64_t)p * S + r];
@@ -221,58 +230,6 @@ __device__ __forceinline__ int64_t cell_id(int cx, int cy, int cz, int NC) {
   return ((int64_t)(cx + 2) * NC + (cy + 2)) * NC + (cz + 2);
 }
 
-__global__ void k_cell_count(const int32_t* __restrict__ members, int64_t M,
-                             const uint64_t* __restrict__ grid, const uint64_t* __restrict__ zero,
-                             int idx, int NC, int32_t* __restrict__ cellcnt,
-                             int64_t* __restrict__ ctr) {
-  int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  int64_t aug = 0;
-  bool k0 = false;
-  if (m < M) {
-    int v = members[m];
-    uint64_t g = grid[v];
-    int lo[3], n[3];
-    cell_span(g, lo, n);
-    for (int i = 0; i < n[0]; ++i)
-      for (int j = 0; j < n[1]; ++j)
-        for (int k = 0; k < n[2]; ++k)
-          atomicAdd(&cellcnt[cell_id(lo[0] + i, lo[1] + j, lo[2] + k, NC)], 1);
-    uint64_t below = (idx >= 64) ? ~0ull : ((1ull << idx) - 1ull);
-    int kz = __popcll(zero[v] & below) + (n[0] - 1) + (n[1] - 1) + (n[2] - 1);
-    aug = 1ll << kz;
-    k0 = kz == 0;
-  }
-  aug = tnp::wave_sum(aug);
-  if (tnp::lane() == 0) atomicAdd((unsigned long long*)&ctr[CTR_A], (unsigned long long)aug);
-  if (__ballot(k0) && tnp::lane() == 0) atomicOr((unsigned long long*)&ctr[CTR_K0], 1ull);
-}
-
-// bucket every (member, spanned cell) entry; the member's packed keys are
-// copied entry-aligned so the pair test reads them contiguously per cell
-__global__ void k_cell_scatter(const int32_t* __restrict__ members, int64_t M,
-                               const uint64_t* __restrict__ grid, const uint64_t* __restrict__ pos,
-                               const uint64_t* __restrict__ zero, int NC,
-                               const int64_t* __restrict__ celloff, int32_t* __restrict__ cellcur,
-                               int32_t* __restrict__ ent_v, uint64_t* __restrict__ ent_g,
-                               uint64_t* __restrict__ ent_p, uint64_t* __restrict__ ent_z) {
-  int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (m >= M) return;
-  int v = members[m];
-  uint64_t g = grid[v], ps = pos[v], zs = zero[v];
-  int lo[3], n[3];
-  cell_span(g, lo, n);
-  for (int i = 0; i < n[0]; ++i)
-    for (int j = 0; j < n[1]; ++j)
-      for (int k = 0; k < n[2]; ++k) {
-        int64_t c = cell_id(lo[0] + i, lo[1] + j, lo[2] + k, NC);
-        int64_t p = celloff[c] + atomicAdd(&cellcur[c], 1);
-        ent_v[p] = v;
-        ent_g[p] = g;
-        ent_p[p] = ps;
-        ent_z[p] = zs;
-      }
-}
-
 // ---- sort-based cell bucketing ---------------------------------------------
 // entries (cell, member) are generated per member in span order, radix-sorted
 // by cell; segment bounds give each cell's member list.  No per-entry
@@ -285,13 +242,15 @@ __device__ __forceinline__ int span_cells(uint64_t g, int lo[3], int n[3]) {
 
 // entries per member; per-block sums of the reference's augmented rows (A)
 __global__ void __launch_bounds__(TNP_BLOCK)
-k_span_count(const int32_t* __restrict__ members, int64_t M, const uint64_t* __restrict__ grid,
-             const uint64_t* __restrict__ zero, int idx, int32_t* __restrict__ cnt,
-             int64_t* __restrict__ part, int64_t* __restrict__ ctr) {
+k_span_count(const int32_t* __restrict__ members, int64_t S, int64_t Mcap,
+             const uint64_t* __restrict__ grid, const uint64_t* __restrict__ zero, int idx,
+             int32_t* __restrict__ cnt, int64_t* __restrict__ part, int64_t* __restrict__ ctr) {
   __shared__ int64_t lds[TNP_WAVES];
+  const int64_t M = S + ctr[CTR_H];  // members = splits ++ hits (device count)
   int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int64_t aug = 0;
   bool k0 = false;
+  if (m < Mcap) cnt[m] = 0;
   if (m < M) {
     int v = members[m];
     int lo[3], n[3];
@@ -315,10 +274,11 @@ k_sum_parts(const int64_t* __restrict__ part, int64_t n, int64_t* __restrict__ c
   if (tnp::lane() == 0 && a) atomicAdd((unsigned long long*)&ctr[slot], (unsigned long long)a);
 }
 
-__global__ void k_span_emit(const int32_t* __restrict__ members, int64_t M,
+__global__ void k_span_emit(const int32_t* __restrict__ members, int64_t S,
                             const uint64_t* __restrict__ grid, int NC,
                             const int64_t* __restrict__ eoff, uint32_t* __restrict__ ekey,
-                            int32_t* __restrict__ eval) {
+                            int32_t* __restrict__ eval, const int64_t* __restrict__ ctr) {
+  const int64_t M = S + ctr[CTR_H];
   int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= M) return;
   int v = members[m];
@@ -441,14 +401,6 @@ __device__ __forceinline__ int64_t upper_bound_i64(const int64_t* __restrict__ a
 constexpr int CIPT = 8;                 // consecutive pair indices per thread
 constexpr int CCH = TNP_BLOCK * CIPT;   // pair indices per block
 
-// cell holding the first pair index of every connect block
-__global__ void k_block_cells(const int64_t* __restrict__ toff, int64_t ncell, int64_t nblk,
-                              int32_t* __restrict__ bcell) {
-  int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= nblk) return;
-  bcell[b] = (int32_t)(upper_bound_i64(toff, 0, ncell, b * (int64_t)CCH) - 1);
-}
-
 __device__ __forceinline__ void cell_coords(int64_t cell, int NC, int cc[3]) {
   cc[2] = (int)(cell % NC) - 2;
   cc[1] = (int)((cell / NC) % NC) - 2;
@@ -463,21 +415,42 @@ __device__ __forceinline__ void cell_coords(int64_t cell, int NC, int cc[3]) {
 // are packed (lo << nb | hi) and appended block-contiguously through ONE
 // atomic per block; their order is restored by the radix sort that follows,
 // so the appended order never reaches the output.
+// chunk b of the pair space starts in cell bcell[b] (written per cell: no
+// host round trip for the pair count)
+__global__ void k_chunk_cells(const int64_t* __restrict__ toff, const int32_t* __restrict__ tcnt,
+                              int64_t ncell, int32_t* __restrict__ bcell, int64_t cap,
+                              int64_t* __restrict__ ctr) {
+  int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= ncell) return;
+  int64_t n = tcnt[c];
+  if (n == 0) return;
+  int64_t lo = toff[c];
+  int64_t b0 = (lo + CCH - 1) / CCH, b1 = (lo + n + CCH - 1) / CCH;
+  if (b1 > cap) atomicOr((unsigned long long*)&ctr[CTR_BOVF], 1ull);
+  for (int64_t b = b0; b < b1 && b < cap; ++b) bcell[b] = (int32_t)c;
+}
+
+// Persistent over the chunks of the pair space (count read on the device);
+// stops at once if the complex is degenerate (pairs above the limit) or the
+// chunk table overflowed -- the host reports either after the fact.
 __global__ void __launch_bounds__(TNP_BLOCK)
 k_connect(const int64_t* __restrict__ toff, const int32_t* __restrict__ cellcnt,
-          const int64_t* __restrict__ celloff, int64_t ncell, int NC, int64_t TT,
-          const int32_t* __restrict__ bcell, int64_t nblk, const int32_t* __restrict__ ent_v,
+          const int64_t* __restrict__ celloff, int64_t ncell, int NC, int64_t max_tests,
+          const int32_t* __restrict__ bcell, const int32_t* __restrict__ ent_v,
           const uint64_t* __restrict__ ent_g, const uint64_t* __restrict__ ent_p,
           const uint64_t* __restrict__ ent_z, int idx, int nb, uint64_t* __restrict__ keys,
           int64_t cap, int64_t* __restrict__ ctr, int64_t* __restrict__ bstat) {
   __shared__ int64_t lds[TNP_WAVES];
   __shared__ int64_t s_base;
-  const int64_t b = blockIdx.x;
-  const int64_t p0 = b * (int64_t)CCH + (int64_t)threadIdx.x * CIPT;
+  const int64_t TT = ctr[CTR_TESTS];
+  if (TT > max_tests || ctr[CTR_BOVF] || ctr[CTR_BIG]) return;
+  const int64_t nblk = (TT + CCH - 1) / CCH;
   const uint64_t below = (idx >= 64) ? ~0ull : ((1ull << idx) - 1ull);
+  int64_t n_compat = 0, n_reg = 0;
+  for (int64_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+  const int64_t p0 = b * (int64_t)CCH + (int64_t)threadIdx.x * CIPT;
   uint64_t kk[CIPT];
   int ne = 0;
-  int64_t n_compat = 0, n_reg = 0;
   if (p0 < TT) {
     const int64_t c_end = (b + 1 < nblk) ? (int64_t)bcell[b + 1] + 1 : ncell;
     int64_t c = upper_bound_i64(toff, bcell[b], c_end, p0) - 1;
@@ -536,12 +509,12 @@ k_connect(const int64_t* __restrict__ toff, const int32_t* __restrict__ cellcnt,
   const int64_t w0 = s_base + off;
   for (int k = 0; k < ne; ++k)
     if (w0 + k < cap) keys[w0 + k] = kk[k];
-  int64_t tc = tnp::block_scan_excl(n_compat, lds, tot);
-  (void)tc;
-  if (threadIdx.x == 0) bstat[2 * b] = tot;
-  int64_t tr = tnp::block_scan_excl(n_reg, lds, tot);
-  (void)tr;
-  if (threadIdx.x == 0) bstat[2 * b + 1] = tot;
+  }
+  int64_t tot;
+  tnp::block_scan_excl(n_compat, lds, tot);
+  if (threadIdx.x == 0) bstat[2 * blockIdx.x] = tot;
+  tnp::block_scan_excl(n_reg, lds, tot);
+  if (threadIdx.x == 0) bstat[2 * blockIdx.x + 1] = tot;
 }
 
 // per-block (compatible pairs, shared regions) -> ctr[CTR_COMPAT], ctr[CTR_P]
@@ -657,7 +630,7 @@ k_prune_emit(EdgeSrc src, int64_t N, uint64_t fmask, uint64_t amask,
     }
   }
   act = tnp::wave_or(act);
-  if (tnp::lane() == 0 && act) atomicOr((unsigned long long*)&ctr[CTR_ACTIVE], act);
+  if (tnp::lane() == 0) tnp::or_sticky(&ctr[CTR_ACTIVE], act);
 }
 
 __global__ void k_gather_vertices(const int32_t* __restrict__ used, const int64_t* __restrict__ nid,
@@ -696,7 +669,7 @@ __global__ void k_active_planes(const int32_t* __restrict__ edges, int64_t E, ui
     act = (pos[a] ^ pos[b]) & ~zero[a] & ~zero[b] & amask;
   }
   act = tnp::wave_or(act);
-  if (tnp::lane() == 0 && act) atomicOr((unsigned long long*)&ctr[CTR_ACTIVE], act);
+  if (tnp::lane() == 0) tnp::or_sticky(&ctr[CTR_ACTIVE], act);
 }
 
 }  // namespace
@@ -740,10 +713,10 @@ int launch_fail_check(const int32_t* sa, const int32_t* sb, int64_t S, int idx,
 }
 int launch_finalize_new(int64_t S, int K, int override_, const uint64_t* shared, float* stage,
                         float eps, float* pre, int64_t ld, int keep_from, int64_t V, uint64_t* pos,
-                        uint64_t* zero, hipStream_t s) {
+                        uint64_t* zero, const int64_t* ctr, hipStream_t s) {
   if (S <= 0) return 0;
   hipLaunchKernelGGL(k_finalize_new, dim3(tnp_grid(S)), dim3(TNP_BLOCK), 0, s, S, K, override_,
-                     shared, stage, eps, pre, ld, keep_from, V, pos, zero);
+                     shared, stage, eps, pre, ld, keep_from, V, pos, zero, ctr);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
@@ -762,39 +735,23 @@ int launch_hit_emit(const float* col, int64_t V, float eps, const int64_t* blkof
   TNP_CHECK(hipGetLastError());
   return 0;
 }
-int launch_cell_count(const int32_t* members, int64_t M, const uint64_t* grid, const uint64_t* zero,
-                      int idx, int NC, int32_t* cellcnt, int64_t* ctr, hipStream_t s) {
+int launch_span_count(const int32_t* members, int64_t S, int64_t M, const uint64_t* grid,
+                      const uint64_t* zero, int idx, int32_t* cnt, int64_t* part, int64_t* ctr,
+                      hipStream_t s) {
   if (M <= 0) return 0;
-  hipLaunchKernelGGL(k_cell_count, dim3(tnp_grid(M)), dim3(TNP_BLOCK), 0, s, members, M, grid,
-                     zero, idx, NC, cellcnt, ctr);
-  TNP_CHECK(hipGetLastError());
-  return 0;
-}
-int launch_cell_scatter(const int32_t* members, int64_t M, const uint64_t* grid,
-                        const uint64_t* pos, const uint64_t* zero, int NC, const int64_t* celloff,
-                        int32_t* cellcur, int32_t* ent_v, uint64_t* ent_g, uint64_t* ent_p,
-                        uint64_t* ent_z, hipStream_t s) {
-  if (M <= 0) return 0;
-  hipLaunchKernelGGL(k_cell_scatter, dim3(tnp_grid(M)), dim3(TNP_BLOCK), 0, s, members, M, grid,
-                     pos, zero, NC, celloff, cellcur, ent_v, ent_g, ent_p, ent_z);
-  TNP_CHECK(hipGetLastError());
-  return 0;
-}
-int launch_span_count(const int32_t* members, int64_t M, const uint64_t* grid, const uint64_t* zero,
-                      int idx, int32_t* cnt, int64_t* part, int64_t* ctr, hipStream_t s) {
-  if (M <= 0) return 0;
-  hipLaunchKernelGGL(k_span_count, dim3(tnp_grid(M)), dim3(TNP_BLOCK), 0, s, members, M, grid, zero,
-                     idx, cnt, part, ctr);
+  hipLaunchKernelGGL(k_span_count, dim3(tnp_grid(M)), dim3(TNP_BLOCK), 0, s, members, S, M, grid,
+                     zero, idx, cnt, part, ctr);
   hipLaunchKernelGGL(k_sum_parts, dim3(1), dim3(TNP_BLOCK), 0, s, part, (int64_t)tnp_grid(M), ctr,
                      (int)CTR_A);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
-int launch_span_emit(const int32_t* members, int64_t M, const uint64_t* grid, int NC,
-                     const int64_t* eoff, uint32_t* ekey, int32_t* eval, hipStream_t s) {
+int launch_span_emit(const int32_t* members, int64_t S, int64_t M, const uint64_t* grid, int NC,
+                     const int64_t* eoff, uint32_t* ekey, int32_t* eval, const int64_t* ctr,
+                     hipStream_t s) {
   if (M <= 0) return 0;
-  hipLaunchKernelGGL(k_span_emit, dim3(tnp_grid(M)), dim3(TNP_BLOCK), 0, s, members, M, grid, NC,
-                     eoff, ekey, eval);
+  hipLaunchKernelGGL(k_span_emit, dim3(tnp_grid(M)), dim3(TNP_BLOCK), 0, s, members, S, grid, NC,
+                     eoff, ekey, eval, ctr);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
@@ -825,23 +782,28 @@ int launch_cell_tcnt(const int32_t* cellcnt, int64_t n, int32_t* tcnt, int64_t* 
   TNP_CHECK(hipGetLastError());
   return 0;
 }
-int64_t connect_blocks(int64_t TT) { return (TT + CCH - 1) / CCH; }
-int launch_connect(const int64_t* toff, const int32_t* cellcnt, const int64_t* celloff,
-                   int64_t ncell, int NC, int64_t TT, int32_t* bcell, const int32_t* ent_v,
-                   const uint64_t* ent_g, const uint64_t* ent_p, const uint64_t* ent_z, int idx,
-                   int nb, uint64_t* keys, int64_t cap, int64_t* ctr, int64_t* bstat,
-                   hipStream_t s) {
-  if (TT <= 0) return 0;
-  int64_t nblk = connect_blocks(TT);
-  hipLaunchKernelGGL(k_block_cells, dim3(tnp_grid(nblk)), dim3(TNP_BLOCK), 0, s, toff, ncell, nblk,
-                     bcell);
-  hipLaunchKernelGGL(k_connect, dim3((unsigned)nblk), dim3(TNP_BLOCK), 0, s, toff, cellcnt, celloff,
-                     ncell, NC, TT, bcell, nblk, ent_v, ent_g, ent_p, ent_z, idx, nb, keys, cap,
-                     ctr, bstat);
-  hipLaunchKernelGGL(k_sum_bstat, dim3(1), dim3(TNP_BLOCK), 0, s, bstat, nblk, ctr);
+constexpr int CONNECT_GRID = 2048;  // persistent blocks (8 per CU)
+int64_t connect_chunks(int64_t TT) { return (TT + CCH - 1) / CCH; }
+int launch_chunk_cells(const int64_t* toff, const int32_t* tcnt, int64_t ncell, int32_t* bcell,
+                       int64_t cap, int64_t* ctr, hipStream_t s) {
+  hipLaunchKernelGGL(k_chunk_cells, dim3(tnp_grid(ncell)), dim3(TNP_BLOCK), 0, s, toff, tcnt, ncell,
+                     bcell, cap, ctr);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
+int launch_connect(const int64_t* toff, const int32_t* cellcnt, const int64_t* celloff,
+                   int64_t ncell, int NC, int64_t max_tests, const int32_t* bcell,
+                   const int32_t* ent_v, const uint64_t* ent_g, const uint64_t* ent_p,
+                   const uint64_t* ent_z, int idx, int nb, uint64_t* keys, int64_t cap,
+                   int64_t* ctr, int64_t* bstat, hipStream_t s) {
+  hipLaunchKernelGGL(k_connect, dim3(CONNECT_GRID), dim3(TNP_BLOCK), 0, s, toff, cellcnt, celloff,
+                     ncell, NC, max_tests, bcell, ent_v, ent_g, ent_p, ent_z, idx, nb, keys, cap, ctr,
+                     bstat);
+  hipLaunchKernelGGL(k_sum_bstat, dim3(1), dim3(TNP_BLOCK), 0, s, bstat, (int64_t)CONNECT_GRID, ctr);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int64_t connect_grid() { return CONNECT_GRID; }
 int launch_prune(bool emit, const int32_t* edges, int64_t E, const int32_t* sb, int64_t S,
                  int64_t V, const uint64_t* ckeys, int nb, int64_t X, int idx,
                  int prune, int last_plane, const uint64_t* pos, const uint64_t* zero,

@@ -122,7 +122,7 @@ class Engine:
         S, fail = C.c_int64(), C.c_int32()
         _hip.check(_hip.lib().tnp_engine_split(self.h, idx, self._s, C.byref(S), C.byref(fail)),
                    "tnp_engine_split")
-        return S.value, bool(fail.value)
+        return S.value, int(fail.value)  # -1: left on the device (single-device flat)
 
     def finish(self, idx: int, prune: bool, override: bool) -> dict:
         st = _hip.TnpStepStats()
@@ -164,7 +164,7 @@ class Engine:
             S, fail = self.split(idx)
             if allreduce is not None:
                 g = allreduce(np.array([S, int(fail)], dtype=np.int64), "max")
-                S_glob, fail = int(g[0]), bool(g[1])
+                S_glob, fail = int(g[0]), int(g[1])
             else:
                 S_glob = S
             if S_glob == 0:
