@@ -35,6 +35,20 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# per-kernel HBM bytes per launch from the committed rocprofv3 --pmc passes
+# (tools/pmc_summary.py: 2*FETCH_SIZE + WRITE_SIZE, gfx950 correction)
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01_bench128_seed6_pmc_traffic.json")
+
+
+def pmc_traffic(kernel: str, marks: int, seed: int):
+    """HBM traffic per launch of `kernel` measured by the PMC passes of the
+    same workload, or None (other workload, or no profile)."""
+    if marks != 128 or seed != 6 or not os.path.isfile(PMC_TRAFFIC):
+        return None
+    with open(PMC_TRAFFIC) as f:
+        ks = json.load(f)["kernels"]
+    k = ks.get("k_" + kernel)
+    return None if k is None else k["traffic_bytes_per_launch"]
 
 
 def synthetic_params(G: int, seed: int = 0, amp: float = 0.1):
@@ -116,40 +130,52 @@ def cpu_baseline(sample_marks: int, seed: int, threads: int):
     return S / dt, S, dt, Vs
 
 
-def small_net_check(dev):
+def small_net_check(dev, force: bool = True):
     """The metric's named config at bunny scale: the stand-in small net
     (levels=4, r 2..32, 49 marks; fitted to a sphere, committed fixture),
-    flat path, end to end through the drop-in subpoly() on the GPU vs the
-    oracle on the host -- splits/s both ways and Chamfer-L2 of the surfaces
-    (chamfer_distance.py:39-48 formula)."""
+    end to end through the drop-in subpoly() on the GPU.  force=True (flat,
+    configs[0]) is checked against the oracle run live on the host (splits/s
+    both ways); force=False (curve-approx on, configs[1]) against the golden
+    produced by the reference itself.  Chamfer-L2 of the surfaces uses the
+    chamfer_distance.py:39-48 formula."""
     import io
     import contextlib
-    import oracle.subdivide as od
     import tropical.subpoly as sp
     from golden_io import load
     from helpers import oracle_net, product_net
-    d = load("small_sphere")
+    name = "small_sphere" if force else "small_sphere_curve"
+    d = load(name)
     net = product_net(d, dev)
     stats = []
     with contextlib.redirect_stdout(io.StringIO()):
-        sp.subpoly(net, 3, 1.2, force=True)  # warm
+        sp.subpoly(net, 3, 1.2, force=force)  # warm
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
-        _, verts, tri = sp.subpoly(net, 3, 1.2, force=True, stats=stats)
+        faces, verts, tri = sp.subpoly(net, 3, 1.2, force=force, stats=stats)
         torch.cuda.synchronize(dev)
         t_gpu = time.perf_counter() - t0
-        ref = oracle_net(d)
-        st = {}
-        t0 = time.perf_counter()
-        with torch.no_grad():
-            _, rv, rtri = od.subpoly(ref, 3, 1.2, 1e-4, True, stats=st)
-        t_cpu = time.perf_counter() - t0
-    S = sum(s["S"] for s in stats)
-    return {"config": "stand-in bunny small net (sphere-fitted, 49 marks), flat, subpoly() end to end",
-            "edges_subdivided": int(S), "gpu_s": round(t_gpu, 4), "cpu_s": round(t_cpu, 3),
-            "gpu_edges_per_s": round(S / t_gpu, 1), "cpu_edges_per_s": round(S / t_cpu, 1),
-            "chamfer_l2_vs_ref": chamfer(verts.cpu().numpy(), rv.numpy()),
-            "faces_bit_exact": bool(np.array_equal(np.asarray(tri), np.asarray(rtri)))}
+        out = {"config": f"stand-in bunny small net (sphere-fitted, 49 marks), "
+                         f"{'flat' if force else 'curve-approx on'}, subpoly() end to end"}
+        S = sum(s["S"] for s in stats)
+        out.update({"edges_subdivided": int(S), "gpu_s": round(t_gpu, 4),
+                    "gpu_edges_per_s": round(S / t_gpu, 1)})
+        if force:
+            import oracle.subdivide as od
+            ref = oracle_net(d)
+            st = {}
+            t0 = time.perf_counter()
+            with torch.no_grad():
+                _, rv, rtri = od.subpoly(ref, 3, 1.2, 1e-4, True, stats=st)
+            t_cpu = time.perf_counter() - t0
+            rv = rv.numpy()
+            out.update({"cpu_s": round(t_cpu, 3), "cpu_edges_per_s": round(S / t_cpu, 1)})
+        else:
+            rv, rtri = d["surf_V"], d["tri"]
+    v = verts.cpu().numpy()
+    out["chamfer_l2_vs_ref"] = chamfer(v, rv)
+    out["faces_bit_exact"] = bool(np.array_equal(np.asarray(tri), np.asarray(rtri)))
+    out["max_vertex_err"] = float(np.abs(v - rv).max()) if v.shape == rv.shape else None
+    return out
 
 
 def chamfer(a: np.ndarray, b: np.ndarray) -> float:
@@ -249,7 +275,8 @@ def main():
             alg = kt["bytes"] / max(kt["launches"], 1)
             ach = alg / (avg_ms * 1e-3) / 1e9
             roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                    "traffic": pmc_traffic(dom, G, args.seed) if world == 1 else None,
                     "avg_launch_us": round(avg_ms * 1e3, 2), "launches": kt["launches"],
                     "alg_bytes_per_launch": int(alg)}
         loop_gbs = bytes_tot / dt_max / 1e9
@@ -279,7 +306,8 @@ def main():
                           f"{args.cpu_sample_marks}^3: {S_cpu} splits in {t_cpu:.1f}s"}
             out["gpu_over_cpu"] = round(value / cps, 1)
         if not args.no_cpu and world == 1:
-            out["small_net"] = small_net_check(dev)
+            out["small_net"] = small_net_check(dev, force=True)
+            out["small_net_curve"] = small_net_check(dev, force=False)
             engine_for(net)  # restore
         print(json.dumps(out), flush=True)
     if world > 1:
