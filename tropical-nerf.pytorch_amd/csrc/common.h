@@ -110,6 +110,80 @@ __device__ __forceinline__ int64_t block_scan_excl(int64_t v, int64_t* lds, int6
 }
 
 // ---------------------------------------------------------------------------
+// Single-pass ordered compaction / scan: decoupled look-back over tiles.
+// Tiles are numbered by a ticket taken at block start (so every tile a block
+// waits on belongs to a block that is already running: no co-residency
+// assumption).  One 64-bit status word per tile holds
+//   bits 63..62 flag (1 = tile aggregate, 2 = inclusive prefix)
+//   bits 61..40 launch epoch (22 bits: stale words of earlier launches never match)
+//   bits 39..0  value
+// so a single relaxed agent-scope atomic load observes a consistent record.
+// The ticket counter is never reset: the host passes the count already issued.
+// ---------------------------------------------------------------------------
+struct TnpLB {
+  unsigned long long* ticket;
+  uint64_t* st;
+  uint64_t tbase;
+  uint32_t epoch;
+};
+
+__device__ __forceinline__ int64_t lb_tile(const TnpLB& lb, int64_t* slot) {
+  if (threadIdx.x == 0) *slot = (int64_t)(atomicAdd(lb.ticket, 1ull) - lb.tbase);
+  __syncthreads();
+  int64_t t = *slot;
+  __syncthreads();
+  return t;
+}
+
+// exclusive prefix of tile `tile` whose aggregate is `agg` (block-uniform);
+// publishes the tile's inclusive prefix.  All threads call it.
+__device__ __forceinline__ int64_t lb_prefix(const TnpLB& lb, int64_t tile, int64_t agg,
+                                             int64_t* slot) {
+  constexpr uint64_t VMASK = (1ull << 40) - 1ull;
+  const uint64_t tag = (uint64_t)(lb.epoch & 0x3FFFFFu) << 40;
+  if (threadIdx.x < 64) {
+    int64_t prefix = 0;
+    if (tile == 0) {
+      if (lane() == 0)
+        __hip_atomic_store(&lb.st[0], (2ull << 62) | tag | (uint64_t)agg, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      if (lane() == 0)
+        __hip_atomic_store(&lb.st[tile], (1ull << 62) | tag | (uint64_t)agg, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      int64_t w = tile - 1;
+      while (true) {
+        const int64_t t = w - lane();
+        uint64_t word = 0;
+        int flag = 2;  // before tile 0: an inclusive zero
+        if (t >= 0) {
+          while (true) {
+            word = __hip_atomic_load(&lb.st[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            flag = ((word & (0x3FFFFFull << 40)) == tag) ? (int)(word >> 62) : 0;
+            if (flag) break;
+            __builtin_amdgcn_s_sleep(1);
+          }
+        }
+        const uint64_t incl = __ballot(flag == 2);
+        const int first = incl ? __builtin_ctzll(incl) : 64;
+        int64_t v = (lane() <= first && t >= 0) ? (int64_t)(word & VMASK) : 0;
+        prefix += wave_sum(v);
+        if (incl) break;
+        w -= 64;
+      }
+      if (lane() == 0)
+        __hip_atomic_store(&lb.st[tile], (2ull << 62) | tag | (uint64_t)(prefix + agg),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (threadIdx.x == 0) *slot = prefix;
+  }
+  __syncthreads();
+  int64_t r = *slot;
+  __syncthreads();
+  return r;
+}
+
+// ---------------------------------------------------------------------------
 // Packed per-vertex grid word (cell offsets + on-grid-plane flags).
 //   bits  0..15  offset x + 2      bits 48..50 zero flag per dim (on a mark)
 //   bits 16..31  offset y + 2
@@ -124,3 +198,5 @@ __device__ __forceinline__ bool grid_zero(uint64_t g, int d) {
 }
 
 }  // namespace tnp
+
+using tnp::TnpLB;

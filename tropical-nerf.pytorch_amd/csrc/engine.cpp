@@ -135,6 +135,13 @@ struct tnp_engine {
   int64_t V = 0, E = 0;
   int keep_all = 0;
   int valid_from = 0;  // pre planes [valid_from, K) are valid for every vertex
+  // Lazy compaction: during the hot loop vertex ids are SLOTS (V = slots in
+  // use); pruned vertices stay in place, flagged dead in `used` (the live
+  // flags).  Slot order == the reference's compacted id order (compaction
+  // preserves ascending ids), so every id-ordered result is unchanged;
+  // compact_now() renumbers once, before anything exports or reads ids.
+  bool dirty = false;
+  int64_t V_live = 0;
   // step scratch
   Buf spcnt, spoff, part, ekey_a, ekey_b, eval_b, cellend, sort_scr2;
   Buf blk, blkoff, scan_scr, sa, sb, stage, shared, members, cellcnt, cellcur, celloff, ent_v,
@@ -145,9 +152,13 @@ struct tnp_engine {
   // pending split
   int pend_idx = -1;
   int64_t pend_S = 0, pend_dup = 0;
+  bool pend_fused = false;  // the pending split ran k_forward_new (flat path)
   // faces output
   Buf tri, faces;
   int64_t n_tri = 0, n_faces = 0, dbg_F = 0, dbg_W = 0;
+  Buf lb;                  // look-back state: [0] ticket counter, [1..] tile status words
+  uint64_t lb_tickets = 0;  // tickets issued so far
+  uint32_t lb_epoch = 0;
   Buf fscr[12];
   Buf fscr2[32];
   Buf cv[CV_N];
@@ -184,11 +195,33 @@ static void ktimer_end(tnp_engine* e, int t, hipStream_t s) {
     ktimer_end(e, _t, s);                                          \
   } while (0)
 
+// look-back state for a single-pass launch of `tiles` tiles (common.h TnpLB)
+static int lb_begin(tnp_engine* e, int64_t tiles, hipStream_t s, TnpLB* out) {
+  size_t need = (size_t)(tiles + 1) * sizeof(uint64_t);
+  if (need > e->lb.bytes || !e->lb.p) {
+    if (buf_ensure(e->lb, std::max(need, (size_t)64 << 10), s)) return -1;
+    TNP_CHECK(hipMemsetAsync(e->lb.p, 0, e->lb.bytes, s));  // flag 0: no record
+    e->lb_tickets = 0;
+  }
+  e->lb_epoch = (e->lb_epoch + 1) & 0x3FFFFFu;
+  if (e->lb_epoch == 0) {  // wrapped: clear records that could carry a reused epoch
+    TNP_CHECK(hipMemsetAsync(e->lb.p, 0, e->lb.bytes, s));
+    e->lb_tickets = 0;
+    e->lb_epoch = 1;
+  }
+  out->ticket = static_cast<unsigned long long*>(e->lb.p);
+  out->st = static_cast<uint64_t*>(e->lb.p) + 1;
+  out->tbase = e->lb_tickets;
+  out->epoch = e->lb_epoch;
+  e->lb_tickets += (uint64_t)tiles;
+  return 0;
+}
+
 static int scan_counts(tnp_engine* e, const int32_t* in, int64_t* out, int64_t n, int slot,
                        hipStream_t s) {
-  if (buf_ensure(e->scan_scr, scan_scratch_bytes(n), s)) return -1;
-  TIMED("scan", 16.0 * n,
-        scan_i32_to_i64(in, out, n, P<int64_t>(e->ctr) + slot, e->scan_scr.p, e->scan_scr.bytes, s));
+  TnpLB lb;
+  if (n > 0 && lb_begin(e, scan_tiles(n), s, &lb)) return -1;
+  TIMED("scan", 12.0 * n, scan_i32_to_i64(in, out, n, P<int64_t>(e->ctr) + slot, lb, s));
   return 0;
 }
 
@@ -227,6 +260,49 @@ static int keys_for(tnp_engine* e, VSet& v, int64_t from, int64_t n, hipStream_t
                      P<uint64_t>(v.grid) + from, s);
 }
 
+// live flags of slots [from, from + n) := 1 (kept capacity: earlier flags stay)
+static int set_alive(tnp_engine* e, int64_t from, int64_t n, hipStream_t s) {
+  if (buf_ensure(e->used, std::max<int64_t>(from + n, 1) * sizeof(int32_t), s, true)) return -1;
+  if (n > 0) TNP_CHECK(hipMemsetD32Async((hipDeviceptr_t)(P<int32_t>(e->used) + from), 1, n, s));
+  return 0;
+}
+
+// a freshly loaded complex: every slot live, ids dense
+static int reset_live(tnp_engine* e, hipStream_t s) {
+  e->dirty = false;
+  e->V_live = e->V;
+  return set_alive(e, 0, e->V, s);
+}
+
+// renumber the live slots densely (the reference's per-step compaction,
+// subpoly.py:266-277, done once): scan of the live flags, gather of the
+// vertex rows (planes >= valid_from), edge remap
+static int compact_now(tnp_engine* e, hipStream_t s) {
+  if (!e->dirty) return 0;
+  const int64_t NV = e->V;
+  if (buf_ensure(e->nid, std::max<int64_t>(NV, 1) * sizeof(int64_t), s)) return -1;
+  if (scan_counts(e, P<int32_t>(e->used), P<int64_t>(e->nid), NV, CTR_AUX, s)) return -1;
+  if (vset_ensure(e, e->alt, NV, 0, s)) return -1;
+  VSet& c = e->cur;
+  VSet& a = e->alt;
+  TIMED("gather_vertices", 4.0 * NV + 2.0 * (12 + 4.0 * (e->K - e->valid_from) + 24) * e->V_live,
+        launch_gather_vertices(P<int32_t>(e->used), P<int64_t>(e->nid), NV, e->K, e->valid_from,
+                               P<float>(c.xyz), P<float>(c.pre), c.cap, P<uint64_t>(c.pos),
+                               P<uint64_t>(c.zero), P<uint64_t>(c.grid), P<float>(a.xyz),
+                               P<float>(a.pre), a.cap, P<uint64_t>(a.pos), P<uint64_t>(a.zero),
+                               P<uint64_t>(a.grid), s));
+  TIMED("remap_edges", 32.0 * e->E, launch_remap_edges(P<int32_t>(e->edges), e->E, P<int64_t>(e->nid), s));
+  if (read_ctr(e, s)) return -1;
+  const int64_t V2 = e->h_ctr[CTR_AUX];
+  if (V2 != e->V_live) {
+    tnp_set_error("compaction: %lld live slots, %lld expected", (long long)V2, (long long)e->V_live);
+    return -1;
+  }
+  std::swap(e->cur, e->alt);
+  e->V = V2;
+  return reset_live(e, s);
+}
+
 // ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
@@ -257,7 +333,7 @@ extern "C" void tnp_engine_destroy(tnp_engine* e) {
                  &e->stage, &e->shared, &e->members, &e->cellcnt, &e->cellcur, &e->celloff,
                  &e->ent_v, &e->ent_g, &e->ent_p, &e->ent_z, &e->tcnt, &e->toff, &e->bcell,
                  &e->bstat, &e->ckeys_a, &e->ckeys_b, &e->sort_scr, &e->flags, &e->used, &e->nid,
-                 &e->ctr, &e->tri, &e->faces};
+                 &e->ctr, &e->tri, &e->faces, &e->lb};
   for (Buf* b : bufs) buf_free(*b, s);
   for (Buf& b : e->fscr) buf_free(b, s);
   for (Buf& b : e->fscr2) buf_free(b, s);
@@ -369,11 +445,11 @@ extern "C" int tnp_engine_load(tnp_engine* e, const float* d_xyz, int64_t V, con
   e->keep_all = keep_all;
   e->valid_from = 0;
   e->pend_idx = -1;
-  return 0;
+  return reset_live(e, s);
 }
 
 extern "C" int tnp_engine_sizes(tnp_engine* e, int64_t* V, int64_t* E) {
-  *V = e->V;
+  *V = e->V_live;
   *E = e->E;
   return 0;
 }
@@ -547,44 +623,51 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
   const float eps = e->net.eps;
   const float* col = P<float>(e->cur.pre) + (int64_t)idx * e->cur.cap;
   TNP_CHECK(hipMemsetAsync(e->ctr.p, 0, CTR_N * sizeof(int64_t), s));
-  int64_t tiles = step_tiles(e->E);
-  if (buf_ensure(e->blk, (tiles + 1) * sizeof(int32_t), s)) return -1;
-  if (buf_ensure(e->blkoff, (tiles + 1) * sizeof(int64_t), s)) return -1;
   int64_t S = 0;
   if (e->E > 0) {
-    TIMED("split_count", 16.0 * e->E, launch_split_count(P<int32_t>(e->edges), e->E, col, eps, P<int32_t>(e->blk), s));
-    if (scan_counts(e, P<int32_t>(e->blk), P<int64_t>(e->blkoff), tiles, CTR_S, s)) return -1;
+    // single pass; the id buffers hold the upper bound E (capacity is kept)
+    if (buf_ensure(e->sa, e->E * sizeof(int32_t), s)) return -1;
+    if (buf_ensure(e->sb, e->E * sizeof(int32_t), s)) return -1;
+    if (e->curve && buf_ensure(e->cv[CV_EIDX], e->E * sizeof(int32_t), s)) return -1;
+    TnpLB lb;
+    if (lb_begin(e, lb_tiles(e->E), s, &lb)) return -1;
+    TIMED("split", 16.0 * e->E,
+          launch_split_lb(P<int32_t>(e->edges), e->E, col, eps, e->V, P<int32_t>(e->sa),
+                          P<int32_t>(e->sb), e->dup_mark, P<uint64_t>(e->cur.grid), P<int64_t>(e->ctr),
+                          e->curve ? P<int32_t>(e->cv[CV_EIDX]) : nullptr, lb, s));
     if (read_ctr(e, s)) return -1;
     S = e->h_ctr[CTR_S];
   }
   *fail = 0;
   if (S > 0) {
-    if (buf_ensure(e->sa, S * sizeof(int32_t), s)) return -1;
-    if (buf_ensure(e->sb, S * sizeof(int32_t), s)) return -1;
-    if (e->curve && buf_ensure(e->cv[CV_EIDX], S * sizeof(int32_t), s)) return -1;
-    TIMED("split_emit", 16.0 * e->E + 12.0 * S,
-          launch_split_emit(P<int32_t>(e->edges), e->E, col, eps, P<int64_t>(e->blkoff), e->V,
-                            P<int32_t>(e->sa), P<int32_t>(e->sb), e->dup_mark,
-                            P<uint64_t>(e->cur.grid), P<int64_t>(e->ctr),
-                            e->curve ? P<int32_t>(e->cv[CV_EIDX]) : nullptr, s));
     if (vset_ensure(e, e->cur, e->V + S, e->V, s)) return -1;
     col = P<float>(e->cur.pre) + (int64_t)idx * e->cur.cap;  // may have moved
     TIMED("new_vertices", 52.0 * S,
           launch_new_vertices(P<int32_t>(e->sa), P<int32_t>(e->sb), S, col, eps, P<float>(e->cur.xyz),
                               e->V, s));
     if (e->curve && curve_correct(e, idx, S, s)) return -1;
-    if (buf_ensure(e->stage, (size_t)S * e->K * sizeof(float), s)) return -1;
     if (buf_ensure(e->shared, S * sizeof(uint64_t), s)) return -1;
-    TIMED("forward", (12.0 + 4.0 * e->K) * S,
-          launch_forward(e->net, P<float>(e->cur.xyz) + 3 * e->V, S, P<float>(e->stage), S, 1, s));
-    TIMED("fail_check", 40.0 * S,
-          launch_fail_check(P<int32_t>(e->sa), P<int32_t>(e->sb), S, idx, P<uint64_t>(e->cur.zero),
-                            P<float>(e->stage), eps, P<uint64_t>(e->shared), P<int64_t>(e->ctr), s));
-    // grid words of the new vertices (coordinates are final)
-    if (launch_keys(e->net, P<float>(e->cur.xyz) + 3 * e->V, P<float>(e->stage), S, S, 0,
-                    P<uint64_t>(e->cur.pos) + e->V, P<uint64_t>(e->cur.zero) + e->V,
-                    P<uint64_t>(e->cur.grid) + e->V, s))
-      return -1;
+    e->pend_fused = !e->curve;
+    if (e->pend_fused) {
+      // flat: forward + failover test + keys in one pass, straight into the cache
+      TIMED("forward_new", (12.0 + 8.0 + 4.0 * (e->K - e->valid_from) + 32.0) * S,
+            launch_forward_new(e->net, P<float>(e->cur.xyz) + 3 * e->V, S, P<float>(e->cur.pre),
+                               e->cur.cap, e->V, e->valid_from, P<int32_t>(e->sa), P<int32_t>(e->sb),
+                               idx, P<uint64_t>(e->cur.pos), P<uint64_t>(e->cur.zero),
+                               P<uint64_t>(e->cur.grid), P<uint64_t>(e->shared), P<int64_t>(e->ctr), s));
+    } else {
+      if (buf_ensure(e->stage, (size_t)S * e->K * sizeof(float), s)) return -1;
+      TIMED("forward", (12.0 + 4.0 * e->K) * S,
+            launch_forward(e->net, P<float>(e->cur.xyz) + 3 * e->V, S, P<float>(e->stage), S, 1, s));
+      TIMED("fail_check", 40.0 * S,
+            launch_fail_check(P<int32_t>(e->sa), P<int32_t>(e->sb), S, idx, P<uint64_t>(e->cur.zero),
+                              P<float>(e->stage), eps, P<uint64_t>(e->shared), P<int64_t>(e->ctr), s));
+      // grid words of the new vertices (coordinates are final)
+      if (launch_keys(e->net, P<float>(e->cur.xyz) + 3 * e->V, P<float>(e->stage), S, S, 0,
+                      P<uint64_t>(e->cur.pos) + e->V, P<uint64_t>(e->cur.zero) + e->V,
+                      P<uint64_t>(e->cur.grid) + e->V, s))
+        return -1;
+    }
     if (e->curve || e->shards > 1) {
       // the host takes the global override decision (all-reduce) / the curve
       // filter needs it: read it back
@@ -622,27 +705,30 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   uint64_t* grid = P<uint64_t>(c.grid);
 
   // 1. override + keys of the new vertices
-  TIMED("finalize_new", (8.0 + 4.0 * K + 4.0 * (K - e->valid_from) + 16.0) * S,
-        launch_finalize_new(S, K, override_, P<uint64_t>(e->shared), P<float>(e->stage), eps,
-                            P<float>(c.pre), c.cap, e->valid_from, V, pos, zero, ctr, s));
-
-  // 2. members = new vertices ++ hit vertices (ascending)
-  int64_t vt = step_tiles(V);
-  if (buf_ensure(e->blk, (vt + 1) * sizeof(int32_t), s)) return -1;
-  if (buf_ensure(e->blkoff, (vt + 1) * sizeof(int64_t), s)) return -1;
-  if (buf_ensure(e->members, std::max<int64_t>(NV, 1) * sizeof(int32_t), s)) return -1;
-  if (V > 0) {
-    TIMED("hit_count", 4.0 * V, launch_hit_count(col, V, eps, P<int32_t>(e->blk), s));
-    if (scan_counts(e, P<int32_t>(e->blk), P<int64_t>(e->blkoff), vt, CTR_H, s)) return -1;
+  if (e->pend_fused) {
+    TIMED("override_new", 8.0 * S,
+          launch_override_new(S, override_, P<uint64_t>(e->shared), P<float>(c.pre), c.cap,
+                              e->valid_from, V, pos, zero, ctr, s));
+  } else {
+    TIMED("finalize_new", (8.0 + 4.0 * K + 4.0 * (K - e->valid_from) + 16.0) * S,
+          launch_finalize_new(S, K, override_, P<uint64_t>(e->shared), P<float>(e->stage), eps,
+                              P<float>(c.pre), c.cap, e->valid_from, V, pos, zero, ctr, s));
   }
-  TIMED("hit_emit", 4.0 * V + 4.0 * S, launch_hit_emit(col, V, eps, P<int64_t>(e->blkoff), P<int32_t>(e->members), S, s));
+
+  // 2. members = new vertices ++ live hit vertices (ascending)
+  if (buf_ensure(e->members, std::max<int64_t>(NV, 1) * sizeof(int32_t), s)) return -1;
+  {
+    TnpLB lb;
+    if (V > 0 && lb_begin(e, lb_tiles(V), s, &lb)) return -1;
+    TIMED("hits", 8.0 * V + 4.0 * S,
+          launch_hits(col, P<int32_t>(e->used), V, eps, P<int32_t>(e->members), S, ctr, lb, s));
+  }
 
   // 3. bucket members by grid cell (dense cell grid over the marks): one
   //    (cell, member) entry per spanned cell, radix-sorted by cell
   const int NC = e->net.n_marks + 2;
   const int64_t ncell = (int64_t)NC * NC * NC;
   const int64_t M = S + V;  // capacity; the kernels read the hit count on the device
-  if (V == 0) TNP_CHECK(hipMemsetAsync(ctr + CTR_H, 0, sizeof(int64_t), s));
   if (buf_ensure(e->spcnt, std::max<int64_t>(M, 1) * sizeof(int32_t), s)) return -1;
   if (buf_ensure(e->spoff, std::max<int64_t>(M, 1) * sizeof(int64_t), s)) return -1;
   if (buf_ensure(e->part, (int64_t)(tnp_grid(M) + 1) * sizeof(int64_t), s)) return -1;
@@ -704,7 +790,10 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   //    keep their capacity across steps and grow (then redo) on overflow.
   int nb = 1;
   while (nb < 31 && (1ll << nb) < NV) ++nb;
-  if (buf_ensure(e->bstat, 2 * connect_grid() * sizeof(int64_t), s)) return -1;
+  if (buf_ensure(e->bstat, 3 * connect_grid() * sizeof(int64_t), s)) return -1;
+  // connecting edges this step's pruning drops are never appended (sorted,
+  // re-tested): keep_edge() depends on the endpoints only
+  const uint64_t cfmask = prune ? prune_mask(idx, K - 1) : 0ull;
   int64_t bcap = std::max<int64_t>(e->bcell.bytes / sizeof(int32_t), 4096);
   int64_t cap = std::max<int64_t>(e->ckeys_a.bytes / sizeof(uint64_t), 4 * M + 1024);
   int64_t X = 0, TT = 0;
@@ -712,21 +801,24 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   for (int attempt = 0; attempt < 3; ++attempt) {
     if (!chunks_ok) {
       if (buf_ensure(e->bcell, bcap * sizeof(int32_t), s)) return -1;
-      TNP_CHECK(hipMemsetAsync(ctr + CTR_BOVF, 0, sizeof(int64_t), s));
+      if (attempt > 0) TNP_CHECK(hipMemsetAsync(ctr + CTR_BOVF, 0, sizeof(int64_t), s));
       if (launch_chunk_cells(P<int64_t>(e->toff), P<int32_t>(e->tcnt), ncell, P<int32_t>(e->bcell),
                              bcap, ctr, s)) return -1;
     }
     if (buf_ensure(e->ckeys_a, std::max<int64_t>(cap, 1) * sizeof(uint64_t), s)) return -1;
-    TNP_CHECK(hipMemsetAsync(ctr + CTR_X, 0, sizeof(int64_t), s));
-    TNP_CHECK(hipMemsetAsync(ctr + CTR_P, 0, 2 * sizeof(int64_t), s));  // CTR_P, CTR_COMPAT
+    if (attempt > 0) {  // the split zeroed the whole counter block
+      TNP_CHECK(hipMemsetAsync(ctr + CTR_X, 0, sizeof(int64_t), s));
+      TNP_CHECK(hipMemsetAsync(ctr + CTR_XK, 0, sizeof(int64_t), s));
+      TNP_CHECK(hipMemsetAsync(ctr + CTR_P, 0, 2 * sizeof(int64_t), s));  // CTR_P, CTR_COMPAT
+    }
     TIMED("connect", 0.0,
           launch_connect(P<int64_t>(e->toff), P<int32_t>(e->cellcnt), P<int64_t>(e->celloff), ncell,
                          NC, e->max_pair_tests, P<int32_t>(e->bcell), sval, P<uint64_t>(e->ent_g),
-                         P<uint64_t>(e->ent_p), P<uint64_t>(e->ent_z), idx, nb,
+                         P<uint64_t>(e->ent_p), P<uint64_t>(e->ent_z), idx, nb, cfmask,
                          P<uint64_t>(e->ckeys_a), cap, ctr, P<int64_t>(e->bstat), s));
     if (read_ctr(e, s)) return -1;
     TT = e->h_ctr[CTR_TESTS];
-    X = e->h_ctr[CTR_X];
+    X = e->h_ctr[CTR_XK];
     ktimer_set_bytes(e, 32.0 * TT + 8.0 * T);  // known only now
     if (e->h_ctr[CTR_BIG] || TT > e->max_pair_tests) {
       // one linear region holding ~sqrt(2*tests) vertices: the reference would
@@ -767,52 +859,47 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   if (buf_ensure(e->blk, (nt + 1) * sizeof(int32_t), s)) return -1;
   if (buf_ensure(e->blkoff, (nt + 1) * sizeof(int64_t), s)) return -1;
   if (buf_ensure(e->edges_alt, std::max<int64_t>(N, 1) * 2 * sizeof(int32_t), s)) return -1;
-  TNP_CHECK(hipMemsetAsync(ctr + CTR_ACTIVE, 0, sizeof(int64_t), s));
+  // ctr[CTR_ACTIVE] and ctr[CTR_V] are still zero from the split's reset
   const int32_t* eg = P<int32_t>(e->edges);
   int64_t V2 = NV, E2 = N;
   int next_valid = e->valid_from;
   if (prune) {
+    // live flags recomputed from the kept edges; no vertex moves (lazy
+    // compaction): the distinct flagged count is the reference's V'
     if (buf_ensure(e->used, std::max<int64_t>(NV, 1) * sizeof(int32_t), s)) return -1;
-    if (buf_ensure(e->nid, std::max<int64_t>(NV, 1) * sizeof(int64_t), s)) return -1;
     TNP_CHECK(hipMemsetAsync(e->used.p, 0, NV * sizeof(int32_t), s));
-    TIMED("prune_count", 40.0 * N,
-          launch_prune(false, eg, E, P<int32_t>(e->sb), S, V, e->ckeys, nb, X, idx, 1, K - 1, pos, zero, P<int32_t>(e->blk),
-                       nullptr, nullptr, nullptr, ctr, s));
-    if (scan_counts(e, P<int32_t>(e->blk), P<int64_t>(e->blkoff), nt, CTR_E, s)) return -1;
-    TIMED("prune_emit", 40.0 * N,
-          launch_prune(true, eg, E, P<int32_t>(e->sb), S, V, e->ckeys, nb, X, idx, 1, K - 1, pos, zero, nullptr,
-                       P<int64_t>(e->blkoff), P<int32_t>(e->edges_alt), P<int32_t>(e->used), ctr, s));
-    if (scan_counts(e, P<int32_t>(e->used), P<int64_t>(e->nid), NV, CTR_V, s)) return -1;
+    TnpLB lb;
+    if (lb_begin(e, lb_tiles(N), s, &lb)) return -1;
+    TIMED("prune", 40.0 * N,
+          launch_prune_lb(eg, E, P<int32_t>(e->sb), S, V, e->ckeys, nb, X, idx, K - 1, pos, zero,
+                          P<int32_t>(e->edges_alt), P<int32_t>(e->used), ctr, lb, s));
+    TIMED("count_live", 4.0 * NV, launch_count_flags(P<int32_t>(e->used), NV, ctr, CTR_V, s));
     next_valid = e->keep_all ? 0 : std::min(idx + 1, K - 1);
-    if (vset_ensure(e, e->alt, NV, 0, s)) return -1;
-    VSet& a = e->alt;
-    TIMED("gather_vertices", 4.0 * NV + 2.0 * (12 + 4.0 * (K - next_valid) + 24) * NV,
-          launch_gather_vertices(P<int32_t>(e->used), P<int64_t>(e->nid), NV, K, next_valid,
-                                 P<float>(c.xyz), P<float>(c.pre), c.cap, pos, zero, grid,
-                                 P<float>(a.xyz), P<float>(a.pre), a.cap, P<uint64_t>(a.pos),
-                                 P<uint64_t>(a.zero), P<uint64_t>(a.grid), s));
     if (read_ctr(e, s)) return -1;
     E2 = e->h_ctr[CTR_E];
     V2 = e->h_ctr[CTR_V];
-    TIMED("remap_edges", 32.0 * E2, launch_remap_edges(P<int32_t>(e->edges_alt), E2, P<int64_t>(e->nid), s));
-    std::swap(e->cur, e->alt);
+    e->dirty = true;
   } else {
     if (launch_prune(true, eg, E, P<int32_t>(e->sb), S, V, e->ckeys, nb, X, idx, 0, K - 1, pos, zero, nullptr, nullptr,
                      P<int32_t>(e->edges_alt), nullptr, ctr, s))
       return -1;
+    if (set_alive(e, V, S, s)) return -1;
+    V2 = e->V_live + S;
     if (read_ctr(e, s)) return -1;
   }
   std::swap(e->edges, e->edges_alt);
-  e->V = V2;
+  const int64_t V_in_live = e->V_live;
+  e->V = NV;  // slots
+  e->V_live = V2;
   e->E = E2;
   e->valid_from = next_valid;
   if (st) {
     st->idx = idx;
-    st->V_in = V;
+    st->V_in = V_in_live;
     st->E_in = E;
     st->S = S;
     st->H = H;
-    st->X = X;
+    st->X = e->h_ctr[CTR_X];  // all connecting edges (X kept ones were appended)
     st->V_out = V2;
     st->E_out = E2;
     st->A = e->h_ctr[CTR_A];
@@ -829,6 +916,7 @@ extern "C" int tnp_engine_export(tnp_engine* e, float* d_xyz, int64_t* d_edges, 
                                  void* stream) {
   hipStream_t s = (hipStream_t)stream;
   TNP_CHECK(hipSetDevice(e->device));
+  if (compact_now(e, s)) return -1;
   if (d_xyz && e->V > 0)
     TNP_CHECK(hipMemcpyAsync(d_xyz, e->cur.xyz.p, e->V * 3 * sizeof(float), hipMemcpyDeviceToDevice, s));
   if (d_edges && e->E > 0)
@@ -850,6 +938,7 @@ extern "C" int tnp_engine_export(tnp_engine* e, float* d_xyz, int64_t* d_edges, 
 extern "C" int tnp_engine_surface(tnp_engine* e, void* stream, int64_t* V_out, int64_t* E_out) {
   hipStream_t s = (hipStream_t)stream;
   TNP_CHECK(hipSetDevice(e->device));
+  if (compact_now(e, s)) return -1;
   const int64_t V = e->V, E = e->E;
   VSet& c = e->cur;
   const float* col = P<float>(c.pre) + (int64_t)(e->K - 1) * c.cap;
@@ -866,7 +955,7 @@ extern "C" int tnp_engine_surface(tnp_engine* e, void* stream, int64_t* V_out, i
     e->E = 0;
     *V_out = 0;
     *E_out = 0;
-    return 0;
+    return reset_live(e, s);
   }
   int64_t nt = step_tiles(E);
   if (buf_ensure(e->blk, (nt + 1) * sizeof(int32_t), s)) return -1;
@@ -899,7 +988,7 @@ extern "C" int tnp_engine_surface(tnp_engine* e, void* stream, int64_t* V_out, i
   e->E = E2;
   *V_out = V2;
   *E_out = E2;
-  return 0;
+  return reset_live(e, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -974,7 +1063,7 @@ extern "C" int tnp_engine_lattice(tnp_engine* e, int x0, int x1, int keep_all, v
   e->pend_idx = -1;
   *V_out = V;
   *E_out = E;
-  return 0;
+  return reset_live(e, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -1085,7 +1174,7 @@ extern "C" int tnp_engine_skeleton(tnp_engine* e, int unit, float size, void* st
   e->keep_all = 0;
   *V_out = e->V;
   *E_out = e->E;
-  return 0;
+  return reset_live(e, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -1100,6 +1189,7 @@ enum { FS_TABLE, FS_CNT, FS_KC, FS_KF, FS_MEMOFF, FS_RID, FS_MEM, FS_CUR, FS_ROF
 extern "C" int tnp_engine_faces(tnp_engine* e, void* stream, int64_t* n_tri, int64_t* n_faces) {
   hipStream_t s = (hipStream_t)stream;
   TNP_CHECK(hipSetDevice(e->device));
+  if (compact_now(e, s)) return -1;
   static_assert(FS_N <= 32, "face scratch slots");
   Buf* fs = e->fscr2;
   const int64_t V = e->V;

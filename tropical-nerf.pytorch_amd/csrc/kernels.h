@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include "../../include/tropical_hip.h"
+#include "common.h"
 
 // Net descriptor passed BY VALUE as a kernel argument (lives in SGPRs /
 // the kernarg segment; every field is wave-uniform).
@@ -27,6 +28,16 @@ int net_supported(const NetDev& n);  // 1 if an instantiation exists
 // pre plane-major [K][ld]; rows [0, n)
 int launch_forward(const NetDev& net, const float* xyz, int64_t n, float* pre,
                    int64_t ld, int group, hipStream_t s, float* out2 = nullptr);
+// new vertices of a flat step, forward with the fused epilogue (net.hip
+// k_forward_new): cache planes >= keep_from at slots V.., keys, shared
+// planes, failover predicate -> ctr[CTR_FAIL]; then the override itself
+int launch_forward_new(const NetDev& net, const float* xyz, int64_t n, float* pre, int64_t ld,
+                       int64_t V, int keep_from, const int32_t* sa, const int32_t* sb, int idx,
+                       uint64_t* pos, uint64_t* zero, uint64_t* grid, uint64_t* shared,
+                       int64_t* ctr, hipStream_t s);
+int launch_override_new(int64_t n, int override_, const uint64_t* shared, float* pre, int64_t ld,
+                        int keep_from, int64_t V, uint64_t* pos, uint64_t* zero,
+                        const int64_t* ctr, hipStream_t s);
 int launch_encode(const NetDev& net, const float* x01, int64_t n, float* out, hipStream_t s);
 // pre plane-major; writes int64 m[n][3+K] and off[n][3] (Net.region)
 int launch_region(const NetDev& net, const float* xyz, const float* pre, int64_t ld,
@@ -39,7 +50,8 @@ int launch_keys(const NetDev& net, const float* xyz, const float* pre, int64_t l
                 hipStream_t s);
 
 // ---- scan.hip ----
-// exclusive scan of int32 counts into int64 offsets; *total (device) = sum
-int scan_i32_to_i64(const int32_t* in, int64_t* out, int64_t n, int64_t* total,
-                    void* scratch, size_t scratch_bytes, hipStream_t s);
-size_t scan_scratch_bytes(int64_t n);
+// exclusive scan of int32 counts into int64 offsets; *total (device) = sum.
+// lb: look-back state prepared for scan_tiles(n) tiles (engine.cpp lb_begin)
+int scan_i32_to_i64(const int32_t* in, int64_t* out, int64_t n, int64_t* total, const TnpLB& lb,
+                    hipStream_t s);
+int64_t scan_tiles(int64_t n);

@@ -23,6 +23,7 @@
 #include "common.h"
 #include "kernels.h"
 #include "net_device.h"
+#include "step.h"
 
 using namespace tnpnet;
 
@@ -81,6 +82,100 @@ k_forward(NetDev net, const float* __restrict__ xyz, int64_t n, float* __restric
     out2[2 * i] = o[0];
     out2[2 * i + 1] = o[1];
   }
+}
+
+// Forward of the S new vertices of a flat step with the step's epilogue
+// fused (replaces forward -> fail_check -> keys -> finalize_new): the
+// pre-activations of planes >= keep_from go straight into the cache
+// (plane-major, slot V + r), the packed pos/zero/grid keys are written as if
+// no override applies, and the failover predicate of subpoly_debug.py:35-49
+// (a new vertex off one of its shared planes by more than eps) is ORed into
+// ctr[CTR_FAIL]; shared[r] keeps the plane set for k_override_new.  Values
+// and the MKL row-count schedule are those of k_forward (same n = S).
+template <int LV, int H, int NL>
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_forward_new(NetDev net, const float* __restrict__ xyz, int64_t n, float* __restrict__ pre,
+              int64_t ld, int64_t V, int keep_from, const int32_t* __restrict__ sa,
+              const int32_t* __restrict__ sb, int idx, uint64_t* pos, uint64_t* zero,
+              uint64_t* __restrict__ grid, uint64_t* __restrict__ shared, int64_t* __restrict__ ctr) {
+  constexpr int IN = 2 * LV;
+  constexpr int NW = H * IN + H + (NL - 2) * (H * H + H) + 2 * H + 2;
+  __shared__ float w[NW];
+  for (int i = threadIdx.x; i < NW; i += blockDim.x) w[i] = net.weights[i];
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = i < n;
+  const float eps = net.eps;
+  float x[3] = {0.f, 0.f, 0.f};
+  uint64_t m = 0;
+  if (live) {
+    load_point(xyz, i, x);
+    const uint64_t below = (idx >= 64) ? ~0ull : ((1ull << idx) - 1ull);
+    m = (zero[sa[i]] & zero[sb[i]] & below) | (1ull << idx);
+  }
+  float h[H > IN ? H : IN];
+  float a[H];
+  encode<LV>(net, x, h);
+  const float* W = w;
+  int p = 0;
+  uint64_t ps = 0, zs = 0;
+  bool bad = false;
+  const int mh = lin_mode(n, false), mo = lin_mode(n, true);
+  float* col = pre + V + i;
+#pragma unroll
+  for (int layer = 0; layer < NL - 1; ++layer) {
+    if (layer == 0) {
+      linear_mode<IN, H>(W, W + H * IN, h, a, mh);
+      W += H * IN + H;
+    } else {
+      linear_mode<H, H>(W, W + H * H, h, a, mh);
+      W += H * H + H;
+    }
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+      const float v = a[j];
+      if (live && p + j >= keep_from) col[(int64_t)(p + j) * ld] = v;
+      ps |= (uint64_t)(v > eps) << (p + j);
+      zs |= (uint64_t)(fabsf(v) <= eps) << (p + j);
+      bad |= ((m >> (p + j)) & 1) && fabsf(v) > eps;
+      h[j] = fmaxf(v, 0.0f);
+    }
+    p += H;
+  }
+  float o[2];
+  linear_mode<H, 2>(W, W + 2 * H, h, o, mo);
+  const float v = __fsub_rn(o[1], o[0]);
+  if (live) {
+    if (p >= keep_from) col[(int64_t)p * ld] = v;
+    ps |= (uint64_t)(v > eps) << p;
+    zs |= (uint64_t)(fabsf(v) <= eps) << p;
+    bad |= ((m >> p) & 1) && fabsf(v) > eps;
+    pos[V + i] = ps;
+    zero[V + i] = zs;
+    grid[V + i] = grid_word(net.marks, net.n_marks, eps, x);
+    shared[i] = m;
+  }
+  if (__ballot(live && bad) && tnp::lane() == 0) tnp::or_sticky(&ctr[CTR_FAIL], 1ull);
+}
+
+// the override itself (masked_fill_ of the shared planes, subpoly_debug.py:48)
+// on what k_forward_new wrote; override_ < 0: the single-device predicate is
+// still in ctr[CTR_FAIL]
+__global__ void k_override_new(int64_t n, int override_, const uint64_t* __restrict__ shared,
+                               float* __restrict__ pre, int64_t ld, int keep_from, int64_t V,
+                               uint64_t* __restrict__ pos, uint64_t* __restrict__ zero,
+                               const int64_t* __restrict__ ctr) {
+  const bool ov = override_ < 0 ? ctr[CTR_FAIL] != 0 : override_ != 0;
+  if (!ov) return;
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  const uint64_t m = shared[r];
+  for (uint64_t t = m; t; t &= t - 1) {
+    const int p = __builtin_ctzll(t);
+    if (p >= keep_from) pre[(int64_t)p * ld + V + r] = 0.f;
+  }
+  pos[V + r] &= ~m;
+  zero[V + r] |= m;
 }
 
 // TropicalHashGrid.forward: raw encoding of x already in [0,1]^3 -> [n][2L]
@@ -180,6 +275,30 @@ int launch_forward(const NetDev& net, const float* xyz, int64_t n, float* pre, i
       hipLaunchKernelGGL((k_forward<L_, 16, 3, false>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s,
                          net, xyz, n, pre, ld, out2);
   });
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int launch_forward_new(const NetDev& net, const float* xyz, int64_t n, float* pre, int64_t ld,
+                       int64_t V, int keep_from, const int32_t* sa, const int32_t* sb, int idx,
+                       uint64_t* pos, uint64_t* zero, uint64_t* grid, uint64_t* shared,
+                       int64_t* ctr, hipStream_t s) {
+  if (n <= 0) return 0;
+  if (!net_supported(net)) { tnp_set_error("unsupported net shape"); return -1; }
+  TNP_DISPATCH(net.n_levels, {
+    hipLaunchKernelGGL((k_forward_new<L_, 16, 3>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net,
+                       xyz, n, pre, ld, V, keep_from, sa, sb, idx, pos, zero, grid, shared, ctr);
+  });
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int launch_override_new(int64_t n, int override_, const uint64_t* shared, float* pre, int64_t ld,
+                        int keep_from, int64_t V, uint64_t* pos, uint64_t* zero,
+                        const int64_t* ctr, hipStream_t s) {
+  if (n <= 0 || override_ == 0) return 0;
+  hipLaunchKernelGGL(k_override_new, dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, n, override_, shared,
+                     pre, ld, keep_from, V, pos, zero, ctr);
   TNP_CHECK(hipGetLastError());
   return 0;
 }

@@ -29,10 +29,12 @@ enum {
   CTR_TIGHT = 21,   // curve path: a kept c row misses its edge plane by > eps
   CTR_KEEP = 22,    // curve path: splits surviving the strict filter
   CTR_BOVF = 23,    // pair-chunk table overflow
-  CTR_N = 24
+  CTR_XK = 24,      // connecting edges surviving this step's pruning (appended)
+  CTR_N = 25
 };
 
 int64_t step_tiles(int64_t n);
+int64_t lb_tiles(int64_t n);  // tiles of the single-pass (look-back) kernels
 int launch_split_count(const int32_t* edges, int64_t E, const float* col, float eps, int32_t* blk,
                        hipStream_t s);
 // eidx != null (curve path): record each split's edge index instead of
@@ -40,6 +42,11 @@ int launch_split_count(const int32_t* edges, int64_t E, const float* col, float 
 int launch_split_emit(int32_t* edges, int64_t E, const float* col, float eps, const int64_t* blkoff,
                       int64_t V, int32_t* sa, int32_t* sb, int dup_mark, const uint64_t* grid,
                       int64_t* ctr, int32_t* eidx, hipStream_t s);
+// single-pass split over lb_tiles(E) look-back tiles (E > 0): S -> ctr[CTR_S];
+// sa/sb (and eidx if given) need capacity E
+int launch_split_lb(int32_t* edges, int64_t E, const float* col, float eps, int64_t V, int32_t* sa,
+                    int32_t* sb, int dup_mark, const uint64_t* grid, int64_t* ctr, int32_t* eidx,
+                    const TnpLB& lb, hipStream_t s);
 int launch_new_vertices(const int32_t* sa, const int32_t* sb, int64_t S, const float* col,
                         float eps, float* xyz, int64_t V, hipStream_t s);
 int launch_fail_check(const int32_t* sa, const int32_t* sb, int64_t S, int idx,
@@ -48,9 +55,10 @@ int launch_fail_check(const int32_t* sa, const int32_t* sb, int64_t S, int idx,
 int launch_finalize_new(int64_t S, int K, int override_, const uint64_t* shared, float* stage,
                         float eps, float* pre, int64_t ld, int keep_from, int64_t V, uint64_t* pos,
                         uint64_t* zero, const int64_t* ctr, hipStream_t s);
-int launch_hit_count(const float* col, int64_t V, float eps, int32_t* blk, hipStream_t s);
-int launch_hit_emit(const float* col, int64_t V, float eps, const int64_t* blkoff,
-                    int32_t* members, int64_t S, hipStream_t s);
+// members = [V, V + S) ++ live vertices v < V with |col[v]| < eps (ascending,
+// single pass over lb_tiles(V) look-back tiles); count -> ctr[CTR_H]
+int launch_hits(const float* col, const int32_t* alive, int64_t V, float eps, int32_t* members,
+                int64_t S, int64_t* ctr, const TnpLB& lb, hipStream_t s);
 // sort-based cell bucketing: span counts (+ A), (cell, member) entries,
 // segment bounds of the cell-sorted entries, per-cell counts, key copies
 // M = capacity (S + V); the live member count S + ctr[CTR_H] is read on
@@ -71,8 +79,10 @@ int launch_cell_tcnt(const int32_t* cellcnt, int64_t n, int32_t* tcnt, int64_t* 
 // connecting edges over the flattened pair space (cell-major, then (i, j<i));
 // the pair count is read on the device (ctr[CTR_TESTS]).  chunk_cells maps
 // pair chunks to cells (capacity cap chunks, overflow -> CTR_BOVF); connect
-// appends packed keys (lo << nb | hi) to keys[0, cap) and counts them in
-// ctr[CTR_X]; bstat needs 2 * connect_grid() slots.
+// counts every connecting edge in ctr[CTR_X] and appends the packed keys
+// (lo << nb | hi) of those the step's pruning keeps (fmask != 0: endpoint
+// keys differ on the planes of fmask; fmask == 0: all) to keys[0, cap),
+// counted in ctr[CTR_XK]; bstat needs 3 * connect_grid() slots.
 int64_t connect_chunks(int64_t TT);
 int64_t connect_grid();
 int launch_chunk_cells(const int64_t* toff, const int32_t* tcnt, int64_t ncell, int32_t* bcell,
@@ -80,8 +90,19 @@ int launch_chunk_cells(const int64_t* toff, const int32_t* tcnt, int64_t ncell, 
 int launch_connect(const int64_t* toff, const int32_t* cellcnt, const int64_t* celloff,
                    int64_t ncell, int NC, int64_t max_tests, const int32_t* bcell,
                    const int32_t* ent_v, const uint64_t* ent_g, const uint64_t* ent_p,
-                   const uint64_t* ent_z, int idx, int nb, uint64_t* keys, int64_t cap,
-                   int64_t* ctr, int64_t* bstat, hipStream_t s);
+                   const uint64_t* ent_z, int idx, int nb, uint64_t fmask, uint64_t* keys,
+                   int64_t cap, int64_t* ctr, int64_t* bstat, hipStream_t s);
+// single-pass pruning over [edges; e_new; c_new] (lb_tiles(E + S + X)
+// look-back tiles): kept edges in order -> out, used flags (zeroed by the
+// caller), ctr[CTR_E], ctr[CTR_ACTIVE]
+int launch_prune_lb(const int32_t* edges, int64_t E, const int32_t* sb, int64_t S, int64_t V,
+                    const uint64_t* ckeys, int nb, int64_t X, int idx, int last_plane,
+                    const uint64_t* pos, const uint64_t* zero, int32_t* out, int32_t* used,
+                    int64_t* ctr, const TnpLB& lb, hipStream_t s);
+// ctr[slot] += number of non-zero flags in f[0, n) (16-B aligned f)
+int launch_count_flags(const int32_t* f, int64_t n, int64_t* ctr, int slot, hipStream_t s);
+// planes the pruning of step idx compares (idx .. last_plane)
+uint64_t prune_mask(int idx, int last_plane);
 // ---- sort.hip ----
 // ascending LSD radix sort of n u64 keys on bits [0, bits); the sorted keys
 // end in *out (== a or b)

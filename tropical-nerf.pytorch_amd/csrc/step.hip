@@ -28,6 +28,10 @@ namespace {
 
 constexpr int IPT = 8;                  // items per thread per tile
 constexpr int TILE = TNP_BLOCK * IPT;   // tile of a compaction pass
+// single-pass (look-back) compactions: larger tiles, so the per-tile ticket
+// atomic and look-back round trip are amortised over 8192 items
+constexpr int LIPT = 32;
+constexpr int LTILE = TNP_BLOCK * LIPT;
 
 // ---------------------------------------------------------------------------
 // split test: subpoly.py:102-105
@@ -104,6 +108,70 @@ k_split_emit(int32_t* __restrict__ edges, int64_t E, const float* __restrict__ c
   }
 }
 
+// single pass (replaces split_count -> scan -> split_emit): tile by ticket,
+// decoupled look-back for the tile's first new-vertex id; the last tile
+// writes S to ctr[CTR_S].  sa/sb/eidx need capacity E.
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_split_lb(int32_t* __restrict__ edges, int64_t E, int64_t ntiles, const float* __restrict__ col,
+           float eps, int64_t V, int32_t* __restrict__ sa, int32_t* __restrict__ sb, int dup_mark,
+           const uint64_t* __restrict__ grid, int64_t* __restrict__ ctr, int32_t* __restrict__ eidx,
+           TnpLB lb) {
+  __shared__ int cnt[LIPT][TNP_WAVES];
+  __shared__ int64_t slot;
+  const int64_t tile = tnp::lb_tile(lb, &slot);
+  const int64_t base = tile * LTILE;
+  uint64_t bal[LIPT];
+#pragma unroll
+  for (int k = 0; k < LIPT; ++k) {
+    const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
+    const bool f = (i < E) && split_test(col, edges + 2 * i, eps);
+    bal[k] = __ballot(f);
+    if (tnp::lane() == 0) cnt[k][tnp::wave()] = __popcll(bal[k]);
+  }
+  __syncthreads();
+  int64_t agg = 0;
+#pragma unroll
+  for (int k = 0; k < LIPT; ++k)
+#pragma unroll
+    for (int w = 0; w < TNP_WAVES; ++w) agg += cnt[k][w];
+  const int64_t prefix = tnp::lb_prefix(lb, tile, agg, &slot);
+  int64_t run = prefix;
+  int dup = 0;
+#pragma unroll
+  for (int k = 0; k < LIPT; ++k) {
+    int64_t off = run;
+    int tot = 0;
+#pragma unroll
+    for (int w = 0; w < TNP_WAVES; ++w) {
+      const int c = cnt[k][w];
+      off += (w < tnp::wave()) ? c : 0;
+      tot += c;
+    }
+    if ((bal[k] >> tnp::lane()) & 1) {
+      const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
+      const int64_t id = off + tnp::mbcnt(bal[k]);
+      const int a = edges[2 * i], b = edges[2 * i + 1];
+      sa[id] = a;
+      sb[id] = b;
+      if (eidx) eidx[id] = (int32_t)i;
+      else edges[2 * i + 1] = (int32_t)(V + id);
+      if (dup_mark >= 0) {
+        // edge lying in this slab's upper boundary mark plane (x = mark):
+        // the neighbouring slab splits the same edge, count it once
+        const uint64_t ga = grid[a], gb = grid[b];
+        dup += tnp::grid_zero(ga, 0) && tnp::grid_zero(gb, 0) && tnp::grid_off(ga, 0) == dup_mark &&
+               tnp::grid_off(gb, 0) == dup_mark;
+      }
+    }
+    run += tot;
+  }
+  if (tile == ntiles - 1 && threadIdx.x == 0) ctr[CTR_S] = prefix + agg;
+  if (dup_mark >= 0) {
+    dup = tnp::wave_sum(dup);
+    if (tnp::lane() == 0 && dup) atomicAdd((unsigned long long*)&ctr[CTR_DUP], (unsigned long long)dup);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // new vertices: subpoly.py:113-117, 180
 //   d = d/eps; w = |d0| / |d1 - d0|; v = e0*(1-w) + e1*w
@@ -171,40 +239,48 @@ __global__ void k_finalize_new(int64_t S, int K, int override_, const uint64_t* 
 // ---------------------------------------------------------------------------
 // hit vertices: |outputs_[:, idx]| < eps (subpoly.py:233), ascending order
 // ---------------------------------------------------------------------------
+// single pass (decoupled look-back): live vertices on the plane, ascending,
+// appended after the S new members; the last tile writes the count to
+// ctr[CTR_H].  alive: the live-slot flags of the lazily compacted vertex set
 __global__ void __launch_bounds__(TNP_BLOCK)
-k_hit_count(const float* __restrict__ col, int64_t V, float eps, int32_t* __restrict__ blk) {
-  __shared__ int lds[TNP_WAVES];
-  int64_t base = (int64_t)blockIdx.x * TILE;
-  int c = 0;
+k_hit_lb(const float* __restrict__ col, const int32_t* __restrict__ alive, int64_t V,
+         int64_t ntiles, float eps, int32_t* __restrict__ members, int64_t S,
+         int64_t* __restrict__ ctr, TnpLB lb) {
+  __shared__ int cnt[LIPT][TNP_WAVES];
+  __shared__ int64_t slot;
+  const int64_t tile = tnp::lb_tile(lb, &slot);
+  const int64_t base = tile * LTILE;
+  uint64_t bal[LIPT];
 #pragma unroll
-  for (int k = 0; k < IPT; ++k) {
-    int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
-    if (i < V) c += fabsf(col[i]) < eps;
+  for (int k = 0; k < LIPT; ++k) {
+    const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
+    const bool f = (i < V) && (fabsf(col[i]) < eps) && alive[i];
+    bal[k] = __ballot(f);
+    if (tnp::lane() == 0) cnt[k][tnp::wave()] = __popcll(bal[k]);
   }
-  c = tnp::wave_sum(c);
-  if (tnp::lane() == 0) lds[tnp::wave()] = c;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    int t = 0;
-    for (int w = 0; w < TNP_WAVES; ++w) t += lds[w];
-    blk[blockIdx.x] = t;
-  }
-}
-
-__global__ void __launch_bounds__(TNP_BLOCK)
-k_hit_emit(const float* __restrict__ col, int64_t V, float eps, const int64_t* __restrict__ blkoff,
-           int32_t* __restrict__ members, int64_t S) {
-  __shared__ int lds[TNP_WAVES];
-  int64_t base = (int64_t)blockIdx.x * TILE;
-  int64_t run = blkoff[blockIdx.x];
-  for (int k = 0; k < IPT; ++k) {
-    int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
-    bool f = (i < V) && (fabsf(col[i]) < eps);
-    int tot;
-    int r = tnp::block_rank(f, lds, tot);
-    if (f) members[S + run + r] = (int32_t)i;
+  int64_t agg = 0;
+#pragma unroll
+  for (int k = 0; k < LIPT; ++k)
+#pragma unroll
+    for (int w = 0; w < TNP_WAVES; ++w) agg += cnt[k][w];
+  const int64_t prefix = tnp::lb_prefix(lb, tile, agg, &slot);
+  int64_t run = prefix;
+#pragma unroll
+  for (int k = 0; k < LIPT; ++k) {
+    int64_t off = run;
+    int tot = 0;
+#pragma unroll
+    for (int w = 0; w < TNP_WAVES; ++w) {
+      const int c = cnt[k][w];
+      off += (w < tnp::wave()) ? c : 0;
+      tot += c;
+    }
+    if ((bal[k] >> tnp::lane()) & 1)
+      members[S + off + tnp::mbcnt(bal[k])] = (int32_t)(base + (int64_t)k * TNP_BLOCK + threadIdx.x);
     run += tot;
   }
+  if (tile == ntiles - 1 && threadIdx.x == 0) ctr[CTR_H] = prefix + agg;
 }
 
 __global__ void k_new_members(int32_t* __restrict__ members, int64_t S, int64_t V) {
@@ -438,15 +514,16 @@ k_connect(const int64_t* __restrict__ toff, const int32_t* __restrict__ cellcnt,
           const int64_t* __restrict__ celloff, int64_t ncell, int NC, int64_t max_tests,
           const int32_t* __restrict__ bcell, const int32_t* __restrict__ ent_v,
           const uint64_t* __restrict__ ent_g, const uint64_t* __restrict__ ent_p,
-          const uint64_t* __restrict__ ent_z, int idx, int nb, uint64_t* __restrict__ keys,
-          int64_t cap, int64_t* __restrict__ ctr, int64_t* __restrict__ bstat) {
+          const uint64_t* __restrict__ ent_z, int idx, int nb, uint64_t fmask,
+          uint64_t* __restrict__ keys, int64_t cap, int64_t* __restrict__ ctr,
+          int64_t* __restrict__ bstat) {
   __shared__ int64_t lds[TNP_WAVES];
   __shared__ int64_t s_base;
   const int64_t TT = ctr[CTR_TESTS];
   if (TT > max_tests || ctr[CTR_BOVF] || ctr[CTR_BIG]) return;
   const int64_t nblk = (TT + CCH - 1) / CCH;
   const uint64_t below = (idx >= 64) ? ~0ull : ((1ull << idx) - 1ull);
-  int64_t n_compat = 0, n_reg = 0;
+  int64_t n_compat = 0, n_reg = 0, n_conn = 0;
   for (int64_t b = blockIdx.x; b < nblk; b += gridDim.x) {
   const int64_t p0 = b * (int64_t)CCH + (int64_t)threadIdx.x * CIPT;
   uint64_t kk[CIPT];
@@ -470,11 +547,14 @@ k_connect(const int64_t* __restrict__ toff, const int32_t* __restrict__ cellcnt,
       const int64_t p = p0 + k;
       if (p < TT) {
         int64_t e = base + j;
-        PairTest t = pair_test(cc, below, gu, pu, zu, ent_g[e], ent_p[e], ent_z[e]);
+        const uint64_t pv = ent_p[e], zv = ent_z[e];
+        PairTest t = pair_test(cc, below, gu, pu, zu, ent_g[e], pv, zv);
         if (t.compat) {
           n_compat++;
           n_reg += t.regions;
-          if (t.emit) {
+          n_conn += t.emit;
+          // the step's pruning drops it anyway (keep_edge): never appended
+          if (t.emit && (fmask == 0 || (((pu ^ pv) | (zu ^ zv)) & fmask) != 0)) {
             uint32_t vv = (uint32_t)ent_v[e];
             uint32_t lo = (uint32_t)vu < vv ? (uint32_t)vu : vv;
             uint32_t hi = (uint32_t)vu < vv ? vv : (uint32_t)vu;
@@ -504,7 +584,7 @@ k_connect(const int64_t* __restrict__ toff, const int32_t* __restrict__ cellcnt,
   }
   int64_t tot;
   int64_t off = tnp::block_scan_excl((int64_t)ne, lds, tot);
-  if (threadIdx.x == 0) s_base = tot ? (int64_t)atomicAdd((unsigned long long*)&ctr[CTR_X], (unsigned long long)tot) : 0;
+  if (threadIdx.x == 0) s_base = tot ? (int64_t)atomicAdd((unsigned long long*)&ctr[CTR_XK], (unsigned long long)tot) : 0;
   __syncthreads();
   const int64_t w0 = s_base + off;
   for (int k = 0; k < ne; ++k)
@@ -512,24 +592,30 @@ k_connect(const int64_t* __restrict__ toff, const int32_t* __restrict__ cellcnt,
   }
   int64_t tot;
   tnp::block_scan_excl(n_compat, lds, tot);
-  if (threadIdx.x == 0) bstat[2 * blockIdx.x] = tot;
+  if (threadIdx.x == 0) bstat[3 * blockIdx.x] = tot;
   tnp::block_scan_excl(n_reg, lds, tot);
-  if (threadIdx.x == 0) bstat[2 * blockIdx.x + 1] = tot;
+  if (threadIdx.x == 0) bstat[3 * blockIdx.x + 1] = tot;
+  tnp::block_scan_excl(n_conn, lds, tot);
+  if (threadIdx.x == 0) bstat[3 * blockIdx.x + 2] = tot;
 }
 
-// per-block (compatible pairs, shared regions) -> ctr[CTR_COMPAT], ctr[CTR_P]
+// per-block (compatible pairs, shared regions, connecting edges)
+//   -> ctr[CTR_COMPAT], ctr[CTR_P], ctr[CTR_X]
 __global__ void __launch_bounds__(TNP_BLOCK)
 k_sum_bstat(const int64_t* __restrict__ bstat, int64_t nblk, int64_t* __restrict__ ctr) {
-  int64_t a = 0, r = 0;
+  int64_t a = 0, r = 0, x = 0;
   for (int64_t i = threadIdx.x; i < nblk; i += blockDim.x) {
-    a += bstat[2 * i];
-    r += bstat[2 * i + 1];
+    a += bstat[3 * i];
+    r += bstat[3 * i + 1];
+    x += bstat[3 * i + 2];
   }
   a = tnp::wave_sum(a);
   r = tnp::wave_sum(r);
+  x = tnp::wave_sum(x);
   if (tnp::lane() == 0) {
     atomicAdd((unsigned long long*)&ctr[CTR_COMPAT], (unsigned long long)a);
     atomicAdd((unsigned long long*)&ctr[CTR_P], (unsigned long long)r);
+    atomicAdd((unsigned long long*)&ctr[CTR_X], (unsigned long long)x);
   }
 }
 // ---------------------------------------------------------------------------
@@ -633,6 +719,102 @@ k_prune_emit(EdgeSrc src, int64_t N, uint64_t fmask, uint64_t amask,
   if (tnp::lane() == 0) tnp::or_sticky(&ctr[CTR_ACTIVE], act);
 }
 
+// single-pass pruning (replaces prune_count -> scan -> prune_emit): tile by
+// ticket, keep flags per item kept in registers, decoupled look-back for the
+// tile's output offset, then the ordered emit (k-major, then thread, as
+// prune_emit), used flags and the next-active plane mask.  The last tile
+// writes the kept count to ctr[CTR_E].
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, uint64_t fmask, uint64_t amask,
+           const uint64_t* __restrict__ pos, const uint64_t* __restrict__ zero,
+           int32_t* __restrict__ out, int32_t* __restrict__ used, int64_t* __restrict__ ctr,
+           TnpLB lb) {
+  __shared__ int cnt[LIPT][TNP_WAVES];
+  __shared__ int64_t slot;
+  const int64_t tile = tnp::lb_tile(lb, &slot);
+  const int64_t base = tile * LTILE;
+  uint64_t bal[LIPT];
+  uint64_t act = 0;
+#pragma unroll
+  for (int k = 0; k < LIPT; ++k) {
+    const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
+    bool f = false;
+    if (i < N) {
+      int a, b;
+      fetch_edge(src, i, a, b);
+      const uint64_t pa = pos[a], pb = pos[b], za = zero[a], zb = zero[b];
+      f = (((pa ^ pb) | (za ^ zb)) & fmask) != 0;
+      if (f) act |= (pa ^ pb) & ~za & ~zb & amask;
+    }
+    bal[k] = __ballot(f);
+    if (tnp::lane() == 0) cnt[k][tnp::wave()] = __popcll(bal[k]);
+  }
+  __syncthreads();
+  int64_t agg = 0;
+#pragma unroll
+  for (int k = 0; k < LIPT; ++k)
+#pragma unroll
+    for (int w = 0; w < TNP_WAVES; ++w) agg += cnt[k][w];
+  const int64_t prefix = tnp::lb_prefix(lb, tile, agg, &slot);
+  int64_t run = prefix;
+#pragma unroll
+  for (int k = 0; k < LIPT; ++k) {
+    int64_t off = run;
+    int tot = 0;
+#pragma unroll
+    for (int w = 0; w < TNP_WAVES; ++w) {
+      const int c = cnt[k][w];
+      off += (w < tnp::wave()) ? c : 0;
+      tot += c;
+    }
+    if ((bal[k] >> tnp::lane()) & 1) {
+      const int64_t o = off + tnp::mbcnt(bal[k]);
+      int a, b;  // re-fetched: the tile's edges are L2-resident
+      fetch_edge(src, base + (int64_t)k * TNP_BLOCK + threadIdx.x, a, b);
+      out[2 * o] = a;
+      out[2 * o + 1] = b;
+      used[a] = 1;
+      used[b] = 1;
+    }
+    run += tot;
+  }
+  if (tile == ntiles - 1 && threadIdx.x == 0) ctr[CTR_E] = prefix + agg;
+  act = tnp::wave_or(act);
+  __shared__ uint64_t acts[TNP_WAVES];
+  if (tnp::lane() == 0) acts[tnp::wave()] = act;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t t = 0;
+    for (int w = 0; w < TNP_WAVES; ++w) t |= acts[w];
+    tnp::or_sticky(&ctr[CTR_ACTIVE], t);
+  }
+}
+
+// number of set flags -> ctr[slot] (+=, one atomic per block)
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_count_flags(const int32_t* __restrict__ f, int64_t n, int64_t* __restrict__ ctr, int slot) {
+  __shared__ int lds[TNP_WAVES];
+  int c = 0;
+  const int64_t i0 = ((int64_t)blockIdx.x * TNP_BLOCK + threadIdx.x) * 4;
+  const int64_t stride = (int64_t)gridDim.x * TNP_BLOCK * 4;
+  for (int64_t i = i0; i < n; i += stride) {
+    if (i + 3 < n) {
+      const int4 v = *reinterpret_cast<const int4*>(f + i);
+      c += (v.x != 0) + (v.y != 0) + (v.z != 0) + (v.w != 0);
+    } else {
+      for (int64_t j = i; j < n; ++j) c += f[j] != 0;
+    }
+  }
+  c = tnp::wave_sum(c);
+  if (tnp::lane() == 0) lds[tnp::wave()] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+    for (int w = 0; w < TNP_WAVES; ++w) t += lds[w];
+    if (t) atomicAdd((unsigned long long*)&ctr[slot], (unsigned long long)t);
+  }
+}
+
 __global__ void k_gather_vertices(const int32_t* __restrict__ used, const int64_t* __restrict__ nid,
                                   int64_t NV, int K, int keep_from,
                                   const float* __restrict__ xyz, const float* __restrict__ pre,
@@ -658,18 +840,27 @@ __global__ void k_remap_edges(int32_t* __restrict__ edges, int64_t E, const int6
   edges[i] = (int32_t)nid[edges[i]];
 }
 
-// initial next-active mask for an arbitrary edge set
-__global__ void k_active_planes(const int32_t* __restrict__ edges, int64_t E, uint64_t amask,
-                                const uint64_t* __restrict__ pos, const uint64_t* __restrict__ zero,
-                                int64_t* __restrict__ ctr) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// initial next-active mask for an arbitrary edge set (grid-stride, one
+// sticky OR per block)
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_active_planes(const int32_t* __restrict__ edges, int64_t E, uint64_t amask,
+                const uint64_t* __restrict__ pos, const uint64_t* __restrict__ zero,
+                int64_t* __restrict__ ctr) {
+  __shared__ uint64_t lds[TNP_WAVES];
   uint64_t act = 0;
-  if (i < E) {
-    int a = edges[2 * i], b = edges[2 * i + 1];
-    act = (pos[a] ^ pos[b]) & ~zero[a] & ~zero[b] & amask;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < E;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int a = edges[2 * i], b = edges[2 * i + 1];
+    act |= (pos[a] ^ pos[b]) & ~zero[a] & ~zero[b] & amask;
   }
   act = tnp::wave_or(act);
-  if (tnp::lane() == 0) tnp::or_sticky(&ctr[CTR_ACTIVE], act);
+  if (tnp::lane() == 0) lds[tnp::wave()] = act;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t t = 0;
+    for (int w = 0; w < TNP_WAVES; ++w) t |= lds[w];
+    tnp::or_sticky(&ctr[CTR_ACTIVE], t);
+  }
 }
 
 }  // namespace
@@ -678,6 +869,7 @@ __global__ void k_active_planes(const int32_t* __restrict__ edges, int64_t E, ui
 // launchers
 // ----------------------------------------------------------------------------
 int64_t step_tiles(int64_t n) { return (n + TILE - 1) / TILE; }
+int64_t lb_tiles(int64_t n) { return (n + LTILE - 1) / LTILE; }
 
 int launch_split_count(const int32_t* edges, int64_t E, const float* col, float eps, int32_t* blk,
                        hipStream_t s) {
@@ -691,6 +883,15 @@ int launch_split_emit(int32_t* edges, int64_t E, const float* col, float eps, co
                       int64_t* ctr, int32_t* eidx, hipStream_t s) {
   hipLaunchKernelGGL(k_split_emit, dim3((unsigned)step_tiles(E)), dim3(TNP_BLOCK), 0, s, edges, E,
                      col, eps, blkoff, V, sa, sb, dup_mark, grid, ctr, eidx);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_split_lb(int32_t* edges, int64_t E, const float* col, float eps, int64_t V, int32_t* sa,
+                    int32_t* sb, int dup_mark, const uint64_t* grid, int64_t* ctr, int32_t* eidx,
+                    const TnpLB& lb, hipStream_t s) {
+  const int64_t tiles = lb_tiles(E);
+  hipLaunchKernelGGL(k_split_lb, dim3((unsigned)tiles), dim3(TNP_BLOCK), 0, s, edges, E, tiles, col,
+                     eps, V, sa, sb, dup_mark, grid, ctr, eidx, lb);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
@@ -720,16 +921,15 @@ int launch_finalize_new(int64_t S, int K, int override_, const uint64_t* shared,
   TNP_CHECK(hipGetLastError());
   return 0;
 }
-int launch_hit_count(const float* col, int64_t V, float eps, int32_t* blk, hipStream_t s) {
-  hipLaunchKernelGGL(k_hit_count, dim3((unsigned)step_tiles(V)), dim3(TNP_BLOCK), 0, s, col, V,
-                     eps, blk);
-  TNP_CHECK(hipGetLastError());
-  return 0;
-}
-int launch_hit_emit(const float* col, int64_t V, float eps, const int64_t* blkoff,
-                    int32_t* members, int64_t S, hipStream_t s) {
-  hipLaunchKernelGGL(k_hit_emit, dim3((unsigned)step_tiles(V)), dim3(TNP_BLOCK), 0, s, col, V, eps,
-                     blkoff, members, S);
+int launch_hits(const float* col, const int32_t* alive, int64_t V, float eps, int32_t* members,
+                int64_t S, int64_t* ctr, const TnpLB& lb, hipStream_t s) {
+  if (V > 0) {
+    const int64_t tiles = lb_tiles(V);
+    hipLaunchKernelGGL(k_hit_lb, dim3((unsigned)tiles), dim3(TNP_BLOCK), 0, s, col, alive, V, tiles,
+                       eps, members, S, ctr, lb);
+  } else {
+    TNP_CHECK(hipMemsetAsync(ctr + CTR_H, 0, sizeof(int64_t), s));
+  }
   if (S > 0)
     hipLaunchKernelGGL(k_new_members, dim3(tnp_grid(S)), dim3(TNP_BLOCK), 0, s, members, S, V);
   TNP_CHECK(hipGetLastError());
@@ -794,16 +994,21 @@ int launch_chunk_cells(const int64_t* toff, const int32_t* tcnt, int64_t ncell, 
 int launch_connect(const int64_t* toff, const int32_t* cellcnt, const int64_t* celloff,
                    int64_t ncell, int NC, int64_t max_tests, const int32_t* bcell,
                    const int32_t* ent_v, const uint64_t* ent_g, const uint64_t* ent_p,
-                   const uint64_t* ent_z, int idx, int nb, uint64_t* keys, int64_t cap,
-                   int64_t* ctr, int64_t* bstat, hipStream_t s) {
+                   const uint64_t* ent_z, int idx, int nb, uint64_t fmask, uint64_t* keys,
+                   int64_t cap, int64_t* ctr, int64_t* bstat, hipStream_t s) {
   hipLaunchKernelGGL(k_connect, dim3(CONNECT_GRID), dim3(TNP_BLOCK), 0, s, toff, cellcnt, celloff,
-                     ncell, NC, max_tests, bcell, ent_v, ent_g, ent_p, ent_z, idx, nb, keys, cap, ctr,
-                     bstat);
+                     ncell, NC, max_tests, bcell, ent_v, ent_g, ent_p, ent_z, idx, nb, fmask, keys,
+                     cap, ctr, bstat);
   hipLaunchKernelGGL(k_sum_bstat, dim3(1), dim3(TNP_BLOCK), 0, s, bstat, (int64_t)CONNECT_GRID, ctr);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
 int64_t connect_grid() { return CONNECT_GRID; }
+uint64_t prune_mask(int idx, int last_plane) {
+  uint64_t fmask = (idx >= 64) ? 0ull : (~0ull << idx);
+  if (last_plane < 63) fmask &= (1ull << (last_plane + 1)) - 1ull;
+  return fmask;
+}
 int launch_prune(bool emit, const int32_t* edges, int64_t E, const int32_t* sb, int64_t S,
                  int64_t V, const uint64_t* ckeys, int nb, int64_t X, int idx,
                  int prune, int last_plane, const uint64_t* pos, const uint64_t* zero,
@@ -812,8 +1017,7 @@ int launch_prune(bool emit, const int32_t* edges, int64_t E, const int32_t* sb, 
   EdgeSrc src{edges, E, sb, S, V, ckeys, nb, X};
   int64_t N = E + S + X;
   if (N <= 0) return 0;
-  uint64_t fmask = (idx >= 64) ? 0ull : (~0ull << idx);
-  if (last_plane < 63) fmask &= (1ull << (last_plane + 1)) - 1ull;
+  uint64_t fmask = prune_mask(idx, last_plane);
   uint64_t amask = (idx + 1 >= 64) ? 0ull : (~0ull << (idx + 1));
   if (last_plane < 63) amask &= (1ull << (last_plane + 1)) - 1ull;
   if (!emit)
@@ -822,6 +1026,32 @@ int launch_prune(bool emit, const int32_t* edges, int64_t E, const int32_t* sb, 
   else
     hipLaunchKernelGGL(k_prune_emit, dim3((unsigned)step_tiles(N)), dim3(TNP_BLOCK), 0, s, src, N,
                        fmask, amask, pos, zero, blkoff, prune, out, used, ctr);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_prune_lb(const int32_t* edges, int64_t E, const int32_t* sb, int64_t S, int64_t V,
+                    const uint64_t* ckeys, int nb, int64_t X, int idx, int last_plane,
+                    const uint64_t* pos, const uint64_t* zero, int32_t* out, int32_t* used,
+                    int64_t* ctr, const TnpLB& lb, hipStream_t s) {
+  EdgeSrc src{edges, E, sb, S, V, ckeys, nb, X};
+  const int64_t N = E + S + X;
+  if (N <= 0) {
+    TNP_CHECK(hipMemsetAsync(ctr + CTR_E, 0, sizeof(int64_t), s));
+    return 0;
+  }
+  uint64_t fmask = prune_mask(idx, last_plane);
+  uint64_t amask = (idx + 1 >= 64) ? 0ull : (~0ull << (idx + 1));
+  if (last_plane < 63) amask &= (1ull << (last_plane + 1)) - 1ull;
+  const int64_t tiles = lb_tiles(N);
+  hipLaunchKernelGGL(k_prune_lb, dim3((unsigned)tiles), dim3(TNP_BLOCK), 0, s, src, N, tiles, fmask,
+                     amask, pos, zero, out, used, ctr, lb);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_count_flags(const int32_t* f, int64_t n, int64_t* ctr, int slot, hipStream_t s) {
+  if (n <= 0) return 0;
+  const unsigned g = (unsigned)std::min<int64_t>(2048, (n + 4 * TNP_BLOCK - 1) / (4 * TNP_BLOCK));
+  hipLaunchKernelGGL(k_count_flags, dim3(g), dim3(TNP_BLOCK), 0, s, f, n, ctr, slot);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
@@ -848,8 +1078,8 @@ int launch_active_planes(const int32_t* edges, int64_t E, int from, int last_pla
   if (E <= 0) return 0;
   uint64_t amask = (from >= 64) ? 0ull : (~0ull << from);
   if (last_plane < 63) amask &= (1ull << (last_plane + 1)) - 1ull;
-  hipLaunchKernelGGL(k_active_planes, dim3(tnp_grid(E)), dim3(TNP_BLOCK), 0, s, edges, E, amask,
-                     pos, zero, ctr);
+  const unsigned g = (unsigned)std::min<int64_t>(2048, tnp_grid(E));
+  hipLaunchKernelGGL(k_active_planes, dim3(g), dim3(TNP_BLOCK), 0, s, edges, E, amask, pos, zero, ctr);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
