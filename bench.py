@@ -12,9 +12,11 @@ Net(num_layers=3, num_hidden=16, levels=2, r_min=G-1, r_max=G-1, T=19)
 (G marks per axis; hash table U(-0.1,0.1), nn.Linear-bound MLP, numpy PCG64
 seed 6 by default, see --seed), initial edges = the full G^3 lattice.  G = 128 at one GPU; at N GPUs
 the lattice grows to round(128 * N^(1/3)) marks per axis and is cut into N
-x-slabs (weak scaling, one process per GPU, RCCL only for the per-step
-8-byte agreements).  value = edges subdivided by all ranks (each split
-counted once) / max-over-ranks wall time.
+x-slabs of cells, each extracted with a one-cell halo (weak scaling, one
+process per GPU, RCCL only for the per-step 8-byte agreements; the slabs
+are stitched into one complex after the timed region,
+tropical/distributed.py).  value = edges subdivided by all ranks (each
+split counted once, by the rank owning it) / max-over-ranks wall time.
 
 Run: python bench.py [--gpus N --steps K --warmup W]  (torchrun for N > 1)
 """
@@ -67,12 +69,6 @@ def make_net(G, device, seed=0):
     net = Net(**cfg)
     net.load_state_dict({k: torch.from_numpy(v) for k, v in p.items()})
     return net.to(device)
-
-
-def slab(G: int, rank: int, world: int):
-    """Marks [x0, x1] of this rank's x-slab (cells split evenly)."""
-    cuts = [round(r * (G - 1) / world) for r in range(world + 1)]
-    return cuts[rank], cuts[rank + 1]
 
 
 def algorithmic_bytes(st: dict, K: int) -> int:
@@ -208,20 +204,31 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # one rank per GPU; TNP_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs
+    # (collectives then run on host copies)
+    backend = os.environ.get("TNP_DIST_BACKEND", "nccl")
+    local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    comm_dev = dev if backend == "nccl" else torch.device("cpu")
     coll = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
-        coll = Collective(dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+        coll = Collective(comm_dev)
 
     from tropical._engine import engine_for
     G = args.marks if world == 1 else int(round(args.marks * world ** (1.0 / 3.0)))
     net = make_net(G, dev, args.seed)
-    x0, x1 = slab(G, rank, world)
+    from tropical.distributed import slab_cuts, slab_marks
+    cuts = slab_cuts(G, world)
+    x0, x1 = slab_marks(cuts, rank)  # this rank's cells + a one-cell halo
     eng = engine_for(net)
-    eng.set_dup_plane(x1 if rank < world - 1 else -1)
+    if world > 1:
+        eng.set_owned(cuts[rank], cuts[rank + 1])  # halo splits -> S_dup
     eng.set_shards(world)
 
     def one_pass():
@@ -252,9 +259,30 @@ def main():
     ktime = eng.kernel_timer(False)
     barrier()
 
+    from tropical.distributed import complex_hash
+    stitched = None
+    if world == 1:
+        Vf, Ef, _ = eng.export()
+        hv, he = complex_hash(Vf, Ef)
+        stitched = {"vertices": int(Vf.shape[0]), "edges": int(Ef.shape[0]),
+                    "vertex_set_hash": hv, "edge_set_hash": he}
+    else:
+        # the complete sharded output: each slab exported and stitched into one
+        # global complex (tropical/distributed.py; RCCL all_gathers), untimed
+        from tropical.distributed import stitch
+        Vl, El, _ = eng.export()
+        owned, first, gE, own, keep = stitch(Vl.to(comm_dev), El.to(comm_dev), net.enc.marks, cuts,
+                                             masks=True)
+        hv, he = complex_hash(Vl.to(comm_dev), El.to(comm_dev), own, keep)
+        tot = torch.tensor([owned.shape[0], gE.shape[0], hv, he], device=comm_dev, dtype=torch.int64)
+        torch.distributed.all_reduce(tot)  # int64 sums wrap like the 1-rank sums
+        stitched = {"vertices": int(tot[0]), "edges": int(tot[1]),
+                    "vertex_set_hash": int(tot[2]), "edge_set_hash": int(tot[3])}
+        barrier()
+
     splits = sum(s["S"] - s["S_dup"] for st in all_stats for s in st)
     bytes_alg = sum(algorithmic_bytes(s, net.K) for st in all_stats for s in st)
-    vec = torch.tensor([dt, float(splits), float(bytes_alg)], device=dev, dtype=torch.float64)
+    vec = torch.tensor([dt, float(splits), float(bytes_alg)], device=comm_dev, dtype=torch.float64)
     if world > 1:
         mx = vec.clone()
         torch.distributed.all_reduce(mx[:1], op=torch.distributed.ReduceOp.MAX)
@@ -297,6 +325,8 @@ def main():
                                    sorted(ktime.items(), key=lambda kv: -kv[1]["ms"])},
             "active_steps": len(st0),
         }
+        if stitched:
+            out["final_complex" if world == 1 else "stitched_complex"] = stitched
         if not args.no_cpu and world == 1:
             thr = max(1, min(16, len(os.sched_getaffinity(0))))
             cps, S_cpu, t_cpu, Vs_cpu = cpu_baseline(args.cpu_sample_marks, args.seed, thr)

@@ -57,7 +57,7 @@ typedef struct tnp_step_stats {
   int64_t pair_tests; /* member pairs this implementation tested */
   int32_t override_applied;
   uint64_t next_active; /* planes > idx a kept edge would split (pruning steps) */
-  int64_t S_dup;        /* splits on the shared slab boundary plane (multi-GPU) */
+  int64_t S_dup;        /* splits outside the owned slab (multi-GPU halo) */
 } tnp_step_stats;
 
 const char* tnp_last_error(void);
@@ -175,10 +175,12 @@ int tnp_engine_faces_export(tnp_engine* eng, int64_t* d_tri, float* d_faces,
  * Single-device only (the descent's stop criterion is global). */
 int tnp_engine_set_curve(tnp_engine* eng, int on);
 
-/* Multi-GPU x-slabs: count splits of edges lying in mark plane x = mark
- * (the plane this slab shares with its upper neighbour; -1 = none), so the
- * global split count can subtract the replicated boundary work. */
-int tnp_engine_set_dup_plane(tnp_engine* eng, int mark);
+/* Multi-GPU x-slabs with a one-cell halo: this shard OWNS the mark planes
+ * (lo, hi] (lo == 0: [0, hi]) and the cells between them; new vertices
+ * outside (halo work, also computed by the neighbour that owns them) are
+ * counted in tnp_step_stats.S_dup so the global split count counts each
+ * split once.  lo > hi (default) = everything owned.  Flat path only. */
+int tnp_engine_set_owned(tnp_engine* eng, int lo, int hi);
 
 /* world > 1: this engine holds one x-slab of a complex sharded over `world`
  * devices.  A step the other shards split may leave this one without any

@@ -116,7 +116,7 @@ enum {
 
 struct tnp_engine {
   int device = 0;
-  int dup_mark = -1;
+  int own_lo = 1, own_hi = 0;  // owned mark planes (lo, hi]; lo > hi: all
   int curve = 0;          // 1: subpoly_(force=False) semantics
   int shards = 1;         // >1: one x-slab of a sharded complex
   int pend_tight = 0;
@@ -633,7 +633,7 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
     if (lb_begin(e, lb_tiles(e->E), s, &lb)) return -1;
     TIMED("split", 16.0 * e->E,
           launch_split_lb(P<int32_t>(e->edges), e->E, col, eps, e->V, P<int32_t>(e->sa),
-                          P<int32_t>(e->sb), e->dup_mark, P<uint64_t>(e->cur.grid), P<int64_t>(e->ctr),
+                          P<int32_t>(e->sb), P<int64_t>(e->ctr),
                           e->curve ? P<int32_t>(e->cv[CV_EIDX]) : nullptr, lb, s));
     if (read_ctr(e, s)) return -1;
     S = e->h_ctr[CTR_S];
@@ -653,8 +653,9 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
       TIMED("forward_new", (12.0 + 8.0 + 4.0 * (e->K - e->valid_from) + 32.0) * S,
             launch_forward_new(e->net, P<float>(e->cur.xyz) + 3 * e->V, S, P<float>(e->cur.pre),
                                e->cur.cap, e->V, e->valid_from, P<int32_t>(e->sa), P<int32_t>(e->sb),
-                               idx, P<uint64_t>(e->cur.pos), P<uint64_t>(e->cur.zero),
-                               P<uint64_t>(e->cur.grid), P<uint64_t>(e->shared), P<int64_t>(e->ctr), s));
+                               idx, e->own_lo, e->own_hi, P<uint64_t>(e->cur.pos),
+                               P<uint64_t>(e->cur.zero), P<uint64_t>(e->cur.grid),
+                               P<uint64_t>(e->shared), P<int64_t>(e->ctr), s));
     } else {
       if (buf_ensure(e->stage, (size_t)S * e->K * sizeof(float), s)) return -1;
       TIMED("forward", (12.0 + 4.0 * e->K) * S,
@@ -1338,8 +1339,9 @@ extern "C" int tnp_engine_faces_export(tnp_engine* e, int64_t* d_tri, float* d_f
 // ---------------------------------------------------------------------------
 // slab boundary + kernel timer controls
 // ---------------------------------------------------------------------------
-extern "C" int tnp_engine_set_dup_plane(tnp_engine* e, int mark) {
-  e->dup_mark = mark;
+extern "C" int tnp_engine_set_owned(tnp_engine* e, int lo, int hi) {
+  e->own_lo = lo;
+  e->own_hi = hi;
   return 0;
 }
 

@@ -30,11 +30,12 @@ int launch_forward(const NetDev& net, const float* xyz, int64_t n, float* pre,
                    int64_t ld, int group, hipStream_t s, float* out2 = nullptr);
 // new vertices of a flat step, forward with the fused epilogue (net.hip
 // k_forward_new): cache planes >= keep_from at slots V.., keys, shared
-// planes, failover predicate -> ctr[CTR_FAIL]; then the override itself
+// planes, failover predicate -> ctr[CTR_FAIL], new vertices outside the
+// owned slab (own_lo, own_hi] -> ctr[CTR_DUP]; then the override itself
 int launch_forward_new(const NetDev& net, const float* xyz, int64_t n, float* pre, int64_t ld,
                        int64_t V, int keep_from, const int32_t* sa, const int32_t* sb, int idx,
-                       uint64_t* pos, uint64_t* zero, uint64_t* grid, uint64_t* shared,
-                       int64_t* ctr, hipStream_t s);
+                       int own_lo, int own_hi, uint64_t* pos, uint64_t* zero, uint64_t* grid,
+                       uint64_t* shared, int64_t* ctr, hipStream_t s);
 int launch_override_new(int64_t n, int override_, const uint64_t* shared, float* pre, int64_t ld,
                         int keep_from, int64_t V, uint64_t* pos, uint64_t* zero,
                         const int64_t* ctr, hipStream_t s);

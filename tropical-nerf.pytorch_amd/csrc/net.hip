@@ -96,8 +96,9 @@ template <int LV, int H, int NL>
 __global__ void __launch_bounds__(TNP_BLOCK)
 k_forward_new(NetDev net, const float* __restrict__ xyz, int64_t n, float* __restrict__ pre,
               int64_t ld, int64_t V, int keep_from, const int32_t* __restrict__ sa,
-              const int32_t* __restrict__ sb, int idx, uint64_t* pos, uint64_t* zero,
-              uint64_t* __restrict__ grid, uint64_t* __restrict__ shared, int64_t* __restrict__ ctr) {
+              const int32_t* __restrict__ sb, int idx, int own_lo, int own_hi, uint64_t* pos,
+              uint64_t* zero, uint64_t* __restrict__ grid, uint64_t* __restrict__ shared,
+              int64_t* __restrict__ ctr) {
   constexpr int IN = 2 * LV;
   constexpr int NW = H * IN + H + (NL - 2) * (H * H + H) + 2 * H + 2;
   __shared__ float w[NW];
@@ -152,10 +153,22 @@ k_forward_new(NetDev net, const float* __restrict__ xyz, int64_t n, float* __res
     bad |= ((m >> p) & 1) && fabsf(v) > eps;
     pos[V + i] = ps;
     zero[V + i] = zs;
-    grid[V + i] = grid_word(net.marks, net.n_marks, eps, x);
     shared[i] = m;
   }
+  const uint64_t g = grid_word(net.marks, net.n_marks, eps, x);
+  if (live) grid[V + i] = g;
   if (__ballot(live && bad) && tnp::lane() == 0) tnp::or_sticky(&ctr[CTR_FAIL], 1ull);
+  if (own_lo <= own_hi) {
+    // x-slab ownership of the new vertex: on mark plane p -> owned iff
+    // own_lo < p <= own_hi (plane 0 by the first shard); in the cell above
+    // mark c -> owned iff own_lo <= c < own_hi
+    const int c = tnp::grid_off(g, 0);
+    const bool owned = tnp::grid_zero(g, 0) ? ((c > own_lo || (own_lo == 0 && c == 0)) && c <= own_hi)
+                                            : (c >= own_lo && c < own_hi);
+    const uint64_t halo = __ballot(live && !owned);
+    if (halo && tnp::lane() == 0)
+      atomicAdd((unsigned long long*)&ctr[CTR_DUP], (unsigned long long)__popcll(halo));
+  }
 }
 
 // the override itself (masked_fill_ of the shared planes, subpoly_debug.py:48)
@@ -281,13 +294,14 @@ int launch_forward(const NetDev& net, const float* xyz, int64_t n, float* pre, i
 
 int launch_forward_new(const NetDev& net, const float* xyz, int64_t n, float* pre, int64_t ld,
                        int64_t V, int keep_from, const int32_t* sa, const int32_t* sb, int idx,
-                       uint64_t* pos, uint64_t* zero, uint64_t* grid, uint64_t* shared,
-                       int64_t* ctr, hipStream_t s) {
+                       int own_lo, int own_hi, uint64_t* pos, uint64_t* zero, uint64_t* grid,
+                       uint64_t* shared, int64_t* ctr, hipStream_t s) {
   if (n <= 0) return 0;
   if (!net_supported(net)) { tnp_set_error("unsupported net shape"); return -1; }
   TNP_DISPATCH(net.n_levels, {
     hipLaunchKernelGGL((k_forward_new<L_, 16, 3>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net,
-                       xyz, n, pre, ld, V, keep_from, sa, sb, idx, pos, zero, grid, shared, ctr);
+                       xyz, n, pre, ld, V, keep_from, sa, sb, idx, own_lo, own_hi, pos, zero, grid,
+                       shared, ctr);
   });
   TNP_CHECK(hipGetLastError());
   return 0;

@@ -35,18 +35,10 @@ enum {
 
 int64_t step_tiles(int64_t n);
 int64_t lb_tiles(int64_t n);  // tiles of the single-pass (look-back) kernels
-int launch_split_count(const int32_t* edges, int64_t E, const float* col, float eps, int32_t* blk,
-                       hipStream_t s);
-// eidx != null (curve path): record each split's edge index instead of
-// rewiring the edge (the strict filter decides later which splits survive)
-int launch_split_emit(int32_t* edges, int64_t E, const float* col, float eps, const int64_t* blkoff,
-                      int64_t V, int32_t* sa, int32_t* sb, int dup_mark, const uint64_t* grid,
-                      int64_t* ctr, int32_t* eidx, hipStream_t s);
 // single-pass split over lb_tiles(E) look-back tiles (E > 0): S -> ctr[CTR_S];
 // sa/sb (and eidx if given) need capacity E
 int launch_split_lb(int32_t* edges, int64_t E, const float* col, float eps, int64_t V, int32_t* sa,
-                    int32_t* sb, int dup_mark, const uint64_t* grid, int64_t* ctr, int32_t* eidx,
-                    const TnpLB& lb, hipStream_t s);
+                    int32_t* sb, int64_t* ctr, int32_t* eidx, const TnpLB& lb, hipStream_t s);
 int launch_new_vertices(const int32_t* sa, const int32_t* sb, int64_t S, const float* col,
                         float eps, float* xyz, int64_t V, hipStream_t s);
 int launch_fail_check(const int32_t* sa, const int32_t* sb, int64_t S, int idx,

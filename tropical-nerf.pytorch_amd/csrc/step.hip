@@ -42,80 +42,13 @@ __device__ __forceinline__ bool split_test(const float* __restrict__ col, const 
   return (__fmul_rn(d0, d1) < 0.f) && (fabsf(d0) > eps) && (fabsf(d1) > eps);
 }
 
-__global__ void __launch_bounds__(TNP_BLOCK)
-k_split_count(const int32_t* __restrict__ edges, int64_t E, const float* __restrict__ col,
-              float eps, int32_t* __restrict__ blk) {
-  __shared__ int lds[TNP_WAVES];
-  int64_t base = (int64_t)blockIdx.x * TILE;
-  int c = 0;
-#pragma unroll
-  for (int k = 0; k < IPT; ++k) {
-    int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
-    if (i < E) c += split_test(col, edges + 2 * i, eps);
-  }
-  c = tnp::wave_sum(c);
-  if (tnp::lane() == 0) lds[tnp::wave()] = c;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int t = 0;
-    for (int w = 0; w < TNP_WAVES; ++w) t += lds[w];
-    blk[blockIdx.x] = t;
-  }
-}
-
-// new vertex r gets id V + r in edge order (masked_scatter_, subpoly.py:211)
-__global__ void __launch_bounds__(TNP_BLOCK)
-k_split_emit(int32_t* __restrict__ edges, int64_t E, const float* __restrict__ col, float eps,
-             const int64_t* __restrict__ blkoff, int64_t V, int32_t* __restrict__ sa,
-             int32_t* __restrict__ sb, int dup_mark, const uint64_t* __restrict__ grid,
-             int64_t* __restrict__ ctr, int32_t* __restrict__ eidx) {
-  __shared__ int lds[TNP_WAVES];
-  int64_t base = (int64_t)blockIdx.x * TILE;
-  int64_t run = blkoff[blockIdx.x];
-  int dup = 0;
-  for (int k = 0; k < IPT; ++k) {
-    int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
-    bool f = (i < E) && split_test(col, edges + 2 * i, eps);
-    int tot;
-    int r = tnp::block_rank(f, lds, tot);
-    if (f) {
-      int64_t id = run + r;
-      int a = edges[2 * i], b = edges[2 * i + 1];
-      sa[id] = a;
-      sb[id] = b;
-      if (eidx) eidx[id] = (int32_t)i;
-      else edges[2 * i + 1] = (int32_t)(V + id);
-      if (dup_mark >= 0) {
-        // edge lying in this slab's upper boundary mark plane (x = mark):
-        // the neighbouring slab splits the same edge, count it once
-        uint64_t ga = grid[a], gb = grid[b];
-        dup += tnp::grid_zero(ga, 0) && tnp::grid_zero(gb, 0) && tnp::grid_off(ga, 0) == dup_mark &&
-               tnp::grid_off(gb, 0) == dup_mark;
-      }
-    }
-    run += tot;
-  }
-  if (dup_mark >= 0) {  // one atomic per block
-    dup = tnp::wave_sum(dup);
-    __syncthreads();
-    if (tnp::lane() == 0) lds[tnp::wave()] = dup;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      int t = 0;
-      for (int w = 0; w < TNP_WAVES; ++w) t += lds[w];
-      if (t) atomicAdd((unsigned long long*)&ctr[CTR_DUP], (unsigned long long)t);
-    }
-  }
-}
-
 // single pass (replaces split_count -> scan -> split_emit): tile by ticket,
 // decoupled look-back for the tile's first new-vertex id; the last tile
 // writes S to ctr[CTR_S].  sa/sb/eidx need capacity E.
 __global__ void __launch_bounds__(TNP_BLOCK)
 k_split_lb(int32_t* __restrict__ edges, int64_t E, int64_t ntiles, const float* __restrict__ col,
-           float eps, int64_t V, int32_t* __restrict__ sa, int32_t* __restrict__ sb, int dup_mark,
-           const uint64_t* __restrict__ grid, int64_t* __restrict__ ctr, int32_t* __restrict__ eidx,
-           TnpLB lb) {
+           float eps, int64_t V, int32_t* __restrict__ sa, int32_t* __restrict__ sb,
+           int64_t* __restrict__ ctr, int32_t* __restrict__ eidx, TnpLB lb) {
   __shared__ int cnt[LIPT][TNP_WAVES];
   __shared__ int64_t slot;
   const int64_t tile = tnp::lb_tile(lb, &slot);
@@ -136,7 +69,6 @@ k_split_lb(int32_t* __restrict__ edges, int64_t E, int64_t ntiles, const float* 
     for (int w = 0; w < TNP_WAVES; ++w) agg += cnt[k][w];
   const int64_t prefix = tnp::lb_prefix(lb, tile, agg, &slot);
   int64_t run = prefix;
-  int dup = 0;
 #pragma unroll
   for (int k = 0; k < LIPT; ++k) {
     int64_t off = run;
@@ -155,21 +87,10 @@ k_split_lb(int32_t* __restrict__ edges, int64_t E, int64_t ntiles, const float* 
       sb[id] = b;
       if (eidx) eidx[id] = (int32_t)i;
       else edges[2 * i + 1] = (int32_t)(V + id);
-      if (dup_mark >= 0) {
-        // edge lying in this slab's upper boundary mark plane (x = mark):
-        // the neighbouring slab splits the same edge, count it once
-        const uint64_t ga = grid[a], gb = grid[b];
-        dup += tnp::grid_zero(ga, 0) && tnp::grid_zero(gb, 0) && tnp::grid_off(ga, 0) == dup_mark &&
-               tnp::grid_off(gb, 0) == dup_mark;
-      }
     }
     run += tot;
   }
   if (tile == ntiles - 1 && threadIdx.x == 0) ctr[CTR_S] = prefix + agg;
-  if (dup_mark >= 0) {
-    dup = tnp::wave_sum(dup);
-    if (tnp::lane() == 0 && dup) atomicAdd((unsigned long long*)&ctr[CTR_DUP], (unsigned long long)dup);
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -871,27 +792,11 @@ k_active_planes(const int32_t* __restrict__ edges, int64_t E, uint64_t amask,
 int64_t step_tiles(int64_t n) { return (n + TILE - 1) / TILE; }
 int64_t lb_tiles(int64_t n) { return (n + LTILE - 1) / LTILE; }
 
-int launch_split_count(const int32_t* edges, int64_t E, const float* col, float eps, int32_t* blk,
-                       hipStream_t s) {
-  hipLaunchKernelGGL(k_split_count, dim3((unsigned)step_tiles(E)), dim3(TNP_BLOCK), 0, s, edges,
-                     E, col, eps, blk);
-  TNP_CHECK(hipGetLastError());
-  return 0;
-}
-int launch_split_emit(int32_t* edges, int64_t E, const float* col, float eps, const int64_t* blkoff,
-                      int64_t V, int32_t* sa, int32_t* sb, int dup_mark, const uint64_t* grid,
-                      int64_t* ctr, int32_t* eidx, hipStream_t s) {
-  hipLaunchKernelGGL(k_split_emit, dim3((unsigned)step_tiles(E)), dim3(TNP_BLOCK), 0, s, edges, E,
-                     col, eps, blkoff, V, sa, sb, dup_mark, grid, ctr, eidx);
-  TNP_CHECK(hipGetLastError());
-  return 0;
-}
 int launch_split_lb(int32_t* edges, int64_t E, const float* col, float eps, int64_t V, int32_t* sa,
-                    int32_t* sb, int dup_mark, const uint64_t* grid, int64_t* ctr, int32_t* eidx,
-                    const TnpLB& lb, hipStream_t s) {
+                    int32_t* sb, int64_t* ctr, int32_t* eidx, const TnpLB& lb, hipStream_t s) {
   const int64_t tiles = lb_tiles(E);
   hipLaunchKernelGGL(k_split_lb, dim3((unsigned)tiles), dim3(TNP_BLOCK), 0, s, edges, E, tiles, col,
-                     eps, V, sa, sb, dup_mark, grid, ctr, eidx, lb);
+                     eps, V, sa, sb, ctr, eidx, lb);
   TNP_CHECK(hipGetLastError());
   return 0;
 }

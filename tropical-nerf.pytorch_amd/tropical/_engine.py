@@ -93,8 +93,10 @@ class Engine:
         _hip.check(_hip.lib().tnp_engine_set_shards(self.h, int(world)), "tnp_engine_set_shards")
         return self
 
-    def set_dup_plane(self, mark: int):
-        _hip.check(_hip.lib().tnp_engine_set_dup_plane(self.h, int(mark)), "tnp_engine_set_dup_plane")
+    def set_owned(self, lo: int = 1, hi: int = 0):
+        """This shard owns mark planes (lo, hi] and the cells between
+        (lo > hi: everything); splits outside are reported as S_dup."""
+        _hip.check(_hip.lib().tnp_engine_set_owned(self.h, int(lo), int(hi)), "tnp_engine_set_owned")
 
     def kernel_timer(self, on: bool):
         """on=True: start HIP-event timing of every engine launch; on=False:
