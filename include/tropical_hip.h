@@ -206,6 +206,40 @@ int tnp_debug_ops(const float* d_a, const float* d_b, const float* d_c, int64_t 
 int tnp_engine_faces_debug(tnp_engine* eng, float* d_scores, int64_t cap, int64_t* F,
                            int64_t* width, void* stream);
 
+/* ---- `-e` evaluation stack (train.py:275-354; csrc/evaluate.hip) ------- */
+
+/* Marching cubes over vol[n0][n1][n2] (x slowest), inside = value < iso,
+ * case table int8 [256][16] (tropical/utils/mc_table.py).  Replaces
+ * mcubes.marching_cubes (train.py:284).  Phase 1: d_eoff [3*n0*n1*n2 + 1]
+ * int64 -> vertex id of every crossed lattice edge (point-major, axis
+ * minor), d_coff [(n0-1)(n1-1)(n2-1) + 1] int64 -> first triangle of every
+ * cube; returns the vertex and triangle counts.  Phase 2: vertices fp32
+ * [n_verts][3] in index space, triangles int64 [n_tris][3]. */
+int tnp_mc_count(const float* d_vol, int n0, int n1, int n2, float iso, const int8_t* d_table,
+                 int64_t* d_eoff, int64_t* d_coff, int64_t* n_verts, int64_t* n_tris,
+                 void* stream);
+int tnp_mc_emit(const float* d_vol, int n0, int n1, int n2, float iso, const int8_t* d_table,
+                const int64_t* d_eoff, const int64_t* d_coff, float* d_verts, int64_t* d_tris,
+                void* stream);
+
+/* Nearest-hit ray casting against a triangle mesh (replaces
+ * cubvh.cuBVH(vertices, faces).ray_trace, chamfer_distance.py:184-212):
+ * uniform-grid acceleration over the caller's bounding box; the mesh
+ * buffers must outlive the caster.  cast: t (fp32, +inf on a miss) and face
+ * id (-1 on a miss) per ray; rays are origins/directions fp32 [n][3]. */
+typedef struct tnp_raycaster tnp_raycaster;
+int tnp_raycaster_create(tnp_raycaster** out, int device);
+void tnp_raycaster_destroy(tnp_raycaster* rc);
+int tnp_raycaster_build(tnp_raycaster* rc, const float* d_V, int64_t nV, const int32_t* d_F,
+                        int64_t nF, const float* bbox_lo, const float* bbox_hi, void* stream);
+int tnp_raycaster_cast(tnp_raycaster* rc, const float* d_o, const float* d_d, int64_t nR,
+                       float* d_t, int32_t* d_face, void* stream);
+
+/* Exact nearest-neighbour L2 distance of every point of a [na][3] to the set
+ * b [nb][3] (replaces sklearn NearestNeighbors in chamfer_distance.py:39-48). */
+int tnp_nn_min_dist(const float* d_a, int64_t na, const float* d_b, int64_t nb, float* d_out,
+                    void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -73,6 +73,14 @@ SIGNATURES = {
     "tnp_debug_ops": (C.c_int, [_VP, _VP, _VP, C.c_int64, _VP, _VP]),
     "tnp_engine_faces_debug": (C.c_int, [_VP, _VP, C.c_int64, _P64, _P64, _VP]),
     "tnp_engine_kernel_timer": (C.c_int, [_VP, C.c_int, _VP, _P32]),
+    "tnp_mc_count": (C.c_int, [_VP, C.c_int, C.c_int, C.c_int, _F, _VP, _VP, _VP, _P64, _P64, _VP]),
+    "tnp_mc_emit": (C.c_int, [_VP, C.c_int, C.c_int, C.c_int, _F, _VP, _VP, _VP, _VP, _VP, _VP]),
+    "tnp_raycaster_create": (C.c_int, [C.POINTER(_VP), C.c_int]),
+    "tnp_raycaster_destroy": (None, [_VP]),
+    "tnp_raycaster_build": (C.c_int, [_VP, _VP, _I64, _VP, _I64, C.POINTER(C.c_float),
+                                      C.POINTER(C.c_float), _VP]),
+    "tnp_raycaster_cast": (C.c_int, [_VP, _VP, _VP, _I64, _VP, _VP, _VP]),
+    "tnp_nn_min_dist": (C.c_int, [_VP, _I64, _VP, _I64, _VP, _VP]),
     "tnp_engine_kernel_stat": (C.c_int, [_VP, C.c_int, C.c_char_p, C.c_int, C.POINTER(C.c_double),
                                          _P64, C.POINTER(C.c_double)]),
 }
