@@ -156,9 +156,11 @@ struct tnp_engine {
   // faces output
   Buf tri, faces;
   int64_t n_tri = 0, n_faces = 0, dbg_F = 0, dbg_W = 0;
-  Buf lb;                  // look-back state: [0] ticket counter, [1..] tile status words
-  uint64_t lb_tickets = 0;  // tickets issued so far
-  uint32_t lb_epoch = 0;
+  // look-back states (a kernel may run two chains): [0] ticket counter,
+  // [1..] tile status words; tickets issued so far; launch epoch
+  Buf lb[2];
+  uint64_t lb_tickets[2] = {0, 0};
+  uint32_t lb_epoch[2] = {0, 0};
   Buf fscr[12];
   Buf fscr2[32];
   Buf cv[CV_N];
@@ -195,25 +197,26 @@ static void ktimer_end(tnp_engine* e, int t, hipStream_t s) {
     ktimer_end(e, _t, s);                                          \
   } while (0)
 
-// look-back state for a single-pass launch of `tiles` tiles (common.h TnpLB)
-static int lb_begin(tnp_engine* e, int64_t tiles, hipStream_t s, TnpLB* out) {
+// look-back state `w` for a single-pass launch of `tiles` tiles (common.h TnpLB)
+static int lb_begin(tnp_engine* e, int64_t tiles, hipStream_t s, TnpLB* out, int w = 0) {
+  Buf& b = e->lb[w];
   size_t need = (size_t)(tiles + 1) * sizeof(uint64_t);
-  if (need > e->lb.bytes || !e->lb.p) {
-    if (buf_ensure(e->lb, std::max(need, (size_t)64 << 10), s)) return -1;
-    TNP_CHECK(hipMemsetAsync(e->lb.p, 0, e->lb.bytes, s));  // flag 0: no record
-    e->lb_tickets = 0;
+  if (need > b.bytes || !b.p) {
+    if (buf_ensure(b, std::max(need, (size_t)64 << 10), s)) return -1;
+    TNP_CHECK(hipMemsetAsync(b.p, 0, b.bytes, s));  // flag 0: no record
+    e->lb_tickets[w] = 0;
   }
-  e->lb_epoch = (e->lb_epoch + 1) & 0x3FFFFFu;
-  if (e->lb_epoch == 0) {  // wrapped: clear records that could carry a reused epoch
-    TNP_CHECK(hipMemsetAsync(e->lb.p, 0, e->lb.bytes, s));
-    e->lb_tickets = 0;
-    e->lb_epoch = 1;
+  e->lb_epoch[w] = (e->lb_epoch[w] + 1) & 0x3FFFFFu;
+  if (e->lb_epoch[w] == 0) {  // wrapped: clear records that could carry a reused epoch
+    TNP_CHECK(hipMemsetAsync(b.p, 0, b.bytes, s));
+    e->lb_tickets[w] = 0;
+    e->lb_epoch[w] = 1;
   }
-  out->ticket = static_cast<unsigned long long*>(e->lb.p);
-  out->st = static_cast<uint64_t*>(e->lb.p) + 1;
-  out->tbase = e->lb_tickets;
-  out->epoch = e->lb_epoch;
-  e->lb_tickets += (uint64_t)tiles;
+  out->ticket = static_cast<unsigned long long*>(b.p);
+  out->st = static_cast<uint64_t*>(b.p) + 1;
+  out->tbase = e->lb_tickets[w];
+  out->epoch = e->lb_epoch[w];
+  e->lb_tickets[w] += (uint64_t)tiles;
   return 0;
 }
 
@@ -333,7 +336,7 @@ extern "C" void tnp_engine_destroy(tnp_engine* e) {
                  &e->stage, &e->shared, &e->members, &e->cellcnt, &e->cellcur, &e->celloff,
                  &e->ent_v, &e->ent_g, &e->ent_p, &e->ent_z, &e->tcnt, &e->toff, &e->bcell,
                  &e->bstat, &e->ckeys_a, &e->ckeys_b, &e->sort_scr, &e->flags, &e->used, &e->nid,
-                 &e->ctr, &e->tri, &e->faces, &e->lb};
+                 &e->ctr, &e->tri, &e->faces, &e->lb[0], &e->lb[1]};
   for (Buf* b : bufs) buf_free(*b, s);
   for (Buf& b : e->fscr) buf_free(b, s);
   for (Buf& b : e->fscr2) buf_free(b, s);
@@ -630,7 +633,7 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
     if (buf_ensure(e->sb, e->E * sizeof(int32_t), s)) return -1;
     if (e->curve && buf_ensure(e->cv[CV_EIDX], e->E * sizeof(int32_t), s)) return -1;
     TnpLB lb;
-    if (lb_begin(e, lb_tiles(e->E), s, &lb)) return -1;
+    if (lb_begin(e, split_tiles(e->E), s, &lb)) return -1;
     TIMED("split", 16.0 * e->E,
           launch_split_lb(P<int32_t>(e->edges), e->E, col, eps, e->V, P<int32_t>(e->sa),
                           P<int32_t>(e->sb), P<int64_t>(e->ctr),
@@ -720,7 +723,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   if (buf_ensure(e->members, std::max<int64_t>(NV, 1) * sizeof(int32_t), s)) return -1;
   {
     TnpLB lb;
-    if (V > 0 && lb_begin(e, lb_tiles(V), s, &lb)) return -1;
+    if (V > 0 && lb_begin(e, split_tiles(V), s, &lb)) return -1;
     TIMED("hits", 8.0 * V + 4.0 * S,
           launch_hits(col, P<int32_t>(e->used), V, eps, P<int32_t>(e->members), S, ctr, lb, s));
   }
@@ -729,7 +732,10 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   //    (cell, member) entry per spanned cell, radix-sorted by cell
   const int NC = e->net.n_marks + 2;
   const int64_t ncell = (int64_t)NC * NC * NC;
-  const int64_t M = S + V;  // capacity; the kernels read the hit count on the device
+  // the live member count sizes the span pass and its scan (V counts every
+  // slot, live or dead: sizing by it would scan ~V elements per step)
+  if (read_ctr(e, s)) return -1;
+  const int64_t M = S + e->h_ctr[CTR_H];
   if (buf_ensure(e->spcnt, std::max<int64_t>(M, 1) * sizeof(int32_t), s)) return -1;
   if (buf_ensure(e->spoff, std::max<int64_t>(M, 1) * sizeof(int64_t), s)) return -1;
   if (buf_ensure(e->part, (int64_t)(tnp_grid(M) + 1) * sizeof(int64_t), s)) return -1;
@@ -768,22 +774,25 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   if (buf_ensure(e->celloff, ncell * sizeof(int64_t), s)) return -1;
   if (buf_ensure(e->cellend, ncell * sizeof(int64_t), s)) return -1;
   if (buf_ensure(e->cellcnt, ncell * sizeof(int32_t), s)) return -1;
-  if (buf_ensure(e->tcnt, ncell * sizeof(int32_t), s)) return -1;
-  if (buf_ensure(e->toff, ncell * sizeof(int64_t), s)) return -1;
+  if (buf_ensure(e->tcnt, ncell * sizeof(int32_t), s)) return -1;  // pair cells (ids)
+  if (buf_ensure(e->toff, ncell * sizeof(int64_t), s)) return -1;  // their first pair
   TNP_CHECK(hipMemsetAsync(e->celloff.p, 0, ncell * sizeof(int64_t), s));
   TNP_CHECK(hipMemsetAsync(e->cellend.p, 0, ncell * sizeof(int64_t), s));
   TIMED("cell_bounds", 12.0 * T,
         launch_cell_bounds(skey, T, P<int64_t>(e->celloff), P<int64_t>(e->cellend), s));
-  // member pairs per cell -> flattened pair space offsets (total = tests)
-  if (launch_cell_counts(P<int64_t>(e->celloff), P<int64_t>(e->cellend), ncell, P<int32_t>(e->cellcnt),
-                         P<int32_t>(e->tcnt), ctr, s)) return -1;
-  if (scan_counts(e, P<int32_t>(e->tcnt), P<int64_t>(e->toff), ncell, CTR_TESTS, s)) return -1;
-  if (buf_ensure(e->ent_g, T1 * sizeof(uint64_t), s)) return -1;
-  if (buf_ensure(e->ent_p, T1 * sizeof(uint64_t), s)) return -1;
-  if (buf_ensure(e->ent_z, T1 * sizeof(uint64_t), s)) return -1;
+  // cells holding member pairs, compacted, with their flattened pair space
+  // offsets (total = tests); one pass, two look-back chains
+  {
+    TnpLB lr, lp;
+    const int64_t pt = pair_cell_tiles(ncell);
+    if (lb_begin(e, pt, s, &lr, 0) || lb_begin(e, pt, s, &lp, 1)) return -1;
+    TIMED("pair_cells", 28.0 * ncell,
+          launch_pair_cells(P<int64_t>(e->celloff), P<int64_t>(e->cellend), ncell, P<int32_t>(e->cellcnt),
+                            P<int32_t>(e->tcnt), P<int64_t>(e->toff), ctr, lr, lp, s));
+  }
+  if (buf_ensure(e->ent_g, T1 * sizeof(CellEnt), s)) return -1;
   TIMED("entry_keys", 52.0 * T,
-        launch_entry_keys(sval, T, grid, pos, zero, P<uint64_t>(e->ent_g), P<uint64_t>(e->ent_p),
-                          P<uint64_t>(e->ent_z), s));
+        launch_entry_keys(sval, T, grid, pos, zero, P<CellEnt>(e->ent_g), s));
 
   // 4. connecting edges: test every in-cell member pair once, append the
   //    emitted ones, radix-sort them (lexicographic c_new, subpoly.py:243-244).
@@ -803,8 +812,8 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     if (!chunks_ok) {
       if (buf_ensure(e->bcell, bcap * sizeof(int32_t), s)) return -1;
       if (attempt > 0) TNP_CHECK(hipMemsetAsync(ctr + CTR_BOVF, 0, sizeof(int64_t), s));
-      if (launch_chunk_cells(P<int64_t>(e->toff), P<int32_t>(e->tcnt), ncell, P<int32_t>(e->bcell),
-                             bcap, ctr, s)) return -1;
+      if (launch_chunk_cells(P<int64_t>(e->toff), P<int32_t>(e->tcnt), P<int32_t>(e->cellcnt), ncell,
+                             P<int32_t>(e->bcell), bcap, ctr, s)) return -1;
     }
     if (buf_ensure(e->ckeys_a, std::max<int64_t>(cap, 1) * sizeof(uint64_t), s)) return -1;
     if (attempt > 0) {  // the split zeroed the whole counter block
@@ -813,10 +822,10 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
       TNP_CHECK(hipMemsetAsync(ctr + CTR_P, 0, 2 * sizeof(int64_t), s));  // CTR_P, CTR_COMPAT
     }
     TIMED("connect", 0.0,
-          launch_connect(P<int64_t>(e->toff), P<int32_t>(e->cellcnt), P<int64_t>(e->celloff), ncell,
-                         NC, e->max_pair_tests, P<int32_t>(e->bcell), sval, P<uint64_t>(e->ent_g),
-                         P<uint64_t>(e->ent_p), P<uint64_t>(e->ent_z), idx, nb, cfmask,
-                         P<uint64_t>(e->ckeys_a), cap, ctr, P<int64_t>(e->bstat), s));
+          launch_connect(P<int64_t>(e->toff), P<int32_t>(e->tcnt), P<int32_t>(e->cellcnt),
+                         P<int64_t>(e->celloff), NC, e->max_pair_tests, P<int32_t>(e->bcell),
+                         P<CellEnt>(e->ent_g), idx, nb, cfmask, P<uint64_t>(e->ckeys_a), cap, ctr,
+                         P<int64_t>(e->bstat), s));
     if (read_ctr(e, s)) return -1;
     TT = e->h_ctr[CTR_TESTS];
     X = e->h_ctr[CTR_XK];

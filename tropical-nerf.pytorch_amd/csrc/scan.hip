@@ -22,12 +22,27 @@ k_scan_lb(const int32_t* __restrict__ in, int64_t n, int64_t ntiles, int64_t* __
   int64_t base = tile * TILE + (int64_t)threadIdx.x * IPT;
   int32_t v[IPT];
   int64_t s = 0;
+  if (base + IPT <= n && ((reinterpret_cast<uintptr_t>(in) & 15) == 0)) {
+    // full run: 16-byte loads, all in flight (a bounds branch per element
+    // would serialise them)
+    const int4* p4 = reinterpret_cast<const int4*>(in + base);
 #pragma unroll
-  for (int k = 0; k < IPT; ++k) {
-    int64_t i = base + k;
-    v[k] = i < n ? in[i] : 0;
-    s += v[k];
+    for (int q = 0; q < IPT / 4; ++q) {
+      const int4 x = p4[q];
+      v[4 * q] = x.x;
+      v[4 * q + 1] = x.y;
+      v[4 * q + 2] = x.z;
+      v[4 * q + 3] = x.w;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+      const int64_t i = base + k;
+      v[k] = i < n ? in[i] : 0;
+    }
   }
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) s += v[k];
   int64_t tot;
   int64_t ex = tnp::block_scan_excl(s, lds, tot);
   const int64_t prefix = tnp::lb_prefix(lb, tile, tot, &slot);

@@ -30,12 +30,14 @@ enum {
   CTR_KEEP = 22,    // curve path: splits surviving the strict filter
   CTR_BOVF = 23,    // pair-chunk table overflow
   CTR_XK = 24,      // connecting edges surviving this step's pruning (appended)
-  CTR_N = 25
+  CTR_R = 25,       // cells with at least one member pair
+  CTR_N = 26
 };
 
 int64_t step_tiles(int64_t n);
-int64_t lb_tiles(int64_t n);  // tiles of the single-pass (look-back) kernels
-// single-pass split over lb_tiles(E) look-back tiles (E > 0): S -> ctr[CTR_S];
+int64_t lb_tiles(int64_t n);     // tiles of the single-pass prune
+int64_t split_tiles(int64_t n);  // tiles of the single-pass split and hit passes
+// single-pass split over split_tiles(E) look-back tiles (E > 0): S -> ctr[CTR_S];
 // sa/sb (and eidx if given) need capacity E
 int launch_split_lb(int32_t* edges, int64_t E, const float* col, float eps, int64_t V, int32_t* sa,
                     int32_t* sb, int64_t* ctr, int32_t* eidx, const TnpLB& lb, hipStream_t s);
@@ -48,7 +50,7 @@ int launch_finalize_new(int64_t S, int K, int override_, const uint64_t* shared,
                         float eps, float* pre, int64_t ld, int keep_from, int64_t V, uint64_t* pos,
                         uint64_t* zero, const int64_t* ctr, hipStream_t s);
 // members = [V, V + S) ++ live vertices v < V with |col[v]| < eps (ascending,
-// single pass over lb_tiles(V) look-back tiles); count -> ctr[CTR_H]
+// single pass over split_tiles(V) look-back tiles); count -> ctr[CTR_H]
 int launch_hits(const float* col, const int32_t* alive, int64_t V, float eps, int32_t* members,
                 int64_t S, int64_t* ctr, const TnpLB& lb, hipStream_t s);
 // sort-based cell bucketing: span counts (+ A), (cell, member) entries,
@@ -62,27 +64,39 @@ int launch_span_emit(const int32_t* members, int64_t S, int64_t M, const uint64_
                      const int64_t* eoff, uint32_t* ekey, int32_t* eval, const int64_t* ctr,
                      hipStream_t s);
 int launch_cell_bounds(const uint32_t* key, int64_t T, int64_t* cstart, int64_t* cend, hipStream_t s);
-int launch_cell_counts(const int64_t* cstart, const int64_t* cend, int64_t n, int32_t* cellcnt,
-                       int32_t* tcnt, int64_t* ctr, hipStream_t s);
+// cells with >= 2 members, compacted (single pass, two look-back chains:
+// rank and pair offset): pcell[r] = cell id, ptoff[r] = first pair index of
+// that cell in the flattened pair space; cellcnt[c] = members of every cell;
+// R -> ctr[CTR_R], pairs -> ctr[CTR_TESTS], a cell above 65535 -> CTR_BIG
+int launch_pair_cells(const int64_t* cstart, const int64_t* cend, int64_t ncell, int32_t* cellcnt,
+                      int32_t* pcell, int64_t* ptoff, int64_t* ctr, const TnpLB& lb_rank,
+                      const TnpLB& lb_pairs, hipStream_t s);
+int64_t pair_cell_tiles(int64_t ncell);
+// one cell entry as the pair test reads it: the member's three packed keys
+// and id in one 32-byte record (one cache segment per entry)
+struct alignas(32) CellEnt {
+  uint64_t g, p, z;
+  int32_t v, pad;
+};
 int launch_entry_keys(const int32_t* ent_v, int64_t T, const uint64_t* grid, const uint64_t* pos,
-                      const uint64_t* zero, uint64_t* ent_g, uint64_t* ent_p, uint64_t* ent_z,
+                      const uint64_t* zero, CellEnt* ent,
                       hipStream_t s);
-int launch_cell_tcnt(const int32_t* cellcnt, int64_t n, int32_t* tcnt, int64_t* ctr, hipStream_t s);
-// connecting edges over the flattened pair space (cell-major, then (i, j<i));
-// the pair count is read on the device (ctr[CTR_TESTS]).  chunk_cells maps
-// pair chunks to cells (capacity cap chunks, overflow -> CTR_BOVF); connect
-// counts every connecting edge in ctr[CTR_X] and appends the packed keys
-// (lo << nb | hi) of those the step's pruning keeps (fmask != 0: endpoint
-// keys differ on the planes of fmask; fmask == 0: all) to keys[0, cap),
-// counted in ctr[CTR_XK]; bstat needs 3 * connect_grid() slots.
+
+// connecting edges over the flattened pair space (pair cells in order, then
+// (i, j<i) inside a cell); the pair count and R are read on the device.
+// chunk_cells maps pair chunks to pair cells (capacity cap chunks, overflow
+// -> CTR_BOVF); connect counts every connecting edge in ctr[CTR_X] and
+// appends the packed keys (lo << nb | hi) of those the step's pruning keeps
+// (fmask != 0: endpoint keys differ on the planes of fmask; fmask == 0: all)
+// to keys[0, cap), counted in ctr[CTR_XK]; bstat needs 3 * connect_grid()
+// slots.
 int64_t connect_chunks(int64_t TT);
 int64_t connect_grid();
-int launch_chunk_cells(const int64_t* toff, const int32_t* tcnt, int64_t ncell, int32_t* bcell,
-                       int64_t cap, int64_t* ctr, hipStream_t s);
-int launch_connect(const int64_t* toff, const int32_t* cellcnt, const int64_t* celloff,
-                   int64_t ncell, int NC, int64_t max_tests, const int32_t* bcell,
-                   const int32_t* ent_v, const uint64_t* ent_g, const uint64_t* ent_p,
-                   const uint64_t* ent_z, int idx, int nb, uint64_t fmask, uint64_t* keys,
+int launch_chunk_cells(const int64_t* ptoff, const int32_t* pcell, const int32_t* cellcnt,
+                       int64_t rcap, int32_t* bcell, int64_t cap, int64_t* ctr, hipStream_t s);
+int launch_connect(const int64_t* ptoff, const int32_t* pcell, const int32_t* cellcnt,
+                   const int64_t* celloff, int NC, int64_t max_tests, const int32_t* bcell,
+                   const CellEnt* ent, int idx, int nb, uint64_t fmask, uint64_t* keys,
                    int64_t cap, int64_t* ctr, int64_t* bstat, hipStream_t s);
 // single-pass pruning over [edges; e_new; c_new] (lb_tiles(E + S + X)
 // look-back tiles): kept edges in order -> out, used flags (zeroed by the

@@ -28,9 +28,12 @@ namespace {
 
 constexpr int IPT = 8;                  // items per thread per tile
 constexpr int TILE = TNP_BLOCK * IPT;   // tile of a compaction pass
-// single-pass (look-back) compactions: larger tiles, so the per-tile ticket
-// atomic and look-back round trip are amortised over 8192 items
-constexpr int LIPT = 32;
+// single-pass (look-back) compactions: items per thread of the split / hit
+// pass (SIPT) and of the prune pass (LIPT); every item's loads are issued
+// before any is used
+constexpr int SIPT = 16;
+constexpr int STILE = TNP_BLOCK * SIPT;
+constexpr int LIPT = 8;
 constexpr int LTILE = TNP_BLOCK * LIPT;
 
 // ---------------------------------------------------------------------------
@@ -44,33 +47,50 @@ __device__ __forceinline__ bool split_test(const float* __restrict__ col, const 
 
 // single pass (replaces split_count -> scan -> split_emit): tile by ticket,
 // decoupled look-back for the tile's first new-vertex id; the last tile
-// writes S to ctr[CTR_S].  sa/sb/eidx need capacity E.
+// writes S to ctr[CTR_S].  sa/sb/eidx need capacity E.  Loads are issued
+// unconditionally (clamped index) in two batches -- the edge pairs, then the
+// plane-column gathers -- so a thread has SIPT * 2 loads in flight instead
+// of a bounds branch serialising every item.
 __global__ void __launch_bounds__(TNP_BLOCK)
 k_split_lb(int32_t* __restrict__ edges, int64_t E, int64_t ntiles, const float* __restrict__ col,
            float eps, int64_t V, int32_t* __restrict__ sa, int32_t* __restrict__ sb,
            int64_t* __restrict__ ctr, int32_t* __restrict__ eidx, TnpLB lb) {
-  __shared__ int cnt[LIPT][TNP_WAVES];
+  __shared__ int cnt[SIPT][TNP_WAVES];
   __shared__ int64_t slot;
   const int64_t tile = tnp::lb_tile(lb, &slot);
-  const int64_t base = tile * LTILE;
-  uint64_t bal[LIPT];
+  const int64_t base = tile * STILE;
+  const int2* e2 = reinterpret_cast<const int2*>(edges);
+  int2 ab[SIPT];
+  float c0[SIPT], c1[SIPT];
+  uint64_t bal[SIPT];
 #pragma unroll
-  for (int k = 0; k < LIPT; ++k) {
+  for (int k = 0; k < SIPT; ++k) {
     const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
-    const bool f = (i < E) && split_test(col, edges + 2 * i, eps);
+    ab[k] = e2[i < E ? i : E - 1];
+  }
+#pragma unroll
+  for (int k = 0; k < SIPT; ++k) {
+    c0[k] = col[ab[k].x];
+    c1[k] = col[ab[k].y];
+  }
+#pragma unroll
+  for (int k = 0; k < SIPT; ++k) {
+    const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
+    const bool f = (i < E) && (__fmul_rn(c0[k], c1[k]) < 0.f) && (fabsf(c0[k]) > eps) &&
+                   (fabsf(c1[k]) > eps);
     bal[k] = __ballot(f);
     if (tnp::lane() == 0) cnt[k][tnp::wave()] = __popcll(bal[k]);
   }
   __syncthreads();
   int64_t agg = 0;
 #pragma unroll
-  for (int k = 0; k < LIPT; ++k)
+  for (int k = 0; k < SIPT; ++k)
 #pragma unroll
     for (int w = 0; w < TNP_WAVES; ++w) agg += cnt[k][w];
   const int64_t prefix = tnp::lb_prefix(lb, tile, agg, &slot);
   int64_t run = prefix;
 #pragma unroll
-  for (int k = 0; k < LIPT; ++k) {
+  for (int k = 0; k < SIPT; ++k) {
     int64_t off = run;
     int tot = 0;
 #pragma unroll
@@ -82,9 +102,8 @@ k_split_lb(int32_t* __restrict__ edges, int64_t E, int64_t ntiles, const float* 
     if ((bal[k] >> tnp::lane()) & 1) {
       const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
       const int64_t id = off + tnp::mbcnt(bal[k]);
-      const int a = edges[2 * i], b = edges[2 * i + 1];
-      sa[id] = a;
-      sb[id] = b;
+      sa[id] = ab[k].x;
+      sb[id] = ab[k].y;
       if (eidx) eidx[id] = (int32_t)i;
       else edges[2 * i + 1] = (int32_t)(V + id);
     }
@@ -167,35 +186,43 @@ __global__ void __launch_bounds__(TNP_BLOCK)
 k_hit_lb(const float* __restrict__ col, const int32_t* __restrict__ alive, int64_t V,
          int64_t ntiles, float eps, int32_t* __restrict__ members, int64_t S,
          int64_t* __restrict__ ctr, TnpLB lb) {
-  __shared__ int cnt[LIPT][TNP_WAVES];
+  __shared__ int cnt[SIPT][TNP_WAVES];
   __shared__ int64_t slot;
   const int64_t tile = tnp::lb_tile(lb, &slot);
-  const int64_t base = tile * LTILE;
-  uint64_t bal[LIPT];
+  const int64_t base = tile * STILE;
+  float c[SIPT];
+  int32_t al[SIPT];
+  uint64_t bal[SIPT];
 #pragma unroll
-  for (int k = 0; k < LIPT; ++k) {
+  for (int k = 0; k < SIPT; ++k) {  // unconditional (clamped) loads, all in flight
     const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
-    const bool f = (i < V) && (fabsf(col[i]) < eps) && alive[i];
-    bal[k] = __ballot(f);
+    const int64_t ic = i < V ? i : V - 1;
+    c[k] = col[ic];
+    al[k] = alive[ic];
+  }
+#pragma unroll
+  for (int k = 0; k < SIPT; ++k) {
+    const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
+    bal[k] = __ballot((i < V) && (fabsf(c[k]) < eps) && al[k]);
     if (tnp::lane() == 0) cnt[k][tnp::wave()] = __popcll(bal[k]);
   }
   __syncthreads();
   int64_t agg = 0;
 #pragma unroll
-  for (int k = 0; k < LIPT; ++k)
+  for (int k = 0; k < SIPT; ++k)
 #pragma unroll
     for (int w = 0; w < TNP_WAVES; ++w) agg += cnt[k][w];
   const int64_t prefix = tnp::lb_prefix(lb, tile, agg, &slot);
   int64_t run = prefix;
 #pragma unroll
-  for (int k = 0; k < LIPT; ++k) {
+  for (int k = 0; k < SIPT; ++k) {
     int64_t off = run;
     int tot = 0;
 #pragma unroll
     for (int w = 0; w < TNP_WAVES; ++w) {
-      const int c = cnt[k][w];
-      off += (w < tnp::wave()) ? c : 0;
-      tot += c;
+      const int cc = cnt[k][w];
+      off += (w < tnp::wave()) ? cc : 0;
+      tot += cc;
     }
     if ((bal[k] >> tnp::lane()) & 1)
       members[S + off + tnp::mbcnt(bal[k])] = (int32_t)(base + (int64_t)k * TNP_BLOCK + threadIdx.x);
@@ -301,33 +328,80 @@ __global__ void k_cell_bounds(const uint32_t* __restrict__ key, int64_t T,
   if (i == T - 1 || key[i + 1] != k) cend[k] = i + 1;
 }
 
-// member count and member pairs n (n - 1) / 2 per cell (CTR_BIG: > 65535)
-__global__ void k_cell_counts(const int64_t* __restrict__ cstart, const int64_t* __restrict__ cend,
-                              int64_t n, int32_t* __restrict__ cellcnt, int32_t* __restrict__ tcnt,
-                              int64_t* __restrict__ ctr) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// Pair cells: cells with >= 2 members, compacted in cell order (single pass
+// over thread-contiguous runs of PIPT cells, two decoupled look-back chains:
+// the compacted rank and the flattened pair offset).  Also the member count
+// of every cell; a cell above 65535 members flags CTR_BIG (one linear region
+// that large is the degenerate case the host refuses anyway).
+constexpr int PIPT = 16;
+constexpr int PTILE = TNP_BLOCK * PIPT;
+
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_pair_cells_lb(const int64_t* __restrict__ cstart, const int64_t* __restrict__ cend, int64_t ncell,
+                int64_t ntiles, int32_t* __restrict__ cellcnt, int32_t* __restrict__ pcell,
+                int64_t* __restrict__ ptoff, int64_t* __restrict__ ctr, TnpLB lbr, TnpLB lbp) {
+  __shared__ int64_t lds[TNP_WAVES];
+  __shared__ int64_t slot;
+  const int64_t tile = tnp::lb_tile(lbr, &slot);
+  const int64_t base = tile * PTILE + (int64_t)threadIdx.x * PIPT;
+  int32_t n[PIPT];
+  int64_t m[PIPT];
+  int64_t nr = 0, np = 0;
   bool big = false;
-  if (i < n) {
-    int64_t c = cend[i] - cstart[i];
-    big = c > 65535;
-    cellcnt[i] = (int32_t)c;
-    tcnt[i] = big ? 0 : (int32_t)(c * (c - 1) / 2);
+#pragma unroll
+  for (int k = 0; k < PIPT; ++k) {  // clamped, unconditional loads: all in flight
+    const int64_t c = base + k < ncell ? base + k : ncell - 1;
+    m[k] = cend[c] - cstart[c];
+  }
+#pragma unroll
+  for (int k = 0; k < PIPT; ++k) {
+    const int64_t c = base + k;
+    n[k] = 0;
+    if (c < ncell) {
+      big |= m[k] > 65535;
+      n[k] = m[k] > 65535 ? 0 : (int32_t)m[k];
+      cellcnt[c] = (int32_t)m[k];
+    }
+    nr += n[k] >= 2;
+    np += (int64_t)n[k] * (n[k] - 1) / 2;
   }
   if (__ballot(big) && tnp::lane() == 0) atomicOr((unsigned long long*)&ctr[CTR_BIG], 1ull);
+  int64_t tr, tp;
+  int64_t er = tnp::block_scan_excl(nr, lds, tr);
+  int64_t ep = tnp::block_scan_excl(np, lds, tp);
+  er += tnp::lb_prefix(lbr, tile, tr, &slot);
+  const int64_t pp = tnp::lb_prefix(lbp, tile, tp, &slot);
+  ep += pp;
+#pragma unroll
+  for (int k = 0; k < PIPT; ++k) {
+    if (n[k] >= 2) {
+      pcell[er] = (int32_t)(base + k);
+      ptoff[er] = ep;
+      ++er;
+      ep += (int64_t)n[k] * (n[k] - 1) / 2;
+    }
+  }
+  if (tile == ntiles - 1 && threadIdx.x == TNP_BLOCK - 1) {
+    ctr[CTR_R] = er;
+    ctr[CTR_TESTS] = ep;
+  }
 }
 
 // entry-aligned copies of the members' packed keys (read contiguously per
 // cell by the pair test)
 __global__ void k_entry_keys(const int32_t* __restrict__ ent_v, int64_t T,
                              const uint64_t* __restrict__ grid, const uint64_t* __restrict__ pos,
-                             const uint64_t* __restrict__ zero, uint64_t* __restrict__ ent_g,
-                             uint64_t* __restrict__ ent_p, uint64_t* __restrict__ ent_z) {
+                             const uint64_t* __restrict__ zero, CellEnt* __restrict__ ent) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= T) return;
-  int v = ent_v[i];
-  ent_g[i] = grid[v];
-  ent_p[i] = pos[v];
-  ent_z[i] = zero[v];
+  const int v = ent_v[i];
+  CellEnt r;
+  r.g = grid[v];
+  r.p = pos[v];
+  r.z = zero[v];
+  r.v = v;
+  r.pad = 0;
+  ent[i] = r;
 }
 
 // ---------------------------------------------------------------------------
@@ -369,21 +443,6 @@ __device__ __forceinline__ PairTest pair_test(const int cc[3], uint64_t below, u
   return t;
 }
 
-// member pairs a cell tests: n (n - 1) / 2 (cells above 65535 members flag
-// CTR_BIG: one linear region that large is the degenerate case the host
-// refuses anyway)
-__global__ void k_cell_tcnt(const int32_t* __restrict__ cellcnt, int64_t n, int32_t* __restrict__ tcnt,
-                            int64_t* __restrict__ ctr) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  bool big = false;
-  if (i < n) {
-    int64_t c = cellcnt[i];
-    big = c > 65535;
-    tcnt[i] = big ? 0 : (int32_t)(c * (c - 1) / 2);
-  }
-  if (__ballot(big) && tnp::lane() == 0) atomicOr((unsigned long long*)&ctr[CTR_BIG], 1ull);
-}
-
 // first index in [lo, hi) with a[i] > x (hi if none)
 __device__ __forceinline__ int64_t upper_bound_i64(const int64_t* __restrict__ a, int64_t lo,
                                                    int64_t hi, int64_t x) {
@@ -396,6 +455,7 @@ __device__ __forceinline__ int64_t upper_bound_i64(const int64_t* __restrict__ a
 }
 
 constexpr int CIPT = 8;                 // consecutive pair indices per thread
+constexpr int CONNECT_CELLS = TNP_BLOCK * 8 + 2;  // >= pair cells a chunk can touch
 constexpr int CCH = TNP_BLOCK * CIPT;   // pair indices per block
 
 __device__ __forceinline__ void cell_coords(int64_t cell, int NC, int cc[3]) {
@@ -414,69 +474,92 @@ __device__ __forceinline__ void cell_coords(int64_t cell, int NC, int cc[3]) {
 // so the appended order never reaches the output.
 // chunk b of the pair space starts in cell bcell[b] (written per cell: no
 // host round trip for the pair count)
-__global__ void k_chunk_cells(const int64_t* __restrict__ toff, const int32_t* __restrict__ tcnt,
-                              int64_t ncell, int32_t* __restrict__ bcell, int64_t cap,
-                              int64_t* __restrict__ ctr) {
-  int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= ncell) return;
-  int64_t n = tcnt[c];
-  if (n == 0) return;
-  int64_t lo = toff[c];
+__global__ void k_chunk_cells(const int64_t* __restrict__ ptoff, const int32_t* __restrict__ pcell,
+                              const int32_t* __restrict__ cellcnt, int64_t rcap,
+                              int32_t* __restrict__ bcell, int64_t cap, int64_t* __restrict__ ctr) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= rcap || r >= ctr[CTR_R]) return;
+  const int64_t m = cellcnt[pcell[r]];
+  const int64_t n = m * (m - 1) / 2;
+  const int64_t lo = ptoff[r];
   int64_t b0 = (lo + CCH - 1) / CCH, b1 = (lo + n + CCH - 1) / CCH;
   if (b1 > cap) atomicOr((unsigned long long*)&ctr[CTR_BOVF], 1ull);
-  for (int64_t b = b0; b < b1 && b < cap; ++b) bcell[b] = (int32_t)c;
+  for (int64_t b = b0; b < b1 && b < cap; ++b) bcell[b] = (int32_t)r;
 }
 
 // Persistent over the chunks of the pair space (count read on the device);
 // stops at once if the complex is degenerate (pairs above the limit) or the
 // chunk table overflowed -- the host reports either after the fact.
 __global__ void __launch_bounds__(TNP_BLOCK)
-k_connect(const int64_t* __restrict__ toff, const int32_t* __restrict__ cellcnt,
-          const int64_t* __restrict__ celloff, int64_t ncell, int NC, int64_t max_tests,
-          const int32_t* __restrict__ bcell, const int32_t* __restrict__ ent_v,
-          const uint64_t* __restrict__ ent_g, const uint64_t* __restrict__ ent_p,
-          const uint64_t* __restrict__ ent_z, int idx, int nb, uint64_t fmask,
-          uint64_t* __restrict__ keys, int64_t cap, int64_t* __restrict__ ctr,
-          int64_t* __restrict__ bstat) {
+k_connect(const int64_t* __restrict__ ptoff, const int32_t* __restrict__ pcell,
+          const int32_t* __restrict__ cellcnt, const int64_t* __restrict__ celloff, int NC,
+          int64_t max_tests, const int32_t* __restrict__ bcell, const CellEnt* __restrict__ ent,
+          int idx, int nb, uint64_t fmask, uint64_t* __restrict__ keys, int64_t cap,
+          int64_t* __restrict__ ctr, int64_t* __restrict__ bstat) {
   __shared__ int64_t lds[TNP_WAVES];
   __shared__ int64_t s_base;
+  // the chunk's pair-cell offsets relative to its first pair (clamped to
+  // [-1, 2^30]): every thread's cell search runs in LDS
+  __shared__ int32_t soff[CONNECT_CELLS];
   const int64_t TT = ctr[CTR_TESTS];
+  const int64_t R = ctr[CTR_R];
   if (TT > max_tests || ctr[CTR_BOVF] || ctr[CTR_BIG]) return;
   const int64_t nblk = (TT + CCH - 1) / CCH;
   const uint64_t below = (idx >= 64) ? ~0ull : ((1ull << idx) - 1ull);
   int64_t n_compat = 0, n_reg = 0, n_conn = 0;
   for (int64_t b = blockIdx.x; b < nblk; b += gridDim.x) {
-  const int64_t p0 = b * (int64_t)CCH + (int64_t)threadIdx.x * CIPT;
+  const int64_t pb = b * (int64_t)CCH;
+  const int64_t r0 = bcell[b];
+  const int64_t r_end = (b + 1 < nblk) ? (int64_t)bcell[b + 1] + 1 : R;
+  const int nr = (int)(r_end - r0);  // <= CCH + 1: every pair cell holds >= 1 pair
+  __syncthreads();  // the previous chunk is done with soff[]
+  for (int t = threadIdx.x; t < nr; t += blockDim.x) {
+    const int64_t v = ptoff[r0 + t] - pb;
+    soff[t] = (int32_t)(v < -1 ? -1 : (v > (1 << 30) ? (1 << 30) : v));
+  }
+  __syncthreads();
+  // first local cell index with soff > x (nr if none)
+  auto upper = [&](int lo, int64_t x) {
+    int hi = nr;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (soff[mid] <= x) lo = mid + 1;
+      else hi = mid;
+    }
+    return lo;
+  };
+  const int64_t p0 = pb + (int64_t)threadIdx.x * CIPT;
   uint64_t kk[CIPT];
   int ne = 0;
   if (p0 < TT) {
-    const int64_t c_end = (b + 1 < nblk) ? (int64_t)bcell[b + 1] + 1 : ncell;
-    int64_t c = upper_bound_i64(toff, bcell[b], c_end, p0) - 1;
-    int64_t q = p0 - toff[c];
+    int lc = upper(0, p0 - pb) - 1;
+    int cell = pcell[r0 + lc];
+    int64_t q = p0 - ptoff[r0 + lc];
     int64_t i = (int64_t)((1.0 + sqrt(1.0 + 8.0 * (double)q)) * 0.5);
     while (i * (i - 1) / 2 > q) --i;
     while ((i + 1) * i / 2 <= q) ++i;
     int64_t j = q - i * (i - 1) / 2;
-    int n = cellcnt[c];
-    int64_t base = celloff[c];
+    int n = cellcnt[cell];
+    int64_t base = celloff[cell];
     int cc[3];
-    cell_coords(c, NC, cc);
-    int vu = ent_v[base + i];
-    uint64_t gu = ent_g[base + i], pu = ent_p[base + i], zu = ent_z[base + i];
+    cell_coords(cell, NC, cc);
+    CellEnt eu = ent[base + i];
+    int vu = eu.v;
+    uint64_t gu = eu.g, pu = eu.p, zu = eu.z;
 #pragma unroll
     for (int k = 0; k < CIPT; ++k) {
       const int64_t p = p0 + k;
       if (p < TT) {
-        int64_t e = base + j;
-        const uint64_t pv = ent_p[e], zv = ent_z[e];
-        PairTest t = pair_test(cc, below, gu, pu, zu, ent_g[e], pv, zv);
+        const CellEnt ev = ent[base + j];
+        const uint64_t pv = ev.p, zv = ev.z;
+        PairTest t = pair_test(cc, below, gu, pu, zu, ev.g, pv, zv);
         if (t.compat) {
           n_compat++;
           n_reg += t.regions;
           n_conn += t.emit;
           // the step's pruning drops it anyway (keep_edge): never appended
           if (t.emit && (fmask == 0 || (((pu ^ pv) | (zu ^ zv)) & fmask) != 0)) {
-            uint32_t vv = (uint32_t)ent_v[e];
+            uint32_t vv = (uint32_t)ev.v;
             uint32_t lo = (uint32_t)vu < vv ? (uint32_t)vu : vv;
             uint32_t hi = (uint32_t)vu < vv ? vv : (uint32_t)vu;
             kk[ne++] = ((uint64_t)lo << nb) | hi;
@@ -486,18 +569,20 @@ k_connect(const int64_t* __restrict__ toff, const int32_t* __restrict__ cellcnt,
           j = 0;
           if (++i == n) {
             if (p + 1 < TT && k + 1 < CIPT) {
-              c = upper_bound_i64(toff, c + 1, c_end, p + 1) - 1;
-              n = cellcnt[c];
-              base = celloff[c];
-              cell_coords(c, NC, cc);
+              lc = upper(lc + 1, p + 1 - pb) - 1;
+              cell = pcell[r0 + lc];
+              n = cellcnt[cell];
+              base = celloff[cell];
+              cell_coords(cell, NC, cc);
               i = 1;
             }
           }
           if (k + 1 < CIPT && i < n) {
-            vu = ent_v[base + i];
-            gu = ent_g[base + i];
-            pu = ent_p[base + i];
-            zu = ent_z[base + i];
+            eu = ent[base + i];
+            vu = eu.v;
+            gu = eu.g;
+            pu = eu.p;
+            zu = eu.z;
           }
         }
       }
@@ -652,21 +737,63 @@ k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, uint64_t fmask, uint64_t amas
            TnpLB lb) {
   __shared__ int cnt[LIPT][TNP_WAVES];
   __shared__ int64_t slot;
+  __shared__ uint64_t acts[TNP_WAVES];
   const int64_t tile = tnp::lb_tile(lb, &slot);
   const int64_t base = tile * LTILE;
+  const int64_t last = (base + LTILE < N ? base + LTILE : N) - 1;  // last item of the tile
+  // block-uniform source of the tile: all old edges / all e_new / all c_new
+  // (straight-line loads) or a tile straddling two segments (per-item branch)
+  const int64_t ES = src.E + src.S;
+  const int kind = last < src.E ? 0 : (base >= src.E && last < ES) ? 1 : (base >= ES ? 2 : 3);
+  int a[LIPT], b[LIPT];
+  if (kind == 0) {
+    const int2* e2 = reinterpret_cast<const int2*>(src.edges);
+#pragma unroll
+    for (int k = 0; k < LIPT; ++k) {
+      const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
+      const int2 ab = e2[i < last ? i : last];
+      a[k] = ab.x;
+      b[k] = ab.y;
+    }
+  } else if (kind == 1) {
+#pragma unroll
+    for (int k = 0; k < LIPT; ++k) {
+      const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
+      const int64_t r = (i < last ? i : last) - src.E;
+      a[k] = src.sb[r];
+      b[k] = (int)(src.V + r);
+    }
+  } else if (kind == 2) {
+    const uint64_t lo_mask = (1ull << src.nb) - 1ull;
+#pragma unroll
+    for (int k = 0; k < LIPT; ++k) {
+      const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
+      const uint64_t key = src.ckeys[(i < last ? i : last) - ES];
+      a[k] = (int)(key >> src.nb);
+      b[k] = (int)(key & lo_mask);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < LIPT; ++k) {
+      const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
+      fetch_edge(src, i < last ? i : last, a[k], b[k]);
+    }
+  }
+  uint64_t pa[LIPT], pb[LIPT], za[LIPT], zb[LIPT];
+#pragma unroll
+  for (int k = 0; k < LIPT; ++k) {
+    pa[k] = pos[a[k]];
+    pb[k] = pos[b[k]];
+    za[k] = zero[a[k]];
+    zb[k] = zero[b[k]];
+  }
   uint64_t bal[LIPT];
   uint64_t act = 0;
 #pragma unroll
   for (int k = 0; k < LIPT; ++k) {
     const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
-    bool f = false;
-    if (i < N) {
-      int a, b;
-      fetch_edge(src, i, a, b);
-      const uint64_t pa = pos[a], pb = pos[b], za = zero[a], zb = zero[b];
-      f = (((pa ^ pb) | (za ^ zb)) & fmask) != 0;
-      if (f) act |= (pa ^ pb) & ~za & ~zb & amask;
-    }
+    const bool f = (i <= last) && ((((pa[k] ^ pb[k]) | (za[k] ^ zb[k])) & fmask) != 0);
+    if (f) act |= (pa[k] ^ pb[k]) & ~za[k] & ~zb[k] & amask;
     bal[k] = __ballot(f);
     if (tnp::lane() == 0) cnt[k][tnp::wave()] = __popcll(bal[k]);
   }
@@ -690,18 +817,14 @@ k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, uint64_t fmask, uint64_t amas
     }
     if ((bal[k] >> tnp::lane()) & 1) {
       const int64_t o = off + tnp::mbcnt(bal[k]);
-      int a, b;  // re-fetched: the tile's edges are L2-resident
-      fetch_edge(src, base + (int64_t)k * TNP_BLOCK + threadIdx.x, a, b);
-      out[2 * o] = a;
-      out[2 * o + 1] = b;
-      used[a] = 1;
-      used[b] = 1;
+      reinterpret_cast<int2*>(out)[o] = make_int2(a[k], b[k]);
+      used[a[k]] = 1;
+      used[b[k]] = 1;
     }
     run += tot;
   }
   if (tile == ntiles - 1 && threadIdx.x == 0) ctr[CTR_E] = prefix + agg;
   act = tnp::wave_or(act);
-  __shared__ uint64_t acts[TNP_WAVES];
   if (tnp::lane() == 0) acts[tnp::wave()] = act;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -791,10 +914,11 @@ k_active_planes(const int32_t* __restrict__ edges, int64_t E, uint64_t amask,
 // ----------------------------------------------------------------------------
 int64_t step_tiles(int64_t n) { return (n + TILE - 1) / TILE; }
 int64_t lb_tiles(int64_t n) { return (n + LTILE - 1) / LTILE; }
+int64_t split_tiles(int64_t n) { return (n + STILE - 1) / STILE; }
 
 int launch_split_lb(int32_t* edges, int64_t E, const float* col, float eps, int64_t V, int32_t* sa,
                     int32_t* sb, int64_t* ctr, int32_t* eidx, const TnpLB& lb, hipStream_t s) {
-  const int64_t tiles = lb_tiles(E);
+  const int64_t tiles = split_tiles(E);
   hipLaunchKernelGGL(k_split_lb, dim3((unsigned)tiles), dim3(TNP_BLOCK), 0, s, edges, E, tiles, col,
                      eps, V, sa, sb, ctr, eidx, lb);
   TNP_CHECK(hipGetLastError());
@@ -829,7 +953,7 @@ int launch_finalize_new(int64_t S, int K, int override_, const uint64_t* shared,
 int launch_hits(const float* col, const int32_t* alive, int64_t V, float eps, int32_t* members,
                 int64_t S, int64_t* ctr, const TnpLB& lb, hipStream_t s) {
   if (V > 0) {
-    const int64_t tiles = lb_tiles(V);
+    const int64_t tiles = split_tiles(V);
     hipLaunchKernelGGL(k_hit_lb, dim3((unsigned)tiles), dim3(TNP_BLOCK), 0, s, col, alive, V, tiles,
                        eps, members, S, ctr, lb);
   } else {
@@ -866,44 +990,40 @@ int launch_cell_bounds(const uint32_t* key, int64_t T, int64_t* cstart, int64_t*
   TNP_CHECK(hipGetLastError());
   return 0;
 }
-int launch_cell_counts(const int64_t* cstart, const int64_t* cend, int64_t n, int32_t* cellcnt,
-                       int32_t* tcnt, int64_t* ctr, hipStream_t s) {
-  hipLaunchKernelGGL(k_cell_counts, dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, cstart, cend, n, cellcnt,
-                     tcnt, ctr);
+int64_t pair_cell_tiles(int64_t ncell) { return (ncell + PTILE - 1) / PTILE; }
+int launch_pair_cells(const int64_t* cstart, const int64_t* cend, int64_t ncell, int32_t* cellcnt,
+                      int32_t* pcell, int64_t* ptoff, int64_t* ctr, const TnpLB& lb_rank,
+                      const TnpLB& lb_pairs, hipStream_t s) {
+  const int64_t tiles = pair_cell_tiles(ncell);
+  hipLaunchKernelGGL(k_pair_cells_lb, dim3((unsigned)tiles), dim3(TNP_BLOCK), 0, s, cstart, cend, ncell,
+                     tiles, cellcnt, pcell, ptoff, ctr, lb_rank, lb_pairs);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
 int launch_entry_keys(const int32_t* ent_v, int64_t T, const uint64_t* grid, const uint64_t* pos,
-                      const uint64_t* zero, uint64_t* ent_g, uint64_t* ent_p, uint64_t* ent_z,
-                      hipStream_t s) {
+                      const uint64_t* zero, CellEnt* ent, hipStream_t s) {
   if (T <= 0) return 0;
   hipLaunchKernelGGL(k_entry_keys, dim3(tnp_grid(T)), dim3(TNP_BLOCK), 0, s, ent_v, T, grid, pos, zero,
-                     ent_g, ent_p, ent_z);
-  TNP_CHECK(hipGetLastError());
-  return 0;
-}
-int launch_cell_tcnt(const int32_t* cellcnt, int64_t n, int32_t* tcnt, int64_t* ctr, hipStream_t s) {
-  hipLaunchKernelGGL(k_cell_tcnt, dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, cellcnt, n, tcnt, ctr);
+                     ent);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
 constexpr int CONNECT_GRID = 2048;  // persistent blocks (8 per CU)
 int64_t connect_chunks(int64_t TT) { return (TT + CCH - 1) / CCH; }
-int launch_chunk_cells(const int64_t* toff, const int32_t* tcnt, int64_t ncell, int32_t* bcell,
-                       int64_t cap, int64_t* ctr, hipStream_t s) {
-  hipLaunchKernelGGL(k_chunk_cells, dim3(tnp_grid(ncell)), dim3(TNP_BLOCK), 0, s, toff, tcnt, ncell,
-                     bcell, cap, ctr);
+int launch_chunk_cells(const int64_t* ptoff, const int32_t* pcell, const int32_t* cellcnt,
+                       int64_t rcap, int32_t* bcell, int64_t cap, int64_t* ctr, hipStream_t s) {
+  hipLaunchKernelGGL(k_chunk_cells, dim3(tnp_grid(rcap)), dim3(TNP_BLOCK), 0, s, ptoff, pcell, cellcnt,
+                     rcap, bcell, cap, ctr);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
-int launch_connect(const int64_t* toff, const int32_t* cellcnt, const int64_t* celloff,
-                   int64_t ncell, int NC, int64_t max_tests, const int32_t* bcell,
-                   const int32_t* ent_v, const uint64_t* ent_g, const uint64_t* ent_p,
-                   const uint64_t* ent_z, int idx, int nb, uint64_t fmask, uint64_t* keys,
+int launch_connect(const int64_t* ptoff, const int32_t* pcell, const int32_t* cellcnt,
+                   const int64_t* celloff, int NC, int64_t max_tests, const int32_t* bcell,
+                   const CellEnt* ent, int idx, int nb, uint64_t fmask, uint64_t* keys,
                    int64_t cap, int64_t* ctr, int64_t* bstat, hipStream_t s) {
-  hipLaunchKernelGGL(k_connect, dim3(CONNECT_GRID), dim3(TNP_BLOCK), 0, s, toff, cellcnt, celloff,
-                     ncell, NC, max_tests, bcell, ent_v, ent_g, ent_p, ent_z, idx, nb, fmask, keys,
-                     cap, ctr, bstat);
+  static_assert(CONNECT_CELLS >= CCH + 2, "chunk cell window");
+  hipLaunchKernelGGL(k_connect, dim3(CONNECT_GRID), dim3(TNP_BLOCK), 0, s, ptoff, pcell, cellcnt,
+                     celloff, NC, max_tests, bcell, ent, idx, nb, fmask, keys, cap, ctr, bstat);
   hipLaunchKernelGGL(k_sum_bstat, dim3(1), dim3(TNP_BLOCK), 0, s, bstat, (int64_t)CONNECT_GRID, ctr);
   TNP_CHECK(hipGetLastError());
   return 0;
