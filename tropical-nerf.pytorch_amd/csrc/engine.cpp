@@ -98,6 +98,7 @@ static T* P(Buf& b) { return static_cast<T*>(b.p); }
 
 struct VSet {
   Buf xyz, pre, pos, zero, grid;
+  Buf pz;  // (pos, zero) interleaved, 16 B per vertex: one gather for both
   int64_t cap = 0;  // rows; pre leading dimension == cap
 };
 
@@ -240,6 +241,7 @@ static int vset_ensure(tnp_engine* e, VSet& v, int64_t rows, int64_t keep_rows, 
   if (buf_ensure(n.pos, nc * sizeof(uint64_t), s)) return -1;
   if (buf_ensure(n.zero, nc * sizeof(uint64_t), s)) return -1;
   if (buf_ensure(n.grid, nc * sizeof(uint64_t), s)) return -1;
+  if (buf_ensure(n.pz, nc * 2 * sizeof(uint64_t), s)) return -1;
   if (keep_rows > 0 && v.cap > 0) {
     TNP_CHECK(hipMemcpyAsync(n.xyz.p, v.xyz.p, keep_rows * 3 * sizeof(float), hipMemcpyDeviceToDevice, s));
     TNP_CHECK(hipMemcpy2DAsync(n.pre.p, nc * sizeof(float), v.pre.p, v.cap * sizeof(float),
@@ -247,12 +249,14 @@ static int vset_ensure(tnp_engine* e, VSet& v, int64_t rows, int64_t keep_rows, 
     TNP_CHECK(hipMemcpyAsync(n.pos.p, v.pos.p, keep_rows * 8, hipMemcpyDeviceToDevice, s));
     TNP_CHECK(hipMemcpyAsync(n.zero.p, v.zero.p, keep_rows * 8, hipMemcpyDeviceToDevice, s));
     TNP_CHECK(hipMemcpyAsync(n.grid.p, v.grid.p, keep_rows * 8, hipMemcpyDeviceToDevice, s));
+    TNP_CHECK(hipMemcpyAsync(n.pz.p, v.pz.p, keep_rows * 16, hipMemcpyDeviceToDevice, s));
   }
   buf_free(v.xyz, s);
   buf_free(v.pre, s);
   buf_free(v.pos, s);
   buf_free(v.zero, s);
   buf_free(v.grid, s);
+  buf_free(v.pz, s);
   v = n;
   return 0;
 }
@@ -260,7 +264,7 @@ static int vset_ensure(tnp_engine* e, VSet& v, int64_t rows, int64_t keep_rows, 
 static int keys_for(tnp_engine* e, VSet& v, int64_t from, int64_t n, hipStream_t s) {
   return launch_keys(e->net, P<float>(v.xyz) + 3 * from, P<float>(v.pre) + from, v.cap, n, e->K,
                      P<uint64_t>(v.pos) + from, P<uint64_t>(v.zero) + from,
-                     P<uint64_t>(v.grid) + from, s);
+                     P<uint64_t>(v.grid) + from, s, P<uint64_t>(v.pz) + 2 * from);
 }
 
 // live flags of slots [from, from + n) := 1 (kept capacity: earlier flags stay)
@@ -293,7 +297,7 @@ static int compact_now(tnp_engine* e, hipStream_t s) {
                                P<float>(c.xyz), P<float>(c.pre), c.cap, P<uint64_t>(c.pos),
                                P<uint64_t>(c.zero), P<uint64_t>(c.grid), P<float>(a.xyz),
                                P<float>(a.pre), a.cap, P<uint64_t>(a.pos), P<uint64_t>(a.zero),
-                               P<uint64_t>(a.grid), s));
+                               P<uint64_t>(a.grid), P<uint64_t>(a.pz), s));
   TIMED("remap_edges", 32.0 * e->E, launch_remap_edges(P<int32_t>(e->edges), e->E, P<int64_t>(e->nid), s));
   if (read_ctr(e, s)) return -1;
   const int64_t V2 = e->h_ctr[CTR_AUX];
@@ -331,6 +335,7 @@ extern "C" void tnp_engine_destroy(tnp_engine* e) {
   VSet* sets[2] = {&e->cur, &e->alt};
   for (VSet* v : sets) {
     buf_free(v->xyz, s); buf_free(v->pre, s); buf_free(v->pos, s); buf_free(v->zero, s); buf_free(v->grid, s);
+    buf_free(v->pz, s);
   }
   Buf* bufs[] = {&e->edges, &e->edges_alt, &e->blk, &e->blkoff, &e->scan_scr, &e->sa, &e->sb,
                  &e->stage, &e->shared, &e->members, &e->cellcnt, &e->cellcur, &e->celloff,
@@ -645,20 +650,24 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
   if (S > 0) {
     if (vset_ensure(e, e->cur, e->V + S, e->V, s)) return -1;
     col = P<float>(e->cur.pre) + (int64_t)idx * e->cur.cap;  // may have moved
-    TIMED("new_vertices", 52.0 * S,
-          launch_new_vertices(P<int32_t>(e->sa), P<int32_t>(e->sb), S, col, eps, P<float>(e->cur.xyz),
-                              e->V, s));
-    if (e->curve && curve_correct(e, idx, S, s)) return -1;
+    if (e->curve) {
+      TIMED("new_vertices", 52.0 * S,
+            launch_new_vertices(P<int32_t>(e->sa), P<int32_t>(e->sb), S, col, eps, P<float>(e->cur.xyz),
+                                e->V, s));
+      if (curve_correct(e, idx, S, s)) return -1;
+    }
     if (buf_ensure(e->shared, S * sizeof(uint64_t), s)) return -1;
     e->pend_fused = !e->curve;
     if (e->pend_fused) {
-      // flat: forward + failover test + keys in one pass, straight into the cache
-      TIMED("forward_new", (12.0 + 8.0 + 4.0 * (e->K - e->valid_from) + 32.0) * S,
+      // flat: split points + forward + failover test + keys in one pass,
+      // straight into the cache
+      TIMED("forward_new", (8.0 + 8.0 + 24.0 + 12.0 + 16.0 + 4.0 * (e->K - e->valid_from) + 48.0) * S,
             launch_forward_new(e->net, P<float>(e->cur.xyz) + 3 * e->V, S, P<float>(e->cur.pre),
                                e->cur.cap, e->V, e->valid_from, P<int32_t>(e->sa), P<int32_t>(e->sb),
                                idx, e->own_lo, e->own_hi, P<uint64_t>(e->cur.pos),
                                P<uint64_t>(e->cur.zero), P<uint64_t>(e->cur.grid),
-                               P<uint64_t>(e->shared), P<int64_t>(e->ctr), s));
+                               P<uint64_t>(e->shared), P<int64_t>(e->ctr), P<uint64_t>(e->cur.pz),
+                               col, s));
     } else {
       if (buf_ensure(e->stage, (size_t)S * e->K * sizeof(float), s)) return -1;
       TIMED("forward", (12.0 + 4.0 * e->K) * S,
@@ -712,11 +721,12 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   if (e->pend_fused) {
     TIMED("override_new", 8.0 * S,
           launch_override_new(S, override_, P<uint64_t>(e->shared), P<float>(c.pre), c.cap,
-                              e->valid_from, V, pos, zero, ctr, s));
+                              e->valid_from, V, pos, zero, ctr, P<uint64_t>(c.pz), s));
   } else {
     TIMED("finalize_new", (8.0 + 4.0 * K + 4.0 * (K - e->valid_from) + 16.0) * S,
           launch_finalize_new(S, K, override_, P<uint64_t>(e->shared), P<float>(e->stage), eps,
-                              P<float>(c.pre), c.cap, e->valid_from, V, pos, zero, ctr, s));
+                              P<float>(c.pre), c.cap, e->valid_from, V, pos, zero, ctr,
+                              P<uint64_t>(c.pz), s));
   }
 
   // 2. members = new vertices ++ live hit vertices (ascending)
@@ -792,7 +802,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   }
   if (buf_ensure(e->ent_g, T1 * sizeof(CellEnt), s)) return -1;
   TIMED("entry_keys", 52.0 * T,
-        launch_entry_keys(sval, T, grid, pos, zero, P<CellEnt>(e->ent_g), s));
+        launch_entry_keys(sval, T, grid, P<uint64_t>(c.pz), P<CellEnt>(e->ent_g), s));
 
   // 4. connecting edges: test every in-cell member pair once, append the
   //    emitted ones, radix-sort them (lexicographic c_new, subpoly.py:243-244).
@@ -881,8 +891,8 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     TnpLB lb;
     if (lb_begin(e, lb_tiles(N), s, &lb)) return -1;
     TIMED("prune", 40.0 * N,
-          launch_prune_lb(eg, E, P<int32_t>(e->sb), S, V, e->ckeys, nb, X, idx, K - 1, pos, zero,
-                          P<int32_t>(e->edges_alt), P<int32_t>(e->used), ctr, lb, s));
+          launch_prune_lb(eg, E, P<int32_t>(e->sb), S, V, e->ckeys, nb, X, idx, K - 1,
+                          P<uint64_t>(c.pz), P<int32_t>(e->edges_alt), P<int32_t>(e->used), ctr, lb, s));
     TIMED("count_live", 4.0 * NV, launch_count_flags(P<int32_t>(e->used), NV, ctr, CTR_V, s));
     next_valid = e->keep_all ? 0 : std::min(idx + 1, K - 1);
     if (read_ctr(e, s)) return -1;
@@ -987,7 +997,7 @@ extern "C" int tnp_engine_surface(tnp_engine* e, void* stream, int64_t* V_out, i
                              P<float>(c.xyz), P<float>(c.pre), c.cap, P<uint64_t>(c.pos),
                              P<uint64_t>(c.zero), P<uint64_t>(c.grid), P<float>(a.xyz),
                              P<float>(a.pre), a.cap, P<uint64_t>(a.pos), P<uint64_t>(a.zero),
-                             P<uint64_t>(a.grid), s))
+                             P<uint64_t>(a.grid), P<uint64_t>(a.pz), s))
     return -1;
   if (read_ctr(e, s)) return -1;
   int64_t E2 = e->h_ctr[CTR_E], V2 = e->h_ctr[CTR_V];

@@ -29,16 +29,18 @@ int net_supported(const NetDev& n);  // 1 if an instantiation exists
 int launch_forward(const NetDev& net, const float* xyz, int64_t n, float* pre,
                    int64_t ld, int group, hipStream_t s, float* out2 = nullptr);
 // new vertices of a flat step, forward with the fused epilogue (net.hip
-// k_forward_new): cache planes >= keep_from at slots V.., keys, shared
+// k_forward_new); col != null: the split points are computed here too from
+// the plane column (xyz = slot V: written); cache planes >= keep_from at
+// slots V.., keys, shared
 // planes, failover predicate -> ctr[CTR_FAIL], new vertices outside the
 // owned slab (own_lo, own_hi] -> ctr[CTR_DUP]; then the override itself
 int launch_forward_new(const NetDev& net, const float* xyz, int64_t n, float* pre, int64_t ld,
                        int64_t V, int keep_from, const int32_t* sa, const int32_t* sb, int idx,
                        int own_lo, int own_hi, uint64_t* pos, uint64_t* zero, uint64_t* grid,
-                       uint64_t* shared, int64_t* ctr, hipStream_t s);
+                       uint64_t* shared, int64_t* ctr, uint64_t* pz, const float* col, hipStream_t s);
 int launch_override_new(int64_t n, int override_, const uint64_t* shared, float* pre, int64_t ld,
                         int keep_from, int64_t V, uint64_t* pos, uint64_t* zero,
-                        const int64_t* ctr, hipStream_t s);
+                        const int64_t* ctr, uint64_t* pz, hipStream_t s);
 int launch_encode(const NetDev& net, const float* x01, int64_t n, float* out, hipStream_t s);
 // pre plane-major; writes int64 m[n][3+K] and off[n][3] (Net.region)
 int launch_region(const NetDev& net, const float* xyz, const float* pre, int64_t ld,
@@ -48,7 +50,7 @@ int launch_sdf_grad(const NetDev& net, const float* xyz, int64_t n, float* sdf,
 // packed keys from pre (planes [0,K)) + grid word from coordinates
 int launch_keys(const NetDev& net, const float* xyz, const float* pre, int64_t ld,
                 int64_t n, int K, uint64_t* pos, uint64_t* zero, uint64_t* grid,
-                hipStream_t s);
+                hipStream_t s, uint64_t* pz = nullptr);  // pz: interleaved (pos, zero) copy
 
 // ---- scan.hip ----
 // exclusive scan of int32 counts into int64 offsets; *total (device) = sum.

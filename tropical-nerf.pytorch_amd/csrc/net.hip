@@ -94,11 +94,11 @@ k_forward(NetDev net, const float* __restrict__ xyz, int64_t n, float* __restric
 // and the MKL row-count schedule are those of k_forward (same n = S).
 template <int LV, int H, int NL>
 __global__ void __launch_bounds__(TNP_BLOCK)
-k_forward_new(NetDev net, const float* __restrict__ xyz, int64_t n, float* __restrict__ pre,
+k_forward_new(NetDev net, const float* xyz, int64_t n, float* __restrict__ pre,
               int64_t ld, int64_t V, int keep_from, const int32_t* __restrict__ sa,
               const int32_t* __restrict__ sb, int idx, int own_lo, int own_hi, uint64_t* pos,
               uint64_t* zero, uint64_t* __restrict__ grid, uint64_t* __restrict__ shared,
-              int64_t* __restrict__ ctr) {
+              int64_t* __restrict__ ctr, ulonglong2* __restrict__ pz, const float* __restrict__ scol) {
   constexpr int IN = 2 * LV;
   constexpr int NW = H * IN + H + (NL - 2) * (H * H + H) + 2 * H + 2;
   __shared__ float w[NW];
@@ -110,9 +110,27 @@ k_forward_new(NetDev net, const float* __restrict__ xyz, int64_t n, float* __res
   float x[3] = {0.f, 0.f, 0.f};
   uint64_t m = 0;
   if (live) {
-    load_point(xyz, i, x);
+    const int a = sa[i], b = sb[i];
+    if (scol) {
+      // the split point itself (k_new_vertices, subpoly.py:113-117, 180), fused:
+      // d = d/eps; w = |d0| / |d1 - d0|; v = e0*(1-w) + e1*w
+      const float* base = xyz - 3 * V;  // xyz points at slot V
+      const float d0 = __fdiv_rn(scol[a], eps), d1 = __fdiv_rn(scol[b], eps);
+      const float w = __fdiv_rn(fabsf(d0), fabsf(__fsub_rn(d1, d0)));
+      const float om = __fsub_rn(1.0f, w);
+      float* out = const_cast<float*>(xyz) + 3 * i;
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        const float v = __fadd_rn(__fmul_rn(base[3 * (int64_t)a + d], om),
+                                  __fmul_rn(base[3 * (int64_t)b + d], w));
+        out[d] = v;
+        x[d] = __fdiv_rn(__fadd_rn(v, 1.0f), 2.0f);  // Net.preprocess, as load_point
+      }
+    } else {
+      load_point(xyz, i, x);
+    }
     const uint64_t below = (idx >= 64) ? ~0ull : ((1ull << idx) - 1ull);
-    m = (zero[sa[i]] & zero[sb[i]] & below) | (1ull << idx);
+    m = (zero[a] & zero[b] & below) | (1ull << idx);
   }
   float h[H > IN ? H : IN];
   float a[H];
@@ -153,6 +171,7 @@ k_forward_new(NetDev net, const float* __restrict__ xyz, int64_t n, float* __res
     bad |= ((m >> p) & 1) && fabsf(v) > eps;
     pos[V + i] = ps;
     zero[V + i] = zs;
+    pz[V + i] = make_ulonglong2(ps, zs);
     shared[i] = m;
   }
   const uint64_t g = grid_word(net.marks, net.n_marks, eps, x);
@@ -177,7 +196,7 @@ k_forward_new(NetDev net, const float* __restrict__ xyz, int64_t n, float* __res
 __global__ void k_override_new(int64_t n, int override_, const uint64_t* __restrict__ shared,
                                float* __restrict__ pre, int64_t ld, int keep_from, int64_t V,
                                uint64_t* __restrict__ pos, uint64_t* __restrict__ zero,
-                               const int64_t* __restrict__ ctr) {
+                               const int64_t* __restrict__ ctr, ulonglong2* __restrict__ pz) {
   const bool ov = override_ < 0 ? ctr[CTR_FAIL] != 0 : override_ != 0;
   if (!ov) return;
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -187,8 +206,10 @@ __global__ void k_override_new(int64_t n, int override_, const uint64_t* __restr
     const int p = __builtin_ctzll(t);
     if (p >= keep_from) pre[(int64_t)p * ld + V + r] = 0.f;
   }
-  pos[V + r] &= ~m;
-  zero[V + r] |= m;
+  const uint64_t p = pos[V + r] & ~m, z = zero[V + r] | m;
+  pos[V + r] = p;
+  zero[V + r] = z;
+  pz[V + r] = make_ulonglong2(p, z);
 }
 
 // TropicalHashGrid.forward: raw encoding of x already in [0,1]^3 -> [n][2L]
@@ -225,7 +246,8 @@ __global__ void k_region(NetDev net, const float* __restrict__ xyz,
 
 __global__ void k_keys(NetDev net, const float* __restrict__ xyz, const float* __restrict__ pre,
                        int64_t ld, int64_t n, int K, uint64_t* __restrict__ pos,
-                       uint64_t* __restrict__ zero, uint64_t* __restrict__ grid) {
+                       uint64_t* __restrict__ zero, uint64_t* __restrict__ grid,
+                       ulonglong2* __restrict__ pz) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   float x[3];
@@ -239,6 +261,7 @@ __global__ void k_keys(NetDev net, const float* __restrict__ xyz, const float* _
   }
   pos[i] = ps;
   zero[i] = zs;
+  if (pz) pz[i] = make_ulonglong2(ps, zs);
 }
 
 // SDF = tanh(o1 - o0) and its input gradient (Net.sdf / Net.normal).
@@ -295,13 +318,13 @@ int launch_forward(const NetDev& net, const float* xyz, int64_t n, float* pre, i
 int launch_forward_new(const NetDev& net, const float* xyz, int64_t n, float* pre, int64_t ld,
                        int64_t V, int keep_from, const int32_t* sa, const int32_t* sb, int idx,
                        int own_lo, int own_hi, uint64_t* pos, uint64_t* zero, uint64_t* grid,
-                       uint64_t* shared, int64_t* ctr, hipStream_t s) {
+                       uint64_t* shared, int64_t* ctr, uint64_t* pz, const float* col, hipStream_t s) {
   if (n <= 0) return 0;
   if (!net_supported(net)) { tnp_set_error("unsupported net shape"); return -1; }
   TNP_DISPATCH(net.n_levels, {
     hipLaunchKernelGGL((k_forward_new<L_, 16, 3>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net,
                        xyz, n, pre, ld, V, keep_from, sa, sb, idx, own_lo, own_hi, pos, zero, grid,
-                       shared, ctr);
+                       shared, ctr, reinterpret_cast<ulonglong2*>(pz), col);
   });
   TNP_CHECK(hipGetLastError());
   return 0;
@@ -309,10 +332,10 @@ int launch_forward_new(const NetDev& net, const float* xyz, int64_t n, float* pr
 
 int launch_override_new(int64_t n, int override_, const uint64_t* shared, float* pre, int64_t ld,
                         int keep_from, int64_t V, uint64_t* pos, uint64_t* zero,
-                        const int64_t* ctr, hipStream_t s) {
+                        const int64_t* ctr, uint64_t* pz, hipStream_t s) {
   if (n <= 0 || override_ == 0) return 0;
   hipLaunchKernelGGL(k_override_new, dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, n, override_, shared,
-                     pre, ld, keep_from, V, pos, zero, ctr);
+                     pre, ld, keep_from, V, pos, zero, ctr, reinterpret_cast<ulonglong2*>(pz));
   TNP_CHECK(hipGetLastError());
   return 0;
 }
@@ -327,10 +350,10 @@ int launch_region(const NetDev& net, const float* xyz, const float* pre, int64_t
 }
 
 int launch_keys(const NetDev& net, const float* xyz, const float* pre, int64_t ld, int64_t n,
-                int K, uint64_t* pos, uint64_t* zero, uint64_t* grid, hipStream_t s) {
+                int K, uint64_t* pos, uint64_t* zero, uint64_t* grid, hipStream_t s, uint64_t* pz) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(k_keys, dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net, xyz, pre, ld, n, K,
-                     pos, zero, grid);
+                     pos, zero, grid, reinterpret_cast<ulonglong2*>(pz));
   TNP_CHECK(hipGetLastError());
   return 0;
 }

@@ -48,7 +48,7 @@ int launch_fail_check(const int32_t* sa, const int32_t* sb, int64_t S, int idx,
                       int64_t* ctr, hipStream_t s);
 int launch_finalize_new(int64_t S, int K, int override_, const uint64_t* shared, float* stage,
                         float eps, float* pre, int64_t ld, int keep_from, int64_t V, uint64_t* pos,
-                        uint64_t* zero, const int64_t* ctr, hipStream_t s);
+                        uint64_t* zero, const int64_t* ctr, uint64_t* pz, hipStream_t s);
 // members = [V, V + S) ++ live vertices v < V with |col[v]| < eps (ascending,
 // single pass over split_tiles(V) look-back tiles); count -> ctr[CTR_H]
 int launch_hits(const float* col, const int32_t* alive, int64_t V, float eps, int32_t* members,
@@ -78,9 +78,9 @@ struct alignas(32) CellEnt {
   uint64_t g, p, z;
   int32_t v, pad;
 };
-int launch_entry_keys(const int32_t* ent_v, int64_t T, const uint64_t* grid, const uint64_t* pos,
-                      const uint64_t* zero, CellEnt* ent,
-                      hipStream_t s);
+// pz: the interleaved (pos, zero) copy of the vertex keys
+int launch_entry_keys(const int32_t* ent_v, int64_t T, const uint64_t* grid, const uint64_t* pz,
+                      CellEnt* ent, hipStream_t s);
 
 // connecting edges over the flattened pair space (pair cells in order, then
 // (i, j<i) inside a cell); the pair count and R are read on the device.
@@ -103,8 +103,8 @@ int launch_connect(const int64_t* ptoff, const int32_t* pcell, const int32_t* ce
 // caller), ctr[CTR_E], ctr[CTR_ACTIVE]
 int launch_prune_lb(const int32_t* edges, int64_t E, const int32_t* sb, int64_t S, int64_t V,
                     const uint64_t* ckeys, int nb, int64_t X, int idx, int last_plane,
-                    const uint64_t* pos, const uint64_t* zero, int32_t* out, int32_t* used,
-                    int64_t* ctr, const TnpLB& lb, hipStream_t s);
+                    const uint64_t* pz, int32_t* out, int32_t* used, int64_t* ctr, const TnpLB& lb,
+                    hipStream_t s);
 // ctr[slot] += number of non-zero flags in f[0, n) (16-B aligned f)
 int launch_count_flags(const int32_t* f, int64_t n, int64_t* ctr, int slot, hipStream_t s);
 // planes the pruning of step idx compares (idx .. last_plane)
@@ -129,7 +129,7 @@ int launch_gather_vertices(const int32_t* used, const int64_t* nid, int64_t NV, 
                            int keep_from, const float* xyz, const float* pre, int64_t ld,
                            const uint64_t* pos, const uint64_t* zero, const uint64_t* grid,
                            float* xyz2, float* pre2, int64_t ld2, uint64_t* pos2, uint64_t* zero2,
-                           uint64_t* grid2, hipStream_t s);
+                           uint64_t* grid2, uint64_t* pz2, hipStream_t s);
 int launch_remap_edges(int32_t* edges, int64_t E, const int64_t* nid, hipStream_t s);
 int launch_active_planes(const int32_t* edges, int64_t E, int from, int last_plane,
                          const uint64_t* pos, const uint64_t* zero, int64_t* ctr, hipStream_t s);

@@ -159,7 +159,8 @@ __global__ void k_fail_check(const int32_t* __restrict__ sa, const int32_t* __re
 __global__ void k_finalize_new(int64_t S, int K, int override_, const uint64_t* __restrict__ shared,
                                float* __restrict__ stage, float eps, float* __restrict__ pre,
                                int64_t ld, int keep_from, int64_t V, uint64_t* __restrict__ pos,
-                               uint64_t* __restrict__ zero, const int64_t* __restrict__ ctr) {
+                               uint64_t* __restrict__ zero, const int64_t* __restrict__ ctr,
+                               ulonglong2* __restrict__ pz) {
   int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= S) return;
   const bool ov = override_ < 0 ? ctr[CTR_FAIL] != 0 : override_ != 0;
@@ -174,6 +175,7 @@ __global__ void k_finalize_new(int64_t S, int K, int override_, const uint64_t* 
   }
   pos[V + r] = ps;
   zero[V + r] = zs;
+  pz[V + r] = make_ulonglong2(ps, zs);
 }
 
 // ---------------------------------------------------------------------------
@@ -390,15 +392,16 @@ k_pair_cells_lb(const int64_t* __restrict__ cstart, const int64_t* __restrict__ 
 // entry-aligned copies of the members' packed keys (read contiguously per
 // cell by the pair test)
 __global__ void k_entry_keys(const int32_t* __restrict__ ent_v, int64_t T,
-                             const uint64_t* __restrict__ grid, const uint64_t* __restrict__ pos,
-                             const uint64_t* __restrict__ zero, CellEnt* __restrict__ ent) {
+                             const uint64_t* __restrict__ grid, const ulonglong2* __restrict__ pz,
+                             CellEnt* __restrict__ ent) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= T) return;
   const int v = ent_v[i];
+  const ulonglong2 k = pz[v];  // pos and zero in one 16-byte gather
   CellEnt r;
   r.g = grid[v];
-  r.p = pos[v];
-  r.z = zero[v];
+  r.p = k.x;
+  r.z = k.y;
   r.v = v;
   r.pad = 0;
   ent[i] = r;
@@ -455,7 +458,7 @@ __device__ __forceinline__ int64_t upper_bound_i64(const int64_t* __restrict__ a
 }
 
 constexpr int CIPT = 8;                 // consecutive pair indices per thread
-constexpr int CONNECT_CELLS = TNP_BLOCK * 8 + 2;  // >= pair cells a chunk can touch
+constexpr int CONNECT_CELLS = TNP_BLOCK * CIPT + 2;  // >= pair cells a chunk can touch
 constexpr int CCH = TNP_BLOCK * CIPT;   // pair indices per block
 
 __device__ __forceinline__ void cell_coords(int64_t cell, int NC, int cc[3]) {
@@ -732,9 +735,8 @@ k_prune_emit(EdgeSrc src, int64_t N, uint64_t fmask, uint64_t amask,
 // writes the kept count to ctr[CTR_E].
 __global__ void __launch_bounds__(TNP_BLOCK)
 k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, uint64_t fmask, uint64_t amask,
-           const uint64_t* __restrict__ pos, const uint64_t* __restrict__ zero,
-           int32_t* __restrict__ out, int32_t* __restrict__ used, int64_t* __restrict__ ctr,
-           TnpLB lb) {
+           const ulonglong2* __restrict__ pz, int32_t* __restrict__ out,
+           int32_t* __restrict__ used, int64_t* __restrict__ ctr, TnpLB lb) {
   __shared__ int cnt[LIPT][TNP_WAVES];
   __shared__ int64_t slot;
   __shared__ uint64_t acts[TNP_WAVES];
@@ -781,11 +783,12 @@ k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, uint64_t fmask, uint64_t amas
   }
   uint64_t pa[LIPT], pb[LIPT], za[LIPT], zb[LIPT];
 #pragma unroll
-  for (int k = 0; k < LIPT; ++k) {
-    pa[k] = pos[a[k]];
-    pb[k] = pos[b[k]];
-    za[k] = zero[a[k]];
-    zb[k] = zero[b[k]];
+  for (int k = 0; k < LIPT; ++k) {  // (pos, zero) of an endpoint: one 16-byte gather
+    const ulonglong2 ka = pz[a[k]], kb = pz[b[k]];
+    pa[k] = ka.x;
+    za[k] = ka.y;
+    pb[k] = kb.x;
+    zb[k] = kb.y;
   }
   uint64_t bal[LIPT];
   uint64_t act = 0;
@@ -866,15 +869,17 @@ __global__ void k_gather_vertices(const int32_t* __restrict__ used, const int64_
                                   const uint64_t* __restrict__ zero, const uint64_t* __restrict__ grid,
                                   float* __restrict__ xyz2, float* __restrict__ pre2, int64_t ld2,
                                   uint64_t* __restrict__ pos2, uint64_t* __restrict__ zero2,
-                                  uint64_t* __restrict__ grid2) {
+                                  uint64_t* __restrict__ grid2, ulonglong2* __restrict__ pz2) {
   int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= NV || !used[v]) return;
   int64_t n = nid[v];
 #pragma unroll
   for (int d = 0; d < 3; ++d) xyz2[3 * n + d] = xyz[3 * v + d];
   for (int p = keep_from; p < K; ++p) pre2[(int64_t)p * ld2 + n] = pre[(int64_t)p * ld + v];
-  pos2[n] = pos[v];
-  zero2[n] = zero[v];
+  const uint64_t p = pos[v], z = zero[v];
+  pos2[n] = p;
+  zero2[n] = z;
+  pz2[n] = make_ulonglong2(p, z);
   grid2[n] = grid[v];
 }
 
@@ -943,10 +948,10 @@ int launch_fail_check(const int32_t* sa, const int32_t* sb, int64_t S, int idx,
 }
 int launch_finalize_new(int64_t S, int K, int override_, const uint64_t* shared, float* stage,
                         float eps, float* pre, int64_t ld, int keep_from, int64_t V, uint64_t* pos,
-                        uint64_t* zero, const int64_t* ctr, hipStream_t s) {
+                        uint64_t* zero, const int64_t* ctr, uint64_t* pz, hipStream_t s) {
   if (S <= 0) return 0;
   hipLaunchKernelGGL(k_finalize_new, dim3(tnp_grid(S)), dim3(TNP_BLOCK), 0, s, S, K, override_,
-                     shared, stage, eps, pre, ld, keep_from, V, pos, zero, ctr);
+                     shared, stage, eps, pre, ld, keep_from, V, pos, zero, ctr, reinterpret_cast<ulonglong2*>(pz));
   TNP_CHECK(hipGetLastError());
   return 0;
 }
@@ -1000,11 +1005,11 @@ int launch_pair_cells(const int64_t* cstart, const int64_t* cend, int64_t ncell,
   TNP_CHECK(hipGetLastError());
   return 0;
 }
-int launch_entry_keys(const int32_t* ent_v, int64_t T, const uint64_t* grid, const uint64_t* pos,
-                      const uint64_t* zero, CellEnt* ent, hipStream_t s) {
+int launch_entry_keys(const int32_t* ent_v, int64_t T, const uint64_t* grid, const uint64_t* pz,
+                      CellEnt* ent, hipStream_t s) {
   if (T <= 0) return 0;
-  hipLaunchKernelGGL(k_entry_keys, dim3(tnp_grid(T)), dim3(TNP_BLOCK), 0, s, ent_v, T, grid, pos, zero,
-                     ent);
+  hipLaunchKernelGGL(k_entry_keys, dim3(tnp_grid(T)), dim3(TNP_BLOCK), 0, s, ent_v, T, grid,
+                     reinterpret_cast<const ulonglong2*>(pz), ent);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
@@ -1056,8 +1061,8 @@ int launch_prune(bool emit, const int32_t* edges, int64_t E, const int32_t* sb, 
 }
 int launch_prune_lb(const int32_t* edges, int64_t E, const int32_t* sb, int64_t S, int64_t V,
                     const uint64_t* ckeys, int nb, int64_t X, int idx, int last_plane,
-                    const uint64_t* pos, const uint64_t* zero, int32_t* out, int32_t* used,
-                    int64_t* ctr, const TnpLB& lb, hipStream_t s) {
+                    const uint64_t* pz, int32_t* out, int32_t* used, int64_t* ctr, const TnpLB& lb,
+                    hipStream_t s) {
   EdgeSrc src{edges, E, sb, S, V, ckeys, nb, X};
   const int64_t N = E + S + X;
   if (N <= 0) {
@@ -1069,7 +1074,7 @@ int launch_prune_lb(const int32_t* edges, int64_t E, const int32_t* sb, int64_t 
   if (last_plane < 63) amask &= (1ull << (last_plane + 1)) - 1ull;
   const int64_t tiles = lb_tiles(N);
   hipLaunchKernelGGL(k_prune_lb, dim3((unsigned)tiles), dim3(TNP_BLOCK), 0, s, src, N, tiles, fmask,
-                     amask, pos, zero, out, used, ctr, lb);
+                     amask, reinterpret_cast<const ulonglong2*>(pz), out, used, ctr, lb);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
@@ -1084,11 +1089,11 @@ int launch_gather_vertices(const int32_t* used, const int64_t* nid, int64_t NV, 
                            int keep_from, const float* xyz, const float* pre, int64_t ld,
                            const uint64_t* pos, const uint64_t* zero, const uint64_t* grid,
                            float* xyz2, float* pre2, int64_t ld2, uint64_t* pos2, uint64_t* zero2,
-                           uint64_t* grid2, hipStream_t s) {
+                           uint64_t* grid2, uint64_t* pz2, hipStream_t s) {
   if (NV <= 0) return 0;
   hipLaunchKernelGGL(k_gather_vertices, dim3(tnp_grid(NV)), dim3(TNP_BLOCK), 0, s, used, nid, NV,
                      K, keep_from, xyz, pre, ld, pos, zero, grid, xyz2, pre2, ld2, pos2, zero2,
-                     grid2);
+                     grid2, reinterpret_cast<ulonglong2*>(pz2));
   TNP_CHECK(hipGetLastError());
   return 0;
 }
