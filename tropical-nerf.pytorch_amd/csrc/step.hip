@@ -493,6 +493,20 @@ __global__ void k_chunk_cells(const int64_t* __restrict__ ptoff, const int32_t* 
 // Persistent over the chunks of the pair space (count read on the device);
 // stops at once if the complex is degenerate (pairs above the limit) or the
 // chunk table overflowed -- the host reports either after the fact.
+// row i and column j (j < i) of in-cell pair q (q = i (i - 1) / 2 + j)
+__device__ __forceinline__ void pair_row(int q, int& i, int& j) {
+  int r = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)q)) * 0.5f);
+  while ((int64_t)r * (r - 1) / 2 > q) --r;
+  while ((int64_t)(r + 1) * r / 2 <= q) ++r;
+  i = r;
+  j = q - (int)((int64_t)r * (r - 1) / 2);
+}
+
+// Lane-interleaved enumeration: the 64 lanes of a wave take 64 CONSECUTIVE
+// pairs per step, so within a cell row they share the row entry (broadcast)
+// and read consecutive column entries (coalesced 32-byte records); a wave
+// walks CIPT such steps.  The chunk's pair cells (offset, id, member count,
+// first entry) sit in LDS, so locating a pair is an LDS walk.
 __global__ void __launch_bounds__(TNP_BLOCK)
 k_connect(const int64_t* __restrict__ ptoff, const int32_t* __restrict__ pcell,
           const int32_t* __restrict__ cellcnt, const int64_t* __restrict__ celloff, int NC,
@@ -501,9 +515,10 @@ k_connect(const int64_t* __restrict__ ptoff, const int32_t* __restrict__ pcell,
           int64_t* __restrict__ ctr, int64_t* __restrict__ bstat) {
   __shared__ int64_t lds[TNP_WAVES];
   __shared__ int64_t s_base;
-  // the chunk's pair-cell offsets relative to its first pair (clamped to
-  // [-1, 2^30]): every thread's cell search runs in LDS
-  __shared__ int32_t soff[CONNECT_CELLS];
+  __shared__ int32_t s_off[CONNECT_CELLS];  // first pair of the cell - chunk start
+  __shared__ int32_t s_cell[CONNECT_CELLS];
+  __shared__ int32_t s_n[CONNECT_CELLS];
+  __shared__ int32_t s_ent[CONNECT_CELLS];  // first entry of the cell
   const int64_t TT = ctr[CTR_TESTS];
   const int64_t R = ctr[CTR_R];
   if (TT > max_tests || ctr[CTR_BOVF] || ctr[CTR_BIG]) return;
@@ -515,78 +530,53 @@ k_connect(const int64_t* __restrict__ ptoff, const int32_t* __restrict__ pcell,
   const int64_t r0 = bcell[b];
   const int64_t r_end = (b + 1 < nblk) ? (int64_t)bcell[b + 1] + 1 : R;
   const int nr = (int)(r_end - r0);  // <= CCH + 1: every pair cell holds >= 1 pair
-  __syncthreads();  // the previous chunk is done with soff[]
+  __syncthreads();  // the previous chunk is done with the cell window
   for (int t = threadIdx.x; t < nr; t += blockDim.x) {
-    const int64_t v = ptoff[r0 + t] - pb;
-    soff[t] = (int32_t)(v < -1 ? -1 : (v > (1 << 30) ? (1 << 30) : v));
+    const int c = pcell[r0 + t];
+    s_off[t] = (int32_t)(ptoff[r0 + t] - pb);  // > -2^31: a cell holds < 2^31 pairs
+    s_cell[t] = c;
+    s_n[t] = cellcnt[c];
+    s_ent[t] = (int32_t)celloff[c];
   }
   __syncthreads();
-  // first local cell index with soff > x (nr if none)
-  auto upper = [&](int lo, int64_t x) {
-    int hi = nr;
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (soff[mid] <= x) lo = mid + 1;
-      else hi = mid;
-    }
-    return lo;
-  };
-  const int64_t p0 = pb + (int64_t)threadIdx.x * CIPT;
+  const int64_t pw = pb + (int64_t)tnp::wave() * 64 * CIPT + tnp::lane();
   uint64_t kk[CIPT];
   int ne = 0;
-  if (p0 < TT) {
-    int lc = upper(0, p0 - pb) - 1;
-    int cell = pcell[r0 + lc];
-    int64_t q = p0 - ptoff[r0 + lc];
-    int64_t i = (int64_t)((1.0 + sqrt(1.0 + 8.0 * (double)q)) * 0.5);
-    while (i * (i - 1) / 2 > q) --i;
-    while ((i + 1) * i / 2 <= q) ++i;
-    int64_t j = q - i * (i - 1) / 2;
-    int n = cellcnt[cell];
-    int64_t base = celloff[cell];
-    int cc[3];
-    cell_coords(cell, NC, cc);
-    CellEnt eu = ent[base + i];
-    int vu = eu.v;
-    uint64_t gu = eu.g, pu = eu.p, zu = eu.z;
+  int lc = 0;
+  {  // the lane's first cell: binary search, then a forward walk per step
+    const int64_t x = pw - pb;
+    int lo = 0, hi = nr;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (s_off[mid] <= x) lo = mid + 1;
+      else hi = mid;
+    }
+    lc = lo > 0 ? lo - 1 : 0;
+  }
 #pragma unroll
-    for (int k = 0; k < CIPT; ++k) {
-      const int64_t p = p0 + k;
-      if (p < TT) {
-        const CellEnt ev = ent[base + j];
-        const uint64_t pv = ev.p, zv = ev.z;
-        PairTest t = pair_test(cc, below, gu, pu, zu, ev.g, pv, zv);
-        if (t.compat) {
-          n_compat++;
-          n_reg += t.regions;
-          n_conn += t.emit;
-          // the step's pruning drops it anyway (keep_edge): never appended
-          if (t.emit && (fmask == 0 || (((pu ^ pv) | (zu ^ zv)) & fmask) != 0)) {
-            uint32_t vv = (uint32_t)ev.v;
-            uint32_t lo = (uint32_t)vu < vv ? (uint32_t)vu : vv;
-            uint32_t hi = (uint32_t)vu < vv ? vv : (uint32_t)vu;
-            kk[ne++] = ((uint64_t)lo << nb) | hi;
-          }
-        }
-        if (++j == i) {
-          j = 0;
-          if (++i == n) {
-            if (p + 1 < TT && k + 1 < CIPT) {
-              lc = upper(lc + 1, p + 1 - pb) - 1;
-              cell = pcell[r0 + lc];
-              n = cellcnt[cell];
-              base = celloff[cell];
-              cell_coords(cell, NC, cc);
-              i = 1;
-            }
-          }
-          if (k + 1 < CIPT && i < n) {
-            eu = ent[base + i];
-            vu = eu.v;
-            gu = eu.g;
-            pu = eu.p;
-            zu = eu.z;
-          }
+  for (int k = 0; k < CIPT; ++k) {
+    const int64_t p = pw + 64 * k;
+    if (p < TT) {
+      const int x = (int)(p - pb);
+      while (lc + 1 < nr && s_off[lc + 1] <= x) ++lc;
+      int i, j;
+      pair_row(x - s_off[lc], i, j);
+      const int cell = s_cell[lc];
+      const int64_t base = s_ent[lc];
+      int cc[3];
+      cell_coords(cell, NC, cc);
+      const CellEnt eu = ent[base + i];
+      const CellEnt ev = ent[base + j];
+      PairTest t = pair_test(cc, below, eu.g, eu.p, eu.z, ev.g, ev.p, ev.z);
+      if (t.compat) {
+        n_compat++;
+        n_reg += t.regions;
+        n_conn += t.emit;
+        // the step's pruning drops it anyway (keep_edge): never appended
+        if (t.emit && (fmask == 0 || (((eu.p ^ ev.p) | (eu.z ^ ev.z)) & fmask) != 0)) {
+          const uint32_t vu = (uint32_t)eu.v, vv = (uint32_t)ev.v;
+          const uint32_t lo = vu < vv ? vu : vv, hi = vu < vv ? vv : vu;
+          kk[ne++] = ((uint64_t)lo << nb) | hi;
         }
       }
     }
