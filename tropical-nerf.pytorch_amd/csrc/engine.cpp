@@ -133,6 +133,10 @@ struct tnp_engine {
   bool has_net = false;
   VSet cur, alt;
   Buf edges, edges_alt;
+  // per-edge key masks (step.hip k_prune_lb): dm = endpoint keys differ,
+  // sm = planes that split the edge; valid when masks_valid
+  Buf edm, esm, edm_alt, esm_alt;
+  bool masks_valid = false;
   int64_t V = 0, E = 0;
   int keep_all = 0;
   int valid_from = 0;  // pre planes [valid_from, K) are valid for every vertex
@@ -274,11 +278,25 @@ static int set_alive(tnp_engine* e, int64_t from, int64_t n, hipStream_t s) {
   return 0;
 }
 
-// a freshly loaded complex: every slot live, ids dense
-static int reset_live(tnp_engine* e, hipStream_t s) {
+// a freshly loaded complex: every slot live, ids dense, edge masks to compute
+static int reset_live(tnp_engine* e, hipStream_t s, bool edges_changed = true) {
+  if (edges_changed) e->masks_valid = false;
   e->dirty = false;
   e->V_live = e->V;
   return set_alive(e, 0, e->V, s);
+}
+
+// per-edge masks from the endpoint keys, if the edges changed without them
+static int ensure_masks(tnp_engine* e, hipStream_t s) {
+  if (e->masks_valid) return 0;
+  const int64_t E1 = std::max<int64_t>(e->E, 1);
+  if (buf_ensure(e->edm, E1 * sizeof(uint64_t), s)) return -1;
+  if (buf_ensure(e->esm, E1 * sizeof(uint64_t), s)) return -1;
+  TIMED("edge_masks", 40.0 * e->E,
+        launch_edge_masks(P<int32_t>(e->edges), e->E, P<uint64_t>(e->cur.pz), P<uint64_t>(e->edm),
+                          P<uint64_t>(e->esm), 0, 63, nullptr, s));
+  e->masks_valid = true;
+  return 0;
 }
 
 // renumber the live slots densely (the reference's per-step compaction,
@@ -307,7 +325,7 @@ static int compact_now(tnp_engine* e, hipStream_t s) {
   }
   std::swap(e->cur, e->alt);
   e->V = V2;
-  return reset_live(e, s);
+  return reset_live(e, s, false);  // same edges, same order: masks stay valid
 }
 
 // ---------------------------------------------------------------------------
@@ -341,7 +359,8 @@ extern "C" void tnp_engine_destroy(tnp_engine* e) {
                  &e->stage, &e->shared, &e->members, &e->cellcnt, &e->cellcur, &e->celloff,
                  &e->ent_v, &e->ent_g, &e->ent_p, &e->ent_z, &e->tcnt, &e->toff, &e->bcell,
                  &e->bstat, &e->ckeys_a, &e->ckeys_b, &e->sort_scr, &e->flags, &e->used, &e->nid,
-                 &e->ctr, &e->tri, &e->faces, &e->lb[0], &e->lb[1]};
+                 &e->ctr, &e->tri, &e->faces, &e->lb[0], &e->lb[1], &e->edm, &e->esm,
+                 &e->edm_alt, &e->esm_alt};
   for (Buf* b : bufs) buf_free(*b, s);
   for (Buf& b : e->fscr) buf_free(b, s);
   for (Buf& b : e->fscr2) buf_free(b, s);
@@ -383,7 +402,7 @@ static int check_net(const tnp_net* n) {
                   n->num_layers, n->num_hidden);
     return -1;
   }
-  if (net_K(d) > 64) { tnp_set_error("more than 64 planes"); return -1; }
+  if (net_K(d) > 63) { tnp_set_error("more than 63 planes (edge masks reserve all-ones)"); return -1; }
   return 0;
 }
 
@@ -467,9 +486,15 @@ extern "C" int tnp_engine_active_planes(tnp_engine* e, int from, uint64_t* mask,
   TNP_CHECK(hipSetDevice(e->device));
   if (buf_ensure(e->ctr, CTR_N * sizeof(int64_t), s)) return -1;
   TNP_CHECK(hipMemsetAsync(P<int64_t>(e->ctr) + CTR_ACTIVE, 0, sizeof(int64_t), s));
-  if (launch_active_planes(P<int32_t>(e->edges), e->E, from, e->K - 1, P<uint64_t>(e->cur.pos),
-                           P<uint64_t>(e->cur.zero), P<int64_t>(e->ctr), s))
+  // the per-edge masks are (re)computed here and the OR of their split planes
+  // taken in the same pass
+  const int64_t E1 = std::max<int64_t>(e->E, 1);
+  if (buf_ensure(e->edm, E1 * sizeof(uint64_t), s)) return -1;
+  if (buf_ensure(e->esm, E1 * sizeof(uint64_t), s)) return -1;
+  if (launch_edge_masks(P<int32_t>(e->edges), e->E, P<uint64_t>(e->cur.pz), P<uint64_t>(e->edm),
+                        P<uint64_t>(e->esm), from, e->K - 1, P<int64_t>(e->ctr), s))
     return -1;
+  e->masks_valid = true;
   if (read_ctr(e, s)) return -1;
   *mask = (uint64_t)e->h_ctr[CTR_ACTIVE];
   return 0;
@@ -637,11 +662,12 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
     if (buf_ensure(e->sa, e->E * sizeof(int32_t), s)) return -1;
     if (buf_ensure(e->sb, e->E * sizeof(int32_t), s)) return -1;
     if (e->curve && buf_ensure(e->cv[CV_EIDX], e->E * sizeof(int32_t), s)) return -1;
+    if (ensure_masks(e, s)) return -1;
     TnpLB lb;
     if (lb_begin(e, split_tiles(e->E), s, &lb)) return -1;
-    TIMED("split", 16.0 * e->E,
-          launch_split_lb(P<int32_t>(e->edges), e->E, col, eps, e->V, P<int32_t>(e->sa),
-                          P<int32_t>(e->sb), P<int64_t>(e->ctr),
+    TIMED("split", 8.0 * e->E,
+          launch_split_lb(P<int32_t>(e->edges), e->E, P<uint64_t>(e->esm), P<uint64_t>(e->edm), idx,
+                          e->V, P<int32_t>(e->sa), P<int32_t>(e->sb), P<int64_t>(e->ctr),
                           e->curve ? P<int32_t>(e->cv[CV_EIDX]) : nullptr, lb, s));
     if (read_ctr(e, s)) return -1;
     S = e->h_ctr[CTR_S];
@@ -707,7 +733,10 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   const float eps = e->net.eps;
   const int K = e->K;
   int64_t S_kept = e->pend_S;
-  if (e->curve && curve_filter(e, idx, override_, s, &S_kept)) return -1;
+  if (e->curve) {
+    if (curve_filter(e, idx, override_, s, &S_kept)) return -1;
+    e->masks_valid = false;  // the filter rewired the kept split edges
+  }
   const int64_t V = e->V, E = e->E, S = S_kept;
   const int64_t NV = V + S;
   VSet& c = e->cur;
@@ -888,11 +917,19 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     // compaction): the distinct flagged count is the reference's V'
     if (buf_ensure(e->used, std::max<int64_t>(NV, 1) * sizeof(int32_t), s)) return -1;
     TNP_CHECK(hipMemsetAsync(e->used.p, 0, NV * sizeof(int32_t), s));
+    if (ensure_masks(e, s)) return -1;  // (curve path: recomputed after the rewiring)
+    const int64_t N1 = std::max<int64_t>(N, 1);
+    if (buf_ensure(e->edm_alt, N1 * sizeof(uint64_t), s)) return -1;
+    if (buf_ensure(e->esm_alt, N1 * sizeof(uint64_t), s)) return -1;
     TnpLB lb;
     if (lb_begin(e, lb_tiles(N), s, &lb)) return -1;
-    TIMED("prune", 40.0 * N,
+    TIMED("prune", 24.0 * E + 48.0 * (S + X),
           launch_prune_lb(eg, E, P<int32_t>(e->sb), S, V, e->ckeys, nb, X, idx, K - 1,
-                          P<uint64_t>(c.pz), P<int32_t>(e->edges_alt), P<int32_t>(e->used), ctr, lb, s));
+                          P<uint64_t>(c.pz), P<uint64_t>(e->edm), P<uint64_t>(e->esm),
+                          P<int32_t>(e->edges_alt), P<uint64_t>(e->edm_alt), P<uint64_t>(e->esm_alt),
+                          P<int32_t>(e->used), ctr, lb, s));
+    std::swap(e->edm, e->edm_alt);
+    std::swap(e->esm, e->esm_alt);
     TIMED("count_live", 4.0 * NV, launch_count_flags(P<int32_t>(e->used), NV, ctr, CTR_V, s));
     next_valid = e->keep_all ? 0 : std::min(idx + 1, K - 1);
     if (read_ctr(e, s)) return -1;
@@ -905,6 +942,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
       return -1;
     if (set_alive(e, V, S, s)) return -1;
     V2 = e->V_live + S;
+    e->masks_valid = false;  // the concatenated edge list carries no masks
     if (read_ctr(e, s)) return -1;
   }
   std::swap(e->edges, e->edges_alt);

@@ -37,10 +37,17 @@ enum {
 int64_t step_tiles(int64_t n);
 int64_t lb_tiles(int64_t n);     // tiles of the single-pass prune
 int64_t split_tiles(int64_t n);  // tiles of the single-pass split and hit passes
-// single-pass split over split_tiles(E) look-back tiles (E > 0): S -> ctr[CTR_S];
-// sa/sb (and eidx if given) need capacity E
-int launch_split_lb(int32_t* edges, int64_t E, const float* col, float eps, int64_t V, int32_t* sa,
-                    int32_t* sb, int64_t* ctr, int32_t* eidx, const TnpLB& lb, hipStream_t s);
+// single-pass split over split_tiles(E) look-back tiles (E > 0) from the
+// edges' split masks (bit idx): S -> ctr[CTR_S]; sa/sb (and eidx if given)
+// need capacity E; without eidx the split edges are rewired in place and
+// their masks marked stale
+int launch_split_lb(int32_t* edges, int64_t E, const uint64_t* sm, uint64_t* dm, int idx, int64_t V,
+                    int32_t* sa, int32_t* sb, int64_t* ctr, int32_t* eidx, const TnpLB& lb,
+                    hipStream_t s);
+// per-edge masks from the endpoint keys (pz): dm = keys differ, sm = split
+// planes; ctr != null: OR of sm over planes [from, last_plane] -> CTR_ACTIVE
+int launch_edge_masks(const int32_t* edges, int64_t E, const uint64_t* pz, uint64_t* dm,
+                      uint64_t* sm, int from, int last_plane, int64_t* ctr, hipStream_t s);
 int launch_new_vertices(const int32_t* sa, const int32_t* sb, int64_t S, const float* col,
                         float eps, float* xyz, int64_t V, hipStream_t s);
 int launch_fail_check(const int32_t* sa, const int32_t* sb, int64_t S, int idx,
@@ -103,7 +110,8 @@ int launch_connect(const int64_t* ptoff, const int32_t* pcell, const int32_t* ce
 // caller), ctr[CTR_E], ctr[CTR_ACTIVE]
 int launch_prune_lb(const int32_t* edges, int64_t E, const int32_t* sb, int64_t S, int64_t V,
                     const uint64_t* ckeys, int nb, int64_t X, int idx, int last_plane,
-                    const uint64_t* pz, int32_t* out, int32_t* used, int64_t* ctr, const TnpLB& lb,
+                    const uint64_t* pz, const uint64_t* dm, const uint64_t* sm, int32_t* out,
+                    uint64_t* odm, uint64_t* osm, int32_t* used, int64_t* ctr, const TnpLB& lb,
                     hipStream_t s);
 // ctr[slot] += number of non-zero flags in f[0, n) (16-B aligned f)
 int launch_count_flags(const int32_t* f, int64_t n, int64_t* ctr, int slot, hipStream_t s);

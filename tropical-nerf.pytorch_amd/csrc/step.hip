@@ -26,6 +26,7 @@
 
 namespace {
 
+constexpr uint64_t EDGE_STALE = ~0ull;  // edge masks to recompute (K <= 63: never a real mask)
 constexpr int IPT = 8;                  // items per thread per tile
 constexpr int TILE = TNP_BLOCK * IPT;   // tile of a compaction pass
 // single-pass (look-back) compactions: items per thread of the split / hit
@@ -52,33 +53,24 @@ __device__ __forceinline__ bool split_test(const float* __restrict__ col, const 
 // plane-column gathers -- so a thread has SIPT * 2 loads in flight instead
 // of a bounds branch serialising every item.
 __global__ void __launch_bounds__(TNP_BLOCK)
-k_split_lb(int32_t* __restrict__ edges, int64_t E, int64_t ntiles, const float* __restrict__ col,
-           float eps, int64_t V, int32_t* __restrict__ sa, int32_t* __restrict__ sb,
-           int64_t* __restrict__ ctr, int32_t* __restrict__ eidx, TnpLB lb) {
+k_split_lb(int32_t* __restrict__ edges, int64_t E, int64_t ntiles, const uint64_t* __restrict__ sm,
+           uint64_t* __restrict__ dm, int idx, int64_t V, int32_t* __restrict__ sa,
+           int32_t* __restrict__ sb, int64_t* __restrict__ ctr, int32_t* __restrict__ eidx, TnpLB lb) {
   __shared__ int cnt[SIPT][TNP_WAVES];
   __shared__ int64_t slot;
   const int64_t tile = tnp::lb_tile(lb, &slot);
   const int64_t base = tile * STILE;
-  const int2* e2 = reinterpret_cast<const int2*>(edges);
-  int2 ab[SIPT];
-  float c0[SIPT], c1[SIPT];
   uint64_t bal[SIPT];
+  uint64_t mk[SIPT];
 #pragma unroll
-  for (int k = 0; k < SIPT; ++k) {
+  for (int k = 0; k < SIPT; ++k) {  // coalesced, unconditional (clamped) loads
     const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
-    ab[k] = e2[i < E ? i : E - 1];
-  }
-#pragma unroll
-  for (int k = 0; k < SIPT; ++k) {
-    c0[k] = col[ab[k].x];
-    c1[k] = col[ab[k].y];
+    mk[k] = sm[i < E ? i : E - 1];
   }
 #pragma unroll
   for (int k = 0; k < SIPT; ++k) {
     const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
-    const bool f = (i < E) && (__fmul_rn(c0[k], c1[k]) < 0.f) && (fabsf(c0[k]) > eps) &&
-                   (fabsf(c1[k]) > eps);
-    bal[k] = __ballot(f);
+    bal[k] = __ballot((i < E) && ((mk[k] >> idx) & 1));
     if (tnp::lane() == 0) cnt[k][tnp::wave()] = __popcll(bal[k]);
   }
   __syncthreads();
@@ -102,10 +94,15 @@ k_split_lb(int32_t* __restrict__ edges, int64_t E, int64_t ntiles, const float* 
     if ((bal[k] >> tnp::lane()) & 1) {
       const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
       const int64_t id = off + tnp::mbcnt(bal[k]);
-      sa[id] = ab[k].x;
-      sb[id] = ab[k].y;
-      if (eidx) eidx[id] = (int32_t)i;
-      else edges[2 * i + 1] = (int32_t)(V + id);
+      const int2 ab = reinterpret_cast<const int2*>(edges)[i];
+      sa[id] = ab.x;
+      sb[id] = ab.y;
+      if (eidx) {
+        eidx[id] = (int32_t)i;
+      } else {
+        edges[2 * i + 1] = (int32_t)(V + id);
+        dm[i] = EDGE_STALE;  // rewired: the prune recomputes its masks
+      }
     }
     run += tot;
   }
@@ -723,10 +720,19 @@ k_prune_emit(EdgeSrc src, int64_t N, uint64_t fmask, uint64_t amask,
 // tile's output offset, then the ordered emit (k-major, then thread, as
 // prune_emit), used flags and the next-active plane mask.  The last tile
 // writes the kept count to ctr[CTR_E].
+// Per-edge key masks travel with the edges: dm = endpoint keys differ
+// ((pos ^ pos') | (zero ^ zero')) and sm = the planes that split the edge
+// ((pos ^ pos') & ~zero & ~zero': both non-zero, opposite signs -- exactly
+// the split test of subpoly.py:104-105).  Vertex keys never change after
+// creation, so an edge's masks change only when the edge does: the prune
+// reads them coalesced for the old edges and gathers the endpoint keys only
+// for rewired (dm == EDGE_STALE), e_new and c_new edges.
 __global__ void __launch_bounds__(TNP_BLOCK)
 k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, uint64_t fmask, uint64_t amask,
-           const ulonglong2* __restrict__ pz, int32_t* __restrict__ out,
-           int32_t* __restrict__ used, int64_t* __restrict__ ctr, TnpLB lb) {
+           const ulonglong2* __restrict__ pz, const uint64_t* __restrict__ dm,
+           const uint64_t* __restrict__ sm, int32_t* __restrict__ out, uint64_t* __restrict__ odm,
+           uint64_t* __restrict__ osm, int32_t* __restrict__ used, int64_t* __restrict__ ctr,
+           TnpLB lb) {
   __shared__ int cnt[LIPT][TNP_WAVES];
   __shared__ int64_t slot;
   __shared__ uint64_t acts[TNP_WAVES];
@@ -738,55 +744,66 @@ k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, uint64_t fmask, uint64_t amas
   const int64_t ES = src.E + src.S;
   const int kind = last < src.E ? 0 : (base >= src.E && last < ES) ? 1 : (base >= ES ? 2 : 3);
   int a[LIPT], b[LIPT];
+  uint64_t d[LIPT], m[LIPT];
   if (kind == 0) {
     const int2* e2 = reinterpret_cast<const int2*>(src.edges);
 #pragma unroll
     for (int k = 0; k < LIPT; ++k) {
       const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
-      const int2 ab = e2[i < last ? i : last];
+      const int64_t ic = i < last ? i : last;
+      const int2 ab = e2[ic];
       a[k] = ab.x;
       b[k] = ab.y;
-    }
-  } else if (kind == 1) {
-#pragma unroll
-    for (int k = 0; k < LIPT; ++k) {
-      const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
-      const int64_t r = (i < last ? i : last) - src.E;
-      a[k] = src.sb[r];
-      b[k] = (int)(src.V + r);
-    }
-  } else if (kind == 2) {
-    const uint64_t lo_mask = (1ull << src.nb) - 1ull;
-#pragma unroll
-    for (int k = 0; k < LIPT; ++k) {
-      const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
-      const uint64_t key = src.ckeys[(i < last ? i : last) - ES];
-      a[k] = (int)(key >> src.nb);
-      b[k] = (int)(key & lo_mask);
+      d[k] = dm[ic];
+      m[k] = sm[ic];
     }
   } else {
+    if (kind == 1) {
+#pragma unroll
+      for (int k = 0; k < LIPT; ++k) {
+        const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
+        const int64_t r = (i < last ? i : last) - src.E;
+        a[k] = src.sb[r];
+        b[k] = (int)(src.V + r);
+      }
+    } else if (kind == 2) {
+      const uint64_t lo_mask = (1ull << src.nb) - 1ull;
+#pragma unroll
+      for (int k = 0; k < LIPT; ++k) {
+        const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
+        const uint64_t key = src.ckeys[(i < last ? i : last) - ES];
+        a[k] = (int)(key >> src.nb);
+        b[k] = (int)(key & lo_mask);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < LIPT; ++k) {
+        const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
+        fetch_edge(src, i < last ? i : last, a[k], b[k]);
+      }
+    }
 #pragma unroll
     for (int k = 0; k < LIPT; ++k) {
       const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
-      fetch_edge(src, i < last ? i : last, a[k], b[k]);
+      d[k] = (i < src.E) ? dm[i] : EDGE_STALE;  // mixed tile: old edges keep theirs
+      m[k] = (i < src.E) ? sm[i] : 0ull;
     }
   }
-  uint64_t pa[LIPT], pb[LIPT], za[LIPT], zb[LIPT];
 #pragma unroll
-  for (int k = 0; k < LIPT; ++k) {  // (pos, zero) of an endpoint: one 16-byte gather
-    const ulonglong2 ka = pz[a[k]], kb = pz[b[k]];
-    pa[k] = ka.x;
-    za[k] = ka.y;
-    pb[k] = kb.x;
-    zb[k] = kb.y;
+  for (int k = 0; k < LIPT; ++k) {
+    if (d[k] == EDGE_STALE) {  // new or rewired edge: masks from the endpoint keys
+      const ulonglong2 ka = pz[a[k]], kb = pz[b[k]];
+      d[k] = (ka.x ^ kb.x) | (ka.y ^ kb.y);
+      m[k] = (ka.x ^ kb.x) & ~ka.y & ~kb.y;
+    }
   }
   uint64_t bal[LIPT];
   uint64_t act = 0;
 #pragma unroll
   for (int k = 0; k < LIPT; ++k) {
     const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
-    const bool f = (i <= last) && ((((pa[k] ^ pb[k]) | (za[k] ^ zb[k])) & fmask) != 0);
-    if (f) act |= (pa[k] ^ pb[k]) & ~za[k] & ~zb[k] & amask;
+    const bool f = (i <= last) && ((d[k] & fmask) != 0);
+    if (f) act |= m[k] & amask;
     bal[k] = __ballot(f);
     if (tnp::lane() == 0) cnt[k][tnp::wave()] = __popcll(bal[k]);
   }
@@ -811,6 +828,8 @@ k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, uint64_t fmask, uint64_t amas
     if ((bal[k] >> tnp::lane()) & 1) {
       const int64_t o = off + tnp::mbcnt(bal[k]);
       reinterpret_cast<int2*>(out)[o] = make_int2(a[k], b[k]);
+      odm[o] = d[k];
+      osm[o] = m[k];
       used[a[k]] = 1;
       used[b[k]] = 1;
     }
@@ -823,6 +842,35 @@ k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, uint64_t fmask, uint64_t amas
   if (threadIdx.x == 0) {
     uint64_t t = 0;
     for (int w = 0; w < TNP_WAVES; ++w) t |= acts[w];
+    tnp::or_sticky(&ctr[CTR_ACTIVE], t);
+  }
+}
+
+// masks of every edge from the endpoint keys (after a load, or when the
+// curve path rewired edges); OR of the split masks on planes of amask into
+// ctr[CTR_ACTIVE] when ctr != null
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_edge_masks(const int32_t* __restrict__ edges, int64_t E, const ulonglong2* __restrict__ pz,
+             uint64_t* __restrict__ dm, uint64_t* __restrict__ sm, uint64_t amask,
+             int64_t* __restrict__ ctr) {
+  __shared__ uint64_t lds[TNP_WAVES];
+  uint64_t act = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < E;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int2 ab = reinterpret_cast<const int2*>(edges)[i];
+    const ulonglong2 ka = pz[ab.x], kb = pz[ab.y];
+    const uint64_t s = (ka.x ^ kb.x) & ~ka.y & ~kb.y;
+    dm[i] = (ka.x ^ kb.x) | (ka.y ^ kb.y);
+    sm[i] = s;
+    act |= s & amask;
+  }
+  if (!ctr) return;
+  act = tnp::wave_or(act);
+  if (tnp::lane() == 0) lds[tnp::wave()] = act;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t t = 0;
+    for (int w = 0; w < TNP_WAVES; ++w) t |= lds[w];
     tnp::or_sticky(&ctr[CTR_ACTIVE], t);
   }
 }
@@ -911,11 +959,12 @@ int64_t step_tiles(int64_t n) { return (n + TILE - 1) / TILE; }
 int64_t lb_tiles(int64_t n) { return (n + LTILE - 1) / LTILE; }
 int64_t split_tiles(int64_t n) { return (n + STILE - 1) / STILE; }
 
-int launch_split_lb(int32_t* edges, int64_t E, const float* col, float eps, int64_t V, int32_t* sa,
-                    int32_t* sb, int64_t* ctr, int32_t* eidx, const TnpLB& lb, hipStream_t s) {
+int launch_split_lb(int32_t* edges, int64_t E, const uint64_t* sm, uint64_t* dm, int idx, int64_t V,
+                    int32_t* sa, int32_t* sb, int64_t* ctr, int32_t* eidx, const TnpLB& lb,
+                    hipStream_t s) {
   const int64_t tiles = split_tiles(E);
-  hipLaunchKernelGGL(k_split_lb, dim3((unsigned)tiles), dim3(TNP_BLOCK), 0, s, edges, E, tiles, col,
-                     eps, V, sa, sb, ctr, eidx, lb);
+  hipLaunchKernelGGL(k_split_lb, dim3((unsigned)tiles), dim3(TNP_BLOCK), 0, s, edges, E, tiles, sm, dm,
+                     idx, V, sa, sb, ctr, eidx, lb);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
@@ -1051,7 +1100,8 @@ int launch_prune(bool emit, const int32_t* edges, int64_t E, const int32_t* sb, 
 }
 int launch_prune_lb(const int32_t* edges, int64_t E, const int32_t* sb, int64_t S, int64_t V,
                     const uint64_t* ckeys, int nb, int64_t X, int idx, int last_plane,
-                    const uint64_t* pz, int32_t* out, int32_t* used, int64_t* ctr, const TnpLB& lb,
+                    const uint64_t* pz, const uint64_t* dm, const uint64_t* sm, int32_t* out,
+                    uint64_t* odm, uint64_t* osm, int32_t* used, int64_t* ctr, const TnpLB& lb,
                     hipStream_t s) {
   EdgeSrc src{edges, E, sb, S, V, ckeys, nb, X};
   const int64_t N = E + S + X;
@@ -1064,7 +1114,8 @@ int launch_prune_lb(const int32_t* edges, int64_t E, const int32_t* sb, int64_t 
   if (last_plane < 63) amask &= (1ull << (last_plane + 1)) - 1ull;
   const int64_t tiles = lb_tiles(N);
   hipLaunchKernelGGL(k_prune_lb, dim3((unsigned)tiles), dim3(TNP_BLOCK), 0, s, src, N, tiles, fmask,
-                     amask, reinterpret_cast<const ulonglong2*>(pz), out, used, ctr, lb);
+                     amask, reinterpret_cast<const ulonglong2*>(pz), dm, sm, out, odm, osm, used, ctr,
+                     lb);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
@@ -1072,6 +1123,17 @@ int launch_count_flags(const int32_t* f, int64_t n, int64_t* ctr, int slot, hipS
   if (n <= 0) return 0;
   const unsigned g = (unsigned)std::min<int64_t>(2048, (n + 4 * TNP_BLOCK - 1) / (4 * TNP_BLOCK));
   hipLaunchKernelGGL(k_count_flags, dim3(g), dim3(TNP_BLOCK), 0, s, f, n, ctr, slot);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_edge_masks(const int32_t* edges, int64_t E, const uint64_t* pz, uint64_t* dm,
+                      uint64_t* sm, int from, int last_plane, int64_t* ctr, hipStream_t s) {
+  if (E <= 0) return 0;
+  uint64_t amask = (from >= 64) ? 0ull : (~0ull << from);
+  if (last_plane < 63) amask &= (1ull << (last_plane + 1)) - 1ull;
+  const unsigned g = (unsigned)std::min<int64_t>(4096, tnp_grid(E));
+  hipLaunchKernelGGL(k_edge_masks, dim3(g), dim3(TNP_BLOCK), 0, s, edges, E,
+                     reinterpret_cast<const ulonglong2*>(pz), dm, sm, amask, ctr);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
