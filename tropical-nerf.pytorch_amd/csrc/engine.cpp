@@ -147,6 +147,7 @@ struct tnp_engine {
   // compact_now() renumbers once, before anything exports or reads ids.
   bool dirty = false;
   int64_t V_live = 0;
+  Buf live;  // live-slot flags (uint8) of the lazily compacted vertex set
   // step scratch
   Buf spcnt, spoff, part, ekey_a, ekey_b, eval_b, cellend, sort_scr2;
   Buf blk, blkoff, scan_scr, sa, sb, stage, shared, members, cellcnt, cellcur, celloff, ent_v,
@@ -273,8 +274,8 @@ static int keys_for(tnp_engine* e, VSet& v, int64_t from, int64_t n, hipStream_t
 
 // live flags of slots [from, from + n) := 1 (kept capacity: earlier flags stay)
 static int set_alive(tnp_engine* e, int64_t from, int64_t n, hipStream_t s) {
-  if (buf_ensure(e->used, std::max<int64_t>(from + n, 1) * sizeof(int32_t), s, true)) return -1;
-  if (n > 0) TNP_CHECK(hipMemsetD32Async((hipDeviceptr_t)(P<int32_t>(e->used) + from), 1, n, s));
+  if (buf_ensure(e->live, std::max<int64_t>(from + n, 16), s, true)) return -1;
+  if (n > 0) TNP_CHECK(hipMemsetAsync(P<uint8_t>(e->live) + from, 1, n, s));
   return 0;
 }
 
@@ -306,6 +307,8 @@ static int compact_now(tnp_engine* e, hipStream_t s) {
   if (!e->dirty) return 0;
   const int64_t NV = e->V;
   if (buf_ensure(e->nid, std::max<int64_t>(NV, 1) * sizeof(int64_t), s)) return -1;
+  if (buf_ensure(e->used, std::max<int64_t>(NV, 1) * sizeof(int32_t), s)) return -1;
+  if (launch_widen_flags(P<uint8_t>(e->live), NV, P<int32_t>(e->used), s)) return -1;
   if (scan_counts(e, P<int32_t>(e->used), P<int64_t>(e->nid), NV, CTR_AUX, s)) return -1;
   if (vset_ensure(e, e->alt, NV, 0, s)) return -1;
   VSet& c = e->cur;
@@ -360,7 +363,7 @@ extern "C" void tnp_engine_destroy(tnp_engine* e) {
                  &e->ent_v, &e->ent_g, &e->ent_p, &e->ent_z, &e->tcnt, &e->toff, &e->bcell,
                  &e->bstat, &e->ckeys_a, &e->ckeys_b, &e->sort_scr, &e->flags, &e->used, &e->nid,
                  &e->ctr, &e->tri, &e->faces, &e->lb[0], &e->lb[1], &e->edm, &e->esm,
-                 &e->edm_alt, &e->esm_alt};
+                 &e->edm_alt, &e->esm_alt, &e->live};
   for (Buf* b : bufs) buf_free(*b, s);
   for (Buf& b : e->fscr) buf_free(b, s);
   for (Buf& b : e->fscr2) buf_free(b, s);
@@ -764,7 +767,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     TnpLB lb;
     if (V > 0 && lb_begin(e, split_tiles(V), s, &lb)) return -1;
     TIMED("hits", 8.0 * V + 4.0 * S,
-          launch_hits(col, P<int32_t>(e->used), V, eps, P<int32_t>(e->members), S, ctr, lb, s));
+          launch_hits(col, P<uint8_t>(e->live), V, eps, P<int32_t>(e->members), S, ctr, lb, s));
   }
 
   // 3. bucket members by grid cell (dense cell grid over the marks): one
@@ -915,8 +918,8 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   if (prune) {
     // live flags recomputed from the kept edges; no vertex moves (lazy
     // compaction): the distinct flagged count is the reference's V'
-    if (buf_ensure(e->used, std::max<int64_t>(NV, 1) * sizeof(int32_t), s)) return -1;
-    TNP_CHECK(hipMemsetAsync(e->used.p, 0, NV * sizeof(int32_t), s));
+    if (buf_ensure(e->live, std::max<int64_t>(NV, 16), s)) return -1;
+    TNP_CHECK(hipMemsetAsync(e->live.p, 0, NV, s));
     if (ensure_masks(e, s)) return -1;  // (curve path: recomputed after the rewiring)
     const int64_t N1 = std::max<int64_t>(N, 1);
     if (buf_ensure(e->edm_alt, N1 * sizeof(uint64_t), s)) return -1;
@@ -927,10 +930,10 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
           launch_prune_lb(eg, E, P<int32_t>(e->sb), S, V, e->ckeys, nb, X, idx, K - 1,
                           P<uint64_t>(c.pz), P<uint64_t>(e->edm), P<uint64_t>(e->esm),
                           P<int32_t>(e->edges_alt), P<uint64_t>(e->edm_alt), P<uint64_t>(e->esm_alt),
-                          P<int32_t>(e->used), ctr, lb, s));
+                          P<uint8_t>(e->live), ctr, lb, s));
     std::swap(e->edm, e->edm_alt);
     std::swap(e->esm, e->esm_alt);
-    TIMED("count_live", 4.0 * NV, launch_count_flags(P<int32_t>(e->used), NV, ctr, CTR_V, s));
+    TIMED("count_live", 1.0 * NV, launch_count_flags(P<uint8_t>(e->live), NV, ctr, CTR_V, s));
     next_valid = e->keep_all ? 0 : std::min(idx + 1, K - 1);
     if (read_ctr(e, s)) return -1;
     E2 = e->h_ctr[CTR_E];

@@ -58,7 +58,7 @@ int launch_finalize_new(int64_t S, int K, int override_, const uint64_t* shared,
                         uint64_t* zero, const int64_t* ctr, uint64_t* pz, hipStream_t s);
 // members = [V, V + S) ++ live vertices v < V with |col[v]| < eps (ascending,
 // single pass over split_tiles(V) look-back tiles); count -> ctr[CTR_H]
-int launch_hits(const float* col, const int32_t* alive, int64_t V, float eps, int32_t* members,
+int launch_hits(const float* col, const uint8_t* alive, int64_t V, float eps, int32_t* members,
                 int64_t S, int64_t* ctr, const TnpLB& lb, hipStream_t s);
 // sort-based cell bucketing: span counts (+ A), (cell, member) entries,
 // segment bounds of the cell-sorted entries, per-cell counts, key copies
@@ -111,10 +111,11 @@ int launch_connect(const int64_t* ptoff, const int32_t* pcell, const int32_t* ce
 int launch_prune_lb(const int32_t* edges, int64_t E, const int32_t* sb, int64_t S, int64_t V,
                     const uint64_t* ckeys, int nb, int64_t X, int idx, int last_plane,
                     const uint64_t* pz, const uint64_t* dm, const uint64_t* sm, int32_t* out,
-                    uint64_t* odm, uint64_t* osm, int32_t* used, int64_t* ctr, const TnpLB& lb,
+                    uint64_t* odm, uint64_t* osm, uint8_t* used, int64_t* ctr, const TnpLB& lb,
                     hipStream_t s);
-// ctr[slot] += number of non-zero flags in f[0, n) (16-B aligned f)
-int launch_count_flags(const int32_t* f, int64_t n, int64_t* ctr, int slot, hipStream_t s);
+// ctr[slot] += number of set byte flags in f[0, n) (16-B aligned f, 0/1 bytes)
+int launch_count_flags(const uint8_t* f, int64_t n, int64_t* ctr, int slot, hipStream_t s);
+int launch_widen_flags(const uint8_t* f, int64_t n, int32_t* out, hipStream_t s);
 // planes the pruning of step idx compares (idx .. last_plane)
 uint64_t prune_mask(int idx, int last_plane);
 // ---- sort.hip ----

@@ -182,7 +182,7 @@ __global__ void k_finalize_new(int64_t S, int K, int override_, const uint64_t* 
 // appended after the S new members; the last tile writes the count to
 // ctr[CTR_H].  alive: the live-slot flags of the lazily compacted vertex set
 __global__ void __launch_bounds__(TNP_BLOCK)
-k_hit_lb(const float* __restrict__ col, const int32_t* __restrict__ alive, int64_t V,
+k_hit_lb(const float* __restrict__ col, const uint8_t* __restrict__ alive, int64_t V,
          int64_t ntiles, float eps, int32_t* __restrict__ members, int64_t S,
          int64_t* __restrict__ ctr, TnpLB lb) {
   __shared__ int cnt[SIPT][TNP_WAVES];
@@ -190,7 +190,7 @@ k_hit_lb(const float* __restrict__ col, const int32_t* __restrict__ alive, int64
   const int64_t tile = tnp::lb_tile(lb, &slot);
   const int64_t base = tile * STILE;
   float c[SIPT];
-  int32_t al[SIPT];
+  uint8_t al[SIPT];
   uint64_t bal[SIPT];
 #pragma unroll
   for (int k = 0; k < SIPT; ++k) {  // unconditional (clamped) loads, all in flight
@@ -731,7 +731,7 @@ __global__ void __launch_bounds__(TNP_BLOCK)
 k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, uint64_t fmask, uint64_t amask,
            const ulonglong2* __restrict__ pz, const uint64_t* __restrict__ dm,
            const uint64_t* __restrict__ sm, int32_t* __restrict__ out, uint64_t* __restrict__ odm,
-           uint64_t* __restrict__ osm, int32_t* __restrict__ used, int64_t* __restrict__ ctr,
+           uint64_t* __restrict__ osm, uint8_t* __restrict__ used, int64_t* __restrict__ ctr,
            TnpLB lb) {
   __shared__ int cnt[LIPT][TNP_WAVES];
   __shared__ int64_t slot;
@@ -875,17 +875,20 @@ k_edge_masks(const int32_t* __restrict__ edges, int64_t E, const ulonglong2* __r
   }
 }
 
-// number of set flags -> ctr[slot] (+=, one atomic per block)
+// number of set byte flags -> ctr[slot] (+=, one atomic per block)
 __global__ void __launch_bounds__(TNP_BLOCK)
-k_count_flags(const int32_t* __restrict__ f, int64_t n, int64_t* __restrict__ ctr, int slot) {
+k_count_flags(const uint8_t* __restrict__ f, int64_t n, int64_t* __restrict__ ctr, int slot) {
   __shared__ int lds[TNP_WAVES];
   int c = 0;
-  const int64_t i0 = ((int64_t)blockIdx.x * TNP_BLOCK + threadIdx.x) * 4;
-  const int64_t stride = (int64_t)gridDim.x * TNP_BLOCK * 4;
+  const int64_t i0 = ((int64_t)blockIdx.x * TNP_BLOCK + threadIdx.x) * 16;
+  const int64_t stride = (int64_t)gridDim.x * TNP_BLOCK * 16;
   for (int64_t i = i0; i < n; i += stride) {
-    if (i + 3 < n) {
-      const int4 v = *reinterpret_cast<const int4*>(f + i);
-      c += (v.x != 0) + (v.y != 0) + (v.z != 0) + (v.w != 0);
+    if (i + 15 < n) {
+      const uint4 v = *reinterpret_cast<const uint4*>(f + i);
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q)  // bytes are 0/1
+        c += __popc(w[q] & 0x01010101u);
     } else {
       for (int64_t j = i; j < n; ++j) c += f[j] != 0;
     }
@@ -898,6 +901,12 @@ k_count_flags(const int32_t* __restrict__ f, int64_t n, int64_t* __restrict__ ct
     for (int w = 0; w < TNP_WAVES; ++w) t += lds[w];
     if (t) atomicAdd((unsigned long long*)&ctr[slot], (unsigned long long)t);
   }
+}
+
+// byte flags -> int32 flags (the compaction scan's input)
+__global__ void k_widen_flags(const uint8_t* __restrict__ f, int64_t n, int32_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = f[i];
 }
 
 __global__ void k_gather_vertices(const int32_t* __restrict__ used, const int64_t* __restrict__ nid,
@@ -994,7 +1003,7 @@ int launch_finalize_new(int64_t S, int K, int override_, const uint64_t* shared,
   TNP_CHECK(hipGetLastError());
   return 0;
 }
-int launch_hits(const float* col, const int32_t* alive, int64_t V, float eps, int32_t* members,
+int launch_hits(const float* col, const uint8_t* alive, int64_t V, float eps, int32_t* members,
                 int64_t S, int64_t* ctr, const TnpLB& lb, hipStream_t s) {
   if (V > 0) {
     const int64_t tiles = split_tiles(V);
@@ -1101,7 +1110,7 @@ int launch_prune(bool emit, const int32_t* edges, int64_t E, const int32_t* sb, 
 int launch_prune_lb(const int32_t* edges, int64_t E, const int32_t* sb, int64_t S, int64_t V,
                     const uint64_t* ckeys, int nb, int64_t X, int idx, int last_plane,
                     const uint64_t* pz, const uint64_t* dm, const uint64_t* sm, int32_t* out,
-                    uint64_t* odm, uint64_t* osm, int32_t* used, int64_t* ctr, const TnpLB& lb,
+                    uint64_t* odm, uint64_t* osm, uint8_t* used, int64_t* ctr, const TnpLB& lb,
                     hipStream_t s) {
   EdgeSrc src{edges, E, sb, S, V, ckeys, nb, X};
   const int64_t N = E + S + X;
@@ -1119,9 +1128,15 @@ int launch_prune_lb(const int32_t* edges, int64_t E, const int32_t* sb, int64_t 
   TNP_CHECK(hipGetLastError());
   return 0;
 }
-int launch_count_flags(const int32_t* f, int64_t n, int64_t* ctr, int slot, hipStream_t s) {
+int launch_widen_flags(const uint8_t* f, int64_t n, int32_t* out, hipStream_t s) {
   if (n <= 0) return 0;
-  const unsigned g = (unsigned)std::min<int64_t>(2048, (n + 4 * TNP_BLOCK - 1) / (4 * TNP_BLOCK));
+  hipLaunchKernelGGL(k_widen_flags, dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, f, n, out);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_count_flags(const uint8_t* f, int64_t n, int64_t* ctr, int slot, hipStream_t s) {
+  if (n <= 0) return 0;
+  const unsigned g = (unsigned)std::min<int64_t>(2048, (n + 16 * TNP_BLOCK - 1) / (16 * TNP_BLOCK));
   hipLaunchKernelGGL(k_count_flags, dim3(g), dim3(TNP_BLOCK), 0, s, f, n, ctr, slot);
   TNP_CHECK(hipGetLastError());
   return 0;
