@@ -111,18 +111,27 @@ k_forward_new(NetDev net, const float* xyz, int64_t n, float* __restrict__ pre,
   uint64_t m = 0;
   if (live) {
     const int a = sa[i], b = sb[i];
+    // every gather the endpoints need, issued before the first store (the
+    // coordinate store could alias zero[] for the compiler)
+    const uint64_t za = zero[a], zb = zero[b];
     if (scol) {
       // the split point itself (k_new_vertices, subpoly.py:113-117, 180), fused:
       // d = d/eps; w = |d0| / |d1 - d0|; v = e0*(1-w) + e1*w
       const float* base = xyz - 3 * V;  // xyz points at slot V
-      const float d0 = __fdiv_rn(scol[a], eps), d1 = __fdiv_rn(scol[b], eps);
+      const float c0 = scol[a], c1 = scol[b];
+      float ea[3], eb[3];
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        ea[d] = base[3 * (int64_t)a + d];
+        eb[d] = base[3 * (int64_t)b + d];
+      }
+      const float d0 = __fdiv_rn(c0, eps), d1 = __fdiv_rn(c1, eps);
       const float w = __fdiv_rn(fabsf(d0), fabsf(__fsub_rn(d1, d0)));
       const float om = __fsub_rn(1.0f, w);
       float* out = const_cast<float*>(xyz) + 3 * i;
 #pragma unroll
       for (int d = 0; d < 3; ++d) {
-        const float v = __fadd_rn(__fmul_rn(base[3 * (int64_t)a + d], om),
-                                  __fmul_rn(base[3 * (int64_t)b + d], w));
+        const float v = __fadd_rn(__fmul_rn(ea[d], om), __fmul_rn(eb[d], w));
         out[d] = v;
         x[d] = __fdiv_rn(__fadd_rn(v, 1.0f), 2.0f);  // Net.preprocess, as load_point
       }
@@ -130,7 +139,7 @@ k_forward_new(NetDev net, const float* xyz, int64_t n, float* __restrict__ pre,
       load_point(xyz, i, x);
     }
     const uint64_t below = (idx >= 64) ? ~0ull : ((1ull << idx) - 1ull);
-    m = (zero[a] & zero[b] & below) | (1ull << idx);
+    m = (za & zb & below) | (1ull << idx);
   }
   float h[H > IN ? H : IN];
   float a[H];
