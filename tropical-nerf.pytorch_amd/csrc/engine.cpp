@@ -773,6 +773,10 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   // 3. bucket members by grid cell (dense cell grid over the marks): one
   //    (cell, member) entry per spanned cell, radix-sorted by cell
   const int NC = e->net.n_marks + 2;
+  if (NC > 1023) {  // connect packs cell coordinates in 10 bits each
+    tnp_set_error("more than 1021 marks per axis");
+    return -1;
+  }
   const int64_t ncell = (int64_t)NC * NC * NC;
   // the live member count sizes the span pass and its scan (V counts every
   // slot, live or dead: sizing by it would scan ~V elements per step)

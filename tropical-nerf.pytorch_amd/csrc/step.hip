@@ -490,13 +490,15 @@ __global__ void k_chunk_cells(const int64_t* __restrict__ ptoff, const int32_t* 
 // Persistent over the chunks of the pair space (count read on the device);
 // stops at once if the complex is degenerate (pairs above the limit) or the
 // chunk table overflowed -- the host reports either after the fact.
-// row i and column j (j < i) of in-cell pair q (q = i (i - 1) / 2 + j)
+// row i and column j (j < i) of in-cell pair q (q = i (i - 1) / 2 + j);
+// q < 2^31 (a cell holds <= 65535 members), so 32-bit unsigned arithmetic
 __device__ __forceinline__ void pair_row(int q, int& i, int& j) {
-  int r = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)q)) * 0.5f);
-  while ((int64_t)r * (r - 1) / 2 > q) --r;
-  while ((int64_t)(r + 1) * r / 2 <= q) ++r;
-  i = r;
-  j = q - (int)((int64_t)r * (r - 1) / 2);
+  const uint32_t uq = (uint32_t)q;
+  uint32_t r = (uint32_t)((1.0f + sqrtf(1.0f + 8.0f * (float)q)) * 0.5f);
+  while (r * (r - 1) / 2 > uq) --r;
+  while ((r + 1) * r / 2 <= uq) ++r;
+  i = (int)r;
+  j = (int)(uq - r * (r - 1) / 2);
 }
 
 // Lane-interleaved enumeration: the 64 lanes of a wave take 64 CONSECUTIVE
@@ -513,9 +515,9 @@ k_connect(const int64_t* __restrict__ ptoff, const int32_t* __restrict__ pcell,
   __shared__ int64_t lds[TNP_WAVES];
   __shared__ int64_t s_base;
   __shared__ int32_t s_off[CONNECT_CELLS];  // first pair of the cell - chunk start
-  __shared__ int32_t s_cell[CONNECT_CELLS];
   __shared__ int32_t s_n[CONNECT_CELLS];
   __shared__ int32_t s_ent[CONNECT_CELLS];  // first entry of the cell
+  __shared__ int32_t s_cc[CONNECT_CELLS];   // cell coordinates + 2, 10 bits each
   const int64_t TT = ctr[CTR_TESTS];
   const int64_t R = ctr[CTR_R];
   if (TT > max_tests || ctr[CTR_BOVF] || ctr[CTR_BIG]) return;
@@ -531,9 +533,10 @@ k_connect(const int64_t* __restrict__ ptoff, const int32_t* __restrict__ pcell,
   for (int t = threadIdx.x; t < nr; t += blockDim.x) {
     const int c = pcell[r0 + t];
     s_off[t] = (int32_t)(ptoff[r0 + t] - pb);  // > -2^31: a cell holds < 2^31 pairs
-    s_cell[t] = c;
     s_n[t] = cellcnt[c];
     s_ent[t] = (int32_t)celloff[c];
+    const int cz = c % NC, cy = (c / NC) % NC, cx = c / (NC * NC);  // = cell_coords + 2
+    s_cc[t] = cx | (cy << 10) | (cz << 20);
   }
   __syncthreads();
   const int64_t pw = pb + (int64_t)tnp::wave() * 64 * CIPT + tnp::lane();
@@ -558,10 +561,9 @@ k_connect(const int64_t* __restrict__ ptoff, const int32_t* __restrict__ pcell,
       while (lc + 1 < nr && s_off[lc + 1] <= x) ++lc;
       int i, j;
       pair_row(x - s_off[lc], i, j);
-      const int cell = s_cell[lc];
       const int64_t base = s_ent[lc];
-      int cc[3];
-      cell_coords(cell, NC, cc);
+      const int pc = s_cc[lc];
+      const int cc[3] = {(pc & 1023) - 2, ((pc >> 10) & 1023) - 2, ((pc >> 20) & 1023) - 2};
       const CellEnt eu = ent[base + i];
       const CellEnt ev = ent[base + j];
       PairTest t = pair_test(cc, below, eu.g, eu.p, eu.z, ev.g, ev.p, ev.z);
