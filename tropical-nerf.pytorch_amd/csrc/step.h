@@ -129,6 +129,8 @@ int sort_pairs_u32(uint32_t* ka, uint32_t* kb, int32_t* va, int32_t* vb, int64_t
                    void* scratch, size_t scratch_bytes, uint32_t** ko, int32_t** vo, hipStream_t s);
 int sort_keys_u64(uint64_t* a, uint64_t* b, int64_t n, int bits, void* scratch, size_t scratch_bytes,
                   uint64_t** out, hipStream_t s);
+// the final (non-pruning) step's edge list [edges; e_new; c_new] with
+// prune = 0 (emit must be true; the pruning steps use launch_prune_lb)
 int launch_prune(bool emit, const int32_t* edges, int64_t E, const int32_t* sb, int64_t S,
                  int64_t V, const uint64_t* ckeys, int nb, int64_t X, int idx,
                  int prune, int last_plane, const uint64_t* pos, const uint64_t* zero,
@@ -140,8 +142,7 @@ int launch_gather_vertices(const int32_t* used, const int64_t* nid, int64_t NV, 
                            float* xyz2, float* pre2, int64_t ld2, uint64_t* pos2, uint64_t* zero2,
                            uint64_t* grid2, uint64_t* pz2, hipStream_t s);
 int launch_remap_edges(int32_t* edges, int64_t E, const int64_t* nid, hipStream_t s);
-int launch_active_planes(const int32_t* edges, int64_t E, int from, int last_plane,
-                         const uint64_t* pos, const uint64_t* zero, int64_t* ctr, hipStream_t s);
+
 
 // ---- surface.hip ----
 int launch_surface_flags(const float* xyz, const float* col, int64_t V, float eps, int32_t* on,

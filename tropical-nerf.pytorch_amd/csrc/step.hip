@@ -647,30 +647,6 @@ __device__ __forceinline__ bool keep_edge(int a, int b, uint64_t fmask, const ui
   return ((pos[a] ^ pos[b]) & fmask) != 0 || ((zero[a] ^ zero[b]) & fmask) != 0;
 }
 
-__global__ void __launch_bounds__(TNP_BLOCK)
-k_prune_count(EdgeSrc src, int64_t N, uint64_t fmask, const uint64_t* __restrict__ pos,
-              const uint64_t* __restrict__ zero, int32_t* __restrict__ blk) {
-  __shared__ int lds[TNP_WAVES];
-  int64_t base = (int64_t)blockIdx.x * TILE;
-  int c = 0;
-#pragma unroll
-  for (int k = 0; k < IPT; ++k) {
-    int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
-    if (i < N) {
-      int a, b;
-      fetch_edge(src, i, a, b);
-      c += keep_edge(a, b, fmask, pos, zero);
-    }
-  }
-  c = tnp::wave_sum(c);
-  if (tnp::lane() == 0) lds[tnp::wave()] = c;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int t = 0;
-    for (int w = 0; w < TNP_WAVES; ++w) t += lds[w];
-    blk[blockIdx.x] = t;
-  }
-}
 
 // emits kept edges in order, flags used vertices and ORs the next-active
 // plane mask: planes > idx on which a kept edge has non-zero opposite signs
@@ -938,28 +914,6 @@ __global__ void k_remap_edges(int32_t* __restrict__ edges, int64_t E, const int6
   edges[i] = (int32_t)nid[edges[i]];
 }
 
-// initial next-active mask for an arbitrary edge set (grid-stride, one
-// sticky OR per block)
-__global__ void __launch_bounds__(TNP_BLOCK)
-k_active_planes(const int32_t* __restrict__ edges, int64_t E, uint64_t amask,
-                const uint64_t* __restrict__ pos, const uint64_t* __restrict__ zero,
-                int64_t* __restrict__ ctr) {
-  __shared__ uint64_t lds[TNP_WAVES];
-  uint64_t act = 0;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < E;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int a = edges[2 * i], b = edges[2 * i + 1];
-    act |= (pos[a] ^ pos[b]) & ~zero[a] & ~zero[b] & amask;
-  }
-  act = tnp::wave_or(act);
-  if (tnp::lane() == 0) lds[tnp::wave()] = act;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint64_t t = 0;
-    for (int w = 0; w < TNP_WAVES; ++w) t |= lds[w];
-    tnp::or_sticky(&ctr[CTR_ACTIVE], t);
-  }
-}
 
 }  // namespace
 
@@ -1100,12 +1054,10 @@ int launch_prune(bool emit, const int32_t* edges, int64_t E, const int32_t* sb, 
   uint64_t fmask = prune_mask(idx, last_plane);
   uint64_t amask = (idx + 1 >= 64) ? 0ull : (~0ull << (idx + 1));
   if (last_plane < 63) amask &= (1ull << (last_plane + 1)) - 1ull;
-  if (!emit)
-    hipLaunchKernelGGL(k_prune_count, dim3((unsigned)step_tiles(N)), dim3(TNP_BLOCK), 0, s, src, N,
-                       fmask, pos, zero, blk);
-  else
-    hipLaunchKernelGGL(k_prune_emit, dim3((unsigned)step_tiles(N)), dim3(TNP_BLOCK), 0, s, src, N,
-                       fmask, amask, pos, zero, blkoff, prune, out, used, ctr);
+  (void)emit;
+  (void)blk;
+  hipLaunchKernelGGL(k_prune_emit, dim3((unsigned)step_tiles(N)), dim3(TNP_BLOCK), 0, s, src, N,
+                     fmask, amask, pos, zero, blkoff, prune, out, used, ctr);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
@@ -1169,16 +1121,6 @@ int launch_gather_vertices(const int32_t* used, const int64_t* nid, int64_t NV, 
 int launch_remap_edges(int32_t* edges, int64_t E, const int64_t* nid, hipStream_t s) {
   if (E <= 0) return 0;
   hipLaunchKernelGGL(k_remap_edges, dim3(tnp_grid(2 * E)), dim3(TNP_BLOCK), 0, s, edges, E, nid);
-  TNP_CHECK(hipGetLastError());
-  return 0;
-}
-int launch_active_planes(const int32_t* edges, int64_t E, int from, int last_plane,
-                         const uint64_t* pos, const uint64_t* zero, int64_t* ctr, hipStream_t s) {
-  if (E <= 0) return 0;
-  uint64_t amask = (from >= 64) ? 0ull : (~0ull << from);
-  if (last_plane < 63) amask &= (1ull << (last_plane + 1)) - 1ull;
-  const unsigned g = (unsigned)std::min<int64_t>(2048, tnp_grid(E));
-  hipLaunchKernelGGL(k_active_planes, dim3(g), dim3(TNP_BLOCK), 0, s, edges, E, amask, pos, zero, ctr);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
