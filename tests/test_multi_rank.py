@@ -23,7 +23,9 @@ from golden_io import load
 from helpers import oracle_net
 
 CASE = "synth24"
-CUTS = [0, 11, 23]  # cells of marks [0, 11] -> rank 0, [11, 23] -> rank 1
+# world 2: cells of marks [0, 11] -> rank 0, [11, 23] -> rank 1; world 3:
+# three slabs, so the middle rank has a halo and a shared plane on both sides
+CUTS = {2: [0, 11, 23], 3: [0, 7, 15, 23]}
 
 
 def _free_port():
@@ -41,7 +43,7 @@ def _canon(V, E):
     return verts, edges
 
 
-def _slab_worker(rank, world, port, outdir):
+def _slab_worker(rank, world, port, outdir, cuts):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -54,8 +56,8 @@ def _slab_worker(rank, world, port, outdir):
         net = oracle_net(d)
         n = int(d["lattice_n"])
         from tropical.distributed import gather_complex, slab_marks, stitch
-        assert CUTS[-1] == n - 1
-        x0, x1 = slab_marks(CUTS, rank)
+        assert cuts[-1] == n - 1
+        x0, x1 = slab_marks(cuts, rank)
         V, E = slab_lattice(d["marks"], x0, x1)
         coll = bench.Collective(torch.device("cpu"))
 
@@ -64,7 +66,7 @@ def _slab_worker(rank, world, port, outdir):
 
         with torch.no_grad():
             V, E, _ = od.run_steps(torch.from_numpy(V), torch.from_numpy(E), net, 1e-4, sync=sync)
-        owned, first, gE = stitch(V, E, torch.from_numpy(d["marks"]), CUTS)
+        owned, first, gE = stitch(V, E, torch.from_numpy(d["marks"]), cuts)
         SV, SE = gather_complex(owned, first, gE)
         if rank == 0:
             np.savez(os.path.join(outdir, "stitched.npz"), V=SV.numpy(), E=SE.numpy())
@@ -94,10 +96,12 @@ def test_owner_rule_matches_cells_and_planes():
 
 
 @pytest.mark.slow
-def test_two_gloo_ranks_reproduce_the_unsharded_complex(tmp_path):
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_ranks_reproduce_the_unsharded_complex(tmp_path, world):
     import oracle.subdivide as od
     from tropical.synthetic import lattice_edges, lattice_vertices
-    mp.spawn(_slab_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    mp.spawn(_slab_worker, args=(world, _free_port(), str(tmp_path), CUTS[world]), nprocs=world,
+             join=True)
     d = load(CASE)
     net = oracle_net(d)
     n = int(d["lattice_n"])
