@@ -150,9 +150,11 @@ struct tnp_engine {
   Buf live;  // live-slot flags (uint8) of the lazily compacted vertex set
   // step scratch
   Buf spcnt, spoff, part, ekey_a, ekey_b, eval_b, cellend, sort_scr2;
-  Buf blk, blkoff, scan_scr, sa, sb, stage, shared, members, cellcnt, cellcur, celloff, ent_v,
-      ent_g, ent_p, ent_z, tcnt, toff, bcell, bstat, ckeys_a, ckeys_b, sort_scr, flags, used, nid,
-      ctr;
+  // (pcell/ptoff: compacted pair cells and their first pair; ents: CellEnt
+  // records in cell order; used/nid/flags: int32 scratch of compaction,
+  // surface and skeleton)
+  Buf blk, blkoff, scan_scr, sa, sb, stage, shared, members, cellcnt, celloff, ent_v,
+      ents, pcell, ptoff, bcell, bstat, ckeys_a, ckeys_b, sort_scr, flags, used, nid, ctr;
   uint64_t* ckeys = nullptr;  // sorted connecting edges of the current step
   int64_t* h_ctr = nullptr;  // pinned mirror of ctr
   // pending split
@@ -359,8 +361,8 @@ extern "C" void tnp_engine_destroy(tnp_engine* e) {
     buf_free(v->pz, s);
   }
   Buf* bufs[] = {&e->edges, &e->edges_alt, &e->blk, &e->blkoff, &e->scan_scr, &e->sa, &e->sb,
-                 &e->stage, &e->shared, &e->members, &e->cellcnt, &e->cellcur, &e->celloff,
-                 &e->ent_v, &e->ent_g, &e->ent_p, &e->ent_z, &e->tcnt, &e->toff, &e->bcell,
+                 &e->stage, &e->shared, &e->members, &e->cellcnt, &e->celloff,
+                 &e->ent_v, &e->ents, &e->pcell, &e->ptoff, &e->bcell,
                  &e->bstat, &e->ckeys_a, &e->ckeys_b, &e->sort_scr, &e->flags, &e->used, &e->nid,
                  &e->ctr, &e->tri, &e->faces, &e->lb[0], &e->lb[1], &e->edm, &e->esm,
                  &e->edm_alt, &e->esm_alt, &e->live};
@@ -820,8 +822,8 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   if (buf_ensure(e->celloff, ncell * sizeof(int64_t), s)) return -1;
   if (buf_ensure(e->cellend, ncell * sizeof(int64_t), s)) return -1;
   if (buf_ensure(e->cellcnt, ncell * sizeof(int32_t), s)) return -1;
-  if (buf_ensure(e->tcnt, ncell * sizeof(int32_t), s)) return -1;  // pair cells (ids)
-  if (buf_ensure(e->toff, ncell * sizeof(int64_t), s)) return -1;  // their first pair
+  if (buf_ensure(e->pcell, ncell * sizeof(int32_t), s)) return -1;
+  if (buf_ensure(e->ptoff, ncell * sizeof(int64_t), s)) return -1;
   TNP_CHECK(hipMemsetAsync(e->celloff.p, 0, ncell * sizeof(int64_t), s));
   TNP_CHECK(hipMemsetAsync(e->cellend.p, 0, ncell * sizeof(int64_t), s));
   TIMED("cell_bounds", 12.0 * T,
@@ -834,11 +836,11 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     if (lb_begin(e, pt, s, &lr, 0) || lb_begin(e, pt, s, &lp, 1)) return -1;
     TIMED("pair_cells", 28.0 * ncell,
           launch_pair_cells(P<int64_t>(e->celloff), P<int64_t>(e->cellend), ncell, P<int32_t>(e->cellcnt),
-                            P<int32_t>(e->tcnt), P<int64_t>(e->toff), ctr, lr, lp, s));
+                            P<int32_t>(e->pcell), P<int64_t>(e->ptoff), ctr, lr, lp, s));
   }
-  if (buf_ensure(e->ent_g, T1 * sizeof(CellEnt), s)) return -1;
+  if (buf_ensure(e->ents, T1 * sizeof(CellEnt), s)) return -1;
   TIMED("entry_keys", 52.0 * T,
-        launch_entry_keys(sval, T, grid, P<uint64_t>(c.pz), P<CellEnt>(e->ent_g), s));
+        launch_entry_keys(sval, T, grid, P<uint64_t>(c.pz), P<CellEnt>(e->ents), s));
 
   // 4. connecting edges: test every in-cell member pair once, append the
   //    emitted ones, radix-sort them (lexicographic c_new, subpoly.py:243-244).
@@ -858,7 +860,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     if (!chunks_ok) {
       if (buf_ensure(e->bcell, bcap * sizeof(int32_t), s)) return -1;
       if (attempt > 0) TNP_CHECK(hipMemsetAsync(ctr + CTR_BOVF, 0, sizeof(int64_t), s));
-      if (launch_chunk_cells(P<int64_t>(e->toff), P<int32_t>(e->tcnt), P<int32_t>(e->cellcnt), ncell,
+      if (launch_chunk_cells(P<int64_t>(e->ptoff), P<int32_t>(e->pcell), P<int32_t>(e->cellcnt), ncell,
                              P<int32_t>(e->bcell), bcap, ctr, s)) return -1;
     }
     if (buf_ensure(e->ckeys_a, std::max<int64_t>(cap, 1) * sizeof(uint64_t), s)) return -1;
@@ -868,9 +870,9 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
       TNP_CHECK(hipMemsetAsync(ctr + CTR_P, 0, 2 * sizeof(int64_t), s));  // CTR_P, CTR_COMPAT
     }
     TIMED("connect", 0.0,
-          launch_connect(P<int64_t>(e->toff), P<int32_t>(e->tcnt), P<int32_t>(e->cellcnt),
+          launch_connect(P<int64_t>(e->ptoff), P<int32_t>(e->pcell), P<int32_t>(e->cellcnt),
                          P<int64_t>(e->celloff), NC, e->max_pair_tests, P<int32_t>(e->bcell),
-                         P<CellEnt>(e->ent_g), idx, nb, cfmask, P<uint64_t>(e->ckeys_a), cap, ctr,
+                         P<CellEnt>(e->ents), idx, nb, cfmask, P<uint64_t>(e->ckeys_a), cap, ctr,
                          P<int64_t>(e->bstat), s));
     if (read_ctr(e, s)) return -1;
     TT = e->h_ctr[CTR_TESTS];
