@@ -705,7 +705,7 @@ k_prune_emit(EdgeSrc src, int64_t N, uint64_t fmask, uint64_t amask,
 // creation, so an edge's masks change only when the edge does: the prune
 // reads them coalesced for the old edges and gathers the endpoint keys only
 // for rewired (dm == EDGE_STALE), e_new and c_new edges.
-__global__ void __launch_bounds__(TNP_BLOCK)
+__global__ void __launch_bounds__(TNP_BLOCK, 4)
 k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, uint64_t fmask, uint64_t amask,
            const ulonglong2* __restrict__ pz, const uint64_t* __restrict__ dm,
            const uint64_t* __restrict__ sm, int32_t* __restrict__ out, uint64_t* __restrict__ odm,
