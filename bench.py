@@ -92,15 +92,15 @@ class Collective:
         self.device = device
 
     def __call__(self, vec: np.ndarray, op: str):
-        t = torch.tensor(vec.astype(np.int64).view(np.int64), device=self.device)
         if op == "or":
-            # OR of 64-bit masks: gather and OR on the host (RCCL has no BOR)
-            out = [torch.empty_like(t) for _ in range(self.dist.get_world_size())]
-            self.dist.all_gather(out, t)
-            acc = np.zeros_like(vec)
-            for o in out:
-                acc |= o.cpu().numpy().view(vec.dtype)
-            return acc
+            # OR of 64-bit plane masks as ONE all_reduce(MAX) over their bits
+            # (RCCL has no bitwise-or reduction)
+            bits = np.unpackbits(vec.astype(np.uint64).view(np.uint8), bitorder="little")
+            t = torch.tensor(bits, dtype=torch.int32, device=self.device)
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+            out = np.packbits(t.cpu().numpy().astype(np.uint8), bitorder="little")
+            return out.view(np.uint64).astype(vec.dtype)
+        t = torch.tensor(vec.astype(np.int64).view(np.int64), device=self.device)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return t.cpu().numpy()
 
