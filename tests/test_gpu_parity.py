@@ -179,3 +179,21 @@ def test_subpoly_step_dropin(cuda):
         l, h = divmod(int(idx), net.num_hidden)
         V, E, o = sp.subpoly_(V, E, net, l, h, 1e-4, o, force=True)
         assert sha(V.cpu().numpy(), E.cpu().numpy(), o.cpu().numpy()) == str(d["step_sha"][step])
+
+
+def test_tied_levels_layout(cuda, monkeypatch):
+    """The synthetic lattice nets have identical levels (r_min == r_max), so
+    the engine runs on its level-interleaved table copy (NetDev::tied); the
+    complex must be bitwise the one the per-level tcnn layout gives."""
+    from tropical._engine import engine_for
+    d = load("synth32")
+    net = product_net(d, cuda)
+    runs = []
+    for untied in (False, True):
+        if untied:
+            monkeypatch.setenv("TNP_NO_TIED", "1")
+        eng = engine_for(net)
+        eng.lattice(keep_all=True)
+        runs.append(engine_steps(eng))
+    assert runs[0] == runs[1]
+    assert runs[0][-1][:2] == (int(d["step_V"][-1]), int(d["step_E"][-1]))

@@ -587,7 +587,6 @@ __device__ __forceinline__ void plane_pair_grad(const NetDev& net, const float* 
       g[d] = (uint32_t)(int)fl;
     }
     const uint32_t res = (uint32_t)net.res[l];
-    const float2* tab = reinterpret_cast<const float2*>(net.table) + net.offsets[l];
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
       float fc[3];
@@ -601,7 +600,7 @@ __device__ __forceinline__ void plane_pair_grad(const NetDev& net, const float* 
       uint32_t id = net.dense[l] ? (gc[0] + gc[1] * res + gc[2] * (res * res))
                                  : (gc[0] ^ (gc[1] * P1) ^ (gc[2] * P2));
       id %= net.sizes[l];
-      float2 v = tab[id];
+      float2 v = table_entry(net, l, id);
       float dv = __fadd_rn(__fmul_rn(v.x, df[2 * l]), __fmul_rn(v.y, df[2 * l + 1]));
 #pragma unroll
       for (int d = 0; d < 3; ++d) {

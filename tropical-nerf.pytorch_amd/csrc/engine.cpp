@@ -163,6 +163,7 @@ struct tnp_engine {
   bool pend_fused = false;  // the pending split ran k_forward_new (flat path)
   // faces output
   Buf tri, faces;
+  Buf tied_table;  // level-interleaved copy of the caller's table (NetDev::tied)
   int64_t n_tri = 0, n_faces = 0, dbg_F = 0, dbg_W = 0;
   // look-back states (a kernel may run two chains): [0] ticket counter,
   // [1..] tile status words; tickets issued so far; launch epoch
@@ -365,7 +366,7 @@ extern "C" void tnp_engine_destroy(tnp_engine* e) {
                  &e->ent_v, &e->ents, &e->pcell, &e->ptoff, &e->bcell,
                  &e->bstat, &e->ckeys_a, &e->ckeys_b, &e->sort_scr, &e->flags, &e->used, &e->nid,
                  &e->ctr, &e->tri, &e->faces, &e->lb[0], &e->lb[1], &e->edm, &e->esm,
-                 &e->edm_alt, &e->esm_alt, &e->live};
+                 &e->edm_alt, &e->esm_alt, &e->live, &e->tied_table};
   for (Buf* b : bufs) buf_free(*b, s);
   for (Buf& b : e->fscr) buf_free(b, s);
   for (Buf& b : e->fscr2) buf_free(b, s);
@@ -411,9 +412,35 @@ static int check_net(const tnp_net* n) {
   return 0;
 }
 
+// Levels with the same fp32 scale, resolution, table size and addressing
+// (e.g. the synthetic lattice nets, r_min == r_max) share corner weights and
+// hash indices: the engine keeps a level-interleaved copy of the table so a
+// corner is one 16-B gather for two levels (net_device.h encode_tied).
+static bool levels_tied(const tnp_net* n) {
+  if (n->n_levels < 2 || n->n_levels % 2 != 0 || getenv("TNP_NO_TIED")) return false;
+  for (int l = 1; l < n->n_levels; ++l)
+    if (memcmp(&n->scales[l], &n->scales[0], sizeof(float)) != 0 || n->res[l] != n->res[0] ||
+        n->sizes[l] != n->sizes[0] || n->dense[l] != n->dense[0])
+      return false;
+  return true;
+}
+
 extern "C" int tnp_engine_set_net(tnp_engine* e, const tnp_net* n) {
   if (check_net(n)) return -1;
+  TNP_CHECK(hipSetDevice(e->device));
   e->net = to_dev(n);
+  if (levels_tied(n)) {
+    const int L = n->n_levels;
+    const size_t entry = 2 * sizeof(float);
+    if (buf_ensure(e->tied_table, (size_t)n->sizes[0] * L * entry, 0)) return -1;
+    for (int l = 0; l < L; ++l)
+      TNP_CHECK(hipMemcpy2DAsync(static_cast<char*>(e->tied_table.p) + l * entry, L * entry,
+                                 n->d_table + 2 * (size_t)n->offsets[l], entry, entry, n->sizes[0],
+                                 hipMemcpyDeviceToDevice, 0));
+    TNP_CHECK(hipStreamSynchronize(0));
+    e->net.table = P<float>(e->tied_table);
+    e->net.tied = 1;
+  }
   e->K = net_K(e->net);
   e->has_net = true;
   return 0;

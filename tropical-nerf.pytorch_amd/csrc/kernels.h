@@ -19,6 +19,11 @@ struct NetDev {
   const float* marks;
   int32_t n_levels, num_layers, num_hidden, n_marks;
   float eps;
+  // 1: every level has the same scale/res/size/dense, so one set of corner
+  // weights and hash indices serves all levels, and `table` is the engine's
+  // level-interleaved copy: entry idx of level l at float2 (idx * L + l) --
+  // one 16-B gather per corner instead of L 8-B gathers in L cache lines
+  int32_t tied;
 };
 
 static inline int net_K(const NetDev& n) { return (n.num_layers - 1) * n.num_hidden + 1; }

@@ -10,8 +10,72 @@ namespace tnpnet {
 constexpr uint32_t P1 = 2654435761u;
 constexpr uint32_t P2 = 805459861u;
 
+// float2 entry `idx` of level l in either table layout (NetDev::tied)
+__device__ __forceinline__ float2 table_entry(const NetDev& net, int l, uint32_t idx) {
+  const float2* tab = reinterpret_cast<const float2*>(net.table);
+  return net.tied ? tab[(size_t)idx * net.n_levels + l] : tab[net.offsets[l] + idx];
+}
+
+// Tied levels: positions, weights and indices are those of level 0 for
+// every level (same fp32 scale), the per-level sums keep the corner order
+// of the untied path, so the features are bitwise the same.
+template <int LV>
+__device__ __forceinline__ void encode_tied(const NetDev& net, const float x[3], float* feat) {
+  const float s = net.scales[0];
+  float t[3];
+  uint32_t g[3];
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    float pos = __fadd_rn(__fmul_rn(x[d], s), 0.5f);
+    float fl = floorf(pos);
+    t[d] = __fsub_rn(pos, fl);
+    g[d] = (uint32_t)(int)fl;
+  }
+  const uint32_t res = (uint32_t)net.res[0];
+  const uint32_t size = net.sizes[0];
+  const bool dense = net.dense[0] != 0;
+  const float4* tab = reinterpret_cast<const float4*>(net.table);
+  float acc[2 * LV];
+#pragma unroll
+  for (int q = 0; q < 2 * LV; ++q) acc[q] = 0.f;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    float w = 1.0f;
+    uint32_t gc[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      if ((c >> d) & 1) {
+        w = __fmul_rn(w, t[d]);
+        gc[d] = g[d] + 1u;
+      } else {
+        w = __fmul_rn(w, __fsub_rn(1.0f, t[d]));
+        gc[d] = g[d];
+      }
+    }
+    uint32_t idx = dense ? (gc[0] + gc[1] * res + gc[2] * (res * res))
+                         : (gc[0] ^ (gc[1] * P1) ^ (gc[2] * P2));
+    idx %= size;
+#pragma unroll
+    for (int q = 0; q < LV / 2; ++q) {
+      const float4 v = tab[(size_t)idx * (LV / 2) + q];
+      acc[4 * q + 0] = __fadd_rn(acc[4 * q + 0], __fmul_rn(w, v.x));
+      acc[4 * q + 1] = __fadd_rn(acc[4 * q + 1], __fmul_rn(w, v.y));
+      acc[4 * q + 2] = __fadd_rn(acc[4 * q + 2], __fmul_rn(w, v.z));
+      acc[4 * q + 3] = __fadd_rn(acc[4 * q + 3], __fmul_rn(w, v.w));
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 2 * LV; ++q) feat[q] = acc[q];
+}
+
 template <int LV>
 __device__ __forceinline__ void encode(const NetDev& net, const float x[3], float* feat) {
+  if constexpr (LV % 2 == 0) {
+    if (net.tied) {
+      encode_tied<LV>(net, x, feat);
+      return;
+    }
+  }
 #pragma unroll
   for (int l = 0; l < LV; ++l) {
     const float s = net.scales[l];
@@ -155,7 +219,6 @@ __device__ __forceinline__ float sdf_grad(const NetDev& net, const float* w, con
       g[d] = (uint32_t)(int)fl;
     }
     const uint32_t res = (uint32_t)net.res[l];
-    const float2* tab = reinterpret_cast<const float2*>(net.table) + net.offsets[l];
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
       float fc[3];
@@ -169,7 +232,7 @@ __device__ __forceinline__ float sdf_grad(const NetDev& net, const float* w, con
       uint32_t idx = net.dense[l] ? (gc[0] + gc[1] * res + gc[2] * (res * res))
                                   : (gc[0] ^ (gc[1] * P1) ^ (gc[2] * P2));
       idx %= net.sizes[l];
-      float2 v = tab[idx];
+      float2 v = table_entry(net, l, idx);
       float dv = v.x * df[2 * l] + v.y * df[2 * l + 1];
 #pragma unroll
       for (int d = 0; d < 3; ++d) {
