@@ -160,6 +160,7 @@ struct tnp_engine {
   // pending split
   int pend_idx = -1;
   int64_t pend_S = 0, pend_dup = 0;
+  bool pend_hits = false;   // the pending split also found the plane's hit vertices
   bool pend_fused = false;  // the pending split ran k_forward_new (flat path)
   // faces output
   Buf tri, faces;
@@ -689,6 +690,7 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
   const float* col = P<float>(e->cur.pre) + (int64_t)idx * e->cur.cap;
   TNP_CHECK(hipMemsetAsync(e->ctr.p, 0, CTR_N * sizeof(int64_t), s));
   int64_t S = 0;
+  e->pend_hits = false;
   if (e->E > 0) {
     // single pass; the id buffers hold the upper bound E (capacity is kept)
     if (buf_ensure(e->sa, e->E * sizeof(int32_t), s)) return -1;
@@ -701,6 +703,18 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
           launch_split_lb(P<int32_t>(e->edges), e->E, P<uint64_t>(e->esm), P<uint64_t>(e->edm), idx,
                           e->V, P<int32_t>(e->sa), P<int32_t>(e->sb), P<int64_t>(e->ctr),
                           e->curve ? P<int32_t>(e->cv[CV_EIDX]) : nullptr, lb, s));
+    if (!e->curve && e->V > 0) {
+      // flat path: the plane's hit vertices right behind the split (they read
+      // only the cached column and the live flags), so one readback returns
+      // S and H; members holds [V, V+S) ++ hits, S <= E
+      if (buf_ensure(e->members, (e->E + e->V) * sizeof(int32_t), s)) return -1;
+      TnpLB lh;
+      if (lb_begin(e, split_tiles(e->V), s, &lh)) return -1;
+      TIMED("hits", 8.0 * e->V,
+            launch_hits(col, P<uint8_t>(e->live), e->V, eps, P<int32_t>(e->members), -1,
+                        P<int64_t>(e->ctr), lh, s));
+      e->pend_hits = true;
+    }
     if (read_ctr(e, s)) return -1;
     S = e->h_ctr[CTR_S];
   }
@@ -762,6 +776,8 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   TNP_CHECK(hipSetDevice(e->device));
   if (e->pend_idx != idx) { tnp_set_error("finish(%d) without split(%d)", idx, idx); return -1; }
   e->pend_idx = -1;
+  const bool hits_done = e->pend_hits;
+  e->pend_hits = false;
   const float eps = e->net.eps;
   const int K = e->K;
   int64_t S_kept = e->pend_S;
@@ -791,8 +807,10 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   }
 
   // 2. members = new vertices ++ live hit vertices (ascending)
-  if (buf_ensure(e->members, std::max<int64_t>(NV, 1) * sizeof(int32_t), s)) return -1;
-  {
+  if (buf_ensure(e->members, std::max<int64_t>(NV, 1) * sizeof(int32_t), s, hits_done)) return -1;
+  if (hits_done) {
+    if (launch_new_members(P<int32_t>(e->members), S, V, s)) return -1;
+  } else {
     TnpLB lb;
     if (V > 0 && lb_begin(e, split_tiles(V), s, &lb)) return -1;
     TIMED("hits", 8.0 * V + 4.0 * S,
@@ -809,7 +827,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   const int64_t ncell = (int64_t)NC * NC * NC;
   // the live member count sizes the span pass and its scan (V counts every
   // slot, live or dead: sizing by it would scan ~V elements per step)
-  if (read_ctr(e, s)) return -1;
+  if (!hits_done && read_ctr(e, s)) return -1;  // else: H came back with S
   const int64_t M = S + e->h_ctr[CTR_H];
   if (buf_ensure(e->spcnt, std::max<int64_t>(M, 1) * sizeof(int32_t), s)) return -1;
   if (buf_ensure(e->spoff, std::max<int64_t>(M, 1) * sizeof(int64_t), s)) return -1;

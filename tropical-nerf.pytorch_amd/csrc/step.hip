@@ -183,10 +183,12 @@ __global__ void k_finalize_new(int64_t S, int K, int override_, const uint64_t* 
 // ctr[CTR_H].  alive: the live-slot flags of the lazily compacted vertex set
 __global__ void __launch_bounds__(TNP_BLOCK)
 k_hit_lb(const float* __restrict__ col, const uint8_t* __restrict__ alive, int64_t V,
-         int64_t ntiles, float eps, int32_t* __restrict__ members, int64_t S,
+         int64_t ntiles, float eps, int32_t* __restrict__ members, int64_t S_arg,
          int64_t* __restrict__ ctr, TnpLB lb) {
   __shared__ int cnt[SIPT][TNP_WAVES];
   __shared__ int64_t slot;
+  // S_arg < 0: launched right behind the split, whose count is on the device
+  const int64_t S = S_arg < 0 ? ctr[CTR_S] : S_arg;
   const int64_t tile = tnp::lb_tile(lb, &slot);
   const int64_t base = tile * STILE;
   float c[SIPT];
@@ -968,8 +970,13 @@ int launch_hits(const float* col, const uint8_t* alive, int64_t V, float eps, in
   } else {
     TNP_CHECK(hipMemsetAsync(ctr + CTR_H, 0, sizeof(int64_t), s));
   }
-  if (S > 0)
-    hipLaunchKernelGGL(k_new_members, dim3(tnp_grid(S)), dim3(TNP_BLOCK), 0, s, members, S, V);
+  if (S > 0) return launch_new_members(members, S, V, s);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_new_members(int32_t* members, int64_t S, int64_t V, hipStream_t s) {
+  if (S <= 0) return 0;
+  hipLaunchKernelGGL(k_new_members, dim3(tnp_grid(S)), dim3(TNP_BLOCK), 0, s, members, S, V);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
