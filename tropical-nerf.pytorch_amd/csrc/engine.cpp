@@ -149,11 +149,11 @@ struct tnp_engine {
   int64_t V_live = 0;
   Buf live;  // live-slot flags (uint8) of the lazily compacted vertex set
   // step scratch
-  Buf spcnt, spoff, part, ekey_a, ekey_b, eval_b, cellend, sort_scr2;
+  Buf spcnt, spoff, part, ekey_a, ekey_b, eval_b, sort_scr2;
   // (pcell/ptoff: compacted pair cells and their first pair; ents: CellEnt
   // records in cell order; used/nid/flags: int32 scratch of compaction,
   // surface and skeleton)
-  Buf blk, blkoff, scan_scr, sa, sb, stage, shared, members, cellcnt, celloff, ent_v,
+  Buf blk, blkoff, scan_scr, sa, sb, stage, shared, members, pcn, pent, rstart, ent_v,
       ents, pcell, ptoff, bcell, bstat, ckeys_a, ckeys_b, sort_scr, flags, used, nid, ctr;
   uint64_t* ckeys = nullptr;  // sorted connecting edges of the current step
   int64_t* h_ctr = nullptr;  // pinned mirror of ctr
@@ -363,7 +363,7 @@ extern "C" void tnp_engine_destroy(tnp_engine* e) {
     buf_free(v->pz, s);
   }
   Buf* bufs[] = {&e->edges, &e->edges_alt, &e->blk, &e->blkoff, &e->scan_scr, &e->sa, &e->sb,
-                 &e->stage, &e->shared, &e->members, &e->cellcnt, &e->celloff,
+                 &e->stage, &e->shared, &e->members, &e->pcn, &e->pent, &e->rstart,
                  &e->ent_v, &e->ents, &e->pcell, &e->ptoff, &e->bcell,
                  &e->bstat, &e->ckeys_a, &e->ckeys_b, &e->sort_scr, &e->flags, &e->used, &e->nid,
                  &e->ctr, &e->tri, &e->faces, &e->lb[0], &e->lb[1], &e->edm, &e->esm,
@@ -372,7 +372,7 @@ extern "C" void tnp_engine_destroy(tnp_engine* e) {
   for (Buf& b : e->fscr) buf_free(b, s);
   for (Buf& b : e->fscr2) buf_free(b, s);
   for (Buf& b : e->cv) buf_free(b, s);
-  for (Buf* b : {&e->spcnt, &e->spoff, &e->part, &e->ekey_a, &e->ekey_b, &e->eval_b, &e->cellend,
+  for (Buf* b : {&e->spcnt, &e->spoff, &e->part, &e->ekey_a, &e->ekey_b, &e->eval_b,
                  &e->sort_scr2})
     buf_free(*b, s);
   (void)hipDeviceSynchronize();
@@ -864,24 +864,26 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
                          P<int32_t>(e->eval_b), T, cbits, e->sort_scr2.p, e->sort_scr2.bytes, &skey,
                          &sval, s));
   }
-  if (buf_ensure(e->celloff, ncell * sizeof(int64_t), s)) return -1;
-  if (buf_ensure(e->cellend, ncell * sizeof(int64_t), s)) return -1;
-  if (buf_ensure(e->cellcnt, ncell * sizeof(int32_t), s)) return -1;
-  if (buf_ensure(e->pcell, ncell * sizeof(int32_t), s)) return -1;
-  if (buf_ensure(e->ptoff, ncell * sizeof(int64_t), s)) return -1;
-  TNP_CHECK(hipMemsetAsync(e->celloff.p, 0, ncell * sizeof(int64_t), s));
-  TNP_CHECK(hipMemsetAsync(e->cellend.p, 0, ncell * sizeof(int64_t), s));
-  TIMED("cell_bounds", 12.0 * T,
-        launch_cell_bounds(skey, T, P<int64_t>(e->celloff), P<int64_t>(e->cellend), s));
-  // cells holding member pairs, compacted, with their flattened pair space
-  // offsets (total = tests); one pass, two look-back chains
+  // cells holding member pairs straight from the runs of the sorted keys
+  // (compacted, with their flattened pair space offsets; total = tests)
   {
-    TnpLB lr, lp;
-    const int64_t pt = pair_cell_tiles(ncell);
-    if (lb_begin(e, pt, s, &lr, 0) || lb_begin(e, pt, s, &lp, 1)) return -1;
-    TIMED("pair_cells", 28.0 * ncell,
-          launch_pair_cells(P<int64_t>(e->celloff), P<int64_t>(e->cellend), ncell, P<int32_t>(e->cellcnt),
-                            P<int32_t>(e->pcell), P<int64_t>(e->ptoff), ctr, lr, lp, s));
+    const int64_t RC = T1 / 2 + 1;  // a pair cell holds >= 2 entries
+    if (buf_ensure(e->pcell, RC * sizeof(int32_t), s)) return -1;
+    if (buf_ensure(e->pent, RC * sizeof(int32_t), s)) return -1;
+    if (buf_ensure(e->pcn, RC * sizeof(int32_t), s)) return -1;
+    if (buf_ensure(e->ptoff, RC * sizeof(int64_t), s)) return -1;
+    if (buf_ensure(e->rstart, (T1 + 1) * sizeof(int32_t), s)) return -1;
+    if (T > 0) {
+      TnpLB la, lr, lp;
+      if (lb_begin(e, split_tiles(T), s, &la, 0)) return -1;
+      TIMED("run_starts", 8.0 * T,
+            launch_run_starts(skey, T, P<int32_t>(e->rstart), ctr, la, s));
+      const int64_t pt = pair_run_tiles(T);
+      if (lb_begin(e, pt, s, &lr, 0) || lb_begin(e, pt, s, &lp, 1)) return -1;
+      TIMED("pair_cells", 0.0,
+            launch_pair_runs(skey, P<int32_t>(e->rstart), T, P<int32_t>(e->pcell), P<int32_t>(e->pent),
+                             P<int32_t>(e->pcn), P<int64_t>(e->ptoff), ctr, lr, lp, s));
+    }
   }
   if (buf_ensure(e->ents, T1 * sizeof(CellEnt), s)) return -1;
   TIMED("entry_keys", 52.0 * T,
@@ -905,7 +907,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     if (!chunks_ok) {
       if (buf_ensure(e->bcell, bcap * sizeof(int32_t), s)) return -1;
       if (attempt > 0) TNP_CHECK(hipMemsetAsync(ctr + CTR_BOVF, 0, sizeof(int64_t), s));
-      if (launch_chunk_cells(P<int64_t>(e->ptoff), P<int32_t>(e->pcell), P<int32_t>(e->cellcnt), ncell,
+      if (launch_chunk_cells(P<int64_t>(e->ptoff), P<int32_t>(e->pcn), T1 / 2 + 1,
                              P<int32_t>(e->bcell), bcap, ctr, s)) return -1;
     }
     if (buf_ensure(e->ckeys_a, std::max<int64_t>(cap, 1) * sizeof(uint64_t), s)) return -1;
@@ -915,8 +917,8 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
       TNP_CHECK(hipMemsetAsync(ctr + CTR_P, 0, 2 * sizeof(int64_t), s));  // CTR_P, CTR_COMPAT
     }
     TIMED("connect", 0.0,
-          launch_connect(P<int64_t>(e->ptoff), P<int32_t>(e->pcell), P<int32_t>(e->cellcnt),
-                         P<int64_t>(e->celloff), NC, e->max_pair_tests, P<int32_t>(e->bcell),
+          launch_connect(P<int64_t>(e->ptoff), P<int32_t>(e->pcell), P<int32_t>(e->pcn),
+                         P<int32_t>(e->pent), NC, e->max_pair_tests, P<int32_t>(e->bcell),
                          P<CellEnt>(e->ents), idx, nb, cfmask, P<uint64_t>(e->ckeys_a), cap, ctr,
                          P<int64_t>(e->bstat), s));
     if (read_ctr(e, s)) return -1;

@@ -31,7 +31,8 @@ enum {
   CTR_BOVF = 23,    // pair-chunk table overflow
   CTR_XK = 24,      // connecting edges surviving this step's pruning (appended)
   CTR_R = 25,       // cells with at least one member pair
-  CTR_N = 26
+  CTR_RUNS = 26,    // occupied cells (runs of equal keys in the sorted entries)
+  CTR_N = 27
 };
 
 int64_t step_tiles(int64_t n);
@@ -73,15 +74,22 @@ int launch_span_count(const int32_t* members, int64_t S, int64_t M, const uint64
 int launch_span_emit(const int32_t* members, int64_t S, int64_t M, const uint64_t* grid, int NC,
                      const int64_t* eoff, uint32_t* ekey, int32_t* eval, const int64_t* ctr,
                      hipStream_t s);
-int launch_cell_bounds(const uint32_t* key, int64_t T, int64_t* cstart, int64_t* cend, hipStream_t s);
-// cells with >= 2 members, compacted (single pass, two look-back chains:
-// rank and pair offset): pcell[r] = cell id, ptoff[r] = first pair index of
-// that cell in the flattened pair space; cellcnt[c] = members of every cell;
-// R -> ctr[CTR_R], pairs -> ctr[CTR_TESTS], a cell above 65535 -> CTR_BIG
-int launch_pair_cells(const int64_t* cstart, const int64_t* cend, int64_t ncell, int32_t* cellcnt,
-                      int32_t* pcell, int64_t* ptoff, int64_t* ctr, const TnpLB& lb_rank,
-                      const TnpLB& lb_pairs, hipStream_t s);
-int64_t pair_cell_tiles(int64_t ncell);
+// pair cells from the cell-sorted entry keys (runs of equal keys): the r-th
+// cell with >= 2 members (cell order) -> pcell[r] = cell id, pent[r] = its
+// first entry, pn[r] = its member count, ptoff[r] = its first pair in the
+// flattened pair space; R -> ctr[CTR_R], pairs -> ctr[CTR_TESTS], a cell
+// above 65535 members -> CTR_BIG.  Arrays sized >= T / 2 + 1.
+// Two passes: run starts (rstart[r] = first entry of the r-th occupied
+// cell, rstart[runs] = T, runs -> ctr[CTR_RUNS]; split_tiles(T) look-back
+// tiles, rstart sized >= T + 1), then the runs with >= 2 entries
+// (pair_run_tiles(T) look-back tiles for each of lb_rank / lb_pairs; the
+// run count is read on the device).
+int launch_run_starts(const uint32_t* key, int64_t T, int32_t* rstart, int64_t* ctr, const TnpLB& lb,
+                      hipStream_t s);
+int launch_pair_runs(const uint32_t* key, const int32_t* rstart, int64_t T, int32_t* pcell,
+                     int32_t* pent, int32_t* pn, int64_t* ptoff, int64_t* ctr, const TnpLB& lb_rank,
+                     const TnpLB& lb_pairs, hipStream_t s);
+int64_t pair_run_tiles(int64_t T);
 // one cell entry as the pair test reads it: the member's three packed keys
 // and id in one 32-byte record (one cache segment per entry)
 struct alignas(32) CellEnt {
@@ -102,10 +110,10 @@ int launch_entry_keys(const int32_t* ent_v, int64_t T, const uint64_t* grid, con
 // slots.
 int64_t connect_chunks(int64_t TT);
 int64_t connect_grid();
-int launch_chunk_cells(const int64_t* ptoff, const int32_t* pcell, const int32_t* cellcnt,
-                       int64_t rcap, int32_t* bcell, int64_t cap, int64_t* ctr, hipStream_t s);
-int launch_connect(const int64_t* ptoff, const int32_t* pcell, const int32_t* cellcnt,
-                   const int64_t* celloff, int NC, int64_t max_tests, const int32_t* bcell,
+int launch_chunk_cells(const int64_t* ptoff, const int32_t* pn, int64_t rcap, int32_t* bcell,
+                       int64_t cap, int64_t* ctr, hipStream_t s);
+int launch_connect(const int64_t* ptoff, const int32_t* pcell, const int32_t* pn,
+                   const int32_t* pent, int NC, int64_t max_tests, const int32_t* bcell,
                    const CellEnt* ent, int idx, int nb, uint64_t fmask, uint64_t* keys,
                    int64_t cap, int64_t* ctr, int64_t* bstat, hipStream_t s);
 // single-pass pruning over [edges; e_new; c_new] (lb_tiles(E + S + X)

@@ -319,52 +319,103 @@ __global__ void k_span_emit(const int32_t* __restrict__ members, int64_t S,
       }
 }
 
-// segment [start, end) of every cell in the cell-sorted entries
-__global__ void k_cell_bounds(const uint32_t* __restrict__ key, int64_t T,
-                              int64_t* __restrict__ cstart, int64_t* __restrict__ cend) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= T) return;
-  uint32_t k = key[i];
-  if (i == 0 || key[i - 1] != k) cstart[k] = i;
-  if (i == T - 1 || key[i + 1] != k) cend[k] = i + 1;
+// Pair cells straight from the cell-sorted entries (no dense cell grid):
+// a run of equal keys is one cell's member list.
+// (1) run starts, compacted in entry order (single pass, lane-interleaved
+//     items, decoupled look-back); the last tile closes the list with T.
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_run_starts_lb(const uint32_t* __restrict__ key, int64_t T, int64_t ntiles,
+                int32_t* __restrict__ rstart, int64_t* __restrict__ ctr, TnpLB lb) {
+  __shared__ int cnt[SIPT][TNP_WAVES];
+  __shared__ int64_t slot;
+  const int64_t tile = tnp::lb_tile(lb, &slot);
+  const int64_t base = tile * STILE;
+  uint32_t kc[SIPT], kp[SIPT];
+#pragma unroll
+  for (int k = 0; k < SIPT; ++k) {  // unconditional (clamped) loads, all in flight
+    const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
+    const int64_t ic = i < T ? i : T - 1;
+    kc[k] = key[ic];
+    kp[k] = key[ic > 0 ? ic - 1 : 0];
+  }
+  uint64_t bal[SIPT];
+#pragma unroll
+  for (int k = 0; k < SIPT; ++k) {
+    const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
+    bal[k] = __ballot(i < T && (i == 0 || kp[k] != kc[k]));
+    if (tnp::lane() == 0) cnt[k][tnp::wave()] = __popcll(bal[k]);
+  }
+  __syncthreads();
+  int64_t agg = 0;
+#pragma unroll
+  for (int k = 0; k < SIPT; ++k)
+#pragma unroll
+    for (int w = 0; w < TNP_WAVES; ++w) agg += cnt[k][w];
+  const int64_t prefix = tnp::lb_prefix(lb, tile, agg, &slot);
+  int64_t run = prefix;
+#pragma unroll
+  for (int k = 0; k < SIPT; ++k) {
+    int64_t off = run;
+    int tot = 0;
+#pragma unroll
+    for (int w = 0; w < TNP_WAVES; ++w) {
+      const int cc = cnt[k][w];
+      off += (w < tnp::wave()) ? cc : 0;
+      tot += cc;
+    }
+    if ((bal[k] >> tnp::lane()) & 1)
+      rstart[off + tnp::mbcnt(bal[k])] = (int32_t)(base + (int64_t)k * TNP_BLOCK + threadIdx.x);
+    run += tot;
+  }
+  if (tile == ntiles - 1 && threadIdx.x == 0) {
+    rstart[prefix + agg] = (int32_t)T;
+    ctr[CTR_RUNS] = prefix + agg;
+  }
 }
 
-// Pair cells: cells with >= 2 members, compacted in cell order (single pass
-// over thread-contiguous runs of PIPT cells, two decoupled look-back chains:
-// the compacted rank and the flattened pair offset).  Also the member count
-// of every cell; a cell above 65535 members flags CTR_BIG (one linear region
-// that large is the degenerate case the host refuses anyway).
+// (2) runs with >= 2 members, compacted in cell order with their flattened
+// pair offsets: thread-contiguous groups of PIPT runs, two decoupled
+// look-back chains (rank, pair offset).  Launched over an upper bound of
+// tiles; the blocks past the device-side run count leave at once.  A cell above 65535 members flags CTR_BIG
+// (one linear region that large is the degenerate case the host refuses).
 constexpr int PIPT = 16;
 constexpr int PTILE = TNP_BLOCK * PIPT;
 
 __global__ void __launch_bounds__(TNP_BLOCK)
-k_pair_cells_lb(const int64_t* __restrict__ cstart, const int64_t* __restrict__ cend, int64_t ncell,
-                int64_t ntiles, int32_t* __restrict__ cellcnt, int32_t* __restrict__ pcell,
-                int64_t* __restrict__ ptoff, int64_t* __restrict__ ctr, TnpLB lbr, TnpLB lbp) {
+k_pair_runs_lb(const uint32_t* __restrict__ key, const int32_t* __restrict__ rstart,
+               int32_t* __restrict__ pcell, int32_t* __restrict__ pent, int32_t* __restrict__ pn,
+               int64_t* __restrict__ ptoff, int64_t* __restrict__ ctr, TnpLB lbr, TnpLB lbp) {
   __shared__ int64_t lds[TNP_WAVES];
   __shared__ int64_t slot;
+  const int64_t R = ctr[CTR_RUNS];
+  const int64_t ntiles = (R + PTILE - 1) / PTILE;
+  // exactly ntiles blocks take a ticket (the ticket is one same-address
+  // atomic per block: the surplus blocks must not queue on it).  The host
+  // advanced its ticket base by gridDim.x, so the surplus is added in one
+  // step: by the last tile (every ticket is taken by then), or by block 0
+  // when there is no tile at all.
+  if ((int64_t)blockIdx.x >= ntiles) {
+    if (ntiles == 0 && blockIdx.x == 0 && threadIdx.x == 0)
+      atomicAdd(lbr.ticket, (unsigned long long)gridDim.x);
+    return;
+  }
   const int64_t tile = tnp::lb_tile(lbr, &slot);
+  if (tile == ntiles - 1 && threadIdx.x == 0 && (int64_t)gridDim.x > ntiles)
+    atomicAdd(lbr.ticket, (unsigned long long)(gridDim.x - ntiles));
   const int64_t base = tile * PTILE + (int64_t)threadIdx.x * PIPT;
+  int32_t st[PIPT + 1];
+#pragma unroll
+  for (int g = 0; g <= PIPT; ++g) st[g] = rstart[base + g <= R ? base + g : R];
   int32_t n[PIPT];
-  int64_t m[PIPT];
   int64_t nr = 0, np = 0;
   bool big = false;
 #pragma unroll
-  for (int k = 0; k < PIPT; ++k) {  // clamped, unconditional loads: all in flight
-    const int64_t c = base + k < ncell ? base + k : ncell - 1;
-    m[k] = cend[c] - cstart[c];
-  }
-#pragma unroll
-  for (int k = 0; k < PIPT; ++k) {
-    const int64_t c = base + k;
-    n[k] = 0;
-    if (c < ncell) {
-      big |= m[k] > 65535;
-      n[k] = m[k] > 65535 ? 0 : (int32_t)m[k];
-      cellcnt[c] = (int32_t)m[k];
-    }
-    nr += n[k] >= 2;
-    np += (int64_t)n[k] * (n[k] - 1) / 2;
+  for (int g = 0; g < PIPT; ++g) {
+    const int32_t m = base + g < R ? st[g + 1] - st[g] : 0;
+    big |= m > 65535;
+    n[g] = m > 65535 ? 0 : m;
+    nr += n[g] >= 2;
+    np += (int64_t)n[g] * (n[g] - 1) / 2;
   }
   if (__ballot(big) && tnp::lane() == 0) atomicOr((unsigned long long*)&ctr[CTR_BIG], 1ull);
   int64_t tr, tp;
@@ -374,12 +425,14 @@ k_pair_cells_lb(const int64_t* __restrict__ cstart, const int64_t* __restrict__ 
   const int64_t pp = tnp::lb_prefix(lbp, tile, tp, &slot);
   ep += pp;
 #pragma unroll
-  for (int k = 0; k < PIPT; ++k) {
-    if (n[k] >= 2) {
-      pcell[er] = (int32_t)(base + k);
+  for (int g = 0; g < PIPT; ++g) {
+    if (n[g] >= 2) {
+      pcell[er] = (int32_t)key[st[g]];
+      pent[er] = st[g];
+      pn[er] = n[g];
       ptoff[er] = ep;
       ++er;
-      ep += (int64_t)n[k] * (n[k] - 1) / 2;
+      ep += (int64_t)n[g] * (n[g] - 1) / 2;
     }
   }
   if (tile == ntiles - 1 && threadIdx.x == TNP_BLOCK - 1) {
@@ -476,12 +529,12 @@ __device__ __forceinline__ void cell_coords(int64_t cell, int NC, int cc[3]) {
 // so the appended order never reaches the output.
 // chunk b of the pair space starts in cell bcell[b] (written per cell: no
 // host round trip for the pair count)
-__global__ void k_chunk_cells(const int64_t* __restrict__ ptoff, const int32_t* __restrict__ pcell,
-                              const int32_t* __restrict__ cellcnt, int64_t rcap,
+__global__ void k_chunk_cells(const int64_t* __restrict__ ptoff, const int32_t* __restrict__ pn,
+                              int64_t rcap,
                               int32_t* __restrict__ bcell, int64_t cap, int64_t* __restrict__ ctr) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= rcap || r >= ctr[CTR_R]) return;
-  const int64_t m = cellcnt[pcell[r]];
+  const int64_t m = pn[r];
   const int64_t n = m * (m - 1) / 2;
   const int64_t lo = ptoff[r];
   int64_t b0 = (lo + CCH - 1) / CCH, b1 = (lo + n + CCH - 1) / CCH;
@@ -510,7 +563,7 @@ __device__ __forceinline__ void pair_row(int q, int& i, int& j) {
 // first entry) sit in LDS, so locating a pair is an LDS walk.
 __global__ void __launch_bounds__(TNP_BLOCK)
 k_connect(const int64_t* __restrict__ ptoff, const int32_t* __restrict__ pcell,
-          const int32_t* __restrict__ cellcnt, const int64_t* __restrict__ celloff, int NC,
+          const int32_t* __restrict__ pn, const int32_t* __restrict__ pent, int NC,
           int64_t max_tests, const int32_t* __restrict__ bcell, const CellEnt* __restrict__ ent,
           int idx, int nb, uint64_t fmask, uint64_t* __restrict__ keys, int64_t cap,
           int64_t* __restrict__ ctr, int64_t* __restrict__ bstat) {
@@ -535,8 +588,8 @@ k_connect(const int64_t* __restrict__ ptoff, const int32_t* __restrict__ pcell,
   for (int t = threadIdx.x; t < nr; t += blockDim.x) {
     const int c = pcell[r0 + t];
     s_off[t] = (int32_t)(ptoff[r0 + t] - pb);  // > -2^31: a cell holds < 2^31 pairs
-    s_n[t] = cellcnt[c];
-    s_ent[t] = (int32_t)celloff[c];
+    s_n[t] = pn[r0 + t];
+    s_ent[t] = pent[r0 + t];
     const int cz = c % NC, cy = (c / NC) % NC, cx = c / (NC * NC);  // = cell_coords + 2
     s_cc[t] = cx | (cy << 10) | (cz << 20);
   }
@@ -1000,19 +1053,22 @@ int launch_span_emit(const int32_t* members, int64_t S, int64_t M, const uint64_
   TNP_CHECK(hipGetLastError());
   return 0;
 }
-int launch_cell_bounds(const uint32_t* key, int64_t T, int64_t* cstart, int64_t* cend, hipStream_t s) {
+int64_t pair_run_tiles(int64_t T) { return (T + PTILE - 1) / PTILE; }
+int launch_run_starts(const uint32_t* key, int64_t T, int32_t* rstart, int64_t* ctr, const TnpLB& lb,
+                      hipStream_t s) {
   if (T <= 0) return 0;
-  hipLaunchKernelGGL(k_cell_bounds, dim3(tnp_grid(T)), dim3(TNP_BLOCK), 0, s, key, T, cstart, cend);
+  const int64_t tiles = split_tiles(T);
+  hipLaunchKernelGGL(k_run_starts_lb, dim3((unsigned)tiles), dim3(TNP_BLOCK), 0, s, key, T, tiles,
+                     rstart, ctr, lb);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
-int64_t pair_cell_tiles(int64_t ncell) { return (ncell + PTILE - 1) / PTILE; }
-int launch_pair_cells(const int64_t* cstart, const int64_t* cend, int64_t ncell, int32_t* cellcnt,
-                      int32_t* pcell, int64_t* ptoff, int64_t* ctr, const TnpLB& lb_rank,
-                      const TnpLB& lb_pairs, hipStream_t s) {
-  const int64_t tiles = pair_cell_tiles(ncell);
-  hipLaunchKernelGGL(k_pair_cells_lb, dim3((unsigned)tiles), dim3(TNP_BLOCK), 0, s, cstart, cend, ncell,
-                     tiles, cellcnt, pcell, ptoff, ctr, lb_rank, lb_pairs);
+int launch_pair_runs(const uint32_t* key, const int32_t* rstart, int64_t T, int32_t* pcell,
+                     int32_t* pent, int32_t* pn, int64_t* ptoff, int64_t* ctr, const TnpLB& lb_rank,
+                     const TnpLB& lb_pairs, hipStream_t s) {
+  if (T <= 0) return 0;
+  hipLaunchKernelGGL(k_pair_runs_lb, dim3((unsigned)pair_run_tiles(T)), dim3(TNP_BLOCK), 0, s, key,
+                     rstart, pcell, pent, pn, ptoff, ctr, lb_rank, lb_pairs);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
@@ -1026,20 +1082,20 @@ int launch_entry_keys(const int32_t* ent_v, int64_t T, const uint64_t* grid, con
 }
 constexpr int CONNECT_GRID = 2048;  // persistent blocks (8 per CU)
 int64_t connect_chunks(int64_t TT) { return (TT + CCH - 1) / CCH; }
-int launch_chunk_cells(const int64_t* ptoff, const int32_t* pcell, const int32_t* cellcnt,
-                       int64_t rcap, int32_t* bcell, int64_t cap, int64_t* ctr, hipStream_t s) {
-  hipLaunchKernelGGL(k_chunk_cells, dim3(tnp_grid(rcap)), dim3(TNP_BLOCK), 0, s, ptoff, pcell, cellcnt,
-                     rcap, bcell, cap, ctr);
+int launch_chunk_cells(const int64_t* ptoff, const int32_t* pn, int64_t rcap, int32_t* bcell,
+                       int64_t cap, int64_t* ctr, hipStream_t s) {
+  hipLaunchKernelGGL(k_chunk_cells, dim3(tnp_grid(rcap)), dim3(TNP_BLOCK), 0, s, ptoff, pn, rcap,
+                     bcell, cap, ctr);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
-int launch_connect(const int64_t* ptoff, const int32_t* pcell, const int32_t* cellcnt,
-                   const int64_t* celloff, int NC, int64_t max_tests, const int32_t* bcell,
+int launch_connect(const int64_t* ptoff, const int32_t* pcell, const int32_t* pn,
+                   const int32_t* pent, int NC, int64_t max_tests, const int32_t* bcell,
                    const CellEnt* ent, int idx, int nb, uint64_t fmask, uint64_t* keys,
                    int64_t cap, int64_t* ctr, int64_t* bstat, hipStream_t s) {
   static_assert(CONNECT_CELLS >= CCH + 2, "chunk cell window");
-  hipLaunchKernelGGL(k_connect, dim3(CONNECT_GRID), dim3(TNP_BLOCK), 0, s, ptoff, pcell, cellcnt,
-                     celloff, NC, max_tests, bcell, ent, idx, nb, fmask, keys, cap, ctr, bstat);
+  hipLaunchKernelGGL(k_connect, dim3(CONNECT_GRID), dim3(TNP_BLOCK), 0, s, ptoff, pcell, pn,
+                     pent, NC, max_tests, bcell, ent, idx, nb, fmask, keys, cap, ctr, bstat);
   hipLaunchKernelGGL(k_sum_bstat, dim3(1), dim3(TNP_BLOCK), 0, s, bstat, (int64_t)CONNECT_GRID, ctr);
   TNP_CHECK(hipGetLastError());
   return 0;
