@@ -836,6 +836,17 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
         launch_span_count(P<int32_t>(e->members), S, M, grid, zero, idx, P<int32_t>(e->spcnt),
                           P<int64_t>(e->part), ctr, s));
   if (scan_counts(e, P<int32_t>(e->spcnt), P<int64_t>(e->spoff), M, CTR_T, s)) return -1;
+  // a member spans <= 8 cells (2 per axis when on a mark plane): the entry
+  // buffers take the bound 8 M, so the emit is queued ahead of the readback
+  // of T and runs while the host waits for it
+  const int64_t TB = std::max<int64_t>(8 * M, 1);
+  if (buf_ensure(e->ekey_a, TB * sizeof(uint32_t), s)) return -1;
+  if (buf_ensure(e->ekey_b, TB * sizeof(uint32_t), s)) return -1;
+  if (buf_ensure(e->ent_v, TB * sizeof(int32_t), s)) return -1;
+  if (buf_ensure(e->eval_b, TB * sizeof(int32_t), s)) return -1;
+  TIMED("span_emit", 28.0 * M,
+        launch_span_emit(P<int32_t>(e->members), S, M, grid, NC, P<int64_t>(e->spoff),
+                         P<uint32_t>(e->ekey_a), P<int32_t>(e->ent_v), ctr, s));
   if (read_ctr(e, s)) return -1;
   if (e->h_ctr[CTR_K0]) {
     // the reference builds torch.cartesian_prod() of zero tensors (subpoly.py:317)
@@ -845,13 +856,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   const int64_t H = e->h_ctr[CTR_H];
   const int64_t T = e->h_ctr[CTR_T];
   const int64_t T1 = std::max<int64_t>(T, 1);
-  if (buf_ensure(e->ekey_a, T1 * sizeof(uint32_t), s)) return -1;
-  if (buf_ensure(e->ekey_b, T1 * sizeof(uint32_t), s)) return -1;
-  if (buf_ensure(e->ent_v, T1 * sizeof(int32_t), s)) return -1;
-  if (buf_ensure(e->eval_b, T1 * sizeof(int32_t), s)) return -1;
-  TIMED("span_emit", 20.0 * M + 8.0 * T,
-        launch_span_emit(P<int32_t>(e->members), S, M, grid, NC, P<int64_t>(e->spoff),
-                         P<uint32_t>(e->ekey_a), P<int32_t>(e->ent_v), ctr, s));
+  ktimer_set_bytes(e, 20.0 * M + 8.0 * T);  // span_emit's bytes, known only now
   int cbits = 1;
   while (cbits < 32 && (1ll << cbits) < ncell) ++cbits;
   uint32_t* skey = nullptr;

@@ -509,9 +509,17 @@ __device__ __forceinline__ int64_t upper_bound_i64(const int64_t* __restrict__ a
   return lo;
 }
 
-constexpr int CIPT = 8;                 // consecutive pair indices per thread
+#ifndef TNP_CONNECT_CIPT
+#define TNP_CONNECT_CIPT 8
+#endif
+constexpr int CIPT = TNP_CONNECT_CIPT;  // consecutive pair indices per thread
 constexpr int CONNECT_CELLS = TNP_BLOCK * CIPT + 2;  // >= pair cells a chunk can touch
 constexpr int CCH = TNP_BLOCK * CIPT;   // pair indices per block
+#ifndef TNP_CONNECT_CB
+#define TNP_CONNECT_CB 1
+#endif
+constexpr int CONNECT_CB = TNP_CONNECT_CB;  // pairs whose record loads are in flight together
+static_assert(CONNECT_CB == 0 || CIPT % CONNECT_CB == 0, "connect batches");
 
 __device__ __forceinline__ void cell_coords(int64_t cell, int NC, int cc[3]) {
   cc[2] = (int)(cell % NC) - 2;
@@ -608,6 +616,7 @@ k_connect(const int64_t* __restrict__ ptoff, const int32_t* __restrict__ pcell,
     }
     lc = lo > 0 ? lo - 1 : 0;
   }
+#if TNP_CONNECT_CB == 0
 #pragma unroll
   for (int k = 0; k < CIPT; ++k) {
     const int64_t p = pw + 64 * k;
@@ -635,6 +644,61 @@ k_connect(const int64_t* __restrict__ ptoff, const int32_t* __restrict__ pcell,
       }
     }
   }
+#else
+  // CB pairs at a time: locate them (LDS only), issue all 4·CB record loads
+  // (unconditional: an out-of-range pair reads entry 0 of its cell), then
+  // test -- CB loads in flight per lane instead of one dependent pair
+#pragma unroll
+  for (int k0 = 0; k0 < CIPT; k0 += CONNECT_CB) {
+    int iu[CONNECT_CB], iv[CONNECT_CB], pcs[CONNECT_CB];
+    bool ok[CONNECT_CB];
+#pragma unroll
+    for (int kb = 0; kb < CONNECT_CB; ++kb) {
+      const int64_t p = pw + 64 * (k0 + kb);
+      ok[kb] = p < TT;
+      int i = 0, j = 0;
+      if (ok[kb]) {
+        const int x = (int)(p - pb);
+        while (lc + 1 < nr && s_off[lc + 1] <= x) ++lc;
+        pair_row(x - s_off[lc], i, j);
+      }
+      const int base = s_ent[lc];
+      iu[kb] = base + i;
+      iv[kb] = base + j;
+      pcs[kb] = s_cc[lc];
+    }
+    ulonglong2 ua[CONNECT_CB], va[CONNECT_CB];
+    uint64_t zua[CONNECT_CB], zva[CONNECT_CB];
+    const ulonglong2* er = reinterpret_cast<const ulonglong2*>(ent);
+#pragma unroll
+    for (int kb = 0; kb < CONNECT_CB; ++kb) {
+      ua[kb] = er[2 * (int64_t)iu[kb]];  // (g, p)
+      zua[kb] = ent[iu[kb]].z;
+      va[kb] = er[2 * (int64_t)iv[kb]];
+      zva[kb] = ent[iv[kb]].z;
+    }
+#pragma unroll
+    for (int kb = 0; kb < CONNECT_CB; ++kb) {
+      if (!ok[kb]) continue;
+      const int pc = pcs[kb];
+      const int cc[3] = {(pc & 1023) - 2, ((pc >> 10) & 1023) - 2, ((pc >> 20) & 1023) - 2};
+      const uint64_t gu = ua[kb].x, pu = ua[kb].y, zu = zua[kb];
+      const uint64_t gv = va[kb].x, pv = va[kb].y, zv = zva[kb];
+      PairTest t = pair_test(cc, below, gu, pu, zu, gv, pv, zv);
+      if (t.compat) {
+        n_compat++;
+        n_reg += t.regions;
+        n_conn += t.emit;
+        // the step's pruning drops it anyway (keep_edge): never appended
+        if (t.emit && (fmask == 0 || (((pu ^ pv) | (zu ^ zv)) & fmask) != 0)) {
+          const uint32_t vu = (uint32_t)ent[iu[kb]].v, vv = (uint32_t)ent[iv[kb]].v;
+          const uint32_t lo = vu < vv ? vu : vv, hi = vu < vv ? vv : vu;
+          kk[ne++] = ((uint64_t)lo << nb) | hi;
+        }
+      }
+    }
+  }
+#endif
   int64_t tot;
   int64_t off = tnp::block_scan_excl((int64_t)ne, lds, tot);
   if (threadIdx.x == 0) s_base = tot ? (int64_t)atomicAdd((unsigned long long*)&ctr[CTR_XK], (unsigned long long)tot) : 0;
@@ -1080,7 +1144,22 @@ int launch_entry_keys(const int32_t* ent_v, int64_t T, const uint64_t* grid, con
   TNP_CHECK(hipGetLastError());
   return 0;
 }
-constexpr int CONNECT_GRID = 2048;  // persistent blocks (8 per CU)
+// persistent blocks: exactly the resident ones (occupancy x CUs), so the
+// static chunk stride never leaves a second, late wave of blocks as a tail
+static int connect_grid_size() {
+  static int g = 0;
+  if (!g) {
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_connect, TNP_BLOCK, 0) != hipSuccess ||
+        cus <= 0 || per_cu <= 0)
+      g = 2048;
+    else
+      g = cus * per_cu;
+  }
+  return g;
+}
 int64_t connect_chunks(int64_t TT) { return (TT + CCH - 1) / CCH; }
 int launch_chunk_cells(const int64_t* ptoff, const int32_t* pn, int64_t rcap, int32_t* bcell,
                        int64_t cap, int64_t* ctr, hipStream_t s) {
@@ -1094,13 +1173,14 @@ int launch_connect(const int64_t* ptoff, const int32_t* pcell, const int32_t* pn
                    const CellEnt* ent, int idx, int nb, uint64_t fmask, uint64_t* keys,
                    int64_t cap, int64_t* ctr, int64_t* bstat, hipStream_t s) {
   static_assert(CONNECT_CELLS >= CCH + 2, "chunk cell window");
-  hipLaunchKernelGGL(k_connect, dim3(CONNECT_GRID), dim3(TNP_BLOCK), 0, s, ptoff, pcell, pn,
+  const int grid = connect_grid_size();
+  hipLaunchKernelGGL(k_connect, dim3(grid), dim3(TNP_BLOCK), 0, s, ptoff, pcell, pn,
                      pent, NC, max_tests, bcell, ent, idx, nb, fmask, keys, cap, ctr, bstat);
-  hipLaunchKernelGGL(k_sum_bstat, dim3(1), dim3(TNP_BLOCK), 0, s, bstat, (int64_t)CONNECT_GRID, ctr);
+  hipLaunchKernelGGL(k_sum_bstat, dim3(1), dim3(TNP_BLOCK), 0, s, bstat, (int64_t)grid, ctr);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
-int64_t connect_grid() { return CONNECT_GRID; }
+int64_t connect_grid() { return connect_grid_size(); }
 uint64_t prune_mask(int idx, int last_plane) {
   uint64_t fmask = (idx >= 64) ? 0ull : (~0ull << idx);
   if (last_plane < 63) fmask &= (1ull << (last_plane + 1)) - 1ull;

@@ -12,7 +12,10 @@ import os
 
 import torch  # noqa: F401  (must load before the HIP library)
 
-_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libtropical_hip.so")
+# TNP_LIB names an alternative build of the same library (A/B kernel variants
+# built in-tree under _lib/); the default is the Makefile's output
+_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib",
+                         os.environ.get("TNP_LIB", "libtropical_hip.so"))
 MAX_LEVELS = 8
 
 
