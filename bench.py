@@ -12,13 +12,14 @@ Net(num_layers=3, num_hidden=16, levels=2, r_min=G-1, r_max=G-1, T=19)
 (G marks per axis; hash table U(-0.1,0.1), nn.Linear-bound MLP, numpy PCG64
 seed 6 by default, see --seed), initial edges = the full G^3 lattice.  G = 128 at one GPU; at N GPUs
 the lattice grows to round(128 * N^(1/3)) marks per axis and is cut into N
-x-slabs of cells, each extracted with a one-cell halo (weak scaling, one
+x-slabs of cells, each extracted with a two-cell halo (weak scaling, one
 process per GPU, RCCL only for the per-step 8-byte agreements; the slabs
 are stitched into one complex after the timed region,
 tropical/distributed.py).  value = edges subdivided by all ranks (each
 split counted once, by the rank owning it) / max-over-ranks wall time.
 
-Run: python bench.py [--gpus N --steps K --warmup W]  (torchrun for N > 1)
+Run: python bench.py [--gpus N --steps K --warmup W]  (N > 1: one process per GPU,
+relaunched under torch.distributed.run unless already launched by it)
 """
 import argparse
 import json
@@ -71,6 +72,18 @@ def make_net(G, device, seed=0):
     return net.to(device)
 
 
+def reference_fingerprint(G: int, seed: int):
+    """(V, E, vertex-set hash, edge-set hash) of the reference's final
+    complex on this workload, when a golden holds it (bench128: the
+    reference run on the 128^3 seed-6 lattice in the build container)."""
+    from golden_io import GOLDEN
+    path = os.path.join(GOLDEN, "bench128.npz")
+    if G != 128 or seed != 6 or not os.path.isfile(path):
+        return None
+    with np.load(path, allow_pickle=False) as z:
+        return tuple(int(x) for x in z["pre_VE"]) + tuple(int(x) for x in z["complex_hash"])
+
+
 def algorithmic_bytes(st: dict, K: int) -> int:
     """SURVEY §8d per-step traffic model B_s (bytes the step must move)."""
     E_in, S, V_in = st["E_in"], st["S"], st["V_in"]
@@ -84,25 +97,26 @@ def algorithmic_bytes(st: dict, K: int) -> int:
 
 class Collective:
     """Per-step agreements between slab ranks (the reference's global
-    decisions, subpoly.py:110 and subpoly_debug.py:43-49)."""
+    decisions, subpoly.py:110 and subpoly_debug.py:43-49): ONE all_gather of
+    each rank's few int64 words (RCCL over xGMI, or gloo on the host), reduced
+    on the host -- OR for the 64-bit plane masks (RCCL has no bitwise-or
+    reduction), MAX for {split count, failover flag}; one readback."""
 
     def __init__(self, device):
         import torch.distributed as dist
         self.dist = dist
         self.device = device
+        self.world = dist.get_world_size()
 
     def __call__(self, vec: np.ndarray, op: str):
+        words = np.ascontiguousarray(vec.astype(np.uint64 if op == "or" else np.int64)).view(np.int64)
+        t = torch.from_numpy(words.copy()).to(self.device)
+        out = torch.empty(self.world * t.numel(), dtype=torch.int64, device=self.device)
+        self.dist.all_gather_into_tensor(out, t)
+        a = out.cpu().numpy().reshape(self.world, -1)
         if op == "or":
-            # OR of 64-bit plane masks as ONE all_reduce(MAX) over their bits
-            # (RCCL has no bitwise-or reduction)
-            bits = np.unpackbits(vec.astype(np.uint64).view(np.uint8), bitorder="little")
-            t = torch.tensor(bits, dtype=torch.int32, device=self.device)
-            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
-            out = np.packbits(t.cpu().numpy().astype(np.uint8), bitorder="little")
-            return out.view(np.uint64).astype(vec.dtype)
-        t = torch.tensor(vec.astype(np.int64).view(np.int64), device=self.device)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
-        return t.cpu().numpy()
+            return np.bitwise_or.reduce(a.view(np.uint64), axis=0).astype(vec.dtype)
+        return a.max(axis=0)
 
 
 def cpu_baseline(sample_marks: int, seed: int, threads: int):
@@ -202,6 +216,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU: relaunch under torch.distributed.run as a CHILD
+        # process (nothing here has touched the GPU yet) and exit with its code
+        import socket
+        import subprocess
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+               f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+               f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+        raise SystemExit(subprocess.call(cmd))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     # one rank per GPU; TNP_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs
@@ -225,7 +251,7 @@ def main():
     net = make_net(G, dev, args.seed)
     from tropical.distributed import slab_cuts, slab_marks
     cuts = slab_cuts(G, world)
-    x0, x1 = slab_marks(cuts, rank)  # this rank's cells + a one-cell halo
+    x0, x1 = slab_marks(cuts, rank)  # this rank's cells + a HALO-cell halo each side
     eng = engine_for(net)
     if world > 1:
         eng.set_owned(cuts[rank], cuts[rank + 1])  # halo splits -> S_dup
@@ -266,11 +292,22 @@ def main():
         hv, he = complex_hash(Vf, Ef)
         stitched = {"vertices": int(Vf.shape[0]), "edges": int(Ef.shape[0]),
                     "vertex_set_hash": hv, "edge_set_hash": he}
+        ref = reference_fingerprint(G, args.seed)
+        if ref is not None:
+            # parity of the measured workload: the reference itself, run on the
+            # same net and lattice (tests/golden/make_golden.py bench128)
+            got = (stitched["vertices"], stitched["edges"], hv, he)
+            if got != ref:
+                raise SystemExit(f"final complex {got} differs from the reference's {ref}")
+            stitched["matches_reference"] = True
     else:
-        # the complete sharded output: each slab exported and stitched into one
-        # global complex (tropical/distributed.py; RCCL all_gathers), untimed
-        from tropical.distributed import stitch
+        # the complete sharded output: each slab exported, the neighbours'
+        # views next to every cut compared (fails loudly if a halo was too
+        # narrow), stitched into one global complex (tropical/distributed.py;
+        # RCCL all_gathers), untimed
+        from tropical.distributed import halo_check, stitch
         Vl, El, _ = eng.export()
+        halo_check(Vl.to(comm_dev), El.to(comm_dev), net.enc.marks, cuts)
         owned, first, gE, own, keep = stitch(Vl.to(comm_dev), El.to(comm_dev), net.enc.marks, cuts,
                                              masks=True)
         hv, he = complex_hash(Vl.to(comm_dev), El.to(comm_dev), own, keep)

@@ -148,6 +148,12 @@ int tnp_engine_finish(tnp_engine* eng, int idx, int prune, int override,
 
 int tnp_engine_sizes(tnp_engine* eng, int64_t* V, int64_t* E);
 
+/* Curve path: after tnp_engine_finish, the strict filter's keep flags
+ * (int32 0/1) of the step's n candidate splits in edge order -- the mask
+ * debug.strict_check returns (subpoly_debug.py:234-271) that the reference's
+ * masked_scatter_ rewrites the caller's edges with (subpoly.py:209-212). */
+int tnp_engine_split_keep(tnp_engine* eng, int32_t* d_keep, int64_t n, void* stream);
+
 /* Copy the complex out: d_xyz V x 3, d_edges E x 2 int64, d_pre V x K
  * row-major (requires keep_all_planes, else may be null). */
 int tnp_engine_export(tnp_engine* eng, float* d_xyz, int64_t* d_edges,
@@ -175,7 +181,8 @@ int tnp_engine_faces_export(tnp_engine* eng, int64_t* d_tri, float* d_faces,
  * Single-device only (the descent's stop criterion is global). */
 int tnp_engine_set_curve(tnp_engine* eng, int on);
 
-/* Multi-GPU x-slabs with a one-cell halo: this shard OWNS the mark planes
+/* Multi-GPU x-slabs with a halo of HALO (= 2) cells each side (tropical/
+ * distributed.py): this shard OWNS the mark planes
  * (lo, hi] (lo == 0: [0, hi]) and the cells between them; new vertices
  * outside (halo work, also computed by the neighbour that owns them) are
  * counted in tnp_step_stats.S_dup so the global split count counts each

@@ -49,12 +49,12 @@ def sha(*arrays) -> str:
     return h.hexdigest()
 
 
-def fit_sdf(cfg, fn, seed, iters=1000, batch=4096):
+def fit_sdf(cfg, fn, seed, iters=1000, batch=4096, lr=1e-2):
     """Fit the oracle net to an analytic SDF on CPU (stand-in pretrained net)."""
     from oracle.subdivide import RefNet, load_params
     net = RefNet(**cfg)
     load_params(net, syn.random_params(net.enc.module.params.numel(), net.num_nodes, seed, 1e-4))
-    opt = torch.optim.Adam(net.parameters(), lr=1e-2)
+    opt = torch.optim.Adam(net.parameters(), lr=lr)
     sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, iters)
     g = torch.Generator().manual_seed(seed)
     for it in range(iters):
@@ -78,7 +78,8 @@ def torus(x):
 
 
 CASES = {
-    # name: (kind, cfg, weights, extra)
+    # name: (kind, cfg, weights, extra); lattice extra = marks per axis or
+    # (marks, T): T < 19 hashes the lattice's levels (res = marks - 1)
     "synth24": ("lattice", None, ("rand", 1, 0.1), 24),
     "synth32": ("lattice", None, ("rand", 2, 0.1), 32),
     "synth32u": ("lattice", None, ("rand_uncentered", 0, 0.1), 32),
@@ -89,7 +90,21 @@ CASES = {
     "small_sphere_curve": ("curve", SMALL, ("same", "small_sphere"), None),
     "small_torus_curve": ("curve", SMALL, ("same", "small_torus"), None),
     "small_rand_curve": ("curve", SMALL, ("same", "small_rand"), None),
+    # hashed levels (31^3 > 2^14, 63^3 > 2^17): the prime-XOR branch of the
+    # encoding and the tied-table layout under hashing
+    "synth32h": ("lattice", None, ("rand", 3, 0.1), (32, 14)),
+    "synth64h": ("lattice", None, ("rand", 4, 0.1), (64, 17)),
+    # BASELINE config 3 net class: 201 marks, level 3 hashed (128^3 > 2^19),
+    # 2x2x2 skeleton tiles with the 127-stride overlap; weights fitted to a
+    # sphere and stored as fp16 (exactly representable in fp32)
+    "large_sphere": ("subpoly", LARGE, ("fit16", sphere, 13), None),
+    # the bench headline workload (bench.py: 128^3 lattice, seed 6, amp 0.1,
+    # uncentred): per-step hashes + order-free final fingerprints
+    "bench128": ("lattice", None, ("rand_uncentered", 6, 0.1), (128, 19)),
 }
+# table params above this many floats are stored as the generator spec
+# (tropical/synthetic.py random_params) instead of the values
+GEN_MAX = 200_000
 
 
 def _surface_check(*args, **kwargs):
@@ -113,30 +128,49 @@ def build_params(cfg, spec, net):
             with torch.no_grad():
                 return net(torch.from_numpy(x), gather=True)[1][-1][:, 0].numpy()
         return syn.center_sdf_bias(p, col, spec[1])
+    if spec[0] == "fit16":
+        p = fit_sdf(cfg, spec[1], spec[2])
+        return {k: v.astype(np.float16) for k, v in p.items()}
     return fit_sdf(cfg, spec[1], spec[2])
 
 
 def run_case(name):
     sp, model = __import__("ref_loader").import_reference()
     kind, cfg, wspec, n = CASES[name]
+    T = 19
     if kind == "lattice":
-        cfg = syn.net_config_for_lattice(n)
+        n, T = (n, 19) if isinstance(n, int) else n
+        cfg = syn.net_config_for_lattice(n, T)
     net = model.Net(**cfg)
     params = build_params(cfg, wspec, net)
-    net.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()})
+    net.load_state_dict({k: torch.from_numpy(v.astype(np.float32)) for k, v in params.items()})
     out = {"case": name, "kind": kind, "cfg_keys": np.array(list(cfg.keys())),
            "cfg_vals": np.array(list(cfg.values()), dtype=np.int64),
            "marks": net.enc.marks.numpy()}
-    for k, v in params.items():
-        out["p:" + k] = v
+    n_table = params["enc.module.params"].size
+    if wspec[0] in ("rand", "rand_uncentered") and n_table > GEN_MAX:
+        # regenerated by tests/golden_io.py (synthetic.random_params); the
+        # centred output bias is stored as a value
+        out["gen"] = np.array([wspec[1], wspec[2], n_table], dtype=np.float64)
+        if wspec[0] == "rand":
+            out["p:fc.2.bias"] = params["fc.2.bias"]
+    else:
+        for k, v in params.items():
+            out["p:" + k] = v
 
     steps = []
     orig = sp.subpoly_
+    memo = {}
 
     def wrapped(vertices, edges, net_, l, h, eps, outputs_=None, **kw):
         v, e, o = orig(vertices, edges, net_, l, h, eps, outputs_, **kw)
-        steps.append((l * net_.num_hidden + h, v.shape[0], e.shape[0],
-                      sha(v.numpy(), e.numpy().astype(np.int64), o.numpy())))
+        key = (id(v), id(e), id(o), v.data_ptr(), e.data_ptr(), o.data_ptr())
+        if key != memo.get("key"):  # an S == 0 step returns its inputs unchanged
+            memo["key"] = key
+            memo["sha"] = sha(v.numpy(), e.numpy().astype(np.int64), o.numpy())
+        steps.append((l * net_.num_hidden + h, v.shape[0], e.shape[0], memo["sha"]))
+        print(f"  step {steps[-1][0]}: V={v.shape[0]} E={e.shape[0]} ({time.time() - t0:.0f}s)",
+              flush=True)
         return v, e, o
 
     sp.subpoly_ = wrapped
@@ -157,6 +191,15 @@ def run_case(name):
             V, E, o = sp.subpoly_(V, E, net, net.num_layers - 2, net.num_hidden, 1e-4, o,
                                   force=True)
             out["pre_VE"] = np.array([V.shape[0], E.shape[0]])
+            # the product's fingerprint, loaded by path (``tropical`` here is
+            # the reference package)
+            dspec = importlib.util.spec_from_file_location(
+                "_distributed", os.path.join(REPO, "tropical-nerf.pytorch_amd", "tropical",
+                                             "distributed.py"))
+            dmod = importlib.util.module_from_spec(dspec)
+            dspec.loader.exec_module(dmod)
+            complex_hash = dmod.complex_hash
+            out["complex_hash"] = np.array(complex_hash(V, E), dtype=np.int64)
             Vs, Es, used = sp.extract_skeleton(V, E, net, 1e-4, o)
             out["surf_V"] = Vs.numpy()
             out["surf_E"] = Es.numpy()
@@ -168,6 +211,8 @@ def run_case(name):
                     break
             out["skel_V"] = V0.numpy()
             out["skel_E"] = E0.numpy()
+            # duplicate edges from the 127-stride tile overlap (tropical.py:176-181)
+            out["skel_dups"] = np.int64(E0.shape[0] - np.unique(E0.numpy(), axis=0).shape[0])
             if not force:
                 last = {}
                 orig_ex = sp.extract_skeleton
@@ -208,7 +253,36 @@ def run_case(name):
           f"steps={len(steps)} {out['ref_seconds']:.1f}s -> {os.path.getsize(path)/1e3:.0f} kB")
 
 
+def annotate_skeleton(name):
+    """Add ``skel_dups`` to an existing skeleton golden: re-run the
+    reference's skeleton on the stored weights, check it against the stored
+    hash, count duplicate edges."""
+    sp, model = __import__("ref_loader").import_reference()
+    sys.path.insert(0, os.path.dirname(HERE))
+    from golden_io import load
+    d = load(name)
+    net = model.Net(**d["cfg"])
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in d["params"].items()})
+    for m in net.modules():
+        if isinstance(m, sys.modules["tropical"].TropicalHashGrid):
+            V0, E0 = m.skeleton(net)
+            break
+    if "sha_skel" in d:
+        assert sha(V0.numpy(), E0.numpy().astype(np.int64)) == str(d["sha_skel"])
+    path = os.path.join(HERE, f"{name}.npz")
+    with np.load(path, allow_pickle=False) as z:
+        out = {k: z[k] for k in z.files}
+    out["skel_dups"] = np.int64(E0.shape[0] - np.unique(E0.numpy(), axis=0).shape[0])
+    out["skel_VE"] = np.array([V0.shape[0], E0.shape[0]])
+    np.savez_compressed(path, **out)
+    print(f"{name}: skeleton {tuple(out['skel_VE'])}, {out['skel_dups']} duplicate edges")
+
+
 if __name__ == "__main__":
+    if sys.argv[1:2] == ["--annotate"]:
+        for nm in sys.argv[2:]:
+            annotate_skeleton(nm)
+        sys.exit(0)
     if os.environ.get("GOLDEN_TRACE"):
         import faulthandler
         faulthandler.dump_traceback_later(int(os.environ["GOLDEN_TRACE"]), exit=True)

@@ -29,6 +29,9 @@ def engine_steps(eng, record=True):
         S, fail = eng.split(idx)
         if S > 0:
             eng.finish(idx, idx < K - 1, fail)
+        elif out:  # nothing split: the state (and its hash) is unchanged
+            out.append(out[-1])
+            continue
         if record:
             v, e, p = eng.export(pre=True)
             out.append((v.shape[0], e.shape[0],

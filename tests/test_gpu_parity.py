@@ -51,8 +51,12 @@ def test_forward_small_batches_bitwise(cuda, n):
         assert torch.equal(got, want)
 
 
-def test_encoding_bitwise(cuda):
-    d = load("synth32u")
+@pytest.mark.parametrize("name", [n for n in ("synth32u", "synth32h", "synth64h", "large_sphere")
+                                  if n in cases()])
+def test_encoding_bitwise(cuda, name):
+    """Dense levels (synth32u) and prime-XOR hashed levels (synth32h: 31^3 >
+    2^14; synth64h; large_sphere level 3: 128^3 > 2^19)."""
+    d = load(name)
     net, ref = product_net(d, cuda), oracle_net(d)
     x = (_rand_points(5000, 2) + 1) / 2
     got = net.enc(x.to(cuda)).cpu()
@@ -129,6 +133,11 @@ def test_skeleton_bitwise(cuda, name):
         np.testing.assert_array_equal(e.cpu().numpy(), d["skel_E"])
     else:
         assert sha(v.cpu().numpy(), e.cpu().numpy()) == str(d["sha_skel"])
+    if "skel_dups" in d:
+        # multi-tile skeleton: the 127-stride tile overlap duplicates edges
+        # (reference tropical.py:176-181); they are kept, as the reference does
+        assert int(d["skel_dups"]) > 0
+        assert e.shape[0] - torch.unique(e, dim=0).shape[0] == int(d["skel_dups"])
 
 
 @pytest.mark.parametrize("name", cases("subpoly"))
@@ -197,3 +206,31 @@ def test_tied_levels_layout(cuda, monkeypatch):
         runs.append(engine_steps(eng))
     assert runs[0] == runs[1]
     assert runs[0][-1][:2] == (int(d["step_V"][-1]), int(d["step_E"][-1]))
+
+
+@pytest.mark.parametrize("force", [True, False])
+def test_subpoly_step_rewrites_caller_edges(cuda, force):
+    """subpoly.py:209-212: a splitting step rewrites the caller's edges[:, 1]
+    in place (masked_scatter_ of the new vertex ids).  With pruning=False the
+    returned edge list is [rewritten edges; e_new; c_new], so its head must
+    equal the caller's tensor after the call."""
+    import tropical.subpoly as sp
+    from tropical.synthetic import lattice_edges, lattice_vertices
+    d = load("synth24")
+    net = product_net(d, cuda)
+    V = torch.from_numpy(lattice_vertices(d["marks"])).to(cuda)
+    E = torch.from_numpy(lattice_edges(int(d["lattice_n"]))).to(cuda)
+    o = None
+    for idx in range(net.K):
+        l, h = divmod(idx, net.num_hidden)
+        E_in = E.clone()
+        V2, E2, o2 = sp.subpoly_(V, E, net, l, h, 1e-4, o, pruning=False, force=force)
+        if V2.shape[0] == V.shape[0]:
+            assert torch.equal(E, E_in)  # nothing split: untouched
+            V, E, o = V2, E2, o2
+            continue
+        changed = (E != E_in).any(dim=1)
+        assert changed.any() and torch.equal(E[:, 0], E_in[:, 0])
+        assert torch.equal(E2[:E.shape[0]], E)
+        assert int(E[changed, 1].min()) >= V.shape[0]
+        break

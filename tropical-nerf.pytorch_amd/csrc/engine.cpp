@@ -669,6 +669,18 @@ static int curve_filter(tnp_engine* e, int idx, int override_, hipStream_t s, in
   return 0;
 }
 
+extern "C" int tnp_engine_split_keep(tnp_engine* e, int32_t* d_keep, int64_t n, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  TNP_CHECK(hipSetDevice(e->device));
+  if (!e->curve || n <= 0) return 0;
+  if (e->cv[CV_KEEP].bytes < (size_t)n * sizeof(int32_t)) {
+    tnp_set_error("split_keep: no strict filter ran for %lld splits", (long long)n);
+    return -1;
+  }
+  TNP_CHECK(hipMemcpyAsync(d_keep, e->cv[CV_KEEP].p, n * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+  return 0;
+}
+
 extern "C" int tnp_engine_set_shards(tnp_engine* e, int world) {
   e->shards = world < 1 ? 1 : world;
   return 0;

@@ -132,6 +132,14 @@ class Engine:
                                                 C.byref(st)), "tnp_engine_finish")
         return st.as_dict()
 
+    def split_keep(self, n: int) -> torch.Tensor:
+        """Curve path: the strict filter's keep flags of the last step's n
+        candidate splits (edge order)."""
+        keep = torch.empty(n, dtype=torch.int32, device=self.device)
+        _hip.check(_hip.lib().tnp_engine_split_keep(self.h, _hip.ptr(keep), n, self._s),
+                   "tnp_engine_split_keep")
+        return keep.bool()
+
     def surface(self):
         V, E = C.c_int64(), C.c_int64()
         _hip.check(_hip.lib().tnp_engine_surface(self.h, self._s, C.byref(V), C.byref(E)),

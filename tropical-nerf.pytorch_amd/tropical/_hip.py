@@ -66,6 +66,7 @@ SIGNATURES = {
     "tnp_engine_split": (C.c_int, [_VP, C.c_int, _VP, _P64, _P32]),
     "tnp_engine_finish": (C.c_int, [_VP, C.c_int, C.c_int, C.c_int, _VP, C.POINTER(TnpStepStats)]),
     "tnp_engine_sizes": (C.c_int, [_VP, _P64, _P64]),
+    "tnp_engine_split_keep": (C.c_int, [_VP, _VP, _I64, _VP]),
     "tnp_engine_export": (C.c_int, [_VP, _VP, _VP, _VP, _VP]),
     "tnp_engine_surface": (C.c_int, [_VP, _VP, _P64, _P64]),
     "tnp_engine_faces": (C.c_int, [_VP, _VP, _P64, _P64]),

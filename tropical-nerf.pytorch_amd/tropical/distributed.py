@@ -31,6 +31,18 @@ Regions are (grid cell x sign pattern), so pairs, connecting edges and faces
 never span cells: the stitched complex equals the unsharded one up to the
 vertex numbering (the reference interleaves tiles), which is why parity at
 N > 1 is checked after canonicalisation (tests/test_multi_rank.py).
+
+Exactness is CHECKED, not assumed: halo_check() has both neighbours of every
+cut fingerprint the complex they each computed in the two cells next to the
+cut (and the cut plane), and raises on any difference.  A slab's own errors
+start at its outer halo boundary; to reach anything a rank keeps they must
+cross those two cells, where the neighbour -- for which they are interior --
+computed them from a different boundary.
+
+Stanford nets (BASELINE config 4): every rank computes the reference's
+skeleton on its 128-mark tiles (tropical.py:176-181, per-tile max_grad),
+cuts the x axis into slabs of equal skeleton-edge count (balanced_cuts) and
+keeps its slab plus halo (slab_restrict) -- subpoly_sharded().
 """
 from __future__ import annotations
 
@@ -50,6 +62,22 @@ HALO = 2  # cell columns extracted beyond each cut plane
 def slab_marks(cuts: list, rank: int, halo: int = HALO):
     """Marks [x0, x1] a rank extracts: its cells plus `halo` cells each side."""
     return max(cuts[rank] - halo, cuts[0]), min(cuts[rank + 1] + halo, cuts[-1])
+
+
+def balanced_cuts(cell_load: Tensor, world: int) -> list:
+    """Cut the x cells 0..n-1 (n = n_marks - 1) into `world` slabs of about
+    equal load (e.g. skeleton edges per x cell); every slab gets >= 1 cell."""
+    n = int(cell_load.shape[0])
+    if world > n:
+        raise ValueError(f"{world} slabs of {n} cells")
+    c = torch.cumsum(cell_load.to(torch.float64).cpu(), 0)
+    tot = float(c[-1]) if n else 0.0
+    cuts = [0]
+    for r in range(1, world):
+        k = int(torch.searchsorted(c, torch.tensor(tot * r / world, dtype=torch.float64)).item()) + 1
+        cuts.append(min(max(k, cuts[-1] + 1), n - (world - r)))
+    cuts.append(n)
+    return cuts
 
 
 def x_grid(vertices: Tensor, marks: Tensor, eps: float = 1e-4):
@@ -73,6 +101,28 @@ def owner_of(vertices: Tensor, marks: Tensor, cuts: list, eps: float = 1e-4) -> 
     r_cell = torch.searchsorted(c, off, right=True) - 1
     r = torch.where(on, r_plane, r_cell)
     return r.clamp(0, len(cuts) - 2)
+
+
+def slab_restrict(vertices: Tensor, edges: Tensor, marks: Tensor, x0: int, x1: int,
+                  eps: float = 1e-4):
+    """The sub-complex of a complex whose vertices lie on mark planes (a
+    skeleton) between x planes x0 and x1: vertices kept in order (ids
+    renumbered order-preserving, as slab_lattice numbers the lattice),
+    edges with both endpoints kept, in order (duplicates included)."""
+    off, on = x_grid(vertices, marks.to(vertices.device), eps)
+    if not bool(on.all()):
+        raise ValueError("slab_restrict: vertices off the x mark planes")
+    keep = (off >= x0) & (off <= x1)
+    nid = torch.cumsum(keep.to(torch.int64), 0) - 1
+    e = edges.to(vertices.device)
+    ke = keep[e[:, 0]] & keep[e[:, 1]]
+    return vertices[keep], nid[e[ke]]
+
+
+def comm_device(group, device) -> torch.device:
+    """Where a collective's tensors must live: the GPU for RCCL ("nccl"),
+    host memory for gloo (multi-rank rehearsals sharing one GPU)."""
+    return torch.device("cpu") if dist.get_backend(group) == "gloo" else torch.device(device)
 
 
 def _all_gather_padded(t: Tensor, group=None) -> list:
@@ -112,6 +162,43 @@ def complex_hash(vertices: Tensor, edges: Tensor, vmask: Tensor = None, emask: T
     if emask is not None:
         he = he[emask]
     return int(hv.sum().item()), int(he.sum().item())
+
+
+def cut_fingerprint(vertices: Tensor, edges: Tensor, marks: Tensor, cut: int, eps: float = 1e-4):
+    """(#vertices, #edges, vertex-set hash, edge-set hash) of the complex
+    strictly between mark planes cut-1 and cut+1: cells cut-1 and cut and
+    the cut plane, edges with both endpoints there."""
+    off, on = x_grid(vertices, marks.to(vertices.device), eps)
+    sel = torch.where(on, off == cut, (off == cut - 1) | (off == cut))
+    e = edges.to(vertices.device)
+    emask = sel[e[:, 0]] & sel[e[:, 1]]
+    hv, he = complex_hash(vertices, e, sel, emask)
+    return [int(sel.sum().item()), int(emask.sum().item()), hv, he]
+
+
+def halo_check(vertices: Tensor, edges: Tensor, marks: Tensor, cuts: list, eps: float = 1e-4,
+               group=None):
+    """Compare, across every cut, the two neighbours' complexes next to the
+    cut (cut_fingerprint); raise RuntimeError on any difference.  Returns the
+    per-cut fingerprints (rank 0's view) for logging."""
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    mine = torch.zeros(2, 4, dtype=torch.int64, device=comm_device(group, vertices.device))
+    if rank > 0:
+        mine[0] = torch.tensor(cut_fingerprint(vertices, edges, marks, cuts[rank], eps))
+    if rank < world - 1:
+        mine[1] = torch.tensor(cut_fingerprint(vertices, edges, marks, cuts[rank + 1], eps))
+    allv = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allv, mine, group=group)
+    bad = []
+    for r in range(world - 1):
+        lo, hi = allv[r][1].tolist(), allv[r + 1][0].tolist()
+        if lo != hi:
+            bad.append(f"cut {cuts[r + 1]}: rank {r} sees {lo[:2]} (hash {lo[2]:x}/{lo[3]:x}), "
+                       f"rank {r + 1} sees {hi[:2]} (hash {hi[2]:x}/{hi[3]:x})")
+    if bad:
+        raise RuntimeError("halo_check: the shards disagree next to a cut (halo too narrow): "
+                           + "; ".join(bad))
+    return [allv[r][1].tolist() for r in range(world - 1)]
 
 
 def stitch(vertices: Tensor, edges: Tensor, marks: Tensor, cuts: list, eps: float = 1e-4,
@@ -181,3 +268,42 @@ def gather_complex(owned: Tensor, first: int, gedges: Tensor, dst: int = 0, grou
     if rank != dst:
         return None, None
     return torch.cat(vs, dim=0), torch.cat(es, dim=0)
+
+
+def subpoly_sharded(net, size: float = 1.2, group=None, allreduce=None, stats: list = None,
+                    halo: int = HALO):
+    """The hot loop of subpoly() (subpoly.py:45-69) sharded over the ranks of
+    `group` (one GPU each): the skeleton (tropical.py:158-225, computed whole
+    on every rank -- a few lattice passes), x-slabs of equal skeleton-edge
+    load, each rank's slab + halo through every hyperplane step with the
+    reference's global decisions made by `allreduce(vec, op)`, then
+    halo_check and stitch.  Returns (engine, owned vertices, first global
+    id, global edges, cuts): the engine still holds this rank's slab complex."""
+    from ._engine import engine_for
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    eng = engine_for(net)
+    eng.set_shards(world)
+    V0, E0 = eng.skeleton(unit=128, size=size)
+    v, e, _ = eng.export()
+    marks = net.enc.marks.to(v.device)
+    off, on = x_grid(v, marks, net.eps)
+    if not bool(on.all()):
+        raise NotImplementedError("subpoly_sharded: the skeleton fell back to get_hypercube "
+                                  "(subpoly.py:51-52); nothing to shard")
+    n_cells = marks.shape[0] - 1
+    # an edge's x cell: the lower of its endpoints' x planes (x-edges span one
+    # cell; y/z edges lie in a plane, charged to the cell on its right)
+    ex = torch.minimum(off[e[:, 0]], off[e[:, 1]]).clamp(0, n_cells - 1)
+    load = torch.bincount(ex, minlength=n_cells)
+    cuts = balanced_cuts(load, world)
+    x0, x1 = slab_marks(cuts, rank, halo)
+    vs, es = slab_restrict(v, e, marks, x0, x1, net.eps)
+    eng.load(vs, es)
+    eng.set_owned(cuts[rank], cuts[rank + 1])
+    eng.run_steps(stats, allreduce)
+    Vl, El, _ = eng.export()
+    cd = comm_device(group, Vl.device)
+    Vl, El = Vl.to(cd), El.to(cd)
+    halo_check(Vl, El, marks, cuts, net.eps, group)
+    owned, first, gE = stitch(Vl, El, marks, cuts, net.eps, group)
+    return eng, owned, first, gE, cuts

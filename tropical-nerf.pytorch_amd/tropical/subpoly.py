@@ -82,9 +82,9 @@ def subpoly_(vertices, edges, net, l, h, eps, outputs_=None, pruning=True, stric
     """One hyperplane step (subpoly.py:90-279); ``force=False`` is the curve
     branch (strict filter on, as the reference's default ``strict=True``).
 
-    Deviation: the caller's ``edges`` tensor is not rewritten in place (the
-    reference's masked_scatter_ side effect at subpoly.py:211); the returned
-    edges are identical."""
+    Like the reference, a step that splits rewrites the caller's ``edges``
+    in place: the second endpoint of every split edge becomes its new vertex
+    (``masked_scatter_``, subpoly.py:209-212)."""
     _check_eps(net, eps)
     if not force and not strict:
         raise NotImplementedError("subpoly_(force=False, strict=False) is not on the extraction path")
@@ -95,7 +95,19 @@ def subpoly_(vertices, edges, net, l, h, eps, outputs_=None, pruning=True, stric
     if S == 0:
         v, e, o = eng.export(pre=True)
         return v, e, o
+    # the split mask of subpoly.py:102-105 over the caller's cached column
+    col = outputs_[:, idx] if outputs_ is not None else None
+    if col is None:
+        col = torch.cat(net(vertices.to(net.device()), gather=True)[1], dim=-1)[:, idx]
+    d = col.to(edges.device)[edges]
+    m = (d[:, 0] * d[:, 1]) < 0
+    m &= (d[:, 0].abs() > eps) & (d[:, 1].abs() > eps)
     eng.finish(idx, bool(h < net.num_hidden and pruning), fail)
+    if not force:  # the strict filter's survivors (subpoly_debug.py:234-271)
+        m[m.clone()] = eng.split_keep(S).to(edges.device)
+    n_new = int(m.sum())
+    edges[:, 1].masked_scatter_(m, torch.arange(n_new, device=edges.device).to(edges)
+                                + vertices.shape[0])
     return eng.export(pre=True)
 
 

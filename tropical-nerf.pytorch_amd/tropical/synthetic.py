@@ -17,9 +17,11 @@ from __future__ import annotations
 import numpy as np
 
 
-def net_config_for_lattice(n_marks: int) -> dict:
+def net_config_for_lattice(n_marks: int, T: int = 19) -> dict:
+    """T < 19 hashes smaller lattices: level res = n_marks - 1 is prime-hashed
+    once (n_marks - 1)^3 > 2^T (tcnn semantics)."""
     return dict(num_layers=3, num_hidden=16, levels=2, r_min=n_marks - 1,
-                r_max=n_marks - 1, T=19)
+                r_max=n_marks - 1, T=T)
 
 
 def random_params(n_table: int, num_nodes, seed: int, amp: float = 0.1) -> dict:
