@@ -66,6 +66,8 @@ def _slab_worker(rank, world, port, outdir, cuts):
 
         with torch.no_grad():
             V, E, _ = od.run_steps(torch.from_numpy(V), torch.from_numpy(E), net, 1e-4, sync=sync)
+        from tropical.distributed import halo_check
+        halo_check(V, E, torch.from_numpy(d["marks"]), cuts)
         owned, first, gE = stitch(V, E, torch.from_numpy(d["marks"]), cuts)
         SV, SE = gather_complex(owned, first, gE)
         if rank == 0:
@@ -115,3 +117,80 @@ def test_gloo_ranks_reproduce_the_unsharded_complex(tmp_path, world):
     assert z["V"].shape[0] == V.shape[0] and z["E"].shape[0] == E.shape[0]
     sv, se = _canon(z["V"], z["E"])
     assert sv == whole_v and se == whole_e
+
+
+def _halo_worker(rank, world, port, outdir, corrupt):
+    """Both ranks hold the same unsharded complex (exact views); rank 1
+    optionally drops one edge next to the cut: halo_check must raise."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from tropical.distributed import halo_check, x_grid
+        d = load(CASE)
+        z = np.load(os.path.join(outdir, "whole.npz"))
+        V, E = torch.from_numpy(z["V"]), torch.from_numpy(z["E"])
+        marks = torch.from_numpy(d["marks"])
+        cuts = CUTS[2]
+        if corrupt and rank == 1:
+            off, on = x_grid(V, marks)
+            near = (off[E[:, 0]] == cuts[1]) & ~on[E[:, 0]] & (off[E[:, 1]] == cuts[1])
+            drop = int(torch.nonzero(near)[0])
+            E = torch.cat([E[:drop], E[drop + 1:]])
+        try:
+            halo_check(V, E, marks, cuts)
+            res = "ok"
+        except RuntimeError as ex:
+            res = str(ex)
+        with open(os.path.join(outdir, f"r{rank}.txt"), "w") as f:
+            f.write(res)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("corrupt", [False, True])
+def test_halo_check_detects_a_missing_edge(tmp_path, corrupt):
+    import oracle.subdivide as od
+    from tropical.synthetic import lattice_edges, lattice_vertices
+    d = load(CASE)
+    net = oracle_net(d)
+    with torch.no_grad():
+        V, E, _ = od.run_steps(torch.from_numpy(lattice_vertices(d["marks"])),
+                               torch.from_numpy(lattice_edges(int(d["lattice_n"]))), net, 1e-4)
+    np.savez(tmp_path / "whole.npz", V=V.numpy(), E=E.numpy())
+    mp.spawn(_halo_worker, args=(2, _free_port(), str(tmp_path), corrupt), nprocs=2, join=True)
+    res = [(tmp_path / f"r{r}.txt").read_text() for r in range(2)]
+    if corrupt:
+        assert all("halo_check" in r and f"cut {CUTS[2][1]}" in r for r in res)
+    else:
+        assert res == ["ok", "ok"]
+
+
+def test_balanced_cuts():
+    from tropical.distributed import balanced_cuts
+    load_ = torch.tensor([0, 0, 10, 10, 0, 0, 10, 10, 0, 0])
+    assert balanced_cuts(load_, 1) == [0, 10]
+    c = balanced_cuts(load_, 2)
+    assert c[0] == 0 and c[-1] == 10 and 3 <= c[1] <= 6
+    c = balanced_cuts(torch.zeros(5, dtype=torch.int64), 5)
+    assert c == [0, 1, 2, 3, 4, 5]
+    c = balanced_cuts(torch.tensor([100, 0, 0, 0, 0, 0]), 3)
+    assert c == sorted(set(c)) and len(c) == 4
+
+
+def test_slab_restrict_matches_slab_lattice():
+    """The skeleton shard's restriction of a mark-plane complex equals the
+    lattice slab layout (order-preserving ids, edges in order)."""
+    from tropical.distributed import slab_restrict
+    from tropical.synthetic import lattice_edges, lattice_vertices, slab_lattice
+    d = load(CASE)
+    n = int(d["lattice_n"])
+    V = torch.from_numpy(lattice_vertices(d["marks"]))
+    E = torch.from_numpy(lattice_edges(n))
+    for x0, x1 in ((0, 5), (7, 15), (20, n - 1)):
+        v, e = slab_restrict(V, E, torch.from_numpy(d["marks"]), x0, x1)
+        sv, se = slab_lattice(d["marks"], x0, x1)
+        assert torch.equal(v, torch.from_numpy(sv))
+        # the lattice slab orders x-edges, then y, then z: the same subsequence
+        assert sorted(map(tuple, e.tolist())) == sorted(map(tuple, se.tolist()))
+        assert e.shape[0] == se.shape[0]
