@@ -58,6 +58,7 @@ typedef struct tnp_step_stats {
   int32_t override_applied;
   uint64_t next_active; /* planes > idx a kept edge would split (pruning steps) */
   int64_t S_dup;        /* splits outside the owned slab (multi-GPU halo) */
+  int64_t T;            /* (cell, member) entries of the pair test */
 } tnp_step_stats;
 
 const char* tnp_last_error(void);

@@ -1,0 +1,438 @@
+// Grouping of a step's region members by grid cell without a global sort
+// (the bucketing behind regions_to_vertices / r_idx_as_tensor /
+// extract_every_valid_edge, subpoly.py:281-370, 484-535).
+//
+// A member (new vertex or hit vertex) belongs to every grid cell its
+// eps-region spans: 1 cell per axis, 2 when it lies on a mark plane
+// (subpoly.py:327-332).  The pair test needs, per cell, the contiguous list
+// of its members.  Instead of radix-sorting every (cell, member) entry over
+// the whole cell-id range (3 global passes), cells are grouped in spatial
+// BUCKETS of (2^sh)^3 cells:
+//
+//   bucket_count    member -> its entries' buckets: LDS histogram per block,
+//                   one global add per non-empty bin (+ the reference's
+//                   augmented-row count A, the k=0 guard)
+//   bucket_scan     bucket bases (one block)
+//   bucket_scatter  (local cell, vertex) entries into their bucket's range
+//   bucket_group    one block per bucket: LDS counting sort by local cell,
+//                   the 32-byte pair-test records written cell-contiguous,
+//                   the bucket's pair cells (>= 2 members) in local cell
+//                   order with their local pair offsets
+//   pair_scan       per-bucket pair-cell / pair totals -> global offsets
+//   pair_gather     the global pair-cell list (cell, first entry, members,
+//                   first pair) that k_connect walks
+//
+// Every count the host needs stays on the device (no readback between the
+// split and the connect kernel).  Within a cell the entry order is whatever
+// the atomics produce: nothing downstream depends on it (the pair test is
+// symmetric, the emitted edges are sorted), so results stay bitwise
+// deterministic.  Traffic per entry: 8 B scatter write + 8 B read + 24 B key
+// gather + 32 B record write, against ~70 B for three 8-bit radix passes.
+#include <algorithm>
+
+#include "common.h"
+#include "step.h"
+
+namespace {
+
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_sum_parts_b(const int64_t* __restrict__ part, int64_t n, int64_t* __restrict__ ctr, int slot) {
+  __shared__ int64_t lds[TNP_WAVES];
+  int64_t a = 0;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) a += part[i];
+  int64_t tot;
+  tnp::block_scan_excl(a, lds, tot);
+  if (threadIdx.x == 0) ctr[slot] = tot;
+}
+
+constexpr int BK_IPT = 8;  // members per thread in the member passes
+
+struct BGeom {
+  int NC;   // cell coordinates (+2) per axis: [0, NC)
+  int sh;   // log2 of the bucket edge in cells
+  int NBd;  // buckets per axis
+};
+
+__device__ __forceinline__ void span_of(uint64_t g, int lo[3], int n[3]) {
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    const int o = tnp::grid_off(g, d);
+    const bool z = tnp::grid_zero(g, d);
+    lo[d] = (z ? o - 1 : o) + 2;  // cell coordinate + 2 (cell_id convention)
+    n[d] = z ? 2 : 1;
+  }
+}
+
+__device__ __forceinline__ int bucket_of(const BGeom& G, int cx, int cy, int cz) {
+  return ((cx >> G.sh) * G.NBd + (cy >> G.sh)) * G.NBd + (cz >> G.sh);
+}
+
+__device__ __forceinline__ int local_of(const BGeom& G, int cx, int cy, int cz) {
+  const int m = (1 << G.sh) - 1;
+  return ((cx & m) << (2 * G.sh)) | ((cy & m) << G.sh) | (cz & m);
+}
+
+// (1) per-bucket entry counts; per-block augmented-row sums -> part[]
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_bucket_count(const int32_t* __restrict__ members, int64_t M, const uint64_t* __restrict__ grid,
+               const uint64_t* __restrict__ zero, int idx, BGeom G, int NB,
+               int32_t* __restrict__ bcount, int64_t* __restrict__ part, int64_t* __restrict__ ctr) {
+  __shared__ int hist[BUCKET_MAX];
+  __shared__ int64_t lds[TNP_WAVES];
+  for (int i = threadIdx.x; i < NB; i += TNP_BLOCK) hist[i] = 0;
+  __syncthreads();
+  const uint64_t below = (idx >= 64) ? ~0ull : ((1ull << idx) - 1ull);
+  const int64_t base = (int64_t)blockIdx.x * TNP_BLOCK * BK_IPT;
+  int64_t aug = 0;
+  bool k0 = false;
+#pragma unroll
+  for (int k = 0; k < BK_IPT; ++k) {
+    const int64_t m = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
+    if (m >= M) break;
+    const int v = members[m];
+    int lo[3], n[3];
+    span_of(grid[v], lo, n);
+    for (int i = 0; i < n[0]; ++i)
+      for (int j = 0; j < n[1]; ++j)
+        for (int q = 0; q < n[2]; ++q) atomicAdd(&hist[bucket_of(G, lo[0] + i, lo[1] + j, lo[2] + q)], 1);
+    const int kz = __popcll(zero[v] & below) + (n[0] - 1) + (n[1] - 1) + (n[2] - 1);
+    aug += 1ll << kz;
+    k0 |= kz == 0;
+  }
+  if (__ballot(k0) && tnp::lane() == 0) atomicOr((unsigned long long*)&ctr[CTR_K0], 1ull);
+  __syncthreads();
+  for (int i = threadIdx.x; i < NB; i += TNP_BLOCK)
+    if (hist[i]) atomicAdd(&bcount[i], hist[i]);
+  int64_t tot;
+  tnp::block_scan_excl(aug, lds, tot);
+  if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+
+// (2) exclusive scan of n int32 counts -> int64 bases [0, n]; total ->
+// ctr[slot] (one block; n is a few thousand)
+__global__ void __launch_bounds__(1024)
+k_small_scan(const int32_t* __restrict__ cnt, int n, int64_t* __restrict__ out, int64_t* __restrict__ ctr,
+             int slot) {
+  __shared__ int64_t lds[16];
+  const int per = (n + 1023) / 1024;
+  const int b = threadIdx.x * per;
+  int64_t s = 0;
+  for (int i = b; i < b + per && i < n; ++i) s += cnt[i];
+  int64_t inc = tnp::wave_scan_incl(s);
+  if (tnp::lane() == 63) lds[tnp::wave()] = inc;
+  __syncthreads();
+  int64_t off = 0, tot = 0;
+  for (int w = 0; w < 16; ++w) {
+    off += (w < tnp::wave()) ? lds[w] : 0;
+    tot += lds[w];
+  }
+  int64_t run = off + inc - s;
+  for (int i = b; i < b + per && i < n; ++i) {
+    out[i] = run;
+    run += cnt[i];
+  }
+  if (threadIdx.x == 0) {
+    out[n] = tot;
+    if (ctr) ctr[slot] = tot;
+  }
+}
+
+// the same for int64 values (pair counts)
+__global__ void __launch_bounds__(1024)
+k_small_scan64(const int64_t* __restrict__ cnt, int n, int64_t* __restrict__ out, int64_t* __restrict__ ctr,
+               int slot) {
+  __shared__ int64_t lds[16];
+  const int per = (n + 1023) / 1024;
+  const int b = threadIdx.x * per;
+  int64_t s = 0;
+  for (int i = b; i < b + per && i < n; ++i) s += cnt[i];
+  int64_t inc = tnp::wave_scan_incl(s);
+  if (tnp::lane() == 63) lds[tnp::wave()] = inc;
+  __syncthreads();
+  int64_t off = 0, tot = 0;
+  for (int w = 0; w < 16; ++w) {
+    off += (w < tnp::wave()) ? lds[w] : 0;
+    tot += lds[w];
+  }
+  int64_t run = off + inc - s;
+  for (int i = b; i < b + per && i < n; ++i) {
+    out[i] = run;
+    run += cnt[i];
+  }
+  if (threadIdx.x == 0) {
+    out[n] = tot;
+    if (ctr) ctr[slot] = tot;
+  }
+}
+
+// (3) entries into their bucket ranges: a block reserves one range per
+// non-empty bin (one global add), then places its entries inside it
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_bucket_scatter(const int32_t* __restrict__ members, int64_t M, const uint64_t* __restrict__ grid,
+                 BGeom G, int NB, const int64_t* __restrict__ bbase, int32_t* __restrict__ bcur,
+                 uint64_t* __restrict__ ekv) {
+  __shared__ int hist[BUCKET_MAX];
+  __shared__ int rel[BUCKET_MAX];
+  for (int i = threadIdx.x; i < NB; i += TNP_BLOCK) hist[i] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * TNP_BLOCK * BK_IPT;
+  int vv[BK_IPT];
+  uint64_t gg[BK_IPT];
+#pragma unroll
+  for (int k = 0; k < BK_IPT; ++k) {
+    const int64_t m = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
+    vv[k] = m < M ? members[m] : -1;
+  }
+#pragma unroll
+  for (int k = 0; k < BK_IPT; ++k) gg[k] = grid[vv[k] >= 0 ? vv[k] : 0];
+#pragma unroll
+  for (int k = 0; k < BK_IPT; ++k) {
+    if (vv[k] < 0) continue;
+    int lo[3], n[3];
+    span_of(gg[k], lo, n);
+    for (int i = 0; i < n[0]; ++i)
+      for (int j = 0; j < n[1]; ++j)
+        for (int q = 0; q < n[2]; ++q) atomicAdd(&hist[bucket_of(G, lo[0] + i, lo[1] + j, lo[2] + q)], 1);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < NB; i += TNP_BLOCK) {
+    const int c = hist[i];
+    rel[i] = c ? atomicAdd(&bcur[i], c) : 0;
+    hist[i] = 0;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < BK_IPT; ++k) {
+    if (vv[k] < 0) continue;
+    int lo[3], n[3];
+    span_of(gg[k], lo, n);
+    for (int i = 0; i < n[0]; ++i)
+      for (int j = 0; j < n[1]; ++j)
+        for (int q = 0; q < n[2]; ++q) {
+          const int cx = lo[0] + i, cy = lo[1] + j, cz = lo[2] + q;
+          const int b = bucket_of(G, cx, cy, cz);
+          const int64_t pos = bbase[b] + rel[b] + atomicAdd(&hist[b], 1);
+          // cell flags (CellEnt::f): the member's lowest cell along d is
+          // this one iff it is the first of its span there
+          const uint32_t f = (uint32_t)(i == 0) | ((uint32_t)(j == 0) << 1) | ((uint32_t)(q == 0) << 2) |
+                             ((uint32_t)(n[0] - 1) << 3) | ((uint32_t)(n[1] - 1) << 4) |
+                             ((uint32_t)(n[2] - 1) << 5);
+          ekv[pos] = ((uint64_t)local_of(G, cx, cy, cz) << 40) | ((uint64_t)f << 32) | (uint32_t)vv[k];
+        }
+  }
+}
+
+// (4) one block per bucket: counting sort by local cell in LDS, records,
+// the bucket's pair cells.  Pair-cell lists are written to the bucket's own
+// area [bbase / 2, bbase / 2 + n / 2] (a pair cell holds >= 2 entries).
+// Entries go through in batches of GIPT per thread, every batch's loads in
+// flight together (a bucket can hold 10^5 entries: a block walking them one
+// dependent load -> atomic -> store chain at a time is latency-bound).
+constexpr int GIPT = 8;
+
+template <int SH>
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __restrict__ ekv,
+               const ulonglong2* __restrict__ pz, CellEnt* __restrict__ ents,
+               int32_t* __restrict__ lcell, int32_t* __restrict__ lent, int32_t* __restrict__ ln,
+               int64_t* __restrict__ lpoff, int32_t* __restrict__ bnpc, int64_t* __restrict__ bnpairs,
+               int64_t* __restrict__ ctr) {
+  constexpr int LC = 1 << (3 * SH);
+  __shared__ int cnt[LC];
+  __shared__ int cur[LC];
+  __shared__ int64_t lds[TNP_WAVES];
+  const int b = blockIdx.x;
+  const int64_t base = bbase[b];
+  const int64_t n = bbase[b + 1] - base;
+  if (n < 2) {
+    if (threadIdx.x == 0) {
+      bnpc[b] = 0;
+      bnpairs[b] = 0;
+    }
+    return;
+  }
+  for (int i = threadIdx.x; i < LC; i += TNP_BLOCK) cnt[i] = 0;
+  __syncthreads();
+  const uint64_t* kv = ekv + base;
+  for (int64_t e0 = 0; e0 < n; e0 += TNP_BLOCK * GIPT) {
+    uint64_t w[GIPT];
+#pragma unroll
+    for (int k = 0; k < GIPT; ++k) {
+      const int64_t e = e0 + k * TNP_BLOCK + threadIdx.x;
+      w[k] = e < n ? kv[e] : ~0ull;
+    }
+#pragma unroll
+    for (int k = 0; k < GIPT; ++k)
+      if (w[k] != ~0ull) atomicAdd(&cnt[(int)(w[k] >> 40)], 1);
+  }
+  __syncthreads();
+  // exclusive scan of cnt into cur (contiguous chunk per thread)
+  constexpr int per = LC / TNP_BLOCK > 0 ? LC / TNP_BLOCK : 1;
+  const int c0 = threadIdx.x * per;
+  int64_t s = 0;
+  for (int i = c0; i < c0 + per && i < LC; ++i) s += cnt[i];
+  int64_t tot;
+  int64_t run = tnp::block_scan_excl(s, lds, tot);
+  for (int i = c0; i < c0 + per && i < LC; ++i) {
+    cur[i] = (int)run;
+    run += cnt[i];
+  }
+  __syncthreads();
+  // records, cell-contiguous: the member keys gathered here (the members of
+  // one bucket are spatially close: their slots cluster)
+  for (int64_t e0 = 0; e0 < n; e0 += TNP_BLOCK * GIPT) {
+    uint64_t w[GIPT];
+    int pos[GIPT];
+    ulonglong2 k2[GIPT];
+#pragma unroll
+    for (int k = 0; k < GIPT; ++k) {
+      const int64_t e = e0 + k * TNP_BLOCK + threadIdx.x;
+      w[k] = e < n ? kv[e] : ~0ull;
+    }
+#pragma unroll
+    for (int k = 0; k < GIPT; ++k) {
+      pos[k] = w[k] != ~0ull ? atomicAdd(&cur[(int)(w[k] >> 40)], 1) : 0;
+      k2[k] = pz[w[k] != ~0ull ? (uint32_t)w[k] : 0u];
+    }
+#pragma unroll
+    for (int k = 0; k < GIPT; ++k) {
+      if (w[k] == ~0ull) continue;
+      CellEnt r;
+      r.p = k2[k].x;
+      r.z = k2[k].y;
+      r.v = (int32_t)(uint32_t)w[k];
+      r.f = (uint32_t)(w[k] >> 32) & 63u;
+      r.pad = 0;
+      ents[base + pos[k]] = r;
+    }
+  }
+  __syncthreads();
+  // pair cells in local-cell order (cur[i] now = end of cell i)
+  int npc = 0;
+  int64_t np = 0;
+  bool big = false;
+  for (int i = c0; i < c0 + per && i < LC; ++i) {
+    const int m = cnt[i];
+    big |= m > 65535;
+    if (m >= 2 && m <= 65535) {
+      ++npc;
+      np += (int64_t)m * (m - 1) / 2;
+    }
+  }
+  if (__ballot(big) && tnp::lane() == 0) atomicOr((unsigned long long*)&ctr[CTR_BIG], 1ull);
+  int64_t tpc, tp;
+  int64_t opc = tnp::block_scan_excl((int64_t)npc, lds, tpc);
+  int64_t op = tnp::block_scan_excl(np, lds, tp);
+  const int64_t area = base / 2;
+  const int m_ = (1 << G.sh) - 1;
+  const int bz = b % G.NBd, by = (b / G.NBd) % G.NBd, bx = b / (G.NBd * G.NBd);
+  for (int i = c0; i < c0 + per && i < LC; ++i) {
+    const int m = cnt[i];
+    if (m >= 2 && m <= 65535) {
+      const int cx = (bx << G.sh) | (i >> (2 * G.sh));
+      const int cy = (by << G.sh) | ((i >> G.sh) & m_);
+      const int cz = (bz << G.sh) | (i & m_);
+      lcell[area + opc] = (cx * G.NC + cy) * G.NC + cz;
+      lent[area + opc] = (int32_t)(base + cur[i] - m);
+      ln[area + opc] = m;
+      lpoff[area + opc] = op;
+      ++opc;
+      op += (int64_t)m * (m - 1) / 2;
+    }
+  }
+  if (threadIdx.x == 0) {
+    bnpc[b] = (int32_t)tpc;
+    bnpairs[b] = tp;
+  }
+}
+
+// (6) the global pair-cell list k_connect walks: bucket order, then local
+// cell order
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_pair_gather(const int64_t* __restrict__ bbase, const int32_t* __restrict__ bnpc,
+              const int64_t* __restrict__ pcoff, const int64_t* __restrict__ pairoff,
+              const int32_t* __restrict__ lcell, const int32_t* __restrict__ lent,
+              const int32_t* __restrict__ ln, const int64_t* __restrict__ lpoff,
+              int32_t* __restrict__ pcell, int32_t* __restrict__ pent, int32_t* __restrict__ pn,
+              int64_t* __restrict__ ptoff) {
+  const int b = blockIdx.x;
+  const int cnt = bnpc[b];
+  if (cnt == 0) return;
+  const int64_t area = bbase[b] / 2, o = pcoff[b], po = pairoff[b];
+  for (int i = threadIdx.x; i < cnt; i += TNP_BLOCK) {
+    pcell[o + i] = lcell[area + i];
+    pent[o + i] = lent[area + i];
+    pn[o + i] = ln[area + i];
+    ptoff[o + i] = po + lpoff[area + i];
+  }
+}
+
+}  // namespace
+
+int bucket_geometry(int n_marks, int* sh, int* NBd, int* NB) {
+  const int NC = n_marks + 2;
+  int s = 3;
+  while (s < 5 && NC > 17 * (1 << s)) ++s;  // k_bucket_group is built for 3 and 4
+  if ((1 << (3 * s)) > BUCKET_LOCAL_MAX) return -1;
+  const int nbd = (NC + (1 << s) - 1) >> s;
+  if (nbd * nbd * nbd > BUCKET_MAX) return -1;
+  *sh = s;
+  *NBd = nbd;
+  *NB = nbd * nbd * nbd;
+  return 0;
+}
+
+int launch_bucket_entries(const int32_t* members, int64_t M, const uint64_t* grid, const uint64_t* zero,
+                          int idx, int n_marks, int32_t* bcount, int32_t* bcur, int64_t* bbase,
+                          int64_t* part, uint64_t* ekv, int64_t* ctr, hipStream_t s) {
+  int sh, NBd, NB;
+  if (bucket_geometry(n_marks, &sh, &NBd, &NB)) {
+    tnp_set_error("bucket geometry: %d marks", n_marks);
+    return -1;
+  }
+  const BGeom G{n_marks + 2, sh, NBd};
+  TNP_CHECK(hipMemsetAsync(bcount, 0, NB * sizeof(int32_t), s));
+  TNP_CHECK(hipMemsetAsync(bcur, 0, NB * sizeof(int32_t), s));
+  const int64_t per = (int64_t)TNP_BLOCK * BK_IPT;
+  const unsigned nblk = (unsigned)std::max<int64_t>((M + per - 1) / per, 1);
+  if (M > 0)
+    hipLaunchKernelGGL(k_bucket_count, dim3(nblk), dim3(TNP_BLOCK), 0, s, members, M, grid, zero, idx, G,
+                       NB, bcount, part, ctr);
+  else
+    TNP_CHECK(hipMemsetAsync(part, 0, sizeof(int64_t), s));
+  hipLaunchKernelGGL(k_sum_parts_b, dim3(1), dim3(TNP_BLOCK), 0, s, part, (int64_t)(M > 0 ? nblk : 1),
+                     ctr, (int)CTR_A);
+  hipLaunchKernelGGL(k_small_scan, dim3(1), dim3(1024), 0, s, bcount, NB, bbase, ctr, (int)CTR_T);
+  if (M > 0)
+    hipLaunchKernelGGL(k_bucket_scatter, dim3(nblk), dim3(TNP_BLOCK), 0, s, members, M, grid, G, NB, bbase,
+                       bcur, ekv);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int launch_bucket_pairs(int n_marks, const int64_t* bbase, const uint64_t* ekv, const uint64_t* pz,
+                        CellEnt* ents, int32_t* lcell,
+                        int32_t* lent, int32_t* ln, int64_t* lpoff, int32_t* bnpc, int64_t* bnpairs,
+                        int64_t* pcoff, int64_t* pairoff, int32_t* pcell, int32_t* pent, int32_t* pn,
+                        int64_t* ptoff, int64_t* ctr, hipStream_t s) {
+  int sh, NBd, NB;
+  if (bucket_geometry(n_marks, &sh, &NBd, &NB)) {
+    tnp_set_error("bucket geometry: %d marks", n_marks);
+    return -1;
+  }
+  const BGeom G{n_marks + 2, sh, NBd};
+  if (sh == 3)
+    hipLaunchKernelGGL(k_bucket_group<3>, dim3(NB), dim3(TNP_BLOCK), 0, s, G, bbase, ekv,
+                       reinterpret_cast<const ulonglong2*>(pz), ents, lcell, lent, ln, lpoff, bnpc, bnpairs,
+                       ctr);
+  else
+    hipLaunchKernelGGL(k_bucket_group<4>, dim3(NB), dim3(TNP_BLOCK), 0, s, G, bbase, ekv,
+                       reinterpret_cast<const ulonglong2*>(pz), ents, lcell, lent, ln, lpoff, bnpc, bnpairs,
+                       ctr);
+  hipLaunchKernelGGL(k_small_scan, dim3(1), dim3(1024), 0, s, bnpc, NB, pcoff, ctr, (int)CTR_R);
+  hipLaunchKernelGGL(k_small_scan64, dim3(1), dim3(1024), 0, s, bnpairs, NB, pairoff, ctr, (int)CTR_TESTS);
+  hipLaunchKernelGGL(k_pair_gather, dim3(NB), dim3(TNP_BLOCK), 0, s, bbase, bnpc, pcoff, pairoff, lcell, lent,
+                     ln, lpoff, pcell, pent, pn, ptoff);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}

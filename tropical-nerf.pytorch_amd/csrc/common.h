@@ -30,6 +30,14 @@ namespace tnp {
 __device__ __forceinline__ int lane() { return threadIdx.x & 63; }
 __device__ __forceinline__ int wave() { return threadIdx.x >> 6; }
 
+// XCD-aware block remap (bijective for any grid): blocks the dispatcher
+// places on one XCD (blockIdx % 8 share an L2) take one CONTIGUOUS chunk of
+// the work, so spatially coherent work items share that XCD's L2
+__device__ __forceinline__ int64_t xcd_block(int64_t bid, int64_t nwg) {
+  const int64_t q = nwg / 8, r = nwg % 8, x = bid % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+}
+
 // rank of this lane among the lanes of its wave whose bit is set in `mask`
 __device__ __forceinline__ int mbcnt(uint64_t mask) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),

@@ -173,6 +173,9 @@ struct tnp_engine {
   uint32_t lb_epoch[2] = {0, 0};
   Buf fscr[12];
   Buf fscr2[32];
+  Buf sents;                // bucket-ordered packed entries before the in-bucket grouping
+  Buf bk[12];               // bucket.hip scratch (per-bucket counts, bases, pair-cell areas)
+  bool radix_cells = false; // TNP_RADIX_CELLS=1: the radix-sort bucketing path
   Buf cv[CV_N];
 };
 
@@ -343,6 +346,7 @@ extern "C" int tnp_engine_create(tnp_engine** out, int device) {
   tnp_engine* e = new tnp_engine();
   e->device = device;
   if (const char* lim = getenv("TNP_MAX_PAIR_TESTS")) e->max_pair_tests = atoll(lim);
+  if (const char* rc = getenv("TNP_RADIX_CELLS")) e->radix_cells = atoi(rc) != 0;
   if (hipHostMalloc((void**)&e->h_ctr, CTR_N * sizeof(int64_t), hipHostMallocDefault) != hipSuccess) {
     delete e;
     tnp_set_error("hipHostMalloc failed");
@@ -371,6 +375,8 @@ extern "C" void tnp_engine_destroy(tnp_engine* e) {
   for (Buf* b : bufs) buf_free(*b, s);
   for (Buf& b : e->fscr) buf_free(b, s);
   for (Buf& b : e->fscr2) buf_free(b, s);
+  for (Buf& b : e->bk) buf_free(b, s);
+  buf_free(e->sents, s);
   for (Buf& b : e->cv) buf_free(b, s);
   for (Buf* b : {&e->spcnt, &e->spoff, &e->part, &e->ekey_a, &e->ekey_b, &e->eval_b,
                  &e->sort_scr2})
@@ -841,71 +847,100 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   // slot, live or dead: sizing by it would scan ~V elements per step)
   if (!hits_done && read_ctr(e, s)) return -1;  // else: H came back with S
   const int64_t M = S + e->h_ctr[CTR_H];
-  if (buf_ensure(e->spcnt, std::max<int64_t>(M, 1) * sizeof(int32_t), s)) return -1;
-  if (buf_ensure(e->spoff, std::max<int64_t>(M, 1) * sizeof(int64_t), s)) return -1;
-  if (buf_ensure(e->part, (int64_t)(tnp_grid(M) + 1) * sizeof(int64_t), s)) return -1;
-  TIMED("span_count", 28.0 * M,
-        launch_span_count(P<int32_t>(e->members), S, M, grid, zero, idx, P<int32_t>(e->spcnt),
-                          P<int64_t>(e->part), ctr, s));
-  if (scan_counts(e, P<int32_t>(e->spcnt), P<int64_t>(e->spoff), M, CTR_T, s)) return -1;
-  // a member spans <= 8 cells (2 per axis when on a mark plane): the entry
-  // buffers take the bound 8 M, so the emit is queued ahead of the readback
-  // of T and runs while the host waits for it
+  // a member spans <= 8 cells (2 per axis when on a mark plane): entry
+  // buffers take the bound 8 M, so nothing waits for the entry count T
   const int64_t TB = std::max<int64_t>(8 * M, 1);
-  if (buf_ensure(e->ekey_a, TB * sizeof(uint32_t), s)) return -1;
-  if (buf_ensure(e->ekey_b, TB * sizeof(uint32_t), s)) return -1;
-  if (buf_ensure(e->ent_v, TB * sizeof(int32_t), s)) return -1;
-  if (buf_ensure(e->eval_b, TB * sizeof(int32_t), s)) return -1;
-  TIMED("span_emit", 28.0 * M,
-        launch_span_emit(P<int32_t>(e->members), S, M, grid, NC, P<int64_t>(e->spoff),
-                         P<uint32_t>(e->ekey_a), P<int32_t>(e->ent_v), ctr, s));
-  if (read_ctr(e, s)) return -1;
-  if (e->h_ctr[CTR_K0]) {
-    // the reference builds torch.cartesian_prod() of zero tensors (subpoly.py:317)
-    tnp_set_error("meshgrid expects a non-empty TensorList (a region row without zeros, plane %d)", idx);
-    return -1;
-  }
-  const int64_t H = e->h_ctr[CTR_H];
-  const int64_t T = e->h_ctr[CTR_T];
-  const int64_t T1 = std::max<int64_t>(T, 1);
-  ktimer_set_bytes(e, 20.0 * M + 8.0 * T);  // span_emit's bytes, known only now
-  int cbits = 1;
-  while (cbits < 32 && (1ll << cbits) < ncell) ++cbits;
-  uint32_t* skey = nullptr;
-  int32_t* sval = nullptr;
-  {
-    size_t need = sort_pairs_scratch_bytes(T, cbits);
-    if (buf_ensure(e->sort_scr2, std::max<size_t>(need, 16), s)) return -1;
-    TIMED("cell_sort", 16.0 * T * ((cbits + 7) / 8),
-          sort_pairs_u32(P<uint32_t>(e->ekey_a), P<uint32_t>(e->ekey_b), P<int32_t>(e->ent_v),
-                         P<int32_t>(e->eval_b), T, cbits, e->sort_scr2.p, e->sort_scr2.bytes, &skey,
-                         &sval, s));
-  }
-  // cells holding member pairs straight from the runs of the sorted keys
-  // (compacted, with their flattened pair space offsets; total = tests)
-  {
-    const int64_t RC = T1 / 2 + 1;  // a pair cell holds >= 2 entries
-    if (buf_ensure(e->pcell, RC * sizeof(int32_t), s)) return -1;
-    if (buf_ensure(e->pent, RC * sizeof(int32_t), s)) return -1;
-    if (buf_ensure(e->pcn, RC * sizeof(int32_t), s)) return -1;
-    if (buf_ensure(e->ptoff, RC * sizeof(int64_t), s)) return -1;
-    if (buf_ensure(e->rstart, (T1 + 1) * sizeof(int32_t), s)) return -1;
-    if (T > 0) {
-      TnpLB la, lr, lp;
-      if (lb_begin(e, split_tiles(T), s, &la, 0)) return -1;
-      TIMED("run_starts", 8.0 * T,
-            launch_run_starts(skey, T, P<int32_t>(e->rstart), ctr, la, s));
-      const int64_t pt = pair_run_tiles(T);
-      if (lb_begin(e, pt, s, &lr, 0) || lb_begin(e, pt, s, &lp, 1)) return -1;
-      TIMED("pair_cells", 0.0,
-            launch_pair_runs(skey, P<int32_t>(e->rstart), T, P<int32_t>(e->pcell), P<int32_t>(e->pent),
-                             P<int32_t>(e->pcn), P<int64_t>(e->ptoff), ctr, lr, lp, s));
+  const int64_t RC = TB / 2 + 1;  // a pair cell holds >= 2 entries
+  if (buf_ensure(e->ents, TB * sizeof(CellEnt), s)) return -1;
+  if (buf_ensure(e->pcell, RC * sizeof(int32_t), s)) return -1;
+  if (buf_ensure(e->pent, RC * sizeof(int32_t), s)) return -1;
+  if (buf_ensure(e->pcn, RC * sizeof(int32_t), s)) return -1;
+  if (buf_ensure(e->ptoff, RC * sizeof(int64_t), s)) return -1;
+  int bsh = 0, bnd = 0, NB = 0;
+  const bool buckets = !e->radix_cells && bucket_geometry(e->net.n_marks, &bsh, &bnd, &NB) == 0;
+  int64_t H = 0, T = 0;
+  if (buckets) {
+    // spatial buckets, every count on the device (bucket.hip)
+    if (buf_ensure(e->bk[0], NB * sizeof(int32_t), s)) return -1;        // counts
+    if (buf_ensure(e->bk[1], NB * sizeof(int32_t), s)) return -1;        // cursors
+    if (buf_ensure(e->bk[2], (NB + 1) * sizeof(int64_t), s)) return -1;  // bases
+    if (buf_ensure(e->bk[3], NB * sizeof(int32_t), s)) return -1;        // pair cells
+    if (buf_ensure(e->bk[4], NB * sizeof(int64_t), s)) return -1;        // pairs
+    if (buf_ensure(e->bk[5], (NB + 1) * sizeof(int64_t), s)) return -1;  // pair-cell offsets
+    if (buf_ensure(e->bk[6], (NB + 1) * sizeof(int64_t), s)) return -1;  // pair offsets
+    if (buf_ensure(e->bk[7], (M / 2048 + 2) * sizeof(int64_t), s)) return -1;  // block parts
+    for (int k = 8; k < 11; ++k)
+      if (buf_ensure(e->bk[k], RC * sizeof(int32_t), s)) return -1;  // per-bucket pair-cell areas
+    if (buf_ensure(e->bk[11], RC * sizeof(int64_t), s)) return -1;
+    if (buf_ensure(e->sents, TB * sizeof(uint64_t), s)) return -1;
+    TIMED("bucket_entries", 24.0 * M,
+          launch_bucket_entries(P<int32_t>(e->members), M, grid, zero, idx, e->net.n_marks,
+                                P<int32_t>(e->bk[0]), P<int32_t>(e->bk[1]), P<int64_t>(e->bk[2]),
+                                P<int64_t>(e->bk[7]), P<uint64_t>(e->sents), ctr, s));
+    TIMED("bucket_group", 0.0,
+          launch_bucket_pairs(e->net.n_marks, P<int64_t>(e->bk[2]), P<uint64_t>(e->sents),
+                              P<uint64_t>(c.pz), P<CellEnt>(e->ents),
+                              P<int32_t>(e->bk[8]), P<int32_t>(e->bk[9]), P<int32_t>(e->bk[10]),
+                              P<int64_t>(e->bk[11]), P<int32_t>(e->bk[3]), P<int64_t>(e->bk[4]),
+                              P<int64_t>(e->bk[5]), P<int64_t>(e->bk[6]), P<int32_t>(e->pcell),
+                              P<int32_t>(e->pent), P<int32_t>(e->pcn), P<int64_t>(e->ptoff), ctr, s));
+  } else {
+    // radix-sort path (grids finer than the bucket geometry, TNP_RADIX_CELLS=1)
+    if (buf_ensure(e->spcnt, std::max<int64_t>(M, 1) * sizeof(int32_t), s)) return -1;
+    if (buf_ensure(e->spoff, std::max<int64_t>(M, 1) * sizeof(int64_t), s)) return -1;
+    if (buf_ensure(e->part, (int64_t)(tnp_grid(M) + 1) * sizeof(int64_t), s)) return -1;
+    TIMED("span_count", 28.0 * M,
+          launch_span_count(P<int32_t>(e->members), S, M, grid, zero, idx, P<int32_t>(e->spcnt),
+                            P<int64_t>(e->part), ctr, s));
+    if (scan_counts(e, P<int32_t>(e->spcnt), P<int64_t>(e->spoff), M, CTR_T, s)) return -1;
+    if (buf_ensure(e->ekey_a, TB * sizeof(uint32_t), s)) return -1;
+    if (buf_ensure(e->ent_v, TB * sizeof(int32_t), s)) return -1;
+    if (buf_ensure(e->ekey_b, TB * sizeof(uint32_t), s)) return -1;
+    if (buf_ensure(e->eval_b, TB * sizeof(int32_t), s)) return -1;
+    TIMED("span_emit", 28.0 * M,
+          launch_span_emit(P<int32_t>(e->members), S, M, grid, NC, P<int64_t>(e->spoff),
+                           P<uint32_t>(e->ekey_a), P<int32_t>(e->ent_v), ctr, s));
+    if (read_ctr(e, s)) return -1;
+    if (e->h_ctr[CTR_K0]) {
+      // the reference builds torch.cartesian_prod() of zero tensors (subpoly.py:317)
+      tnp_set_error("meshgrid expects a non-empty TensorList (a region row without zeros, plane %d)", idx);
+      return -1;
     }
+    H = e->h_ctr[CTR_H];
+    T = e->h_ctr[CTR_T];
+    const int64_t T1 = std::max<int64_t>(T, 1);
+    ktimer_set_bytes(e, 20.0 * M + 8.0 * T);  // span_emit's bytes, known only now
+    int cbits = 1;
+    while (cbits < 32 && (1ll << cbits) < ncell) ++cbits;
+    uint32_t* skey = nullptr;
+    int32_t* sval = nullptr;
+    {
+      size_t need = sort_pairs_scratch_bytes(T, cbits);
+      if (buf_ensure(e->sort_scr2, std::max<size_t>(need, 16), s)) return -1;
+      TIMED("cell_sort", 16.0 * T * ((cbits + 7) / 8),
+            sort_pairs_u32(P<uint32_t>(e->ekey_a), P<uint32_t>(e->ekey_b), P<int32_t>(e->ent_v),
+                           P<int32_t>(e->eval_b), T, cbits, e->sort_scr2.p, e->sort_scr2.bytes, &skey,
+                           &sval, s));
+    }
+    // cells holding member pairs straight from the runs of the sorted keys
+    // (compacted, with their flattened pair space offsets; total = tests)
+    {
+      if (buf_ensure(e->rstart, (T1 + 1) * sizeof(int32_t), s)) return -1;
+      if (T > 0) {
+        TnpLB la, lr, lp;
+        if (lb_begin(e, split_tiles(T), s, &la, 0)) return -1;
+        TIMED("run_starts", 8.0 * T,
+              launch_run_starts(skey, T, P<int32_t>(e->rstart), ctr, la, s));
+        const int64_t pt = pair_run_tiles(T);
+        if (lb_begin(e, pt, s, &lr, 0) || lb_begin(e, pt, s, &lp, 1)) return -1;
+        TIMED("pair_cells", 0.0,
+              launch_pair_runs(skey, P<int32_t>(e->rstart), T, P<int32_t>(e->pcell), P<int32_t>(e->pent),
+                               P<int32_t>(e->pcn), P<int64_t>(e->ptoff), ctr, lr, lp, s));
+      }
+    }
+    TIMED("entry_keys", 52.0 * T,
+          launch_entry_keys(sval, skey, NC, T, grid, P<uint64_t>(c.pz), P<CellEnt>(e->ents), s));
   }
-  if (buf_ensure(e->ents, T1 * sizeof(CellEnt), s)) return -1;
-  TIMED("entry_keys", 52.0 * T,
-        launch_entry_keys(sval, T, grid, P<uint64_t>(c.pz), P<CellEnt>(e->ents), s));
-
   // 4. connecting edges: test every in-cell member pair once, append the
   //    emitted ones, radix-sort them (lexicographic c_new, subpoly.py:243-244).
   //    The pair count stays on the device; the chunk table and the key buffer
@@ -924,7 +959,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     if (!chunks_ok) {
       if (buf_ensure(e->bcell, bcap * sizeof(int32_t), s)) return -1;
       if (attempt > 0) TNP_CHECK(hipMemsetAsync(ctr + CTR_BOVF, 0, sizeof(int64_t), s));
-      if (launch_chunk_cells(P<int64_t>(e->ptoff), P<int32_t>(e->pcn), T1 / 2 + 1,
+      if (launch_chunk_cells(P<int64_t>(e->ptoff), P<int32_t>(e->pcn), RC,
                              P<int32_t>(e->bcell), bcap, ctr, s)) return -1;
     }
     if (buf_ensure(e->ckeys_a, std::max<int64_t>(cap, 1) * sizeof(uint64_t), s)) return -1;
@@ -939,6 +974,16 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
                          P<CellEnt>(e->ents), idx, nb, cfmask, P<uint64_t>(e->ckeys_a), cap, ctr,
                          P<int64_t>(e->bstat), s));
     if (read_ctr(e, s)) return -1;
+    if (buckets) {
+      if (e->h_ctr[CTR_K0]) {
+        // the reference builds torch.cartesian_prod() of zero tensors (subpoly.py:317)
+        tnp_set_error("meshgrid expects a non-empty TensorList (a region row without zeros, plane %d)",
+                      idx);
+        return -1;
+      }
+      H = e->h_ctr[CTR_H];
+      T = e->h_ctr[CTR_T];
+    }
     TT = e->h_ctr[CTR_TESTS];
     X = e->h_ctr[CTR_XK];
     ktimer_set_bytes(e, 32.0 * TT + 8.0 * T);  // known only now
@@ -1039,6 +1084,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     st->override_applied = override_ < 0 ? (e->h_ctr[CTR_FAIL] != 0) : override_;
     st->next_active = (uint64_t)e->h_ctr[CTR_ACTIVE];
     st->S_dup = e->pend_dup;
+    st->T = T;
   }
   return 0;
 }

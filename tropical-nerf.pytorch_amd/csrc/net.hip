@@ -104,7 +104,9 @@ k_forward_new(NetDev net, const float* xyz, int64_t n, float* __restrict__ pre,
   __shared__ float w[NW];
   for (int i = threadIdx.x; i < NW; i += blockDim.x) w[i] = net.weights[i];
   __syncthreads();
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // XCD-contiguous chunks of the (edge-ordered, spatially coherent) splits:
+  // the hash-table lines one XCD's splits touch then mostly fit its L2
+  const int64_t i = tnp::xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   const bool live = i < n;
   const float eps = net.eps;
   float x[3] = {0.f, 0.f, 0.f};

@@ -90,15 +90,33 @@ int launch_pair_runs(const uint32_t* key, const int32_t* rstart, int64_t T, int3
                      int32_t* pent, int32_t* pn, int64_t* ptoff, int64_t* ctr, const TnpLB& lb_rank,
                      const TnpLB& lb_pairs, hipStream_t s);
 int64_t pair_run_tiles(int64_t T);
-// one cell entry as the pair test reads it: the member's three packed keys
-// and id in one 32-byte record (one cache segment per entry)
+// one cell entry as the pair test reads it: the member's sign keys, its id
+// and its grid relation to THIS cell in 6 bits (cell_flags): bit d = the
+// member's lowest spanned cell along axis d is this cell, bit 3 + d = the
+// member lies on a mark plane of axis d.  One 32-byte record per entry.
 struct alignas(32) CellEnt {
-  uint64_t g, p, z;
-  int32_t v, pad;
+  uint64_t p, z;
+  int32_t v;
+  uint32_t f;
+  uint64_t pad;
 };
+// cell_flags of a member (grid word g) in the cell with coordinates c (+2)
+__device__ __forceinline__ uint32_t cell_flags(uint64_t g, int cx, int cy, int cz) {
+  const int c[3] = {cx, cy, cz};
+  uint32_t f = 0;
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    const int o = tnp::grid_off(g, d);
+    const bool zd = tnp::grid_zero(g, d);
+    const int lo = (zd ? o - 1 : o) + 2;
+    f |= (uint32_t)(lo == c[d]) << d;
+    f |= (uint32_t)zd << (3 + d);
+  }
+  return f;
+}
 // pz: the interleaved (pos, zero) copy of the vertex keys
-int launch_entry_keys(const int32_t* ent_v, int64_t T, const uint64_t* grid, const uint64_t* pz,
-                      CellEnt* ent, hipStream_t s);
+int launch_entry_keys(const int32_t* ent_v, const uint32_t* ekey, int NC, int64_t T,
+                      const uint64_t* grid, const uint64_t* pz, CellEnt* ent, hipStream_t s);
 
 // connecting edges over the flattened pair space (pair cells in order, then
 // (i, j<i) inside a cell); the pair count and R are read on the device.
@@ -129,6 +147,30 @@ int launch_count_flags(const uint8_t* f, int64_t n, int64_t* ctr, int slot, hipS
 int launch_widen_flags(const uint8_t* f, int64_t n, int32_t* out, hipStream_t s);
 // planes the pruning of step idx compares (idx .. last_plane)
 uint64_t prune_mask(int idx, int last_plane);
+// ---- bucket.hip: members grouped by grid cell in spatial buckets ----------
+constexpr int BUCKET_MAX = 4913;        // buckets (17^3)
+constexpr int BUCKET_LOCAL_MAX = 4096;  // cells per bucket (16^3)
+// bucket edge 2^sh cells, NBd buckets per axis, NB in total; -1: the grid is
+// too fine for the bucket path (the radix-sort path takes it)
+int bucket_geometry(int n_marks, int* sh, int* NBd, int* NB);
+// members -> (local cell, vertex) entries in bucket ranges; A -> ctr[CTR_A],
+// T -> ctr[CTR_T], k=0 rows -> ctr[CTR_K0].  bcount/bcur: NB int32,
+// bbase: NB + 1, part: ceil(M / 2048) + 1 int64; ekey/ev: 8 M capacity
+// ekv: the entries in bucket order, packed (local cell << 40 | cell flags
+// << 32 | vertex) (8 M capacity)
+int launch_bucket_entries(const int32_t* members, int64_t M, const uint64_t* grid, const uint64_t* zero,
+                          int idx, int n_marks, int32_t* bcount, int32_t* bcur, int64_t* bbase,
+                          int64_t* part, uint64_t* ekv, int64_t* ctr, hipStream_t s);
+// per bucket: cell-contiguous CellEnt records (ents, entry positions), the
+// pair cells; then the global pair-cell list (pcell, pent, pn, ptoff; R ->
+// ctr[CTR_R], pairs -> ctr[CTR_TESTS]) that launch_connect walks.
+// lcell/lent/ln/lpoff: 4 M + 1 capacity; bnpc/bnpairs: NB; pcoff/pairoff: NB + 1
+int launch_bucket_pairs(int n_marks, const int64_t* bbase, const uint64_t* ekv, const uint64_t* pz,
+                        CellEnt* ents, int32_t* lcell,
+                        int32_t* lent, int32_t* ln, int64_t* lpoff, int32_t* bnpc, int64_t* bnpairs,
+                        int64_t* pcoff, int64_t* pairoff, int32_t* pcell, int32_t* pent, int32_t* pn,
+                        int64_t* ptoff, int64_t* ctr, hipStream_t s);
+
 // ---- sort.hip ----
 // ascending LSD radix sort of n u64 keys on bits [0, bits); the sorted keys
 // end in *out (== a or b)

@@ -441,20 +441,21 @@ k_pair_runs_lb(const uint32_t* __restrict__ key, const int32_t* __restrict__ rst
   }
 }
 
-// entry-aligned copies of the members' packed keys (read contiguously per
-// cell by the pair test)
-__global__ void k_entry_keys(const int32_t* __restrict__ ent_v, int64_t T,
-                             const uint64_t* __restrict__ grid, const ulonglong2* __restrict__ pz,
-                             CellEnt* __restrict__ ent) {
+// entry-aligned records of the cell-sorted (cell, member) entries (radix
+// path): the member's keys and its cell flags in that cell
+__global__ void k_entry_keys(const int32_t* __restrict__ ent_v, const uint32_t* __restrict__ ekey, int NC,
+                             int64_t T, const uint64_t* __restrict__ grid,
+                             const ulonglong2* __restrict__ pz, CellEnt* __restrict__ ent) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= T) return;
   const int v = ent_v[i];
+  const uint32_t c = ekey[i];
   const ulonglong2 k = pz[v];  // pos and zero in one 16-byte gather
   CellEnt r;
-  r.g = grid[v];
   r.p = k.x;
   r.z = k.y;
   r.v = v;
+  r.f = cell_flags(grid[v], (int)(c / ((uint32_t)NC * NC)), (int)((c / NC) % NC), (int)(c % NC));
   r.pad = 0;
   ent[i] = r;
 }
@@ -462,11 +463,15 @@ __global__ void k_entry_keys(const int32_t* __restrict__ ent_v, int64_t T,
 // ---------------------------------------------------------------------------
 // connecting-edge pair test (subpoly.py:484-535 in closed form).
 // Two members share an augmented region iff, per coordinate, their augmented
-// value sets intersect: grid dim d -> [lo, off] intervals overlap; plane
+// value sets intersect: grid dim d -> their cell spans overlap; plane
 // j < idx -> not (both non-zero with opposite signs).  The reference keeps
-// the pair iff they share >= 1 zero plane (grid zeros only with equal
-// offsets).  Each pair is emitted once, in the canonical cell
-// (per-dim max of the two interval lows).
+// the pair iff they share >= 1 zero plane (grid zeros only on the SAME mark
+// plane).  Each pair is emitted once, in the canonical cell (per-dim max of
+// the two span lows).  In terms of the entries' cell flags (CellEnt::f) for
+// the cell under test, which both spans contain:
+//   canonical       <=> per axis, one of the two spans starts here
+//   same mark plane <=> both on a plane of the axis and both spans start here
+// and the shared regions double per same-plane axis and per common zero plane.
 // ---------------------------------------------------------------------------
 struct PairTest {
   bool emit;
@@ -474,27 +479,17 @@ struct PairTest {
   int64_t regions;  // shared regions (for the reference's candidate count P)
 };
 
-__device__ __forceinline__ PairTest pair_test(const int cc[3], uint64_t below, uint64_t gu,
-                                              uint64_t pu, uint64_t zu, uint64_t gv, uint64_t pv,
-                                              uint64_t zv) {
+__device__ __forceinline__ PairTest pair_test(uint64_t below, uint32_t fu, uint64_t pu, uint64_t zu,
+                                              uint32_t fv, uint64_t pv, uint64_t zv) {
   PairTest t{false, false, 0};
-  int64_t reg = 1;
-  bool grid_share = false;
-#pragma unroll
-  for (int d = 0; d < 3; ++d) {
-    int ou = tnp::grid_off(gu, d), ov = tnp::grid_off(gv, d);
-    bool zdu = tnp::grid_zero(gu, d), zdv = tnp::grid_zero(gv, d);
-    int lu = zdu ? ou - 1 : ou, lv = zdv ? ov - 1 : ov;
-    int lo = lu > lv ? lu : lv;
-    int hi = ou < ov ? ou : ov;
-    if (cc[d] != lo) return t;  // not the canonical cell (or no overlap)
-    reg *= (hi - lo + 1);
-    grid_share |= zdu && zdv && (ou == ov);
-  }
+  if (((fu | fv) & 7u) != 7u) return t;  // not the canonical cell
   if (((pu ^ pv) & ~zu & ~zv & below) != 0) return t;
+  const uint32_t a = fu & fv;
+  const uint32_t sp = a & (a >> 3) & 7u;  // axes where both lie on the same mark plane
+  const uint64_t zz = zu & zv & below;
   t.compat = true;
-  t.regions = reg << __popcll(zu & zv & below);
-  t.emit = grid_share || ((zu & zv & below) != 0);
+  t.regions = (int64_t)1 << (__popc(sp) + __popcll(zz));
+  t.emit = sp != 0 || zz != 0;
   return t;
 }
 
@@ -580,7 +575,6 @@ k_connect(const int64_t* __restrict__ ptoff, const int32_t* __restrict__ pcell,
   __shared__ int32_t s_off[CONNECT_CELLS];  // first pair of the cell - chunk start
   __shared__ int32_t s_n[CONNECT_CELLS];
   __shared__ int32_t s_ent[CONNECT_CELLS];  // first entry of the cell
-  __shared__ int32_t s_cc[CONNECT_CELLS];   // cell coordinates + 2, 10 bits each
   const int64_t TT = ctr[CTR_TESTS];
   const int64_t R = ctr[CTR_R];
   if (TT > max_tests || ctr[CTR_BOVF] || ctr[CTR_BIG]) return;
@@ -594,12 +588,9 @@ k_connect(const int64_t* __restrict__ ptoff, const int32_t* __restrict__ pcell,
   const int nr = (int)(r_end - r0);  // <= CCH + 1: every pair cell holds >= 1 pair
   __syncthreads();  // the previous chunk is done with the cell window
   for (int t = threadIdx.x; t < nr; t += blockDim.x) {
-    const int c = pcell[r0 + t];
     s_off[t] = (int32_t)(ptoff[r0 + t] - pb);  // > -2^31: a cell holds < 2^31 pairs
     s_n[t] = pn[r0 + t];
     s_ent[t] = pent[r0 + t];
-    const int cz = c % NC, cy = (c / NC) % NC, cx = c / (NC * NC);  // = cell_coords + 2
-    s_cc[t] = cx | (cy << 10) | (cz << 20);
   }
   __syncthreads();
   const int64_t pw = pb + (int64_t)tnp::wave() * 64 * CIPT + tnp::lane();
@@ -626,11 +617,9 @@ k_connect(const int64_t* __restrict__ ptoff, const int32_t* __restrict__ pcell,
       int i, j;
       pair_row(x - s_off[lc], i, j);
       const int64_t base = s_ent[lc];
-      const int pc = s_cc[lc];
-      const int cc[3] = {(pc & 1023) - 2, ((pc >> 10) & 1023) - 2, ((pc >> 20) & 1023) - 2};
       const CellEnt eu = ent[base + i];
       const CellEnt ev = ent[base + j];
-      PairTest t = pair_test(cc, below, eu.g, eu.p, eu.z, ev.g, ev.p, ev.z);
+      PairTest t = pair_test(below, eu.f, eu.p, eu.z, ev.f, ev.p, ev.z);
       if (t.compat) {
         n_compat++;
         n_reg += t.regions;
@@ -650,7 +639,7 @@ k_connect(const int64_t* __restrict__ ptoff, const int32_t* __restrict__ pcell,
   // test -- CB loads in flight per lane instead of one dependent pair
 #pragma unroll
   for (int k0 = 0; k0 < CIPT; k0 += CONNECT_CB) {
-    int iu[CONNECT_CB], iv[CONNECT_CB], pcs[CONNECT_CB];
+    int iu[CONNECT_CB], iv[CONNECT_CB];
     bool ok[CONNECT_CB];
 #pragma unroll
     for (int kb = 0; kb < CONNECT_CB; ++kb) {
@@ -665,33 +654,31 @@ k_connect(const int64_t* __restrict__ ptoff, const int32_t* __restrict__ pcell,
       const int base = s_ent[lc];
       iu[kb] = base + i;
       iv[kb] = base + j;
-      pcs[kb] = s_cc[lc];
     }
     ulonglong2 ua[CONNECT_CB], va[CONNECT_CB];
-    uint64_t zua[CONNECT_CB], zva[CONNECT_CB];
+    uint2 fua[CONNECT_CB], fva[CONNECT_CB];
     const ulonglong2* er = reinterpret_cast<const ulonglong2*>(ent);
+    const uint2* ef = reinterpret_cast<const uint2*>(ent);
 #pragma unroll
     for (int kb = 0; kb < CONNECT_CB; ++kb) {
-      ua[kb] = er[2 * (int64_t)iu[kb]];  // (g, p)
-      zua[kb] = ent[iu[kb]].z;
+      ua[kb] = er[2 * (int64_t)iu[kb]];  // (p, z)
+      fua[kb] = ef[4 * (int64_t)iu[kb] + 2];  // (v, f)
       va[kb] = er[2 * (int64_t)iv[kb]];
-      zva[kb] = ent[iv[kb]].z;
+      fva[kb] = ef[4 * (int64_t)iv[kb] + 2];
     }
 #pragma unroll
     for (int kb = 0; kb < CONNECT_CB; ++kb) {
       if (!ok[kb]) continue;
-      const int pc = pcs[kb];
-      const int cc[3] = {(pc & 1023) - 2, ((pc >> 10) & 1023) - 2, ((pc >> 20) & 1023) - 2};
-      const uint64_t gu = ua[kb].x, pu = ua[kb].y, zu = zua[kb];
-      const uint64_t gv = va[kb].x, pv = va[kb].y, zv = zva[kb];
-      PairTest t = pair_test(cc, below, gu, pu, zu, gv, pv, zv);
+      const uint64_t pu = ua[kb].x, zu = ua[kb].y;
+      const uint64_t pv = va[kb].x, zv = va[kb].y;
+      PairTest t = pair_test(below, fua[kb].y, pu, zu, fva[kb].y, pv, zv);
       if (t.compat) {
         n_compat++;
         n_reg += t.regions;
         n_conn += t.emit;
         // the step's pruning drops it anyway (keep_edge): never appended
         if (t.emit && (fmask == 0 || (((pu ^ pv) | (zu ^ zv)) & fmask) != 0)) {
-          const uint32_t vu = (uint32_t)ent[iu[kb]].v, vv = (uint32_t)ent[iv[kb]].v;
+          const uint32_t vu = fua[kb].x, vv = fva[kb].x;
           const uint32_t lo = vu < vv ? vu : vv, hi = vu < vv ? vv : vu;
           kk[ne++] = ((uint64_t)lo << nb) | hi;
         }
@@ -1136,10 +1123,10 @@ int launch_pair_runs(const uint32_t* key, const int32_t* rstart, int64_t T, int3
   TNP_CHECK(hipGetLastError());
   return 0;
 }
-int launch_entry_keys(const int32_t* ent_v, int64_t T, const uint64_t* grid, const uint64_t* pz,
-                      CellEnt* ent, hipStream_t s) {
+int launch_entry_keys(const int32_t* ent_v, const uint32_t* ekey, int NC, int64_t T,
+                      const uint64_t* grid, const uint64_t* pz, CellEnt* ent, hipStream_t s) {
   if (T <= 0) return 0;
-  hipLaunchKernelGGL(k_entry_keys, dim3(tnp_grid(T)), dim3(TNP_BLOCK), 0, s, ent_v, T, grid,
+  hipLaunchKernelGGL(k_entry_keys, dim3(tnp_grid(T)), dim3(TNP_BLOCK), 0, s, ent_v, ekey, NC, T, grid,
                      reinterpret_cast<const ulonglong2*>(pz), ent);
   TNP_CHECK(hipGetLastError());
   return 0;

@@ -37,6 +37,7 @@ class TnpStepStats(C.Structure):
         ("X", C.c_int64), ("V_out", C.c_int64), ("E_out", C.c_int64),
         ("A", C.c_int64), ("P", C.c_int64), ("pair_tests", C.c_int64),
         ("override_applied", C.c_int32), ("next_active", C.c_uint64), ("S_dup", C.c_int64),
+        ("T", C.c_int64),
     ]
 
     def as_dict(self):
