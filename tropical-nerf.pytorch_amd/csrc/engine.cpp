@@ -133,8 +133,9 @@ struct tnp_engine {
   bool has_net = false;
   VSet cur, alt;
   Buf edges, edges_alt;
-  // per-edge key masks (step.hip k_prune_lb): dm = endpoint keys differ,
-  // sm = planes that split the edge; valid when masks_valid
+  // per-edge key masks (step.hip k_prune_lb): dm = 1 + the highest plane on
+  // which the endpoint keys differ (uint8), sm = planes that split the edge
+  // (uint64); valid when masks_valid
   Buf edm, esm, edm_alt, esm_alt;
   bool masks_valid = false;
   int64_t V = 0, E = 0;
@@ -298,10 +299,10 @@ static int reset_live(tnp_engine* e, hipStream_t s, bool edges_changed = true) {
 static int ensure_masks(tnp_engine* e, hipStream_t s) {
   if (e->masks_valid) return 0;
   const int64_t E1 = std::max<int64_t>(e->E, 1);
-  if (buf_ensure(e->edm, E1 * sizeof(uint64_t), s)) return -1;
+  if (buf_ensure(e->edm, E1 * sizeof(uint8_t), s)) return -1;
   if (buf_ensure(e->esm, E1 * sizeof(uint64_t), s)) return -1;
   TIMED("edge_masks", 40.0 * e->E,
-        launch_edge_masks(P<int32_t>(e->edges), e->E, P<uint64_t>(e->cur.pz), P<uint64_t>(e->edm),
+        launch_edge_masks(P<int32_t>(e->edges), e->E, P<uint64_t>(e->cur.pz), P<uint8_t>(e->edm),
                           P<uint64_t>(e->esm), 0, 63, nullptr, s));
   e->masks_valid = true;
   return 0;
@@ -528,9 +529,9 @@ extern "C" int tnp_engine_active_planes(tnp_engine* e, int from, uint64_t* mask,
   // the per-edge masks are (re)computed here and the OR of their split planes
   // taken in the same pass
   const int64_t E1 = std::max<int64_t>(e->E, 1);
-  if (buf_ensure(e->edm, E1 * sizeof(uint64_t), s)) return -1;
+  if (buf_ensure(e->edm, E1 * sizeof(uint8_t), s)) return -1;
   if (buf_ensure(e->esm, E1 * sizeof(uint64_t), s)) return -1;
-  if (launch_edge_masks(P<int32_t>(e->edges), e->E, P<uint64_t>(e->cur.pz), P<uint64_t>(e->edm),
+  if (launch_edge_masks(P<int32_t>(e->edges), e->E, P<uint64_t>(e->cur.pz), P<uint8_t>(e->edm),
                         P<uint64_t>(e->esm), from, e->K - 1, P<int64_t>(e->ctr), s))
     return -1;
   e->masks_valid = true;
@@ -718,7 +719,7 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
     TnpLB lb;
     if (lb_begin(e, split_tiles(e->E), s, &lb)) return -1;
     TIMED("split", 8.0 * e->E,
-          launch_split_lb(P<int32_t>(e->edges), e->E, P<uint64_t>(e->esm), P<uint64_t>(e->edm), idx,
+          launch_split_lb(P<int32_t>(e->edges), e->E, P<uint64_t>(e->esm), P<uint8_t>(e->edm), idx,
                           e->V, P<int32_t>(e->sa), P<int32_t>(e->sb), P<int64_t>(e->ctr),
                           e->curve ? P<int32_t>(e->cv[CV_EIDX]) : nullptr, lb, s));
     if (!e->curve && e->V > 0) {
@@ -1037,14 +1038,14 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     TNP_CHECK(hipMemsetAsync(e->live.p, 0, NV, s));
     if (ensure_masks(e, s)) return -1;  // (curve path: recomputed after the rewiring)
     const int64_t N1 = std::max<int64_t>(N, 1);
-    if (buf_ensure(e->edm_alt, N1 * sizeof(uint64_t), s)) return -1;
+    if (buf_ensure(e->edm_alt, N1 * sizeof(uint8_t), s)) return -1;
     if (buf_ensure(e->esm_alt, N1 * sizeof(uint64_t), s)) return -1;
     TnpLB lb;
     if (lb_begin(e, lb_tiles(N), s, &lb)) return -1;
     TIMED("prune", 24.0 * E + 48.0 * (S + X),
           launch_prune_lb(eg, E, P<int32_t>(e->sb), S, V, e->ckeys, nb, X, idx, K - 1,
-                          P<uint64_t>(c.pz), P<uint64_t>(e->edm), P<uint64_t>(e->esm),
-                          P<int32_t>(e->edges_alt), P<uint64_t>(e->edm_alt), P<uint64_t>(e->esm_alt),
+                          P<uint64_t>(c.pz), P<uint8_t>(e->edm), P<uint64_t>(e->esm),
+                          P<int32_t>(e->edges_alt), P<uint8_t>(e->edm_alt), P<uint64_t>(e->esm_alt),
                           P<uint8_t>(e->live), ctr, lb, s));
     std::swap(e->edm, e->edm_alt);
     std::swap(e->esm, e->esm_alt);

@@ -93,7 +93,7 @@ k_forward(NetDev net, const float* __restrict__ xyz, int64_t n, float* __restric
 // ctr[CTR_FAIL]; shared[r] keeps the plane set for k_override_new.  Values
 // and the MKL row-count schedule are those of k_forward (same n = S).
 template <int LV, int H, int NL>
-__global__ void __launch_bounds__(TNP_BLOCK, 5)
+__global__ void __launch_bounds__(TNP_BLOCK, 4)
 k_forward_new(NetDev net, const float* xyz, int64_t n, float* __restrict__ pre,
               int64_t ld, int64_t V, int keep_from, const int32_t* __restrict__ sa,
               const int32_t* __restrict__ sb, int idx, int own_lo, int own_hi, uint64_t* pos,

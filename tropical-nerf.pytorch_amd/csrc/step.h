@@ -42,12 +42,13 @@ int64_t split_tiles(int64_t n);  // tiles of the single-pass split and hit passe
 // edges' split masks (bit idx): S -> ctr[CTR_S]; sa/sb (and eidx if given)
 // need capacity E; without eidx the split edges are rewired in place and
 // their masks marked stale
-int launch_split_lb(int32_t* edges, int64_t E, const uint64_t* sm, uint64_t* dm, int idx, int64_t V,
+int launch_split_lb(int32_t* edges, int64_t E, const uint64_t* sm, uint8_t* dm, int idx, int64_t V,
                     int32_t* sa, int32_t* sb, int64_t* ctr, int32_t* eidx, const TnpLB& lb,
                     hipStream_t s);
-// per-edge masks from the endpoint keys (pz): dm = keys differ, sm = split
-// planes; ctr != null: OR of sm over planes [from, last_plane] -> CTR_ACTIVE
-int launch_edge_masks(const int32_t* edges, int64_t E, const uint64_t* pz, uint64_t* dm,
+// per-edge masks from the endpoint keys (pz): dm = 1 + highest plane where
+// the keys differ (0: none), sm = split planes; ctr != null: OR of sm over
+// planes [from, last_plane] -> CTR_ACTIVE
+int launch_edge_masks(const int32_t* edges, int64_t E, const uint64_t* pz, uint8_t* dm,
                       uint64_t* sm, int from, int last_plane, int64_t* ctr, hipStream_t s);
 int launch_new_vertices(const int32_t* sa, const int32_t* sb, int64_t S, const float* col,
                         float eps, float* xyz, int64_t V, hipStream_t s);
@@ -139,8 +140,8 @@ int launch_connect(const int64_t* ptoff, const int32_t* pcell, const int32_t* pn
 // caller), ctr[CTR_E], ctr[CTR_ACTIVE]
 int launch_prune_lb(const int32_t* edges, int64_t E, const int32_t* sb, int64_t S, int64_t V,
                     const uint64_t* ckeys, int nb, int64_t X, int idx, int last_plane,
-                    const uint64_t* pz, const uint64_t* dm, const uint64_t* sm, int32_t* out,
-                    uint64_t* odm, uint64_t* osm, uint8_t* used, int64_t* ctr, const TnpLB& lb,
+                    const uint64_t* pz, const uint8_t* dm, const uint64_t* sm, int32_t* out,
+                    uint8_t* odm, uint64_t* osm, uint8_t* used, int64_t* ctr, const TnpLB& lb,
                     hipStream_t s);
 // ctr[slot] += number of set byte flags in f[0, n) (16-B aligned f, 0/1 bytes)
 int launch_count_flags(const uint8_t* f, int64_t n, int64_t* ctr, int slot, hipStream_t s);

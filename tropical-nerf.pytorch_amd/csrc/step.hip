@@ -26,7 +26,12 @@
 
 namespace {
 
-constexpr uint64_t EDGE_STALE = ~0ull;  // edge masks to recompute (K <= 63: never a real mask)
+// per-edge high plane h = 1 + the highest plane on which the endpoint keys
+// differ (0: equal keys); the pruning of step idx keeps an edge iff h > idx
+constexpr uint8_t EDGE_STALE = 0xFF;  // rewired edge: recompute from the endpoint keys
+__device__ __forceinline__ uint8_t high_plane(uint64_t dm) {
+  return (uint8_t)(dm ? 64 - __clzll(dm) : 0);
+}
 constexpr int IPT = 8;                  // items per thread per tile
 constexpr int TILE = TNP_BLOCK * IPT;   // tile of a compaction pass
 // single-pass (look-back) compactions: items per thread of the split / hit
@@ -54,7 +59,7 @@ __device__ __forceinline__ bool split_test(const float* __restrict__ col, const 
 // of a bounds branch serialising every item.
 __global__ void __launch_bounds__(TNP_BLOCK)
 k_split_lb(int32_t* __restrict__ edges, int64_t E, int64_t ntiles, const uint64_t* __restrict__ sm,
-           uint64_t* __restrict__ dm, int idx, int64_t V, int32_t* __restrict__ sa,
+           uint8_t* __restrict__ dm, int idx, int64_t V, int32_t* __restrict__ sa,
            int32_t* __restrict__ sb, int64_t* __restrict__ ctr, int32_t* __restrict__ eidx, TnpLB lb) {
   __shared__ int cnt[SIPT][TNP_WAVES];
   __shared__ int64_t slot;
@@ -812,9 +817,9 @@ k_prune_emit(EdgeSrc src, int64_t N, uint64_t fmask, uint64_t amask,
 // reads them coalesced for the old edges and gathers the endpoint keys only
 // for rewired (dm == EDGE_STALE), e_new and c_new edges.
 __global__ void __launch_bounds__(TNP_BLOCK, 4)
-k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, uint64_t fmask, uint64_t amask,
-           const ulonglong2* __restrict__ pz, const uint64_t* __restrict__ dm,
-           const uint64_t* __restrict__ sm, int32_t* __restrict__ out, uint64_t* __restrict__ odm,
+k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, int idx, uint64_t amask,
+           const ulonglong2* __restrict__ pz, const uint8_t* __restrict__ dm,
+           const uint64_t* __restrict__ sm, int32_t* __restrict__ out, uint8_t* __restrict__ odm,
            uint64_t* __restrict__ osm, uint8_t* __restrict__ used, int64_t* __restrict__ ctr,
            TnpLB lb) {
   __shared__ int cnt[LIPT][TNP_WAVES];
@@ -828,7 +833,8 @@ k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, uint64_t fmask, uint64_t amas
   const int64_t ES = src.E + src.S;
   const int kind = last < src.E ? 0 : (base >= src.E && last < ES) ? 1 : (base >= ES ? 2 : 3);
   int a[LIPT], b[LIPT];
-  uint64_t d[LIPT], m[LIPT];
+  uint32_t d[LIPT];
+  uint64_t m[LIPT];
   if (kind == 0) {
     const int2* e2 = reinterpret_cast<const int2*>(src.edges);
 #pragma unroll
@@ -877,7 +883,7 @@ k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, uint64_t fmask, uint64_t amas
   for (int k = 0; k < LIPT; ++k) {
     if (d[k] == EDGE_STALE) {  // new or rewired edge: masks from the endpoint keys
       const ulonglong2 ka = pz[a[k]], kb = pz[b[k]];
-      d[k] = (ka.x ^ kb.x) | (ka.y ^ kb.y);
+      d[k] = high_plane((ka.x ^ kb.x) | (ka.y ^ kb.y));
       m[k] = (ka.x ^ kb.x) & ~ka.y & ~kb.y;
     }
   }
@@ -886,7 +892,7 @@ k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, uint64_t fmask, uint64_t amas
 #pragma unroll
   for (int k = 0; k < LIPT; ++k) {
     const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
-    const bool f = (i <= last) && ((d[k] & fmask) != 0);
+    const bool f = (i <= last) && ((int)d[k] > idx);
     if (f) act |= m[k] & amask;
     bal[k] = __ballot(f);
     if (tnp::lane() == 0) cnt[k][tnp::wave()] = __popcll(bal[k]);
@@ -912,7 +918,7 @@ k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, uint64_t fmask, uint64_t amas
     if ((bal[k] >> tnp::lane()) & 1) {
       const int64_t o = off + tnp::mbcnt(bal[k]);
       reinterpret_cast<int2*>(out)[o] = make_int2(a[k], b[k]);
-      odm[o] = d[k];
+      odm[o] = (uint8_t)d[k];
       osm[o] = m[k];
       used[a[k]] = 1;
       used[b[k]] = 1;
@@ -935,7 +941,7 @@ k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, uint64_t fmask, uint64_t amas
 // ctr[CTR_ACTIVE] when ctr != null
 __global__ void __launch_bounds__(TNP_BLOCK)
 k_edge_masks(const int32_t* __restrict__ edges, int64_t E, const ulonglong2* __restrict__ pz,
-             uint64_t* __restrict__ dm, uint64_t* __restrict__ sm, uint64_t amask,
+             uint8_t* __restrict__ dm, uint64_t* __restrict__ sm, uint64_t amask,
              int64_t* __restrict__ ctr) {
   __shared__ uint64_t lds[TNP_WAVES];
   uint64_t act = 0;
@@ -944,7 +950,7 @@ k_edge_masks(const int32_t* __restrict__ edges, int64_t E, const ulonglong2* __r
     const int2 ab = reinterpret_cast<const int2*>(edges)[i];
     const ulonglong2 ka = pz[ab.x], kb = pz[ab.y];
     const uint64_t s = (ka.x ^ kb.x) & ~ka.y & ~kb.y;
-    dm[i] = (ka.x ^ kb.x) | (ka.y ^ kb.y);
+    dm[i] = high_plane((ka.x ^ kb.x) | (ka.y ^ kb.y));
     sm[i] = s;
     act |= s & amask;
   }
@@ -1030,7 +1036,7 @@ int64_t step_tiles(int64_t n) { return (n + TILE - 1) / TILE; }
 int64_t lb_tiles(int64_t n) { return (n + LTILE - 1) / LTILE; }
 int64_t split_tiles(int64_t n) { return (n + STILE - 1) / STILE; }
 
-int launch_split_lb(int32_t* edges, int64_t E, const uint64_t* sm, uint64_t* dm, int idx, int64_t V,
+int launch_split_lb(int32_t* edges, int64_t E, const uint64_t* sm, uint8_t* dm, int idx, int64_t V,
                     int32_t* sa, int32_t* sb, int64_t* ctr, int32_t* eidx, const TnpLB& lb,
                     hipStream_t s) {
   const int64_t tiles = split_tiles(E);
@@ -1193,8 +1199,8 @@ int launch_prune(bool emit, const int32_t* edges, int64_t E, const int32_t* sb, 
 }
 int launch_prune_lb(const int32_t* edges, int64_t E, const int32_t* sb, int64_t S, int64_t V,
                     const uint64_t* ckeys, int nb, int64_t X, int idx, int last_plane,
-                    const uint64_t* pz, const uint64_t* dm, const uint64_t* sm, int32_t* out,
-                    uint64_t* odm, uint64_t* osm, uint8_t* used, int64_t* ctr, const TnpLB& lb,
+                    const uint64_t* pz, const uint8_t* dm, const uint64_t* sm, int32_t* out,
+                    uint8_t* odm, uint64_t* osm, uint8_t* used, int64_t* ctr, const TnpLB& lb,
                     hipStream_t s) {
   EdgeSrc src{edges, E, sb, S, V, ckeys, nb, X};
   const int64_t N = E + S + X;
@@ -1206,7 +1212,8 @@ int launch_prune_lb(const int32_t* edges, int64_t E, const int32_t* sb, int64_t 
   uint64_t amask = (idx + 1 >= 64) ? 0ull : (~0ull << (idx + 1));
   if (last_plane < 63) amask &= (1ull << (last_plane + 1)) - 1ull;
   const int64_t tiles = lb_tiles(N);
-  hipLaunchKernelGGL(k_prune_lb, dim3((unsigned)tiles), dim3(TNP_BLOCK), 0, s, src, N, tiles, fmask,
+  (void)fmask;
+  hipLaunchKernelGGL(k_prune_lb, dim3((unsigned)tiles), dim3(TNP_BLOCK), 0, s, src, N, tiles, idx,
                      amask, reinterpret_cast<const ulonglong2*>(pz), dm, sm, out, odm, osm, used, ctr,
                      lb);
   TNP_CHECK(hipGetLastError());
@@ -1225,7 +1232,7 @@ int launch_count_flags(const uint8_t* f, int64_t n, int64_t* ctr, int slot, hipS
   TNP_CHECK(hipGetLastError());
   return 0;
 }
-int launch_edge_masks(const int32_t* edges, int64_t E, const uint64_t* pz, uint64_t* dm,
+int launch_edge_masks(const int32_t* edges, int64_t E, const uint64_t* pz, uint8_t* dm,
                       uint64_t* sm, int from, int last_plane, int64_t* ctr, hipStream_t s) {
   if (E <= 0) return 0;
   uint64_t amask = (from >= 64) ? 0ull : (~0ull << from);
