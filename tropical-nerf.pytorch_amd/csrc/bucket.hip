@@ -236,7 +236,7 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
                const ulonglong2* __restrict__ pz, CellEnt* __restrict__ ents,
                int32_t* __restrict__ lcell, int32_t* __restrict__ lent, int32_t* __restrict__ ln,
                int64_t* __restrict__ lpoff, int32_t* __restrict__ bnpc, int64_t* __restrict__ bnpairs,
-               int64_t* __restrict__ ctr) {
+               int64_t* __restrict__ bspairs, int64_t* __restrict__ ctr) {
   constexpr int LC = 1 << (3 * SH);
   __shared__ int cnt[LC];
   __shared__ int cur[LC];
@@ -248,6 +248,19 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
     if (threadIdx.x == 0) {
       bnpc[b] = 0;
       bnpairs[b] = 0;
+      bspairs[b] = 0;
+    }
+    if (n == 1 && threadIdx.x == 0) {  // a lone entry: a record the window pass can read
+      const uint64_t w = ekv[base];
+      const ulonglong2 k = pz[(uint32_t)w];
+      CellEnt r;
+      r.p = k.x;
+      r.z = k.y;
+      r.v = (int32_t)(uint32_t)w;
+      r.f = (uint32_t)(w >> 32) & 63u;
+      r.tag = (uint32_t)b * (uint32_t)LC + (uint32_t)(w >> 40);
+      r.pad = 0;
+      ents[base] = r;
     }
     return;
   }
@@ -297,38 +310,46 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
 #pragma unroll
     for (int k = 0; k < GIPT; ++k) {
       if (w[k] == ~0ull) continue;
+      const int lc = (int)(w[k] >> 40);
       CellEnt r;
       r.p = k2[k].x;
       r.z = k2[k].y;
       r.v = (int32_t)(uint32_t)w[k];
       r.f = (uint32_t)(w[k] >> 32) & 63u;
+      // the cell's tag for the window pass; cells above WCELL members are
+      // flagged: the flattened pair-space pass (k_connect) takes them
+      r.tag = ((uint32_t)b * (uint32_t)LC + (uint32_t)lc) | (cnt[lc] > WCELL ? 0x80000000u : 0u);
       r.pad = 0;
       ents[base + pos[k]] = r;
     }
   }
   __syncthreads();
-  // pair cells in local-cell order (cur[i] now = end of cell i)
+  // pair cells above WCELL members in local-cell order (cur[i] now = end
+  // of cell i); the pairs of the smaller cells are the window pass's
   int npc = 0;
-  int64_t np = 0;
+  int64_t np = 0, nsp = 0;
   bool big = false;
   for (int i = c0; i < c0 + per && i < LC; ++i) {
     const int m = cnt[i];
     big |= m > 65535;
-    if (m >= 2 && m <= 65535) {
+    if (m > WCELL && m <= 65535) {
       ++npc;
       np += (int64_t)m * (m - 1) / 2;
+    } else if (m >= 2 && m <= WCELL) {
+      nsp += (int64_t)m * (m - 1) / 2;
     }
   }
   if (__ballot(big) && tnp::lane() == 0) atomicOr((unsigned long long*)&ctr[CTR_BIG], 1ull);
-  int64_t tpc, tp;
+  int64_t tpc, tp, tsp;
   int64_t opc = tnp::block_scan_excl((int64_t)npc, lds, tpc);
   int64_t op = tnp::block_scan_excl(np, lds, tp);
+  tnp::block_scan_excl(nsp, lds, tsp);
   const int64_t area = base / 2;
   const int m_ = (1 << G.sh) - 1;
   const int bz = b % G.NBd, by = (b / G.NBd) % G.NBd, bx = b / (G.NBd * G.NBd);
   for (int i = c0; i < c0 + per && i < LC; ++i) {
     const int m = cnt[i];
-    if (m >= 2 && m <= 65535) {
+    if (m > WCELL && m <= 65535) {
       const int cx = (bx << G.sh) | (i >> (2 * G.sh));
       const int cy = (by << G.sh) | ((i >> G.sh) & m_);
       const int cz = (bz << G.sh) | (i & m_);
@@ -343,6 +364,7 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
   if (threadIdx.x == 0) {
     bnpc[b] = (int32_t)tpc;
     bnpairs[b] = tp;
+    bspairs[b] = tsp;
   }
 }
 
@@ -413,8 +435,9 @@ int launch_bucket_entries(const int32_t* members, int64_t M, const uint64_t* gri
 int launch_bucket_pairs(int n_marks, const int64_t* bbase, const uint64_t* ekv, const uint64_t* pz,
                         CellEnt* ents, int32_t* lcell,
                         int32_t* lent, int32_t* ln, int64_t* lpoff, int32_t* bnpc, int64_t* bnpairs,
-                        int64_t* pcoff, int64_t* pairoff, int32_t* pcell, int32_t* pent, int32_t* pn,
-                        int64_t* ptoff, int64_t* ctr, hipStream_t s) {
+                        int64_t* bspairs, int64_t* spoff, int64_t* pcoff, int64_t* pairoff,
+                        int32_t* pcell, int32_t* pent, int32_t* pn, int64_t* ptoff, int64_t* ctr,
+                        hipStream_t s) {
   int sh, NBd, NB;
   if (bucket_geometry(n_marks, &sh, &NBd, &NB)) {
     tnp_set_error("bucket geometry: %d marks", n_marks);
@@ -424,13 +447,14 @@ int launch_bucket_pairs(int n_marks, const int64_t* bbase, const uint64_t* ekv, 
   if (sh == 3)
     hipLaunchKernelGGL(k_bucket_group<3>, dim3(NB), dim3(TNP_BLOCK), 0, s, G, bbase, ekv,
                        reinterpret_cast<const ulonglong2*>(pz), ents, lcell, lent, ln, lpoff, bnpc, bnpairs,
-                       ctr);
+                       bspairs, ctr);
   else
     hipLaunchKernelGGL(k_bucket_group<4>, dim3(NB), dim3(TNP_BLOCK), 0, s, G, bbase, ekv,
                        reinterpret_cast<const ulonglong2*>(pz), ents, lcell, lent, ln, lpoff, bnpc, bnpairs,
-                       ctr);
+                       bspairs, ctr);
   hipLaunchKernelGGL(k_small_scan, dim3(1), dim3(1024), 0, s, bnpc, NB, pcoff, ctr, (int)CTR_R);
   hipLaunchKernelGGL(k_small_scan64, dim3(1), dim3(1024), 0, s, bnpairs, NB, pairoff, ctr, (int)CTR_TESTS);
+  hipLaunchKernelGGL(k_small_scan64, dim3(1), dim3(1024), 0, s, bspairs, NB, spoff, ctr, (int)CTR_SPAIRS);
   hipLaunchKernelGGL(k_pair_gather, dim3(NB), dim3(TNP_BLOCK), 0, s, bbase, bnpc, pcoff, pairoff, lcell, lent,
                      ln, lpoff, pcell, pent, pn, ptoff);
   TNP_CHECK(hipGetLastError());

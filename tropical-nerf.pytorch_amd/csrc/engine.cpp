@@ -175,7 +175,7 @@ struct tnp_engine {
   Buf fscr[12];
   Buf fscr2[32];
   Buf sents;                // bucket-ordered packed entries before the in-bucket grouping
-  Buf bk[12];               // bucket.hip scratch (per-bucket counts, bases, pair-cell areas)
+  Buf bk[14];               // bucket.hip scratch (per-bucket counts, bases, pair-cell areas)
   bool radix_cells = false; // TNP_RADIX_CELLS=1: the radix-sort bucketing path
   Buf cv[CV_N];
 };
@@ -873,6 +873,8 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     for (int k = 8; k < 11; ++k)
       if (buf_ensure(e->bk[k], RC * sizeof(int32_t), s)) return -1;  // per-bucket pair-cell areas
     if (buf_ensure(e->bk[11], RC * sizeof(int64_t), s)) return -1;
+    if (buf_ensure(e->bk[12], NB * sizeof(int64_t), s)) return -1;        // window-pass pairs
+    if (buf_ensure(e->bk[13], (NB + 1) * sizeof(int64_t), s)) return -1;
     if (buf_ensure(e->sents, TB * sizeof(uint64_t), s)) return -1;
     TIMED("bucket_entries", 24.0 * M,
           launch_bucket_entries(P<int32_t>(e->members), M, grid, zero, idx, e->net.n_marks,
@@ -883,6 +885,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
                               P<uint64_t>(c.pz), P<CellEnt>(e->ents),
                               P<int32_t>(e->bk[8]), P<int32_t>(e->bk[9]), P<int32_t>(e->bk[10]),
                               P<int64_t>(e->bk[11]), P<int32_t>(e->bk[3]), P<int64_t>(e->bk[4]),
+                              P<int64_t>(e->bk[12]), P<int64_t>(e->bk[13]),
                               P<int64_t>(e->bk[5]), P<int64_t>(e->bk[6]), P<int32_t>(e->pcell),
                               P<int32_t>(e->pent), P<int32_t>(e->pcn), P<int64_t>(e->ptoff), ctr, s));
   } else {
@@ -948,7 +951,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   //    keep their capacity across steps and grow (then redo) on overflow.
   int nb = 1;
   while (nb < 31 && (1ll << nb) < NV) ++nb;
-  if (buf_ensure(e->bstat, 3 * connect_grid() * sizeof(int64_t), s)) return -1;
+  if (buf_ensure(e->bstat, 6 * connect_grid() * sizeof(int64_t), s)) return -1;
   // connecting edges this step's pruning drops are never appended (sorted,
   // re-tested): keep_edge() depends on the endpoints only
   const uint64_t cfmask = prune ? prune_mask(idx, K - 1) : 0ull;
@@ -969,11 +972,20 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
       TNP_CHECK(hipMemsetAsync(ctr + CTR_XK, 0, sizeof(int64_t), s));
       TNP_CHECK(hipMemsetAsync(ctr + CTR_P, 0, 2 * sizeof(int64_t), s));  // CTR_P, CTR_COMPAT
     }
+    // cells above WCELL members: the flattened pair space (every cell on the
+    // radix path); the others: the window pass
     TIMED("connect", 0.0,
           launch_connect(P<int64_t>(e->ptoff), P<int32_t>(e->pcell), P<int32_t>(e->pcn),
                          P<int32_t>(e->pent), NC, e->max_pair_tests, P<int32_t>(e->bcell),
                          P<CellEnt>(e->ents), idx, nb, cfmask, P<uint64_t>(e->ckeys_a), cap, ctr,
-                         P<int64_t>(e->bstat), s));
+                         P<int64_t>(e->bstat), s, !buckets));
+    if (buckets) {
+      const int g = connect_grid();
+      TIMED("connect_win", 0.0,
+            launch_connect_win(P<CellEnt>(e->ents), idx, nb, cfmask, P<uint64_t>(e->ckeys_a), cap, ctr,
+                               P<int64_t>(e->bstat) + 3 * g, s));
+      if (launch_connect_sum(P<int64_t>(e->bstat), 2 * g, ctr, s)) return -1;
+    }
     if (read_ctr(e, s)) return -1;
     if (buckets) {
       if (e->h_ctr[CTR_K0]) {
@@ -1081,7 +1093,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     st->E_out = E2;
     st->A = e->h_ctr[CTR_A];
     st->P = e->h_ctr[CTR_P];
-    st->pair_tests = e->h_ctr[CTR_TESTS];
+    st->pair_tests = e->h_ctr[CTR_TESTS] + e->h_ctr[CTR_SPAIRS];
     st->override_applied = override_ < 0 ? (e->h_ctr[CTR_FAIL] != 0) : override_;
     st->next_active = (uint64_t)e->h_ctr[CTR_ACTIVE];
     st->S_dup = e->pend_dup;

@@ -32,7 +32,8 @@ enum {
   CTR_XK = 24,      // connecting edges surviving this step's pruning (appended)
   CTR_R = 25,       // cells with at least one member pair
   CTR_RUNS = 26,    // occupied cells (runs of equal keys in the sorted entries)
-  CTR_N = 27
+  CTR_SPAIRS = 27,  // member pairs of the cells the window pass tests (<= WCELL members)
+  CTR_N = 28
 };
 
 int64_t step_tiles(int64_t n);
@@ -95,12 +96,18 @@ int64_t pair_run_tiles(int64_t T);
 // and its grid relation to THIS cell in 6 bits (cell_flags): bit d = the
 // member's lowest spanned cell along axis d is this cell, bit 3 + d = the
 // member lies on a mark plane of axis d.  One 32-byte record per entry.
+// tag: the cell's id for the window pass (bit 31: a cell above WCELL
+// members, left to the flattened pair-space pass); 0 on the radix path
 struct alignas(32) CellEnt {
   uint64_t p, z;
   int32_t v;
   uint32_t f;
-  uint64_t pad;
+  uint32_t tag, pad;
 };
+// cells of at most WCELL members have their pairs tested by the window pass
+// (k_connect_win): a pair (j < i) of such a cell lies in the 64-entry
+// window starting at 32 * floor(j / 32)
+constexpr int WCELL = 33;
 // cell_flags of a member (grid word g) in the cell with coordinates c (+2)
 __device__ __forceinline__ uint32_t cell_flags(uint64_t g, int cx, int cy, int cz) {
   const int c[3] = {cx, cy, cz};
@@ -134,7 +141,9 @@ int launch_chunk_cells(const int64_t* ptoff, const int32_t* pn, int64_t rcap, in
 int launch_connect(const int64_t* ptoff, const int32_t* pcell, const int32_t* pn,
                    const int32_t* pent, int NC, int64_t max_tests, const int32_t* bcell,
                    const CellEnt* ent, int idx, int nb, uint64_t fmask, uint64_t* keys,
-                   int64_t cap, int64_t* ctr, int64_t* bstat, hipStream_t s);
+                   int64_t cap, int64_t* ctr, int64_t* bstat, hipStream_t s, bool sum = true);
+// per-block counters of nblk blocks -> ctr[CTR_COMPAT], ctr[CTR_P], ctr[CTR_X]
+int launch_connect_sum(const int64_t* bstat, int64_t nblk, int64_t* ctr, hipStream_t s);
 // single-pass pruning over [edges; e_new; c_new] (lb_tiles(E + S + X)
 // look-back tiles): kept edges in order -> out, used flags (zeroed by the
 // caller), ctr[CTR_E], ctr[CTR_ACTIVE]
@@ -166,11 +175,20 @@ int launch_bucket_entries(const int32_t* members, int64_t M, const uint64_t* gri
 // pair cells; then the global pair-cell list (pcell, pent, pn, ptoff; R ->
 // ctr[CTR_R], pairs -> ctr[CTR_TESTS]) that launch_connect walks.
 // lcell/lent/ln/lpoff: 4 M + 1 capacity; bnpc/bnpairs: NB; pcoff/pairoff: NB + 1
+// Cells above WCELL members go to the pair-cell list; the pairs of the
+// others -> ctr[CTR_SPAIRS] (bspairs/spoff: NB / NB + 1 int64 scratch).
 int launch_bucket_pairs(int n_marks, const int64_t* bbase, const uint64_t* ekv, const uint64_t* pz,
                         CellEnt* ents, int32_t* lcell,
                         int32_t* lent, int32_t* ln, int64_t* lpoff, int32_t* bnpc, int64_t* bnpairs,
-                        int64_t* pcoff, int64_t* pairoff, int32_t* pcell, int32_t* pent, int32_t* pn,
-                        int64_t* ptoff, int64_t* ctr, hipStream_t s);
+                        int64_t* bspairs, int64_t* spoff, int64_t* pcoff, int64_t* pairoff,
+                        int32_t* pcell, int32_t* pent, int32_t* pn, int64_t* ptoff, int64_t* ctr,
+                        hipStream_t s);
+// window pass over the cell-contiguous entries (count ctr[CTR_T]): every
+// pair of a cell of <= WCELL members, same emission rules and counters as
+// launch_connect (bstat: its own 3 * connect_grid() slots; sum with
+// launch_connect_sum)
+int launch_connect_win(const CellEnt* ent, int idx, int nb, uint64_t fmask, uint64_t* keys, int64_t cap,
+                       int64_t* ctr, int64_t* bstat, hipStream_t s);
 
 // ---- sort.hip ----
 // ascending LSD radix sort of n u64 keys on bits [0, bits); the sorted keys

@@ -461,6 +461,7 @@ __global__ void k_entry_keys(const int32_t* __restrict__ ent_v, const uint32_t* 
   r.z = k.y;
   r.v = v;
   r.f = cell_flags(grid[v], (int)(c / ((uint32_t)NC * NC)), (int)((c / NC) % NC), (int)(c % NC));
+  r.tag = 0x80000000u;  // radix path: every cell goes through k_connect
   r.pad = 0;
   ent[i] = r;
 }
@@ -699,6 +700,119 @@ k_connect(const int64_t* __restrict__ ptoff, const int32_t* __restrict__ pcell,
   for (int k = 0; k < ne; ++k)
     if (w0 + k < cap) keys[w0 + k] = kk[k];
   }
+  int64_t tot;
+  tnp::block_scan_excl(n_compat, lds, tot);
+  if (threadIdx.x == 0) bstat[3 * blockIdx.x] = tot;
+  tnp::block_scan_excl(n_reg, lds, tot);
+  if (threadIdx.x == 0) bstat[3 * blockIdx.x + 1] = tot;
+  tnp::block_scan_excl(n_conn, lds, tot);
+  if (threadIdx.x == 0) bstat[3 * blockIdx.x + 2] = tot;
+}
+
+// ---------------------------------------------------------------------------
+// Window pass: the pairs of every cell of <= WCELL members.  The entries are
+// cell-contiguous; a wave stages the 64 records of window w (entries
+// [32 w, 32 w + 64)) in LDS; each of its first 32 entries j is tested
+// against the later entries of its cell, the (j, partner) tests flattened
+// over the 64 lanes (a wave scan of the per-entry counts, a 6-step search
+// in LDS per test): a pair (j < i) of such a cell is tested exactly once, in
+// window floor(j / 32) (i - j <= 32).  Each record is read once from memory
+// per window; emitted keys go through a per-wave LDS buffer, one global
+// append per 512.
+// ---------------------------------------------------------------------------
+constexpr int WKEYS = 512;
+
+__device__ __forceinline__ void lds_fence() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_connect_win(const CellEnt* __restrict__ ent, int idx, int nb, uint64_t fmask,
+              uint64_t* __restrict__ keys, int64_t cap, int64_t* __restrict__ ctr,
+              int64_t* __restrict__ bstat) {
+  __shared__ CellEnt st[TNP_WAVES][64];
+  __shared__ int exc[TNP_WAVES][64];
+  __shared__ uint64_t kb[TNP_WAVES][WKEYS];
+  __shared__ int64_t lds[TNP_WAVES];
+  const int64_t T = ctr[CTR_T];
+  const int64_t nwin = (T + 31) / 32;
+  const uint64_t below = (idx >= 64) ? ~0ull : ((1ull << idx) - 1ull);
+  const int wv = tnp::wave(), L = tnp::lane();
+  int kn = 0;  // wave-uniform fill of this wave's key buffer
+  int64_t n_compat = 0, n_reg = 0, n_conn = 0;
+  auto flush = [&]() {
+    int64_t base = 0;
+    if (L == 0) base = (int64_t)atomicAdd((unsigned long long*)&ctr[CTR_XK], (unsigned long long)kn);
+    base = __shfl(base, 0, 64);
+    for (int i = L; i < kn; i += 64)
+      if (base + i < cap) keys[base + i] = kb[wv][i];
+    lds_fence();
+    kn = 0;
+  };
+  for (int64_t w = (int64_t)blockIdx.x * TNP_WAVES + wv; w < nwin; w += (int64_t)gridDim.x * TNP_WAVES) {
+    const int64_t e = w * 32 + L;
+    const bool valid = e < T;
+    CellEnt r;
+    if (valid) {
+      r = ent[e];
+    } else {
+      r.p = r.z = 0;
+      r.v = 0;
+      r.f = 0;
+      r.tag = 0xFFFFFFFFu;  // no cell: matches nothing, never initiates
+      r.pad = 0;
+    }
+    st[wv][L] = r;
+    lds_fence();
+    // last lane of my cell inside the window (lane 63 always closes one)
+    const uint32_t nxt = __shfl_down(r.tag, 1, 64);
+    const uint64_t bm = __ballot(L == 63 || nxt != r.tag);
+    const int last = L + __builtin_ctzll(bm >> L);
+    const bool init = valid && L < 32 && !(r.tag & 0x80000000u);
+    const int rounds = init ? last - L : 0;
+    // flatten the window's (initiator, partner) tests over the lanes: test t
+    // belongs to the last initiator j with exc[j] <= t, partner j + 1 + t - exc[j]
+    const int incl = tnp::wave_scan_incl(rounds);
+    const int total = __shfl(incl, 63, 64);
+    exc[wv][L] = incl - rounds;
+    lds_fence();
+    for (int t0 = 0; t0 < total; t0 += 64) {
+      if (kn + 64 > WKEYS) flush();
+      const int t = t0 + L;
+      bool em = false;
+      uint64_t key = 0;
+      if (t < total) {
+        int lo = 0, hi = 62;
+#pragma unroll
+        for (int it = 0; it < 6; ++it) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (exc[wv][mid] <= t) lo = mid;
+          else hi = mid - 1;
+        }
+        const int j = lo, i = j + 1 + (t - exc[wv][j]);
+        const CellEnt u = st[wv][j];
+        const CellEnt q = st[wv][i];
+        const PairTest pt = pair_test(below, u.f, u.p, u.z, q.f, q.p, q.z);
+        if (pt.compat) {
+          n_compat++;
+          n_reg += pt.regions;
+          n_conn += pt.emit;
+          // the step's pruning drops it anyway (keep_edge): never appended
+          if (pt.emit && (fmask == 0 || (((u.p ^ q.p) | (u.z ^ q.z)) & fmask) != 0)) {
+            const uint32_t vu = (uint32_t)u.v, vv = (uint32_t)q.v;
+            const uint32_t lo2 = vu < vv ? vu : vv, hi2 = vu < vv ? vv : vu;
+            key = ((uint64_t)lo2 << nb) | hi2;
+            em = true;
+          }
+        }
+      }
+      const uint64_t eb = __ballot(em);
+      if (em) kb[wv][kn + tnp::mbcnt(eb)] = key;
+      kn += __popcll(eb);
+    }
+    lds_fence();
+  }
+  if (kn) flush();
   int64_t tot;
   tnp::block_scan_excl(n_compat, lds, tot);
   if (threadIdx.x == 0) bstat[3 * blockIdx.x] = tot;
@@ -1139,19 +1253,27 @@ int launch_entry_keys(const int32_t* ent_v, const uint32_t* ekey, int NC, int64_
 }
 // persistent blocks: exactly the resident ones (occupancy x CUs), so the
 // static chunk stride never leaves a second, late wave of blocks as a tail
-static int connect_grid_size() {
-  static int g = 0;
+// (cached per device: one process may drive several devices)
+template <typename K>
+static int resident_grid(K kernel, int slot) {
+  static int cache[2][64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 2048;
+  int& g = cache[slot][dev];
   if (!g) {
-    int dev = 0, cus = 0, per_cu = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_connect, TNP_BLOCK, 0) != hipSuccess ||
+    int cus = 0, per_cu = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, TNP_BLOCK, 0) != hipSuccess ||
         cus <= 0 || per_cu <= 0)
       g = 2048;
     else
       g = cus * per_cu;
   }
   return g;
+}
+static int connect_grid_size() {
+  // the window pass shares the bstat layout: one grid size for both
+  return std::max(resident_grid(k_connect, 0), resident_grid(k_connect_win, 1));
 }
 int64_t connect_chunks(int64_t TT) { return (TT + CCH - 1) / CCH; }
 int launch_chunk_cells(const int64_t* ptoff, const int32_t* pn, int64_t rcap, int32_t* bcell,
@@ -1164,12 +1286,25 @@ int launch_chunk_cells(const int64_t* ptoff, const int32_t* pn, int64_t rcap, in
 int launch_connect(const int64_t* ptoff, const int32_t* pcell, const int32_t* pn,
                    const int32_t* pent, int NC, int64_t max_tests, const int32_t* bcell,
                    const CellEnt* ent, int idx, int nb, uint64_t fmask, uint64_t* keys,
-                   int64_t cap, int64_t* ctr, int64_t* bstat, hipStream_t s) {
+                   int64_t cap, int64_t* ctr, int64_t* bstat, hipStream_t s, bool sum) {
   static_assert(CONNECT_CELLS >= CCH + 2, "chunk cell window");
   const int grid = connect_grid_size();
   hipLaunchKernelGGL(k_connect, dim3(grid), dim3(TNP_BLOCK), 0, s, ptoff, pcell, pn,
                      pent, NC, max_tests, bcell, ent, idx, nb, fmask, keys, cap, ctr, bstat);
-  hipLaunchKernelGGL(k_sum_bstat, dim3(1), dim3(TNP_BLOCK), 0, s, bstat, (int64_t)grid, ctr);
+  if (sum) hipLaunchKernelGGL(k_sum_bstat, dim3(1), dim3(TNP_BLOCK), 0, s, bstat, (int64_t)grid, ctr);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_connect_win(const CellEnt* ent, int idx, int nb, uint64_t fmask, uint64_t* keys, int64_t cap,
+                       int64_t* ctr, int64_t* bstat, hipStream_t s) {
+  const int grid = connect_grid_size();
+  hipLaunchKernelGGL(k_connect_win, dim3(grid), dim3(TNP_BLOCK), 0, s, ent, idx, nb, fmask, keys, cap, ctr,
+                     bstat);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_connect_sum(const int64_t* bstat, int64_t nblk, int64_t* ctr, hipStream_t s) {
+  hipLaunchKernelGGL(k_sum_bstat, dim3(1), dim3(TNP_BLOCK), 0, s, bstat, nblk, ctr);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
