@@ -35,17 +35,13 @@
 
 namespace {
 
-__global__ void __launch_bounds__(TNP_BLOCK)
-k_sum_parts_b(const int64_t* __restrict__ part, int64_t n, int64_t* __restrict__ ctr, int slot) {
-  __shared__ int64_t lds[TNP_WAVES];
-  int64_t a = 0;
-  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) a += part[i];
-  int64_t tot;
-  tnp::block_scan_excl(a, lds, tot);
-  if (threadIdx.x == 0) ctr[slot] = tot;
-}
-
 constexpr int BK_IPT = 8;  // members per thread in the member passes
+
+// member m of a step: the S new vertices are slots V + m (no list needed),
+// the hit vertices follow in members[S..]
+__device__ __forceinline__ int member_of(const int32_t* members, int64_t S, int64_t V, int64_t m) {
+  return m < S ? (int)(V + m) : members[m];
+}
 
 struct BGeom {
   int NC;   // cell coordinates (+2) per axis: [0, NC)
@@ -74,7 +70,8 @@ __device__ __forceinline__ int local_of(const BGeom& G, int cx, int cy, int cz) 
 
 // (1) per-bucket entry counts; per-block augmented-row sums -> part[]
 __global__ void __launch_bounds__(TNP_BLOCK)
-k_bucket_count(const int32_t* __restrict__ members, int64_t M, const uint64_t* __restrict__ grid,
+k_bucket_count(const int32_t* __restrict__ members, int64_t S, int64_t V, int64_t M,
+               const uint64_t* __restrict__ grid,
                const uint64_t* __restrict__ zero, int idx, BGeom G, int NB,
                int32_t* __restrict__ bcount, int64_t* __restrict__ part, int64_t* __restrict__ ctr) {
   __shared__ int hist[BUCKET_MAX];
@@ -89,7 +86,7 @@ k_bucket_count(const int32_t* __restrict__ members, int64_t M, const uint64_t* _
   for (int k = 0; k < BK_IPT; ++k) {
     const int64_t m = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
     if (m >= M) break;
-    const int v = members[m];
+    const int v = member_of(members, S, V, m);
     int lo[3], n[3];
     span_of(grid[v], lo, n);
     for (int i = 0; i < n[0]; ++i)
@@ -112,8 +109,21 @@ k_bucket_count(const int32_t* __restrict__ members, int64_t M, const uint64_t* _
 // ctr[slot] (one block; n is a few thousand)
 __global__ void __launch_bounds__(1024)
 k_small_scan(const int32_t* __restrict__ cnt, int n, int64_t* __restrict__ out, int64_t* __restrict__ ctr,
-             int slot) {
+             int slot, const int64_t* __restrict__ part, int64_t nparts, int pslot) {
   __shared__ int64_t lds[16];
+  if (part) {  // and the sum of the member pass's per-block parts -> ctr[pslot]
+    int64_t a = 0;
+    for (int64_t i = threadIdx.x; i < nparts; i += 1024) a += part[i];
+    a = tnp::wave_sum(a);
+    if (tnp::lane() == 0) lds[tnp::wave()] = a;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int64_t t = 0;
+      for (int w = 0; w < 16; ++w) t += lds[w];
+      ctr[pslot] = t;
+    }
+    __syncthreads();
+  }
   const int per = (n + 1023) / 1024;
   const int b = threadIdx.x * per;
   int64_t s = 0;
@@ -137,11 +147,16 @@ k_small_scan(const int32_t* __restrict__ cnt, int n, int64_t* __restrict__ out, 
   }
 }
 
-// the same for int64 values (pair counts)
+// the same for int64 values (pair counts); blockIdx.y picks one of two
+// (cnt, out, slot) sets
 __global__ void __launch_bounds__(1024)
-k_small_scan64(const int64_t* __restrict__ cnt, int n, int64_t* __restrict__ out, int64_t* __restrict__ ctr,
-               int slot) {
+k_small_scan64(const int64_t* __restrict__ cnt0, int64_t* __restrict__ out0, int slot0,
+               const int64_t* __restrict__ cnt1, int64_t* __restrict__ out1, int slot1, int n,
+               int64_t* __restrict__ ctr) {
   __shared__ int64_t lds[16];
+  const int64_t* cnt = blockIdx.y ? cnt1 : cnt0;
+  int64_t* out = blockIdx.y ? out1 : out0;
+  const int slot = blockIdx.y ? slot1 : slot0;
   const int per = (n + 1023) / 1024;
   const int b = threadIdx.x * per;
   int64_t s = 0;
@@ -168,7 +183,8 @@ k_small_scan64(const int64_t* __restrict__ cnt, int n, int64_t* __restrict__ out
 // (3) entries into their bucket ranges: a block reserves one range per
 // non-empty bin (one global add), then places its entries inside it
 __global__ void __launch_bounds__(TNP_BLOCK)
-k_bucket_scatter(const int32_t* __restrict__ members, int64_t M, const uint64_t* __restrict__ grid,
+k_bucket_scatter(const int32_t* __restrict__ members, int64_t S, int64_t V, int64_t M,
+                 const uint64_t* __restrict__ grid,
                  BGeom G, int NB, const int64_t* __restrict__ bbase, int32_t* __restrict__ bcur,
                  uint64_t* __restrict__ ekv) {
   __shared__ int hist[BUCKET_MAX];
@@ -181,7 +197,7 @@ k_bucket_scatter(const int32_t* __restrict__ members, int64_t M, const uint64_t*
 #pragma unroll
   for (int k = 0; k < BK_IPT; ++k) {
     const int64_t m = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
-    vv[k] = m < M ? members[m] : -1;
+    vv[k] = m < M ? member_of(members, S, V, m) : -1;
   }
 #pragma unroll
   for (int k = 0; k < BK_IPT; ++k) gg[k] = grid[vv[k] >= 0 ? vv[k] : 0];
@@ -376,16 +392,28 @@ k_pair_gather(const int64_t* __restrict__ bbase, const int32_t* __restrict__ bnp
               const int32_t* __restrict__ lcell, const int32_t* __restrict__ lent,
               const int32_t* __restrict__ ln, const int64_t* __restrict__ lpoff,
               int32_t* __restrict__ pcell, int32_t* __restrict__ pent, int32_t* __restrict__ pn,
-              int64_t* __restrict__ ptoff) {
+              int64_t* __restrict__ ptoff, int32_t* __restrict__ bcell, int64_t bcap, int64_t chunk,
+              int32_t* __restrict__ bcount, int32_t* __restrict__ bcur, int64_t* __restrict__ ctr) {
   const int b = blockIdx.x;
+  if (threadIdx.x == 0) {  // the bucket counters are clean for the next step
+    bcount[b] = 0;
+    bcur[b] = 0;
+  }
   const int cnt = bnpc[b];
   if (cnt == 0) return;
   const int64_t area = bbase[b] / 2, o = pcoff[b], po = pairoff[b];
   for (int i = threadIdx.x; i < cnt; i += TNP_BLOCK) {
+    const int m = ln[area + i];
+    const int64_t lo = po + lpoff[area + i];
     pcell[o + i] = lcell[area + i];
     pent[o + i] = lent[area + i];
-    pn[o + i] = ln[area + i];
-    ptoff[o + i] = po + lpoff[area + i];
+    pn[o + i] = m;
+    ptoff[o + i] = lo;
+    // k_connect's chunk table (k_chunk_cells): chunk q starts in pair cell o + i
+    const int64_t n = (int64_t)m * (m - 1) / 2;
+    const int64_t b0 = (lo + chunk - 1) / chunk, b1 = (lo + n + chunk - 1) / chunk;
+    if (b1 > bcap) atomicOr((unsigned long long*)&ctr[CTR_BOVF], 1ull);
+    for (int64_t q = b0; q < b1 && q < bcap; ++q) bcell[q] = (int32_t)(o + i);
   }
 }
 
@@ -404,30 +432,30 @@ int bucket_geometry(int n_marks, int* sh, int* NBd, int* NB) {
   return 0;
 }
 
-int launch_bucket_entries(const int32_t* members, int64_t M, const uint64_t* grid, const uint64_t* zero,
-                          int idx, int n_marks, int32_t* bcount, int32_t* bcur, int64_t* bbase,
-                          int64_t* part, uint64_t* ekv, int64_t* ctr, hipStream_t s) {
+int launch_bucket_entries(const int32_t* members, int64_t S, int64_t V, int64_t M, const uint64_t* grid,
+                          const uint64_t* zero, int idx, int n_marks, int32_t* bcount, int32_t* bcur,
+                          int64_t* bbase, int64_t* part, uint64_t* ekv, bool clean, int64_t* ctr,
+                          hipStream_t s) {
   int sh, NBd, NB;
   if (bucket_geometry(n_marks, &sh, &NBd, &NB)) {
     tnp_set_error("bucket geometry: %d marks", n_marks);
     return -1;
   }
   const BGeom G{n_marks + 2, sh, NBd};
-  TNP_CHECK(hipMemsetAsync(bcount, 0, NB * sizeof(int32_t), s));
-  TNP_CHECK(hipMemsetAsync(bcur, 0, NB * sizeof(int32_t), s));
+  if (!clean) {  // else: zeroed by the previous step's k_pair_gather
+    TNP_CHECK(hipMemsetAsync(bcount, 0, NB * sizeof(int32_t), s));
+    TNP_CHECK(hipMemsetAsync(bcur, 0, NB * sizeof(int32_t), s));
+  }
   const int64_t per = (int64_t)TNP_BLOCK * BK_IPT;
   const unsigned nblk = (unsigned)std::max<int64_t>((M + per - 1) / per, 1);
   if (M > 0)
-    hipLaunchKernelGGL(k_bucket_count, dim3(nblk), dim3(TNP_BLOCK), 0, s, members, M, grid, zero, idx, G,
-                       NB, bcount, part, ctr);
-  else
-    TNP_CHECK(hipMemsetAsync(part, 0, sizeof(int64_t), s));
-  hipLaunchKernelGGL(k_sum_parts_b, dim3(1), dim3(TNP_BLOCK), 0, s, part, (int64_t)(M > 0 ? nblk : 1),
-                     ctr, (int)CTR_A);
-  hipLaunchKernelGGL(k_small_scan, dim3(1), dim3(1024), 0, s, bcount, NB, bbase, ctr, (int)CTR_T);
+    hipLaunchKernelGGL(k_bucket_count, dim3(nblk), dim3(TNP_BLOCK), 0, s, members, S, V, M, grid, zero, idx,
+                       G, NB, bcount, part, ctr);
+  hipLaunchKernelGGL(k_small_scan, dim3(1), dim3(1024), 0, s, bcount, NB, bbase, ctr, (int)CTR_T,
+                     M > 0 ? part : nullptr, (int64_t)nblk, (int)CTR_A);
   if (M > 0)
-    hipLaunchKernelGGL(k_bucket_scatter, dim3(nblk), dim3(TNP_BLOCK), 0, s, members, M, grid, G, NB, bbase,
-                       bcur, ekv);
+    hipLaunchKernelGGL(k_bucket_scatter, dim3(nblk), dim3(TNP_BLOCK), 0, s, members, S, V, M, grid, G, NB,
+                       bbase, bcur, ekv);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
@@ -436,8 +464,8 @@ int launch_bucket_pairs(int n_marks, const int64_t* bbase, const uint64_t* ekv, 
                         CellEnt* ents, int32_t* lcell,
                         int32_t* lent, int32_t* ln, int64_t* lpoff, int32_t* bnpc, int64_t* bnpairs,
                         int64_t* bspairs, int64_t* spoff, int64_t* pcoff, int64_t* pairoff,
-                        int32_t* pcell, int32_t* pent, int32_t* pn, int64_t* ptoff, int64_t* ctr,
-                        hipStream_t s) {
+                        int32_t* pcell, int32_t* pent, int32_t* pn, int64_t* ptoff, int32_t* bcell,
+                        int64_t bcap, int32_t* bcount, int32_t* bcur, int64_t* ctr, hipStream_t s) {
   int sh, NBd, NB;
   if (bucket_geometry(n_marks, &sh, &NBd, &NB)) {
     tnp_set_error("bucket geometry: %d marks", n_marks);
@@ -452,11 +480,12 @@ int launch_bucket_pairs(int n_marks, const int64_t* bbase, const uint64_t* ekv, 
     hipLaunchKernelGGL(k_bucket_group<4>, dim3(NB), dim3(TNP_BLOCK), 0, s, G, bbase, ekv,
                        reinterpret_cast<const ulonglong2*>(pz), ents, lcell, lent, ln, lpoff, bnpc, bnpairs,
                        bspairs, ctr);
-  hipLaunchKernelGGL(k_small_scan, dim3(1), dim3(1024), 0, s, bnpc, NB, pcoff, ctr, (int)CTR_R);
-  hipLaunchKernelGGL(k_small_scan64, dim3(1), dim3(1024), 0, s, bnpairs, NB, pairoff, ctr, (int)CTR_TESTS);
-  hipLaunchKernelGGL(k_small_scan64, dim3(1), dim3(1024), 0, s, bspairs, NB, spoff, ctr, (int)CTR_SPAIRS);
+  hipLaunchKernelGGL(k_small_scan, dim3(1), dim3(1024), 0, s, bnpc, NB, pcoff, ctr, (int)CTR_R, nullptr,
+                     (int64_t)0, 0);
+  hipLaunchKernelGGL(k_small_scan64, dim3(1, 2), dim3(1024), 0, s, bnpairs, pairoff, (int)CTR_TESTS, bspairs,
+                     spoff, (int)CTR_SPAIRS, NB, ctr);
   hipLaunchKernelGGL(k_pair_gather, dim3(NB), dim3(TNP_BLOCK), 0, s, bbase, bnpc, pcoff, pairoff, lcell, lent,
-                     ln, lpoff, pcell, pent, pn, ptoff);
+                     ln, lpoff, pcell, pent, pn, ptoff, bcell, bcap, connect_chunk_pairs(), bcount, bcur, ctr);
   TNP_CHECK(hipGetLastError());
   return 0;
 }

@@ -177,6 +177,7 @@ struct tnp_engine {
   Buf sents;                // bucket-ordered packed entries before the in-bucket grouping
   Buf bk[14];               // bucket.hip scratch (per-bucket counts, bases, pair-cell areas)
   bool radix_cells = false; // TNP_RADIX_CELLS=1: the radix-sort bucketing path
+  bool bk_clean = false;    // bucket counters (bk[0], bk[1]) are zero
   Buf cv[CV_N];
 };
 
@@ -504,10 +505,13 @@ extern "C" int tnp_engine_load(tnp_engine* e, const float* d_xyz, int64_t V, con
       hipLaunchKernelGGL(k_rows_to_planes, dim3(tnp_grid(V)), dim3(TNP_BLOCK), 0, s, d_pre, V, e->K,
                          P<float>(e->cur.pre), e->cur.cap);
     TNP_CHECK(hipGetLastError());
-  } else if (launch_forward(e->net, P<float>(e->cur.xyz), V, P<float>(e->cur.pre), e->cur.cap, 1, s)) {
-    return -1;
+  } else {
+    if (launch_forward(e->net, P<float>(e->cur.xyz), V, P<float>(e->cur.pre), e->cur.cap, 1, s, nullptr,
+                       P<uint64_t>(e->cur.pos), P<uint64_t>(e->cur.zero), P<uint64_t>(e->cur.grid),
+                       P<uint64_t>(e->cur.pz)))
+      return -1;
   }
-  if (keys_for(e, e->cur, 0, V, s)) return -1;
+  if (d_pre && keys_for(e, e->cur, 0, V, s)) return -1;
   e->V = V;
   e->keep_all = keep_all;
   e->valid_from = 0;
@@ -825,10 +829,13 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
                               P<uint64_t>(c.pz), s));
   }
 
-  // 2. members = new vertices ++ live hit vertices (ascending)
+  // 2. members = new vertices ++ live hit vertices (ascending); the bucket
+  //    path reads the new vertices as slots V.. without a list
+  int bsh = 0, bnd = 0, NB = 0;
+  const bool buckets = !e->radix_cells && bucket_geometry(e->net.n_marks, &bsh, &bnd, &NB) == 0;
   if (buf_ensure(e->members, std::max<int64_t>(NV, 1) * sizeof(int32_t), s, hits_done)) return -1;
   if (hits_done) {
-    if (launch_new_members(P<int32_t>(e->members), S, V, s)) return -1;
+    if (!buckets && launch_new_members(P<int32_t>(e->members), S, V, s)) return -1;
   } else {
     TnpLB lb;
     if (V > 0 && lb_begin(e, split_tiles(V), s, &lb)) return -1;
@@ -857,13 +864,18 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   if (buf_ensure(e->pent, RC * sizeof(int32_t), s)) return -1;
   if (buf_ensure(e->pcn, RC * sizeof(int32_t), s)) return -1;
   if (buf_ensure(e->ptoff, RC * sizeof(int64_t), s)) return -1;
-  int bsh = 0, bnd = 0, NB = 0;
-  const bool buckets = !e->radix_cells && bucket_geometry(e->net.n_marks, &bsh, &bnd, &NB) == 0;
   int64_t H = 0, T = 0;
+  // k_connect's chunk table: its capacity is kept across steps (grown on
+  // overflow and redone); the bucket path fills it in its pair-cell gather
+  int64_t bcap = std::max<int64_t>(e->bcell.bytes / sizeof(int32_t), 4096);
+  if (buf_ensure(e->bcell, bcap * sizeof(int32_t), s)) return -1;
   if (buckets) {
     // spatial buckets, every count on the device (bucket.hip)
+    void* const bk0 = e->bk[0].p;
+    void* const bk1 = e->bk[1].p;
     if (buf_ensure(e->bk[0], NB * sizeof(int32_t), s)) return -1;        // counts
     if (buf_ensure(e->bk[1], NB * sizeof(int32_t), s)) return -1;        // cursors
+    if (e->bk[0].p != bk0 || e->bk[1].p != bk1) e->bk_clean = false;     // fresh memory
     if (buf_ensure(e->bk[2], (NB + 1) * sizeof(int64_t), s)) return -1;  // bases
     if (buf_ensure(e->bk[3], NB * sizeof(int32_t), s)) return -1;        // pair cells
     if (buf_ensure(e->bk[4], NB * sizeof(int64_t), s)) return -1;        // pairs
@@ -877,9 +889,10 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     if (buf_ensure(e->bk[13], (NB + 1) * sizeof(int64_t), s)) return -1;
     if (buf_ensure(e->sents, TB * sizeof(uint64_t), s)) return -1;
     TIMED("bucket_entries", 24.0 * M,
-          launch_bucket_entries(P<int32_t>(e->members), M, grid, zero, idx, e->net.n_marks,
+          launch_bucket_entries(P<int32_t>(e->members), S, V, M, grid, zero, idx, e->net.n_marks,
                                 P<int32_t>(e->bk[0]), P<int32_t>(e->bk[1]), P<int64_t>(e->bk[2]),
-                                P<int64_t>(e->bk[7]), P<uint64_t>(e->sents), ctr, s));
+                                P<int64_t>(e->bk[7]), P<uint64_t>(e->sents), e->bk_clean, ctr, s));
+    e->bk_clean = false;  // until the gather below has reset the counters
     TIMED("bucket_group", 0.0,
           launch_bucket_pairs(e->net.n_marks, P<int64_t>(e->bk[2]), P<uint64_t>(e->sents),
                               P<uint64_t>(c.pz), P<CellEnt>(e->ents),
@@ -887,7 +900,10 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
                               P<int64_t>(e->bk[11]), P<int32_t>(e->bk[3]), P<int64_t>(e->bk[4]),
                               P<int64_t>(e->bk[12]), P<int64_t>(e->bk[13]),
                               P<int64_t>(e->bk[5]), P<int64_t>(e->bk[6]), P<int32_t>(e->pcell),
-                              P<int32_t>(e->pent), P<int32_t>(e->pcn), P<int64_t>(e->ptoff), ctr, s));
+                              P<int32_t>(e->pent), P<int32_t>(e->pcn), P<int64_t>(e->ptoff),
+                              P<int32_t>(e->bcell), bcap, P<int32_t>(e->bk[0]), P<int32_t>(e->bk[1]), ctr,
+                              s));
+    e->bk_clean = true;
   } else {
     // radix-sort path (grids finer than the bucket geometry, TNP_RADIX_CELLS=1)
     if (buf_ensure(e->spcnt, std::max<int64_t>(M, 1) * sizeof(int32_t), s)) return -1;
@@ -955,10 +971,9 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   // connecting edges this step's pruning drops are never appended (sorted,
   // re-tested): keep_edge() depends on the endpoints only
   const uint64_t cfmask = prune ? prune_mask(idx, K - 1) : 0ull;
-  int64_t bcap = std::max<int64_t>(e->bcell.bytes / sizeof(int32_t), 4096);
   int64_t cap = std::max<int64_t>(e->ckeys_a.bytes / sizeof(uint64_t), 4 * M + 1024);
   int64_t X = 0, TT = 0;
-  bool chunks_ok = false;
+  bool chunks_ok = buckets;  // the bucket path's gather filled the chunk table
   for (int attempt = 0; attempt < 3; ++attempt) {
     if (!chunks_ok) {
       if (buf_ensure(e->bcell, bcap * sizeof(int32_t), s)) return -1;
@@ -1244,8 +1259,10 @@ extern "C" int tnp_engine_lattice(tnp_engine* e, int x0, int x1, int keep_all, v
   hipLaunchKernelGGL(k_lattice_edges, dim3(tnp_grid(E)), dim3(TNP_BLOCK), 0, s, N, nx,
                      P<int32_t>(e->edges));
   TNP_CHECK(hipGetLastError());
-  if (launch_forward(e->net, P<float>(e->cur.xyz), V, P<float>(e->cur.pre), e->cur.cap, 1, s)) return -1;
-  if (keys_for(e, e->cur, 0, V, s)) return -1;
+  if (launch_forward(e->net, P<float>(e->cur.xyz), V, P<float>(e->cur.pre), e->cur.cap, 1, s, nullptr,
+                     P<uint64_t>(e->cur.pos), P<uint64_t>(e->cur.zero), P<uint64_t>(e->cur.grid),
+                     P<uint64_t>(e->cur.pz)))
+    return -1;
   e->V = V;
   e->E = E;
   e->keep_all = keep_all;
@@ -1359,8 +1376,10 @@ extern "C" int tnp_engine_skeleton(tnp_engine* e, int unit, float size, void* st
     e->V = V;
     e->E = total;
   }
-  if (launch_forward(e->net, P<float>(e->cur.xyz), e->V, P<float>(e->cur.pre), e->cur.cap, 1, s)) return -1;
-  if (keys_for(e, e->cur, 0, e->V, s)) return -1;
+  if (launch_forward(e->net, P<float>(e->cur.xyz), e->V, P<float>(e->cur.pre), e->cur.cap, 1, s, nullptr,
+                     P<uint64_t>(e->cur.pos), P<uint64_t>(e->cur.zero), P<uint64_t>(e->cur.grid),
+                     P<uint64_t>(e->cur.pz)))
+    return -1;
   e->keep_all = 0;
   *V_out = e->V;
   *E_out = e->E;

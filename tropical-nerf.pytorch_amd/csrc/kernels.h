@@ -31,8 +31,12 @@ int net_supported(const NetDev& n);  // 1 if an instantiation exists
 
 // ---- net.hip ----
 // pre plane-major [K][ld]; rows [0, n)
+// pos/zero/grid/pz (group 1 only): the packed keys of k_keys written by the
+// same pass (pre must then hold every plane: keys cover planes [0, K))
 int launch_forward(const NetDev& net, const float* xyz, int64_t n, float* pre,
-                   int64_t ld, int group, hipStream_t s, float* out2 = nullptr);
+                   int64_t ld, int group, hipStream_t s, float* out2 = nullptr,
+                   uint64_t* pos = nullptr, uint64_t* zero = nullptr, uint64_t* grid = nullptr,
+                   uint64_t* pz = nullptr);
 // new vertices of a flat step, forward with the fused epilogue (net.hip
 // k_forward_new); col != null: the split points are computed here too from
 // the plane column (xyz = slot V: written); cache planes >= keep_from at

@@ -35,7 +35,8 @@ namespace {
 template <int LV, int H, int NL, bool GROUPED>
 __global__ void __launch_bounds__(TNP_BLOCK)
 k_forward(NetDev net, const float* __restrict__ xyz, int64_t n, float* __restrict__ pre,
-          int64_t ld, float* __restrict__ out2) {
+          int64_t ld, float* __restrict__ out2, uint64_t* __restrict__ kpos, uint64_t* __restrict__ kzero,
+          uint64_t* __restrict__ kgrid, ulonglong2* __restrict__ kpz) {
   constexpr int IN = 2 * LV;
   constexpr int NW = H * IN + H + (NL - 2) * (H * H + H) + 2 * H + 2;
   __shared__ float w[NW];
@@ -51,6 +52,7 @@ k_forward(NetDev net, const float* __restrict__ xyz, int64_t n, float* __restric
   const float* W = w;
   int p = 0;
   const int mh = lin_mode(n, false), mo = lin_mode(n, true);
+  uint64_t ps = 0, zs = 0;  // packed eps-sign keys (k_keys), when kpos is given
 #pragma unroll
   for (int layer = 0; layer < NL - 1; ++layer) {
     if (layer == 0) {
@@ -62,6 +64,8 @@ k_forward(NetDev net, const float* __restrict__ xyz, int64_t n, float* __restric
     }
 #pragma unroll
     for (int j = 0; j < H; ++j) {
+      ps |= (uint64_t)(a[j] > net.eps) << (p + j);
+      zs |= (uint64_t)(fabsf(a[j]) <= net.eps) << (p + j);
       if (live && pre) pre[(int64_t)(p + j) * ld + i] = a[j];
       if (GROUPED) {
         const int base = (threadIdx.x & 63) & ~7;
@@ -77,10 +81,19 @@ k_forward(NetDev net, const float* __restrict__ xyz, int64_t n, float* __restric
   }
   float o[2];
   linear_mode<H, 2>(W, W + 2 * H, h, o, mo);
-  if (live && pre) pre[(int64_t)p * ld + i] = __fsub_rn(o[1], o[0]);
+  const float v = __fsub_rn(o[1], o[0]);
+  if (live && pre) pre[(int64_t)p * ld + i] = v;
   if (live && out2) {
     out2[2 * i] = o[0];
     out2[2 * i + 1] = o[1];
+  }
+  if (!GROUPED && live && kpos) {  // the keys of k_keys, from the values in registers
+    ps |= (uint64_t)(v > net.eps) << p;
+    zs |= (uint64_t)(fabsf(v) <= net.eps) << p;
+    kpos[i] = ps;
+    kzero[i] = zs;
+    kpz[i] = make_ulonglong2(ps, zs);
+    kgrid[i] = grid_word(net.marks, net.n_marks, net.eps, x);
   }
 }
 
@@ -310,17 +323,19 @@ int net_supported(const NetDev& n) {
 }
 
 int launch_forward(const NetDev& net, const float* xyz, int64_t n, float* pre, int64_t ld,
-                   int group, hipStream_t s, float* out2) {
+                   int group, hipStream_t s, float* out2, uint64_t* pos, uint64_t* zero, uint64_t* grid,
+                   uint64_t* pz) {
   if (n <= 0) return 0;
   if (!net_supported(net)) { tnp_set_error("unsupported net shape"); return -1; }
   if (group != 1 && (group != 8 || n % 8)) { tnp_set_error("group must be 1 or 8 (n%%8==0)"); return -1; }
   TNP_DISPATCH(net.n_levels, {
     if (group == 8)
       hipLaunchKernelGGL((k_forward<L_, 16, 3, true>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s,
-                         net, xyz, n, pre, ld, out2);
+                         net, xyz, n, pre, ld, out2, nullptr, nullptr, nullptr, nullptr);
     else
       hipLaunchKernelGGL((k_forward<L_, 16, 3, false>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s,
-                         net, xyz, n, pre, ld, out2);
+                         net, xyz, n, pre, ld, out2, pos, zero, grid,
+                         reinterpret_cast<ulonglong2*>(pz));
   });
   TNP_CHECK(hipGetLastError());
   return 0;

@@ -168,21 +168,29 @@ int bucket_geometry(int n_marks, int* sh, int* NBd, int* NB);
 // bbase: NB + 1, part: ceil(M / 2048) + 1 int64; ekey/ev: 8 M capacity
 // ekv: the entries in bucket order, packed (local cell << 40 | cell flags
 // << 32 | vertex) (8 M capacity)
-int launch_bucket_entries(const int32_t* members, int64_t M, const uint64_t* grid, const uint64_t* zero,
-                          int idx, int n_marks, int32_t* bcount, int32_t* bcur, int64_t* bbase,
-                          int64_t* part, uint64_t* ekv, int64_t* ctr, hipStream_t s);
+// members: the step's S new vertices are slots V.. (not listed), the hits
+// follow in members[S, M).  clean: bcount/bcur are known to be zero (the
+// previous step's launch_bucket_pairs reset them)
+int launch_bucket_entries(const int32_t* members, int64_t S, int64_t V, int64_t M, const uint64_t* grid,
+                          const uint64_t* zero, int idx, int n_marks, int32_t* bcount, int32_t* bcur,
+                          int64_t* bbase, int64_t* part, uint64_t* ekv, bool clean, int64_t* ctr,
+                          hipStream_t s);
 // per bucket: cell-contiguous CellEnt records (ents, entry positions), the
 // pair cells; then the global pair-cell list (pcell, pent, pn, ptoff; R ->
 // ctr[CTR_R], pairs -> ctr[CTR_TESTS]) that launch_connect walks.
 // lcell/lent/ln/lpoff: 4 M + 1 capacity; bnpc/bnpairs: NB; pcoff/pairoff: NB + 1
-// Cells above WCELL members go to the pair-cell list; the pairs of the
-// others -> ctr[CTR_SPAIRS] (bspairs/spoff: NB / NB + 1 int64 scratch).
+// Cells above WCELL members go to the pair-cell list (and k_connect's chunk
+// table bcell, bcap chunks, overflow -> CTR_BOVF); the pairs of the others
+// -> ctr[CTR_SPAIRS] (bspairs/spoff: NB / NB + 1 int64 scratch).  Leaves
+// bcount/bcur zeroed for the next step.
 int launch_bucket_pairs(int n_marks, const int64_t* bbase, const uint64_t* ekv, const uint64_t* pz,
                         CellEnt* ents, int32_t* lcell,
                         int32_t* lent, int32_t* ln, int64_t* lpoff, int32_t* bnpc, int64_t* bnpairs,
                         int64_t* bspairs, int64_t* spoff, int64_t* pcoff, int64_t* pairoff,
-                        int32_t* pcell, int32_t* pent, int32_t* pn, int64_t* ptoff, int64_t* ctr,
-                        hipStream_t s);
+                        int32_t* pcell, int32_t* pent, int32_t* pn, int64_t* ptoff, int32_t* bcell,
+                        int64_t bcap, int32_t* bcount, int32_t* bcur, int64_t* ctr, hipStream_t s);
+// pair indices per k_connect chunk (its bcell table granularity)
+int64_t connect_chunk_pairs();
 // window pass over the cell-contiguous entries (count ctr[CTR_T]): every
 // pair of a cell of <= WCELL members, same emission rules and counters as
 // launch_connect (bstat: its own 3 * connect_grid() slots; sum with

@@ -1276,6 +1276,7 @@ static int connect_grid_size() {
   return std::max(resident_grid(k_connect, 0), resident_grid(k_connect_win, 1));
 }
 int64_t connect_chunks(int64_t TT) { return (TT + CCH - 1) / CCH; }
+int64_t connect_chunk_pairs() { return CCH; }
 int launch_chunk_cells(const int64_t* ptoff, const int32_t* pn, int64_t rcap, int32_t* bcell,
                        int64_t cap, int64_t* ctr, hipStream_t s) {
   hipLaunchKernelGGL(k_chunk_cells, dim3(tnp_grid(rcap)), dim3(TNP_BLOCK), 0, s, ptoff, pn, rcap,
