@@ -11,10 +11,10 @@
 //   curve_corners 8 box corners per c row (corner 4i+2j+k: x from endpoint
 //                 k, y from j, z from i) + the shared plane p
 //   forward(group=8) over the corners (one activation pattern per box)
-//   curve_solve   quartic in x from the corner values, largest real root in
-//                 [0,1] (the reference's last LAPACK eigenvalue in [0,1] --
-//                 every multi-root case of the goldens is the largest one),
-//                 y from the quadratic ratio, bilinear boxes -> -1
+//   curve_solve   quartic in x from the corner values, the last real root in
+//                 [0,1] in LAPACK's eigenvalue order (sgeev restated for
+//                 companions of degree 2..4), y from the quadratic ratio,
+//                 bilinear boxes -> -1
 //   forward over e0(1-t) + e1 t, curve_dnew  residuals on p and q
 //   descend       normalised gradient descent of p^2 + q^2 (500 iterations
 //                 max, all rows stop together: pass 1 records per-iteration
@@ -23,9 +23,10 @@
 //   (finish) strict_keep + compact_splits: dropped splits stay unsplit, new
 //                 vertex ids follow the surviving edges' order
 //
-// Roots are isolated in double precision (derivative brackets + bisection),
-// so vertices agree with the reference's fp32 LAPACK path to ~1e-7, not
-// bitwise (curve path tolerance 1e-5).
+// Degree 2 reproduces MKL's sgeev bitwise; degree 3/4 follow reference
+// LAPACK's fp32 algorithm (same eigenvalue order as MKL, values to fp32
+// rounding), so vertices agree with the reference to ~1e-7, not bitwise
+// (curve path tolerance 1e-5).
 #include "common.h"
 #include "kernels.h"
 #include "net_device.h"
@@ -79,63 +80,6 @@ __global__ void k_curve_corners(const int32_t* __restrict__ crow, int64_t B,
     if (!m) atomicOr((unsigned long long*)&ctr[CTR_NOPLANE], 1ull);
   }
 }
-
-// ---- polynomial roots in [0, 1] ---------------------------------------------
-// p(x) = a[0] x^N + ... + a[N]; ascending real roots in [0, 1] via the roots
-// of p' as brackets (monotone between them) and bisection to full double
-// precision.
-template <int N>
-struct Roots01 {
-  __device__ static double eval(const double* a, double x) {
-    double r = a[0];
-#pragma unroll
-    for (int k = 1; k <= N; ++k) r = fma(r, x, a[k]);
-    return r;
-  }
-  __device__ static int find(const double* a, double* out) {
-    double da[N];
-#pragma unroll
-    for (int k = 0; k < N; ++k) da[k] = a[k] * (double)(N - k);
-    double br[N + 1];
-    int nb = Roots01<N - 1>::find(da, br + 1);
-    br[0] = 0.0;
-    br[nb + 1] = 1.0;
-    int n = 0;
-    for (int i = 0; i <= nb; ++i) {
-      double lo = br[i], hi = br[i + 1];
-      double flo = eval(a, lo), fhi = eval(a, hi);
-      if (flo == 0.0) {
-        if (n == 0 || out[n - 1] != lo) out[n++] = lo;
-        continue;
-      }
-      if ((flo < 0.0) == (fhi < 0.0) || fhi == 0.0) continue;
-      for (int it = 0; it < 80 && lo < hi; ++it) {
-        double mid = 0.5 * (lo + hi);
-        if (mid <= lo || mid >= hi) break;
-        double fm = eval(a, mid);
-        if (fm == 0.0) { lo = hi = mid; break; }
-        if ((fm < 0.0) == (flo < 0.0)) lo = mid;
-        else hi = mid;
-      }
-      out[n++] = 0.5 * (lo + hi);
-    }
-    if (eval(a, 1.0) == 0.0 && (n == 0 || out[n - 1] != 1.0)) out[n++] = 1.0;
-    return n;
-  }
-};
-template <>
-struct Roots01<1> {
-  __device__ static int find(const double* a, double* out) {
-    if (a[0] == 0.0) return 0;
-    double r = -a[1] / a[0];
-    if (r >= 0.0 && r <= 1.0) {
-      out[0] = r;
-      return 1;
-    }
-    return 0;
-  }
-};
-
 
 // ---- sgeev on a 2x2 real matrix, as x86 MKL computes it ---------------------
 // (torch.linalg.eigvals on the quadratics' companion matrices -- 98% of the
@@ -321,10 +265,314 @@ __device__ void eig2x2(float A[2][2], float wr[2], float wi[2]) {
   slanv2(A[0][0], A[0][1], A[1][0], A[1][1], wr, wi);
 }
 
+// ---- sgeev (eigenvalues only) on a 3x3 / 4x4 real matrix, reference LAPACK --
+// sgebal('B') -> sgehd2 -> slahqr in fp32 with explicit roundings
+// (tools/lapack_eig_port.py is the host restatement).  What the reference's
+// "last real root in [0, 1]" (geometry.py:292-296) depends on is the ORDER
+// of the eigenvalues: the restatement's order equals x86 MKL's
+// (torch.linalg.eigvals) on every random companion checked; the values
+// agree to fp32 rounding, ~1e-4 only for clustered (ill-conditioned) roots.
+template <int N>
+struct SmallEig {
+  float H[N][N];
+  float wr[N], wi[N];
+
+  __device__ static float nrm(const float* v, int n, int stride) {
+    double s = 0.0;
+    for (int i = 0; i < n; ++i) s += (double)v[i * stride] * (double)v[i * stride];
+    return (float)sqrt(s);
+  }
+  // slarfg on (alpha, x[0..n1)): beta -> alpha, tau returned, x scaled
+  __device__ static float slarfg(float& alpha, float* x, int n1) {
+    if (n1 <= 0) return 0.f;
+    double s = 0.0;
+    for (int i = 0; i < n1; ++i) s += (double)x[i] * (double)x[i];
+    const float xnorm = (float)sqrt(s);
+    if (xnorm == 0.f) return 0.f;
+    const float beta = -fsign(slapy2(alpha, xnorm), alpha);
+    const float tau = __fdiv_rn(__fsub_rn(beta, alpha), beta);
+    const float sc = __fdiv_rn(1.f, __fsub_rn(alpha, beta));
+    for (int i = 0; i < n1; ++i) x[i] = __fmul_rn(x[i], sc);
+    alpha = beta;
+    return tau;
+  }
+
+  __device__ void balance(int& k, int& l) {
+    k = 0;
+    l = N - 1;
+    for (;;) {  // rows with zero off-diagonal (columns 0..l) pushed down
+      int found = -1;
+      for (int j = l; j >= 0 && found < 0; --j) {
+        bool z = true;
+        for (int i = 0; i <= l; ++i)
+          if (i != j && H[j][i] != 0.f) z = false;
+        if (z) found = j;
+      }
+      if (found < 0) break;
+      if (found != l) {
+        for (int r = 0; r < N; ++r) { const float t = H[r][found]; H[r][found] = H[r][l]; H[r][l] = t; }
+        for (int c = 0; c < N; ++c) { const float t = H[found][c]; H[found][c] = H[l][c]; H[l][c] = t; }
+      }
+      if (l == 0) { k = l = 0; return; }
+      --l;
+    }
+    for (;;) {  // columns with zero off-diagonal (rows k..l) pushed left
+      int found = -1;
+      for (int j = k; j <= l && found < 0; ++j) {
+        bool z = true;
+        for (int i = k; i <= l; ++i)
+          if (i != j && H[i][j] != 0.f) z = false;
+        if (z) found = j;
+      }
+      if (found < 0) break;
+      if (found != k) {
+        for (int r = 0; r < N; ++r) { const float t = H[r][found]; H[r][found] = H[r][k]; H[r][k] = t; }
+        for (int c = 0; c < N; ++c) { const float t = H[found][c]; H[found][c] = H[k][c]; H[k][c] = t; }
+      }
+      ++k;
+    }
+    if (k >= l) return;
+    const float SAFMIN = 1.17549435e-38f, ULP = 1.1920928955078125e-07f;
+    const float SFMIN1 = SAFMIN / ULP, SFMAX1 = 1.f / SFMIN1;
+    const float SFMIN2 = SFMIN1 * 2.f, SFMAX2 = 1.f / SFMIN2;
+    float scale[N];
+    for (int i = 0; i < N; ++i) scale[i] = 1.f;
+    for (int pass = 0; pass < 100; ++pass) {
+      bool noconv = false;
+      for (int i = k; i <= l; ++i) {
+        float c = nrm(&H[k][i], l - k + 1, N);
+        float r = nrm(&H[i][k], l - k + 1, 1);
+        float ca = 0.f, ra = 0.f;
+        for (int q = 0; q <= l; ++q) ca = fmaxf(ca, fabsf(H[q][i]));
+        for (int q = k; q < N; ++q) ra = fmaxf(ra, fabsf(H[i][q]));
+        if (c == 0.f || r == 0.f) continue;
+        float g = r / 2.f, f = 1.f;
+        const float s = __fadd_rn(c, r);
+        while (!(c >= g || fmaxf(f, fmaxf(c, ca)) >= SFMAX2 || fminf(r, fminf(g, ra)) <= SFMIN2)) {
+          f *= 2.f; c *= 2.f; ca *= 2.f; r /= 2.f; g /= 2.f; ra /= 2.f;
+        }
+        g = c / 2.f;
+        while (!(g < r || fmaxf(r, ra) >= SFMAX2 || fminf(fminf(f, c), fminf(g, ca)) <= SFMIN2)) {
+          f /= 2.f; c /= 2.f; g /= 2.f; ca /= 2.f; r *= 2.f; ra *= 2.f;
+        }
+        if (__fadd_rn(c, r) >= __fmul_rn(0.95f, s)) continue;
+        if (f < 1.f && scale[i] < 1.f && f * scale[i] <= SFMIN1) continue;
+        if (f > 1.f && scale[i] > 1.f && scale[i] >= SFMAX1 / f) continue;
+        const float gi = 1.f / f;
+        scale[i] *= f;
+        noconv = true;
+        for (int q = k; q < N; ++q) H[i][q] = __fmul_rn(H[i][q], gi);
+        for (int q = 0; q <= l; ++q) H[q][i] = __fmul_rn(H[q][i], f);
+      }
+      if (!noconv) break;
+    }
+  }
+
+  __device__ void hessenberg(int ilo, int ihi) {  // sgehd2
+    for (int i = ilo; i < ihi; ++i) {
+      float x[N];
+      const int n1 = ihi - i - 1;
+      for (int j = 0; j < n1; ++j) x[j] = H[i + 2 + j][i];
+      float alpha = H[i + 1][i];
+      const float tau = slarfg(alpha, x, n1);
+      H[i + 1][i] = alpha;
+      for (int j = 0; j < n1; ++j) H[i + 2 + j][i] = x[j];
+      if (tau == 0.f) continue;
+      float v[N];
+      v[0] = 1.f;
+      for (int j = 0; j < n1; ++j) v[j + 1] = x[j];
+      const int nv = n1 + 1;
+      for (int r = 0; r <= ihi; ++r) {  // right: C -= tau (C v) v^T
+        float w = 0.f;
+        for (int q = 0; q < nv; ++q) w = __fadd_rn(w, __fmul_rn(H[r][i + 1 + q], v[q]));
+        for (int q = 0; q < nv; ++q) H[r][i + 1 + q] = __fsub_rn(H[r][i + 1 + q], __fmul_rn(__fmul_rn(tau, w), v[q]));
+      }
+      for (int c = i + 1; c < N; ++c) {  // left: C -= tau v (v^T C)
+        float w = 0.f;
+        for (int q = 0; q < nv; ++q) w = __fadd_rn(w, __fmul_rn(H[i + 1 + q][c], v[q]));
+        for (int q = 0; q < nv; ++q) H[i + 1 + q][c] = __fsub_rn(H[i + 1 + q][c], __fmul_rn(__fmul_rn(tau, v[q]), w));
+      }
+    }
+    for (int i = ilo; i < ihi; ++i)
+      for (int j = i + 2; j < N; ++j) H[j][i] = 0.f;
+  }
+
+  // slahqr (WANTT = WANTZ = false); false if it did not converge
+  __device__ bool qr(int ilo, int ihi) {
+    const float SAFMIN = 1.17549435e-38f, ULP = 1.1920928955078125e-07f;
+    for (int i = 0; i < N; ++i) { wr[i] = H[i][i]; wi[i] = 0.f; }
+    if (ilo == ihi) return true;
+    for (int j = ilo; j < ihi - 2; ++j) { H[j + 2][j] = 0.f; H[j + 3][j] = 0.f; }
+    if (ilo <= ihi - 2) H[ihi][ihi - 2] = 0.f;
+    const int nh = ihi - ilo + 1;
+    const float smlnum = __fmul_rn(SAFMIN, __fdiv_rn((float)nh, ULP));
+    const int itmax = 30 * (nh > 10 ? nh : 10);
+    int kdefl = 0;
+    int i = ihi;
+    while (i >= ilo) {
+      int l = ilo;
+      bool conv = false;
+      for (int its = 0; its <= itmax; ++its) {
+        int k = i;
+        for (; k > l; --k) {
+          if (fabsf(H[k][k - 1]) <= smlnum) break;
+          float tst = __fadd_rn(fabsf(H[k - 1][k - 1]), fabsf(H[k][k]));
+          if (tst == 0.f) {
+            if (k - 2 >= ilo) tst = __fadd_rn(tst, fabsf(H[k - 1][k - 2]));
+            if (k + 1 <= ihi) tst = __fadd_rn(tst, fabsf(H[k + 1][k]));
+          }
+          if (fabsf(H[k][k - 1]) <= __fmul_rn(ULP, tst)) {
+            const float ab = fmaxf(fabsf(H[k][k - 1]), fabsf(H[k - 1][k]));
+            const float ba = fminf(fabsf(H[k][k - 1]), fabsf(H[k - 1][k]));
+            const float dd = fabsf(__fsub_rn(H[k - 1][k - 1], H[k][k]));
+            const float aa = fmaxf(fabsf(H[k][k]), dd), bb = fminf(fabsf(H[k][k]), dd);
+            const float s = __fadd_rn(aa, ab);
+            if (__fmul_rn(ba, __fdiv_rn(ab, s)) <= fmaxf(smlnum, __fmul_rn(ULP, __fmul_rn(bb, __fdiv_rn(aa, s)))))
+              break;
+          }
+        }
+        l = k;
+        if (l > ilo) H[l][l - 1] = 0.f;
+        if (l >= i - 1) { conv = true; break; }
+        ++kdefl;
+        const int i1 = l, i2 = i;
+        float h11, h12, h21, h22;
+        if (kdefl % 20 == 0) {
+          const float s = __fadd_rn(fabsf(H[i][i - 1]), fabsf(H[i - 1][i - 2]));
+          h11 = __fadd_rn(__fmul_rn(0.75f, s), H[i][i]); h12 = __fmul_rn(-0.4375f, s); h21 = s; h22 = h11;
+        } else if (kdefl % 10 == 0) {
+          const float s = __fadd_rn(fabsf(H[l + 1][l]), fabsf(H[l + 2][l + 1]));
+          h11 = __fadd_rn(__fmul_rn(0.75f, s), H[l][l]); h12 = __fmul_rn(-0.4375f, s); h21 = s; h22 = h11;
+        } else {
+          h11 = H[i - 1][i - 1]; h21 = H[i][i - 1]; h12 = H[i - 1][i]; h22 = H[i][i];
+        }
+        float rt1r, rt1i, rt2r, rt2i;
+        float s = __fadd_rn(__fadd_rn(__fadd_rn(fabsf(h11), fabsf(h12)), fabsf(h21)), fabsf(h22));
+        if (s == 0.f) {
+          rt1r = rt1i = rt2r = rt2i = 0.f;
+        } else {
+          h11 = __fdiv_rn(h11, s); h21 = __fdiv_rn(h21, s); h12 = __fdiv_rn(h12, s); h22 = __fdiv_rn(h22, s);
+          const float tr = __fdiv_rn(__fadd_rn(h11, h22), 2.f);
+          const float det = __fsub_rn(__fmul_rn(__fsub_rn(h11, tr), __fsub_rn(h22, tr)), __fmul_rn(h12, h21));
+          const float rtdisc = __fsqrt_rn(fabsf(det));
+          if (det >= 0.f) {
+            rt1r = __fmul_rn(tr, s); rt2r = rt1r; rt1i = __fmul_rn(rtdisc, s); rt2i = -rt1i;
+          } else {
+            rt1r = __fadd_rn(tr, rtdisc); rt2r = __fsub_rn(tr, rtdisc);
+            if (fabsf(__fsub_rn(rt1r, h22)) <= fabsf(__fsub_rn(rt2r, h22))) { rt1r = __fmul_rn(rt1r, s); rt2r = rt1r; }
+            else { rt2r = __fmul_rn(rt2r, s); rt1r = rt2r; }
+            rt1i = rt2i = 0.f;
+          }
+        }
+        int m = i - 2;
+        float v[3];
+        for (;;) {
+          float h21s = H[m + 1][m];
+          s = __fadd_rn(__fadd_rn(fabsf(__fsub_rn(H[m][m], rt2r)), fabsf(rt2i)), fabsf(h21s));
+          h21s = __fdiv_rn(H[m + 1][m], s);
+          v[0] = __fsub_rn(__fadd_rn(__fmul_rn(h21s, H[m][m + 1]),
+                                     __fmul_rn(__fsub_rn(H[m][m], rt1r), __fdiv_rn(__fsub_rn(H[m][m], rt2r), s))),
+                           __fmul_rn(rt1i, __fdiv_rn(rt2i, s)));
+          v[1] = __fmul_rn(h21s, __fsub_rn(__fsub_rn(__fadd_rn(H[m][m], H[m + 1][m + 1]), rt1r), rt2r));
+          v[2] = __fmul_rn(h21s, H[m + 2][m + 1]);
+          s = __fadd_rn(__fadd_rn(fabsf(v[0]), fabsf(v[1])), fabsf(v[2]));
+          v[0] = __fdiv_rn(v[0], s); v[1] = __fdiv_rn(v[1], s); v[2] = __fdiv_rn(v[2], s);
+          if (m == l) break;
+          const float h00 = __fmul_rn(fabsf(H[m][m - 1]), __fadd_rn(fabsf(v[1]), fabsf(v[2])));
+          const float h01 = __fmul_rn(__fmul_rn(ULP, fabsf(v[0])),
+                                      __fadd_rn(__fadd_rn(fabsf(H[m - 1][m - 1]), fabsf(H[m][m])), fabsf(H[m + 1][m + 1])));
+          if (h00 <= h01) break;
+          --m;
+        }
+        for (int k2 = m; k2 < i; ++k2) {
+          const int nr = (3 < i - k2 + 1) ? 3 : i - k2 + 1;
+          if (k2 > m)
+            for (int q = 0; q < nr; ++q) v[q] = H[k2 + q][k2 - 1];
+          float alpha = v[0];
+          const float t1 = slarfg(alpha, v + 1, nr - 1);
+          v[0] = alpha;
+          if (k2 > m) {
+            H[k2][k2 - 1] = v[0];
+            H[k2 + 1][k2 - 1] = 0.f;
+            if (k2 < i - 1) H[k2 + 2][k2 - 1] = 0.f;
+          } else if (m > l) {
+            H[k2][k2 - 1] = __fmul_rn(H[k2][k2 - 1], __fsub_rn(1.f, t1));
+          }
+          const float v2 = v[1], t2 = __fmul_rn(t1, v2);
+          if (nr == 3) {
+            const float v3 = v[2], t3 = __fmul_rn(t1, v3);
+            for (int j = k2; j <= i2; ++j) {
+              const float sm = __fadd_rn(__fadd_rn(H[k2][j], __fmul_rn(v2, H[k2 + 1][j])), __fmul_rn(v3, H[k2 + 2][j]));
+              H[k2][j] = __fsub_rn(H[k2][j], __fmul_rn(sm, t1));
+              H[k2 + 1][j] = __fsub_rn(H[k2 + 1][j], __fmul_rn(sm, t2));
+              H[k2 + 2][j] = __fsub_rn(H[k2 + 2][j], __fmul_rn(sm, t3));
+            }
+            const int jend = (k2 + 3 < i) ? k2 + 3 : i;
+            for (int j = i1; j <= jend; ++j) {
+              const float sm = __fadd_rn(__fadd_rn(H[j][k2], __fmul_rn(v2, H[j][k2 + 1])), __fmul_rn(v3, H[j][k2 + 2]));
+              H[j][k2] = __fsub_rn(H[j][k2], __fmul_rn(sm, t1));
+              H[j][k2 + 1] = __fsub_rn(H[j][k2 + 1], __fmul_rn(sm, t2));
+              H[j][k2 + 2] = __fsub_rn(H[j][k2 + 2], __fmul_rn(sm, t3));
+            }
+          } else if (nr == 2) {
+            for (int j = k2; j <= i2; ++j) {
+              const float sm = __fadd_rn(H[k2][j], __fmul_rn(v2, H[k2 + 1][j]));
+              H[k2][j] = __fsub_rn(H[k2][j], __fmul_rn(sm, t1));
+              H[k2 + 1][j] = __fsub_rn(H[k2 + 1][j], __fmul_rn(sm, t2));
+            }
+            for (int j = i1; j <= i; ++j) {
+              const float sm = __fadd_rn(H[j][k2], __fmul_rn(v2, H[j][k2 + 1]));
+              H[j][k2] = __fsub_rn(H[j][k2], __fmul_rn(sm, t1));
+              H[j][k2 + 1] = __fsub_rn(H[j][k2 + 1], __fmul_rn(sm, t2));
+            }
+          }
+        }
+      }
+      if (!conv) return false;
+      if (l == i) {
+        wr[i] = H[i][i];
+        wi[i] = 0.f;
+      } else {
+        float w2r[2], w2i[2];
+        slanv2(H[i - 1][i - 1], H[i - 1][i], H[i][i - 1], H[i][i], w2r, w2i);
+        wr[i - 1] = w2r[0]; wr[i] = w2r[1]; wi[i - 1] = w2i[0]; wi[i] = w2i[1];
+      }
+      kdefl = 0;
+      i = l - 1;
+    }
+    return true;
+  }
+
+  // eigenvalues of H in LAPACK order; false: no convergence
+  __device__ bool solve() {
+    int k, l;
+    balance(k, l);
+    hessenberg(k, l);
+    return qr(k, l);
+  }
+};
+
+// the reference's choice for a companion of degree N (3 or 4): the last
+// eigenvalue in LAPACK order that is real and in [0, 1]; -1 if none
+template <int N>
+__device__ float last_root01(const float* c, int lead) {
+  SmallEig<N> e;
+  for (int r = 0; r < N; ++r)
+    for (int q = 0; q < N; ++q) e.H[r][q] = (q == r + 1) ? 1.f : 0.f;
+  // C[:, -1] = -coeffs[:-1] / coeffs[lead] on the flipped (ascending) row:
+  // last row entry q is -c_asc[q] / c_lead, c_asc[q] = c[lead + N - q]
+  for (int q = 0; q < N; ++q) e.H[N - 1][q] = __fdiv_rn(-c[lead + N - q], c[lead]);
+  if (!e.solve()) return -1.f;
+  float r = -1.f;
+  for (int q = 0; q < N; ++q)
+    if (fabsf(e.wi[q]) <= ROOT_EPS && e.wr[q] >= 0.f && e.wr[q] <= 1.f) r = e.wr[q];
+  return r;
+}
+
 // batched_polynomial_roots (geometry.py:259-299) for one row of 5 fp32
 // coefficients (leading first): tiny coefficients zeroed, degree from the
 // first non-zero one, companion row r_k = -c_k / c_lead in fp32 (what LAPACK
-// sees), largest real root in [0, 1], -1 if none.
+// sees), the last real eigenvalue in [0, 1] in LAPACK order, -1 if none.
 __device__ float largest_root01(float c[5]) {
 #pragma unroll
   for (int k = 0; k < 5; ++k)
@@ -351,19 +599,7 @@ __device__ float largest_root01(float c[5]) {
       if (fabsf(wi[k]) <= ROOT_EPS && wr[k] >= 0.f && wr[k] <= 1.f) r = wr[k];
     return r;
   }
-  double a[5];
-  a[0] = 1.0;
-  for (int k = 1; k <= N; ++k) a[k] = -(double)__fdiv_rn(-c[i + k], c[i]);
-  double rt[4];
-  int n = 0;
-  switch (N) {
-    case 2: n = Roots01<2>::find(a, rt); break;
-    case 3: n = Roots01<3>::find(a, rt); break;
-    default: n = Roots01<4>::find(a, rt); break;
-  }
-  if (n == 0) return -1.f;
-  float r = (float)rt[n - 1];
-  return (r >= 0.f && r <= 1.f) ? r : -1.f;
+  return N == 3 ? last_root01<3>(c, i) : last_root01<4>(c, i);
 }
 
 // intersection_of_two_planes (geometry.py:24-138), "xz" assumption
