@@ -38,20 +38,36 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-# per-kernel HBM bytes per launch from the committed rocprofv3 --pmc passes
-# (tools/pmc_summary.py: 2*FETCH_SIZE + WRITE_SIZE, gfx950 correction)
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01_bench128_seed6_pmc_traffic.json")
+# per-kernel HBM bytes per launch from the committed rocprofv3 --pmc passes of
+# this workload (tools/pmc_session.sh + tools/pmc_table.py: 2*FETCH_SIZE +
+# WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md "HBM")
+PMC_TABLE = os.path.join(ROOT, "profiles", "r02_bench128_seed6_pmc.json")
+# engine timer name -> device kernel symbol (profiles' short names)
+KERNEL_SYMBOL = {"forward_new": "k_forward_new", "prune": "k_prune_lb", "connect_win": "k_connect_win",
+                 "bucket_group": "k_bucket_group", "split": "k_split_lb", "hits": "k_hit_lb",
+                 "connect": "k_connect", "count_live": "k_count_flags", "override_new": "k_override_new"}
 
 
 def pmc_traffic(kernel: str, marks: int, seed: int):
-    """HBM traffic per launch of `kernel` measured by the PMC passes of the
-    same workload, or None (other workload, or no profile)."""
-    if marks != 128 or seed != 6 or not os.path.isfile(PMC_TRAFFIC):
+    """HBM bytes per launch of `kernel` measured by the PMC passes of the
+    same workload (None: other workload, or no profile)."""
+    if marks != 128 or seed != 6 or not os.path.isfile(PMC_TABLE):
         return None
-    with open(PMC_TRAFFIC) as f:
+    with open(PMC_TABLE) as f:
         ks = json.load(f)["kernels"]
-    k = ks.get("k_" + kernel)
-    return None if k is None else k["traffic_bytes_per_launch"]
+    k = ks.get(KERNEL_SYMBOL.get(kernel, "k_" + kernel))
+    return None if k is None else k.get("traffic_bytes_per_launch")
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def synthetic_params(G: int, seed: int = 0, amp: float = 0.1):
@@ -119,25 +135,24 @@ class Collective:
         return a.max(axis=0)
 
 
-def cpu_baseline(sample_marks: int, seed: int, threads: int):
+def cpu_baseline(G: int, slab: int, seed: int, threads: int):
     """The oracle (PyTorch-CPU restatement of the reference, same op sequence)
-    on a bounded sample: the same synthetic generator at sample_marks^3."""
+    on a bounded sample of the SAME workload: the x-slab of mark planes
+    [0, slab] of the G^3 lattice of the same net, every hyperplane step."""
     import oracle.subdivide as od
-    from tropical.synthetic import lattice_edges, lattice_vertices
+    from tropical.synthetic import slab_lattice
     torch.set_num_threads(threads)
-    cfg, p = synthetic_params(sample_marks, seed)
+    cfg, p = synthetic_params(G, seed)
     ref = od.load_params(od.RefNet(**cfg), p)
-    V = torch.from_numpy(lattice_vertices(ref.enc.marks.numpy()))
-    E = torch.from_numpy(lattice_edges(sample_marks))
+    V, E = slab_lattice(ref.enc.marks.numpy(), 0, slab)
+    V, E = torch.from_numpy(V), torch.from_numpy(E)
     stats = {}
     t0 = time.perf_counter()
     with torch.no_grad():
-        V, E, c = od.run_steps(V, E, ref, 1e-4, None, stats)
+        od.run_steps(V, E, ref, 1e-4, None, stats)
     dt = time.perf_counter() - t0
     S = sum(s["S"] for s in stats["steps"])
-    with torch.no_grad():
-        Vs, Es, used = od.extract_surface(V, E, ref, 1e-4, c)
-    return S / dt, S, dt, Vs
+    return S / dt, S, dt
 
 
 def small_net_check(dev, force: bool = True):
@@ -209,7 +224,9 @@ def main():
     # 12 contain regions of 1e5-1e7 vertices (seed 8: 5.5e13 in-region pairs)
     # that the reference's CPU path could not materialise (tools/seed_scan.py)
     ap.add_argument("--seed", type=int, default=6)
-    ap.add_argument("--cpu-sample-marks", type=int, default=int(os.environ.get("TNP_CPU_SAMPLE", 48)))
+    # the CPU baseline's sample: the x-slab of mark planes [0, N] of the
+    # benchmarked lattice (same net, same cell density), ~20 s of CPU work
+    ap.add_argument("--cpu-slab", type=int, default=int(os.environ.get("TNP_CPU_SLAB", 3)))
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
 
@@ -331,24 +348,29 @@ def main():
         per_pass = splits_tot / args.steps
         value = splits_tot / dt_max
         st0 = all_stats[0]
-        # dominant kernel: HIP events around each launch inside the engine
-        # among the hand-written HIP kernels: the *_sort entries are rocPRIM
-        # radix sorts (several library launches each, no single rocprof row)
+        # dominant kernel: HIP events around each launch inside the engine,
+        # among the hand-written HIP kernels (the *_sort entries are rocPRIM
+        # radix sorts: several library launches each, no single rocprof row)
         own = {k: v for k, v in ktime.items() if not k.endswith("_sort")}
         dom = max(own, key=lambda k: own[k]["ms"]) if own else None
         dom_all = max(ktime, key=lambda k: ktime[k]["ms"]) if ktime else None
         roof = None
+        loop_gbs = bytes_tot / dt_max / 1e9
         if dom:
             kt = ktime[dom]
             avg_ms = kt["ms"] / max(kt["launches"], 1)
-            alg = kt["bytes"] / max(kt["launches"], 1)
+            alg = kt["bytes"] / max(kt["launches"], 1)  # algorithmic bytes per launch
             ach = alg / (avg_ms * 1e-3) / 1e9
+            traffic = pmc_traffic(dom, G, args.seed) if world == 1 else None
             roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                    "traffic": pmc_traffic(dom, G, args.seed) if world == 1 else None,
+                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "traffic_gbs": None if traffic is None else round(traffic / (avg_ms * 1e-3) / 1e9, 1),
                     "avg_launch_us": round(avg_ms * 1e3, 2), "launches": kt["launches"],
-                    "alg_bytes_per_launch": int(alg), "dominant_overall": dom_all}
-        loop_gbs = bytes_tot / dt_max / 1e9
+                    "alg_bytes_per_launch": int(alg), "dominant_overall": dom_all,
+                    # the whole hyperplane loop against the same peak: SURVEY
+                    # §8d's per-step model (bench.algorithmic_bytes) / pass time
+                    "whole_loop_gbs": round(loop_gbs, 1),
+                    "whole_loop_frac": round(loop_gbs / (HBM_PEAK_GBS * world), 4)}
         out = {
             "metric": "edges subdivided/sec", "value": round(value, 1), "unit": "edges/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -370,11 +392,13 @@ def main():
             out["final_complex" if world == 1 else "stitched_complex"] = stitched
         if not args.no_cpu and world == 1:
             thr = max(1, min(16, len(os.sched_getaffinity(0))))
-            cps, S_cpu, t_cpu, Vs_cpu = cpu_baseline(args.cpu_sample_marks, args.seed, thr)
+            cps, S_cpu, t_cpu = cpu_baseline(G, args.cpu_slab, args.seed, thr)
             out["cpu_baseline"] = {
                 "value": round(cps, 1), "unit": "edges/s", "cores": thr, "kind": "port",
-                "sample": f"oracle (PyTorch-CPU restatement of the reference) on the same generator at "
-                          f"{args.cpu_sample_marks}^3: {S_cpu} splits in {t_cpu:.1f}s"}
+                "cpu": cpu_model(),
+                "sample": f"oracle (PyTorch-CPU restatement of the reference, pinned to its goldens) on "
+                          f"the x-slab of mark planes [0, {args.cpu_slab}] of this {G}^3 seed-{args.seed} "
+                          f"lattice (same net): {S_cpu} splits in {t_cpu:.1f}s"}
             out["gpu_over_cpu"] = round(value / cps, 1)
         if not args.no_cpu and world == 1:
             out["small_net"] = small_net_check(dev, force=True)

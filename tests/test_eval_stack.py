@@ -159,3 +159,35 @@ def test_gpu_train_cli_end_to_end(cuda, tmp_path, capsys):
     assert float(ours[3]) < 20.0  # angular distance: face normals agree with the MC normals
     assert (tmp_path / "bunny" / "our_mesh_small_45.ply").is_file()
     assert (tmp_path / "bunny" / "mc256_mesh_small_45.ply").is_file()
+
+
+def test_self_angular_distance_is_the_reference_normalisation(cuda):
+    """The 512 row's AD is the pseudo ground truth against ITSELF, yet not
+    0.0: the reference normalises face normals by (|c| + 1e-9)
+    (chamfer_distance.py:206-207), so every unit normal is short by
+    1e-9 / |c| and arccos(|n|^2) > 0 -- about 0.7 deg at 512^3, where the
+    MC triangles have |c| ~ 1e-5.  (logs/run_small.log prints 0.0 there; it
+    was written by an older revision, SURVEY finding 7.)  This pins that the
+    value comes from that formula alone: no degenerate MC triangle, no ray
+    hit on a sliver, and the mean equals the formula's prediction."""
+    import tropical.stanford.train as tr
+    from golden_io import load
+    from helpers import product_net
+    from tropical.utils.chamfer_distance import RayCaster
+    net = product_net(load("small_sphere"), cuda)
+    mesh = tr.run_marching_cubes(net, 512)
+    tri = mesh.vertices[mesh.faces]
+    c = np.linalg.norm(np.cross(tri[:, 1] - tri[:, 0], tri[:, 2] - tri[:, 0]), axis=-1)
+    assert int((c == 0).sum()) == 0  # no degenerate triangle in the HIP marching cubes
+    torch.manual_seed(0)
+    ro, rd = tr.get_rays()
+    _, fid, _ = RayCaster(mesh.vertices, mesh.faces).ray_trace(ro, rd)
+    f = fid.cpu().numpy()
+    f = f[f >= 0]
+    assert len(f) > 90000 and c[f].min() > 1e-7  # hits land on proper triangles
+    n = np.cross(tri[f, 1] - tri[f, 0], tri[f, 2] - tri[f, 0])
+    n /= (np.linalg.norm(n, axis=-1, keepdims=True) + 1e-9)  # chamfer_distance.py:207
+    ad, _ = tr.angular_distance(n, n)
+    short = c[f] / (c[f] + 1e-9)
+    want = np.degrees(np.arccos(np.clip(short * short, -1, 1))).mean()
+    assert abs(ad - want) < 0.01 and 0.2 < ad < 1.5, (ad, want)

@@ -202,6 +202,15 @@ static int ktimer_begin(tnp_engine* e, const char* name, double bytes, hipStream
 static void ktimer_set_bytes(tnp_engine* e, double bytes) {
   if (e->kt_on && !e->kt.empty()) e->kt.back().bytes = bytes;
 }
+// ... of the latest timed launch named `name` (counts read back later)
+static void ktimer_set_bytes(tnp_engine* e, const char* name, double bytes) {
+  if (!e->kt_on) return;
+  for (size_t i = e->kt.size(); i-- > 0;)
+    if (strcmp(e->kt[i].name, name) == 0) {
+      e->kt[i].bytes = bytes;
+      return;
+    }
+}
 static void ktimer_end(tnp_engine* e, int t, hipStream_t s) {
   if (t >= 0) (void)hipEventRecord(e->kt[t].b, s);
 }
@@ -722,6 +731,8 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
     if (ensure_masks(e, s)) return -1;
     TnpLB lb;
     if (lb_begin(e, split_tiles(e->E), s, &lb)) return -1;
+    // algorithmic bytes: 8 B split mask per edge; per split 8 B endpoints,
+    // 4 B rewired id, 1 B stale mask (set once S is known)
     TIMED("split", 8.0 * e->E,
           launch_split_lb(P<int32_t>(e->edges), e->E, P<uint64_t>(e->esm), P<uint8_t>(e->edm), idx,
                           e->V, P<int32_t>(e->sa), P<int32_t>(e->sb), P<int64_t>(e->ctr),
@@ -740,6 +751,7 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
     }
     if (read_ctr(e, s)) return -1;
     S = e->h_ctr[CTR_S];
+    ktimer_set_bytes(e, "split", 8.0 * e->E + 13.0 * S);
   }
   *fail = 0;
   if (S > 0) {
@@ -756,7 +768,12 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
     if (e->pend_fused) {
       // flat: split points + forward + failover test + keys in one pass,
       // straight into the cache
-      TIMED("forward_new", (8.0 + 8.0 + 24.0 + 12.0 + 16.0 + 4.0 * (e->K - e->valid_from) + 48.0) * S,
+      // per split: reads 8 B endpoint ids, 24 B endpoint coordinates, 8 B
+      // endpoint plane values, 16 B endpoint zero keys, 8 corners x L levels
+      // x 8 B of table entries; writes 12 B coordinates, the cache planes
+      // >= valid_from, 48 B keys (pos, zero, pz, grid, shared)
+      TIMED("forward_new",
+            (8.0 + 24.0 + 8.0 + 16.0 + 64.0 * e->net.n_levels + 12.0 + 4.0 * (e->K - e->valid_from) + 48.0) * S,
             launch_forward_new(e->net, P<float>(e->cur.xyz) + 3 * e->V, S, P<float>(e->cur.pre),
                                e->cur.cap, e->V, e->valid_from, P<int32_t>(e->sa), P<int32_t>(e->sb),
                                idx, e->own_lo, e->own_hi, P<uint64_t>(e->cur.pos),
@@ -888,7 +905,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     if (buf_ensure(e->bk[12], NB * sizeof(int64_t), s)) return -1;        // window-pass pairs
     if (buf_ensure(e->bk[13], (NB + 1) * sizeof(int64_t), s)) return -1;
     if (buf_ensure(e->sents, TB * sizeof(uint64_t), s)) return -1;
-    TIMED("bucket_entries", 24.0 * M,
+    TIMED("bucket_entries", 16.0 * M,  // + 8 B per entry, set once T is known
           launch_bucket_entries(P<int32_t>(e->members), S, V, M, grid, zero, idx, e->net.n_marks,
                                 P<int32_t>(e->bk[0]), P<int32_t>(e->bk[1]), P<int64_t>(e->bk[2]),
                                 P<int64_t>(e->bk[7]), P<uint64_t>(e->sents), e->bk_clean, ctr, s));
@@ -1011,6 +1028,12 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
       }
       H = e->h_ctr[CTR_H];
       T = e->h_ctr[CTR_T];
+      // entries: written once by the scatter; the grouping reads them, gathers
+      // 16 B of member keys and writes the 32 B record; the window pass reads
+      // every record (once, algorithmically) and writes the kept keys
+      ktimer_set_bytes(e, "bucket_entries", 16.0 * M + 8.0 * T);
+      ktimer_set_bytes(e, "bucket_group", 56.0 * T);
+      ktimer_set_bytes(e, "connect_win", 32.0 * T + 8.0 * e->h_ctr[CTR_XK]);
     }
     TT = e->h_ctr[CTR_TESTS];
     X = e->h_ctr[CTR_XK];
@@ -1069,7 +1092,9 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     if (buf_ensure(e->esm_alt, N1 * sizeof(uint64_t), s)) return -1;
     TnpLB lb;
     if (lb_begin(e, lb_tiles(N), s, &lb)) return -1;
-    TIMED("prune", 24.0 * E + 48.0 * (S + X),
+    // old edges: 8 B ids + 1 B high plane + 8 B split mask read; e_new / c_new:
+    // 4 / 8 B ids + 32 B endpoint keys; kept edges: 17 B written + 2 B flags
+    TIMED("prune", 17.0 * E + 36.0 * S + 40.0 * X,
           launch_prune_lb(eg, E, P<int32_t>(e->sb), S, V, e->ckeys, nb, X, idx, K - 1,
                           P<uint64_t>(c.pz), P<uint8_t>(e->edm), P<uint64_t>(e->esm),
                           P<int32_t>(e->edges_alt), P<uint8_t>(e->edm_alt), P<uint64_t>(e->esm_alt),
@@ -1079,6 +1104,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     TIMED("count_live", 1.0 * NV, launch_count_flags(P<uint8_t>(e->live), NV, ctr, CTR_V, s));
     next_valid = e->keep_all ? 0 : std::min(idx + 1, K - 1);
     if (read_ctr(e, s)) return -1;
+    ktimer_set_bytes(e, "prune", 17.0 * E + 36.0 * S + 40.0 * X + 19.0 * e->h_ctr[CTR_E]);
     E2 = e->h_ctr[CTR_E];
     V2 = e->h_ctr[CTR_V];
     e->dirty = true;
