@@ -198,6 +198,12 @@ static int ktimer_begin(tnp_engine* e, const char* name, double bytes, hipStream
   e->kt.push_back(r);
   return (int)e->kt.size() - 1;
 }
+// bytes of the encoding tables (2 fp32 features per entry)
+static double table_bytes(const NetDev& n) {
+  double b = 0;
+  for (int l = 0; l < n.n_levels; ++l) b += 8.0 * n.sizes[l];
+  return b;
+}
 // modelled bytes of the last timed launch, when they depend on its result
 static void ktimer_set_bytes(tnp_engine* e, double bytes) {
   if (e->kt_on && !e->kt.empty()) e->kt.back().bytes = bytes;
@@ -754,6 +760,13 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
     ktimer_set_bytes(e, "split", 8.0 * e->E + 13.0 * S);
   }
   *fail = 0;
+  if (e->V + S >= (int64_t)INT32_MAX) {
+    // slots (dead ones included: compaction is lazy) are int32 ids in sa/sb,
+    // members, edges and the packed pair keys
+    tnp_set_error("plane %d: %lld vertex slots + %lld splits exceed the int32 slot range", idx,
+                  (long long)e->V, (long long)S);
+    return -1;
+  }
   if (S > 0) {
     if (vset_ensure(e, e->cur, e->V + S, e->V, s)) return -1;
     col = P<float>(e->cur.pre) + (int64_t)idx * e->cur.cap;  // may have moved
@@ -768,12 +781,14 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
     if (e->pend_fused) {
       // flat: split points + forward + failover test + keys in one pass,
       // straight into the cache
-      // per split: reads 8 B endpoint ids, 24 B endpoint coordinates, 8 B
-      // endpoint plane values, 16 B endpoint zero keys, 8 corners x L levels
-      // x 8 B of table entries; writes 12 B coordinates, the cache planes
-      // >= valid_from, 48 B keys (pos, zero, pz, grid, shared)
+      // compulsory bytes per split: reads 8 B endpoint ids, 24 B endpoint
+      // coordinates, 8 B endpoint plane values, 16 B endpoint zero keys;
+      // writes 12 B coordinates, the cache planes >= valid_from, 48 B keys
+      // (pos, zero, pz, grid, shared); plus the encoding tables once per
+      // launch (the 8 corners x L levels gathers are cache traffic)
       TIMED("forward_new",
-            (8.0 + 24.0 + 8.0 + 16.0 + 64.0 * e->net.n_levels + 12.0 + 4.0 * (e->K - e->valid_from) + 48.0) * S,
+            (8.0 + 24.0 + 8.0 + 16.0 + 12.0 + 4.0 * (e->K - e->valid_from) + 48.0) * S +
+                table_bytes(e->net),
             launch_forward_new(e->net, P<float>(e->cur.xyz) + 3 * e->V, S, P<float>(e->cur.pre),
                                e->cur.cap, e->V, e->valid_from, P<int32_t>(e->sa), P<int32_t>(e->sb),
                                idx, e->own_lo, e->own_hi, P<uint64_t>(e->cur.pos),
