@@ -908,6 +908,203 @@ k_descend(NetDev net, int64_t G, const int32_t* __restrict__ glist,
   d1s[b] = d1;
 }
 
+__device__ __forceinline__ float lane_f(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+// The same descent with ONE WAVE PER ROW: the 500 iterations are strictly
+// sequential, so a row's latency per iteration is the whole cost (one thread
+// per row left a lone wave issuing ~4k dependent instructions per
+// iteration).  Here lane q holds hash-grid corner q & 7 of level q >> 3 (its
+// table entry is gathered once per iteration and reused by the backward
+// pass) and lane j < H neuron j of each layer; every sum keeps the
+// single-thread order above -- corner sums, sequential fma chains, the
+// 1-row layer-2 tree -- over operands broadcast with v_readlane, so the
+// result is bitwise that of k_descend.
+template <int LV, int H>
+__global__ void __launch_bounds__(64)
+k_descend_wave(NetDev net, int64_t G, const int32_t* __restrict__ glist,
+               const int32_t* __restrict__ crow, const int32_t* __restrict__ sa,
+               const int32_t* __restrict__ sb, const float* __restrict__ xyz,
+               const int32_t* __restrict__ plane, int idx, float eps, int iters, int record,
+               float* __restrict__ ints, float* __restrict__ d0s, float* __restrict__ d1s,
+               unsigned long long* __restrict__ conv) {
+  static_assert(LV * 8 <= 64 && H <= 64, "one wave holds every corner and neuron");
+  constexpr int IN = 2 * LV;
+  constexpr int NW = NetShape<LV, H, 3>::NW;
+  __shared__ float w[NW];
+  for (int i = threadIdx.x; i < NW; i += blockDim.x) w[i] = net.weights[i];
+  __syncthreads();
+  const int64_t g = blockIdx.x;
+  if (g >= G) return;
+  const int lane = threadIdx.x;
+  const int b = glist[g];
+  const int r = crow[b];
+  float e0[3], de[3], x[3];
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    e0[d] = xyz[3 * (int64_t)sa[r] + d];
+    de[d] = __fsub_rn(xyz[3 * (int64_t)sb[r] + d], e0[d]);
+    x[d] = ints[3 * b + d];
+  }
+  const int j0 = plane[b];
+  const int mh = lin_mode(G, false), mo = lin_mode(G, true);
+  const bool one_row = G == 1;
+  // lane roles
+  const int nj = lane & (H - 1);                      // neuron
+  const int lc = min(lane >> 3, LV - 1), c = lane & 7;  // corner c of level lc
+  float sc = 0.f;
+  uint32_t res = 0, size = 1;
+  bool dense = false;
+#pragma unroll
+  for (int l = 0; l < LV; ++l)
+    if (l == lc) {
+      sc = net.scales[l];
+      res = (uint32_t)net.res[l];
+      size = net.sizes[l];
+      dense = net.dense[l] != 0;
+    }
+  const float* W0 = w;
+  const float* W1 = W0 + H * IN + H;
+  const float* W2 = W1 + H * H + H;
+  uint64_t word = 0;  // convergence bits of iterations [64 k, 64 k + 64)
+  float d0 = 1.f, d1 = 1.f;
+  for (int it = 0; it < iters; ++it) {
+    float u[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d)
+      u[d] = __fdiv_rn(__fadd_rn(__fadd_rn(e0[d], __fmul_rn(x[d], de[d])), 1.0f), 2.0f);
+    // this lane's corner (encode's op order)
+    float t[3];
+    uint32_t gc[3];
+    float wc = 1.0f;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      const float pos = __fadd_rn(__fmul_rn(u[d], sc), 0.5f);
+      const float fl = floorf(pos);
+      t[d] = __fsub_rn(pos, fl);
+      const uint32_t gi = (uint32_t)(int)fl;
+      if ((c >> d) & 1) {
+        wc = __fmul_rn(wc, t[d]);
+        gc[d] = gi + 1u;
+      } else {
+        wc = __fmul_rn(wc, __fsub_rn(1.0f, t[d]));
+        gc[d] = gi;
+      }
+    }
+    uint32_t id = dense ? (gc[0] + gc[1] * res + gc[2] * (res * res)) : (gc[0] ^ (gc[1] * P1) ^ (gc[2] * P2));
+    id %= size;
+    const float2 v = table_entry(net, lc, id);
+    const float px = __fmul_rn(wc, v.x), py = __fmul_rn(wc, v.y);
+    float f[IN];
+#pragma unroll
+    for (int l = 0; l < LV; ++l) {
+      float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        a0 = __fadd_rn(a0, lane_f(px, 8 * l + k));
+        a1 = __fadd_rn(a1, lane_f(py, 8 * l + k));
+      }
+      f[2 * l] = a0;
+      f[2 * l + 1] = a1;
+    }
+    // forward, neuron nj per lane
+    const float a1 = neuron_mode<IN, H>(W0, W0 + H * IN, f, nj, mh);
+    float h1[H];
+#pragma unroll
+    for (int j = 0; j < H; ++j) h1[j] = fmaxf(lane_f(a1, j), 0.f);
+    const float a2 = neuron_mode<H, H>(W1, W1 + H * H, h1, nj, mh);
+    float h2[H];
+#pragma unroll
+    for (int j = 0; j < H; ++j) h2[j] = fmaxf(lane_f(a2, j), 0.f);
+    const float o = neuron_mode<H, 2>(W2, W2 + 2 * H, h2, lane & 1, mo);
+    const float last = __fsub_rn(lane_f(o, 1), lane_f(o, 0));
+    d0 = j0 < H ? lane_f(a1, j0) : (j0 < 2 * H ? lane_f(a2, j0 - H) : last);
+    d1 = idx < H ? lane_f(a1, idx) : (idx < 2 * H ? lane_f(a2, idx - H) : last);
+    // backward: seeds of d0^2 + d1^2, neuron nj per lane
+    float g1 = 0.f, g2 = 0.f, go = 0.f;
+    {
+      const int js[2] = {j0, idx};
+      const float ds[2] = {d0, d1};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const float gs = __fmul_rn(2.f, ds[s]);
+        if (js[s] == nj) g1 = __fadd_rn(g1, gs);
+        if (js[s] == H + nj) g2 = __fadd_rn(g2, gs);
+        if (js[s] == 2 * H) go = __fadd_rn(go, gs);
+      }
+    }
+    const float v3 = __fmaf_rn(go, W2[H + nj], __fmul_rn(-go, W2[nj]));
+    if (a2 > 0.f) g2 = __fadd_rn(g2, v3);
+    float g2u[H];
+#pragma unroll
+    for (int j = 0; j < H; ++j) g2u[j] = lane_f(g2, j);
+    float v2;
+    if (one_row) {
+      v2 = mm1_16(g2u, W1, H, nj);
+    } else {
+      v2 = 0.f;
+#pragma unroll
+      for (int j = 0; j < H; ++j) v2 = __fmaf_rn(g2u[j], W1[j * H + nj], v2);
+    }
+    const float ga1 = a1 > 0.f ? __fadd_rn(g1, v2) : g1;
+    float ga1u[H];
+#pragma unroll
+    for (int k = 0; k < H; ++k) ga1u[k] = lane_f(ga1, k);
+    const int m = lane & (IN - 1);
+    float dfm = 0.f;
+#pragma unroll
+    for (int k = 0; k < H; ++k) dfm = __fmaf_rn(ga1u[k], W0[k * IN + m], dfm);
+    // encoding input gradient, this lane's corner; sums in (level, corner) order
+    float dfa = 0.f, dfb = 0.f;
+#pragma unroll
+    for (int l = 0; l < LV; ++l) {
+      const float pa = lane_f(dfm, 2 * l), pb = lane_f(dfm, 2 * l + 1);
+      if (l == lc) {
+        dfa = pa;
+        dfb = pb;
+      }
+    }
+    const float dv = __fadd_rn(__fmul_rn(v.x, dfa), __fmul_rn(v.y, dfb));
+    float fc[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) fc[d] = ((c >> d) & 1) ? t[d] : __fsub_rn(1.f, t[d]);
+    float term[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      const float sg = ((c >> d) & 1) ? 1.f : -1.f;
+      const float fa = fc[d == 0 ? 1 : 0], fb = fc[d == 2 ? 1 : 2];
+      term[d] = __fmul_rn(__fmul_rn(__fmul_rn(__fmul_rn(sg, fa), fb), dv), sc);
+    }
+    float gx[3], nn = 0.f;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      float acc = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8 * LV; ++q) acc = __fadd_rn(acc, lane_f(term[d], q));
+      gx[d] = __fmul_rn(__fmul_rn(acc, 0.5f), de[d]);
+      nn = __fmaf_rn(gx[d], gx[d], nn);
+    }
+    const float den = fmaxf(__fsqrt_rn(nn), 1e-12f);
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      const float vv = __fsub_rn(x[d], __fmul_rn(1e-2f, __fdiv_rn(gx[d], den)));
+      x[d] = fminf(fmaxf(vv, 0.f), 1.f);
+    }
+    if (record && fabsf(d0) <= eps && fabsf(d1) <= eps) word |= 1ull << (it & 63);
+    if ((it & 63) == 63 || it == iters - 1) {
+      if (record && lane == 0) atomicAnd(&conv[it >> 6], (unsigned long long)word);
+      word = 0;
+    }
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int d = 0; d < 3; ++d) ints[3 * b + d] = x[d];
+    d0s[b] = d0;
+    d1s[b] = d1;
+  }
+}
+
 // v = e0 + t (e1 - e0) for c rows (subpoly.py:204-207) and the per-split
 // strict-filter inputs: cinfo bit0 c row, bit1 gg, bit2 |d0| < eps; the
 // global "some kept c row has |d0| > eps" flag (subpoly_debug.py:253-257).
@@ -1039,9 +1236,16 @@ int launch_descend(const NetDev& net, int64_t G, const int32_t* glist, const int
   if (G <= 0) return 0;
   if (!net_supported(net)) { tnp_set_error("unsupported net shape"); return -1; }
   if (iters > 512) { tnp_set_error("descend: at most 512 iterations"); return -1; }
+  // TNP_DESCEND_THREAD=1: the one-thread-per-row kernel (tests compare both)
+  const char* pt = getenv("TNP_DESCEND_THREAD");
+  const bool per_thread = pt && pt[0] == '1';
   TNP_DISPATCH(net.n_levels, {
-    hipLaunchKernelGGL((k_descend<L_, 16>), dim3(tnp_grid(G)), dim3(TNP_BLOCK), 0, s, net, G, glist,
-                       crow, sa, sb, xyz, plane, idx, eps, iters, record, ints, d0s, d1s, conv);
+    if (per_thread)
+      hipLaunchKernelGGL((k_descend<L_, 16>), dim3(tnp_grid(G)), dim3(TNP_BLOCK), 0, s, net, G, glist,
+                         crow, sa, sb, xyz, plane, idx, eps, iters, record, ints, d0s, d1s, conv);
+    else
+      hipLaunchKernelGGL((k_descend_wave<L_, 16>), dim3((unsigned)G), dim3(64), 0, s, net, G, glist,
+                         crow, sa, sb, xyz, plane, idx, eps, iters, record, ints, d0s, d1s, conv);
   });
   TNP_CHECK(hipGetLastError());
   return 0;

@@ -266,6 +266,34 @@ __device__ __forceinline__ float fold_lanes(float* l) {
   return l[0];
 }
 
+// output j of linear_mode<IN, OUT> (the same ops, one output)
+template <int IN, int OUT>
+__device__ __forceinline__ float neuron_mode(const float* __restrict__ W, const float* __restrict__ b,
+                                             const float* in, int j, int mode) {
+  if (mode == LIN_SEQ) {
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k < IN; ++k) acc = __fmaf_rn(in[k], W[j * IN + k], acc);
+    return __fadd_rn(acc, b[j]);
+  }
+  float l[IN];
+#pragma unroll
+  for (int k = 0; k < IN; ++k) l[k] = __fmul_rn(in[k], W[j * IN + k]);
+  float r;
+  if (mode == LIN_FOLD) {
+    r = fold_lanes<IN>(l);
+  } else if (OUT == 2) {
+    float p0 = l[0];
+    l[0] = 0.f;
+    r = __fadd_rn(p0, fold_lanes<IN>(l));
+  } else {
+    l[1] = __fmaf_rn(in[1], W[j * IN + 1], l[0]);
+    l[0] = 0.f;
+    r = fold_lanes<IN>(l);
+  }
+  return __fadd_rn(r, b[j]);
+}
+
 template <int IN, int OUT>
 __device__ __forceinline__ void linear_mode(const float* __restrict__ W, const float* __restrict__ b,
                                             const float* in, float* out, int mode) {
@@ -274,24 +302,7 @@ __device__ __forceinline__ void linear_mode(const float* __restrict__ W, const f
     return;
   }
 #pragma unroll
-  for (int j = 0; j < OUT; ++j) {
-    float l[IN];
-#pragma unroll
-    for (int k = 0; k < IN; ++k) l[k] = __fmul_rn(in[k], W[j * IN + k]);
-    float r;
-    if (mode == LIN_FOLD) {
-      r = fold_lanes<IN>(l);
-    } else if (OUT == 2) {
-      float p0 = l[0];
-      l[0] = 0.f;
-      r = __fadd_rn(p0, fold_lanes<IN>(l));
-    } else {
-      l[1] = __fmaf_rn(in[1], W[j * IN + 1], l[0]);
-      l[0] = 0.f;
-      r = fold_lanes<IN>(l);
-    }
-    out[j] = __fadd_rn(r, b[j]);
-  }
+  for (int j = 0; j < OUT; ++j) out[j] = neuron_mode<IN, OUT>(W, b, in, j, mode);
 }
 
 // per-layer mode for a call on n rows (hidden layers: OUT = H, last: OUT = 2)
