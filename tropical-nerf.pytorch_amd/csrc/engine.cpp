@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -157,7 +159,10 @@ struct tnp_engine {
   Buf blk, blkoff, scan_scr, sa, sb, stage, shared, members, pcn, pent, rstart, ent_v,
       ents, pcell, ptoff, bcell, bstat, ckeys_a, ckeys_b, sort_scr, flags, used, nid, ctr;
   uint64_t* ckeys = nullptr;  // sorted connecting edges of the current step
-  int64_t* h_ctr = nullptr;  // pinned mirror of ctr
+  int64_t* h_ctr = nullptr;  // host copy of ctr (the last readback)
+  int64_t* h_map = nullptr;  // host-mapped mirror written by k_publish ([31]: sequence)
+  int64_t* h_map_dev = nullptr;
+  int64_t pub_seq = 0;
   // pending split
   int pend_idx = -1;
   int64_t pend_S = 0, pend_dup = 0;
@@ -181,9 +186,26 @@ struct tnp_engine {
   Buf cv[CV_N];
 };
 
+// counter readback: k_publish writes the block into host-mapped memory and
+// the host spins on its sequence word (measured on MI355X: 9.9 us per round
+// trip against 15.7 us for a copy + stream synchronise); after 2 ms of
+// spinning (long kernels) it blocks in the stream synchronise instead
 static int read_ctr(tnp_engine* e, hipStream_t s) {
-  TNP_CHECK(hipMemcpyAsync(e->h_ctr, e->ctr.p, CTR_N * sizeof(int64_t), hipMemcpyDeviceToHost, s));
-  TNP_CHECK(hipStreamSynchronize(s));
+  const int64_t seq = ++e->pub_seq;
+  if (launch_publish(P<int64_t>(e->ctr), e->h_map_dev, seq, s)) return -1;
+  volatile int64_t* flag = e->h_map + 31;
+  const auto t0 = std::chrono::steady_clock::now();
+  int n = 0;
+  while (*flag != seq) {
+    if ((++n & 255) == 0 &&
+        std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
+      TNP_CHECK(hipStreamSynchronize(s));
+      if (*flag != seq) { tnp_set_error("counter readback: no publish after the stream drained"); return -1; }
+      break;
+    }
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+  memcpy(e->h_ctr, (const void*)e->h_map, CTR_N * sizeof(int64_t));
   return 0;
 }
 
@@ -364,11 +386,18 @@ extern "C" int tnp_engine_create(tnp_engine** out, int device) {
   e->device = device;
   if (const char* lim = getenv("TNP_MAX_PAIR_TESTS")) e->max_pair_tests = atoll(lim);
   if (const char* rc = getenv("TNP_RADIX_CELLS")) e->radix_cells = atoi(rc) != 0;
-  if (hipHostMalloc((void**)&e->h_ctr, CTR_N * sizeof(int64_t), hipHostMallocDefault) != hipSuccess) {
+  if (hipHostMalloc((void**)&e->h_ctr, CTR_N * sizeof(int64_t), hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc((void**)&e->h_map, 32 * sizeof(int64_t), hipHostMallocMapped | hipHostMallocCoherent) !=
+          hipSuccess ||
+      hipHostGetDevicePointer((void**)&e->h_map_dev, e->h_map, 0) != hipSuccess) {
+    if (e->h_ctr) (void)hipHostFree(e->h_ctr);
+  if (e->h_map) (void)hipHostFree(e->h_map);
+    if (e->h_map) (void)hipHostFree(e->h_map);
     delete e;
     tnp_set_error("hipHostMalloc failed");
     return -1;
   }
+  memset((void*)e->h_map, 0, 32 * sizeof(int64_t));
   *out = e;
   return 0;
 }

@@ -154,6 +154,9 @@ int launch_prune_lb(const int32_t* edges, int64_t E, const int32_t* sb, int64_t 
                     hipStream_t s);
 // ctr[slot] += number of set byte flags in f[0, n) (16-B aligned f, 0/1 bytes)
 int launch_count_flags(const uint8_t* f, int64_t n, int64_t* ctr, int slot, hipStream_t s);
+// the counter block -> a host-mapped mirror, then the sequence word at [31]
+// (the host spins on it instead of a copy + stream synchronise)
+int launch_publish(const int64_t* ctr, int64_t* host, int64_t seq, hipStream_t s);
 int launch_widen_flags(const uint8_t* f, int64_t n, int32_t* out, hipStream_t s);
 // planes the pruning of step idx compares (idx .. last_plane)
 uint64_t prune_mask(int idx, int last_plane);

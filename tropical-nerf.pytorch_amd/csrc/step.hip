@@ -1141,6 +1141,16 @@ __global__ void k_remap_edges(int32_t* __restrict__ edges, int64_t E, const int6
 }
 
 
+// per-step counter readback: every lane stores its own word (the block is
+// tiny), the sequence word last, after a system-scope fence
+__global__ void k_publish(const int64_t* __restrict__ ctr, volatile int64_t* host, int64_t seq) {
+  const int t = threadIdx.x;
+  if (t < CTR_N) host[t] = ctr[t];
+  __threadfence_system();
+  __syncthreads();
+  if (t == 31) host[t] = seq;
+}
+
 }  // namespace
 
 // ----------------------------------------------------------------------------
@@ -1361,6 +1371,12 @@ int launch_widen_flags(const uint8_t* f, int64_t n, int32_t* out, hipStream_t s)
   TNP_CHECK(hipGetLastError());
   return 0;
 }
+int launch_publish(const int64_t* ctr, int64_t* host, int64_t seq, hipStream_t s) {
+  hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, s, ctr, host, seq);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+
 int launch_count_flags(const uint8_t* f, int64_t n, int64_t* ctr, int slot, hipStream_t s) {
   if (n <= 0) return 0;
   const unsigned g = (unsigned)std::min<int64_t>(2048, (n + 16 * TNP_BLOCK - 1) / (16 * TNP_BLOCK));
