@@ -221,13 +221,14 @@ int tnp_engine_faces_debug(tnp_engine* eng, float* d_scores, int64_t cap, int64_
  * mcubes.marching_cubes (train.py:284).  Phase 1: d_eoff [3*n0*n1*n2 + 1]
  * int64 -> vertex id of every crossed lattice edge (point-major, axis
  * minor), d_coff [(n0-1)(n1-1)(n2-1) + 1] int64 -> first triangle of every
- * cube; returns the vertex and triangle counts.  Phase 2: vertices fp32
- * [n_verts][3] in index space, triangles int64 [n_tris][3]. */
+ * cube; returns the vertex and triangle counts.  Phase 2: vertices fp64
+ * [n_verts][3] in index space (interpolated in double, as PyMCubes),
+ * triangles int64 [n_tris][3]. */
 int tnp_mc_count(const float* d_vol, int n0, int n1, int n2, float iso, const int8_t* d_table,
                  int64_t* d_eoff, int64_t* d_coff, int64_t* n_verts, int64_t* n_tris,
                  void* stream);
 int tnp_mc_emit(const float* d_vol, int n0, int n1, int n2, float iso, const int8_t* d_table,
-                const int64_t* d_eoff, const int64_t* d_coff, float* d_verts, int64_t* d_tris,
+                const int64_t* d_eoff, const int64_t* d_coff, double* d_verts, int64_t* d_tris,
                 void* stream);
 
 /* Nearest-hit ray casting against a triangle mesh (replaces

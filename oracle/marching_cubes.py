@@ -5,7 +5,7 @@ HIP kernels in csrc/evaluate.hip (tnp_mc_*), never called by the product.
 Same conventions as the kernels: volume vol[i, j, k] (x, y, z index space),
 inside = value < iso, one vertex per crossed lattice edge, numbered by
 (point-major, axis-minor) lattice-edge order, position p + t * e_axis with
-t = (iso - v0) / (v1 - v0) in fp32; triangles per cube in cube order (x
+t = (iso - v0) / (v1 - v0) in fp64 (from the fp32 samples); triangles per cube in cube order (x
 slowest), table order within a cube.  PyMCubes (the reference's
 `mcubes.marching_cubes`, train.py:284) is absent here and unpinned."""
 import numpy as np
@@ -30,9 +30,10 @@ def marching_cubes(vol: np.ndarray, iso: float, table: np.ndarray):
     v0 = vol[i, j, k]
     step = np.stack([a == 0, a == 1, a == 2], 1).astype(np.int64)
     v1 = vol[i + step[:, 0], j + step[:, 1], k + step[:, 2]]
-    t = (iso - v0) / (v1 - v0)
-    base = np.stack([i, j, k], 1).astype(np.float32)
-    verts = base + step.astype(np.float32) * t[:, None].astype(np.float32)
+    v0, v1 = v0.astype(np.float64), v1.astype(np.float64)
+    t = (np.float64(iso) - v0) / (v1 - v0)
+    base = np.stack([i, j, k], 1).astype(np.float64)
+    verts = base + step.astype(np.float64) * t[:, None]
     # cubes
     c = inside.astype(np.int64)
     case = (c[:-1, :-1, :-1] | c[1:, :-1, :-1] << 1 | c[1:, 1:, :-1] << 2 | c[:-1, 1:, :-1] << 3 |

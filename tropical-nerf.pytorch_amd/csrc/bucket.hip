@@ -36,6 +36,11 @@
 namespace {
 
 constexpr int BK_IPT = 8;  // members per thread in the member passes
+// grids up to this many workgroups finish their scans in the last workgroup
+// (one launch less); larger ones pay more in every workgroup's tail
+// (measured at 128^3: 4,913 buckets +0.26 ms per pass) and scan in a launch
+// of their own
+constexpr unsigned FUSE_MAX_BLOCKS = 512;
 
 // member m of a step: the S new vertices are slots V + m (no list needed),
 // the hit vertices follow in members[S..]
@@ -68,31 +73,91 @@ __device__ __forceinline__ int local_of(const BGeom& G, int cx, int cy, int cz) 
   return ((cx & m) << (2 * G.sh)) | ((cy & m) << G.sh) | (cz & m);
 }
 
-// (1) per-bucket entry counts; per-block augmented-row sums -> part[]
+// exclusive scan of n counts another workgroup of this launch handed over
+// (tnp::last_block; sc1 loads) -> out[0..n] (out[n] = total); one workgroup
+template <typename T>
+__device__ __forceinline__ int64_t scan_handed(const T* cnt, int n, int64_t* out, int64_t* lds) {
+  constexpr int PER = (BUCKET_MAX + TNP_BLOCK - 1) / TNP_BLOCK;  // n <= BUCKET_MAX
+  const int b0 = threadIdx.x * PER;
+  int64_t v[PER];
+  if constexpr (sizeof(T) == 4) {
+    // int32 counts as 8-B pairs (cnt holds n + 1 slots, PER is even): the
+    // compiler keeps 4-B sc1 loads one at a time, 8-B ones in flight together
+    static_assert(PER % 2 == 0, "pairs");
+    const int64_t* c2 = reinterpret_cast<const int64_t*>(cnt);
+#pragma unroll
+    for (int k = 0; k < PER; k += 2) {
+      const int64_t w = b0 + k < n ? tnp::ld_agent(c2 + (b0 + k) / 2) : 0;
+      v[k] = (int32_t)(uint32_t)w;
+      v[k + 1] = b0 + k + 1 < n ? (int64_t)(int32_t)(uint32_t)(w >> 32) : 0;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < PER; ++k) v[k] = b0 + k < n ? (int64_t)tnp::ld_agent(cnt + b0 + k) : 0;  // all in flight
+  }
+  int64_t s = 0;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) s += v[k];
+  int64_t tot;
+  int64_t run = tnp::block_scan_excl(s, lds, tot);
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    if (b0 + k < n) out[b0 + k] = run;
+    run += v[k];
+  }
+  if (threadIdx.x == 0) out[n] = tot;
+  return tot;
+}
+
+// (1) per-bucket entry counts; per-block augmented-row sums -> part[]; the
+// workgroup finishing last scans the counts into the bucket bases (-> T)
+// and sums the parts (-> A).  live (prune steps): the next live-flag set is
+// zeroed here, after the hit pass has read it.
 __global__ void __launch_bounds__(TNP_BLOCK)
 k_bucket_count(const int32_t* __restrict__ members, int64_t S, int64_t V, int64_t M,
                const uint64_t* __restrict__ grid,
                const uint64_t* __restrict__ zero, int idx, BGeom G, int NB,
-               int32_t* __restrict__ bcount, int64_t* __restrict__ part, int64_t* __restrict__ ctr) {
+               int32_t* __restrict__ bcount, int64_t* __restrict__ part, int64_t* __restrict__ bbase,
+               uint8_t* __restrict__ live, int64_t nlive, int fuse, int64_t* __restrict__ ctr) {
   __shared__ int hist[BUCKET_MAX];
   __shared__ int64_t lds[TNP_WAVES];
+  __shared__ int last;
+  if (live) {
+    const int64_t n16 = nlive >> 4;
+    uint4* l4 = reinterpret_cast<uint4*>(live);
+    for (int64_t i = (int64_t)blockIdx.x * TNP_BLOCK + threadIdx.x; i < n16; i += (int64_t)gridDim.x * TNP_BLOCK)
+      l4[i] = make_uint4(0, 0, 0, 0);
+    if (blockIdx.x == 0 && threadIdx.x < (nlive & 15)) live[(n16 << 4) + threadIdx.x] = 0;
+  }
   for (int i = threadIdx.x; i < NB; i += TNP_BLOCK) hist[i] = 0;
   __syncthreads();
   const uint64_t below = (idx >= 64) ? ~0ull : ((1ull << idx) - 1ull);
   const int64_t base = (int64_t)blockIdx.x * TNP_BLOCK * BK_IPT;
   int64_t aug = 0;
   bool k0 = false;
+  // every item's loads in flight before any is used
+  int vv[BK_IPT];
+  uint64_t gg[BK_IPT], zz[BK_IPT];
 #pragma unroll
   for (int k = 0; k < BK_IPT; ++k) {
     const int64_t m = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
-    if (m >= M) break;
-    const int v = member_of(members, S, V, m);
+    vv[k] = m < M ? member_of(members, S, V, m) : -1;
+  }
+#pragma unroll
+  for (int k = 0; k < BK_IPT; ++k) {
+    const int v = vv[k] >= 0 ? vv[k] : 0;
+    gg[k] = grid[v];
+    zz[k] = zero[v];
+  }
+#pragma unroll
+  for (int k = 0; k < BK_IPT; ++k) {
+    if (vv[k] < 0) continue;
     int lo[3], n[3];
-    span_of(grid[v], lo, n);
+    span_of(gg[k], lo, n);
     for (int i = 0; i < n[0]; ++i)
       for (int j = 0; j < n[1]; ++j)
         for (int q = 0; q < n[2]; ++q) atomicAdd(&hist[bucket_of(G, lo[0] + i, lo[1] + j, lo[2] + q)], 1);
-    const int kz = __popcll(zero[v] & below) + (n[0] - 1) + (n[1] - 1) + (n[2] - 1);
+    const int kz = __popcll(zz[k] & below) + (n[0] - 1) + (n[1] - 1) + (n[2] - 1);
     aug += 1ll << kz;
     k0 |= kz == 0;
   }
@@ -102,81 +167,43 @@ k_bucket_count(const int32_t* __restrict__ members, int64_t S, int64_t V, int64_
     if (hist[i]) atomicAdd(&bcount[i], hist[i]);
   int64_t tot;
   tnp::block_scan_excl(aug, lds, tot);
-  if (threadIdx.x == 0) part[blockIdx.x] = tot;
+  if (threadIdx.x == 0) tnp::st_agent(part + blockIdx.x, tot);
+  if (!fuse || !tnp::last_block(&ctr[CTR_TK0], &last)) return;
+  int64_t a = 0;
+  for (int i = threadIdx.x; i < (int)gridDim.x; i += TNP_BLOCK) a += tnp::ld_agent(part + i);
+  int64_t atot;
+  tnp::block_scan_excl(a, lds, atot);
+  const int64_t T = scan_handed(bcount, NB, bbase, lds);
+  if (threadIdx.x == 0) {
+    ctr[CTR_A] = atot;
+    ctr[CTR_T] = T;
+  }
 }
 
-// (2) exclusive scan of n int32 counts -> int64 bases [0, n]; total ->
-// ctr[slot] (one block; n is a few thousand)
-__global__ void __launch_bounds__(1024)
-k_small_scan(const int32_t* __restrict__ cnt, int n, int64_t* __restrict__ out, int64_t* __restrict__ ctr,
-             int slot, const int64_t* __restrict__ part, int64_t nparts, int pslot) {
-  __shared__ int64_t lds[16];
-  if (part) {  // and the sum of the member pass's per-block parts -> ctr[pslot]
+// (2) the same scans as a launch of their own, for grids too large for the
+// last-workgroup hand-off to pay (every workgroup's tail then waits for its
+// stores and a contended ticket): blockIdx.y picks (cnt, out, slot) set y;
+// part != null: set 0 also sums the member pass's per-block parts -> pslot
+struct ScanSet {
+  const void* cnt;
+  int wide;  // 1: int64 counts, 0: int32
+  int64_t* out;
+  int slot;
+};
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_scan_sets(ScanSet s0, ScanSet s1, ScanSet s2, int n, const int64_t* __restrict__ part, int64_t nparts,
+            int pslot, int64_t* __restrict__ ctr) {
+  __shared__ int64_t lds[TNP_WAVES];
+  const ScanSet& q = blockIdx.y == 0 ? s0 : (blockIdx.y == 1 ? s1 : s2);
+  const int64_t t = q.wide ? scan_handed(static_cast<const int64_t*>(q.cnt), n, q.out, lds)
+                           : scan_handed(static_cast<const int32_t*>(q.cnt), n, q.out, lds);
+  if (threadIdx.x == 0) ctr[q.slot] = t;
+  if (part && blockIdx.y == 0) {
     int64_t a = 0;
-    for (int64_t i = threadIdx.x; i < nparts; i += 1024) a += part[i];
-    a = tnp::wave_sum(a);
-    if (tnp::lane() == 0) lds[tnp::wave()] = a;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      int64_t t = 0;
-      for (int w = 0; w < 16; ++w) t += lds[w];
-      ctr[pslot] = t;
-    }
-    __syncthreads();
-  }
-  const int per = (n + 1023) / 1024;
-  const int b = threadIdx.x * per;
-  int64_t s = 0;
-  for (int i = b; i < b + per && i < n; ++i) s += cnt[i];
-  int64_t inc = tnp::wave_scan_incl(s);
-  if (tnp::lane() == 63) lds[tnp::wave()] = inc;
-  __syncthreads();
-  int64_t off = 0, tot = 0;
-  for (int w = 0; w < 16; ++w) {
-    off += (w < tnp::wave()) ? lds[w] : 0;
-    tot += lds[w];
-  }
-  int64_t run = off + inc - s;
-  for (int i = b; i < b + per && i < n; ++i) {
-    out[i] = run;
-    run += cnt[i];
-  }
-  if (threadIdx.x == 0) {
-    out[n] = tot;
-    if (ctr) ctr[slot] = tot;
-  }
-}
-
-// the same for int64 values (pair counts); blockIdx.y picks one of two
-// (cnt, out, slot) sets
-__global__ void __launch_bounds__(1024)
-k_small_scan64(const int64_t* __restrict__ cnt0, int64_t* __restrict__ out0, int slot0,
-               const int64_t* __restrict__ cnt1, int64_t* __restrict__ out1, int slot1, int n,
-               int64_t* __restrict__ ctr) {
-  __shared__ int64_t lds[16];
-  const int64_t* cnt = blockIdx.y ? cnt1 : cnt0;
-  int64_t* out = blockIdx.y ? out1 : out0;
-  const int slot = blockIdx.y ? slot1 : slot0;
-  const int per = (n + 1023) / 1024;
-  const int b = threadIdx.x * per;
-  int64_t s = 0;
-  for (int i = b; i < b + per && i < n; ++i) s += cnt[i];
-  int64_t inc = tnp::wave_scan_incl(s);
-  if (tnp::lane() == 63) lds[tnp::wave()] = inc;
-  __syncthreads();
-  int64_t off = 0, tot = 0;
-  for (int w = 0; w < 16; ++w) {
-    off += (w < tnp::wave()) ? lds[w] : 0;
-    tot += lds[w];
-  }
-  int64_t run = off + inc - s;
-  for (int i = b; i < b + per && i < n; ++i) {
-    out[i] = run;
-    run += cnt[i];
-  }
-  if (threadIdx.x == 0) {
-    out[n] = tot;
-    if (ctr) ctr[slot] = tot;
+    for (int64_t i = threadIdx.x; i < nparts; i += TNP_BLOCK) a += part[i];
+    int64_t atot;
+    tnp::block_scan_excl(a, lds, atot);
+    if (threadIdx.x == 0) ctr[pslot] = atot;
   }
 }
 
@@ -246,40 +273,17 @@ k_bucket_scatter(const int32_t* __restrict__ members, int64_t S, int64_t V, int6
 // dependent load -> atomic -> store chain at a time is latency-bound).
 constexpr int GIPT = 8;
 
+// the grouping of one bucket of n >= 2 entries (k_bucket_group)
 template <int SH>
-__global__ void __launch_bounds__(TNP_BLOCK)
-k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __restrict__ ekv,
-               const ulonglong2* __restrict__ pz, CellEnt* __restrict__ ents,
-               int32_t* __restrict__ lcell, int32_t* __restrict__ lent, int32_t* __restrict__ ln,
-               int64_t* __restrict__ lpoff, int32_t* __restrict__ bnpc, int64_t* __restrict__ bnpairs,
-               int64_t* __restrict__ bspairs, int64_t* __restrict__ ctr) {
+__device__ __forceinline__ void group_bucket(const BGeom& G, int b, int64_t base, int64_t n,
+                                             const uint64_t* __restrict__ ekv,
+                                             const ulonglong2* __restrict__ pz, CellEnt* __restrict__ ents,
+                                             int32_t* __restrict__ lcell, int32_t* __restrict__ lent,
+                                             int32_t* __restrict__ ln, int64_t* __restrict__ lpoff,
+                                             int64_t* __restrict__ bnpc, int64_t* __restrict__ bnpairs,
+                                             int64_t* __restrict__ bspairs, int64_t* __restrict__ ctr,
+                                             int* cnt, int* cur, int64_t* lds) {
   constexpr int LC = 1 << (3 * SH);
-  __shared__ int cnt[LC];
-  __shared__ int cur[LC];
-  __shared__ int64_t lds[TNP_WAVES];
-  const int b = blockIdx.x;
-  const int64_t base = bbase[b];
-  const int64_t n = bbase[b + 1] - base;
-  if (n < 2) {
-    if (threadIdx.x == 0) {
-      bnpc[b] = 0;
-      bnpairs[b] = 0;
-      bspairs[b] = 0;
-    }
-    if (n == 1 && threadIdx.x == 0) {  // a lone entry: a record the window pass can read
-      const uint64_t w = ekv[base];
-      const ulonglong2 k = pz[(uint32_t)w];
-      CellEnt r;
-      r.p = k.x;
-      r.z = k.y;
-      r.v = (int32_t)(uint32_t)w;
-      r.f = (uint32_t)(w >> 32) & 63u;
-      r.tag = (uint32_t)b * (uint32_t)LC + (uint32_t)(w >> 40);
-      r.pad = 0;
-      ents[base] = r;
-    }
-    return;
-  }
   for (int i = threadIdx.x; i < LC; i += TNP_BLOCK) cnt[i] = 0;
   __syncthreads();
   const uint64_t* kv = ekv + base;
@@ -378,16 +382,67 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
     }
   }
   if (threadIdx.x == 0) {
-    bnpc[b] = (int32_t)tpc;
-    bnpairs[b] = tp;
-    bspairs[b] = tsp;
+    tnp::st_agent(bnpc + b, tpc);
+    tnp::st_agent(bnpairs + b, tp);
+    tnp::st_agent(bspairs + b, tsp);
+  }
+}
+
+template <int SH>
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __restrict__ ekv,
+               const ulonglong2* __restrict__ pz, CellEnt* __restrict__ ents,
+               int32_t* __restrict__ lcell, int32_t* __restrict__ lent, int32_t* __restrict__ ln,
+               int64_t* __restrict__ lpoff, int64_t* __restrict__ bnpc, int64_t* __restrict__ bnpairs,
+               int64_t* __restrict__ bspairs, int64_t* __restrict__ pcoff, int64_t* __restrict__ pairoff,
+               int64_t* __restrict__ spoff, int fuse, int64_t* __restrict__ ctr) {
+  constexpr int LC = 1 << (3 * SH);
+  __shared__ int cnt[LC];
+  __shared__ int cur[LC];
+  __shared__ int64_t lds[TNP_WAVES];
+  __shared__ int last;
+  const int b = blockIdx.x;
+  const int64_t base = bbase[b];
+  const int64_t n = bbase[b + 1] - base;
+  if (n < 2) {
+    if (threadIdx.x == 0) {
+      tnp::st_agent(bnpc + b, (int64_t)0);
+      tnp::st_agent(bnpairs + b, (int64_t)0);
+      tnp::st_agent(bspairs + b, (int64_t)0);
+    }
+    if (n == 1 && threadIdx.x == 0) {  // a lone entry: a record the window pass can read
+      const uint64_t w = ekv[base];
+      const ulonglong2 k = pz[(uint32_t)w];
+      CellEnt r;
+      r.p = k.x;
+      r.z = k.y;
+      r.v = (int32_t)(uint32_t)w;
+      r.f = (uint32_t)(w >> 32) & 63u;
+      r.tag = (uint32_t)b * (uint32_t)LC + (uint32_t)(w >> 40);
+      r.pad = 0;
+      ents[base] = r;
+    }
+  } else {
+    group_bucket<SH>(G, b, base, n, ekv, pz, ents, lcell, lent, ln, lpoff, bnpc, bnpairs, bspairs, ctr, cnt,
+                     cur, lds);
+  }
+  if (!fuse || !tnp::last_block(&ctr[CTR_TK1], &last)) return;
+  // every bucket's pair-cell / pair totals -> global offsets (k_pair_gather)
+  const int NB = (int)gridDim.x;
+  const int64_t R = scan_handed(bnpc, NB, pcoff, lds);
+  const int64_t TT = scan_handed(bnpairs, NB, pairoff, lds);
+  const int64_t SP = scan_handed(bspairs, NB, spoff, lds);
+  if (threadIdx.x == 0) {
+    ctr[CTR_R] = R;
+    ctr[CTR_TESTS] = TT;
+    ctr[CTR_SPAIRS] = SP;
   }
 }
 
 // (6) the global pair-cell list k_connect walks: bucket order, then local
 // cell order
 __global__ void __launch_bounds__(TNP_BLOCK)
-k_pair_gather(const int64_t* __restrict__ bbase, const int32_t* __restrict__ bnpc,
+k_pair_gather(const int64_t* __restrict__ bbase, const int64_t* __restrict__ bnpc,
               const int64_t* __restrict__ pcoff, const int64_t* __restrict__ pairoff,
               const int32_t* __restrict__ lcell, const int32_t* __restrict__ lent,
               const int32_t* __restrict__ ln, const int64_t* __restrict__ lpoff,
@@ -399,7 +454,7 @@ k_pair_gather(const int64_t* __restrict__ bbase, const int32_t* __restrict__ bnp
     bcount[b] = 0;
     bcur[b] = 0;
   }
-  const int cnt = bnpc[b];
+  const int cnt = (int)bnpc[b];
   if (cnt == 0) return;
   const int64_t area = bbase[b] / 2, o = pcoff[b], po = pairoff[b];
   for (int i = threadIdx.x; i < cnt; i += TNP_BLOCK) {
@@ -434,8 +489,8 @@ int bucket_geometry(int n_marks, int* sh, int* NBd, int* NB) {
 
 int launch_bucket_entries(const int32_t* members, int64_t S, int64_t V, int64_t M, const uint64_t* grid,
                           const uint64_t* zero, int idx, int n_marks, int32_t* bcount, int32_t* bcur,
-                          int64_t* bbase, int64_t* part, uint64_t* ekv, bool clean, int64_t* ctr,
-                          hipStream_t s) {
+                          int64_t* bbase, int64_t* part, uint64_t* ekv, bool clean, uint8_t* live,
+                          int64_t nlive, int64_t* ctr, hipStream_t s) {
   int sh, NBd, NB;
   if (bucket_geometry(n_marks, &sh, &NBd, &NB)) {
     tnp_set_error("bucket geometry: %d marks", n_marks);
@@ -448,11 +503,12 @@ int launch_bucket_entries(const int32_t* members, int64_t S, int64_t V, int64_t 
   }
   const int64_t per = (int64_t)TNP_BLOCK * BK_IPT;
   const unsigned nblk = (unsigned)std::max<int64_t>((M + per - 1) / per, 1);
-  if (M > 0)
-    hipLaunchKernelGGL(k_bucket_count, dim3(nblk), dim3(TNP_BLOCK), 0, s, members, S, V, M, grid, zero, idx,
-                       G, NB, bcount, part, ctr);
-  hipLaunchKernelGGL(k_small_scan, dim3(1), dim3(1024), 0, s, bcount, NB, bbase, ctr, (int)CTR_T,
-                     M > 0 ? part : nullptr, (int64_t)nblk, (int)CTR_A);
+  const int fuse = nblk <= FUSE_MAX_BLOCKS;
+  hipLaunchKernelGGL(k_bucket_count, dim3(nblk), dim3(TNP_BLOCK), 0, s, members, S, V, M, grid, zero, idx,
+                     G, NB, bcount, part, bbase, live, nlive, fuse, ctr);
+  if (!fuse)
+    hipLaunchKernelGGL(k_scan_sets, dim3(1, 1), dim3(TNP_BLOCK), 0, s, ScanSet{bcount, 0, bbase, CTR_T},
+                       ScanSet{}, ScanSet{}, NB, part, (int64_t)nblk, (int)CTR_A, ctr);
   if (M > 0)
     hipLaunchKernelGGL(k_bucket_scatter, dim3(nblk), dim3(TNP_BLOCK), 0, s, members, S, V, M, grid, G, NB,
                        bbase, bcur, ekv);
@@ -462,7 +518,7 @@ int launch_bucket_entries(const int32_t* members, int64_t S, int64_t V, int64_t 
 
 int launch_bucket_pairs(int n_marks, const int64_t* bbase, const uint64_t* ekv, const uint64_t* pz,
                         CellEnt* ents, int32_t* lcell,
-                        int32_t* lent, int32_t* ln, int64_t* lpoff, int32_t* bnpc, int64_t* bnpairs,
+                        int32_t* lent, int32_t* ln, int64_t* lpoff, int64_t* bnpc, int64_t* bnpairs,
                         int64_t* bspairs, int64_t* spoff, int64_t* pcoff, int64_t* pairoff,
                         int32_t* pcell, int32_t* pent, int32_t* pn, int64_t* ptoff, int32_t* bcell,
                         int64_t bcap, int32_t* bcount, int32_t* bcur, int64_t* ctr, hipStream_t s) {
@@ -472,18 +528,19 @@ int launch_bucket_pairs(int n_marks, const int64_t* bbase, const uint64_t* ekv, 
     return -1;
   }
   const BGeom G{n_marks + 2, sh, NBd};
+  const int fuse = NB <= FUSE_MAX_BLOCKS;
   if (sh == 3)
     hipLaunchKernelGGL(k_bucket_group<3>, dim3(NB), dim3(TNP_BLOCK), 0, s, G, bbase, ekv,
                        reinterpret_cast<const ulonglong2*>(pz), ents, lcell, lent, ln, lpoff, bnpc, bnpairs,
-                       bspairs, ctr);
+                       bspairs, pcoff, pairoff, spoff, fuse, ctr);
   else
     hipLaunchKernelGGL(k_bucket_group<4>, dim3(NB), dim3(TNP_BLOCK), 0, s, G, bbase, ekv,
                        reinterpret_cast<const ulonglong2*>(pz), ents, lcell, lent, ln, lpoff, bnpc, bnpairs,
-                       bspairs, ctr);
-  hipLaunchKernelGGL(k_small_scan, dim3(1), dim3(1024), 0, s, bnpc, NB, pcoff, ctr, (int)CTR_R, nullptr,
-                     (int64_t)0, 0);
-  hipLaunchKernelGGL(k_small_scan64, dim3(1, 2), dim3(1024), 0, s, bnpairs, pairoff, (int)CTR_TESTS, bspairs,
-                     spoff, (int)CTR_SPAIRS, NB, ctr);
+                       bspairs, pcoff, pairoff, spoff, fuse, ctr);
+  if (!fuse)
+    hipLaunchKernelGGL(k_scan_sets, dim3(1, 3), dim3(TNP_BLOCK), 0, s, ScanSet{bnpc, 1, pcoff, CTR_R},
+                       ScanSet{bnpairs, 1, pairoff, CTR_TESTS}, ScanSet{bspairs, 1, spoff, CTR_SPAIRS}, NB,
+                       nullptr, (int64_t)0, 0, ctr);
   hipLaunchKernelGGL(k_pair_gather, dim3(NB), dim3(TNP_BLOCK), 0, s, bbase, bnpc, pcoff, pairoff, lcell, lent,
                      ln, lpoff, pcell, pent, pn, ptoff, bcell, bcap, connect_chunk_pairs(), bcount, bcur, ctr);
   TNP_CHECK(hipGetLastError());

@@ -205,6 +205,32 @@ __device__ __forceinline__ bool grid_zero(uint64_t g, int d) {
   return (g >> (48 + d)) & 1;
 }
 
+// True in every thread of the workgroup that finishes a launch last, so it
+// can finish the launch's reduction without another launch.  Hand-off
+// (MI355X_MICROARCH.md, inter-workgroup visibility, first row): the values
+// handed over are written with agent-scope (sc1) stores or device atomics,
+// every storing wave waits for its stores, then one lane per workgroup adds
+// to a zeroed ticket; the last workgroup reads them with sc1 loads
+// (ld_agent).  Every thread of every workgroup must call it.
+__device__ __forceinline__ bool last_block(int64_t* ticket, int* lds_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long t = atomicAdd((unsigned long long*)ticket, 1ull);
+    *lds_flag = t == (unsigned long long)gridDim.x * gridDim.y - 1ull;
+  }
+  __syncthreads();
+  return *lds_flag != 0;
+}
+template <typename T>
+__device__ __forceinline__ void st_agent(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ T ld_agent(const T* p) {
+  return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 }  // namespace tnp
 
 using tnp::TnpLB;

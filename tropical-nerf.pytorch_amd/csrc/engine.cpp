@@ -157,7 +157,7 @@ struct tnp_engine {
   // records in cell order; used/nid/flags: int32 scratch of compaction,
   // surface and skeleton)
   Buf blk, blkoff, scan_scr, sa, sb, stage, shared, members, pcn, pent, rstart, ent_v,
-      ents, pcell, ptoff, bcell, bstat, ckeys_a, ckeys_b, sort_scr, flags, used, nid, ctr;
+      ents, pcell, ptoff, bcell, ckeys_a, ckeys_b, sort_scr, flags, used, nid, ctr;
   uint64_t* ckeys = nullptr;  // sorted connecting edges of the current step
   int64_t* h_ctr = nullptr;  // host copy of ctr (the last readback)
   int64_t* h_map = nullptr;  // host-mapped mirror written by k_publish ([31]: sequence)
@@ -415,7 +415,7 @@ extern "C" void tnp_engine_destroy(tnp_engine* e) {
   Buf* bufs[] = {&e->edges, &e->edges_alt, &e->blk, &e->blkoff, &e->scan_scr, &e->sa, &e->sb,
                  &e->stage, &e->shared, &e->members, &e->pcn, &e->pent, &e->rstart,
                  &e->ent_v, &e->ents, &e->pcell, &e->ptoff, &e->bcell,
-                 &e->bstat, &e->ckeys_a, &e->ckeys_b, &e->sort_scr, &e->flags, &e->used, &e->nid,
+                 &e->ckeys_a, &e->ckeys_b, &e->sort_scr, &e->flags, &e->used, &e->nid,
                  &e->ctr, &e->tri, &e->faces, &e->lb[0], &e->lb[1], &e->edm, &e->esm,
                  &e->edm_alt, &e->esm_alt, &e->live, &e->tied_table};
   for (Buf* b : bufs) buf_free(*b, s);
@@ -934,11 +934,11 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     // spatial buckets, every count on the device (bucket.hip)
     void* const bk0 = e->bk[0].p;
     void* const bk1 = e->bk[1].p;
-    if (buf_ensure(e->bk[0], NB * sizeof(int32_t), s)) return -1;        // counts
+    if (buf_ensure(e->bk[0], (NB + 1) * sizeof(int32_t), s)) return -1;  // counts (+1: read in pairs)
     if (buf_ensure(e->bk[1], NB * sizeof(int32_t), s)) return -1;        // cursors
     if (e->bk[0].p != bk0 || e->bk[1].p != bk1) e->bk_clean = false;     // fresh memory
     if (buf_ensure(e->bk[2], (NB + 1) * sizeof(int64_t), s)) return -1;  // bases
-    if (buf_ensure(e->bk[3], NB * sizeof(int32_t), s)) return -1;        // pair cells
+    if (buf_ensure(e->bk[3], NB * sizeof(int64_t), s)) return -1;        // pair cells
     if (buf_ensure(e->bk[4], NB * sizeof(int64_t), s)) return -1;        // pairs
     if (buf_ensure(e->bk[5], (NB + 1) * sizeof(int64_t), s)) return -1;  // pair-cell offsets
     if (buf_ensure(e->bk[6], (NB + 1) * sizeof(int64_t), s)) return -1;  // pair offsets
@@ -949,16 +949,20 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     if (buf_ensure(e->bk[12], NB * sizeof(int64_t), s)) return -1;        // window-pass pairs
     if (buf_ensure(e->bk[13], (NB + 1) * sizeof(int64_t), s)) return -1;
     if (buf_ensure(e->sents, TB * sizeof(uint64_t), s)) return -1;
+    // a pruning step recomputes the live flags: zeroed by the bucket count
+    // (after the hit pass read them), re-marked by the prune
+    if (prune && buf_ensure(e->live, std::max<int64_t>(NV, 16), s)) return -1;
     TIMED("bucket_entries", 16.0 * M,  // + 8 B per entry, set once T is known
           launch_bucket_entries(P<int32_t>(e->members), S, V, M, grid, zero, idx, e->net.n_marks,
                                 P<int32_t>(e->bk[0]), P<int32_t>(e->bk[1]), P<int64_t>(e->bk[2]),
-                                P<int64_t>(e->bk[7]), P<uint64_t>(e->sents), e->bk_clean, ctr, s));
+                                P<int64_t>(e->bk[7]), P<uint64_t>(e->sents), e->bk_clean,
+                                prune ? P<uint8_t>(e->live) : nullptr, NV, ctr, s));
     e->bk_clean = false;  // until the gather below has reset the counters
     TIMED("bucket_group", 0.0,
           launch_bucket_pairs(e->net.n_marks, P<int64_t>(e->bk[2]), P<uint64_t>(e->sents),
                               P<uint64_t>(c.pz), P<CellEnt>(e->ents),
                               P<int32_t>(e->bk[8]), P<int32_t>(e->bk[9]), P<int32_t>(e->bk[10]),
-                              P<int64_t>(e->bk[11]), P<int32_t>(e->bk[3]), P<int64_t>(e->bk[4]),
+                              P<int64_t>(e->bk[11]), P<int64_t>(e->bk[3]), P<int64_t>(e->bk[4]),
                               P<int64_t>(e->bk[12]), P<int64_t>(e->bk[13]),
                               P<int64_t>(e->bk[5]), P<int64_t>(e->bk[6]), P<int32_t>(e->pcell),
                               P<int32_t>(e->pent), P<int32_t>(e->pcn), P<int64_t>(e->ptoff),
@@ -1028,7 +1032,6 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   //    keep their capacity across steps and grow (then redo) on overflow.
   int nb = 1;
   while (nb < 31 && (1ll << nb) < NV) ++nb;
-  if (buf_ensure(e->bstat, 6 * connect_grid() * sizeof(int64_t), s)) return -1;
   // connecting edges this step's pruning drops are never appended (sorted,
   // re-tested): keep_edge() depends on the endpoints only
   const uint64_t cfmask = prune ? prune_mask(idx, K - 1) : 0ull;
@@ -1054,13 +1057,10 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
           launch_connect(P<int64_t>(e->ptoff), P<int32_t>(e->pcell), P<int32_t>(e->pcn),
                          P<int32_t>(e->pent), NC, e->max_pair_tests, P<int32_t>(e->bcell),
                          P<CellEnt>(e->ents), idx, nb, cfmask, P<uint64_t>(e->ckeys_a), cap, ctr,
-                         P<int64_t>(e->bstat), s, !buckets));
+                         s));
     if (buckets) {
-      const int g = connect_grid();
       TIMED("connect_win", 0.0,
-            launch_connect_win(P<CellEnt>(e->ents), idx, nb, cfmask, P<uint64_t>(e->ckeys_a), cap, ctr,
-                               P<int64_t>(e->bstat) + 3 * g, s));
-      if (launch_connect_sum(P<int64_t>(e->bstat), 2 * g, ctr, s)) return -1;
+            launch_connect_win(P<CellEnt>(e->ents), idx, nb, cfmask, P<uint64_t>(e->ckeys_a), cap, ctr, s));
     }
     if (read_ctr(e, s)) return -1;
     if (buckets) {
@@ -1129,7 +1129,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     // live flags recomputed from the kept edges; no vertex moves (lazy
     // compaction): the distinct flagged count is the reference's V'
     if (buf_ensure(e->live, std::max<int64_t>(NV, 16), s)) return -1;
-    TNP_CHECK(hipMemsetAsync(e->live.p, 0, NV, s));
+    if (!buckets) TNP_CHECK(hipMemsetAsync(e->live.p, 0, NV, s));  // else zeroed by the bucket count
     if (ensure_masks(e, s)) return -1;  // (curve path: recomputed after the rewiring)
     const int64_t N1 = std::max<int64_t>(N, 1);
     if (buf_ensure(e->edm_alt, N1 * sizeof(uint8_t), s)) return -1;

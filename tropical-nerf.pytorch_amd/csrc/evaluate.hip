@@ -75,23 +75,26 @@ __global__ void k_mc_cube_counts(const float* __restrict__ vol, Dims d, float is
 }
 
 __global__ void k_mc_vertices(const float* __restrict__ vol, Dims d, float iso,
-                              const int64_t* __restrict__ eoff, float* __restrict__ verts) {
+                              const int64_t* __restrict__ eoff, double* __restrict__ verts) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t N = (int64_t)d.n0 * d.n1 * d.n2;
   if (p >= N) return;
   const int k = (int)(p % d.n2), j = (int)((p / d.n2) % d.n1), i = (int)(p / ((int64_t)d.n1 * d.n2));
-  const float v0 = vol[p];
+  const double v0 = vol[p];
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
     const int64_t e = 3 * p + a;
     if (eoff[e + 1] == eoff[e]) continue;  // not crossed
     const int64_t q = pidx(d, i + (a == 0), j + (a == 1), k + (a == 2));
-    const float t = __fdiv_rn(__fsub_rn(iso, v0), __fsub_rn(vol[q], v0));
-    float* o = verts + 3 * eoff[e];
-    o[0] = (float)i;
-    o[1] = (float)j;
-    o[2] = (float)k;
-    o[a] = __fadd_rn(o[a], t);
+    // in double, as PyMCubes interpolates: an fp32 i + t snaps every t below
+    // half an ulp of i onto the lattice point, and two such vertices of one
+    // triangle make it degenerate (a zero normal in the -e angular distance)
+    const double t = __ddiv_rn(__dsub_rn((double)iso, v0), __dsub_rn((double)vol[q], v0));
+    double* o = verts + 3 * eoff[e];
+    o[0] = (double)i;
+    o[1] = (double)j;
+    o[2] = (double)k;
+    o[a] = __dadd_rn(o[a], t);
   }
 }
 
@@ -333,7 +336,7 @@ extern "C" int tnp_mc_count(const float* d_vol, int n0, int n1, int n2, float is
 
 extern "C" int tnp_mc_emit(const float* d_vol, int n0, int n1, int n2, float iso,
                            const int8_t* d_table, const int64_t* d_eoff, const int64_t* d_coff,
-                           float* d_verts, int64_t* d_tris, void* stream) {
+                           double* d_verts, int64_t* d_tris, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const Dims d{n0, n1, n2};
   const int64_t N = (int64_t)n0 * n1 * n2, C = (int64_t)(n0 - 1) * (n1 - 1) * (n2 - 1);

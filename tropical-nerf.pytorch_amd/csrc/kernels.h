@@ -8,6 +8,8 @@
 
 // Net descriptor passed BY VALUE as a kernel argument (lives in SGPRs /
 // the kernarg segment; every field is wave-uniform).
+constexpr int TNP_MAX_MARKS = 1024;  // marks per axis (k_forward_new stages them in LDS)
+
 struct NetDev {
   float scales[TNP_MAX_LEVELS];
   int32_t res[TNP_MAX_LEVELS];

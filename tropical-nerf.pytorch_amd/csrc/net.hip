@@ -115,7 +115,9 @@ k_forward_new(NetDev net, const float* xyz, int64_t n, float* __restrict__ pre,
   constexpr int IN = 2 * LV;
   constexpr int NW = H * IN + H + (NL - 2) * (H * H + H) + 2 * H + 2;
   __shared__ float w[NW];
+  __shared__ float mk[TNP_MAX_MARKS];
   for (int i = threadIdx.x; i < NW; i += blockDim.x) w[i] = net.weights[i];
+  for (int i = threadIdx.x; i < net.n_marks; i += blockDim.x) mk[i] = net.marks[i];
   __syncthreads();
   // XCD-contiguous chunks of the (edge-ordered, spatially coherent) splits:
   // the hash-table lines one XCD's splits touch then mostly fit its L2
@@ -123,12 +125,14 @@ k_forward_new(NetDev net, const float* xyz, int64_t n, float* __restrict__ pre,
   const bool live = i < n;
   const float eps = net.eps;
   float x[3] = {0.f, 0.f, 0.f};
-  uint64_t m = 0;
+  uint64_t m = 0, ga = 0, gb = 0;
   if (live) {
     const int a = sa[i], b = sb[i];
     // every gather the endpoints need, issued before the first store (the
     // coordinate store could alias zero[] for the compiler)
     const uint64_t za = zero[a], zb = zero[b];
+    ga = grid[a];
+    gb = grid[b];
     if (scol) {
       // the split point itself (k_new_vertices, subpoly.py:113-117, 180), fused:
       // d = d/eps; w = |d0| / |d1 - d0|; v = e0*(1-w) + e1*w
@@ -148,7 +152,7 @@ k_forward_new(NetDev net, const float* xyz, int64_t n, float* __restrict__ pre,
       for (int d = 0; d < 3; ++d) {
         const float v = __fadd_rn(__fmul_rn(ea[d], om), __fmul_rn(eb[d], w));
         out[d] = v;
-        x[d] = __fdiv_rn(__fadd_rn(v, 1.0f), 2.0f);  // Net.preprocess, as load_point
+        x[d] = __fmul_rn(__fadd_rn(v, 1.0f), 0.5f);  // Net.preprocess, as load_point (x/2 == x*0.5 exactly)
       }
     } else {
       load_point(xyz, i, x);
@@ -198,7 +202,7 @@ k_forward_new(NetDev net, const float* xyz, int64_t n, float* __restrict__ pre,
     pz[V + i] = make_ulonglong2(ps, zs);
     shared[i] = m;
   }
-  const uint64_t g = grid_word(net.marks, net.n_marks, eps, x);
+  const uint64_t g = scol ? grid_word_near(mk, net.n_marks, eps, x, ga, gb) : grid_word(mk, net.n_marks, eps, x);
   if (live) grid[V + i] = g;
   if (__ballot(live && bad) && tnp::lane() == 0) tnp::or_sticky(&ctr[CTR_FAIL], 1ull);
   if (own_lo <= own_hi) {
@@ -347,6 +351,7 @@ int launch_forward_new(const NetDev& net, const float* xyz, int64_t n, float* pr
                        uint64_t* shared, int64_t* ctr, uint64_t* pz, const float* col, hipStream_t s) {
   if (n <= 0) return 0;
   if (!net_supported(net)) { tnp_set_error("unsupported net shape"); return -1; }
+  if (net.n_marks > TNP_MAX_MARKS) { tnp_set_error("more than %d marks per axis", TNP_MAX_MARKS); return -1; }
   TNP_DISPATCH(net.n_levels, {
     hipLaunchKernelGGL((k_forward_new<L_, 16, 3>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net,
                        xyz, n, pre, ld, V, keep_from, sa, sb, idx, own_lo, own_hi, pos, zero, grid,

@@ -33,7 +33,10 @@ enum {
   CTR_R = 25,       // cells with at least one member pair
   CTR_RUNS = 26,    // occupied cells (runs of equal keys in the sorted entries)
   CTR_SPAIRS = 27,  // member pairs of the cells the window pass tests (<= WCELL members)
-  CTR_N = 28
+  CTR_TK0 = 28,     // last-workgroup tickets (tnp::last_block) of the fused
+  CTR_TK1 = 29,     //   bucket count / bucket group / window pass launches
+  CTR_TK2 = 30,
+  CTR_N = 31        // <= 31: the host-mapped mirror keeps its sequence word at [31]
 };
 
 int64_t step_tiles(int64_t n);
@@ -132,8 +135,9 @@ int launch_entry_keys(const int32_t* ent_v, const uint32_t* ekey, int NC, int64_
 // -> CTR_BOVF); connect counts every connecting edge in ctr[CTR_X] and
 // appends the packed keys (lo << nb | hi) of those the step's pruning keeps
 // (fmask != 0: endpoint keys differ on the planes of fmask; fmask == 0: all)
-// to keys[0, cap), counted in ctr[CTR_XK]; bstat needs 3 * connect_grid()
-// slots.
+// to keys[0, cap), counted in ctr[CTR_XK]; per block, the compatible pairs,
+// shared regions and connecting edges are added to ctr[CTR_COMPAT],
+// ctr[CTR_P], ctr[CTR_X].
 int64_t connect_chunks(int64_t TT);
 int64_t connect_grid();
 int launch_chunk_cells(const int64_t* ptoff, const int32_t* pn, int64_t rcap, int32_t* bcell,
@@ -141,9 +145,7 @@ int launch_chunk_cells(const int64_t* ptoff, const int32_t* pn, int64_t rcap, in
 int launch_connect(const int64_t* ptoff, const int32_t* pcell, const int32_t* pn,
                    const int32_t* pent, int NC, int64_t max_tests, const int32_t* bcell,
                    const CellEnt* ent, int idx, int nb, uint64_t fmask, uint64_t* keys,
-                   int64_t cap, int64_t* ctr, int64_t* bstat, hipStream_t s, bool sum = true);
-// per-block counters of nblk blocks -> ctr[CTR_COMPAT], ctr[CTR_P], ctr[CTR_X]
-int launch_connect_sum(const int64_t* bstat, int64_t nblk, int64_t* ctr, hipStream_t s);
+                   int64_t cap, int64_t* ctr, hipStream_t s);
 // single-pass pruning over [edges; e_new; c_new] (lb_tiles(E + S + X)
 // look-back tiles): kept edges in order -> out, used flags (zeroed by the
 // caller), ctr[CTR_E], ctr[CTR_ACTIVE]
@@ -173,11 +175,12 @@ int bucket_geometry(int n_marks, int* sh, int* NBd, int* NB);
 // << 32 | vertex) (8 M capacity)
 // members: the step's S new vertices are slots V.. (not listed), the hits
 // follow in members[S, M).  clean: bcount/bcur are known to be zero (the
-// previous step's launch_bucket_pairs reset them)
+// previous step's launch_bucket_pairs reset them).  live != null: nlive
+// live flags zeroed on the way (the prune re-marks them).  Uses ctr[CTR_TK0].
 int launch_bucket_entries(const int32_t* members, int64_t S, int64_t V, int64_t M, const uint64_t* grid,
                           const uint64_t* zero, int idx, int n_marks, int32_t* bcount, int32_t* bcur,
-                          int64_t* bbase, int64_t* part, uint64_t* ekv, bool clean, int64_t* ctr,
-                          hipStream_t s);
+                          int64_t* bbase, int64_t* part, uint64_t* ekv, bool clean, uint8_t* live,
+                          int64_t nlive, int64_t* ctr, hipStream_t s);
 // per bucket: cell-contiguous CellEnt records (ents, entry positions), the
 // pair cells; then the global pair-cell list (pcell, pent, pn, ptoff; R ->
 // ctr[CTR_R], pairs -> ctr[CTR_TESTS]) that launch_connect walks.
@@ -188,7 +191,7 @@ int launch_bucket_entries(const int32_t* members, int64_t S, int64_t V, int64_t 
 // bcount/bcur zeroed for the next step.
 int launch_bucket_pairs(int n_marks, const int64_t* bbase, const uint64_t* ekv, const uint64_t* pz,
                         CellEnt* ents, int32_t* lcell,
-                        int32_t* lent, int32_t* ln, int64_t* lpoff, int32_t* bnpc, int64_t* bnpairs,
+                        int32_t* lent, int32_t* ln, int64_t* lpoff, int64_t* bnpc, int64_t* bnpairs,
                         int64_t* bspairs, int64_t* spoff, int64_t* pcoff, int64_t* pairoff,
                         int32_t* pcell, int32_t* pent, int32_t* pn, int64_t* ptoff, int32_t* bcell,
                         int64_t bcap, int32_t* bcount, int32_t* bcur, int64_t* ctr, hipStream_t s);
@@ -196,10 +199,9 @@ int launch_bucket_pairs(int n_marks, const int64_t* bbase, const uint64_t* ekv, 
 int64_t connect_chunk_pairs();
 // window pass over the cell-contiguous entries (count ctr[CTR_T]): every
 // pair of a cell of <= WCELL members, same emission rules and counters as
-// launch_connect (bstat: its own 3 * connect_grid() slots; sum with
-// launch_connect_sum)
+// launch_connect
 int launch_connect_win(const CellEnt* ent, int idx, int nb, uint64_t fmask, uint64_t* keys, int64_t cap,
-                       int64_t* ctr, int64_t* bstat, hipStream_t s);
+                       int64_t* ctr, hipStream_t s);
 
 // ---- sort.hip ----
 // ascending LSD radix sort of n u64 keys on bits [0, bits); the sorted keys

@@ -528,6 +528,21 @@ __device__ __forceinline__ void cell_coords(int64_t cell, int NC, int cc[3]) {
   cc[0] = (int)(cell / ((int64_t)NC * NC)) - 2;
 }
 
+// a block's (compatible pairs, shared regions, connecting edges) totals
+//   -> ctr[CTR_COMPAT], ctr[CTR_P], ctr[CTR_X] (three adds per block)
+__device__ __forceinline__ void add_pair_stats(int64_t a, int64_t r, int64_t x, int64_t* lds,
+                                               int64_t* __restrict__ ctr) {
+  int64_t ta, tr, tx;
+  tnp::block_scan_excl(a, lds, ta);
+  tnp::block_scan_excl(r, lds, tr);
+  tnp::block_scan_excl(x, lds, tx);
+  if (threadIdx.x == 0) {
+    if (ta) atomicAdd((unsigned long long*)&ctr[CTR_COMPAT], (unsigned long long)ta);
+    if (tr) atomicAdd((unsigned long long*)&ctr[CTR_P], (unsigned long long)tr);
+    if (tx) atomicAdd((unsigned long long*)&ctr[CTR_X], (unsigned long long)tx);
+  }
+}
+
 // The flattened pair-index space of all cells (cell-major, then (i, j<i)
 // within the cell's member list) split evenly over threads: every thread
 // tests CIPT consecutive pairs, so a cell of 10^4 members costs the same per
@@ -575,7 +590,7 @@ k_connect(const int64_t* __restrict__ ptoff, const int32_t* __restrict__ pcell,
           const int32_t* __restrict__ pn, const int32_t* __restrict__ pent, int NC,
           int64_t max_tests, const int32_t* __restrict__ bcell, const CellEnt* __restrict__ ent,
           int idx, int nb, uint64_t fmask, uint64_t* __restrict__ keys, int64_t cap,
-          int64_t* __restrict__ ctr, int64_t* __restrict__ bstat) {
+          int64_t* __restrict__ ctr) {
   __shared__ int64_t lds[TNP_WAVES];
   __shared__ int64_t s_base;
   __shared__ int32_t s_off[CONNECT_CELLS];  // first pair of the cell - chunk start
@@ -700,13 +715,7 @@ k_connect(const int64_t* __restrict__ ptoff, const int32_t* __restrict__ pcell,
   for (int k = 0; k < ne; ++k)
     if (w0 + k < cap) keys[w0 + k] = kk[k];
   }
-  int64_t tot;
-  tnp::block_scan_excl(n_compat, lds, tot);
-  if (threadIdx.x == 0) bstat[3 * blockIdx.x] = tot;
-  tnp::block_scan_excl(n_reg, lds, tot);
-  if (threadIdx.x == 0) bstat[3 * blockIdx.x + 1] = tot;
-  tnp::block_scan_excl(n_conn, lds, tot);
-  if (threadIdx.x == 0) bstat[3 * blockIdx.x + 2] = tot;
+  add_pair_stats(n_compat, n_reg, n_conn, lds, ctr);
 }
 
 // ---------------------------------------------------------------------------
@@ -728,8 +737,7 @@ __device__ __forceinline__ void lds_fence() {
 
 __global__ void __launch_bounds__(TNP_BLOCK)
 k_connect_win(const CellEnt* __restrict__ ent, int idx, int nb, uint64_t fmask,
-              uint64_t* __restrict__ keys, int64_t cap, int64_t* __restrict__ ctr,
-              int64_t* __restrict__ bstat) {
+              uint64_t* __restrict__ keys, int64_t cap, int64_t* __restrict__ ctr) {
   __shared__ CellEnt st[TNP_WAVES][64];
   __shared__ int exc[TNP_WAVES][64];
   __shared__ uint64_t kb[TNP_WAVES][WKEYS];
@@ -813,34 +821,9 @@ k_connect_win(const CellEnt* __restrict__ ent, int idx, int nb, uint64_t fmask,
     lds_fence();
   }
   if (kn) flush();
-  int64_t tot;
-  tnp::block_scan_excl(n_compat, lds, tot);
-  if (threadIdx.x == 0) bstat[3 * blockIdx.x] = tot;
-  tnp::block_scan_excl(n_reg, lds, tot);
-  if (threadIdx.x == 0) bstat[3 * blockIdx.x + 1] = tot;
-  tnp::block_scan_excl(n_conn, lds, tot);
-  if (threadIdx.x == 0) bstat[3 * blockIdx.x + 2] = tot;
+  add_pair_stats(n_compat, n_reg, n_conn, lds, ctr);
 }
 
-// per-block (compatible pairs, shared regions, connecting edges)
-//   -> ctr[CTR_COMPAT], ctr[CTR_P], ctr[CTR_X]
-__global__ void __launch_bounds__(TNP_BLOCK)
-k_sum_bstat(const int64_t* __restrict__ bstat, int64_t nblk, int64_t* __restrict__ ctr) {
-  int64_t a = 0, r = 0, x = 0;
-  for (int64_t i = threadIdx.x; i < nblk; i += blockDim.x) {
-    a += bstat[3 * i];
-    r += bstat[3 * i + 1];
-    x += bstat[3 * i + 2];
-  }
-  a = tnp::wave_sum(a);
-  r = tnp::wave_sum(r);
-  x = tnp::wave_sum(x);
-  if (tnp::lane() == 0) {
-    atomicAdd((unsigned long long*)&ctr[CTR_COMPAT], (unsigned long long)a);
-    atomicAdd((unsigned long long*)&ctr[CTR_P], (unsigned long long)r);
-    atomicAdd((unsigned long long*)&ctr[CTR_X], (unsigned long long)x);
-  }
-}
 // ---------------------------------------------------------------------------
 // pruning: keep an edge iff its endpoints' future sign keys (planes >= idx)
 // differ (subpoly.py:252-265).  The candidate list is the concatenation
@@ -1282,7 +1265,6 @@ static int resident_grid(K kernel, int slot) {
   return g;
 }
 static int connect_grid_size() {
-  // the window pass shares the bstat layout: one grid size for both
   return std::max(resident_grid(k_connect, 0), resident_grid(k_connect_win, 1));
 }
 int64_t connect_chunks(int64_t TT) { return (TT + CCH - 1) / CCH; }
@@ -1297,25 +1279,18 @@ int launch_chunk_cells(const int64_t* ptoff, const int32_t* pn, int64_t rcap, in
 int launch_connect(const int64_t* ptoff, const int32_t* pcell, const int32_t* pn,
                    const int32_t* pent, int NC, int64_t max_tests, const int32_t* bcell,
                    const CellEnt* ent, int idx, int nb, uint64_t fmask, uint64_t* keys,
-                   int64_t cap, int64_t* ctr, int64_t* bstat, hipStream_t s, bool sum) {
+                   int64_t cap, int64_t* ctr, hipStream_t s) {
   static_assert(CONNECT_CELLS >= CCH + 2, "chunk cell window");
   const int grid = connect_grid_size();
   hipLaunchKernelGGL(k_connect, dim3(grid), dim3(TNP_BLOCK), 0, s, ptoff, pcell, pn,
-                     pent, NC, max_tests, bcell, ent, idx, nb, fmask, keys, cap, ctr, bstat);
-  if (sum) hipLaunchKernelGGL(k_sum_bstat, dim3(1), dim3(TNP_BLOCK), 0, s, bstat, (int64_t)grid, ctr);
+                     pent, NC, max_tests, bcell, ent, idx, nb, fmask, keys, cap, ctr);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
 int launch_connect_win(const CellEnt* ent, int idx, int nb, uint64_t fmask, uint64_t* keys, int64_t cap,
-                       int64_t* ctr, int64_t* bstat, hipStream_t s) {
+                       int64_t* ctr, hipStream_t s) {
   const int grid = connect_grid_size();
-  hipLaunchKernelGGL(k_connect_win, dim3(grid), dim3(TNP_BLOCK), 0, s, ent, idx, nb, fmask, keys, cap, ctr,
-                     bstat);
-  TNP_CHECK(hipGetLastError());
-  return 0;
-}
-int launch_connect_sum(const int64_t* bstat, int64_t nblk, int64_t* ctr, hipStream_t s) {
-  hipLaunchKernelGGL(k_sum_bstat, dim3(1), dim3(TNP_BLOCK), 0, s, bstat, nblk, ctr);
+  hipLaunchKernelGGL(k_connect_win, dim3(grid), dim3(TNP_BLOCK), 0, s, ent, idx, nb, fmask, keys, cap, ctr);
   TNP_CHECK(hipGetLastError());
   return 0;
 }

@@ -80,9 +80,9 @@ def run_marching_cubes(net, n: int) -> Mesh:
     pts = torch.stack([gx, gy, gz], dim=-1).reshape(-1, 3).to(net.device())
     sdfs = net.sdf(pts)[:, 0].reshape(n, n, n)
     v, t = marching_cubes_torch(-sdfs, 0.0)
-    v = v.double() / (n - 1.0) * 2 * CANVAS_SIZE - CANVAS_SIZE
+    v = v / (n - 1.0) * 2 * CANVAS_SIZE - CANVAS_SIZE
     v = v / R
-    return Mesh(v.float().cpu().numpy(), t.cpu().numpy())
+    return Mesh(v.cpu().numpy(), t.cpu().numpy())  # float64, as the reference's trimesh
 
 
 def get_rays(n: int = 100000):

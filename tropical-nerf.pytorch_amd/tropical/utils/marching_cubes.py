@@ -28,7 +28,7 @@ def _table(device) -> torch.Tensor:
 
 
 def marching_cubes_torch(volume: torch.Tensor, iso: float = 0.0):
-    """volume: fp32 ROCm tensor [n0, n1, n2] -> (vertices fp32 [V, 3],
+    """volume: fp32 ROCm tensor [n0, n1, n2] -> (vertices fp64 [V, 3],
     triangles int64 [F, 3]) on the same device."""
     _hip.require_cuda(volume, "marching_cubes")
     vol = volume.detach().to(torch.float32).contiguous()
@@ -42,7 +42,7 @@ def marching_cubes_torch(volume: torch.Tensor, iso: float = 0.0):
     L = _hip.lib()
     _hip.check(L.tnp_mc_count(_hip.ptr(vol), n0, n1, n2, float(iso), _hip.ptr(tab), _hip.ptr(eoff),
                               _hip.ptr(coff), C.byref(nv), C.byref(nt), s), "tnp_mc_count")
-    verts = torch.empty(nv.value, 3, dtype=torch.float32, device=dev)
+    verts = torch.empty(nv.value, 3, dtype=torch.float64, device=dev)
     tris = torch.empty(nt.value, 3, dtype=torch.int64, device=dev)
     _hip.check(L.tnp_mc_emit(_hip.ptr(vol), n0, n1, n2, float(iso), _hip.ptr(tab), _hip.ptr(eoff),
                              _hip.ptr(coff), _hip.ptr(verts), _hip.ptr(tris), s), "tnp_mc_emit")
@@ -55,4 +55,4 @@ def marching_cubes(volume, iso: float = 0.0):
     if not isinstance(volume, torch.Tensor):
         volume = torch.from_numpy(np.ascontiguousarray(volume, dtype=np.float32)).cuda()
     v, t = marching_cubes_torch(volume, iso)
-    return v.cpu().numpy().astype(np.float64), t.cpu().numpy()
+    return v.cpu().numpy(), t.cpu().numpy()
