@@ -12,7 +12,7 @@ Net(num_layers=3, num_hidden=16, levels=2, r_min=G-1, r_max=G-1, T=19)
 (G marks per axis; hash table U(-0.1,0.1), nn.Linear-bound MLP, numpy PCG64
 seed 6 by default, see --seed), initial edges = the full G^3 lattice.  G = 128 at one GPU; at N GPUs
 the lattice grows to round(128 * N^(1/3)) marks per axis and is cut into N
-x-slabs of cells, each extracted with a two-cell halo (weak scaling, one
+x-slabs of cells, each extracted with a halo of cells (as wide as halo_check needs) (weak scaling, one
 process per GPU, RCCL only for the per-step 8-byte agreements; the slabs
 are stitched into one complex after the timed region,
 tropical/distributed.py).  value = edges subdivided by all ranks (each
@@ -266,19 +266,32 @@ def main():
     from tropical._engine import engine_for
     G = args.marks if world == 1 else int(round(args.marks * world ** (1.0 / 3.0)))
     net = make_net(G, dev, args.seed)
-    from tropical.distributed import slab_cuts, slab_marks
+    from tropical.distributed import HALOS, halo_check, slab_cuts, slab_marks
     cuts = slab_cuts(G, world)
-    x0, x1 = slab_marks(cuts, rank)  # this rank's cells + a HALO-cell halo each side
     eng = engine_for(net)
     if world > 1:
         eng.set_owned(cuts[rank], cuts[rank + 1])  # halo splits -> S_dup
     eng.set_shards(world)
+    slab = [0, G - 1]
 
     def one_pass():
         stats = []
-        eng.lattice(x0, x1)
+        eng.lattice(*slab)
         eng.run_steps(stats, coll)
         return stats
+
+    halo = 0
+    if world > 1:
+        # this rank's cells + a halo each side, as wide as halo_check needs
+        # (untimed: one pass per width tried)
+        for k, halo in enumerate(HALOS):
+            slab[:] = slab_marks(cuts, rank, halo)
+            one_pass()
+            Vl, El, _ = eng.export()
+            ok = halo_check(Vl.to(comm_dev), El.to(comm_dev), net.enc.marks, cuts,
+                            raise_=k == len(HALOS) - 1)
+            if ok is not None:
+                break
 
     def barrier():
         torch.cuda.synchronize(dev)
@@ -322,7 +335,7 @@ def main():
         # views next to every cut compared (fails loudly if a halo was too
         # narrow), stitched into one global complex (tropical/distributed.py;
         # RCCL all_gathers), untimed
-        from tropical.distributed import halo_check, stitch
+        from tropical.distributed import stitch
         Vl, El, _ = eng.export()
         halo_check(Vl.to(comm_dev), El.to(comm_dev), net.enc.marks, cuts)
         owned, first, gE, own, keep = stitch(Vl.to(comm_dev), El.to(comm_dev), net.enc.marks, cuts,
@@ -380,7 +393,8 @@ def main():
                                    f"({'x-slab per GPU' if world > 1 else 'one GPU'}), flat path, all "
                                    f"{net.K} hyperplane steps", "marks_per_axis": G,
                        "lattice_vertices": G ** 3, "edges_subdivided_per_pass": int(per_pass),
-                       "seed": args.seed, "table_amp": 0.1, "parallelism": f"xslab{world}"},
+                       "seed": args.seed, "table_amp": 0.1, "parallelism": f"xslab{world}",
+                       "halo_cells": halo},
             "roofline": roof,
             "loop_model_bytes_per_pass": int(bytes_tot / args.steps),
             "loop_model_gbs": round(loop_gbs, 1),

@@ -1,6 +1,6 @@
 """CPU, world_size 2 over gloo: the N>1 path of bench.py.
 
-Each rank extracts its x-slab of the synthetic lattice with a two-cell halo
+Each rank extracts its x-slab of the synthetic lattice with a two-cell halo (the default HALO)
 (tropical/distributed.py::slab_marks; tropical/synthetic.py::slab_lattice ==
 tnp_engine_lattice's layout) and takes the reference's two whole-complex
 decisions per step -- "does anything split" (subpoly.py:110) and the

@@ -15,9 +15,11 @@ A slab cut exactly at the plane misses those edges (measured: 930 of 21.9M
 splits at 161^3 / 2 ranks).  A halo computes them; what the halo itself
 misses at its OUTER plane can reach one cell further in only through another
 such eps coincidence (a vertex split off a missing edge within eps of the
-next plane), so each halo column divides the residual by the chance of a
-coincidence (one column still left 3 vertices of 23.6M at 161^3; two:
-see tools/multi_rehearsal.sh).  stitch() raises if a residual remains.
+next plane), at most one cell per active step, so each halo column divides
+the residual by the chance of a coincidence (one column still left 3
+vertices of 23.6M at 161^3; two suffice there, three at 203^3 and 256^3 with
+seed 6).  The width is therefore FOUND: bench.py and subpoly_sharded() try
+the widths of HALOS in turn until halo_check (below) passes.
 
 Stitching (one pair of all_gathers, RCCL over xGMI / gloo on CPU):
 * vertex owner = the rank owning its cell or plane (grid sense, eps rule);
@@ -56,7 +58,12 @@ def slab_cuts(n_marks: int, world: int) -> list:
     return [round(r * (n_marks - 1) / world) for r in range(world + 1)]
 
 
-HALO = 2  # cell columns extracted beyond each cut plane
+HALO = 2  # first halo tried: cell columns extracted beyond each cut plane
+# the widths tried in turn while halo_check still sees a difference (the
+# error front of a slab's outer boundary moves inward by at most one cell per
+# active step, and only through eps coincidences: how far it gets depends on
+# the net and the lattice, so the width is found, then checked again)
+HALOS = (2, 3, 4, 6, 8, 12, 16, 24, 33)
 
 
 def slab_marks(cuts: list, rank: int, halo: int = HALO):
@@ -177,10 +184,11 @@ def cut_fingerprint(vertices: Tensor, edges: Tensor, marks: Tensor, cut: int, ep
 
 
 def halo_check(vertices: Tensor, edges: Tensor, marks: Tensor, cuts: list, eps: float = 1e-4,
-               group=None):
+               group=None, raise_: bool = True):
     """Compare, across every cut, the two neighbours' complexes next to the
-    cut (cut_fingerprint); raise RuntimeError on any difference.  Returns the
-    per-cut fingerprints (rank 0's view) for logging."""
+    cut (cut_fingerprint); raise RuntimeError on any difference (raise_=False:
+    return None instead, on every rank).  Returns the per-cut fingerprints
+    (rank 0's view) for logging."""
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     mine = torch.zeros(2, 4, dtype=torch.int64, device=comm_device(group, vertices.device))
     if rank > 0:
@@ -196,6 +204,8 @@ def halo_check(vertices: Tensor, edges: Tensor, marks: Tensor, cuts: list, eps: 
             bad.append(f"cut {cuts[r + 1]}: rank {r} sees {lo[:2]} (hash {lo[2]:x}/{lo[3]:x}), "
                        f"rank {r + 1} sees {hi[:2]} (hash {hi[2]:x}/{hi[3]:x})")
     if bad:
+        if not raise_:
+            return None
         raise RuntimeError("halo_check: the shards disagree next to a cut (halo too narrow): "
                            + "; ".join(bad))
     return [allv[r][1].tolist() for r in range(world - 1)]
@@ -271,14 +281,16 @@ def gather_complex(owned: Tensor, first: int, gedges: Tensor, dst: int = 0, grou
 
 
 def subpoly_sharded(net, size: float = 1.2, group=None, allreduce=None, stats: list = None,
-                    halo: int = HALO):
+                    halo: int = None):
     """The hot loop of subpoly() (subpoly.py:45-69) sharded over the ranks of
     `group` (one GPU each): the skeleton (tropical.py:158-225, computed whole
     on every rank -- a few lattice passes), x-slabs of equal skeleton-edge
     load, each rank's slab + halo through every hyperplane step with the
     reference's global decisions made by `allreduce(vec, op)`, then
-    halo_check and stitch.  Returns (engine, owned vertices, first global
-    id, global edges, cuts): the engine still holds this rank's slab complex."""
+    halo_check and stitch; while halo_check sees a difference, the slabs are
+    redone with the next width of HALOS (halo=None), or it raises (a fixed
+    halo).  Returns (engine, owned vertices, first global id, global edges,
+    cuts): the engine still holds this rank's slab complex."""
     from ._engine import engine_for
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     eng = engine_for(net)
@@ -296,14 +308,20 @@ def subpoly_sharded(net, size: float = 1.2, group=None, allreduce=None, stats: l
     ex = torch.minimum(off[e[:, 0]], off[e[:, 1]]).clamp(0, n_cells - 1)
     load = torch.bincount(ex, minlength=n_cells)
     cuts = balanced_cuts(load, world)
-    x0, x1 = slab_marks(cuts, rank, halo)
-    vs, es = slab_restrict(v, e, marks, x0, x1, net.eps)
-    eng.load(vs, es)
-    eng.set_owned(cuts[rank], cuts[rank + 1])
-    eng.run_steps(stats, allreduce)
-    Vl, El, _ = eng.export()
-    cd = comm_device(group, Vl.device)
-    Vl, El = Vl.to(cd), El.to(cd)
-    halo_check(Vl, El, marks, cuts, net.eps, group)
+    widths = HALOS if halo is None else (halo,)
+    for k, h in enumerate(widths):
+        x0, x1 = slab_marks(cuts, rank, h)
+        vs, es = slab_restrict(v, e, marks, x0, x1, net.eps)
+        eng.load(vs, es)
+        eng.set_owned(cuts[rank], cuts[rank + 1])
+        st = []
+        eng.run_steps(st, allreduce)
+        Vl, El, _ = eng.export()
+        cd = comm_device(group, Vl.device)
+        Vl, El = Vl.to(cd), El.to(cd)
+        if halo_check(Vl, El, marks, cuts, net.eps, group, raise_=k == len(widths) - 1) is not None:
+            break
+    if stats is not None:
+        stats.extend(st)
     owned, first, gE = stitch(Vl, El, marks, cuts, net.eps, group)
     return eng, owned, first, gE, cuts
