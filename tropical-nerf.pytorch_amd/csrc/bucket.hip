@@ -54,6 +54,19 @@ struct BGeom {
   int NBd;  // buckets per axis
 };
 
+// the new vertices' failover override, applied by the bucket count
+// (k_override_new's work; shared == null: not here)
+struct Override {
+  int flag;  // < 0: the device predicate ctr[CTR_FAIL]; else the host's decision
+  const uint64_t* shared;
+  float* pre;
+  int64_t ld;
+  int keep_from;
+  uint64_t* pos;
+  uint64_t* zero;
+  ulonglong2* pz;
+};
+
 __device__ __forceinline__ void span_of(uint64_t g, int lo[3], int n[3]) {
 #pragma unroll
   for (int d = 0; d < 3; ++d) {
@@ -118,7 +131,8 @@ k_bucket_count(const int32_t* __restrict__ members, int64_t S, int64_t V, int64_
                const uint64_t* __restrict__ grid,
                const uint64_t* __restrict__ zero, int idx, BGeom G, int NB,
                int32_t* __restrict__ bcount, int64_t* __restrict__ part, int64_t* __restrict__ bbase,
-               uint8_t* __restrict__ live, int64_t nlive, int fuse, int64_t* __restrict__ ctr) {
+               uint8_t* __restrict__ live, int64_t nlive, int fuse, Override ov,
+               int64_t* __restrict__ ctr) {
   __shared__ int hist[BUCKET_MAX];
   __shared__ int64_t lds[TNP_WAVES];
   __shared__ int last;
@@ -148,6 +162,32 @@ k_bucket_count(const int32_t* __restrict__ members, int64_t S, int64_t V, int64_
     const int v = vv[k] >= 0 ? vv[k] : 0;
     gg[k] = grid[v];
     zz[k] = zero[v];
+  }
+  // the failover override of the new vertices (masked_fill_ of their shared
+  // planes, subpoly_debug.py:48), fused here: new members are slots V + m
+  if (ov.shared && (ov.flag < 0 ? ctr[CTR_FAIL] != 0 : ov.flag != 0)) {
+    uint64_t sh[BK_IPT], ps[BK_IPT];
+#pragma unroll
+    for (int k = 0; k < BK_IPT; ++k) {  // loads first (the stores below could alias them)
+      const int64_t m = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
+      const int64_t mc = m < S ? m : 0;
+      sh[k] = ov.shared[mc];
+      ps[k] = ov.pos[V + mc];
+    }
+#pragma unroll
+    for (int k = 0; k < BK_IPT; ++k) {
+      const int64_t m = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
+      if (m >= S) continue;
+      for (uint64_t t = sh[k]; t; t &= t - 1) {
+        const int p = __builtin_ctzll(t);
+        if (p >= ov.keep_from) ov.pre[(int64_t)p * ov.ld + V + m] = 0.f;
+      }
+      const uint64_t pp = ps[k] & ~sh[k], z = zz[k] | sh[k];
+      ov.pos[V + m] = pp;
+      ov.zero[V + m] = z;
+      ov.pz[V + m] = make_ulonglong2(pp, z);
+      zz[k] = z;
+    }
   }
 #pragma unroll
   for (int k = 0; k < BK_IPT; ++k) {
@@ -271,7 +311,10 @@ k_bucket_scatter(const int32_t* __restrict__ members, int64_t S, int64_t V, int6
 // Entries go through in batches of GIPT per thread, every batch's loads in
 // flight together (a bucket can hold 10^5 entries: a block walking them one
 // dependent load -> atomic -> store chain at a time is latency-bound).
-constexpr int GIPT = 8;
+#ifndef TNP_GIPT
+#define TNP_GIPT 16
+#endif
+constexpr int GIPT = TNP_GIPT;
 
 // the grouping of one bucket of n >= 2 entries (k_bucket_group)
 template <int SH>
@@ -490,7 +533,7 @@ int bucket_geometry(int n_marks, int* sh, int* NBd, int* NB) {
 int launch_bucket_entries(const int32_t* members, int64_t S, int64_t V, int64_t M, const uint64_t* grid,
                           const uint64_t* zero, int idx, int n_marks, int32_t* bcount, int32_t* bcur,
                           int64_t* bbase, int64_t* part, uint64_t* ekv, bool clean, uint8_t* live,
-                          int64_t nlive, int64_t* ctr, hipStream_t s) {
+                          int64_t nlive, const NewOverride* ovr, int64_t* ctr, hipStream_t s) {
   int sh, NBd, NB;
   if (bucket_geometry(n_marks, &sh, &NBd, &NB)) {
     tnp_set_error("bucket geometry: %d marks", n_marks);
@@ -504,8 +547,12 @@ int launch_bucket_entries(const int32_t* members, int64_t S, int64_t V, int64_t 
   const int64_t per = (int64_t)TNP_BLOCK * BK_IPT;
   const unsigned nblk = (unsigned)std::max<int64_t>((M + per - 1) / per, 1);
   const int fuse = nblk <= FUSE_MAX_BLOCKS;
+  Override ov{0, nullptr, nullptr, 0, 0, nullptr, nullptr, nullptr};
+  if (ovr)
+    ov = Override{ovr->flag, ovr->shared, ovr->pre, ovr->ld, ovr->keep_from, ovr->pos, ovr->zero,
+                  reinterpret_cast<ulonglong2*>(ovr->pz)};
   hipLaunchKernelGGL(k_bucket_count, dim3(nblk), dim3(TNP_BLOCK), 0, s, members, S, V, M, grid, zero, idx,
-                     G, NB, bcount, part, bbase, live, nlive, fuse, ctr);
+                     G, NB, bcount, part, bbase, live, nlive, fuse, ov, ctr);
   if (!fuse)
     hipLaunchKernelGGL(k_scan_sets, dim3(1, 1), dim3(TNP_BLOCK), 0, s, ScanSet{bcount, 0, bbase, CTR_T},
                        ScanSet{}, ScanSet{}, NB, part, (int64_t)nblk, (int)CTR_A, ctr);

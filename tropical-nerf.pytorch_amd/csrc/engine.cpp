@@ -878,8 +878,12 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   uint64_t* zero = P<uint64_t>(c.zero);
   uint64_t* grid = P<uint64_t>(c.grid);
 
-  // 1. override + keys of the new vertices
-  if (e->pend_fused) {
+  int bsh = 0, bnd = 0, NB = 0;
+  const bool buckets = !e->radix_cells && bucket_geometry(e->net.n_marks, &bsh, &bnd, &NB) == 0;
+  // 1. override + keys of the new vertices (flat bucket path: the override
+  //    runs inside the bucket count, below)
+  if (e->pend_fused && buckets) {
+  } else if (e->pend_fused) {
     TIMED("override_new", 8.0 * S,
           launch_override_new(S, override_, P<uint64_t>(e->shared), P<float>(c.pre), c.cap,
                               e->valid_from, V, pos, zero, ctr, P<uint64_t>(c.pz), s));
@@ -892,8 +896,6 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
 
   // 2. members = new vertices ++ live hit vertices (ascending); the bucket
   //    path reads the new vertices as slots V.. without a list
-  int bsh = 0, bnd = 0, NB = 0;
-  const bool buckets = !e->radix_cells && bucket_geometry(e->net.n_marks, &bsh, &bnd, &NB) == 0;
   if (buf_ensure(e->members, std::max<int64_t>(NV, 1) * sizeof(int32_t), s, hits_done)) return -1;
   if (hits_done) {
     if (!buckets && launch_new_members(P<int32_t>(e->members), S, V, s)) return -1;
@@ -952,11 +954,14 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     // a pruning step recomputes the live flags: zeroed by the bucket count
     // (after the hit pass read them), re-marked by the prune
     if (prune && buf_ensure(e->live, std::max<int64_t>(NV, 16), s)) return -1;
+    NewOverride nov{override_, P<uint64_t>(e->shared), P<float>(c.pre), c.cap, e->valid_from, pos, zero,
+                    P<uint64_t>(c.pz)};
     TIMED("bucket_entries", 16.0 * M,  // + 8 B per entry, set once T is known
           launch_bucket_entries(P<int32_t>(e->members), S, V, M, grid, zero, idx, e->net.n_marks,
                                 P<int32_t>(e->bk[0]), P<int32_t>(e->bk[1]), P<int64_t>(e->bk[2]),
                                 P<int64_t>(e->bk[7]), P<uint64_t>(e->sents), e->bk_clean,
-                                prune ? P<uint8_t>(e->live) : nullptr, NV, ctr, s));
+                                prune ? P<uint8_t>(e->live) : nullptr, NV, e->pend_fused ? &nov : nullptr,
+                                ctr, s));
     e->bk_clean = false;  // until the gather below has reset the counters
     TIMED("bucket_group", 0.0,
           launch_bucket_pairs(e->net.n_marks, P<int64_t>(e->bk[2]), P<uint64_t>(e->sents),

@@ -177,10 +177,22 @@ int bucket_geometry(int n_marks, int* sh, int* NBd, int* NB);
 // follow in members[S, M).  clean: bcount/bcur are known to be zero (the
 // previous step's launch_bucket_pairs reset them).  live != null: nlive
 // live flags zeroed on the way (the prune re-marks them).  Uses ctr[CTR_TK0].
+// ovr != null: the new vertices' failover override (launch_override_new's
+// work) applied on the way, before any key is read
+struct NewOverride {
+  int flag;  // < 0: the device predicate ctr[CTR_FAIL]; else the host's decision
+  const uint64_t* shared;
+  float* pre;
+  int64_t ld;
+  int keep_from;
+  uint64_t* pos;
+  uint64_t* zero;
+  uint64_t* pz;
+};
 int launch_bucket_entries(const int32_t* members, int64_t S, int64_t V, int64_t M, const uint64_t* grid,
                           const uint64_t* zero, int idx, int n_marks, int32_t* bcount, int32_t* bcur,
                           int64_t* bbase, int64_t* part, uint64_t* ekv, bool clean, uint8_t* live,
-                          int64_t nlive, int64_t* ctr, hipStream_t s);
+                          int64_t nlive, const NewOverride* ovr, int64_t* ctr, hipStream_t s);
 // per bucket: cell-contiguous CellEnt records (ents, entry positions), the
 // pair cells; then the global pair-cell list (pcell, pent, pn, ptoff; R ->
 // ctr[CTR_R], pairs -> ctr[CTR_TESTS]) that launch_connect walks.

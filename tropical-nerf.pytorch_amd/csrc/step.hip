@@ -37,9 +37,15 @@ constexpr int TILE = TNP_BLOCK * IPT;   // tile of a compaction pass
 // single-pass (look-back) compactions: items per thread of the split / hit
 // pass (SIPT) and of the prune pass (LIPT); every item's loads are issued
 // before any is used
-constexpr int SIPT = 16;
+#ifndef TNP_SIPT
+#define TNP_SIPT 32
+#endif
+#ifndef TNP_LIPT
+#define TNP_LIPT 8
+#endif
+constexpr int SIPT = TNP_SIPT;
 constexpr int STILE = TNP_BLOCK * SIPT;
-constexpr int LIPT = 8;
+constexpr int LIPT = TNP_LIPT;
 constexpr int LTILE = TNP_BLOCK * LIPT;
 
 // ---------------------------------------------------------------------------
