@@ -32,6 +32,7 @@
 
 #include "common.h"
 #include "step.h"
+#include "connect.h"
 
 namespace {
 
@@ -52,6 +53,15 @@ struct BGeom {
   int NC;   // cell coordinates (+2) per axis: [0, NC)
   int sh;   // log2 of the bucket edge in cells
   int NBd;  // buckets per axis
+};
+
+// the window pass the grouping kernel runs over each bucket (keys == null:
+// none; the engine then launches k_connect_win)
+struct WinArgs {
+  int idx, nb;
+  uint64_t fmask;
+  uint64_t* keys;
+  int64_t cap;
 };
 
 // the new vertices' failover override, applied by the bucket count
@@ -312,7 +322,7 @@ k_bucket_scatter(const int32_t* __restrict__ members, int64_t S, int64_t V, int6
 // flight together (a bucket can hold 10^5 entries: a block walking them one
 // dependent load -> atomic -> store chain at a time is latency-bound).
 #ifndef TNP_GIPT
-#define TNP_GIPT 16
+#define TNP_GIPT 8
 #endif
 constexpr int GIPT = TNP_GIPT;
 
@@ -438,12 +448,13 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
                int32_t* __restrict__ lcell, int32_t* __restrict__ lent, int32_t* __restrict__ ln,
                int64_t* __restrict__ lpoff, int64_t* __restrict__ bnpc, int64_t* __restrict__ bnpairs,
                int64_t* __restrict__ bspairs, int64_t* __restrict__ pcoff, int64_t* __restrict__ pairoff,
-               int64_t* __restrict__ spoff, int fuse, int64_t* __restrict__ ctr) {
+               int64_t* __restrict__ spoff, int fuse, WinArgs wa, int64_t* __restrict__ ctr) {
   constexpr int LC = 1 << (3 * SH);
   __shared__ int cnt[LC];
   __shared__ int cur[LC];
   __shared__ int64_t lds[TNP_WAVES];
   __shared__ int last;
+  __shared__ WinLds W;
   const int b = blockIdx.x;
   const int64_t base = bbase[b];
   const int64_t n = bbase[b + 1] - base;
@@ -468,6 +479,17 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
   } else {
     group_bucket<SH>(G, b, base, n, ekv, pz, ents, lcell, lent, ln, lpoff, bnpc, bnpairs, bspairs, ctr, cnt,
                      cur, lds);
+    if (wa.keys) {
+      // the window pass over this bucket's records, right behind their
+      // stores (the workgroup's own stores: visible after the barrier)
+      __syncthreads();
+      WinAcc a;
+      const uint64_t below = (wa.idx >= 64) ? ~0ull : ((1ull << wa.idx) - 1ull);
+      window_pass(ents, base, base + n, tnp::wave(), TNP_WAVES, below, wa.nb, wa.fmask, wa.keys, wa.cap, ctr, W,
+                  a);
+      window_flush(wa.keys, wa.cap, ctr, W, a);
+      add_pair_stats(a.n_compat, a.n_reg, a.n_conn, lds, ctr);
+    }
   }
   if (!fuse || !tnp::last_block(&ctr[CTR_TK1], &last)) return;
   // every bucket's pair-cell / pair totals -> global offsets (k_pair_gather)
@@ -568,7 +590,8 @@ int launch_bucket_pairs(int n_marks, const int64_t* bbase, const uint64_t* ekv, 
                         int32_t* lent, int32_t* ln, int64_t* lpoff, int64_t* bnpc, int64_t* bnpairs,
                         int64_t* bspairs, int64_t* spoff, int64_t* pcoff, int64_t* pairoff,
                         int32_t* pcell, int32_t* pent, int32_t* pn, int64_t* ptoff, int32_t* bcell,
-                        int64_t bcap, int32_t* bcount, int32_t* bcur, int64_t* ctr, hipStream_t s) {
+                        int64_t bcap, int32_t* bcount, int32_t* bcur, const ConnectWin* win, int64_t* ctr,
+                        hipStream_t s) {
   int sh, NBd, NB;
   if (bucket_geometry(n_marks, &sh, &NBd, &NB)) {
     tnp_set_error("bucket geometry: %d marks", n_marks);
@@ -576,14 +599,16 @@ int launch_bucket_pairs(int n_marks, const int64_t* bbase, const uint64_t* ekv, 
   }
   const BGeom G{n_marks + 2, sh, NBd};
   const int fuse = NB <= FUSE_MAX_BLOCKS;
+  WinArgs wa{0, 0, 0ull, nullptr, 0};
+  if (win) wa = WinArgs{win->idx, win->nb, win->fmask, win->keys, win->cap};
   if (sh == 3)
     hipLaunchKernelGGL(k_bucket_group<3>, dim3(NB), dim3(TNP_BLOCK), 0, s, G, bbase, ekv,
                        reinterpret_cast<const ulonglong2*>(pz), ents, lcell, lent, ln, lpoff, bnpc, bnpairs,
-                       bspairs, pcoff, pairoff, spoff, fuse, ctr);
+                       bspairs, pcoff, pairoff, spoff, fuse, wa, ctr);
   else
     hipLaunchKernelGGL(k_bucket_group<4>, dim3(NB), dim3(TNP_BLOCK), 0, s, G, bbase, ekv,
                        reinterpret_cast<const ulonglong2*>(pz), ents, lcell, lent, ln, lpoff, bnpc, bnpairs,
-                       bspairs, pcoff, pairoff, spoff, fuse, ctr);
+                       bspairs, pcoff, pairoff, spoff, fuse, wa, ctr);
   if (!fuse)
     hipLaunchKernelGGL(k_scan_sets, dim3(1, 3), dim3(TNP_BLOCK), 0, s, ScanSet{bnpc, 1, pcoff, CTR_R},
                        ScanSet{bnpairs, 1, pairoff, CTR_TESTS}, ScanSet{bspairs, 1, spoff, CTR_SPAIRS}, NB,

@@ -1,0 +1,172 @@
+// Connecting-edge pair test and the window pass over cell-contiguous entry
+// records (subpoly.py:484-535), shared by step.hip (k_connect, k_connect_win)
+// and bucket.hip (the grouping kernel runs the window pass over its own
+// bucket).
+#pragma once
+#include "common.h"
+#include "step.h"
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// connecting-edge pair test (subpoly.py:484-535 in closed form).
+// Two members share an augmented region iff, per coordinate, their augmented
+// value sets intersect: grid dim d -> their cell spans overlap; plane
+// j < idx -> not (both non-zero with opposite signs).  The reference keeps
+// the pair iff they share >= 1 zero plane (grid zeros only on the SAME mark
+// plane).  Each pair is emitted once, in the canonical cell (per-dim max of
+// the two span lows).  In terms of the entries' cell flags (CellEnt::f) for
+// the cell under test, which both spans contain:
+//   canonical       <=> per axis, one of the two spans starts here
+//   same mark plane <=> both on a plane of the axis and both spans start here
+// and the shared regions double per same-plane axis and per common zero plane.
+// ---------------------------------------------------------------------------
+struct PairTest {
+  bool emit;
+  bool compat;
+  int64_t regions;  // shared regions (for the reference's candidate count P)
+};
+
+__device__ __forceinline__ PairTest pair_test(uint64_t below, uint32_t fu, uint64_t pu, uint64_t zu,
+                                              uint32_t fv, uint64_t pv, uint64_t zv) {
+  PairTest t{false, false, 0};
+  if (((fu | fv) & 7u) != 7u) return t;  // not the canonical cell
+  if (((pu ^ pv) & ~zu & ~zv & below) != 0) return t;
+  const uint32_t a = fu & fv;
+  const uint32_t sp = a & (a >> 3) & 7u;  // axes where both lie on the same mark plane
+  const uint64_t zz = zu & zv & below;
+  t.compat = true;
+  t.regions = (int64_t)1 << (__popc(sp) + __popcll(zz));
+  t.emit = sp != 0 || zz != 0;
+  return t;
+}
+
+// a block's (compatible pairs, shared regions, connecting edges) totals
+//   -> ctr[CTR_COMPAT], ctr[CTR_P], ctr[CTR_X] (three adds per block)
+__device__ __forceinline__ void add_pair_stats(int64_t a, int64_t r, int64_t x, int64_t* lds,
+                                               int64_t* __restrict__ ctr) {
+  int64_t ta, tr, tx;
+  tnp::block_scan_excl(a, lds, ta);
+  tnp::block_scan_excl(r, lds, tr);
+  tnp::block_scan_excl(x, lds, tx);
+  if (threadIdx.x == 0) {
+    if (ta) atomicAdd((unsigned long long*)&ctr[CTR_COMPAT], (unsigned long long)ta);
+    if (tr) atomicAdd((unsigned long long*)&ctr[CTR_P], (unsigned long long)tr);
+    if (tx) atomicAdd((unsigned long long*)&ctr[CTR_X], (unsigned long long)tx);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Window pass: the pairs of every cell of <= WCELL members.  The entries are
+// cell-contiguous; a wave stages the 64 records of window w (entries
+// [lo + 32 w, lo + 32 w + 64) of [lo, hi)) in LDS; each of its first 32
+// entries j is tested against the later entries of its cell, the (j,
+// partner) tests flattened over the 64 lanes (a wave scan of the per-entry
+// counts, a 6-step search in LDS per test): a pair (j < i) of such a cell is
+// tested exactly once, in window floor(j / 32) (i - j <= 32).  Each record
+// is read once from memory per window; emitted keys go through a per-wave LDS
+// buffer, one global append per WKEYS.
+// ---------------------------------------------------------------------------
+constexpr int WKEYS = 512;
+
+__device__ __forceinline__ void lds_fence() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+struct WinLds {
+  CellEnt st[TNP_WAVES][64];
+  int exc[TNP_WAVES][64];
+  uint64_t kb[TNP_WAVES][WKEYS];
+};
+struct WinAcc {
+  int kn = 0;  // wave-uniform fill of this wave's key buffer
+  int64_t n_compat = 0, n_reg = 0, n_conn = 0;
+};
+
+// this wave's buffered keys -> keys[] (counted in ctr[CTR_XK])
+__device__ __forceinline__ void window_flush(uint64_t* __restrict__ keys, int64_t cap,
+                                             int64_t* __restrict__ ctr, WinLds& W, WinAcc& a) {
+  if (a.kn == 0) return;
+  const int wv = tnp::wave(), L = tnp::lane();
+  int64_t base = 0;
+  if (L == 0) base = (int64_t)atomicAdd((unsigned long long*)&ctr[CTR_XK], (unsigned long long)a.kn);
+  base = __shfl(base, 0, 64);
+  for (int i = L; i < a.kn; i += 64)
+    if (base + i < cap) keys[base + i] = W.kb[wv][i];
+  lds_fence();
+  a.kn = 0;
+}
+
+// windows w = w0, w0 + dw, ... of the records [lo, hi); one wave each
+__device__ __forceinline__ void window_pass(const CellEnt* __restrict__ ent, int64_t lo, int64_t hi,
+                                            int64_t w0, int64_t dw, uint64_t below, int nb, uint64_t fmask,
+                                            uint64_t* __restrict__ keys, int64_t cap,
+                                            int64_t* __restrict__ ctr, WinLds& W, WinAcc& a) {
+  const int wv = tnp::wave(), L = tnp::lane();
+  const int64_t nwin = (hi - lo + 31) / 32;
+  for (int64_t w = w0; w < nwin; w += dw) {
+    const int64_t e = lo + w * 32 + L;
+    const bool valid = e < hi;
+    CellEnt r;
+    if (valid) {
+      r = ent[e];
+    } else {
+      r.p = r.z = 0;
+      r.v = 0;
+      r.f = 0;
+      r.tag = 0xFFFFFFFFu;  // no cell: matches nothing, never initiates
+      r.pad = 0;
+    }
+    W.st[wv][L] = r;
+    lds_fence();
+    // last lane of my cell inside the window (lane 63 always closes one)
+    const uint32_t nxt = __shfl_down(r.tag, 1, 64);
+    const uint64_t bm = __ballot(L == 63 || nxt != r.tag);
+    const int last = L + __builtin_ctzll(bm >> L);
+    const bool init = valid && L < 32 && !(r.tag & 0x80000000u);
+    const int rounds = init ? last - L : 0;
+    // flatten the window's (initiator, partner) tests over the lanes: test t
+    // belongs to the last initiator j with exc[j] <= t, partner j + 1 + t - exc[j]
+    const int incl = tnp::wave_scan_incl(rounds);
+    const int total = __shfl(incl, 63, 64);
+    W.exc[wv][L] = incl - rounds;
+    lds_fence();
+    for (int t0 = 0; t0 < total; t0 += 64) {
+      if (a.kn + 64 > WKEYS) window_flush(keys, cap, ctr, W, a);
+      const int t = t0 + L;
+      bool em = false;
+      uint64_t key = 0;
+      if (t < total) {
+        int lo2 = 0, hi2 = 62;
+#pragma unroll
+        for (int it = 0; it < 6; ++it) {
+          const int mid = (lo2 + hi2 + 1) >> 1;
+          if (W.exc[wv][mid] <= t) lo2 = mid;
+          else hi2 = mid - 1;
+        }
+        const int j = lo2, i = j + 1 + (t - W.exc[wv][j]);
+        const CellEnt u = W.st[wv][j];
+        const CellEnt q = W.st[wv][i];
+        const PairTest pt = pair_test(below, u.f, u.p, u.z, q.f, q.p, q.z);
+        if (pt.compat) {
+          a.n_compat++;
+          a.n_reg += pt.regions;
+          a.n_conn += pt.emit;
+          // the step's pruning drops it anyway (keep_edge): never appended
+          if (pt.emit && (fmask == 0 || (((u.p ^ q.p) | (u.z ^ q.z)) & fmask) != 0)) {
+            const uint32_t vu = (uint32_t)u.v, vv = (uint32_t)q.v;
+            const uint32_t l3 = vu < vv ? vu : vv, h3 = vu < vv ? vv : vu;
+            key = ((uint64_t)l3 << nb) | h3;
+            em = true;
+          }
+        }
+      }
+      const uint64_t eb = __ballot(em);
+      if (em) W.kb[wv][a.kn + tnp::mbcnt(eb)] = key;
+      a.kn += __popcll(eb);
+    }
+    lds_fence();
+  }
+}
+
+}  // namespace

@@ -962,18 +962,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
                                 P<int64_t>(e->bk[7]), P<uint64_t>(e->sents), e->bk_clean,
                                 prune ? P<uint8_t>(e->live) : nullptr, NV, e->pend_fused ? &nov : nullptr,
                                 ctr, s));
-    e->bk_clean = false;  // until the gather below has reset the counters
-    TIMED("bucket_group", 0.0,
-          launch_bucket_pairs(e->net.n_marks, P<int64_t>(e->bk[2]), P<uint64_t>(e->sents),
-                              P<uint64_t>(c.pz), P<CellEnt>(e->ents),
-                              P<int32_t>(e->bk[8]), P<int32_t>(e->bk[9]), P<int32_t>(e->bk[10]),
-                              P<int64_t>(e->bk[11]), P<int64_t>(e->bk[3]), P<int64_t>(e->bk[4]),
-                              P<int64_t>(e->bk[12]), P<int64_t>(e->bk[13]),
-                              P<int64_t>(e->bk[5]), P<int64_t>(e->bk[6]), P<int32_t>(e->pcell),
-                              P<int32_t>(e->pent), P<int32_t>(e->pcn), P<int64_t>(e->ptoff),
-                              P<int32_t>(e->bcell), bcap, P<int32_t>(e->bk[0]), P<int32_t>(e->bk[1]), ctr,
-                              s));
-    e->bk_clean = true;
+    e->bk_clean = false;  // until the grouping's pair-cell gather has reset the counters
   } else {
     // radix-sort path (grids finer than the bucket geometry, TNP_RADIX_CELLS=1)
     if (buf_ensure(e->spcnt, std::max<int64_t>(M, 1) * sizeof(int32_t), s)) return -1;
@@ -1018,7 +1007,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
       if (buf_ensure(e->rstart, (T1 + 1) * sizeof(int32_t), s)) return -1;
       if (T > 0) {
         TnpLB la, lr, lp;
-        if (lb_begin(e, split_tiles(T), s, &la, 0)) return -1;
+        if (lb_begin(e, run_tiles(T), s, &la, 0)) return -1;
         TIMED("run_starts", 8.0 * T,
               launch_run_starts(skey, T, P<int32_t>(e->rstart), ctr, la, s));
         const int64_t pt = pair_run_tiles(T);
@@ -1042,19 +1031,36 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   const uint64_t cfmask = prune ? prune_mask(idx, K - 1) : 0ull;
   int64_t cap = std::max<int64_t>(e->ckeys_a.bytes / sizeof(uint64_t), 4 * M + 1024);
   int64_t X = 0, TT = 0;
-  bool chunks_ok = buckets;  // the bucket path's gather filled the chunk table
+  bool chunks_ok = false;  // (radix path) the chunk table matches the pair cells
   for (int attempt = 0; attempt < 3; ++attempt) {
-    if (!chunks_ok) {
-      if (buf_ensure(e->bcell, bcap * sizeof(int32_t), s)) return -1;
-      if (attempt > 0) TNP_CHECK(hipMemsetAsync(ctr + CTR_BOVF, 0, sizeof(int64_t), s));
-      if (launch_chunk_cells(P<int64_t>(e->ptoff), P<int32_t>(e->pcn), RC,
-                             P<int32_t>(e->bcell), bcap, ctr, s)) return -1;
-    }
     if (buf_ensure(e->ckeys_a, std::max<int64_t>(cap, 1) * sizeof(uint64_t), s)) return -1;
     if (attempt > 0) {  // the split zeroed the whole counter block
       TNP_CHECK(hipMemsetAsync(ctr + CTR_X, 0, sizeof(int64_t), s));
       TNP_CHECK(hipMemsetAsync(ctr + CTR_XK, 0, sizeof(int64_t), s));
       TNP_CHECK(hipMemsetAsync(ctr + CTR_P, 0, 2 * sizeof(int64_t), s));  // CTR_P, CTR_COMPAT
+      TNP_CHECK(hipMemsetAsync(ctr + CTR_BOVF, 0, sizeof(int64_t), s));
+      TNP_CHECK(hipMemsetAsync(ctr + CTR_TK1, 0, sizeof(int64_t), s));
+    }
+    if (buckets) {
+      // in-bucket grouping + the window pass over each bucket (cells of <=
+      // WCELL members) + pair-cell lists and k_connect's chunk table (bcap)
+      if (buf_ensure(e->bcell, bcap * sizeof(int32_t), s)) return -1;
+      const ConnectWin cw{idx, nb, cfmask, P<uint64_t>(e->ckeys_a), cap};
+      TIMED("bucket_group", 0.0,
+            launch_bucket_pairs(e->net.n_marks, P<int64_t>(e->bk[2]), P<uint64_t>(e->sents),
+                                P<uint64_t>(c.pz), P<CellEnt>(e->ents),
+                                P<int32_t>(e->bk[8]), P<int32_t>(e->bk[9]), P<int32_t>(e->bk[10]),
+                                P<int64_t>(e->bk[11]), P<int64_t>(e->bk[3]), P<int64_t>(e->bk[4]),
+                                P<int64_t>(e->bk[12]), P<int64_t>(e->bk[13]),
+                                P<int64_t>(e->bk[5]), P<int64_t>(e->bk[6]), P<int32_t>(e->pcell),
+                                P<int32_t>(e->pent), P<int32_t>(e->pcn), P<int64_t>(e->ptoff),
+                                P<int32_t>(e->bcell), bcap, P<int32_t>(e->bk[0]), P<int32_t>(e->bk[1]),
+                                &cw, ctr, s));
+      e->bk_clean = true;
+    } else if (!chunks_ok) {
+      if (buf_ensure(e->bcell, bcap * sizeof(int32_t), s)) return -1;
+      if (launch_chunk_cells(P<int64_t>(e->ptoff), P<int32_t>(e->pcn), RC,
+                             P<int32_t>(e->bcell), bcap, ctr, s)) return -1;
     }
     // cells above WCELL members: the flattened pair space (every cell on the
     // radix path); the others: the window pass
@@ -1063,10 +1069,6 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
                          P<int32_t>(e->pent), NC, e->max_pair_tests, P<int32_t>(e->bcell),
                          P<CellEnt>(e->ents), idx, nb, cfmask, P<uint64_t>(e->ckeys_a), cap, ctr,
                          s));
-    if (buckets) {
-      TIMED("connect_win", 0.0,
-            launch_connect_win(P<CellEnt>(e->ents), idx, nb, cfmask, P<uint64_t>(e->ckeys_a), cap, ctr, s));
-    }
     if (read_ctr(e, s)) return -1;
     if (buckets) {
       if (e->h_ctr[CTR_K0]) {
@@ -1081,8 +1083,9 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
       // 16 B of member keys and writes the 32 B record; the window pass reads
       // every record (once, algorithmically) and writes the kept keys
       ktimer_set_bytes(e, "bucket_entries", 16.0 * M + 8.0 * T);
-      ktimer_set_bytes(e, "bucket_group", 56.0 * T);
-      ktimer_set_bytes(e, "connect_win", 32.0 * T + 8.0 * e->h_ctr[CTR_XK]);
+      // the window pass re-reads the records the same workgroup just wrote
+      // (cache traffic): its compulsory bytes are the kept keys
+      ktimer_set_bytes(e, "bucket_group", 56.0 * T + 8.0 * e->h_ctr[CTR_XK]);
     }
     TT = e->h_ctr[CTR_TESTS];
     X = e->h_ctr[CTR_XK];

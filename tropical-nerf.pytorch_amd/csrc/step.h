@@ -42,6 +42,7 @@ enum {
 int64_t step_tiles(int64_t n);
 int64_t lb_tiles(int64_t n);     // tiles of the single-pass prune
 int64_t split_tiles(int64_t n);  // tiles of the single-pass split and hit passes
+int64_t run_tiles(int64_t n);    // tiles of the radix path's run-start pass
 // single-pass split over split_tiles(E) look-back tiles (E > 0) from the
 // edges' split masks (bit idx): S -> ctr[CTR_S]; sa/sb (and eidx if given)
 // need capacity E; without eidx the split edges are rewired in place and
@@ -85,7 +86,7 @@ int launch_span_emit(const int32_t* members, int64_t S, int64_t M, const uint64_
 // flattened pair space; R -> ctr[CTR_R], pairs -> ctr[CTR_TESTS], a cell
 // above 65535 members -> CTR_BIG.  Arrays sized >= T / 2 + 1.
 // Two passes: run starts (rstart[r] = first entry of the r-th occupied
-// cell, rstart[runs] = T, runs -> ctr[CTR_RUNS]; split_tiles(T) look-back
+// cell, rstart[runs] = T, runs -> ctr[CTR_RUNS]; run_tiles(T) look-back
 // tiles, rstart sized >= T + 1), then the runs with >= 2 entries
 // (pair_run_tiles(T) look-back tiles for each of lb_rank / lb_pairs; the
 // run count is read on the device).
@@ -201,12 +202,21 @@ int launch_bucket_entries(const int32_t* members, int64_t S, int64_t V, int64_t 
 // table bcell, bcap chunks, overflow -> CTR_BOVF); the pairs of the others
 // -> ctr[CTR_SPAIRS] (bspairs/spoff: NB / NB + 1 int64 scratch).  Leaves
 // bcount/bcur zeroed for the next step.
+// win != null: the grouping kernel also runs the window pass (launch_connect_win's
+// work) over each bucket's records; uses ctr[CTR_TK1] on small grids
+struct ConnectWin {
+  int idx, nb;
+  uint64_t fmask;
+  uint64_t* keys;
+  int64_t cap;
+};
 int launch_bucket_pairs(int n_marks, const int64_t* bbase, const uint64_t* ekv, const uint64_t* pz,
                         CellEnt* ents, int32_t* lcell,
                         int32_t* lent, int32_t* ln, int64_t* lpoff, int64_t* bnpc, int64_t* bnpairs,
                         int64_t* bspairs, int64_t* spoff, int64_t* pcoff, int64_t* pairoff,
                         int32_t* pcell, int32_t* pent, int32_t* pn, int64_t* ptoff, int32_t* bcell,
-                        int64_t bcap, int32_t* bcount, int32_t* bcur, int64_t* ctr, hipStream_t s);
+                        int64_t bcap, int32_t* bcount, int32_t* bcur, const ConnectWin* win, int64_t* ctr,
+                        hipStream_t s);
 // pair indices per k_connect chunk (its bcell table granularity)
 int64_t connect_chunk_pairs();
 // window pass over the cell-contiguous entries (count ctr[CTR_T]): every

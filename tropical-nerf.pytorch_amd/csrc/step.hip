@@ -21,6 +21,7 @@
 #include "common.h"
 #include "kernels.h"
 #include "step.h"
+#include "connect.h"
 
 #include <algorithm>
 
@@ -37,14 +38,16 @@ constexpr int TILE = TNP_BLOCK * IPT;   // tile of a compaction pass
 // single-pass (look-back) compactions: items per thread of the split / hit
 // pass (SIPT) and of the prune pass (LIPT); every item's loads are issued
 // before any is used
-#ifndef TNP_SIPT
-#define TNP_SIPT 32
-#endif
+// split / hit passes: 32 items per thread on large inputs (more loads in
+// flight), 8 on small ones (more tiles to spread over the CUs)
+constexpr int SIPT_BIG = 32, SIPT_SMALL = 8;
+constexpr int64_t SIPT_BIG_FROM = 1 << 20;
+__host__ __device__ constexpr int split_ipt(int64_t n) { return n >= SIPT_BIG_FROM ? SIPT_BIG : SIPT_SMALL; }
+constexpr int SIPT = 16;  // the radix path's run-start pass
+constexpr int STILE = TNP_BLOCK * SIPT;
 #ifndef TNP_LIPT
 #define TNP_LIPT 8
 #endif
-constexpr int SIPT = TNP_SIPT;
-constexpr int STILE = TNP_BLOCK * SIPT;
 constexpr int LIPT = TNP_LIPT;
 constexpr int LTILE = TNP_BLOCK * LIPT;
 
@@ -63,23 +66,24 @@ __device__ __forceinline__ bool split_test(const float* __restrict__ col, const 
 // unconditionally (clamped index) in two batches -- the edge pairs, then the
 // plane-column gathers -- so a thread has SIPT * 2 loads in flight instead
 // of a bounds branch serialising every item.
+template <int SI>
 __global__ void __launch_bounds__(TNP_BLOCK)
 k_split_lb(int32_t* __restrict__ edges, int64_t E, int64_t ntiles, const uint64_t* __restrict__ sm,
            uint8_t* __restrict__ dm, int idx, int64_t V, int32_t* __restrict__ sa,
            int32_t* __restrict__ sb, int64_t* __restrict__ ctr, int32_t* __restrict__ eidx, TnpLB lb) {
-  __shared__ int cnt[SIPT][TNP_WAVES];
+  __shared__ int cnt[SI][TNP_WAVES];
   __shared__ int64_t slot;
   const int64_t tile = tnp::lb_tile(lb, &slot);
-  const int64_t base = tile * STILE;
-  uint64_t bal[SIPT];
-  uint64_t mk[SIPT];
+  const int64_t base = tile * (TNP_BLOCK * SI);
+  uint64_t bal[SI];
+  uint64_t mk[SI];
 #pragma unroll
-  for (int k = 0; k < SIPT; ++k) {  // coalesced, unconditional (clamped) loads
+  for (int k = 0; k < SI; ++k) {  // coalesced, unconditional (clamped) loads
     const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
     mk[k] = sm[i < E ? i : E - 1];
   }
 #pragma unroll
-  for (int k = 0; k < SIPT; ++k) {
+  for (int k = 0; k < SI; ++k) {
     const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
     bal[k] = __ballot((i < E) && ((mk[k] >> idx) & 1));
     if (tnp::lane() == 0) cnt[k][tnp::wave()] = __popcll(bal[k]);
@@ -87,13 +91,13 @@ k_split_lb(int32_t* __restrict__ edges, int64_t E, int64_t ntiles, const uint64_
   __syncthreads();
   int64_t agg = 0;
 #pragma unroll
-  for (int k = 0; k < SIPT; ++k)
+  for (int k = 0; k < SI; ++k)
 #pragma unroll
     for (int w = 0; w < TNP_WAVES; ++w) agg += cnt[k][w];
   const int64_t prefix = tnp::lb_prefix(lb, tile, agg, &slot);
   int64_t run = prefix;
 #pragma unroll
-  for (int k = 0; k < SIPT; ++k) {
+  for (int k = 0; k < SI; ++k) {
     int64_t off = run;
     int tot = 0;
 #pragma unroll
@@ -192,28 +196,29 @@ __global__ void k_finalize_new(int64_t S, int K, int override_, const uint64_t* 
 // single pass (decoupled look-back): live vertices on the plane, ascending,
 // appended after the S new members; the last tile writes the count to
 // ctr[CTR_H].  alive: the live-slot flags of the lazily compacted vertex set
+template <int SI>
 __global__ void __launch_bounds__(TNP_BLOCK)
 k_hit_lb(const float* __restrict__ col, const uint8_t* __restrict__ alive, int64_t V,
          int64_t ntiles, float eps, int32_t* __restrict__ members, int64_t S_arg,
          int64_t* __restrict__ ctr, TnpLB lb) {
-  __shared__ int cnt[SIPT][TNP_WAVES];
+  __shared__ int cnt[SI][TNP_WAVES];
   __shared__ int64_t slot;
   // S_arg < 0: launched right behind the split, whose count is on the device
   const int64_t S = S_arg < 0 ? ctr[CTR_S] : S_arg;
   const int64_t tile = tnp::lb_tile(lb, &slot);
-  const int64_t base = tile * STILE;
-  float c[SIPT];
-  uint8_t al[SIPT];
-  uint64_t bal[SIPT];
+  const int64_t base = tile * (TNP_BLOCK * SI);
+  float c[SI];
+  uint8_t al[SI];
+  uint64_t bal[SI];
 #pragma unroll
-  for (int k = 0; k < SIPT; ++k) {  // unconditional (clamped) loads, all in flight
+  for (int k = 0; k < SI; ++k) {  // unconditional (clamped) loads, all in flight
     const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
     const int64_t ic = i < V ? i : V - 1;
     c[k] = col[ic];
     al[k] = alive[ic];
   }
 #pragma unroll
-  for (int k = 0; k < SIPT; ++k) {
+  for (int k = 0; k < SI; ++k) {
     const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
     bal[k] = __ballot((i < V) && (fabsf(c[k]) < eps) && al[k]);
     if (tnp::lane() == 0) cnt[k][tnp::wave()] = __popcll(bal[k]);
@@ -221,13 +226,13 @@ k_hit_lb(const float* __restrict__ col, const uint8_t* __restrict__ alive, int64
   __syncthreads();
   int64_t agg = 0;
 #pragma unroll
-  for (int k = 0; k < SIPT; ++k)
+  for (int k = 0; k < SI; ++k)
 #pragma unroll
     for (int w = 0; w < TNP_WAVES; ++w) agg += cnt[k][w];
   const int64_t prefix = tnp::lb_prefix(lb, tile, agg, &slot);
   int64_t run = prefix;
 #pragma unroll
-  for (int k = 0; k < SIPT; ++k) {
+  for (int k = 0; k < SI; ++k) {
     int64_t off = run;
     int tot = 0;
 #pragma unroll
@@ -472,39 +477,6 @@ __global__ void k_entry_keys(const int32_t* __restrict__ ent_v, const uint32_t* 
   ent[i] = r;
 }
 
-// ---------------------------------------------------------------------------
-// connecting-edge pair test (subpoly.py:484-535 in closed form).
-// Two members share an augmented region iff, per coordinate, their augmented
-// value sets intersect: grid dim d -> their cell spans overlap; plane
-// j < idx -> not (both non-zero with opposite signs).  The reference keeps
-// the pair iff they share >= 1 zero plane (grid zeros only on the SAME mark
-// plane).  Each pair is emitted once, in the canonical cell (per-dim max of
-// the two span lows).  In terms of the entries' cell flags (CellEnt::f) for
-// the cell under test, which both spans contain:
-//   canonical       <=> per axis, one of the two spans starts here
-//   same mark plane <=> both on a plane of the axis and both spans start here
-// and the shared regions double per same-plane axis and per common zero plane.
-// ---------------------------------------------------------------------------
-struct PairTest {
-  bool emit;
-  bool compat;
-  int64_t regions;  // shared regions (for the reference's candidate count P)
-};
-
-__device__ __forceinline__ PairTest pair_test(uint64_t below, uint32_t fu, uint64_t pu, uint64_t zu,
-                                              uint32_t fv, uint64_t pv, uint64_t zv) {
-  PairTest t{false, false, 0};
-  if (((fu | fv) & 7u) != 7u) return t;  // not the canonical cell
-  if (((pu ^ pv) & ~zu & ~zv & below) != 0) return t;
-  const uint32_t a = fu & fv;
-  const uint32_t sp = a & (a >> 3) & 7u;  // axes where both lie on the same mark plane
-  const uint64_t zz = zu & zv & below;
-  t.compat = true;
-  t.regions = (int64_t)1 << (__popc(sp) + __popcll(zz));
-  t.emit = sp != 0 || zz != 0;
-  return t;
-}
-
 // first index in [lo, hi) with a[i] > x (hi if none)
 __device__ __forceinline__ int64_t upper_bound_i64(const int64_t* __restrict__ a, int64_t lo,
                                                    int64_t hi, int64_t x) {
@@ -532,21 +504,6 @@ __device__ __forceinline__ void cell_coords(int64_t cell, int NC, int cc[3]) {
   cc[2] = (int)(cell % NC) - 2;
   cc[1] = (int)((cell / NC) % NC) - 2;
   cc[0] = (int)(cell / ((int64_t)NC * NC)) - 2;
-}
-
-// a block's (compatible pairs, shared regions, connecting edges) totals
-//   -> ctr[CTR_COMPAT], ctr[CTR_P], ctr[CTR_X] (three adds per block)
-__device__ __forceinline__ void add_pair_stats(int64_t a, int64_t r, int64_t x, int64_t* lds,
-                                               int64_t* __restrict__ ctr) {
-  int64_t ta, tr, tx;
-  tnp::block_scan_excl(a, lds, ta);
-  tnp::block_scan_excl(r, lds, tr);
-  tnp::block_scan_excl(x, lds, tx);
-  if (threadIdx.x == 0) {
-    if (ta) atomicAdd((unsigned long long*)&ctr[CTR_COMPAT], (unsigned long long)ta);
-    if (tr) atomicAdd((unsigned long long*)&ctr[CTR_P], (unsigned long long)tr);
-    if (tx) atomicAdd((unsigned long long*)&ctr[CTR_X], (unsigned long long)tx);
-  }
 }
 
 // The flattened pair-index space of all cells (cell-major, then (i, j<i)
@@ -724,110 +681,20 @@ k_connect(const int64_t* __restrict__ ptoff, const int32_t* __restrict__ pcell,
   add_pair_stats(n_compat, n_reg, n_conn, lds, ctr);
 }
 
-// ---------------------------------------------------------------------------
-// Window pass: the pairs of every cell of <= WCELL members.  The entries are
-// cell-contiguous; a wave stages the 64 records of window w (entries
-// [32 w, 32 w + 64)) in LDS; each of its first 32 entries j is tested
-// against the later entries of its cell, the (j, partner) tests flattened
-// over the 64 lanes (a wave scan of the per-entry counts, a 6-step search
-// in LDS per test): a pair (j < i) of such a cell is tested exactly once, in
-// window floor(j / 32) (i - j <= 32).  Each record is read once from memory
-// per window; emitted keys go through a per-wave LDS buffer, one global
-// append per 512.
-// ---------------------------------------------------------------------------
-constexpr int WKEYS = 512;
-
-__device__ __forceinline__ void lds_fence() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-}
-
+// the window pass over every cell-contiguous entry (connect.h window_pass);
+// the bucket path runs it inside its grouping kernel instead
 __global__ void __launch_bounds__(TNP_BLOCK)
 k_connect_win(const CellEnt* __restrict__ ent, int idx, int nb, uint64_t fmask,
               uint64_t* __restrict__ keys, int64_t cap, int64_t* __restrict__ ctr) {
-  __shared__ CellEnt st[TNP_WAVES][64];
-  __shared__ int exc[TNP_WAVES][64];
-  __shared__ uint64_t kb[TNP_WAVES][WKEYS];
+  __shared__ WinLds W;
   __shared__ int64_t lds[TNP_WAVES];
   const int64_t T = ctr[CTR_T];
-  const int64_t nwin = (T + 31) / 32;
+  WinAcc a;
   const uint64_t below = (idx >= 64) ? ~0ull : ((1ull << idx) - 1ull);
-  const int wv = tnp::wave(), L = tnp::lane();
-  int kn = 0;  // wave-uniform fill of this wave's key buffer
-  int64_t n_compat = 0, n_reg = 0, n_conn = 0;
-  auto flush = [&]() {
-    int64_t base = 0;
-    if (L == 0) base = (int64_t)atomicAdd((unsigned long long*)&ctr[CTR_XK], (unsigned long long)kn);
-    base = __shfl(base, 0, 64);
-    for (int i = L; i < kn; i += 64)
-      if (base + i < cap) keys[base + i] = kb[wv][i];
-    lds_fence();
-    kn = 0;
-  };
-  for (int64_t w = (int64_t)blockIdx.x * TNP_WAVES + wv; w < nwin; w += (int64_t)gridDim.x * TNP_WAVES) {
-    const int64_t e = w * 32 + L;
-    const bool valid = e < T;
-    CellEnt r;
-    if (valid) {
-      r = ent[e];
-    } else {
-      r.p = r.z = 0;
-      r.v = 0;
-      r.f = 0;
-      r.tag = 0xFFFFFFFFu;  // no cell: matches nothing, never initiates
-      r.pad = 0;
-    }
-    st[wv][L] = r;
-    lds_fence();
-    // last lane of my cell inside the window (lane 63 always closes one)
-    const uint32_t nxt = __shfl_down(r.tag, 1, 64);
-    const uint64_t bm = __ballot(L == 63 || nxt != r.tag);
-    const int last = L + __builtin_ctzll(bm >> L);
-    const bool init = valid && L < 32 && !(r.tag & 0x80000000u);
-    const int rounds = init ? last - L : 0;
-    // flatten the window's (initiator, partner) tests over the lanes: test t
-    // belongs to the last initiator j with exc[j] <= t, partner j + 1 + t - exc[j]
-    const int incl = tnp::wave_scan_incl(rounds);
-    const int total = __shfl(incl, 63, 64);
-    exc[wv][L] = incl - rounds;
-    lds_fence();
-    for (int t0 = 0; t0 < total; t0 += 64) {
-      if (kn + 64 > WKEYS) flush();
-      const int t = t0 + L;
-      bool em = false;
-      uint64_t key = 0;
-      if (t < total) {
-        int lo = 0, hi = 62;
-#pragma unroll
-        for (int it = 0; it < 6; ++it) {
-          const int mid = (lo + hi + 1) >> 1;
-          if (exc[wv][mid] <= t) lo = mid;
-          else hi = mid - 1;
-        }
-        const int j = lo, i = j + 1 + (t - exc[wv][j]);
-        const CellEnt u = st[wv][j];
-        const CellEnt q = st[wv][i];
-        const PairTest pt = pair_test(below, u.f, u.p, u.z, q.f, q.p, q.z);
-        if (pt.compat) {
-          n_compat++;
-          n_reg += pt.regions;
-          n_conn += pt.emit;
-          // the step's pruning drops it anyway (keep_edge): never appended
-          if (pt.emit && (fmask == 0 || (((u.p ^ q.p) | (u.z ^ q.z)) & fmask) != 0)) {
-            const uint32_t vu = (uint32_t)u.v, vv = (uint32_t)q.v;
-            const uint32_t lo2 = vu < vv ? vu : vv, hi2 = vu < vv ? vv : vu;
-            key = ((uint64_t)lo2 << nb) | hi2;
-            em = true;
-          }
-        }
-      }
-      const uint64_t eb = __ballot(em);
-      if (em) kb[wv][kn + tnp::mbcnt(eb)] = key;
-      kn += __popcll(eb);
-    }
-    lds_fence();
-  }
-  if (kn) flush();
-  add_pair_stats(n_compat, n_reg, n_conn, lds, ctr);
+  window_pass(ent, 0, T, (int64_t)blockIdx.x * TNP_WAVES + tnp::wave(), (int64_t)gridDim.x * TNP_WAVES,
+              below, nb, fmask, keys, cap, ctr, W, a);
+  window_flush(keys, cap, ctr, W, a);
+  add_pair_stats(a.n_compat, a.n_reg, a.n_conn, lds, ctr);
 }
 
 // ---------------------------------------------------------------------------
@@ -1147,14 +1014,22 @@ __global__ void k_publish(const int64_t* __restrict__ ctr, volatile int64_t* hos
 // ----------------------------------------------------------------------------
 int64_t step_tiles(int64_t n) { return (n + TILE - 1) / TILE; }
 int64_t lb_tiles(int64_t n) { return (n + LTILE - 1) / LTILE; }
-int64_t split_tiles(int64_t n) { return (n + STILE - 1) / STILE; }
+int64_t split_tiles(int64_t n) {
+  const int64_t t = (int64_t)TNP_BLOCK * split_ipt(n);
+  return (n + t - 1) / t;
+}
+int64_t run_tiles(int64_t n) { return (n + STILE - 1) / STILE; }
 
 int launch_split_lb(int32_t* edges, int64_t E, const uint64_t* sm, uint8_t* dm, int idx, int64_t V,
                     int32_t* sa, int32_t* sb, int64_t* ctr, int32_t* eidx, const TnpLB& lb,
                     hipStream_t s) {
   const int64_t tiles = split_tiles(E);
-  hipLaunchKernelGGL(k_split_lb, dim3((unsigned)tiles), dim3(TNP_BLOCK), 0, s, edges, E, tiles, sm, dm,
-                     idx, V, sa, sb, ctr, eidx, lb);
+  if (split_ipt(E) == SIPT_BIG)
+    hipLaunchKernelGGL(k_split_lb<SIPT_BIG>, dim3((unsigned)tiles), dim3(TNP_BLOCK), 0, s, edges, E, tiles, sm,
+                       dm, idx, V, sa, sb, ctr, eidx, lb);
+  else
+    hipLaunchKernelGGL(k_split_lb<SIPT_SMALL>, dim3((unsigned)tiles), dim3(TNP_BLOCK), 0, s, edges, E, tiles,
+                       sm, dm, idx, V, sa, sb, ctr, eidx, lb);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
@@ -1188,8 +1063,12 @@ int launch_hits(const float* col, const uint8_t* alive, int64_t V, float eps, in
                 int64_t S, int64_t* ctr, const TnpLB& lb, hipStream_t s) {
   if (V > 0) {
     const int64_t tiles = split_tiles(V);
-    hipLaunchKernelGGL(k_hit_lb, dim3((unsigned)tiles), dim3(TNP_BLOCK), 0, s, col, alive, V, tiles,
-                       eps, members, S, ctr, lb);
+    if (split_ipt(V) == SIPT_BIG)
+      hipLaunchKernelGGL(k_hit_lb<SIPT_BIG>, dim3((unsigned)tiles), dim3(TNP_BLOCK), 0, s, col, alive, V,
+                         tiles, eps, members, S, ctr, lb);
+    else
+      hipLaunchKernelGGL(k_hit_lb<SIPT_SMALL>, dim3((unsigned)tiles), dim3(TNP_BLOCK), 0, s, col, alive, V,
+                         tiles, eps, members, S, ctr, lb);
   } else {
     TNP_CHECK(hipMemsetAsync(ctr + CTR_H, 0, sizeof(int64_t), s));
   }
@@ -1227,7 +1106,7 @@ int64_t pair_run_tiles(int64_t T) { return (T + PTILE - 1) / PTILE; }
 int launch_run_starts(const uint32_t* key, int64_t T, int32_t* rstart, int64_t* ctr, const TnpLB& lb,
                       hipStream_t s) {
   if (T <= 0) return 0;
-  const int64_t tiles = split_tiles(T);
+  const int64_t tiles = run_tiles(T);
   hipLaunchKernelGGL(k_run_starts_lb, dim3((unsigned)tiles), dim3(TNP_BLOCK), 0, s, key, T, tiles,
                      rstart, ctr, lb);
   TNP_CHECK(hipGetLastError());
