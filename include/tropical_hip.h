@@ -120,6 +120,13 @@ int tnp_engine_load(tnp_engine* eng, const float* d_xyz, int64_t V,
  * falls back to get_hypercube(3, size) (subpoly.py:51-52, 731-750). */
 int tnp_engine_skeleton(tnp_engine* eng, int unit, float size, void* stream,
                         int64_t* V, int64_t* E);
+/* The same with the reference's pruning mode chosen (TropicalHashGrid.skeleton,
+ * tropical/tropical.py:184-205: PRUNING_MODE is "distance" there; "sign" is
+ * its dormant branch -> _skeleton, tropical.py:80-109, keeping an edge iff
+ * the endpoints' eps-sign vectors over all planes differ). */
+enum { TNP_SKELETON_DISTANCE = 0, TNP_SKELETON_SIGN = 1 };
+int tnp_engine_skeleton_mode(tnp_engine* eng, int unit, float size, int mode, void* stream,
+                             int64_t* n_vertices, int64_t* n_edges);
 
 /* Load the full lattice over the marks restricted to the x-slab of mark
  * indices [x0, x1] (x0=0, x1=n_marks-1: the whole N^3 lattice) in the

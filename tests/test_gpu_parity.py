@@ -140,6 +140,31 @@ def test_skeleton_bitwise(cuda, name):
         assert e.shape[0] - torch.unique(e, dim=0).shape[0] == int(d["skel_dups"])
 
 
+@pytest.mark.parametrize("name,unit", [("small_sphere", 128), ("small_sphere", 16), ("small_rand", 16)])
+def test_skeleton_sign_mode_matches_oracle(cuda, name, unit):
+    """The reference's dormant PRUNING_MODE="sign" (tropical.py:198-202 ->
+    _skeleton, :80-100), against the oracle's restatement (the reference
+    never runs it, so no golden exists): vertices and edges bitwise, tile
+    overlaps (unit 16) included."""
+    import oracle.subdivide as od
+    from tropical._engine import engine_for
+    d = load(name)
+    net = product_net(d, cuda)
+    eng = engine_for(net)
+    eng.skeleton(unit, 1.2, mode="sign")
+    v, e, _ = eng.export()
+    rv, re = od.skeleton(oracle_net(d), unit, mode="sign")
+    assert e.shape[0] > 0
+    np.testing.assert_array_equal(v.cpu().numpy(), rv.numpy())
+    np.testing.assert_array_equal(e.cpu().numpy(), re.numpy())
+    # distance mode is unaffected by the mode switch
+    eng.skeleton(unit, 1.2, mode="distance")
+    v2, e2, _ = eng.export()
+    dv, de = od.skeleton(oracle_net(d), unit)
+    np.testing.assert_array_equal(v2.cpu().numpy(), dv.numpy())
+    np.testing.assert_array_equal(e2.cpu().numpy(), de.numpy())
+
+
 @pytest.mark.parametrize("name", cases("subpoly"))
 def test_subpoly_steps_bitwise(cuda, name):
     from tropical._engine import engine_for

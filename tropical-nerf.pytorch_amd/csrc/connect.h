@@ -62,20 +62,24 @@ __device__ __forceinline__ void add_pair_stats(int64_t a, int64_t r, int64_t x, 
 // [lo + 32 w, lo + 32 w + 64) of [lo, hi)) in LDS; each of its first 32
 // entries j is tested against the later entries of its cell, the (j,
 // partner) tests flattened over the 64 lanes (a wave scan of the per-entry
-// counts, a 6-step search in LDS per test): a pair (j < i) of such a cell is
+// counts; a test finds its pair in a per-window LDS table the initiators
+// fill, or by a 6-step search past WOWN tests): a pair (j < i) of such a cell is
 // tested exactly once, in window floor(j / 32) (i - j <= 32).  Each record
 // is read once from memory per window; emitted keys go through a per-wave LDS
 // buffer, one global append per WKEYS.
 // ---------------------------------------------------------------------------
-constexpr int WKEYS = 512;
+constexpr int WKEYS = 384;
 
 __device__ __forceinline__ void lds_fence() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
+constexpr int WOWN = 512;  // tests of one window resolved by table (more: binary search)
+
 struct WinLds {
   CellEnt st[TNP_WAVES][64];
   int exc[TNP_WAVES][64];
+  uint16_t own[TNP_WAVES][WOWN];  // test t -> initiator | partner << 8
   uint64_t kb[TNP_WAVES][WKEYS];
 };
 struct WinAcc {
@@ -129,7 +133,10 @@ __device__ __forceinline__ void window_pass(const CellEnt* __restrict__ ent, int
     // belongs to the last initiator j with exc[j] <= t, partner j + 1 + t - exc[j]
     const int incl = tnp::wave_scan_incl(rounds);
     const int total = __shfl(incl, 63, 64);
+    const bool table = total <= WOWN;
     W.exc[wv][L] = incl - rounds;
+    if (table)  // each initiator lists its own tests (a few, mostly)
+      for (int r = 0, t = incl - rounds; r < rounds; ++r, ++t) W.own[wv][t] = (uint16_t)(L | ((L + 1 + r) << 8));
     lds_fence();
     for (int t0 = 0; t0 < total; t0 += 64) {
       if (a.kn + 64 > WKEYS) window_flush(keys, cap, ctr, W, a);
@@ -137,14 +144,22 @@ __device__ __forceinline__ void window_pass(const CellEnt* __restrict__ ent, int
       bool em = false;
       uint64_t key = 0;
       if (t < total) {
-        int lo2 = 0, hi2 = 62;
+        int j, i;
+        if (table) {
+          const uint32_t o = W.own[wv][t];
+          j = (int)(o & 0xFFu);
+          i = (int)(o >> 8);
+        } else {
+          int lo2 = 0, hi2 = 62;
 #pragma unroll
-        for (int it = 0; it < 6; ++it) {
-          const int mid = (lo2 + hi2 + 1) >> 1;
-          if (W.exc[wv][mid] <= t) lo2 = mid;
-          else hi2 = mid - 1;
+          for (int it = 0; it < 6; ++it) {
+            const int mid = (lo2 + hi2 + 1) >> 1;
+            if (W.exc[wv][mid] <= t) lo2 = mid;
+            else hi2 = mid - 1;
+          }
+          j = lo2;
+          i = j + 1 + (t - W.exc[wv][j]);
         }
-        const int j = lo2, i = j + 1 + (t - W.exc[wv][j]);
         const CellEnt u = W.st[wv][j];
         const CellEnt q = W.st[wv][i];
         const PairTest pt = pair_test(below, u.f, u.p, u.z, q.f, q.p, q.z);

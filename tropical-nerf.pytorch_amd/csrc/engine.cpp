@@ -1390,6 +1390,11 @@ static int load_hypercube(tnp_engine* e, float size, hipStream_t s) {
 
 extern "C" int tnp_engine_skeleton(tnp_engine* e, int unit, float size, void* stream, int64_t* V_out,
                                    int64_t* E_out) {
+  return tnp_engine_skeleton_mode(e, unit, size, TNP_SKELETON_DISTANCE, stream, V_out, E_out);
+}
+
+extern "C" int tnp_engine_skeleton_mode(tnp_engine* e, int unit, float size, int mode, void* stream,
+                                        int64_t* V_out, int64_t* E_out) {
   hipStream_t s = (hipStream_t)stream;
   if (!e->has_net) { tnp_set_error("engine has no net"); return -1; }
   if (unit < 2) { tnp_set_error("unit must be >= 2"); return -1; }
@@ -1406,8 +1411,21 @@ extern "C" int tnp_engine_skeleton(tnp_engine* e, int unit, float size, void* st
   if (buf_ensure(e->used, LLL * sizeof(int32_t), s)) return -1;
   if (buf_ensure(e->nid, LLL * sizeof(int64_t), s)) return -1;
   TNP_CHECK(hipMemsetAsync(e->used.p, 0, LLL * sizeof(int32_t), s));
+  if (mode != TNP_SKELETON_DISTANCE && mode != TNP_SKELETON_SIGN) {
+    tnp_set_error("skeleton mode %d (0: distance, 1: sign)", mode);
+    return -1;
+  }
+  const bool sign = mode == TNP_SKELETON_SIGN;
   int64_t tile_pts = (int64_t)std::min(unit, L) * std::min(unit, L) * std::min(unit, L);
-  if (buf_ensure(e->stage, tile_pts * sizeof(float), s)) return -1;
+  if (buf_ensure(e->stage, tile_pts * sizeof(float) * (sign ? e->K : 1), s)) return -1;
+  // sign mode: the tile's points, their forward and packed keys (pos, zero,
+  // grid, pz) in the curve path's scratch slots
+  Buf* sk = e->cv;
+  if (sign) {
+    if (buf_ensure(sk[CV_CORNERS], tile_pts * 3 * sizeof(float), s)) return -1;
+    for (int k : {CV_D0, CV_D1, CV_GG}) if (buf_ensure(sk[k], tile_pts * sizeof(uint64_t), s)) return -1;
+    if (buf_ensure(sk[CV_STAGE_C], tile_pts * 2 * sizeof(uint64_t), s)) return -1;
+  }
   if (buf_ensure(e->shared, 16, s)) return -1;
   unsigned int* gmax = P<unsigned int>(e->shared);
   int64_t total = 0;
@@ -1416,13 +1434,26 @@ extern "C" int tnp_engine_skeleton(tnp_engine* e, int unit, float size, void* st
       for (int k0 = 0; k0 < L; k0 += unit - 1) {
         int n0 = std::min(L, i0 + unit) - i0, n1 = std::min(L, j0 + unit) - j0,
             n2 = std::min(L, k0 + unit) - k0;
-        TNP_CHECK(hipMemsetAsync(gmax, 0, sizeof(unsigned int), s));
-        if (launch_skel_eval(e->net, i0, j0, k0, n0, n1, n2, P<float>(e->stage), gmax, s)) return -1;
+        const uint64_t* keys = nullptr;
+        if (sign) {
+          // Net.region on the tile's vertices (tropical.py:199-201): the
+          // forward of every point with its eps-sign keys
+          const int64_t np_ = (int64_t)n0 * n1 * n2;
+          if (launch_skel_points(i0, j0, k0, n0, n1, n2, e->net.marks, P<float>(sk[CV_CORNERS]), s)) return -1;
+          if (launch_forward(e->net, P<float>(sk[CV_CORNERS]), np_, P<float>(e->stage), np_, 1, s, nullptr,
+                             P<uint64_t>(sk[CV_D0]), P<uint64_t>(sk[CV_D1]), P<uint64_t>(sk[CV_GG]),
+                             P<uint64_t>(sk[CV_STAGE_C])))
+            return -1;
+          keys = P<uint64_t>(sk[CV_STAGE_C]);
+        } else {
+          TNP_CHECK(hipMemsetAsync(gmax, 0, sizeof(unsigned int), s));
+          if (launch_skel_eval(e->net, i0, j0, k0, n0, n1, n2, P<float>(e->stage), gmax, s)) return -1;
+        }
         int64_t N = skel_candidates(n0, n1, n2);
         int64_t nt = skel_tiles(N);
         if (buf_ensure(e->blk, (nt + 1) * sizeof(int32_t), s)) return -1;
         if (buf_ensure(e->blkoff, (nt + 1) * sizeof(int64_t), s)) return -1;
-        if (launch_skel_edges(false, i0, j0, k0, n0, n1, n2, L, P<float>(e->stage), dmax, gmax,
+        if (launch_skel_edges(false, i0, j0, k0, n0, n1, n2, L, P<float>(e->stage), keys, dmax, gmax,
                               P<int32_t>(e->blk), nullptr, 0, nullptr, nullptr, s))
           return -1;
         if (scan_counts(e, P<int32_t>(e->blk), P<int64_t>(e->blkoff), nt, CTR_AUX, s)) return -1;
@@ -1430,7 +1461,7 @@ extern "C" int tnp_engine_skeleton(tnp_engine* e, int unit, float size, void* st
         int64_t cnt = e->h_ctr[CTR_AUX];
         if (cnt > 0) {
           if (buf_ensure(e->edges_alt, (total + cnt) * 2 * sizeof(int32_t), s, true)) return -1;
-          if (launch_skel_edges(true, i0, j0, k0, n0, n1, n2, L, P<float>(e->stage), dmax, gmax,
+          if (launch_skel_edges(true, i0, j0, k0, n0, n1, n2, L, P<float>(e->stage), keys, dmax, gmax,
                                 nullptr, P<int64_t>(e->blkoff), total, P<int32_t>(e->edges_alt),
                                 P<int32_t>(e->used), s))
             return -1;

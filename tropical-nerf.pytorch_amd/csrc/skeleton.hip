@@ -1,10 +1,16 @@
-// TropicalHashGrid.skeleton(net, unit=128) with PRUNING_MODE="distance"
-// (tropical/tropical.py:113-225) on the device.
+// TropicalHashGrid.skeleton(net, unit=128) (tropical/tropical.py:158-225) on
+// the device, both pruning modes of the reference:
+//   "distance" (PRUNING_MODE's value there, _skeleton_dist, tropical.py:111-136)
+//   "sign"     (the dormant branch, tropical.py:198-202 -> _skeleton,
+//               tropical.py:80-109: an edge is kept iff its endpoints' eps-sign
+//               vectors over all planes differ)
 //
 // Per reference tile (starts range(0, L, unit-1), 1-mark overlap):
 //   skel_eval   : |sdf| at every tile lattice point + tile max |grad sdf|
-//   skel_edges  : axis edges (hi, lo) with both |sdf| <= sqrt(3)*2*dmax*gmax,
-//                 x then y then z, meshgrid-ij order (count -> scan -> emit)
+//                 (sign mode: skel_points + the forward with packed keys)
+//   skel_edges  : axis edges (hi, lo) with both |sdf| <= sqrt(3)*2*dmax*gmax
+//                 (sign mode: keys differ), x then y then z, meshgrid-ij order
+//                 (count -> scan -> emit)
 // then squeeze: used global ids p2v(i,j,k) -> dense ranks (sorted unique),
 // vertices = marks[v2p(id)]*2-1 with the reference's float32 v2p division.
 // Duplicate edges on tile overlaps are kept, as in the reference.
@@ -57,8 +63,20 @@ struct TileGeom {
   int64_t nx, ny, nz;
 };
 
-__device__ __forceinline__ bool skel_edge(const TileGeom& g, const float* dist, float thr, int64_t c,
-                                          int& hi, int& lo) {
+// the tile's lattice points as vertices (marks * 2 - 1, preprocess_inverse)
+__global__ void k_skel_points(int i0, int j0, int k0, int n0, int n1, int n2, const float* __restrict__ marks,
+                              float* __restrict__ xyz) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)n0 * n1 * n2) return;
+  const int k = (int)(t % n2), j = (int)((t / n2) % n1), i = (int)(t / ((int64_t)n1 * n2));
+  const int ix[3] = {i0 + i, j0 + j, k0 + k};
+#pragma unroll
+  for (int d = 0; d < 3; ++d) xyz[3 * t + d] = __fsub_rn(__fmul_rn(marks[ix[d]], 2.0f), 1.0f);
+}
+
+// keys != null: sign mode (keep iff the endpoints' (pos, zero) keys differ)
+__device__ __forceinline__ bool skel_edge(const TileGeom& g, const float* dist, const ulonglong2* keys,
+                                          float thr, int64_t c, int& hi, int& lo) {
   int a0, a1, a2, b0, b1, b2;  // lo (a) and hi (b) local coords
   if (c < g.nx) {              // shape (n0-1, n1, n2)
     a2 = (int)(c % g.n2); a1 = (int)((c / g.n2) % g.n1); a0 = (int)(c / ((int64_t)g.n1 * g.n2));
@@ -72,12 +90,15 @@ __device__ __forceinline__ bool skel_edge(const TileGeom& g, const float* dist, 
     a2 = (int)(r % (g.n2 - 1)); a1 = (int)((r / (g.n2 - 1)) % g.n1); a0 = (int)(r / ((int64_t)g.n1 * (g.n2 - 1)));
     b0 = a0; b1 = a1; b2 = a2 + 1;
   }
-  float da = dist[((int64_t)a0 * g.n1 + a1) * g.n2 + a2];
-  float db = dist[((int64_t)b0 * g.n1 + b1) * g.n2 + b2];
+  const int64_t ia = ((int64_t)a0 * g.n1 + a1) * g.n2 + a2, ib = ((int64_t)b0 * g.n1 + b1) * g.n2 + b2;
   const int64_t LL = (int64_t)g.L * g.L;
   lo = (int)((g.i0 + a0) * LL + (int64_t)(g.j0 + a1) * g.L + (g.k0 + a2));
   hi = (int)((g.i0 + b0) * LL + (int64_t)(g.j0 + b1) * g.L + (g.k0 + b2));
-  return (db <= thr) && (da <= thr);
+  if (keys) {
+    const ulonglong2 ka = keys[ia], kb = keys[ib];
+    return ka.x != kb.x || ka.y != kb.y;
+  }
+  return (dist[ib] <= thr) && (dist[ia] <= thr);
 }
 
 __device__ __forceinline__ float skel_threshold(float dmax, const unsigned int* gmax_bits) {
@@ -88,17 +109,17 @@ __device__ __forceinline__ float skel_threshold(float dmax, const unsigned int* 
 }
 
 __global__ void __launch_bounds__(TNP_BLOCK)
-k_skel_count(TileGeom g, const float* __restrict__ dist, float dmax,
+k_skel_count(TileGeom g, const float* __restrict__ dist, const ulonglong2* __restrict__ keys, float dmax,
              const unsigned int* __restrict__ gmax_bits, int32_t* __restrict__ blk) {
   __shared__ int lds[TNP_WAVES];
-  const float thr = skel_threshold(dmax, gmax_bits);
+  const float thr = keys ? 0.f : skel_threshold(dmax, gmax_bits);
   const int64_t N = g.nx + g.ny + g.nz;
   int64_t base = (int64_t)blockIdx.x * TILE;
   int c = 0;
   for (int k = 0; k < IPT; ++k) {
     int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
     int hi, lo;
-    if (i < N) c += skel_edge(g, dist, thr, i, hi, lo);
+    if (i < N) c += skel_edge(g, dist, keys, thr, i, hi, lo);
   }
   c = tnp::wave_sum(c);
   if (tnp::lane() == 0) lds[tnp::wave()] = c;
@@ -111,18 +132,18 @@ k_skel_count(TileGeom g, const float* __restrict__ dist, float dmax,
 }
 
 __global__ void __launch_bounds__(TNP_BLOCK)
-k_skel_emit(TileGeom g, const float* __restrict__ dist, float dmax,
+k_skel_emit(TileGeom g, const float* __restrict__ dist, const ulonglong2* __restrict__ keys, float dmax,
             const unsigned int* __restrict__ gmax_bits, const int64_t* __restrict__ blkoff,
             int64_t out_base, int32_t* __restrict__ out, int32_t* __restrict__ used) {
   __shared__ int lds[TNP_WAVES];
-  const float thr = skel_threshold(dmax, gmax_bits);
+  const float thr = keys ? 0.f : skel_threshold(dmax, gmax_bits);
   const int64_t N = g.nx + g.ny + g.nz;
   int64_t base = (int64_t)blockIdx.x * TILE;
   int64_t run = out_base + blkoff[blockIdx.x];
   for (int k = 0; k < IPT; ++k) {
     int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
     int hi = 0, lo = 0;
-    bool f = (i < N) && skel_edge(g, dist, thr, i, hi, lo);
+    bool f = (i < N) && skel_edge(g, dist, keys, thr, i, hi, lo);
     int tot;
     int r = tnp::block_rank(f, lds, tot);
     if (f) {
@@ -190,18 +211,29 @@ static TileGeom geom(int i0, int j0, int k0, int n0, int n1, int n2, int L) {
   return g;
 }
 
+int launch_skel_points(int i0, int j0, int k0, int n0, int n1, int n2, const float* marks, float* xyz,
+                       hipStream_t s) {
+  const int64_t n = (int64_t)n0 * n1 * n2;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_skel_points, dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, i0, j0, k0, n0, n1, n2, marks,
+                     xyz);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+
 int launch_skel_edges(bool emit, int i0, int j0, int k0, int n0, int n1, int n2, int L,
-                      const float* dist, float dmax, const unsigned int* gmax_bits, int32_t* blk,
-                      const int64_t* blkoff, int64_t out_base, int32_t* out, int32_t* used,
+                      const float* dist, const uint64_t* keys, float dmax, const unsigned int* gmax_bits,
+                      int32_t* blk, const int64_t* blkoff, int64_t out_base, int32_t* out, int32_t* used,
                       hipStream_t s) {
   TileGeom g = geom(i0, j0, k0, n0, n1, n2, L);
   int64_t N = g.nx + g.ny + g.nz;
   if (N <= 0) return 0;
+  const ulonglong2* k2 = reinterpret_cast<const ulonglong2*>(keys);
   if (emit)
-    hipLaunchKernelGGL(k_skel_emit, dim3((unsigned)skel_tiles(N)), dim3(TNP_BLOCK), 0, s, g, dist, dmax,
+    hipLaunchKernelGGL(k_skel_emit, dim3((unsigned)skel_tiles(N)), dim3(TNP_BLOCK), 0, s, g, dist, k2, dmax,
                        gmax_bits, blkoff, out_base, out, used);
   else
-    hipLaunchKernelGGL(k_skel_count, dim3((unsigned)skel_tiles(N)), dim3(TNP_BLOCK), 0, s, g, dist,
+    hipLaunchKernelGGL(k_skel_count, dim3((unsigned)skel_tiles(N)), dim3(TNP_BLOCK), 0, s, g, dist, k2,
                        dmax, gmax_bits, blk);
   TNP_CHECK(hipGetLastError());
   return 0;

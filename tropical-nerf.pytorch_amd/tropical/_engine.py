@@ -63,10 +63,17 @@ class Engine:
                                                  C.byref(V), C.byref(E)), "tnp_engine_lattice")
         return V.value, E.value
 
-    def skeleton(self, unit: int = 128, size: float = None):
+    SKELETON_MODES = {"distance": 0, "sign": 1}
+
+    def skeleton(self, unit: int = 128, size: float = None, mode: str = "distance"):
+        """mode: the reference's PRUNING_MODE (tropical.py:184-205)."""
+        if mode not in self.SKELETON_MODES:
+            raise ValueError(f"skeleton pruning mode {mode!r}: 'distance' or 'sign'")
         V, E = C.c_int64(), C.c_int64()
-        _hip.check(_hip.lib().tnp_engine_skeleton(self.h, unit, float(size or 0.0), self._s,
-                                                  C.byref(V), C.byref(E)), "tnp_engine_skeleton")
+        _hip.check(_hip.lib().tnp_engine_skeleton_mode(self.h, unit, float(size or 0.0),
+                                                       self.SKELETON_MODES[mode], self._s,
+                                                       C.byref(V), C.byref(E)),
+                   "tnp_engine_skeleton_mode")
         return V.value, E.value
 
     def sizes(self):

@@ -62,6 +62,7 @@ SIGNATURES = {
     "tnp_engine_set_net": (C.c_int, [_VP, _NETP]),
     "tnp_engine_load": (C.c_int, [_VP, _VP, _I64, _VP, _I64, _VP, C.c_int, _VP]),
     "tnp_engine_skeleton": (C.c_int, [_VP, C.c_int, _F, _VP, _P64, _P64]),
+    "tnp_engine_skeleton_mode": (C.c_int, [_VP, C.c_int, _F, C.c_int, _VP, _P64, _P64]),
     "tnp_engine_lattice": (C.c_int, [_VP, C.c_int, C.c_int, C.c_int, _VP, _P64, _P64]),
     "tnp_engine_active_planes": (C.c_int, [_VP, C.c_int, _PU64, _VP]),
     "tnp_engine_split": (C.c_int, [_VP, C.c_int, _VP, _P64, _P32]),

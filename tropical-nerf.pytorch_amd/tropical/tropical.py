@@ -119,11 +119,14 @@ class TropicalHashGrid(nn.Module):
             v.sub_(p[-1] * L ** i)
         return torch.stack(p, dim=-1)
 
-    def skeleton(self, net: nn.Module, unit: int = 128) -> Tuple[Tensor, Tensor]:
-        """Distance-pruned initial edge set (tropical.py:158-225), on device."""
+    def skeleton(self, net: nn.Module, unit: int = 128, mode: str = "distance") -> Tuple[Tensor, Tensor]:
+        """Pruned initial edge set (tropical.py:158-225), on device.  mode is
+        the reference's PRUNING_MODE: "distance" (its value) or "sign" (its
+        dormant branch, tropical.py:198-202: edges whose endpoints' eps-sign
+        vectors differ)."""
         from ._engine import engine_for
         eng = engine_for(net)
-        V, E = eng.skeleton(unit=unit, size=None)
+        V, E = eng.skeleton(unit=unit, size=None, mode=mode)
         if E == 0:
             dev = self.marks.device
             return torch.zeros(0, device=dev), torch.zeros(0, dtype=torch.int64, device=dev)
