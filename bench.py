@@ -203,6 +203,41 @@ def small_net_check(dev, force: bool = True):
     return out
 
 
+def large_net_check(dev):
+    """BASELINE config 3's net class, Net(3,16,4,8,128,T=19): the committed
+    201-mark large net (sphere-fitted, tests/golden/large_sphere.npz, made by
+    running the reference), subpoly() end to end on the GPU -- multi-tile
+    skeleton, every step, surface and faces -- checked against the reference's
+    own output hashes.  The reference's time is the one make_golden.py
+    measured running it on the 8-core build container (not this host)."""
+    import io
+    import contextlib
+    import tropical.subpoly as sp
+    from golden_io import load, sha
+    from helpers import product_net
+    d = load("large_sphere")
+    net = product_net(d, dev)
+    stats = []
+    with contextlib.redirect_stdout(io.StringIO()):
+        sp.subpoly(net, 3, 1.2, force=True)  # warm
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        faces, verts, fwi = sp.subpoly(net, 3, 1.2, force=True, stats=stats)
+        torch.cuda.synchronize(dev)
+        t_gpu = time.perf_counter() - t0
+    S = sum(s["S"] for s in stats)
+    ok = (sha(verts.cpu().numpy()) == str(d["sha_surf"]) and
+          sha(np.asarray(fwi, dtype=np.int64)) == str(d["sha_tri"]) and
+          sha(np.asarray(faces, dtype=np.float32)) == str(d["sha_faces"]))
+    ref_s = float(d["ref_seconds"])
+    return {"config": "large net Net(3,16,4,8,128,T=19), 201 marks, sphere-fitted stand-in, flat, "
+                      "subpoly() end to end", "edges_subdivided": int(S), "gpu_s": round(t_gpu, 4),
+            "gpu_edges_per_s": round(S / t_gpu, 1), "reference_cpu_s": round(ref_s, 2),
+            "reference_cpu_note": "the reference itself, run once on the 8-core build container "
+                                  "(tests/golden/make_golden.py)",
+            "gpu_over_reference": round(ref_s / t_gpu, 1), "surface_faces_match_reference": bool(ok)}
+
+
 def chamfer(a: np.ndarray, b: np.ndarray) -> float:
     """chamfer_distance.py:39-48 formula (mean NN L2 both ways / 2)."""
     if len(a) == 0 or len(b) == 0:
@@ -417,6 +452,7 @@ def main():
         if not args.no_cpu and world == 1:
             out["small_net"] = small_net_check(dev, force=True)
             out["small_net_curve"] = small_net_check(dev, force=False)
+            out["large_net"] = large_net_check(dev)
             engine_for(net)  # restore
         print(json.dumps(out), flush=True)
     if world > 1:
