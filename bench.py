@@ -48,14 +48,24 @@ KERNEL_SYMBOL = {"forward_new": "k_forward_new", "prune": "k_prune_lb", "connect
                  "connect": "k_connect", "count_live": "k_count_flags", "override_new": "k_override_new"}
 
 
-def pmc_traffic(kernel: str, marks: int, seed: int):
-    """HBM bytes per launch of `kernel` measured by the PMC passes of the
-    same workload (None: other workload, or no profile)."""
+CLOCK_HZ = 2.4e9       # MI355X peak engine clock (MI355X_MICROARCH.md)
+SIMDS = 256 * 4        # 256 CUs x 4 SIMD16: a wave64 VALU instruction issues over 4 cycles
+
+
+def pmc_row(kernel: str, marks: int, seed: int):
+    """The committed PMC counters per launch of `kernel` on the same workload
+    (None: other workload, or no profile)."""
     if marks != 128 or seed != 6 or not os.path.isfile(PMC_TABLE):
         return None
     with open(PMC_TABLE) as f:
         ks = json.load(f)["kernels"]
-    k = ks.get(KERNEL_SYMBOL.get(kernel, "k_" + kernel))
+    return ks.get(KERNEL_SYMBOL.get(kernel, "k_" + kernel))
+
+
+def pmc_traffic(kernel: str, marks: int, seed: int):
+    """HBM bytes per launch of `kernel` measured by the PMC passes of the
+    same workload (None: other workload, or no profile)."""
+    k = pmc_row(kernel, marks, seed)
     return None if k is None else k.get("traffic_bytes_per_launch")
 
 
@@ -415,10 +425,20 @@ def main():
                     "traffic_gbs": None if traffic is None else round(traffic / (avg_ms * 1e-3) / 1e9, 1),
                     "avg_launch_us": round(avg_ms * 1e3, 2), "launches": kt["launches"],
                     "alg_bytes_per_launch": int(alg), "dominant_overall": dom_all,
+                    # what else bounds it, from the same PMC passes: VALU issue
+                    # (wave64 VALU instructions x 4 cycles over every SIMD) and
+                    # the L2 hit rate
+                    "valu_util": None, "l2_hit": None,
                     # the whole hyperplane loop against the same peak: SURVEY
                     # §8d's per-step model (bench.algorithmic_bytes) / pass time
                     "whole_loop_gbs": round(loop_gbs, 1),
                     "whole_loop_frac": round(loop_gbs / (HBM_PEAK_GBS * world), 4)}
+        if roof and world == 1:
+            row = pmc_row(dom, G, args.seed)
+            if row and "SQ_INSTS_VALU" in row:
+                roof["valu_util"] = round(row["SQ_INSTS_VALU"] * 4 / (roof["avg_launch_us"] * 1e-6 * CLOCK_HZ * SIMDS), 3)
+            if row and "TCC_HIT_sum" in row:
+                roof["l2_hit"] = round(row["TCC_HIT_sum"] / max(row["TCC_HIT_sum"] + row["TCC_MISS_sum"], 1), 3)
         out = {
             "metric": "edges subdivided/sec", "value": round(value, 1), "unit": "edges/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,

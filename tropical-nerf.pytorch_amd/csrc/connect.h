@@ -59,12 +59,12 @@ __device__ __forceinline__ void add_pair_stats(int64_t a, int64_t r, int64_t x, 
 // ---------------------------------------------------------------------------
 // Window pass: the pairs of every cell of <= WCELL members.  The entries are
 // cell-contiguous; a wave stages the 64 records of window w (entries
-// [lo + 32 w, lo + 32 w + 64) of [lo, hi)) in LDS; each of its first 32
+// [lo + S w, lo + S w + 64) of [lo, hi), S = WSTRIDE) in LDS; each of its first S
 // entries j is tested against the later entries of its cell, the (j,
 // partner) tests flattened over the 64 lanes (a wave scan of the per-entry
 // counts; a test finds its pair in a per-window LDS table the initiators
 // fill, or by a 6-step search past WOWN tests): a pair (j < i) of such a cell is
-// tested exactly once, in window floor(j / 32) (i - j <= 32).  Each record
+// tested exactly once, in window floor(j / S) (i - j <= 64 - S).  Each record
 // is read once from memory per window; emitted keys go through a per-wave LDS
 // buffer, one global append per WKEYS.
 // ---------------------------------------------------------------------------
@@ -107,9 +107,9 @@ __device__ __forceinline__ void window_pass(const CellEnt* __restrict__ ent, int
                                             uint64_t* __restrict__ keys, int64_t cap,
                                             int64_t* __restrict__ ctr, WinLds& W, WinAcc& a) {
   const int wv = tnp::wave(), L = tnp::lane();
-  const int64_t nwin = (hi - lo + 31) / 32;
+  const int64_t nwin = (hi - lo + WSTRIDE - 1) / WSTRIDE;
   for (int64_t w = w0; w < nwin; w += dw) {
-    const int64_t e = lo + w * 32 + L;
+    const int64_t e = lo + w * WSTRIDE + L;
     const bool valid = e < hi;
     CellEnt r;
     if (valid) {
@@ -127,7 +127,7 @@ __device__ __forceinline__ void window_pass(const CellEnt* __restrict__ ent, int
     const uint32_t nxt = __shfl_down(r.tag, 1, 64);
     const uint64_t bm = __ballot(L == 63 || nxt != r.tag);
     const int last = L + __builtin_ctzll(bm >> L);
-    const bool init = valid && L < 32 && !(r.tag & 0x80000000u);
+    const bool init = valid && L < WSTRIDE && !(r.tag & 0x80000000u);
     const int rounds = init ? last - L : 0;
     // flatten the window's (initiator, partner) tests over the lanes: test t
     // belongs to the last initiator j with exc[j] <= t, partner j + 1 + t - exc[j]

@@ -111,7 +111,11 @@ struct alignas(32) CellEnt {
 // cells of at most WCELL members have their pairs tested by the window pass
 // (k_connect_win): a pair (j < i) of such a cell lies in the 64-entry
 // window starting at 32 * floor(j / 32)
-constexpr int WCELL = 33;
+#ifndef TNP_WSTRIDE
+#define TNP_WSTRIDE 32
+#endif
+constexpr int WSTRIDE = TNP_WSTRIDE;  // window pass: windows of 64 records at this stride
+constexpr int WCELL = 65 - WSTRIDE;    // a pair (j < i) of such a cell has i - j <= 64 - WSTRIDE
 // cell_flags of a member (grid word g) in the cell with coordinates c (+2)
 __device__ __forceinline__ uint32_t cell_flags(uint64_t g, int cx, int cy, int cz) {
   const int c[3] = {cx, cy, cz};
