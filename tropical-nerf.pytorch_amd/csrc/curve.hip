@@ -835,7 +835,7 @@ __device__ __forceinline__ void plane_pair_grad(const NetDev& net, const float* 
       }
       uint32_t id = net.dense[l] ? (gc[0] + gc[1] * res + gc[2] * (res * res))
                                  : (gc[0] ^ (gc[1] * P1) ^ (gc[2] * P2));
-      id %= net.sizes[l];
+      id = wrap_index(id, net.sizes[l]);
       float2 v = table_entry(net, l, id);
       float dv = __fadd_rn(__fmul_rn(v.x, df[2 * l]), __fmul_rn(v.y, df[2 * l + 1]));
 #pragma unroll
@@ -884,7 +884,7 @@ k_descend(NetDev net, int64_t G, const int32_t* __restrict__ glist,
     float u[3], gu[3];
 #pragma unroll
     for (int d = 0; d < 3; ++d)
-      u[d] = __fdiv_rn(__fadd_rn(__fadd_rn(e0[d], __fmul_rn(x[d], de[d])), 1.0f), 2.0f);
+      u[d] = __fmul_rn(__fadd_rn(__fadd_rn(e0[d], __fmul_rn(x[d], de[d])), 1.0f), 0.5f);  // x/2 == x*0.5
     plane_pair_grad<LV, H>(net, w, u, j0, idx, mh, mo, G == 1, d0, d1, gu);
     float gx[3], nn = 0.f;
 #pragma unroll
@@ -973,7 +973,7 @@ k_descend_wave(NetDev net, int64_t G, const int32_t* __restrict__ glist,
     float u[3];
 #pragma unroll
     for (int d = 0; d < 3; ++d)
-      u[d] = __fdiv_rn(__fadd_rn(__fadd_rn(e0[d], __fmul_rn(x[d], de[d])), 1.0f), 2.0f);
+      u[d] = __fmul_rn(__fadd_rn(__fadd_rn(e0[d], __fmul_rn(x[d], de[d])), 1.0f), 0.5f);  // x/2 == x*0.5
     // this lane's corner (encode's op order)
     float t[3];
     uint32_t gc[3];
@@ -993,7 +993,7 @@ k_descend_wave(NetDev net, int64_t G, const int32_t* __restrict__ glist,
       }
     }
     uint32_t id = dense ? (gc[0] + gc[1] * res + gc[2] * (res * res)) : (gc[0] ^ (gc[1] * P1) ^ (gc[2] * P2));
-    id %= size;
+    id = wrap_index(id, size);
     const float2 v = table_entry(net, lc, id);
     const float px = __fmul_rn(wc, v.x), py = __fmul_rn(wc, v.y);
     float f[IN];

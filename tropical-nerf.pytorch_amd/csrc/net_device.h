@@ -10,6 +10,12 @@ namespace tnpnet {
 constexpr uint32_t P1 = 2654435761u;
 constexpr uint32_t P2 = 805459861u;
 
+// idx mod size, without an integer division when size is a power of two
+// (every hashed level: 2^T; the branch is uniform)
+__device__ __forceinline__ uint32_t wrap_index(uint32_t idx, uint32_t size) {
+  return (size & (size - 1u)) == 0u ? (idx & (size - 1u)) : idx % size;
+}
+
 // float2 entry `idx` of level l in either table layout (NetDev::tied)
 __device__ __forceinline__ float2 table_entry(const NetDev& net, int l, uint32_t idx) {
   const float2* tab = reinterpret_cast<const float2*>(net.table);
@@ -54,7 +60,7 @@ __device__ __forceinline__ void encode_tied(const NetDev& net, const float x[3],
     }
     uint32_t idx = dense ? (gc[0] + gc[1] * res + gc[2] * (res * res))
                          : (gc[0] ^ (gc[1] * P1) ^ (gc[2] * P2));
-    idx %= size;
+    idx = wrap_index(idx, size);
 #pragma unroll
     for (int q = 0; q < LV / 2; ++q) {
       const float4 v = tab[(size_t)idx * (LV / 2) + q];
@@ -109,7 +115,7 @@ __device__ __forceinline__ void encode(const NetDev& net, const float x[3], floa
       }
       uint32_t idx = dense ? (gc[0] + gc[1] * res + gc[2] * (res * res))
                            : (gc[0] ^ (gc[1] * P1) ^ (gc[2] * P2));
-      idx %= size;
+      idx = wrap_index(idx, size);
       float2 v = tab[idx];
       a0 = __fadd_rn(a0, __fmul_rn(w, v.x));
       a1 = __fadd_rn(a1, __fmul_rn(w, v.y));
@@ -122,7 +128,7 @@ __device__ __forceinline__ void encode(const NetDev& net, const float x[3], floa
 __device__ __forceinline__ void load_point(const float* xyz, int64_t i, float x[3]) {
   // Net.preprocess: (x + 1) / 2   (model.py:78-79)
 #pragma unroll
-  for (int d = 0; d < 3; ++d) x[d] = __fdiv_rn(__fadd_rn(xyz[3 * i + d], 1.0f), 2.0f);
+  for (int d = 0; d < 3; ++d) x[d] = __fmul_rn(__fadd_rn(xyz[3 * i + d], 1.0f), 0.5f);  // x/2 == x*0.5 exactly
 }
 
 template <int IN, int OUT>
@@ -265,7 +271,7 @@ __device__ __forceinline__ float sdf_grad(const NetDev& net, const float* w, con
       }
       uint32_t idx = net.dense[l] ? (gc[0] + gc[1] * res + gc[2] * (res * res))
                                   : (gc[0] ^ (gc[1] * P1) ^ (gc[2] * P2));
-      idx %= net.sizes[l];
+      idx = wrap_index(idx, net.sizes[l]);
       float2 v = table_entry(net, l, idx);
       float dv = v.x * df[2 * l] + v.y * df[2 * l + 1];
 #pragma unroll

@@ -45,7 +45,7 @@ k_skel_eval(NetDev net, int i0, int j0, int k0, int n0, int n1, int n2,
     for (int d = 0; d < 3; ++d) {
       // vertex = marks*2-1 (preprocess_inverse), then preprocess (x+1)/2
       float v = __fsub_rn(__fmul_rn(net.marks[ix[d]], 2.0f), 1.0f);
-      x[d] = __fdiv_rn(__fadd_rn(v, 1.0f), 2.0f);
+      x[d] = __fmul_rn(__fadd_rn(v, 1.0f), 0.5f);  // x/2 == x*0.5 exactly
     }
     float g[3];
     float y = sdf_grad<LV, H>(net, w, x, g);
