@@ -64,6 +64,15 @@ struct WinArgs {
   int64_t cap;
 };
 
+// the global pair-cell lists the fused last workgroup fills
+struct PairLists {
+  int32_t *pcell, *pent, *pn;
+  int64_t* ptoff;
+  int32_t* bcell;
+  int64_t bcap, chunk;
+  int32_t *bcount, *bcur;
+};
+
 // the new vertices' failover override, applied by the bucket count
 // (k_override_new's work; shared == null: not here)
 struct Override {
@@ -326,6 +335,31 @@ k_bucket_scatter(const int32_t* __restrict__ members, int64_t S, int64_t V, int6
 #endif
 constexpr int GIPT = TNP_GIPT;
 
+// pair cell i of a bucket (its area slot a, global slot o, the bucket's
+// first pair po) into the global lists and k_connect's chunk table; handed:
+// the lists come from other workgroups of the running launch (sc1 loads)
+__device__ __forceinline__ void gather_pair_cell(int64_t a, int64_t o, int64_t po,
+                                                 const int32_t* __restrict__ lcell,
+                                                 const int32_t* __restrict__ lent,
+                                                 const int32_t* __restrict__ ln,
+                                                 const int64_t* __restrict__ lpoff, int32_t* __restrict__ pcell,
+                                                 int32_t* __restrict__ pent, int32_t* __restrict__ pn,
+                                                 int64_t* __restrict__ ptoff, int32_t* __restrict__ bcell,
+                                                 int64_t bcap, int64_t chunk, int64_t* __restrict__ ctr,
+                                                 bool handed) {
+  const int m = handed ? tnp::ld_agent(ln + a) : ln[a];
+  const int64_t lo = po + (handed ? tnp::ld_agent(lpoff + a) : lpoff[a]);
+  pcell[o] = handed ? tnp::ld_agent(lcell + a) : lcell[a];
+  pent[o] = handed ? tnp::ld_agent(lent + a) : lent[a];
+  pn[o] = m;
+  ptoff[o] = lo;
+  // k_connect's chunk table (k_chunk_cells): chunk q starts in pair cell o
+  const int64_t n = (int64_t)m * (m - 1) / 2;
+  const int64_t b0 = (lo + chunk - 1) / chunk, b1 = (lo + n + chunk - 1) / chunk;
+  if (b1 > bcap) atomicOr((unsigned long long*)&ctr[CTR_BOVF], 1ull);
+  for (int64_t q = b0; q < b1 && q < bcap; ++q) bcell[q] = (int32_t)o;
+}
+
 // the grouping of one bucket of n >= 2 entries (k_bucket_group)
 template <int SH>
 __device__ __forceinline__ void group_bucket(const BGeom& G, int b, int64_t base, int64_t n,
@@ -426,10 +460,11 @@ __device__ __forceinline__ void group_bucket(const BGeom& G, int b, int64_t base
       const int cx = (bx << G.sh) | (i >> (2 * G.sh));
       const int cy = (by << G.sh) | ((i >> G.sh) & m_);
       const int cz = (bz << G.sh) | (i & m_);
-      lcell[area + opc] = (cx * G.NC + cy) * G.NC + cz;
-      lent[area + opc] = (int32_t)(base + cur[i] - m);
-      ln[area + opc] = m;
-      lpoff[area + opc] = op;
+      // agent-scope stores: the fused last workgroup gathers them (tnp::last_block)
+      tnp::st_agent(lcell + area + opc, (int32_t)((cx * G.NC + cy) * G.NC + cz));
+      tnp::st_agent(lent + area + opc, (int32_t)(base + cur[i] - m));
+      tnp::st_agent(ln + area + opc, (int32_t)m);
+      tnp::st_agent(lpoff + area + opc, op);
       ++opc;
       op += (int64_t)m * (m - 1) / 2;
     }
@@ -448,7 +483,7 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
                int32_t* __restrict__ lcell, int32_t* __restrict__ lent, int32_t* __restrict__ ln,
                int64_t* __restrict__ lpoff, int64_t* __restrict__ bnpc, int64_t* __restrict__ bnpairs,
                int64_t* __restrict__ bspairs, int64_t* __restrict__ pcoff, int64_t* __restrict__ pairoff,
-               int64_t* __restrict__ spoff, int fuse, WinArgs wa, int64_t* __restrict__ ctr) {
+               int64_t* __restrict__ spoff, int fuse, WinArgs wa, PairLists pl, int64_t* __restrict__ ctr) {
   constexpr int LC = 1 << (3 * SH);
   __shared__ int cnt[LC];
   __shared__ int cur[LC];
@@ -502,10 +537,23 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
     ctr[CTR_TESTS] = TT;
     ctr[CTR_SPAIRS] = SP;
   }
+  __syncthreads();  // pcoff / pairoff: this workgroup's stores
+  // the pair-cell gather (k_pair_gather's work), a thread per bucket, and the
+  // bucket counters cleaned for the next step
+  for (int bb = threadIdx.x; bb < NB; bb += TNP_BLOCK) {
+    pl.bcount[bb] = 0;
+    pl.bcur[bb] = 0;
+    const int cnt = (int)tnp::ld_agent(bnpc + bb);
+    const int64_t area = bbase[bb] / 2, o = pcoff[bb], po = pairoff[bb];
+    for (int i = 0; i < cnt; ++i)
+      gather_pair_cell(area + i, o + i, po, lcell, lent, ln, lpoff, pl.pcell, pl.pent, pl.pn, pl.ptoff, pl.bcell,
+                       pl.bcap, pl.chunk, ctr, true);
+  }
 }
 
 // (6) the global pair-cell list k_connect walks: bucket order, then local
-// cell order
+// cell order (k_pair_gather: a workgroup per bucket; the fused last
+// workgroup of k_bucket_group: a thread per bucket)
 __global__ void __launch_bounds__(TNP_BLOCK)
 k_pair_gather(const int64_t* __restrict__ bbase, const int64_t* __restrict__ bnpc,
               const int64_t* __restrict__ pcoff, const int64_t* __restrict__ pairoff,
@@ -522,19 +570,9 @@ k_pair_gather(const int64_t* __restrict__ bbase, const int64_t* __restrict__ bnp
   const int cnt = (int)bnpc[b];
   if (cnt == 0) return;
   const int64_t area = bbase[b] / 2, o = pcoff[b], po = pairoff[b];
-  for (int i = threadIdx.x; i < cnt; i += TNP_BLOCK) {
-    const int m = ln[area + i];
-    const int64_t lo = po + lpoff[area + i];
-    pcell[o + i] = lcell[area + i];
-    pent[o + i] = lent[area + i];
-    pn[o + i] = m;
-    ptoff[o + i] = lo;
-    // k_connect's chunk table (k_chunk_cells): chunk q starts in pair cell o + i
-    const int64_t n = (int64_t)m * (m - 1) / 2;
-    const int64_t b0 = (lo + chunk - 1) / chunk, b1 = (lo + n + chunk - 1) / chunk;
-    if (b1 > bcap) atomicOr((unsigned long long*)&ctr[CTR_BOVF], 1ull);
-    for (int64_t q = b0; q < b1 && q < bcap; ++q) bcell[q] = (int32_t)(o + i);
-  }
+  for (int i = threadIdx.x; i < cnt; i += TNP_BLOCK)
+    gather_pair_cell(area + i, o + i, po, lcell, lent, ln, lpoff, pcell, pent, pn, ptoff, bcell, bcap, chunk,
+                     ctr, false);
 }
 
 }  // namespace
@@ -599,22 +637,24 @@ int launch_bucket_pairs(int n_marks, const int64_t* bbase, const uint64_t* ekv, 
   }
   const BGeom G{n_marks + 2, sh, NBd};
   const int fuse = NB <= FUSE_MAX_BLOCKS;
+  const PairLists pl{pcell, pent, pn, ptoff, bcell, bcap, connect_chunk_pairs(), bcount, bcur};
   WinArgs wa{0, 0, 0ull, nullptr, 0};
   if (win) wa = WinArgs{win->idx, win->nb, win->fmask, win->keys, win->cap};
   if (sh == 3)
     hipLaunchKernelGGL(k_bucket_group<3>, dim3(NB), dim3(TNP_BLOCK), 0, s, G, bbase, ekv,
                        reinterpret_cast<const ulonglong2*>(pz), ents, lcell, lent, ln, lpoff, bnpc, bnpairs,
-                       bspairs, pcoff, pairoff, spoff, fuse, wa, ctr);
+                       bspairs, pcoff, pairoff, spoff, fuse, wa, pl, ctr);
   else
     hipLaunchKernelGGL(k_bucket_group<4>, dim3(NB), dim3(TNP_BLOCK), 0, s, G, bbase, ekv,
                        reinterpret_cast<const ulonglong2*>(pz), ents, lcell, lent, ln, lpoff, bnpc, bnpairs,
-                       bspairs, pcoff, pairoff, spoff, fuse, wa, ctr);
+                       bspairs, pcoff, pairoff, spoff, fuse, wa, pl, ctr);
   if (!fuse)
     hipLaunchKernelGGL(k_scan_sets, dim3(1, 3), dim3(TNP_BLOCK), 0, s, ScanSet{bnpc, 1, pcoff, CTR_R},
                        ScanSet{bnpairs, 1, pairoff, CTR_TESTS}, ScanSet{bspairs, 1, spoff, CTR_SPAIRS}, NB,
                        nullptr, (int64_t)0, 0, ctr);
-  hipLaunchKernelGGL(k_pair_gather, dim3(NB), dim3(TNP_BLOCK), 0, s, bbase, bnpc, pcoff, pairoff, lcell, lent,
-                     ln, lpoff, pcell, pent, pn, ptoff, bcell, bcap, connect_chunk_pairs(), bcount, bcur, ctr);
+  if (!fuse)
+    hipLaunchKernelGGL(k_pair_gather, dim3(NB), dim3(TNP_BLOCK), 0, s, bbase, bnpc, pcoff, pairoff, lcell, lent,
+                       ln, lpoff, pcell, pent, pn, ptoff, bcell, bcap, connect_chunk_pairs(), bcount, bcur, ctr);
   TNP_CHECK(hipGetLastError());
   return 0;
 }

@@ -953,7 +953,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     if (buf_ensure(e->sents, TB * sizeof(uint64_t), s)) return -1;
     // a pruning step recomputes the live flags: zeroed by the bucket count
     // (after the hit pass read them), re-marked by the prune
-    if (prune && buf_ensure(e->live, std::max<int64_t>(NV, 16), s)) return -1;
+    if (prune && buf_ensure(e->live, std::max<int64_t>(NV + 4, 16), s)) return -1;
     NewOverride nov{override_, P<uint64_t>(e->shared), P<float>(c.pre), c.cap, e->valid_from, pos, zero,
                     P<uint64_t>(c.pz)};
     TIMED("bucket_entries", 16.0 * M,  // + 8 B per entry, set once T is known
@@ -1136,8 +1136,11 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   if (prune) {
     // live flags recomputed from the kept edges; no vertex moves (lazy
     // compaction): the distinct flagged count is the reference's V'
-    if (buf_ensure(e->live, std::max<int64_t>(NV, 16), s)) return -1;
+    if (buf_ensure(e->live, std::max<int64_t>(NV + 4, 16), s)) return -1;  // +4: word atomics
     if (!buckets) TNP_CHECK(hipMemsetAsync(e->live.p, 0, NV, s));  // else zeroed by the bucket count
+    // (word-atomic live counting inside the prune measured slower than the
+    // counting pass even at bunny scale: 0.25 vs 0.13 + 0.07 ms per subpoly)
+    const bool count_in_prune = false;
     if (ensure_masks(e, s)) return -1;  // (curve path: recomputed after the rewiring)
     const int64_t N1 = std::max<int64_t>(N, 1);
     if (buf_ensure(e->edm_alt, N1 * sizeof(uint8_t), s)) return -1;
@@ -1150,10 +1153,11 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
           launch_prune_lb(eg, E, P<int32_t>(e->sb), S, V, e->ckeys, nb, X, idx, K - 1,
                           P<uint64_t>(c.pz), P<uint8_t>(e->edm), P<uint64_t>(e->esm),
                           P<int32_t>(e->edges_alt), P<uint8_t>(e->edm_alt), P<uint64_t>(e->esm_alt),
-                          P<uint8_t>(e->live), ctr, lb, s));
+                          P<uint8_t>(e->live), count_in_prune, ctr, lb, s));
     std::swap(e->edm, e->edm_alt);
     std::swap(e->esm, e->esm_alt);
-    TIMED("count_live", 1.0 * NV, launch_count_flags(P<uint8_t>(e->live), NV, ctr, CTR_V, s));
+    if (!count_in_prune)
+      TIMED("count_live", 1.0 * NV, launch_count_flags(P<uint8_t>(e->live), NV, ctr, CTR_V, s));
     next_valid = e->keep_all ? 0 : std::min(idx + 1, K - 1);
     if (read_ctr(e, s)) return -1;
     ktimer_set_bytes(e, "prune", 17.0 * E + 36.0 * S + 40.0 * X + 19.0 * e->h_ctr[CTR_E]);

@@ -157,8 +157,10 @@ int launch_connect(const int64_t* ptoff, const int32_t* pcell, const int32_t* pn
 int launch_prune_lb(const int32_t* edges, int64_t E, const int32_t* sb, int64_t S, int64_t V,
                     const uint64_t* ckeys, int nb, int64_t X, int idx, int last_plane,
                     const uint64_t* pz, const uint8_t* dm, const uint64_t* sm, int32_t* out,
-                    uint8_t* odm, uint64_t* osm, uint8_t* used, int64_t* ctr, const TnpLB& lb,
-                    hipStream_t s);
+                    uint8_t* odm, uint64_t* osm, uint8_t* used, bool count_live, int64_t* ctr,
+                    const TnpLB& lb, hipStream_t s);
+// count_live: the distinct live endpoints are counted into ctr[CTR_V] on the
+// way (word atomics; for small complexes, instead of launch_count_flags)
 // ctr[slot] += number of set byte flags in f[0, n) (16-B aligned f, 0/1 bytes)
 int launch_count_flags(const uint8_t* f, int64_t n, int64_t* ctr, int slot, hipStream_t s);
 // the counter block -> a host-mapped mirror, then the sequence word at [31]

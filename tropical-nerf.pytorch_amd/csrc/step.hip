@@ -790,8 +790,8 @@ __global__ void __launch_bounds__(TNP_BLOCK, 4)
 k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, int idx, uint64_t amask,
            const ulonglong2* __restrict__ pz, const uint8_t* __restrict__ dm,
            const uint64_t* __restrict__ sm, int32_t* __restrict__ out, uint8_t* __restrict__ odm,
-           uint64_t* __restrict__ osm, uint8_t* __restrict__ used, int64_t* __restrict__ ctr,
-           TnpLB lb) {
+           uint64_t* __restrict__ osm, uint8_t* __restrict__ used, int count_live,
+           int64_t* __restrict__ ctr, TnpLB lb) {
   __shared__ int cnt[LIPT][TNP_WAVES];
   __shared__ int64_t slot;
   __shared__ uint64_t acts[TNP_WAVES];
@@ -875,6 +875,7 @@ k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, int idx, uint64_t amask,
     for (int w = 0; w < TNP_WAVES; ++w) agg += cnt[k][w];
   const int64_t prefix = tnp::lb_prefix(lb, tile, agg, &slot);
   int64_t run = prefix;
+  int newly = 0;  // count_live: endpoints this thread marked live first
 #pragma unroll
   for (int k = 0; k < LIPT; ++k) {
     int64_t off = run;
@@ -890,10 +891,26 @@ k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, int idx, uint64_t amask,
       reinterpret_cast<int2*>(out)[o] = make_int2(a[k], b[k]);
       odm[o] = (uint8_t)d[k];
       osm[o] = m[k];
-      used[a[k]] = 1;
-      used[b[k]] = 1;
+      if (count_live) {
+        // small complexes: the distinct live count without a counting pass
+        // (a word-wide atomic OR tells who set each byte first)
+        unsigned* w4 = reinterpret_cast<unsigned*>(used);
+        const int ab[2] = {a[k], b[k]};
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const unsigned sh = 8u * (unsigned)(ab[q] & 3);
+          newly += ((atomicOr(w4 + (ab[q] >> 2), 1u << sh) >> sh) & 0xFFu) == 0u;
+        }
+      } else {
+        used[a[k]] = 1;
+        used[b[k]] = 1;
+      }
     }
     run += tot;
+  }
+  if (count_live) {
+    const int wn = tnp::wave_sum(newly);
+    if (tnp::lane() == 0 && wn) atomicAdd((unsigned long long*)&ctr[CTR_V], (unsigned long long)wn);
   }
   if (tile == ntiles - 1 && threadIdx.x == 0) ctr[CTR_E] = prefix + agg;
   act = tnp::wave_or(act);
@@ -1206,8 +1223,8 @@ int launch_prune(bool emit, const int32_t* edges, int64_t E, const int32_t* sb, 
 int launch_prune_lb(const int32_t* edges, int64_t E, const int32_t* sb, int64_t S, int64_t V,
                     const uint64_t* ckeys, int nb, int64_t X, int idx, int last_plane,
                     const uint64_t* pz, const uint8_t* dm, const uint64_t* sm, int32_t* out,
-                    uint8_t* odm, uint64_t* osm, uint8_t* used, int64_t* ctr, const TnpLB& lb,
-                    hipStream_t s) {
+                    uint8_t* odm, uint64_t* osm, uint8_t* used, bool count_live, int64_t* ctr,
+                    const TnpLB& lb, hipStream_t s) {
   EdgeSrc src{edges, E, sb, S, V, ckeys, nb, X};
   const int64_t N = E + S + X;
   if (N <= 0) {
@@ -1220,8 +1237,8 @@ int launch_prune_lb(const int32_t* edges, int64_t E, const int32_t* sb, int64_t 
   const int64_t tiles = lb_tiles(N);
   (void)fmask;
   hipLaunchKernelGGL(k_prune_lb, dim3((unsigned)tiles), dim3(TNP_BLOCK), 0, s, src, N, tiles, idx,
-                     amask, reinterpret_cast<const ulonglong2*>(pz), dm, sm, out, odm, osm, used, ctr,
-                     lb);
+                     amask, reinterpret_cast<const ulonglong2*>(pz), dm, sm, out, odm, osm, used,
+                     count_live ? 1 : 0, ctr, lb);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
