@@ -126,15 +126,28 @@ class Collective:
     decisions, subpoly.py:110 and subpoly_debug.py:43-49): ONE all_gather of
     each rank's few int64 words (RCCL over xGMI, or gloo on the host), reduced
     on the host -- OR for the 64-bit plane masks (RCCL has no bitwise-or
-    reduction), MAX for {split count, failover flag}; one readback."""
+    reduction), MAX for {split count, failover flag}; one readback.  When
+    every rank is on this node the words go through host shared memory
+    instead (ShmCollective: no library call, no device copies)."""
 
-    def __init__(self, device):
+    def __init__(self, device, shm: bool = None):
         import torch.distributed as dist
         self.dist = dist
         self.device = device
         self.world = dist.get_world_size()
+        # every rank on this node (torchrun's LOCAL_WORLD_SIZE): the words go
+        # through host shared memory instead (tropical.distributed.ShmCollective)
+        if shm is None:
+            shm = (os.environ.get("TNP_SHM_COLLECTIVE", "1") == "1" and
+                   int(os.environ.get("LOCAL_WORLD_SIZE", "-1")) == self.world)
+        self.shm = None
+        if shm:
+            from tropical.distributed import ShmCollective
+            self.shm = ShmCollective()
 
     def __call__(self, vec: np.ndarray, op: str):
+        if self.shm is not None:
+            return self.shm(vec, op)
         words = np.ascontiguousarray(vec.astype(np.uint64 if op == "or" else np.int64)).view(np.int64)
         t = torch.from_numpy(words.copy()).to(self.device)
         out = torch.empty(self.world * t.numel(), dtype=torch.int64, device=self.device)

@@ -211,15 +211,21 @@ int tnp_engine_kernel_timer(tnp_engine* eng, int on, void* stream, int32_t* n_ke
 int tnp_engine_kernel_stat(tnp_engine* eng, int i, char* name, int cap, double* ms,
                            int64_t* launches, double* bytes);
 
-/* Self-check of the fp32 primitives the bitwise contract relies on:
- * out[8i..8i+7] = sqrt_rn(a), a/b (rn), fma(a,b,c), a*b, a+b, sqrtf(a),
- * a/b (default), tanhf(a). */
-int tnp_debug_ops(const float* d_a, const float* d_b, const float* d_c, int64_t n,
-                  float* d_out, void* stream);
-
-/* Debug: padded angular scores (F x width fp32) of the last faces call. */
-int tnp_engine_faces_debug(tnp_engine* eng, float* d_scores, int64_t cap, int64_t* F,
-                           int64_t* width, void* stream);
+/* ---- single-node rank agreements (bench.py / tropical/distributed.py) ----
+ * The per-step global decisions of the sharded loop (subpoly.py:110 "does
+ * anything split", subpoly_debug.py:43-49 the failover override, and the OR
+ * of the ranks' next-active plane masks) between the processes of ONE node
+ * through a POSIX shared-memory segment: every rank writes <= 8 int64 words,
+ * arrives on an atomic counter and spins until all have (no library
+ * collective, no device copies).  Rank 0 creates the segment (create=1)
+ * before the others open it; it can be unlinked once all have.  allreduce
+ * op: TNP_SHM_MAX, TNP_SHM_OR (bitwise, 64-bit masks) or TNP_SHM_SUM. */
+typedef struct tnp_shm tnp_shm;
+enum { TNP_SHM_MAX = 0, TNP_SHM_OR = 1, TNP_SHM_SUM = 2 };
+int tnp_shm_open(const char* name, int rank, int world, int create, tnp_shm** out);
+int tnp_shm_unlink(const char* name);
+void tnp_shm_close(tnp_shm* shm);
+int tnp_shm_allreduce(tnp_shm* shm, const int64_t* in, int n, int op, int64_t* out);
 
 /* ---- `-e` evaluation stack (train.py:275-354; csrc/evaluate.hip) ------- */
 

@@ -1,18 +1,21 @@
 """CPU: the C-ABI library builds, loads and exports exactly what
-include/tropical_hip.h declares (no compute calls without a GPU)."""
+include/*.h declare -- the product surface tropical_hip.h and the
+diagnostics tropical_hip_debug.h (no compute calls without a GPU)."""
 import os
 import re
 
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(ROOT, "include", "tropical_hip.h")
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("tropical_hip.h", "tropical_hip_debug.h")]
 
 
-def declared_symbols():
-    src = open(HEADER).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(tnp_[a-z0-9_]+)\s*\(", src)))
+def declared_symbols(headers=HEADERS):
+    syms = set()
+    for h in headers:
+        src = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        syms |= set(re.findall(r"\b(tnp_[a-z0-9_]+)\s*\(", src))
+    return sorted(syms)
 
 
 def test_header_declares_engine_and_net_ops():
@@ -20,6 +23,13 @@ def test_header_declares_engine_and_net_ops():
     for s in ("tnp_forward", "tnp_region", "tnp_sdf_grad", "tnp_engine_split",
               "tnp_engine_finish", "tnp_engine_skeleton", "tnp_engine_faces"):
         assert s in syms
+
+
+def test_debug_entry_points_stay_out_of_the_product_header():
+    product = declared_symbols(HEADERS[:1])
+    debug = declared_symbols(HEADERS[1:])
+    assert debug and not set(debug) & set(product)
+    assert all("debug" in s for s in debug)
 
 
 def test_library_exports_every_declared_symbol():

@@ -194,3 +194,36 @@ def test_slab_restrict_matches_slab_lattice():
         # the lattice slab orders x-edges, then y, then z: the same subsequence
         assert sorted(map(tuple, e.tolist())) == sorted(map(tuple, se.tolist()))
         assert e.shape[0] == se.shape[0]
+
+
+def _shm_worker(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        shm = bench.Collective(torch.device("cpu"), shm=True)
+        ref = bench.Collective(torch.device("cpu"), shm=False)
+        rs = np.random.RandomState(rank)
+        bad = []
+        for it in range(200):  # many calls: both banks reused, ranks racing
+            v = rs.randint(-2**40, 2**40, size=3).astype(np.int64)
+            m = np.array([rs.randint(0, 2**62) | (1 << (rank + it % 7))], dtype=np.uint64)
+            for vec, op in ((v, "max"), (m, "or")):
+                a, b = shm(vec, op), ref(vec, op)
+                if not np.array_equal(a, b) or a.dtype != vec.dtype:
+                    bad.append((it, op, a.tolist(), b.tolist()))
+        shm.shm.close()
+        with open(os.path.join(outdir, f"shm{rank}.txt"), "w") as f:
+            f.write(repr(bad))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_shm_collective_matches_the_library_collective(tmp_path, world):
+    """tnp_shm_allreduce (host shared memory, one node) returns what the
+    all_gather + host reduction returns, over 400 racing calls per rank."""
+    mp.spawn(_shm_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
+        assert (tmp_path / f"shm{r}.txt").read_text() == "[]"

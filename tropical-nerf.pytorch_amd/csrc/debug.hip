@@ -2,6 +2,7 @@
 // exactly like IEEE-754 / the host (tests/test_gpu_parity.py::test_fp32_ops).
 #include "common.h"
 #include "kernels.h"
+#include "../../include/tropical_hip_debug.h"
 
 namespace {
 __global__ void k_ops(const float* a, const float* b, const float* c, int64_t n, float* o) {

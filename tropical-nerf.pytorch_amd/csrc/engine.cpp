@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "../../include/tropical_hip.h"
+#include "../../include/tropical_hip_debug.h"
 #include "common.h"
 #include "kernels.h"
 #include "step.h"

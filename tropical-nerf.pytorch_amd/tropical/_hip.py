@@ -62,6 +62,10 @@ SIGNATURES = {
     "tnp_engine_set_net": (C.c_int, [_VP, _NETP]),
     "tnp_engine_load": (C.c_int, [_VP, _VP, _I64, _VP, _I64, _VP, C.c_int, _VP]),
     "tnp_engine_skeleton": (C.c_int, [_VP, C.c_int, _F, _VP, _P64, _P64]),
+    "tnp_shm_open": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int, C.POINTER(_VP)]),
+    "tnp_shm_unlink": (C.c_int, [C.c_char_p]),
+    "tnp_shm_close": (None, [_VP]),
+    "tnp_shm_allreduce": (C.c_int, [_VP, _VP, C.c_int, C.c_int, _VP]),
     "tnp_engine_skeleton_mode": (C.c_int, [_VP, C.c_int, _F, C.c_int, _VP, _P64, _P64]),
     "tnp_engine_lattice": (C.c_int, [_VP, C.c_int, C.c_int, C.c_int, _VP, _P64, _P64]),
     "tnp_engine_active_planes": (C.c_int, [_VP, C.c_int, _PU64, _VP]),

@@ -48,9 +48,59 @@ keeps its slab plus halo (slab_restrict) -- subpoly_sharded().
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 import torch.distributed as dist
 from torch import Tensor
+
+
+class ShmCollective:
+    """The per-step agreements (run_steps' ``allreduce(vec, op)``) between
+    the ranks of ONE node through host shared memory (csrc/shm.cpp,
+    tnp_shm_*): every rank writes its <= 8 words and spins on one atomic
+    counter -- no library collective, no device copies.  Same results as an
+    all_gather + host reduction: "max" (int64), "or" (64-bit masks), "sum"."""
+
+    OPS = {"max": 0, "or": 1, "sum": 2}
+
+    def __init__(self, group=None):
+        import ctypes as C
+        import os
+        import secrets
+        from . import _hip
+        self._C, self._lib = C, _hip.lib()
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        name = [f"/tnp_{os.getpid()}_{secrets.token_hex(6)}" if rank == 0 else None]
+        dist.broadcast_object_list(name, src=dist.get_global_rank(group, 0) if group else 0, group=group)
+        self.name = name[0].encode()
+        h = C.c_void_p()
+        if rank == 0:
+            _hip.check(self._lib.tnp_shm_open(self.name, rank, world, 1, C.byref(h)), "tnp_shm_open")
+        dist.barrier(group=group)
+        if rank != 0:
+            _hip.check(self._lib.tnp_shm_open(self.name, rank, world, 0, C.byref(h)), "tnp_shm_open")
+        dist.barrier(group=group)
+        if rank == 0:
+            self._lib.tnp_shm_unlink(self.name)  # the mappings stay; nothing left in /dev/shm
+        self.h = h
+        self._in = np.zeros(8, dtype=np.int64)
+        self._out = np.zeros(8, dtype=np.int64)
+
+    def __call__(self, vec, op: str):
+        from . import _hip
+        vec = np.asarray(vec)
+        n = vec.size
+        words = np.ascontiguousarray(vec.astype(np.uint64 if op == "or" else np.int64)).view(np.int64)
+        self._in[:n] = words
+        _hip.check(self._lib.tnp_shm_allreduce(self.h, self._in.ctypes.data, n, self.OPS[op],
+                                               self._out.ctypes.data), "tnp_shm_allreduce")
+        res = self._out[:n].copy()
+        return res.view(np.uint64).astype(vec.dtype) if op == "or" else res
+
+    def close(self):
+        if self.h:
+            self._lib.tnp_shm_close(self.h)
+            self.h = None
 
 
 def slab_cuts(n_marks: int, world: int) -> list:
