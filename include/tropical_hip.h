@@ -227,6 +227,30 @@ int tnp_shm_unlink(const char* name);
 void tnp_shm_close(tnp_shm* shm);
 int tnp_shm_allreduce(tnp_shm* shm, const int64_t* in, int n, int op, int64_t* out);
 
+/* ---- SDF training (train.py:169-224, dataset.py:80-96; csrc/train.hip) --
+ * Gradient of one batch's loss (train.py:181-201) for the n points d_x
+ * (n x 3 in [-1, 1]^3) with target distances d_gt (n):
+ *   L = mean |clamp(sdf(x)) - clamp(gt)| + eik_w (||J||_F - 1)^2 / n,
+ * clamp to [-clamp_t, clamp_t], sdf = tanh(o1 - o0) (model.py:84-87),
+ * J = d sdf / d x (n x 3) -- the L1 and eikonal terms; the weight-norm term
+ * (train.py:200-201) involves only the fc weights and is the caller's.  The
+ * eikonal term's parameter gradient (the reference's double backward) is
+ * written out in closed form.  ACCUMULATES into d_grad_table (the table's
+ * own layout, params[(offset_l + idx) * 2 + f]) and d_grad_weights (the
+ * packed weight layout of tnp_net); d_stats (2 doubles, device, zeroed by
+ * the call) receives sum |clamp(sdf) - clamp(gt)| and sum ||J_i||^2.  Float
+ * atomics: the summation order is not fixed.  3-layer nets, 16 hidden. */
+int tnp_sdf_train_grad(const tnp_net* net, const float* d_x, const float* d_gt, int64_t n, float clamp_t,
+                       float eik_w, float* d_grad_table, float* d_grad_weights, double* d_stats, void* stream);
+
+/* Signed distance of n points d_p (n x 3) to a closed triangle mesh (d_V
+ * nV x 3 fp32, d_F nF x 3 int32, indices in [0, nV)): replaces
+ * cubvh.cuBVH(V, F).signed_distance (dataset.py:77, 92).  Exact distance to
+ * the closest triangle; the sign from the generalized winding number,
+ * positive inside (dataset.py:96).  d_work: 2 n floats of scratch. */
+int tnp_mesh_signed_distance(const float* d_V, int64_t nV, const int32_t* d_F, int64_t nF, const float* d_p,
+                             int64_t n, float* d_work, float* d_dist, void* stream);
+
 /* ---- `-e` evaluation stack (train.py:275-354; csrc/evaluate.hip) ------- */
 
 /* Marching cubes over vol[n0][n1][n2] (x slowest), inside = value < iso,

@@ -76,6 +76,19 @@ def _slab_worker(rank, world, port, outdir, cuts):
         dist.destroy_process_group()
 
 
+@pytest.fixture(scope="module")
+def whole():
+    """The unsharded complex of CASE (oracle), computed once for the module."""
+    import oracle.subdivide as od
+    from tropical.synthetic import lattice_edges, lattice_vertices
+    d = load(CASE)
+    net = oracle_net(d)
+    with torch.no_grad():
+        V, E, _ = od.run_steps(torch.from_numpy(lattice_vertices(d["marks"])),
+                               torch.from_numpy(lattice_edges(int(d["lattice_n"]))), net, 1e-4)
+    return V, E
+
+
 def test_slab_cuts_cover_the_lattice():
     from tropical.distributed import slab_cuts, slab_marks
     for G, world in ((128, 1), (161, 2), (203, 4), (256, 8)):
@@ -99,17 +112,11 @@ def test_owner_rule_matches_cells_and_planes():
 
 @pytest.mark.slow
 @pytest.mark.parametrize("world", [2, 3])
-def test_gloo_ranks_reproduce_the_unsharded_complex(tmp_path, world):
-    import oracle.subdivide as od
-    from tropical.synthetic import lattice_edges, lattice_vertices
+def test_gloo_ranks_reproduce_the_unsharded_complex(tmp_path, world, whole):
     mp.spawn(_slab_worker, args=(world, _free_port(), str(tmp_path), CUTS[world]), nprocs=world,
              join=True)
     d = load(CASE)
-    net = oracle_net(d)
-    n = int(d["lattice_n"])
-    with torch.no_grad():
-        V, E, _ = od.run_steps(torch.from_numpy(lattice_vertices(d["marks"])),
-                               torch.from_numpy(lattice_edges(n)), net, 1e-4)
+    V, E = whole
     assert (V.shape[0], E.shape[0]) == tuple(d["pre_VE"])
     whole_v, whole_e = _canon(V.numpy(), E.numpy())
     # stitched: one global numbering, no vertex or edge twice, same complex
@@ -149,14 +156,8 @@ def _halo_worker(rank, world, port, outdir, corrupt):
 
 
 @pytest.mark.parametrize("corrupt", [False, True])
-def test_halo_check_detects_a_missing_edge(tmp_path, corrupt):
-    import oracle.subdivide as od
-    from tropical.synthetic import lattice_edges, lattice_vertices
-    d = load(CASE)
-    net = oracle_net(d)
-    with torch.no_grad():
-        V, E, _ = od.run_steps(torch.from_numpy(lattice_vertices(d["marks"])),
-                               torch.from_numpy(lattice_edges(int(d["lattice_n"]))), net, 1e-4)
+def test_halo_check_detects_a_missing_edge(tmp_path, corrupt, whole):
+    V, E = whole
     np.savez(tmp_path / "whole.npz", V=V.numpy(), E=E.numpy())
     mp.spawn(_halo_worker, args=(2, _free_port(), str(tmp_path), corrupt), nprocs=2, join=True)
     res = [(tmp_path / f"r{r}.txt").read_text() for r in range(2)]

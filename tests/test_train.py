@@ -1,0 +1,191 @@
+"""SDF training (reference tropical/stanford/train.py:153-231,
+dataset.py:25-99).
+
+CPU: the PLY reader on the layouts the scans come in, the oracle's
+double-backward gradients against finite differences, the oracle's signed
+distance against a sphere.  GPU: the closed-form batch gradient
+(tnp_sdf_train_grad) against the oracle's autograd double backward, the mesh
+signed distance kernel against the oracle, and the `train` entry point
+training a net on a sphere mesh end to end.  tcnn and cubvh are absent, so
+parity with their arithmetic is unpinned; the tolerances below are the fp32
+kernel against the float64 oracle (float atomics: the summation order is
+free)."""
+import numpy as np
+import pytest
+import torch
+
+
+def icosphere(level: int = 3, r: float = 1.0):
+    """Closed, outward-oriented sphere mesh (icosahedron, `level` 4:1 splits)."""
+    t = (1 + 5 ** 0.5) / 2
+    V = [(-1, t, 0), (1, t, 0), (-1, -t, 0), (1, -t, 0), (0, -1, t), (0, 1, t), (0, -1, -t), (0, 1, -t),
+         (t, 0, -1), (t, 0, 1), (-t, 0, -1), (-t, 0, 1)]
+    F = [(0, 11, 5), (0, 5, 1), (0, 1, 7), (0, 7, 10), (0, 10, 11), (1, 5, 9), (5, 11, 4), (11, 10, 2),
+         (10, 7, 6), (7, 1, 8), (3, 9, 4), (3, 4, 2), (3, 2, 6), (3, 6, 8), (3, 8, 9), (4, 9, 5),
+         (2, 4, 11), (6, 2, 10), (8, 6, 7), (9, 8, 1)]
+    V = [np.array(v, dtype=np.float64) / np.linalg.norm(v) for v in V]
+    for _ in range(level):
+        mid = {}
+
+        def m(a, b):
+            k = (min(a, b), max(a, b))
+            if k not in mid:
+                p = V[a] + V[b]
+                V.append(p / np.linalg.norm(p))
+                mid[k] = len(V) - 1
+            return mid[k]
+        F = [f for a, b, c in F for f in ((a, m(a, b), m(c, a)), (b, m(b, c), m(a, b)),
+                                           (c, m(c, a), m(b, c)), (m(a, b), m(b, c), m(c, a)))]
+    return np.array(V) * r, np.array(F, dtype=np.int64)
+
+
+def _small_net(levels=4, r_min=2, r_max=32, T=19, seed=0, amp=0.1):
+    from tropical.stanford.model import Net
+    torch.manual_seed(seed)
+    net = Net(num_layers=3, num_hidden=16, levels=levels, r_min=r_min, r_max=r_max, T=T)
+    with torch.no_grad():
+        net.enc.module.params.uniform_(-amp, amp)
+    return net
+
+
+# ---------------------------------------------------------------- CPU -----
+
+def test_ply_reader_layouts(tmp_path):
+    from tropical.utils.mesh import load_ply
+    # ascii, extra vertex property, a quad (fan-triangulated)
+    (tmp_path / "a.ply").write_text(
+        "ply\nformat ascii 1.0\ncomment scan\nelement vertex 4\nproperty float x\nproperty float y\n"
+        "property float z\nproperty float confidence\nelement face 1\nproperty list uchar int vertex_indices\n"
+        "end_header\n0 0 0 1\n1 0 0 .5\n1 1 0 1\n0 1 0 1\n4 0 1 2 3\n")
+    m = load_ply(str(tmp_path / "a.ply"))
+    assert m.vertices.tolist() == [[0, 0, 0], [1, 0, 0], [1, 1, 0], [0, 1, 0]]
+    assert m.faces.tolist() == [[0, 1, 2], [0, 2, 3]]
+    # binary big endian, double coordinates, extra properties, int counts
+    V = np.array([[0, 0, 0], [1, 0, 0], [0, 1, 0], [0, 0, 1]], dtype=np.float64)
+    F = [[0, 2, 1], [0, 1, 3], [1, 2, 3], [0, 3, 2]]
+    head = ("ply\nformat binary_big_endian 1.0\nelement vertex 4\nproperty double x\nproperty double y\n"
+            "property double z\nproperty uchar intensity\nelement face 4\n"
+            "property list int uint vertex_indices\nend_header\n").encode()
+    body = b"".join(v.astype(">f8").tobytes() + b"\x07" for v in V)
+    body += b"".join(np.array([3] + f, dtype=">u4").tobytes() for f in F)
+    (tmp_path / "b.ply").write_bytes(head + body)
+    m = load_ply(str(tmp_path / "b.ply"))
+    assert np.array_equal(m.vertices, V) and m.faces.tolist() == F
+
+
+def test_oracle_gradients_match_finite_differences():
+    """The oracle's double backward (the reference's create_graph=True path)
+    against central differences of its own loss, float64."""
+    from oracle.encoding import level_meta
+    from oracle.train import train_loss_grads
+    g = torch.Generator().manual_seed(3)
+    meta = level_meta(2, 2, 4.0, 12)
+    n_par = meta[-1] * 2
+    table = (torch.rand(n_par, generator=g, dtype=torch.float64) * 2 - 1) * 0.3
+    shapes = [(16, 4), (16,), (16, 16), (16,), (2, 16), (2,)]
+    ws = [(torch.rand(s, generator=g, dtype=torch.float64) * 2 - 1) * 0.6 for s in shapes]
+    x = (torch.rand(24, 3, generator=g, dtype=torch.float64) * 2 - 1) * 0.9
+    gt = (torch.rand(24, generator=g, dtype=torch.float64) * 2 - 1) * 0.5
+
+    def loss(tab, w):
+        l1, eik, _ = train_loss_grads(tab, w, meta, x, gt)
+        return float(l1 + eik)
+
+    _, _, grads = train_loss_grads(table, ws, meta, x, gt)
+    h = 1e-6
+    # the table entries with the largest gradient, and a few weights
+    top = torch.argsort(grads[0].abs(), descending=True)[:6]
+    for k in top.tolist():
+        tp, tm = table.clone(), table.clone()
+        tp[k] += h
+        tm[k] -= h
+        fd = (loss(tp, ws) - loss(tm, ws)) / (2 * h)
+        assert abs(fd - float(grads[0][k])) <= 1e-5 * max(1.0, abs(fd)), (k, fd, float(grads[0][k]))
+    for wi, idx in ((0, (3, 1)), (2, (5, 7)), (4, (1, 2)), (3, (4,)), (5, (1,))):
+        wp = [w.clone() for w in ws]
+        wm = [w.clone() for w in ws]
+        wp[wi][idx] += h
+        wm[wi][idx] -= h
+        fd = (loss(table, wp) - loss(table, wm)) / (2 * h)
+        assert abs(fd - float(grads[1 + wi][idx])) <= 1e-5 * max(1.0, abs(fd)), (wi, idx, fd)
+
+
+def test_oracle_signed_distance_on_a_sphere():
+    from oracle.train import signed_distance
+    V, F = icosphere(3)
+    rng = np.random.default_rng(0)
+    P = rng.uniform(-1.4, 1.4, (300, 3))
+    d, w = signed_distance(V, F, P)
+    r = np.linalg.norm(P, axis=1)
+    inside = r < 0.985  # the icosphere's faces sit at most ~1.3% inside the unit sphere
+    outside = r > 1.0
+    assert (d[inside] > 0).all() and (d[outside] < 0).all()
+    assert np.allclose(np.abs(w[inside]), 1, atol=1e-6) and np.allclose(w[outside], 0, atol=1e-6)
+    assert np.abs(np.abs(d) - np.abs(r - 1)).max() < 0.02
+
+
+# ---------------------------------------------------------------- GPU -----
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [dict(levels=4, r_min=2, r_max=32, T=19),     # small: dense levels
+                                 dict(levels=4, r_min=8, r_max=128, T=14)])   # hashed levels
+def test_train_grads_match_oracle(cuda, cfg):
+    from oracle.train import train_loss_grads
+    from tropical.stanford.sdf_train import EIK_W, SDFTrainer
+    net = _small_net(**cfg).to(cuda)
+    g = torch.Generator().manual_seed(1)
+    n = 777
+    x = (torch.rand(n, 3, generator=g) * 2 - 1) * 0.95
+    gt = (torch.rand(n, generator=g) * 2 - 1) * 0.3
+    tr = SDFTrainer(net)
+    l1, eik = tr.data_grads(x.to(cuda), gt.to(cuda))
+    ws = [t.detach().cpu() for lin in net.fc for t in (lin.weight, lin.bias)]
+    rl1, reik, ref = train_loss_grads(net.enc.module.params.detach().cpu(), ws, net.enc.meta, x, gt,
+                                      eik_w=EIK_W)
+    assert abs(float(l1) - float(rl1)) <= 1e-5 * max(1.0, float(rl1))
+    assert abs(float(eik) - float(reik)) <= 1e-4 * max(1e-3, float(reik))
+    got = [tr.g_table.cpu()]
+    off = 0
+    for t in ws:
+        got.append(tr.g_w[off:off + t.numel()].view_as(t).cpu())
+        off += t.numel()
+    for name, a, b in zip(["table", "W0", "b0", "W1", "b1", "W2", "b2"], got, ref):
+        scale = float(b.abs().max())
+        err = float((a.double() - b).abs().max())
+        assert err <= 2e-4 * scale + 1e-9, (name, err, scale)
+
+
+@pytest.mark.gpu
+def test_mesh_signed_distance_matches_oracle(cuda):
+    from oracle.train import signed_distance
+    from tropical.stanford.sdf_train import mesh_signed_distance
+    V, F = icosphere(2, r=0.7)
+    V = V + np.array([0.05, -0.1, 0.02])
+    rng = np.random.default_rng(1)
+    P = rng.uniform(-1.1, 1.1, (3000, 3)).astype(np.float32)
+    ref, wind = signed_distance(V, F, P)
+    got = mesh_signed_distance(torch.tensor(V, dtype=torch.float32, device=cuda),
+                               torch.tensor(F, device=cuda), torch.from_numpy(P).to(cuda)).cpu().numpy()
+    assert np.abs(np.abs(got) - np.abs(ref)).max() < 2e-6
+    clear = np.abs(ref) > 1e-4
+    assert (np.sign(got[clear]) == np.sign(ref[clear])).all()
+
+
+@pytest.mark.gpu
+def test_train_entry_point_fits_a_sphere(cuda, tmp_path, capsys):
+    """`train -c --mesh sphere.ply`: the reference's loop on a sphere scan
+    stand-in; the extracted surface must lie on the (normalised) sphere."""
+    from tropical.stanford.train import R, main
+    from tropical.utils.mesh import Mesh, load_ply
+    V, F = icosphere(4, r=0.37)
+    Mesh(V, F).export(str(tmp_path / "sphere.ply"))
+    rc = main(["-d", "bunny", "-c", "--mesh", str(tmp_path / "sphere.ply"), "--out", str(tmp_path / "meshes"),
+               "--epochs", "4"])
+    assert rc == 0
+    out = capsys.readouterr().out
+    assert "Finished training." in out and "[4,    50] lr:" in out and " take " in out
+    losses = [float(l.split("loss: ")[1].split()[0]) for l in out.splitlines() if "loss: " in l]
+    assert losses[-1] < losses[0]
+    m = load_ply(str(tmp_path / "meshes" / "bunny" / "our_mesh_small_45.ply"))
+    r = np.linalg.norm(m.vertices * R, axis=1)  # back to the normalised frame (radius 1)
+    assert len(r) > 100 and abs(np.median(r) - 1.0) < 0.05 and np.percentile(np.abs(r - 1), 95) < 0.12

@@ -590,7 +590,7 @@ int bucket_geometry(int n_marks, int* sh, int* NBd, int* NB) {
   return 0;
 }
 
-int launch_bucket_entries(const int32_t* members, int64_t S, int64_t V, int64_t M, const uint64_t* grid,
+int launch_bucket_entries(const int32_t* members, int64_t S, int64_t V, int64_t M, const uint64_t* keys,
                           const uint64_t* zero, int idx, int n_marks, int32_t* bcount, int32_t* bcur,
                           int64_t* bbase, int64_t* part, uint64_t* ekv, bool clean, uint8_t* live,
                           int64_t nlive, const NewOverride* ovr, int64_t* ctr, hipStream_t s) {
@@ -606,18 +606,25 @@ int launch_bucket_entries(const int32_t* members, int64_t S, int64_t V, int64_t 
   }
   const int64_t per = (int64_t)TNP_BLOCK * BK_IPT;
   const unsigned nblk = (unsigned)std::max<int64_t>((M + per - 1) / per, 1);
-  const int fuse = nblk <= FUSE_MAX_BLOCKS;
+  // the live-flag zeroing rides along: a step with few members still gets
+  // enough workgroups for it (64 B per thread; the extra ones count nothing)
+  unsigned grid = nblk;
+  if (live) {
+    const int64_t nz = ((nlive >> 4) + 4 * TNP_BLOCK - 1) / (4 * TNP_BLOCK);
+    grid = std::max<unsigned>(nblk, (unsigned)std::min<int64_t>(nz, FUSE_MAX_BLOCKS));
+  }
+  const int fuse = grid <= FUSE_MAX_BLOCKS;
   Override ov{0, nullptr, nullptr, 0, 0, nullptr, nullptr, nullptr};
   if (ovr)
     ov = Override{ovr->flag, ovr->shared, ovr->pre, ovr->ld, ovr->keep_from, ovr->pos, ovr->zero,
                   reinterpret_cast<ulonglong2*>(ovr->pz)};
-  hipLaunchKernelGGL(k_bucket_count, dim3(nblk), dim3(TNP_BLOCK), 0, s, members, S, V, M, grid, zero, idx,
+  hipLaunchKernelGGL(k_bucket_count, dim3(grid), dim3(TNP_BLOCK), 0, s, members, S, V, M, keys, zero, idx,
                      G, NB, bcount, part, bbase, live, nlive, fuse, ov, ctr);
   if (!fuse)
     hipLaunchKernelGGL(k_scan_sets, dim3(1, 1), dim3(TNP_BLOCK), 0, s, ScanSet{bcount, 0, bbase, CTR_T},
-                       ScanSet{}, ScanSet{}, NB, part, (int64_t)nblk, (int)CTR_A, ctr);
+                       ScanSet{}, ScanSet{}, NB, part, (int64_t)grid, (int)CTR_A, ctr);
   if (M > 0)
-    hipLaunchKernelGGL(k_bucket_scatter, dim3(nblk), dim3(TNP_BLOCK), 0, s, members, S, V, M, grid, G, NB,
+    hipLaunchKernelGGL(k_bucket_scatter, dim3(nblk), dim3(TNP_BLOCK), 0, s, members, S, V, M, keys, G, NB,
                        bbase, bcur, ekv);
   TNP_CHECK(hipGetLastError());
   return 0;

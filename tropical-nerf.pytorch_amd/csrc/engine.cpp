@@ -525,6 +525,21 @@ extern "C" int tnp_sdf_grad(const tnp_net* n, const float* xyz, int64_t N, float
   return launch_sdf_grad(to_dev(n), xyz, N, sdf, grad, (hipStream_t)stream);
 }
 
+extern "C" int tnp_sdf_train_grad(const tnp_net* n, const float* xyz, const float* gt, int64_t N, float clamp_t,
+                                  float eik_w, float* d_grad_table, float* d_grad_weights, double* d_stats,
+                                  void* stream) {
+  if (check_net(n)) return -1;
+  if (N < 0 || !d_grad_table || !d_grad_weights || !d_stats) { tnp_set_error("sdf_train_grad: bad arguments"); return -1; }
+  return launch_train_grad(to_dev(n), xyz, gt, N, clamp_t, eik_w, d_grad_table, d_grad_weights, d_stats,
+                           (hipStream_t)stream);
+}
+
+extern "C" int tnp_mesh_signed_distance(const float* d_V, int64_t nV, const int32_t* d_F, int64_t nF,
+                                        const float* d_p, int64_t n, float* d_work, float* d_dist, void* stream) {
+  if (n < 0) { tnp_set_error("mesh_signed_distance: n < 0"); return -1; }
+  return launch_mesh_sd(d_V, nV, d_F, nF, d_p, n, d_work, d_dist, (hipStream_t)stream);
+}
+
 static int set_edges_i64(tnp_engine* e, const int64_t* d_edges, int64_t E, hipStream_t s) {
   if (buf_ensure(e->edges, std::max<int64_t>(E, 1) * 2 * sizeof(int32_t), s)) return -1;
   if (E > 0)
@@ -945,7 +960,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     if (buf_ensure(e->bk[4], NB * sizeof(int64_t), s)) return -1;        // pairs
     if (buf_ensure(e->bk[5], (NB + 1) * sizeof(int64_t), s)) return -1;  // pair-cell offsets
     if (buf_ensure(e->bk[6], (NB + 1) * sizeof(int64_t), s)) return -1;  // pair offsets
-    if (buf_ensure(e->bk[7], (M / 2048 + 2) * sizeof(int64_t), s)) return -1;  // block parts
+    if (buf_ensure(e->bk[7], (std::max<int64_t>(M / 2048, 512) + 2) * sizeof(int64_t), s)) return -1;  // block parts
     for (int k = 8; k < 11; ++k)
       if (buf_ensure(e->bk[k], RC * sizeof(int32_t), s)) return -1;  // per-bucket pair-cell areas
     if (buf_ensure(e->bk[11], RC * sizeof(int64_t), s)) return -1;

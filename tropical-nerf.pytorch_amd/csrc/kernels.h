@@ -56,6 +56,13 @@ int launch_encode(const NetDev& net, const float* x01, int64_t n, float* out, hi
 // pre plane-major; writes int64 m[n][3+K] and off[n][3] (Net.region)
 int launch_region(const NetDev& net, const float* xyz, const float* pre, int64_t ld,
                   int64_t n, float eps, int64_t* m, int64_t* off, hipStream_t s);
+// ---- train.hip ----
+// SDF training gradients of one batch (train.py:181-201); stats: 2 doubles
+int launch_train_grad(const NetDev& net, const float* xyz, const float* gt, int64_t n, float clamp_t, float eik_w,
+                      float* g_table, float* g_w, double* stats, hipStream_t s);
+// mesh signed distance (dataset.py:92); work: 2 n floats
+int launch_mesh_sd(const float* V, int64_t nV, const int32_t* F, int64_t nF, const float* P, int64_t n, float* work,
+                   float* out, hipStream_t s);
 int launch_sdf_grad(const NetDev& net, const float* xyz, int64_t n, float* sdf,
                     float* grad, hipStream_t s);
 // packed keys from pre (planes [0,K)) + grid word from coordinates

@@ -14,10 +14,16 @@ runs on the GPU: subpoly on the HIP engine, the SDF grid through the fused
 net kernel, marching cubes, ray casting and nearest neighbours in
 csrc/evaluate.hip.
 
-Not on this path: SDF training, which needs the Stanford scans
-and cubvh signed distances (train.py:164-224, dataset.py) -- without a
-checkpoint the command stops with a message.  Extra flag: --weights PATH
-loads a state_dict from PATH instead of the cache location.
+Without a cached model (or with -c) the net is trained first, as the
+reference's loop (train.py:153-231): StanfordDataset samples (dataset.py,
+signed distances by the HIP mesh kernel), batches of 1000, Adam + cosine
+schedule, one closed-form gradient call per batch (csrc/train.hip), the
+reference's progress lines, one subpoly per 10 batches once past 5 * EPOCH
+of them, the state_dict saved to the cache path.  The Stanford scans are not
+part of this repository: pass --mesh PATH (any closed PLY mesh) when the
+dataset's own file is absent.  Extra flags: --weights PATH loads a
+state_dict from PATH instead of the cache location; --epochs overrides
+EPOCH (train.py:67).
 """
 from __future__ import annotations
 
@@ -56,6 +62,8 @@ def parse_args(argv=None):
     p.add_argument("-f", "--force", default=True, action="store_false",
                    help="Force flat assumption to skip curve approximation.")
     p.add_argument("--weights", default=None, help="state_dict to load instead of the cache path")
+    p.add_argument("--mesh", default=None, help="training mesh (PLY) instead of the dataset's scan file")
+    p.add_argument("--epochs", default=None, type=int, help="training epochs (default: the reference's EPOCH)")
     p.add_argument("--out", default="meshes", help="mesh output directory")
     return p.parse_args(argv)
 
@@ -137,6 +145,52 @@ def evaluate(net, our_mesh: Mesh, our_t: float, out_dir: str, tag: str, sizes=No
     return rows
 
 
+BATCH_SIZE = 1000  # train.py:66
+
+
+def draw_canvas(net, force: bool):
+    """train.py:117-129 without the matplotlib canvas: subpoly, timed."""
+    t = time.time()
+    polygons, vertices, faces_with_indices = sp.subpoly(net, DIM, CANVAS_SIZE, force=force)
+    torch.cuda.synchronize()
+    our_t = time.time() - t
+    print(f" take {our_t:.2f}")
+    return polygons, vertices, faces_with_indices, our_t
+
+
+def train_sdf(net, args, path: str):
+    """The training loop of train.py:153-231 (no checkpoint, or -c)."""
+    from tropical.stanford.dataset import StanfordDataset
+    from tropical.stanford.sdf_train import SDFTrainer
+    epochs = args.epochs or (6 if "drill" == args.dataset else 10)  # train.py:67
+    print(f"warning: cannot find a pretrained model for seed ({args.seed})! This training code is not "
+          f"guarantee the convergence of training nor a reliable SDF.", flush=True)
+    training_data = StanfordDataset(args.dataset, mesh=args.mesh)
+    loader = torch.utils.data.DataLoader(training_data, batch_size=BATCH_SIZE, shuffle=True)
+    trainer = SDFTrainer(net, lr=1e-3, T_max=epochs * len(training_data) / BATCH_SIZE)
+    result = None
+    for epoch in range(epochs):
+        running_loss = torch.zeros((), device=net.device())
+        training_data.resample()  # train.py:170 (also before the first epoch)
+        for i, (inputs, labels) in enumerate(loader):
+            loss, l1 = trainer.step(inputs.cuda(), labels.cuda())
+            running_loss += loss
+            if i % 10 == 9:
+                print(f"[{epoch + 1}, {i + 1:5d}] lr: {trainer.sched.get_last_lr()[0]:.4f}, "
+                      f"loss: {running_loss.item() / 10:.5f}", f"l1: {l1.item() / 10:.5f}", end="")
+                running_loss.zero_()
+                it = len(training_data) * epoch // BATCH_SIZE // 10 + (i + 1) // 10
+                if 5 * epochs > it:
+                    print(" mesh calculation skipped.")
+                    continue
+                result = draw_canvas(net, args.force)
+    print("Finished training.", flush=True)
+    if args.cache:
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        torch.save(net.state_dict(), path)
+    return result
+
+
 def main(argv=None):
     args = parse_args(argv)
     print(args)
@@ -148,20 +202,18 @@ def main(argv=None):
         raise SystemExit("tropical.stanford.train needs a ROCm GPU (no CPU fallback)")
     net = Net(**net_config(args.model_size, args.dataset)).cuda()
     path = args.weights or model_path(args.dataset, args.model_size, seed)
-    if not ((args.cache or args.weights) and os.path.isfile(path)):
-        print(f"warning: cannot find a pretrained model for seed ({seed})! ({path})", flush=True)
-        raise SystemExit("SDF training needs the Stanford scans and is not part of this path "
-                         "(SURVEY §8f); place the released state_dict at the path above or pass "
-                         "--weights")
-    sd = torch.load(path, map_location=net.device(), weights_only=True)
-    net.load_state_dict(sd)
-    print(f"The pretrained model loaded from {path}")
-
-    t = time.time()
-    polygons, vertices, faces_with_indices = sp.subpoly(net, DIM, CANVAS_SIZE, force=args.force)
-    torch.cuda.synchronize()
-    our_t = time.time() - t
-    print(f" take {our_t:.2f}")
+    if (args.cache or args.weights) and os.path.isfile(path):
+        sd = torch.load(path, map_location=net.device(), weights_only=True)
+        net.load_state_dict(sd)
+        print(f"The pretrained model loaded from {path}")
+        polygons, vertices, faces_with_indices, our_t = draw_canvas(net, args.force)
+    else:
+        if args.weights:
+            raise SystemExit(f"--weights: no file at {path}")
+        result = train_sdf(net, args, path)
+        if result is None:
+            result = draw_canvas(net, args.force)
+        polygons, vertices, faces_with_indices, our_t = result
 
     verts = vertices.cpu().numpy() / R
     our_mesh = Mesh(verts, np.asarray(faces_with_indices, dtype=np.int64))
