@@ -7,9 +7,9 @@ Same constructor, attributes (``enc``, ``fc``, ``num_layers``,
 (``forward(x, gather, group)``, ``preprocess``, ``preprocess_inverse``,
 ``sdf``, ``region``, ``normal``).  Every evaluation is a fused HIP kernel
 (encoding + MLP, csrc/net.hip) on the net's ROCm device; the forward is
-bitwise equal to the reference's PyTorch-CPU evaluation.  Training
-(autograd through the hash grid) is out of scope for this build
-(DESIGN.md), so these ops are inference-only.
+bitwise equal to the reference's PyTorch-CPU evaluation.  These ops carry
+no autograd graph: training takes its gradients in closed form from
+``tropical.stanford.sdf_train.SDFTrainer`` (csrc/train.hip).
 """
 from __future__ import annotations
 
