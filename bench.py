@@ -452,6 +452,20 @@ def main():
                 roof["valu_util"] = round(row["SQ_INSTS_VALU"] * 4 / (roof["avg_launch_us"] * 1e-6 * CLOCK_HZ * SIMDS), 3)
             if row and "TCC_HIT_sum" in row:
                 roof["l2_hit"] = round(row["TCC_HIT_sum"] / max(row["TCC_HIT_sum"] + row["TCC_MISS_sum"], 1), 3)
+        if roof:
+            # what actually limits the kernel, from the counters: HBM is the
+            # roof it is priced against ("bound"); below ~half of it with the
+            # fabric traffic also well under peak, the kernel is issue/latency
+            # bound (VALU share of the SIMD cycles, gathers waiting on L2/MALL)
+            tg = roof["traffic_gbs"]
+            if roof["frac"] >= 0.5 or (tg is not None and tg >= 0.5 * HBM_PEAK_GBS):
+                roof["limiter"] = "hbm"
+            elif roof["valu_util"] is not None:
+                roof["limiter"] = (f"issue/latency: VALU busy {roof['valu_util']:.0%} of SIMD cycles, "
+                                   f"L2 hit {roof['l2_hit']:.0%}, fabric traffic "
+                                   f"{(tg or 0) / HBM_PEAK_GBS:.0%} of HBM peak")
+            else:
+                roof["limiter"] = "issue/latency (no PMC pass for this kernel)"
         out = {
             "metric": "edges subdivided/sec", "value": round(value, 1), "unit": "edges/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,

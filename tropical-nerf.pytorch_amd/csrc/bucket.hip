@@ -297,10 +297,26 @@ k_bucket_scatter(const int32_t* __restrict__ members, int64_t S, int64_t V, int6
         for (int q = 0; q < n[2]; ++q) atomicAdd(&hist[bucket_of(G, lo[0] + i, lo[1] + j, lo[2] + q)], 1);
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < NB; i += TNP_BLOCK) {
-    const int c = hist[i];
-    rel[i] = c ? atomicAdd(&bcur[i], c) : 0;
-    hist[i] = 0;
+  {
+    // one range per non-empty bin; every returning atomic of the thread in
+    // flight together (a runtime-bound loop would wait for each in turn)
+    constexpr int PB = (BUCKET_MAX + TNP_BLOCK - 1) / TNP_BLOCK;
+    int c[PB], r[PB];
+#pragma unroll
+    for (int k = 0; k < PB; ++k) {
+      const int i = k * TNP_BLOCK + threadIdx.x;
+      c[k] = i < NB ? hist[i] : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < PB; ++k) r[k] = c[k] ? atomicAdd(&bcur[k * TNP_BLOCK + threadIdx.x], c[k]) : 0;
+#pragma unroll
+    for (int k = 0; k < PB; ++k) {
+      const int i = k * TNP_BLOCK + threadIdx.x;
+      if (i < NB) {
+        rel[i] = r[k];
+        hist[i] = 0;
+      }
+    }
   }
   __syncthreads();
 #pragma unroll

@@ -136,11 +136,13 @@ struct tnp_engine {
   bool has_net = false;
   VSet cur, alt;
   Buf edges, edges_alt;
-  // per-edge key masks (step.hip k_prune_lb): dm = 1 + the highest plane on
-  // which the endpoint keys differ (uint8), sm = planes that split the edge
-  // (uint64); valid when masks_valid
-  Buf edm, esm, edm_alt, esm_alt;
+  // per-edge key bytes (step.hip k_prune_lb): dm = 1 + the highest plane on
+  // which the endpoint keys differ, ef = the first plane >= mask_from that
+  // splits the edge (EDGE_NOSPLIT: none); valid when masks_valid
+  Buf edm, eef, edm_alt, eef_alt;
   bool masks_valid = false;
+  int mask_from = 0;       // plane the stored first split planes start at
+  uint64_t act_bits = 0;   // OR of the edges' first split planes (bit p: plane p splits an edge)
   int64_t V = 0, E = 0;
   int keep_all = 0;
   int valid_from = 0;  // pre planes [valid_from, K) are valid for every vertex
@@ -334,17 +336,30 @@ static int reset_live(tnp_engine* e, hipStream_t s, bool edges_changed = true) {
   return set_alive(e, 0, e->V, s);
 }
 
-// per-edge masks from the endpoint keys, if the edges changed without them
-static int ensure_masks(tnp_engine* e, hipStream_t s) {
-  if (e->masks_valid) return 0;
+// per-edge high plane and first split plane (>= from) from the endpoint
+// keys; ctr != null: the OR of the first split planes -> ctr[CTR_ACTIVE]
+static int compute_masks(tnp_engine* e, int from, int64_t* ctr, hipStream_t s) {
   const int64_t E1 = std::max<int64_t>(e->E, 1);
   if (buf_ensure(e->edm, E1 * sizeof(uint8_t), s)) return -1;
-  if (buf_ensure(e->esm, E1 * sizeof(uint64_t), s)) return -1;
-  TIMED("edge_masks", 40.0 * e->E,
+  if (buf_ensure(e->eef, E1 * sizeof(uint8_t), s)) return -1;
+  TIMED("edge_masks", 42.0 * e->E,
         launch_edge_masks(P<int32_t>(e->edges), e->E, P<uint64_t>(e->cur.pz), P<uint8_t>(e->edm),
-                          P<uint64_t>(e->esm), 0, 63, nullptr, s));
+                          P<uint8_t>(e->eef), from, e->K - 1, ctr, s));
   e->masks_valid = true;
+  e->mask_from = from;
   return 0;
+}
+
+// the masks a step at plane idx can use: the stored first split planes were
+// taken from mask_from, so they are the ones of idx unless a plane in
+// [mask_from, idx) still splits some edge (a step the caller skipped) --
+// then they are recomputed from idx.  Returns 1 if recomputed (the OR of
+// the first planes is then in ctr[CTR_ACTIVE], ctr zeroed by the caller).
+static int ensure_masks(tnp_engine* e, int idx, hipStream_t s) {
+  const uint64_t below = idx >= 64 ? ~0ull : ((1ull << idx) - 1ull);
+  const uint64_t from = e->mask_from >= 64 ? ~0ull : ((1ull << e->mask_from) - 1ull);
+  if (e->masks_valid && idx >= e->mask_from && (e->act_bits & below & ~from) == 0) return 0;
+  return compute_masks(e, idx, P<int64_t>(e->ctr), s) ? -1 : 1;
 }
 
 // renumber the live slots densely (the reference's per-step compaction,
@@ -392,7 +407,6 @@ extern "C" int tnp_engine_create(tnp_engine** out, int device) {
           hipSuccess ||
       hipHostGetDevicePointer((void**)&e->h_map_dev, e->h_map, 0) != hipSuccess) {
     if (e->h_ctr) (void)hipHostFree(e->h_ctr);
-  if (e->h_map) (void)hipHostFree(e->h_map);
     if (e->h_map) (void)hipHostFree(e->h_map);
     delete e;
     tnp_set_error("hipHostMalloc failed");
@@ -417,8 +431,8 @@ extern "C" void tnp_engine_destroy(tnp_engine* e) {
                  &e->stage, &e->shared, &e->members, &e->pcn, &e->pent, &e->rstart,
                  &e->ent_v, &e->ents, &e->pcell, &e->ptoff, &e->bcell,
                  &e->ckeys_a, &e->ckeys_b, &e->sort_scr, &e->flags, &e->used, &e->nid,
-                 &e->ctr, &e->tri, &e->faces, &e->lb[0], &e->lb[1], &e->edm, &e->esm,
-                 &e->edm_alt, &e->esm_alt, &e->live, &e->tied_table};
+                 &e->ctr, &e->tri, &e->faces, &e->lb[0], &e->lb[1], &e->edm, &e->eef,
+                 &e->edm_alt, &e->eef_alt, &e->live, &e->tied_table};
   for (Buf* b : bufs) buf_free(*b, s);
   for (Buf& b : e->fscr) buf_free(b, s);
   for (Buf& b : e->fscr2) buf_free(b, s);
@@ -590,17 +604,12 @@ extern "C" int tnp_engine_active_planes(tnp_engine* e, int from, uint64_t* mask,
   TNP_CHECK(hipSetDevice(e->device));
   if (buf_ensure(e->ctr, CTR_N * sizeof(int64_t), s)) return -1;
   TNP_CHECK(hipMemsetAsync(P<int64_t>(e->ctr) + CTR_ACTIVE, 0, sizeof(int64_t), s));
-  // the per-edge masks are (re)computed here and the OR of their split planes
-  // taken in the same pass
-  const int64_t E1 = std::max<int64_t>(e->E, 1);
-  if (buf_ensure(e->edm, E1 * sizeof(uint8_t), s)) return -1;
-  if (buf_ensure(e->esm, E1 * sizeof(uint64_t), s)) return -1;
-  if (launch_edge_masks(P<int32_t>(e->edges), e->E, P<uint64_t>(e->cur.pz), P<uint8_t>(e->edm),
-                        P<uint64_t>(e->esm), from, e->K - 1, P<int64_t>(e->ctr), s))
-    return -1;
-  e->masks_valid = true;
+  // the per-edge masks are (re)computed here and the OR of their first split
+  // planes taken in the same pass: the planes the next steps must visit
+  if (compute_masks(e, from, P<int64_t>(e->ctr), s)) return -1;
   if (read_ctr(e, s)) return -1;
   *mask = (uint64_t)e->h_ctr[CTR_ACTIVE];
+  e->act_bits = *mask;
   return 0;
 }
 
@@ -779,13 +788,14 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
     if (buf_ensure(e->sa, e->E * sizeof(int32_t), s)) return -1;
     if (buf_ensure(e->sb, e->E * sizeof(int32_t), s)) return -1;
     if (e->curve && buf_ensure(e->cv[CV_EIDX], e->E * sizeof(int32_t), s)) return -1;
-    if (ensure_masks(e, s)) return -1;
+    const int fresh = ensure_masks(e, idx, s);
+    if (fresh < 0) return -1;
     TnpLB lb;
     if (lb_begin(e, split_tiles(e->E), s, &lb)) return -1;
-    // algorithmic bytes: 8 B split mask per edge; per split 8 B endpoints,
-    // 4 B rewired id, 1 B stale mask (set once S is known)
-    TIMED("split", 8.0 * e->E,
-          launch_split_lb(P<int32_t>(e->edges), e->E, P<uint64_t>(e->esm), P<uint8_t>(e->edm), idx,
+    // algorithmic bytes: 1 B first split plane per edge; per split 8 B
+    // endpoints, 4 B rewired id, 1 B stale mask (set once S is known)
+    TIMED("split", 1.0 * e->E,
+          launch_split_lb(P<int32_t>(e->edges), e->E, P<uint8_t>(e->eef), P<uint8_t>(e->edm), idx,
                           e->V, P<int32_t>(e->sa), P<int32_t>(e->sb), P<int64_t>(e->ctr),
                           e->curve ? P<int32_t>(e->cv[CV_EIDX]) : nullptr, lb, s));
     if (!e->curve && e->V > 0) {
@@ -802,7 +812,12 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
     }
     if (read_ctr(e, s)) return -1;
     S = e->h_ctr[CTR_S];
-    ktimer_set_bytes(e, "split", 8.0 * e->E + 13.0 * S);
+    if (fresh) e->act_bits = (uint64_t)e->h_ctr[CTR_ACTIVE];
+    if (e->h_ctr[CTR_MISSED]) {  // ensure_masks keeps this from happening
+      tnp_set_error("plane %d: an edge's first split plane lies below the step (stale edge masks)", idx);
+      return -1;
+    }
+    ktimer_set_bytes(e, "split", 1.0 * e->E + 13.0 * S);
   }
   *fail = 0;
   if (e->V + S >= (int64_t)INT32_MAX) {
@@ -1157,28 +1172,32 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     // (word-atomic live counting inside the prune measured slower than the
     // counting pass even at bunny scale: 0.25 vs 0.13 + 0.07 ms per subpoly)
     const bool count_in_prune = false;
-    if (ensure_masks(e, s)) return -1;  // (curve path: recomputed after the rewiring)
+    // (curve path: recomputed after the rewiring, first split planes above idx)
+    if (!e->masks_valid && compute_masks(e, idx + 1, nullptr, s)) return -1;
     const int64_t N1 = std::max<int64_t>(N, 1);
     if (buf_ensure(e->edm_alt, N1 * sizeof(uint8_t), s)) return -1;
-    if (buf_ensure(e->esm_alt, N1 * sizeof(uint64_t), s)) return -1;
+    if (buf_ensure(e->eef_alt, N1 * sizeof(uint8_t), s)) return -1;
     TnpLB lb;
     if (lb_begin(e, lb_tiles(N), s, &lb)) return -1;
-    // old edges: 8 B ids + 1 B high plane + 8 B split mask read; e_new / c_new:
-    // 4 / 8 B ids + 32 B endpoint keys; kept edges: 17 B written + 2 B flags
-    TIMED("prune", 17.0 * E + 36.0 * S + 40.0 * X,
+    // old edges: 8 B ids + 1 B high plane + 1 B first split plane read; e_new /
+    // c_new: 4 / 8 B ids + 32 B endpoint keys; kept edges: 10 B written + 2 B flags
+    TIMED("prune", 10.0 * E + 36.0 * S + 40.0 * X,
           launch_prune_lb(eg, E, P<int32_t>(e->sb), S, V, e->ckeys, nb, X, idx, K - 1,
-                          P<uint64_t>(c.pz), P<uint8_t>(e->edm), P<uint64_t>(e->esm),
-                          P<int32_t>(e->edges_alt), P<uint8_t>(e->edm_alt), P<uint64_t>(e->esm_alt),
+                          P<uint64_t>(c.pz), P<uint8_t>(e->edm), P<uint8_t>(e->eef),
+                          P<int32_t>(e->edges_alt), P<uint8_t>(e->edm_alt), P<uint8_t>(e->eef_alt),
                           P<uint8_t>(e->live), count_in_prune, ctr, lb, s));
     std::swap(e->edm, e->edm_alt);
-    std::swap(e->esm, e->esm_alt);
+    std::swap(e->eef, e->eef_alt);
     if (!count_in_prune)
       TIMED("count_live", 1.0 * NV, launch_count_flags(P<uint8_t>(e->live), NV, ctr, CTR_V, s));
     next_valid = e->keep_all ? 0 : std::min(idx + 1, K - 1);
     if (read_ctr(e, s)) return -1;
-    ktimer_set_bytes(e, "prune", 17.0 * E + 36.0 * S + 40.0 * X + 19.0 * e->h_ctr[CTR_E]);
+    ktimer_set_bytes(e, "prune", 10.0 * E + 36.0 * S + 40.0 * X + 12.0 * e->h_ctr[CTR_E]);
     E2 = e->h_ctr[CTR_E];
     V2 = e->h_ctr[CTR_V];
+    // the kept edges' first split planes are above idx now
+    e->mask_from = idx + 1;
+    e->act_bits = (uint64_t)e->h_ctr[CTR_ACTIVE];
     e->dirty = true;
   } else {
     if (launch_prune(true, eg, E, P<int32_t>(e->sb), S, V, e->ckeys, nb, X, idx, 0, K - 1, pos, zero, nullptr, nullptr,

@@ -169,40 +169,6 @@ __device__ __forceinline__ uint64_t grid_word(const float* marks, int M, float e
 }
 
 
-// grid_word of a point on the segment between two vertices with grid words
-// ga, gb: each axis's lower_bound runs over the endpoints' mark range widened
-// by one mark per side (the split point can round an ulp past an endpoint)
-// and is accepted only when the range provably holds the answer; otherwise
-// the full search.  Same result as grid_word, a few steps instead of
-// log2(M).  marks: the sorted marks (LDS copy in k_forward_new).
-__device__ __forceinline__ uint64_t grid_word_near(const float* marks, int M, float eps, const float x[3],
-                                                   uint64_t ga, uint64_t gb) {
-  uint64_t g = 0;
-#pragma unroll
-  for (int d = 0; d < 3; ++d) {
-    const float v = __fadd_rn(x[d], eps);
-    const int oa = tnp::grid_off(ga, d), ob = tnp::grid_off(gb, d);
-    int lo = max(min(oa, ob), 0), hi = min(max(oa, ob) + 3, M);
-    int r;
-    if ((lo == 0 || marks[lo - 1] < v) && (hi == M || !(marks[hi - 1] < v))) {
-      while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (marks[mid] < v) lo = mid + 1;
-        else hi = mid;
-      }
-      r = lo;
-    } else {
-      r = search_left(marks, M, v);
-    }
-    const int off = r - 1;
-    const float mk = marks[off < 0 ? off + M : off];
-    const bool zero = !(fabsf(__fsub_rn(mk, x[d])) > eps);
-    g |= (uint64_t)(uint32_t)(off + 2) << (16 * d);
-    g |= (uint64_t)(zero ? 1 : 0) << (48 + d);
-  }
-  return g;
-}
-
 // SDF = tanh(o1 - o0) and d SDF / d x (input gradient through ReLU masks and
 // the trilinear encoding; floor() has zero gradient so the cell on the right
 // is used on grid lines, as autograd through tcnn does).  w: packed weights.

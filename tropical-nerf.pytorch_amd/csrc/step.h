@@ -34,8 +34,8 @@ enum {
   CTR_RUNS = 26,    // occupied cells (runs of equal keys in the sorted entries)
   CTR_SPAIRS = 27,  // member pairs of the cells the window pass tests (<= WCELL members)
   CTR_TK0 = 28,     // last-workgroup tickets (tnp::last_block) of the fused
-  CTR_TK1 = 29,     //   bucket count / bucket group / window pass launches
-  CTR_TK2 = 30,
+  CTR_TK1 = 29,     //   bucket count / bucket group launches
+  CTR_MISSED = 30,  // split: an edge whose first split plane lies below the step (masks to redo)
   CTR_N = 31        // <= 31: the host-mapped mirror keeps its sequence word at [31]
 };
 
@@ -44,17 +44,20 @@ int64_t lb_tiles(int64_t n);     // tiles of the single-pass prune
 int64_t split_tiles(int64_t n);  // tiles of the single-pass split and hit passes
 int64_t run_tiles(int64_t n);    // tiles of the radix path's run-start pass
 // single-pass split over split_tiles(E) look-back tiles (E > 0) from the
-// edges' split masks (bit idx): S -> ctr[CTR_S]; sa/sb (and eidx if given)
-// need capacity E; without eidx the split edges are rewired in place and
-// their masks marked stale
-int launch_split_lb(int32_t* edges, int64_t E, const uint64_t* sm, uint8_t* dm, int idx, int64_t V,
+// edges' first split planes (ef == idx): S -> ctr[CTR_S]; an edge whose
+// first split plane is below idx sets ctr[CTR_MISSED] (its masks are older
+// than the caller's step order: redo them from idx); sa/sb (and eidx if
+// given) need capacity E; without eidx the split edges are rewired in place
+// and their masks marked stale
+int launch_split_lb(int32_t* edges, int64_t E, const uint8_t* ef, uint8_t* dm, int idx, int64_t V,
                     int32_t* sa, int32_t* sb, int64_t* ctr, int32_t* eidx, const TnpLB& lb,
                     hipStream_t s);
 // per-edge masks from the endpoint keys (pz): dm = 1 + highest plane where
-// the keys differ (0: none), sm = split planes; ctr != null: OR of sm over
-// planes [from, last_plane] -> CTR_ACTIVE
+// the keys differ (0: none), ef = the first plane in [from, last_plane] that
+// splits the edge (EDGE_NOSPLIT: none); ctr != null: OR of those first
+// planes -> CTR_ACTIVE
 int launch_edge_masks(const int32_t* edges, int64_t E, const uint64_t* pz, uint8_t* dm,
-                      uint64_t* sm, int from, int last_plane, int64_t* ctr, hipStream_t s);
+                      uint8_t* ef, int from, int last_plane, int64_t* ctr, hipStream_t s);
 int launch_new_vertices(const int32_t* sa, const int32_t* sb, int64_t S, const float* col,
                         float eps, float* xyz, int64_t V, hipStream_t s);
 int launch_fail_check(const int32_t* sa, const int32_t* sb, int64_t S, int idx,
@@ -156,8 +159,8 @@ int launch_connect(const int64_t* ptoff, const int32_t* pcell, const int32_t* pn
 // caller), ctr[CTR_E], ctr[CTR_ACTIVE]
 int launch_prune_lb(const int32_t* edges, int64_t E, const int32_t* sb, int64_t S, int64_t V,
                     const uint64_t* ckeys, int nb, int64_t X, int idx, int last_plane,
-                    const uint64_t* pz, const uint8_t* dm, const uint64_t* sm, int32_t* out,
-                    uint8_t* odm, uint64_t* osm, uint8_t* used, bool count_live, int64_t* ctr,
+                    const uint64_t* pz, const uint8_t* dm, const uint8_t* ef, int32_t* out,
+                    uint8_t* odm, uint8_t* oef, uint8_t* used, bool count_live, int64_t* ctr,
                     const TnpLB& lb, hipStream_t s);
 // count_live: the distinct live endpoints are counted into ctr[CTR_V] on the
 // way (word atomics; for small complexes, instead of launch_count_flags)

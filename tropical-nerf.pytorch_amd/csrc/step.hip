@@ -33,6 +33,16 @@ constexpr uint8_t EDGE_STALE = 0xFF;  // rewired edge: recompute from the endpoi
 __device__ __forceinline__ uint8_t high_plane(uint64_t dm) {
   return (uint8_t)(dm ? 64 - __clzll(dm) : 0);
 }
+// per-edge first split plane ef: the lowest plane >= the next step that
+// splits the edge (endpoints non-zero with opposite signs, exactly the split
+// test of subpoly.py:104-105); EDGE_NOSPLIT: none.  An edge splits at most
+// once more as it stands: at plane ef it is replaced by its two halves,
+// whose planes come from the new keys, so one byte per edge carries every
+// future split test (instead of the 64-bit mask of all its split planes)
+constexpr uint8_t EDGE_NOSPLIT = 0xFF;
+__device__ __forceinline__ uint8_t first_plane(uint64_t m) {
+  return (uint8_t)(m ? __builtin_ctzll(m) : EDGE_NOSPLIT);
+}
 constexpr int IPT = 8;                  // items per thread per tile
 constexpr int TILE = TNP_BLOCK * IPT;   // tile of a compaction pass
 // single-pass (look-back) compactions: items per thread of the split / hit
@@ -68,7 +78,7 @@ __device__ __forceinline__ bool split_test(const float* __restrict__ col, const 
 // of a bounds branch serialising every item.
 template <int SI>
 __global__ void __launch_bounds__(TNP_BLOCK)
-k_split_lb(int32_t* __restrict__ edges, int64_t E, int64_t ntiles, const uint64_t* __restrict__ sm,
+k_split_lb(int32_t* __restrict__ edges, int64_t E, int64_t ntiles, const uint8_t* __restrict__ ef,
            uint8_t* __restrict__ dm, int idx, int64_t V, int32_t* __restrict__ sa,
            int32_t* __restrict__ sb, int64_t* __restrict__ ctr, int32_t* __restrict__ eidx, TnpLB lb) {
   __shared__ int cnt[SI][TNP_WAVES];
@@ -76,18 +86,21 @@ k_split_lb(int32_t* __restrict__ edges, int64_t E, int64_t ntiles, const uint64_
   const int64_t tile = tnp::lb_tile(lb, &slot);
   const int64_t base = tile * (TNP_BLOCK * SI);
   uint64_t bal[SI];
-  uint64_t mk[SI];
+  uint32_t fp[SI];
 #pragma unroll
   for (int k = 0; k < SI; ++k) {  // coalesced, unconditional (clamped) loads
     const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
-    mk[k] = sm[i < E ? i : E - 1];
+    fp[k] = ef[i < E ? i : E - 1];
   }
+  bool missed = false;
 #pragma unroll
   for (int k = 0; k < SI; ++k) {
     const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
-    bal[k] = __ballot((i < E) && ((mk[k] >> idx) & 1));
+    bal[k] = __ballot((i < E) && fp[k] == (uint32_t)idx);
+    missed |= (i < E) && fp[k] < (uint32_t)idx;
     if (tnp::lane() == 0) cnt[k][tnp::wave()] = __popcll(bal[k]);
   }
+  if (__ballot(missed) && tnp::lane() == 0) tnp::or_sticky(&ctr[CTR_MISSED], 1ull);
   __syncthreads();
   int64_t agg = 0;
 #pragma unroll
@@ -779,18 +792,19 @@ k_prune_emit(EdgeSrc src, int64_t N, uint64_t fmask, uint64_t amask,
 // tile's output offset, then the ordered emit (k-major, then thread, as
 // prune_emit), used flags and the next-active plane mask.  The last tile
 // writes the kept count to ctr[CTR_E].
-// Per-edge key masks travel with the edges: dm = endpoint keys differ
-// ((pos ^ pos') | (zero ^ zero')) and sm = the planes that split the edge
-// ((pos ^ pos') & ~zero & ~zero': both non-zero, opposite signs -- exactly
-// the split test of subpoly.py:104-105).  Vertex keys never change after
+// Per-edge key bytes travel with the edges: dm = the high plane of the
+// endpoint keys' difference ((pos ^ pos') | (zero ^ zero')) and ef = the
+// first plane above idx that splits the edge ((pos ^ pos') & ~zero & ~zero':
+// both non-zero, opposite signs -- exactly the split test of
+// subpoly.py:104-105).  Vertex keys never change after
 // creation, so an edge's masks change only when the edge does: the prune
 // reads them coalesced for the old edges and gathers the endpoint keys only
 // for rewired (dm == EDGE_STALE), e_new and c_new edges.
 __global__ void __launch_bounds__(TNP_BLOCK, 4)
 k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, int idx, uint64_t amask,
            const ulonglong2* __restrict__ pz, const uint8_t* __restrict__ dm,
-           const uint64_t* __restrict__ sm, int32_t* __restrict__ out, uint8_t* __restrict__ odm,
-           uint64_t* __restrict__ osm, uint8_t* __restrict__ used, int count_live,
+           const uint8_t* __restrict__ ef, int32_t* __restrict__ out, uint8_t* __restrict__ odm,
+           uint8_t* __restrict__ oef, uint8_t* __restrict__ used, int count_live,
            int64_t* __restrict__ ctr, TnpLB lb) {
   __shared__ int cnt[LIPT][TNP_WAVES];
   __shared__ int64_t slot;
@@ -803,8 +817,7 @@ k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, int idx, uint64_t amask,
   const int64_t ES = src.E + src.S;
   const int kind = last < src.E ? 0 : (base >= src.E && last < ES) ? 1 : (base >= ES ? 2 : 3);
   int a[LIPT], b[LIPT];
-  uint32_t d[LIPT];
-  uint64_t m[LIPT];
+  uint32_t d[LIPT], m[LIPT];  // high plane, first split plane
   if (kind == 0) {
     const int2* e2 = reinterpret_cast<const int2*>(src.edges);
 #pragma unroll
@@ -815,7 +828,7 @@ k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, int idx, uint64_t amask,
       a[k] = ab.x;
       b[k] = ab.y;
       d[k] = dm[ic];
-      m[k] = sm[ic];
+      m[k] = ef[ic];
     }
   } else {
     if (kind == 1) {
@@ -846,7 +859,7 @@ k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, int idx, uint64_t amask,
     for (int k = 0; k < LIPT; ++k) {
       const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
       d[k] = (i < src.E) ? dm[i] : EDGE_STALE;  // mixed tile: old edges keep theirs
-      m[k] = (i < src.E) ? sm[i] : 0ull;
+      m[k] = (i < src.E) ? ef[i] : EDGE_NOSPLIT;
     }
   }
 #pragma unroll
@@ -854,7 +867,7 @@ k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, int idx, uint64_t amask,
     if (d[k] == EDGE_STALE) {  // new or rewired edge: masks from the endpoint keys
       const ulonglong2 ka = pz[a[k]], kb = pz[b[k]];
       d[k] = high_plane((ka.x ^ kb.x) | (ka.y ^ kb.y));
-      m[k] = (ka.x ^ kb.x) & ~ka.y & ~kb.y;
+      m[k] = first_plane((ka.x ^ kb.x) & ~ka.y & ~kb.y & amask);
     }
   }
   uint64_t bal[LIPT];
@@ -863,7 +876,8 @@ k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, int idx, uint64_t amask,
   for (int k = 0; k < LIPT; ++k) {
     const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
     const bool f = (i <= last) && ((int)d[k] > idx);
-    if (f) act |= m[k] & amask;
+    // (an old edge's first split plane is above idx: else it would have split)
+    if (f && m[k] != EDGE_NOSPLIT) act |= 1ull << m[k];
     bal[k] = __ballot(f);
     if (tnp::lane() == 0) cnt[k][tnp::wave()] = __popcll(bal[k]);
   }
@@ -890,7 +904,7 @@ k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, int idx, uint64_t amask,
       const int64_t o = off + tnp::mbcnt(bal[k]);
       reinterpret_cast<int2*>(out)[o] = make_int2(a[k], b[k]);
       odm[o] = (uint8_t)d[k];
-      osm[o] = m[k];
+      oef[o] = (uint8_t)m[k];
       if (count_live) {
         // small complexes: the distinct live count without a counting pass
         // (a word-wide atomic OR tells who set each byte first)
@@ -928,7 +942,7 @@ k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, int idx, uint64_t amask,
 // ctr[CTR_ACTIVE] when ctr != null
 __global__ void __launch_bounds__(TNP_BLOCK)
 k_edge_masks(const int32_t* __restrict__ edges, int64_t E, const ulonglong2* __restrict__ pz,
-             uint8_t* __restrict__ dm, uint64_t* __restrict__ sm, uint64_t amask,
+             uint8_t* __restrict__ dm, uint8_t* __restrict__ ef, uint64_t amask,
              int64_t* __restrict__ ctr) {
   __shared__ uint64_t lds[TNP_WAVES];
   uint64_t act = 0;
@@ -936,10 +950,10 @@ k_edge_masks(const int32_t* __restrict__ edges, int64_t E, const ulonglong2* __r
        i += (int64_t)gridDim.x * blockDim.x) {
     const int2 ab = reinterpret_cast<const int2*>(edges)[i];
     const ulonglong2 ka = pz[ab.x], kb = pz[ab.y];
-    const uint64_t s = (ka.x ^ kb.x) & ~ka.y & ~kb.y;
+    const uint8_t f = first_plane((ka.x ^ kb.x) & ~ka.y & ~kb.y & amask);
     dm[i] = high_plane((ka.x ^ kb.x) | (ka.y ^ kb.y));
-    sm[i] = s;
-    act |= s & amask;
+    ef[i] = f;
+    if (f != EDGE_NOSPLIT) act |= 1ull << f;
   }
   if (!ctr) return;
   act = tnp::wave_or(act);
@@ -1037,7 +1051,7 @@ int64_t split_tiles(int64_t n) {
 }
 int64_t run_tiles(int64_t n) { return (n + STILE - 1) / STILE; }
 
-int launch_split_lb(int32_t* edges, int64_t E, const uint64_t* sm, uint8_t* dm, int idx, int64_t V,
+int launch_split_lb(int32_t* edges, int64_t E, const uint8_t* sm, uint8_t* dm, int idx, int64_t V,
                     int32_t* sa, int32_t* sb, int64_t* ctr, int32_t* eidx, const TnpLB& lb,
                     hipStream_t s) {
   const int64_t tiles = split_tiles(E);
@@ -1222,8 +1236,8 @@ int launch_prune(bool emit, const int32_t* edges, int64_t E, const int32_t* sb, 
 }
 int launch_prune_lb(const int32_t* edges, int64_t E, const int32_t* sb, int64_t S, int64_t V,
                     const uint64_t* ckeys, int nb, int64_t X, int idx, int last_plane,
-                    const uint64_t* pz, const uint8_t* dm, const uint64_t* sm, int32_t* out,
-                    uint8_t* odm, uint64_t* osm, uint8_t* used, bool count_live, int64_t* ctr,
+                    const uint64_t* pz, const uint8_t* dm, const uint8_t* ef, int32_t* out,
+                    uint8_t* odm, uint8_t* oef, uint8_t* used, bool count_live, int64_t* ctr,
                     const TnpLB& lb, hipStream_t s) {
   EdgeSrc src{edges, E, sb, S, V, ckeys, nb, X};
   const int64_t N = E + S + X;
@@ -1237,7 +1251,7 @@ int launch_prune_lb(const int32_t* edges, int64_t E, const int32_t* sb, int64_t 
   const int64_t tiles = lb_tiles(N);
   (void)fmask;
   hipLaunchKernelGGL(k_prune_lb, dim3((unsigned)tiles), dim3(TNP_BLOCK), 0, s, src, N, tiles, idx,
-                     amask, reinterpret_cast<const ulonglong2*>(pz), dm, sm, out, odm, osm, used,
+                     amask, reinterpret_cast<const ulonglong2*>(pz), dm, ef, out, odm, oef, used,
                      count_live ? 1 : 0, ctr, lb);
   TNP_CHECK(hipGetLastError());
   return 0;
@@ -1262,7 +1276,7 @@ int launch_count_flags(const uint8_t* f, int64_t n, int64_t* ctr, int slot, hipS
   return 0;
 }
 int launch_edge_masks(const int32_t* edges, int64_t E, const uint64_t* pz, uint8_t* dm,
-                      uint64_t* sm, int from, int last_plane, int64_t* ctr, hipStream_t s) {
+                      uint8_t* sm, int from, int last_plane, int64_t* ctr, hipStream_t s) {
   if (E <= 0) return 0;
   uint64_t amask = (from >= 64) ? 0ull : (~0ull << from);
   if (last_plane < 63) amask &= (1ull << (last_plane + 1)) - 1ull;
