@@ -530,7 +530,7 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
   } else {
     group_bucket<SH>(G, b, base, n, ekv, pz, ents, lcell, lent, ln, lpoff, bnpc, bnpairs, bspairs, ctr, cnt,
                      cur, lds);
-    if (wa.keys) {
+    if (wa.keys && !(TNP_EXP_WIN & 2)) {
       // the window pass over this bucket's records, right behind their
       // stores (the workgroup's own stores: visible after the barrier)
       __syncthreads();

@@ -69,6 +69,9 @@ __device__ __forceinline__ void add_pair_stats(int64_t a, int64_t r, int64_t x, 
 // buffer, one global append per WKEYS.
 // ---------------------------------------------------------------------------
 constexpr int WKEYS = 384;
+#ifndef TNP_EXP_WIN
+#define TNP_EXP_WIN 0  // timing experiments only (2: no window pass, 4: no tests, 8: no test table)
+#endif
 
 __device__ __forceinline__ void lds_fence() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -132,10 +135,11 @@ __device__ __forceinline__ void window_pass(const CellEnt* __restrict__ ent, int
     // flatten the window's (initiator, partner) tests over the lanes: test t
     // belongs to the last initiator j with exc[j] <= t, partner j + 1 + t - exc[j]
     const int incl = tnp::wave_scan_incl(rounds);
-    const int total = __shfl(incl, 63, 64);
+    int total = __shfl(incl, 63, 64);
     const bool table = total <= WOWN;
     W.exc[wv][L] = incl - rounds;
-    if (table)  // each initiator lists its own tests (a few, mostly)
+    if (TNP_EXP_WIN & 4) total = 0;  // timing experiment: no tests
+    if (table && !(TNP_EXP_WIN & 8))  // each initiator lists its own tests (a few, mostly)
       for (int r = 0, t = incl - rounds; r < rounds; ++r, ++t) W.own[wv][t] = (uint16_t)(L | ((L + 1 + r) << 8));
     lds_fence();
     for (int t0 = 0; t0 < total; t0 += 64) {
@@ -162,19 +166,22 @@ __device__ __forceinline__ void window_pass(const CellEnt* __restrict__ ent, int
         }
         const CellEnt u = W.st[wv][j];
         const CellEnt q = W.st[wv][i];
-        const PairTest pt = pair_test(below, u.f, u.p, u.z, q.f, q.p, q.z);
-        if (pt.compat) {
-          a.n_compat++;
-          a.n_reg += pt.regions;
-          a.n_conn += pt.emit;
-          // the step's pruning drops it anyway (keep_edge): never appended
-          if (pt.emit && (fmask == 0 || (((u.p ^ q.p) | (u.z ^ q.z)) & fmask) != 0)) {
-            const uint32_t vu = (uint32_t)u.v, vv = (uint32_t)q.v;
-            const uint32_t l3 = vu < vv ? vu : vv, h3 = vu < vv ? vv : vu;
-            key = ((uint64_t)l3 << nb) | h3;
-            em = true;
-          }
-        }
+        // pair_test without branches: both records are read once, every
+        // predicate is a select (branches here cost exec-mask juggling and a
+        // second dependent LDS round trip per test)
+        const uint64_t d = (u.p ^ q.p) & ~u.z & ~q.z & below;
+        const uint32_t af = u.f & q.f;
+        const uint32_t sp = af & (af >> 3) & 7u;
+        const uint64_t zz = u.z & q.z & below;
+        const bool compat = (((u.f | q.f) & 7u) == 7u) & (d == 0);
+        const bool emit = compat & ((sp != 0) | (zz != 0));
+        a.n_compat += compat;
+        a.n_reg += compat ? ((int64_t)1 << (__popc(sp) + __popcll(zz))) : 0;
+        a.n_conn += emit;
+        // the step's pruning drops it anyway (keep_edge): never appended
+        em = emit & ((fmask == 0) | ((((u.p ^ q.p) | (u.z ^ q.z)) & fmask) != 0));
+        const uint32_t vu = (uint32_t)u.v, vv = (uint32_t)q.v;
+        key = ((uint64_t)min(vu, vv) << nb) | max(vu, vv);
       }
       const uint64_t eb = __ballot(em);
       if (em) W.kb[wv][a.kn + tnp::mbcnt(eb)] = key;

@@ -1376,10 +1376,11 @@ extern "C" int tnp_engine_lattice(tnp_engine* e, int x0, int x1, int keep_all, v
   hipLaunchKernelGGL(k_lattice_edges, dim3(tnp_grid(E)), dim3(TNP_BLOCK), 0, s, N, nx,
                      P<int32_t>(e->edges));
   TNP_CHECK(hipGetLastError());
-  if (launch_forward(e->net, P<float>(e->cur.xyz), V, P<float>(e->cur.pre), e->cur.cap, 1, s, nullptr,
-                     P<uint64_t>(e->cur.pos), P<uint64_t>(e->cur.zero), P<uint64_t>(e->cur.grid),
-                     P<uint64_t>(e->cur.pz)))
-    return -1;
+  // the lattice's full forward (12 B coordinates in; K planes, 40 B of keys out)
+  TIMED("forward", (12.0 + 4.0 * e->K + 40.0) * V + table_bytes(e->net),
+        launch_forward(e->net, P<float>(e->cur.xyz), V, P<float>(e->cur.pre), e->cur.cap, 1, s, nullptr,
+                       P<uint64_t>(e->cur.pos), P<uint64_t>(e->cur.zero), P<uint64_t>(e->cur.grid),
+                       P<uint64_t>(e->cur.pz)));
   e->V = V;
   e->E = E;
   e->keep_all = keep_all;

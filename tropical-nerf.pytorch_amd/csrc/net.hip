@@ -40,7 +40,10 @@ k_forward(NetDev net, const float* __restrict__ xyz, int64_t n, float* __restric
   constexpr int IN = 2 * LV;
   constexpr int NW = H * IN + H + (NL - 2) * (H * H + H) + 2 * H + 2;
   __shared__ float w[NW];
+  __shared__ float mk[GROUPED ? 1 : TNP_MAX_MARKS];  // the marks for the grid words (keys)
   for (int i = threadIdx.x; i < NW; i += blockDim.x) w[i] = net.weights[i];
+  if (!GROUPED && kpos)
+    for (int i = threadIdx.x; i < net.n_marks; i += blockDim.x) mk[i] = net.marks[i];
   __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = i < n;
@@ -93,7 +96,7 @@ k_forward(NetDev net, const float* __restrict__ xyz, int64_t n, float* __restric
     kpos[i] = ps;
     kzero[i] = zs;
     kpz[i] = make_ulonglong2(ps, zs);
-    kgrid[i] = grid_word(net.marks, net.n_marks, net.eps, x);
+    kgrid[i] = grid_word(mk, net.n_marks, net.eps, x);
   }
 }
 
@@ -333,6 +336,7 @@ int launch_forward(const NetDev& net, const float* xyz, int64_t n, float* pre, i
   if (n <= 0) return 0;
   if (!net_supported(net)) { tnp_set_error("unsupported net shape"); return -1; }
   if (group != 1 && (group != 8 || n % 8)) { tnp_set_error("group must be 1 or 8 (n%%8==0)"); return -1; }
+  if (pos && net.n_marks > TNP_MAX_MARKS) { tnp_set_error("more than %d marks per axis", TNP_MAX_MARKS); return -1; }
   TNP_DISPATCH(net.n_levels, {
     if (group == 8)
       hipLaunchKernelGGL((k_forward<L_, 16, 3, true>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s,
