@@ -62,6 +62,7 @@ struct WinArgs {
   uint64_t fmask;
   uint64_t* keys;
   int64_t cap;
+  int64_t* xs;  // per-XCD shards of the appends and pair statistics (step.h)
 };
 
 // the global pair-cell lists the fused last workgroup fills
@@ -530,16 +531,16 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
   } else {
     group_bucket<SH>(G, b, base, n, ekv, pz, ents, lcell, lent, ln, lpoff, bnpc, bnpairs, bspairs, ctr, cnt,
                      cur, lds);
-    if (wa.keys && !(TNP_EXP_WIN & 2)) {
+    if (wa.keys) {
       // the window pass over this bucket's records, right behind their
       // stores (the workgroup's own stores: visible after the barrier)
       __syncthreads();
       WinAcc a;
       const uint64_t below = (wa.idx >= 64) ? ~0ull : ((1ull << wa.idx) - 1ull);
-      window_pass(ents, base, base + n, tnp::wave(), TNP_WAVES, below, wa.nb, wa.fmask, wa.keys, wa.cap, ctr, W,
-                  a);
-      window_flush(wa.keys, wa.cap, ctr, W, a);
-      add_pair_stats(a.n_compat, a.n_reg, a.n_conn, lds, ctr);
+      window_pass(ents, base, base + n, tnp::wave(), TNP_WAVES, below, wa.nb, wa.fmask, wa.keys, wa.cap, wa.xs,
+                  W, a);
+      window_flush(wa.keys, wa.cap, wa.xs, W, a);
+      add_pair_stats(a.n_compat, a.n_reg, a.n_conn, lds, wa.xs);
     }
   }
   if (!fuse || !tnp::last_block(&ctr[CTR_TK1], &last)) return;
@@ -661,8 +662,8 @@ int launch_bucket_pairs(int n_marks, const int64_t* bbase, const uint64_t* ekv, 
   const BGeom G{n_marks + 2, sh, NBd};
   const int fuse = NB <= FUSE_MAX_BLOCKS;
   const PairLists pl{pcell, pent, pn, ptoff, bcell, bcap, connect_chunk_pairs(), bcount, bcur};
-  WinArgs wa{0, 0, 0ull, nullptr, 0};
-  if (win) wa = WinArgs{win->idx, win->nb, win->fmask, win->keys, win->cap};
+  WinArgs wa{0, 0, 0ull, nullptr, 0, nullptr};
+  if (win) wa = WinArgs{win->idx, win->nb, win->fmask, win->keys, win->cap, win->xs};
   if (sh == 3)
     hipLaunchKernelGGL(k_bucket_group<3>, dim3(NB), dim3(TNP_BLOCK), 0, s, G, bbase, ekv,
                        reinterpret_cast<const ulonglong2*>(pz), ents, lcell, lent, ln, lpoff, bnpc, bnpairs,

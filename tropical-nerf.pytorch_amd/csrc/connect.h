@@ -42,17 +42,19 @@ __device__ __forceinline__ PairTest pair_test(uint64_t below, uint32_t fu, uint6
 }
 
 // a block's (compatible pairs, shared regions, connecting edges) totals
-//   -> ctr[CTR_COMPAT], ctr[CTR_P], ctr[CTR_X] (three adds per block)
+//   -> its XCD shard of each (three adds per block; k_keys_finish sums them
+//   into ctr[CTR_COMPAT], ctr[CTR_P], ctr[CTR_X])
 __device__ __forceinline__ void add_pair_stats(int64_t a, int64_t r, int64_t x, int64_t* lds,
-                                               int64_t* __restrict__ ctr) {
+                                               int64_t* __restrict__ xs) {
   int64_t ta, tr, tx;
   tnp::block_scan_excl(a, lds, ta);
   tnp::block_scan_excl(r, lds, tr);
   tnp::block_scan_excl(x, lds, tx);
   if (threadIdx.x == 0) {
-    if (ta) atomicAdd((unsigned long long*)&ctr[CTR_COMPAT], (unsigned long long)ta);
-    if (tr) atomicAdd((unsigned long long*)&ctr[CTR_P], (unsigned long long)tr);
-    if (tx) atomicAdd((unsigned long long*)&ctr[CTR_X], (unsigned long long)tx);
+    const int sh = blockIdx.x % XS_N;
+    if (ta) atomicAdd((unsigned long long*)&xs[xs_word(XS_COMPAT, sh)], (unsigned long long)ta);
+    if (tr) atomicAdd((unsigned long long*)&xs[xs_word(XS_P, sh)], (unsigned long long)tr);
+    if (tx) atomicAdd((unsigned long long*)&xs[xs_word(XS_X, sh)], (unsigned long long)tx);
   }
 }
 
@@ -69,9 +71,7 @@ __device__ __forceinline__ void add_pair_stats(int64_t a, int64_t r, int64_t x, 
 // buffer, one global append per WKEYS.
 // ---------------------------------------------------------------------------
 constexpr int WKEYS = 384;
-#ifndef TNP_EXP_WIN
-#define TNP_EXP_WIN 0  // timing experiments only (2: no window pass, 4: no tests, 8: no test table)
-#endif
+
 
 __device__ __forceinline__ void lds_fence() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -90,16 +90,19 @@ struct WinAcc {
   int64_t n_compat = 0, n_reg = 0, n_conn = 0;
 };
 
-// this wave's buffered keys -> keys[] (counted in ctr[CTR_XK])
+// this wave's buffered keys -> its XCD shard's key region (counted there)
 __device__ __forceinline__ void window_flush(uint64_t* __restrict__ keys, int64_t cap,
-                                             int64_t* __restrict__ ctr, WinLds& W, WinAcc& a) {
+                                             int64_t* __restrict__ xs, WinLds& W, WinAcc& a) {
   if (a.kn == 0) return;
   const int wv = tnp::wave(), L = tnp::lane();
+  const int sh = blockIdx.x % XS_N;
+  const int64_t rc = cap / XS_N;
   int64_t base = 0;
-  if (L == 0) base = (int64_t)atomicAdd((unsigned long long*)&ctr[CTR_XK], (unsigned long long)a.kn);
+  if (L == 0) base = (int64_t)atomicAdd((unsigned long long*)&xs[xs_word(XS_KEYS, sh)], (unsigned long long)a.kn);
   base = __shfl(base, 0, 64);
+  uint64_t* dst = keys + sh * rc;
   for (int i = L; i < a.kn; i += 64)
-    if (base + i < cap) keys[base + i] = W.kb[wv][i];
+    if (base + i < rc) dst[base + i] = W.kb[wv][i];
   lds_fence();
   a.kn = 0;
 }
@@ -108,7 +111,7 @@ __device__ __forceinline__ void window_flush(uint64_t* __restrict__ keys, int64_
 __device__ __forceinline__ void window_pass(const CellEnt* __restrict__ ent, int64_t lo, int64_t hi,
                                             int64_t w0, int64_t dw, uint64_t below, int nb, uint64_t fmask,
                                             uint64_t* __restrict__ keys, int64_t cap,
-                                            int64_t* __restrict__ ctr, WinLds& W, WinAcc& a) {
+                                            int64_t* __restrict__ xs, WinLds& W, WinAcc& a) {
   const int wv = tnp::wave(), L = tnp::lane();
   const int64_t nwin = (hi - lo + WSTRIDE - 1) / WSTRIDE;
   for (int64_t w = w0; w < nwin; w += dw) {
@@ -135,15 +138,14 @@ __device__ __forceinline__ void window_pass(const CellEnt* __restrict__ ent, int
     // flatten the window's (initiator, partner) tests over the lanes: test t
     // belongs to the last initiator j with exc[j] <= t, partner j + 1 + t - exc[j]
     const int incl = tnp::wave_scan_incl(rounds);
-    int total = __shfl(incl, 63, 64);
+    const int total = __shfl(incl, 63, 64);
     const bool table = total <= WOWN;
     W.exc[wv][L] = incl - rounds;
-    if (TNP_EXP_WIN & 4) total = 0;  // timing experiment: no tests
-    if (table && !(TNP_EXP_WIN & 8))  // each initiator lists its own tests (a few, mostly)
+    if (table)  // each initiator lists its own tests (a few, mostly)
       for (int r = 0, t = incl - rounds; r < rounds; ++r, ++t) W.own[wv][t] = (uint16_t)(L | ((L + 1 + r) << 8));
     lds_fence();
     for (int t0 = 0; t0 < total; t0 += 64) {
-      if (a.kn + 64 > WKEYS) window_flush(keys, cap, ctr, W, a);
+      if (a.kn + 64 > WKEYS) window_flush(keys, cap, xs, W, a);
       const int t = t0 + L;
       bool em = false;
       uint64_t key = 0;

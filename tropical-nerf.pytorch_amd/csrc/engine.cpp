@@ -140,6 +140,8 @@ struct tnp_engine {
   // which the endpoint keys differ, ef = the first plane >= mask_from that
   // splits the edge (EDGE_NOSPLIT: none); valid when masks_valid
   Buf edm, eef, edm_alt, eef_alt;
+  Buf xs;                // per-XCD shards of the connect phase (step.h XS_*)
+  bool xs_clean = false;
   bool masks_valid = false;
   int mask_from = 0;       // plane the stored first split planes start at
   uint64_t act_bits = 0;   // OR of the edges' first split planes (bit p: plane p splits an edge)
@@ -432,7 +434,7 @@ extern "C" void tnp_engine_destroy(tnp_engine* e) {
                  &e->ent_v, &e->ents, &e->pcell, &e->ptoff, &e->bcell,
                  &e->ckeys_a, &e->ckeys_b, &e->sort_scr, &e->flags, &e->used, &e->nid,
                  &e->ctr, &e->tri, &e->faces, &e->lb[0], &e->lb[1], &e->edm, &e->eef,
-                 &e->edm_alt, &e->eef_alt, &e->live, &e->tied_table};
+                 &e->edm_alt, &e->eef_alt, &e->live, &e->tied_table, &e->xs};
   for (Buf* b : bufs) buf_free(*b, s);
   for (Buf& b : e->fscr) buf_free(b, s);
   for (Buf& b : e->fscr2) buf_free(b, s);
@@ -1060,23 +1062,27 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   // connecting edges this step's pruning drops are never appended (sorted,
   // re-tested): keep_edge() depends on the endpoints only
   const uint64_t cfmask = prune ? prune_mask(idx, K - 1) : 0ull;
+  // the kept keys go to XS_N per-XCD regions of cap / XS_N keys (step.h)
   int64_t cap = std::max<int64_t>(e->ckeys_a.bytes / sizeof(uint64_t), 4 * M + 1024);
+  cap = (cap + XS_N - 1) / XS_N * XS_N;
+  if (buf_ensure(e->xs, XS_WORDS * sizeof(int64_t), s)) return -1;
   int64_t X = 0, TT = 0;
   bool chunks_ok = false;  // (radix path) the chunk table matches the pair cells
   for (int attempt = 0; attempt < 3; ++attempt) {
     if (buf_ensure(e->ckeys_a, std::max<int64_t>(cap, 1) * sizeof(uint64_t), s)) return -1;
     if (attempt > 0) {  // the split zeroed the whole counter block
-      TNP_CHECK(hipMemsetAsync(ctr + CTR_X, 0, sizeof(int64_t), s));
-      TNP_CHECK(hipMemsetAsync(ctr + CTR_XK, 0, sizeof(int64_t), s));
-      TNP_CHECK(hipMemsetAsync(ctr + CTR_P, 0, 2 * sizeof(int64_t), s));  // CTR_P, CTR_COMPAT
       TNP_CHECK(hipMemsetAsync(ctr + CTR_BOVF, 0, sizeof(int64_t), s));
       TNP_CHECK(hipMemsetAsync(ctr + CTR_TK1, 0, sizeof(int64_t), s));
     }
+    // the shards are left zero by k_keys_finish; cleared here after an
+    // aborted step or on fresh memory
+    if (!e->xs_clean) TNP_CHECK(hipMemsetAsync(e->xs.p, 0, XS_WORDS * sizeof(int64_t), s));
+    e->xs_clean = false;
     if (buckets) {
       // in-bucket grouping + the window pass over each bucket (cells of <=
       // WCELL members) + pair-cell lists and k_connect's chunk table (bcap)
       if (buf_ensure(e->bcell, bcap * sizeof(int32_t), s)) return -1;
-      const ConnectWin cw{idx, nb, cfmask, P<uint64_t>(e->ckeys_a), cap};
+      const ConnectWin cw{idx, nb, cfmask, P<uint64_t>(e->ckeys_a), cap, P<int64_t>(e->xs)};
       TIMED("bucket_group", 0.0,
             launch_bucket_pairs(e->net.n_marks, P<int64_t>(e->bk[2]), P<uint64_t>(e->sents),
                                 P<uint64_t>(c.pz), P<CellEnt>(e->ents),
@@ -1098,8 +1104,10 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     TIMED("connect", 0.0,
           launch_connect(P<int64_t>(e->ptoff), P<int32_t>(e->pcell), P<int32_t>(e->pcn),
                          P<int32_t>(e->pent), NC, e->max_pair_tests, P<int32_t>(e->bcell),
-                         P<CellEnt>(e->ents), idx, nb, cfmask, P<uint64_t>(e->ckeys_a), cap, ctr,
-                         s));
+                         P<CellEnt>(e->ents), idx, nb, cfmask, P<uint64_t>(e->ckeys_a), cap, P<int64_t>(e->xs),
+                         ctr, s));
+    if (launch_keys_finish(P<int64_t>(e->xs), cap, ctr, s)) return -1;
+    e->xs_clean = true;
     if (read_ctr(e, s)) return -1;
     if (buckets) {
       if (e->h_ctr[CTR_K0]) {
@@ -1146,11 +1154,14 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     return -1;
   }
   if (buf_ensure(e->ckeys_b, std::max<int64_t>(X, 1) * sizeof(uint64_t), s)) return -1;
+  // the regions concatenated (a, per-XCD -> b), then sorted (b <-> a)
+  TIMED("keys_compact", 16.0 * X,
+        launch_keys_compact(P<uint64_t>(e->ckeys_a), cap, P<int64_t>(e->xs), X, P<uint64_t>(e->ckeys_b), s));
   {
     size_t need = sort_scratch_bytes(X, 2 * nb);
     if (buf_ensure(e->sort_scr, std::max<size_t>(need, 16), s)) return -1;
     TIMED("pair_sort", 16.0 * X * ((2 * nb + 7) / 8),
-          sort_keys_u64(P<uint64_t>(e->ckeys_a), P<uint64_t>(e->ckeys_b), X, 2 * nb, e->sort_scr.p,
+          sort_keys_u64(P<uint64_t>(e->ckeys_b), P<uint64_t>(e->ckeys_a), X, 2 * nb, e->sort_scr.p,
                         e->sort_scr.bytes, &e->ckeys, s));
   }
 

@@ -153,7 +153,7 @@ int launch_chunk_cells(const int64_t* ptoff, const int32_t* pn, int64_t rcap, in
 int launch_connect(const int64_t* ptoff, const int32_t* pcell, const int32_t* pn,
                    const int32_t* pent, int NC, int64_t max_tests, const int32_t* bcell,
                    const CellEnt* ent, int idx, int nb, uint64_t fmask, uint64_t* keys,
-                   int64_t cap, int64_t* ctr, hipStream_t s);
+                   int64_t cap, int64_t* xs, int64_t* ctr, hipStream_t s);
 // single-pass pruning over [edges; e_new; c_new] (lb_tiles(E + S + X)
 // look-back tiles): kept edges in order -> out, used flags (zeroed by the
 // caller), ctr[CTR_E], ctr[CTR_ACTIVE]
@@ -213,11 +213,33 @@ int launch_bucket_entries(const int32_t* members, int64_t S, int64_t V, int64_t 
 // bcount/bcur zeroed for the next step.
 // win != null: the grouping kernel also runs the window pass (launch_connect_win's
 // work) over each bucket's records; uses ctr[CTR_TK1] on small grids
+// Per-XCD shards of the connect phase's appends and pair statistics.  One
+// device-scope atomic per workgroup (or per wave flush) on ONE word
+// serialises at ~11 ns (MI355X_MICROARCH.md fan-in: ~88 per microsecond);
+// shard x = blockIdx.x % 8 (the dispatcher's XCD) has a 128-B line per
+// counter and its own key region keys[x * rc, (x + 1) * rc), rc = cap / 8.
+// k_keys_finish folds the shards into ctr and the regions' output offsets;
+// k_keys_compact concatenates the regions.
+constexpr int XS_N = 8;      // shards
+constexpr int XS_LINE = 16;  // int64 words per counter line
+enum { XS_KEYS = 0, XS_COMPAT = 1, XS_P = 2, XS_X = 3, XS_STATS = 4 };
+__host__ __device__ constexpr int xs_word(int stat, int shard) { return (stat * XS_N + shard) * XS_LINE; }
+constexpr int XS_OFF = XS_STATS * XS_N * XS_LINE;  // + [0, XS_N]: region output offsets
+constexpr int XS_WORDS = XS_OFF + 2 * XS_LINE;
+// counts of the shards -> ctr[CTR_XK] (all keys, or XS_N x the largest
+// region count when a region overflowed: the caller grows cap to it and
+// redoes), ctr[CTR_COMPAT / CTR_P / CTR_X]; region offsets; shards zeroed
+int launch_keys_finish(int64_t* xs, int64_t cap, int64_t* ctr, hipStream_t s);
+// the X keys of the regions, concatenated in shard order -> out
+int launch_keys_compact(const uint64_t* keys, int64_t cap, const int64_t* xs, int64_t X, uint64_t* out,
+                        hipStream_t s);
+
 struct ConnectWin {
   int idx, nb;
   uint64_t fmask;
   uint64_t* keys;
   int64_t cap;
+  int64_t* xs;
 };
 int launch_bucket_pairs(int n_marks, const int64_t* bbase, const uint64_t* ekv, const uint64_t* pz,
                         CellEnt* ents, int32_t* lcell,
@@ -232,7 +254,7 @@ int64_t connect_chunk_pairs();
 // pair of a cell of <= WCELL members, same emission rules and counters as
 // launch_connect
 int launch_connect_win(const CellEnt* ent, int idx, int nb, uint64_t fmask, uint64_t* keys, int64_t cap,
-                       int64_t* ctr, hipStream_t s);
+                       int64_t* xs, int64_t* ctr, hipStream_t s);
 
 // ---- sort.hip ----
 // ascending LSD radix sort of n u64 keys on bits [0, bits); the sorted keys

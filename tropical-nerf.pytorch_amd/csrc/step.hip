@@ -56,7 +56,7 @@ __host__ __device__ constexpr int split_ipt(int64_t n) { return n >= SIPT_BIG_FR
 constexpr int SIPT = 16;  // the radix path's run-start pass
 constexpr int STILE = TNP_BLOCK * SIPT;
 #ifndef TNP_LIPT
-#define TNP_LIPT 8
+#define TNP_LIPT 16  // 16: half the look-back tickets of 8 (one returning atomic per tile on one word)
 #endif
 constexpr int LIPT = TNP_LIPT;
 constexpr int LTILE = TNP_BLOCK * LIPT;
@@ -566,7 +566,7 @@ k_connect(const int64_t* __restrict__ ptoff, const int32_t* __restrict__ pcell,
           const int32_t* __restrict__ pn, const int32_t* __restrict__ pent, int NC,
           int64_t max_tests, const int32_t* __restrict__ bcell, const CellEnt* __restrict__ ent,
           int idx, int nb, uint64_t fmask, uint64_t* __restrict__ keys, int64_t cap,
-          int64_t* __restrict__ ctr) {
+          int64_t* __restrict__ xs, int64_t* __restrict__ ctr) {
   __shared__ int64_t lds[TNP_WAVES];
   __shared__ int64_t s_base;
   __shared__ int32_t s_off[CONNECT_CELLS];  // first pair of the cell - chunk start
@@ -685,29 +685,71 @@ k_connect(const int64_t* __restrict__ ptoff, const int32_t* __restrict__ pcell,
 #endif
   int64_t tot;
   int64_t off = tnp::block_scan_excl((int64_t)ne, lds, tot);
-  if (threadIdx.x == 0) s_base = tot ? (int64_t)atomicAdd((unsigned long long*)&ctr[CTR_XK], (unsigned long long)tot) : 0;
+  const int sh = blockIdx.x % XS_N;
+  const int64_t rc = cap / XS_N;
+  if (threadIdx.x == 0)
+    s_base = tot ? (int64_t)atomicAdd((unsigned long long*)&xs[xs_word(XS_KEYS, sh)], (unsigned long long)tot) : 0;
   __syncthreads();
   const int64_t w0 = s_base + off;
   for (int k = 0; k < ne; ++k)
-    if (w0 + k < cap) keys[w0 + k] = kk[k];
+    if (w0 + k < rc) keys[sh * rc + w0 + k] = kk[k];
   }
-  add_pair_stats(n_compat, n_reg, n_conn, lds, ctr);
+  add_pair_stats(n_compat, n_reg, n_conn, lds, xs);
 }
 
 // the window pass over every cell-contiguous entry (connect.h window_pass);
 // the bucket path runs it inside its grouping kernel instead
 __global__ void __launch_bounds__(TNP_BLOCK)
 k_connect_win(const CellEnt* __restrict__ ent, int idx, int nb, uint64_t fmask,
-              uint64_t* __restrict__ keys, int64_t cap, int64_t* __restrict__ ctr) {
+              uint64_t* __restrict__ keys, int64_t cap, int64_t* __restrict__ xs, int64_t* __restrict__ ctr) {
   __shared__ WinLds W;
   __shared__ int64_t lds[TNP_WAVES];
   const int64_t T = ctr[CTR_T];
   WinAcc a;
   const uint64_t below = (idx >= 64) ? ~0ull : ((1ull << idx) - 1ull);
   window_pass(ent, 0, T, (int64_t)blockIdx.x * TNP_WAVES + tnp::wave(), (int64_t)gridDim.x * TNP_WAVES,
-              below, nb, fmask, keys, cap, ctr, W, a);
-  window_flush(keys, cap, ctr, W, a);
-  add_pair_stats(a.n_compat, a.n_reg, a.n_conn, lds, ctr);
+              below, nb, fmask, keys, cap, xs, W, a);
+  window_flush(keys, cap, xs, W, a);
+  add_pair_stats(a.n_compat, a.n_reg, a.n_conn, lds, xs);
+}
+
+// the shards -> ctr and the regions' output offsets; shards zeroed for the
+// next step (one wave)
+__global__ void k_keys_finish(int64_t* __restrict__ xs, int64_t cap, int64_t* __restrict__ ctr) {
+  const int L = threadIdx.x;
+  const int64_t rc = cap / XS_N;
+  const int64_t c = L < XS_N ? xs[xs_word(XS_KEYS, L)] : 0;
+  const int64_t incl = tnp::wave_scan_incl(c);
+  if (L <= XS_N) xs[XS_OFF + L] = incl - c;  // lane XS_N: the total
+  int64_t mx = c;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
+  const int64_t total = __shfl(incl, 63, 64);
+  int64_t st[3];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) st[q] = tnp::wave_sum(L < XS_N ? xs[xs_word(XS_COMPAT + q, L)] : (int64_t)0);
+  if (L == 0) {
+    ctr[CTR_XK] = mx > rc ? mx * XS_N : total;  // overflow: the capacity every region needs
+    ctr[CTR_COMPAT] = st[0];
+    ctr[CTR_P] = st[1];
+    ctr[CTR_X] = st[2];
+  }
+  if (L < XS_N * XS_STATS) xs[xs_word(L / XS_N, L % XS_N)] = 0;
+}
+
+// out[i] = the i-th key of the regions in shard order
+__global__ void k_keys_compact(const uint64_t* __restrict__ keys, int64_t cap, const int64_t* __restrict__ xs,
+                               int64_t X, uint64_t* __restrict__ out) {
+  const int64_t rc = cap / XS_N;
+  int64_t off[XS_N];
+#pragma unroll
+  for (int r = 0; r < XS_N; ++r) off[r] = xs[XS_OFF + r];
+  for (int64_t i = (int64_t)blockIdx.x * TNP_BLOCK + threadIdx.x; i < X; i += (int64_t)gridDim.x * TNP_BLOCK) {
+    int r = 0;
+#pragma unroll
+    for (int q = 1; q < XS_N; ++q) r += off[q] <= i;
+    out[i] = keys[r * rc + (i - off[r])];
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1195,18 +1237,31 @@ int launch_chunk_cells(const int64_t* ptoff, const int32_t* pn, int64_t rcap, in
 int launch_connect(const int64_t* ptoff, const int32_t* pcell, const int32_t* pn,
                    const int32_t* pent, int NC, int64_t max_tests, const int32_t* bcell,
                    const CellEnt* ent, int idx, int nb, uint64_t fmask, uint64_t* keys,
-                   int64_t cap, int64_t* ctr, hipStream_t s) {
+                   int64_t cap, int64_t* xs, int64_t* ctr, hipStream_t s) {
   static_assert(CONNECT_CELLS >= CCH + 2, "chunk cell window");
   const int grid = connect_grid_size();
   hipLaunchKernelGGL(k_connect, dim3(grid), dim3(TNP_BLOCK), 0, s, ptoff, pcell, pn,
-                     pent, NC, max_tests, bcell, ent, idx, nb, fmask, keys, cap, ctr);
+                     pent, NC, max_tests, bcell, ent, idx, nb, fmask, keys, cap, xs, ctr);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
 int launch_connect_win(const CellEnt* ent, int idx, int nb, uint64_t fmask, uint64_t* keys, int64_t cap,
-                       int64_t* ctr, hipStream_t s) {
+                       int64_t* xs, int64_t* ctr, hipStream_t s) {
   const int grid = connect_grid_size();
-  hipLaunchKernelGGL(k_connect_win, dim3(grid), dim3(TNP_BLOCK), 0, s, ent, idx, nb, fmask, keys, cap, ctr);
+  hipLaunchKernelGGL(k_connect_win, dim3(grid), dim3(TNP_BLOCK), 0, s, ent, idx, nb, fmask, keys, cap, xs, ctr);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_keys_finish(int64_t* xs, int64_t cap, int64_t* ctr, hipStream_t s) {
+  hipLaunchKernelGGL(k_keys_finish, dim3(1), dim3(64), 0, s, xs, cap, ctr);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_keys_compact(const uint64_t* keys, int64_t cap, const int64_t* xs, int64_t X, uint64_t* out,
+                        hipStream_t s) {
+  if (X <= 0) return 0;
+  const unsigned g = (unsigned)std::min<int64_t>(tnp_grid(X), 4096);
+  hipLaunchKernelGGL(k_keys_compact, dim3(g), dim3(TNP_BLOCK), 0, s, keys, cap, xs, X, out);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
@@ -1270,7 +1325,9 @@ int launch_publish(const int64_t* ctr, int64_t* host, int64_t seq, hipStream_t s
 
 int launch_count_flags(const uint8_t* f, int64_t n, int64_t* ctr, int slot, hipStream_t s) {
   if (n <= 0) return 0;
-  const unsigned g = (unsigned)std::min<int64_t>(2048, (n + 16 * TNP_BLOCK - 1) / (16 * TNP_BLOCK));
+  // one device-scope atomic per workgroup on one word: they serialise at
+  // ~11 ns each (MI355X_MICROARCH.md fan-in), so few workgroups that loop
+  const unsigned g = (unsigned)std::min<int64_t>(256, (n + 16 * TNP_BLOCK - 1) / (16 * TNP_BLOCK));
   hipLaunchKernelGGL(k_count_flags, dim3(g), dim3(TNP_BLOCK), 0, s, f, n, ctr, slot);
   TNP_CHECK(hipGetLastError());
   return 0;
