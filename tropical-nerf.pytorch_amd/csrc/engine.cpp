@@ -805,11 +805,9 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
       // only the cached column and the live flags), so one readback returns
       // S and H; members holds [V, V+S) ++ hits, S <= E
       if (buf_ensure(e->members, (e->E + e->V) * sizeof(int32_t), s)) return -1;
-      TnpLB lh;
-      if (lb_begin(e, split_tiles(e->V), s, &lh)) return -1;
-      TIMED("hits", 8.0 * e->V,
+      TIMED("hits", 5.0 * e->V,
             launch_hits(col, P<uint8_t>(e->live), e->V, eps, P<int32_t>(e->members), -1,
-                        P<int64_t>(e->ctr), lh, s));
+                        P<int64_t>(e->ctr), s));
       e->pend_hits = true;
     }
     if (read_ctr(e, s)) return -1;
@@ -927,16 +925,14 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
                               P<uint64_t>(c.pz), s));
   }
 
-  // 2. members = new vertices ++ live hit vertices (ascending); the bucket
+  // 2. members = new vertices ++ live hit vertices (any order); the bucket
   //    path reads the new vertices as slots V.. without a list
   if (buf_ensure(e->members, std::max<int64_t>(NV, 1) * sizeof(int32_t), s, hits_done)) return -1;
   if (hits_done) {
     if (!buckets && launch_new_members(P<int32_t>(e->members), S, V, s)) return -1;
   } else {
-    TnpLB lb;
-    if (V > 0 && lb_begin(e, split_tiles(V), s, &lb)) return -1;
-    TIMED("hits", 8.0 * V + 4.0 * S,
-          launch_hits(col, P<uint8_t>(e->live), V, eps, P<int32_t>(e->members), S, ctr, lb, s));
+    TIMED("hits", 5.0 * V + 4.0 * S,
+          launch_hits(col, P<uint8_t>(e->live), V, eps, P<int32_t>(e->members), S, ctr, s));
   }
 
   // 3. bucket members by grid cell (dense cell grid over the marks): one

@@ -66,12 +66,12 @@ int launch_fail_check(const int32_t* sa, const int32_t* sb, int64_t S, int idx,
 int launch_finalize_new(int64_t S, int K, int override_, const uint64_t* shared, float* stage,
                         float eps, float* pre, int64_t ld, int keep_from, int64_t V, uint64_t* pos,
                         uint64_t* zero, const int64_t* ctr, uint64_t* pz, hipStream_t s);
-// members = [V, V + S) ++ live vertices v < V with |col[v]| < eps (ascending,
-// single pass over split_tiles(V) look-back tiles); count -> ctr[CTR_H].
+// members = [V, V + S) ++ live vertices v < V with |col[v]| < eps (in no
+// particular order: atomic appends); count -> ctr[CTR_H] (zero on entry).
 // S < 0: the hits only, placed after ctr[CTR_S] members (launched behind
 // the split kernel; launch_new_members fills [0, S) once S is known)
 int launch_hits(const float* col, const uint8_t* alive, int64_t V, float eps, int32_t* members,
-                int64_t S, int64_t* ctr, const TnpLB& lb, hipStream_t s);
+                int64_t S, int64_t* ctr, hipStream_t s);
 int launch_new_members(int32_t* members, int64_t S, int64_t V, hipStream_t s);
 // sort-based cell bucketing: span counts (+ A), (cell, member) entries,
 // segment bounds of the cell-sorted entries, per-cell counts, key copies

@@ -204,61 +204,68 @@ __global__ void k_finalize_new(int64_t S, int K, int override_, const uint64_t* 
 }
 
 // ---------------------------------------------------------------------------
-// hit vertices: |outputs_[:, idx]| < eps (subpoly.py:233), ascending order
+// hit vertices: |outputs_[:, idx]| < eps (subpoly.py:233)
 // ---------------------------------------------------------------------------
-// single pass (decoupled look-back): live vertices on the plane, ascending,
-// appended after the S new members; the last tile writes the count to
-// ctr[CTR_H].  alive: the live-slot flags of the lazily compacted vertex set
-template <int SI>
+// live vertices on the plane, appended after the S new members in no
+// particular order (every consumer is order-free: the bucket / cell grouping
+// keeps arbitrary in-cell order and the emitted edges are sorted), count ->
+// ctr[CTR_H] (zero on entry).  A fixed grid of workgroups walks the slots in
+// chunks, collects its hits in LDS and appends them with one device atomic
+// per flush: no tickets, no look-back (one returning atomic per workgroup on
+// one word serialises chip-wide).  alive: the live-slot flags of the lazily
+// compacted vertex set.
+constexpr int HIPT = 16;                    // slots per thread per chunk
+constexpr int HCHUNK = TNP_BLOCK * HIPT;    // slots per chunk
+constexpr int HBUF = 2 * HCHUNK;            // LDS hit buffer (a chunk always fits after a flush)
+constexpr int HIT_GRID = 512;
+
 __global__ void __launch_bounds__(TNP_BLOCK)
-k_hit_lb(const float* __restrict__ col, const uint8_t* __restrict__ alive, int64_t V,
-         int64_t ntiles, float eps, int32_t* __restrict__ members, int64_t S_arg,
-         int64_t* __restrict__ ctr, TnpLB lb) {
-  __shared__ int cnt[SI][TNP_WAVES];
-  __shared__ int64_t slot;
+k_hit_append(const float* __restrict__ col, const uint8_t* __restrict__ alive, int64_t V, float eps,
+             int32_t* __restrict__ members, int64_t S_arg, int64_t* __restrict__ ctr) {
+  __shared__ int32_t hb[HBUF];
+  __shared__ int hn;
+  __shared__ int64_t hbase;
   // S_arg < 0: launched right behind the split, whose count is on the device
   const int64_t S = S_arg < 0 ? ctr[CTR_S] : S_arg;
-  const int64_t tile = tnp::lb_tile(lb, &slot);
-  const int64_t base = tile * (TNP_BLOCK * SI);
-  float c[SI];
-  uint8_t al[SI];
-  uint64_t bal[SI];
+  if (threadIdx.x == 0) hn = 0;
+  __syncthreads();
+  auto flush = [&]() {
+    const int n = hn;
+    if (n == 0) return;
+    if (threadIdx.x == 0) hbase = (int64_t)atomicAdd((unsigned long long*)&ctr[CTR_H], (unsigned long long)n);
+    __syncthreads();
+    for (int q = threadIdx.x; q < n; q += TNP_BLOCK) members[S + hbase + q] = hb[q];
+    __syncthreads();
+    if (threadIdx.x == 0) hn = 0;
+    __syncthreads();
+  };
+  for (int64_t base = (int64_t)blockIdx.x * HCHUNK; base < V; base += (int64_t)gridDim.x * HCHUNK) {
+    float c[HIPT];
+    uint8_t al[HIPT];
 #pragma unroll
-  for (int k = 0; k < SI; ++k) {  // unconditional (clamped) loads, all in flight
-    const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
-    const int64_t ic = i < V ? i : V - 1;
-    c[k] = col[ic];
-    al[k] = alive[ic];
-  }
+    for (int k = 0; k < HIPT; ++k) {  // unconditional (clamped) loads, all in flight
+      const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
+      const int64_t ic = i < V ? i : V - 1;
+      c[k] = col[ic];
+      al[k] = alive[ic];
+    }
 #pragma unroll
-  for (int k = 0; k < SI; ++k) {
-    const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
-    bal[k] = __ballot((i < V) && (fabsf(c[k]) < eps) && al[k]);
-    if (tnp::lane() == 0) cnt[k][tnp::wave()] = __popcll(bal[k]);
+    for (int k = 0; k < HIPT; ++k) {
+      const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
+      const bool h = (i < V) && (fabsf(c[k]) < eps) && al[k];
+      const uint64_t b = __ballot(h);
+      if (b) {
+        int w0 = 0;
+        if (tnp::lane() == 0) w0 = atomicAdd(&hn, __popcll(b));  // LDS
+        w0 = __shfl(w0, 0, 64);
+        if (h) hb[w0 + tnp::mbcnt(b)] = (int32_t)i;
+      }
+    }
+    __syncthreads();
+    if (hn > HBUF - HCHUNK) flush();
   }
   __syncthreads();
-  int64_t agg = 0;
-#pragma unroll
-  for (int k = 0; k < SI; ++k)
-#pragma unroll
-    for (int w = 0; w < TNP_WAVES; ++w) agg += cnt[k][w];
-  const int64_t prefix = tnp::lb_prefix(lb, tile, agg, &slot);
-  int64_t run = prefix;
-#pragma unroll
-  for (int k = 0; k < SI; ++k) {
-    int64_t off = run;
-    int tot = 0;
-#pragma unroll
-    for (int w = 0; w < TNP_WAVES; ++w) {
-      const int cc = cnt[k][w];
-      off += (w < tnp::wave()) ? cc : 0;
-      tot += cc;
-    }
-    if ((bal[k] >> tnp::lane()) & 1)
-      members[S + off + tnp::mbcnt(bal[k])] = (int32_t)(base + (int64_t)k * TNP_BLOCK + threadIdx.x);
-    run += tot;
-  }
-  if (tile == ntiles - 1 && threadIdx.x == 0) ctr[CTR_H] = prefix + agg;
+  flush();
 }
 
 __global__ void k_new_members(int32_t* __restrict__ members, int64_t S, int64_t V) {
@@ -1133,17 +1140,10 @@ int launch_finalize_new(int64_t S, int K, int override_, const uint64_t* shared,
   return 0;
 }
 int launch_hits(const float* col, const uint8_t* alive, int64_t V, float eps, int32_t* members,
-                int64_t S, int64_t* ctr, const TnpLB& lb, hipStream_t s) {
+                int64_t S, int64_t* ctr, hipStream_t s) {
   if (V > 0) {
-    const int64_t tiles = split_tiles(V);
-    if (split_ipt(V) == SIPT_BIG)
-      hipLaunchKernelGGL(k_hit_lb<SIPT_BIG>, dim3((unsigned)tiles), dim3(TNP_BLOCK), 0, s, col, alive, V,
-                         tiles, eps, members, S, ctr, lb);
-    else
-      hipLaunchKernelGGL(k_hit_lb<SIPT_SMALL>, dim3((unsigned)tiles), dim3(TNP_BLOCK), 0, s, col, alive, V,
-                         tiles, eps, members, S, ctr, lb);
-  } else {
-    TNP_CHECK(hipMemsetAsync(ctr + CTR_H, 0, sizeof(int64_t), s));
+    const unsigned g = (unsigned)std::min<int64_t>(HIT_GRID, (V + HCHUNK - 1) / HCHUNK);
+    hipLaunchKernelGGL(k_hit_append, dim3(g), dim3(TNP_BLOCK), 0, s, col, alive, V, eps, members, S, ctr);
   }
   if (S > 0) return launch_new_members(members, S, V, s);
   TNP_CHECK(hipGetLastError());
