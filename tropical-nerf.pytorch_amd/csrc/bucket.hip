@@ -62,7 +62,7 @@ struct WinArgs {
   uint64_t fmask;
   uint64_t* keys;
   int64_t cap;
-  int64_t* xs;  // per-XCD shards of the appends and pair statistics (step.h)
+  int64_t* xs;  // per-XCD shards of the appends and pair statistics (step.h); null: ctr
 };
 
 // the global pair-cell lists the fused last workgroup fills
@@ -538,9 +538,9 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
       WinAcc a;
       const uint64_t below = (wa.idx >= 64) ? ~0ull : ((1ull << wa.idx) - 1ull);
       window_pass(ents, base, base + n, tnp::wave(), TNP_WAVES, below, wa.nb, wa.fmask, wa.keys, wa.cap, wa.xs,
-                  W, a);
-      window_flush(wa.keys, wa.cap, wa.xs, W, a);
-      add_pair_stats(a.n_compat, a.n_reg, a.n_conn, lds, wa.xs);
+                  ctr, W, a);
+      window_flush(wa.keys, wa.cap, wa.xs, ctr, W, a);
+      add_pair_stats(a.n_compat, a.n_reg, a.n_conn, lds, wa.xs, ctr);
     }
   }
   if (!fuse || !tnp::last_block(&ctr[CTR_TK1], &last)) return;

@@ -41,20 +41,27 @@ __device__ __forceinline__ PairTest pair_test(uint64_t below, uint32_t fu, uint6
   return t;
 }
 
+// where the connect phase counts its appended keys and pair statistics:
+// this workgroup's XCD shard (xs != null: large grids, k_keys_finish folds
+// the shards into ctr) or the counter block itself (small grids: a few
+// hundred workgroups, no fold or concatenation launches)
+__device__ __forceinline__ int64_t* sink_word(int64_t* xs, int64_t* ctr, int stat) {
+  constexpr int slot[4] = {CTR_XK, CTR_COMPAT, CTR_P, CTR_X};
+  return xs ? &xs[xs_word(stat, blockIdx.x % XS_N)] : &ctr[slot[stat]];
+}
+
 // a block's (compatible pairs, shared regions, connecting edges) totals
-//   -> its XCD shard of each (three adds per block; k_keys_finish sums them
-//   into ctr[CTR_COMPAT], ctr[CTR_P], ctr[CTR_X])
+//   -> ctr[CTR_COMPAT], ctr[CTR_P], ctr[CTR_X] (or their shards)
 __device__ __forceinline__ void add_pair_stats(int64_t a, int64_t r, int64_t x, int64_t* lds,
-                                               int64_t* __restrict__ xs) {
+                                               int64_t* __restrict__ xs, int64_t* __restrict__ ctr) {
   int64_t ta, tr, tx;
   tnp::block_scan_excl(a, lds, ta);
   tnp::block_scan_excl(r, lds, tr);
   tnp::block_scan_excl(x, lds, tx);
   if (threadIdx.x == 0) {
-    const int sh = blockIdx.x % XS_N;
-    if (ta) atomicAdd((unsigned long long*)&xs[xs_word(XS_COMPAT, sh)], (unsigned long long)ta);
-    if (tr) atomicAdd((unsigned long long*)&xs[xs_word(XS_P, sh)], (unsigned long long)tr);
-    if (tx) atomicAdd((unsigned long long*)&xs[xs_word(XS_X, sh)], (unsigned long long)tx);
+    if (ta) atomicAdd((unsigned long long*)sink_word(xs, ctr, XS_COMPAT), (unsigned long long)ta);
+    if (tr) atomicAdd((unsigned long long*)sink_word(xs, ctr, XS_P), (unsigned long long)tr);
+    if (tx) atomicAdd((unsigned long long*)sink_word(xs, ctr, XS_X), (unsigned long long)tx);
   }
 }
 
@@ -90,15 +97,17 @@ struct WinAcc {
   int64_t n_compat = 0, n_reg = 0, n_conn = 0;
 };
 
-// this wave's buffered keys -> its XCD shard's key region (counted there)
+// this wave's buffered keys -> its XCD shard's key region (xs != null) or
+// the one key array, counted there
 __device__ __forceinline__ void window_flush(uint64_t* __restrict__ keys, int64_t cap,
-                                             int64_t* __restrict__ xs, WinLds& W, WinAcc& a) {
+                                             int64_t* __restrict__ xs, int64_t* __restrict__ ctr, WinLds& W,
+                                             WinAcc& a) {
   if (a.kn == 0) return;
   const int wv = tnp::wave(), L = tnp::lane();
-  const int sh = blockIdx.x % XS_N;
-  const int64_t rc = cap / XS_N;
+  const int sh = xs ? blockIdx.x % XS_N : 0;
+  const int64_t rc = xs ? cap / XS_N : cap;
   int64_t base = 0;
-  if (L == 0) base = (int64_t)atomicAdd((unsigned long long*)&xs[xs_word(XS_KEYS, sh)], (unsigned long long)a.kn);
+  if (L == 0) base = (int64_t)atomicAdd((unsigned long long*)sink_word(xs, ctr, XS_KEYS), (unsigned long long)a.kn);
   base = __shfl(base, 0, 64);
   uint64_t* dst = keys + sh * rc;
   for (int i = L; i < a.kn; i += 64)
@@ -111,7 +120,8 @@ __device__ __forceinline__ void window_flush(uint64_t* __restrict__ keys, int64_
 __device__ __forceinline__ void window_pass(const CellEnt* __restrict__ ent, int64_t lo, int64_t hi,
                                             int64_t w0, int64_t dw, uint64_t below, int nb, uint64_t fmask,
                                             uint64_t* __restrict__ keys, int64_t cap,
-                                            int64_t* __restrict__ xs, WinLds& W, WinAcc& a) {
+                                            int64_t* __restrict__ xs, int64_t* __restrict__ ctr, WinLds& W,
+                                            WinAcc& a) {
   const int wv = tnp::wave(), L = tnp::lane();
   const int64_t nwin = (hi - lo + WSTRIDE - 1) / WSTRIDE;
   for (int64_t w = w0; w < nwin; w += dw) {
@@ -145,7 +155,7 @@ __device__ __forceinline__ void window_pass(const CellEnt* __restrict__ ent, int
       for (int r = 0, t = incl - rounds; r < rounds; ++r, ++t) W.own[wv][t] = (uint16_t)(L | ((L + 1 + r) << 8));
     lds_fence();
     for (int t0 = 0; t0 < total; t0 += 64) {
-      if (a.kn + 64 > WKEYS) window_flush(keys, cap, xs, W, a);
+      if (a.kn + 64 > WKEYS) window_flush(keys, cap, xs, ctr, W, a);
       const int t = t0 + L;
       bool em = false;
       uint64_t key = 0;

@@ -1058,27 +1058,33 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   // connecting edges this step's pruning drops are never appended (sorted,
   // re-tested): keep_edge() depends on the endpoints only
   const uint64_t cfmask = prune ? prune_mask(idx, K - 1) : 0ull;
-  // the kept keys go to XS_N per-XCD regions of cap / XS_N keys (step.h)
+  // the kept keys go to XS_N per-XCD regions of cap / XS_N keys (step.h) on
+  // grids of many bucket workgroups; small grids count in ctr directly
+  const bool shard = !buckets || NB > 512;
+  if (shard && buf_ensure(e->xs, XS_WORDS * sizeof(int64_t), s)) return -1;
+  int64_t* const xs = shard ? P<int64_t>(e->xs) : nullptr;
   int64_t cap = std::max<int64_t>(e->ckeys_a.bytes / sizeof(uint64_t), 4 * M + 1024);
   cap = (cap + XS_N - 1) / XS_N * XS_N;
-  if (buf_ensure(e->xs, XS_WORDS * sizeof(int64_t), s)) return -1;
   int64_t X = 0, TT = 0;
   bool chunks_ok = false;  // (radix path) the chunk table matches the pair cells
   for (int attempt = 0; attempt < 3; ++attempt) {
     if (buf_ensure(e->ckeys_a, std::max<int64_t>(cap, 1) * sizeof(uint64_t), s)) return -1;
     if (attempt > 0) {  // the split zeroed the whole counter block
+      TNP_CHECK(hipMemsetAsync(ctr + CTR_X, 0, sizeof(int64_t), s));
+      TNP_CHECK(hipMemsetAsync(ctr + CTR_XK, 0, sizeof(int64_t), s));
+      TNP_CHECK(hipMemsetAsync(ctr + CTR_P, 0, 2 * sizeof(int64_t), s));  // CTR_P, CTR_COMPAT
       TNP_CHECK(hipMemsetAsync(ctr + CTR_BOVF, 0, sizeof(int64_t), s));
       TNP_CHECK(hipMemsetAsync(ctr + CTR_TK1, 0, sizeof(int64_t), s));
     }
     // the shards are left zero by k_keys_finish; cleared here after an
     // aborted step or on fresh memory
-    if (!e->xs_clean) TNP_CHECK(hipMemsetAsync(e->xs.p, 0, XS_WORDS * sizeof(int64_t), s));
-    e->xs_clean = false;
+    if (shard && !e->xs_clean) TNP_CHECK(hipMemsetAsync(e->xs.p, 0, XS_WORDS * sizeof(int64_t), s));
+    if (shard) e->xs_clean = false;
     if (buckets) {
       // in-bucket grouping + the window pass over each bucket (cells of <=
       // WCELL members) + pair-cell lists and k_connect's chunk table (bcap)
       if (buf_ensure(e->bcell, bcap * sizeof(int32_t), s)) return -1;
-      const ConnectWin cw{idx, nb, cfmask, P<uint64_t>(e->ckeys_a), cap, P<int64_t>(e->xs)};
+      const ConnectWin cw{idx, nb, cfmask, P<uint64_t>(e->ckeys_a), cap, xs};
       TIMED("bucket_group", 0.0,
             launch_bucket_pairs(e->net.n_marks, P<int64_t>(e->bk[2]), P<uint64_t>(e->sents),
                                 P<uint64_t>(c.pz), P<CellEnt>(e->ents),
@@ -1100,10 +1106,11 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     TIMED("connect", 0.0,
           launch_connect(P<int64_t>(e->ptoff), P<int32_t>(e->pcell), P<int32_t>(e->pcn),
                          P<int32_t>(e->pent), NC, e->max_pair_tests, P<int32_t>(e->bcell),
-                         P<CellEnt>(e->ents), idx, nb, cfmask, P<uint64_t>(e->ckeys_a), cap, P<int64_t>(e->xs),
-                         ctr, s));
-    if (launch_keys_finish(P<int64_t>(e->xs), cap, ctr, s)) return -1;
-    e->xs_clean = true;
+                         P<CellEnt>(e->ents), idx, nb, cfmask, P<uint64_t>(e->ckeys_a), cap, xs, ctr, s));
+    if (shard) {
+      if (launch_keys_finish(xs, cap, ctr, s)) return -1;
+      e->xs_clean = true;
+    }
     if (read_ctr(e, s)) return -1;
     if (buckets) {
       if (e->h_ctr[CTR_K0]) {
@@ -1150,15 +1157,18 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     return -1;
   }
   if (buf_ensure(e->ckeys_b, std::max<int64_t>(X, 1) * sizeof(uint64_t), s)) return -1;
-  // the regions concatenated (a, per-XCD -> b), then sorted (b <-> a)
-  TIMED("keys_compact", 16.0 * X,
-        launch_keys_compact(P<uint64_t>(e->ckeys_a), cap, P<int64_t>(e->xs), X, P<uint64_t>(e->ckeys_b), s));
+  // sharded: the regions concatenated (a, per-XCD -> b), then sorted (b <-> a)
+  uint64_t* kin = P<uint64_t>(e->ckeys_a);
+  uint64_t* kalt = P<uint64_t>(e->ckeys_b);
+  if (shard) {
+    TIMED("keys_compact", 16.0 * X, launch_keys_compact(kin, cap, xs, X, kalt, s));
+    std::swap(kin, kalt);
+  }
   {
     size_t need = sort_scratch_bytes(X, 2 * nb);
     if (buf_ensure(e->sort_scr, std::max<size_t>(need, 16), s)) return -1;
     TIMED("pair_sort", 16.0 * X * ((2 * nb + 7) / 8),
-          sort_keys_u64(P<uint64_t>(e->ckeys_b), P<uint64_t>(e->ckeys_a), X, 2 * nb, e->sort_scr.p,
-                        e->sort_scr.bytes, &e->ckeys, s));
+          sort_keys_u64(kin, kalt, X, 2 * nb, e->sort_scr.p, e->sort_scr.bytes, &e->ckeys, s));
   }
 
   // 5. pruning over [edges; e_new; c_new] + vertex compaction

@@ -692,16 +692,16 @@ k_connect(const int64_t* __restrict__ ptoff, const int32_t* __restrict__ pcell,
 #endif
   int64_t tot;
   int64_t off = tnp::block_scan_excl((int64_t)ne, lds, tot);
-  const int sh = blockIdx.x % XS_N;
-  const int64_t rc = cap / XS_N;
+  const int sh = xs ? blockIdx.x % XS_N : 0;
+  const int64_t rc = xs ? cap / XS_N : cap;
   if (threadIdx.x == 0)
-    s_base = tot ? (int64_t)atomicAdd((unsigned long long*)&xs[xs_word(XS_KEYS, sh)], (unsigned long long)tot) : 0;
+    s_base = tot ? (int64_t)atomicAdd((unsigned long long*)sink_word(xs, ctr, XS_KEYS), (unsigned long long)tot) : 0;
   __syncthreads();
   const int64_t w0 = s_base + off;
   for (int k = 0; k < ne; ++k)
     if (w0 + k < rc) keys[sh * rc + w0 + k] = kk[k];
   }
-  add_pair_stats(n_compat, n_reg, n_conn, lds, xs);
+  add_pair_stats(n_compat, n_reg, n_conn, lds, xs, ctr);
 }
 
 // the window pass over every cell-contiguous entry (connect.h window_pass);
@@ -715,9 +715,9 @@ k_connect_win(const CellEnt* __restrict__ ent, int idx, int nb, uint64_t fmask,
   WinAcc a;
   const uint64_t below = (idx >= 64) ? ~0ull : ((1ull << idx) - 1ull);
   window_pass(ent, 0, T, (int64_t)blockIdx.x * TNP_WAVES + tnp::wave(), (int64_t)gridDim.x * TNP_WAVES,
-              below, nb, fmask, keys, cap, xs, W, a);
-  window_flush(keys, cap, xs, W, a);
-  add_pair_stats(a.n_compat, a.n_reg, a.n_conn, lds, xs);
+              below, nb, fmask, keys, cap, xs, ctr, W, a);
+  window_flush(keys, cap, xs, ctr, W, a);
+  add_pair_stats(a.n_compat, a.n_reg, a.n_conn, lds, xs, ctr);
 }
 
 // the shards -> ctr and the regions' output offsets; shards zeroed for the
