@@ -220,12 +220,15 @@ int launch_bucket_entries(const int32_t* members, int64_t S, int64_t V, int64_t 
 // counter and its own key region keys[x * rc, (x + 1) * rc), rc = cap / 8.
 // k_keys_finish folds the shards into ctr and the regions' output offsets;
 // k_keys_compact concatenates the regions.
-constexpr int XS_N = 8;      // shards
+#ifndef TNP_XS_N
+#define TNP_XS_N 8
+#endif
+constexpr int XS_N = TNP_XS_N;  // shards (<= 63: k_keys_finish folds them in one wave)
 constexpr int XS_LINE = 16;  // int64 words per counter line
 enum { XS_KEYS = 0, XS_COMPAT = 1, XS_P = 2, XS_X = 3, XS_STATS = 4 };
 __host__ __device__ constexpr int xs_word(int stat, int shard) { return (stat * XS_N + shard) * XS_LINE; }
 constexpr int XS_OFF = XS_STATS * XS_N * XS_LINE;  // + [0, XS_N]: region output offsets
-constexpr int XS_WORDS = XS_OFF + 2 * XS_LINE;
+constexpr int XS_WORDS = XS_OFF + 64 + 1;  // + the XS_N + 1 offsets
 // counts of the shards -> ctr[CTR_XK] (all keys, or XS_N x the largest
 // region count when a region overflowed: the caller grows cap to it and
 // redoes), ctr[CTR_COMPAT / CTR_P / CTR_X]; region offsets; shards zeroed

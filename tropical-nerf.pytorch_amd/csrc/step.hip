@@ -741,7 +741,7 @@ __global__ void k_keys_finish(int64_t* __restrict__ xs, int64_t cap, int64_t* __
     ctr[CTR_P] = st[1];
     ctr[CTR_X] = st[2];
   }
-  if (L < XS_N * XS_STATS) xs[xs_word(L / XS_N, L % XS_N)] = 0;
+  for (int q = L; q < XS_N * XS_STATS; q += 64) xs[xs_word(q / XS_N, q % XS_N)] = 0;
 }
 
 // out[i] = the i-th key of the regions in shard order
