@@ -191,6 +191,77 @@ __device__ __forceinline__ int64_t lb_prefix(const TnpLB& lb, int64_t tile, int6
   return r;
 }
 
+// Ticket-free variant: the tile is blockIdx.x, so no block takes a ticket
+// (one returning atomic per block on ONE word: they serialise, ~11 ns each,
+// a floor of tiles * 11 ns per launch).  Without tickets a predecessor tile
+// may belong to a block that is not running yet, so the look-back never
+// waits unboundedly: a predecessor still unpublished after `spin` polls has
+// its aggregate recomputed by the waiting wave through `tile_agg(t)` (called
+// by all 64 lanes of wave 0 with a wave-uniform t; returns the tile's
+// aggregate in every lane).  Deadlock-free for any dispatch order; with the
+// in-order dispatch the hardware actually does, the recompute is rare.
+template <class F>
+__device__ __forceinline__ int64_t lb_prefix_rc(const TnpLB& lb, int64_t tile, int64_t agg,
+                                                int64_t* slot, F&& tile_agg, int spin = 64) {
+  constexpr uint64_t VMASK = (1ull << 40) - 1ull;
+  const uint64_t tag = (uint64_t)(lb.epoch & 0x3FFFFFu) << 40;
+  if (threadIdx.x < 64) {
+    int64_t prefix = 0;
+    if (tile == 0) {
+      if (lane() == 0)
+        __hip_atomic_store(&lb.st[0], (2ull << 62) | tag | (uint64_t)agg, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      if (lane() == 0)
+        __hip_atomic_store(&lb.st[tile], (1ull << 62) | tag | (uint64_t)agg, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      int64_t w = tile - 1;
+      while (true) {
+        const int64_t t = w - lane();
+        int64_t val = 0;
+        uint64_t word = 0;
+        int flag = 2;  // before tile 0: an inclusive zero
+        if (t >= 0) {
+          for (int k = 0;; ++k) {
+            word = __hip_atomic_load(&lb.st[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            flag = ((word & (0x3FFFFFull << 40)) == tag) ? (int)(word >> 62) : 0;
+            val = (int64_t)(word & VMASK);
+            if (flag || k >= spin) break;
+            __builtin_amdgcn_s_sleep(1);
+          }
+        }
+        const uint64_t incl = __ballot(flag == 2);
+        const int first = incl ? __builtin_ctzll(incl) : 64;
+        const uint64_t upto = first >= 63 ? ~0ull : ((2ull << first) - 1ull);
+        uint64_t miss = __ballot(flag == 0) & upto;
+        while (miss) {  // unpublished predecessors: recompute their aggregates
+          const int l = __builtin_ctzll(miss);
+          miss &= miss - 1ull;
+          const int64_t v = tile_agg(w - l);
+          if (lane() == l) {
+            val = v;
+            // publish it as that tile's aggregate unless its owner has since
+            // published (so later waiters need not recompute it again)
+            atomicCAS((unsigned long long*)&lb.st[w - l], (unsigned long long)word,
+                      (unsigned long long)((1ull << 62) | tag | (uint64_t)v));
+          }
+        }
+        prefix += wave_sum((lane() <= first && t >= 0) ? val : (int64_t)0);
+        if (incl) break;
+        w -= 64;
+      }
+      if (lane() == 0)
+        __hip_atomic_store(&lb.st[tile], (2ull << 62) | tag | (uint64_t)(prefix + agg),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (threadIdx.x == 0) *slot = prefix;
+  }
+  __syncthreads();
+  int64_t r = *slot;
+  __syncthreads();
+  return r;
+}
+
 // ---------------------------------------------------------------------------
 // Packed per-vertex grid word (cell offsets + on-grid-plane flags).
 //   bits  0..15  offset x + 2      bits 48..50 zero flag per dim (on a mark)

@@ -255,7 +255,9 @@ static void ktimer_end(tnp_engine* e, int t, hipStream_t s) {
   } while (0)
 
 // look-back state `w` for a single-pass launch of `tiles` tiles (common.h TnpLB)
-static int lb_begin(tnp_engine* e, int64_t tiles, hipStream_t s, TnpLB* out, int w = 0) {
+// (`ticketed` false: the kernel numbers tiles by blockIdx and takes no ticket)
+static int lb_begin(tnp_engine* e, int64_t tiles, hipStream_t s, TnpLB* out, int w = 0,
+                    bool ticketed = true) {
   Buf& b = e->lb[w];
   size_t need = (size_t)(tiles + 1) * sizeof(uint64_t);
   if (need > b.bytes || !b.p) {
@@ -273,7 +275,7 @@ static int lb_begin(tnp_engine* e, int64_t tiles, hipStream_t s, TnpLB* out, int
   out->st = static_cast<uint64_t*>(b.p) + 1;
   out->tbase = e->lb_tickets[w];
   out->epoch = e->lb_epoch[w];
-  e->lb_tickets[w] += (uint64_t)tiles;
+  if (ticketed) e->lb_tickets[w] += (uint64_t)tiles;
   return 0;
 }
 
@@ -793,7 +795,7 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
     const int fresh = ensure_masks(e, idx, s);
     if (fresh < 0) return -1;
     TnpLB lb;
-    if (lb_begin(e, split_tiles(e->E), s, &lb)) return -1;
+    if (lb_begin(e, split_tiles(e->E), s, &lb, 0, false)) return -1;
     // algorithmic bytes: 1 B first split plane per edge; per split 8 B
     // endpoints, 4 B rewired id, 1 B stale mask (set once S is known)
     TIMED("split", 1.0 * e->E,
@@ -1195,7 +1197,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     if (buf_ensure(e->edm_alt, N1 * sizeof(uint8_t), s)) return -1;
     if (buf_ensure(e->eef_alt, N1 * sizeof(uint8_t), s)) return -1;
     TnpLB lb;
-    if (lb_begin(e, lb_tiles(N), s, &lb)) return -1;
+    if (lb_begin(e, lb_tiles(N), s, &lb, 0, false)) return -1;
     // old edges: 8 B ids + 1 B high plane + 1 B first split plane read; e_new /
     // c_new: 4 / 8 B ids + 32 B endpoint keys; kept edges: 10 B written + 2 B flags
     TIMED("prune", 10.0 * E + 36.0 * S + 40.0 * X,

@@ -59,6 +59,9 @@ constexpr int STILE = TNP_BLOCK * SIPT;
 #define TNP_LIPT 16  // 16: half the look-back tickets of 8 (one returning atomic per tile on one word)
 #endif
 constexpr int LIPT = TNP_LIPT;
+#ifndef TNP_PRUNE_SPIN
+#define TNP_PRUNE_SPIN 1024
+#endif
 constexpr int LTILE = TNP_BLOCK * LIPT;
 
 // ---------------------------------------------------------------------------
@@ -83,7 +86,7 @@ k_split_lb(int32_t* __restrict__ edges, int64_t E, int64_t ntiles, const uint8_t
            int32_t* __restrict__ sb, int64_t* __restrict__ ctr, int32_t* __restrict__ eidx, TnpLB lb) {
   __shared__ int cnt[SI][TNP_WAVES];
   __shared__ int64_t slot;
-  const int64_t tile = tnp::lb_tile(lb, &slot);
+  const int64_t tile = blockIdx.x;  // ticket-free look-back (lb_prefix_rc)
   const int64_t base = tile * (TNP_BLOCK * SI);
   uint64_t bal[SI];
   uint32_t fp[SI];
@@ -107,7 +110,23 @@ k_split_lb(int32_t* __restrict__ edges, int64_t E, int64_t ntiles, const uint8_t
   for (int k = 0; k < SI; ++k)
 #pragma unroll
     for (int w = 0; w < TNP_WAVES; ++w) agg += cnt[k][w];
-  const int64_t prefix = tnp::lb_prefix(lb, tile, agg, &slot);
+  // a predecessor tile not yet published: count its split edges (ef == idx)
+  // four bytes per load; tiles start on multiples of TNP_BLOCK * SI
+  const uint32_t rep = (uint32_t)idx * 0x01010101u;
+  auto tile_agg = [&](int64_t t) -> int64_t {
+    const int64_t b0 = t * (TNP_BLOCK * SI), b1 = b0 + TNP_BLOCK * SI < E ? b0 + TNP_BLOCK * SI : E;
+    int c = 0;
+    for (int64_t j = b0 + 4 * tnp::lane(); j < b1; j += 256) {
+      if (j + 4 <= b1) {
+        const uint32_t x = *reinterpret_cast<const uint32_t*>(ef + j) ^ rep;
+        c += ((x & 0xFFu) == 0) + ((x & 0xFF00u) == 0) + ((x & 0xFF0000u) == 0) + ((x >> 24) == 0);
+      } else {
+        for (int64_t q = j; q < b1; ++q) c += ef[q] == (uint8_t)idx;
+      }
+    }
+    return tnp::wave_sum((int64_t)c);
+  };
+  const int64_t prefix = tnp::lb_prefix_rc(lb, tile, agg, &slot, tile_agg);
   int64_t run = prefix;
 #pragma unroll
   for (int k = 0; k < SI; ++k) {
@@ -858,7 +877,7 @@ k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, int idx, uint64_t amask,
   __shared__ int cnt[LIPT][TNP_WAVES];
   __shared__ int64_t slot;
   __shared__ uint64_t acts[TNP_WAVES];
-  const int64_t tile = tnp::lb_tile(lb, &slot);
+  const int64_t tile = blockIdx.x;  // ticket-free look-back (lb_prefix_rc)
   const int64_t base = tile * LTILE;
   const int64_t last = (base + LTILE < N ? base + LTILE : N) - 1;  // last item of the tile
   // block-uniform source of the tile: all old edges / all e_new / all c_new
@@ -936,7 +955,24 @@ k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, int idx, uint64_t amask,
   for (int k = 0; k < LIPT; ++k)
 #pragma unroll
     for (int w = 0; w < TNP_WAVES; ++w) agg += cnt[k][w];
-  const int64_t prefix = tnp::lb_prefix(lb, tile, agg, &slot);
+  // a predecessor tile not yet published: count its kept edges item by item
+  auto tile_agg = [&](int64_t t) -> int64_t {
+    const int64_t b0 = t * LTILE, b1 = b0 + LTILE < N ? b0 + LTILE : N;
+    int c = 0;
+    for (int64_t i = b0 + tnp::lane(); i < b1; i += 64) {
+      uint32_t dd = (i < src.E) ? dm[i] : EDGE_STALE;
+      if (dd == EDGE_STALE) {
+        int ea, eb;
+        fetch_edge(src, i, ea, eb);
+        const ulonglong2 ka = pz[ea], kb = pz[eb];
+        dd = high_plane((ka.x ^ kb.x) | (ka.y ^ kb.y));
+      }
+      c += (int)dd > idx;
+    }
+    return tnp::wave_sum((int64_t)c);
+  };
+  // (its tiles publish tens of µs after dispatch: poll long before recomputing)
+  const int64_t prefix = tnp::lb_prefix_rc(lb, tile, agg, &slot, tile_agg, TNP_PRUNE_SPIN);
   int64_t run = prefix;
   int newly = 0;  // count_live: endpoints this thread marked live first
 #pragma unroll
