@@ -233,6 +233,27 @@ def test_tied_levels_layout(cuda, monkeypatch):
     assert runs[0][-1][:2] == (int(d["step_V"][-1]), int(d["step_E"][-1]))
 
 
+def test_lookback_recompute_path(cuda, monkeypatch):
+    """The split and the prune number tiles by blockIdx and, after a bounded
+    wait, recompute an unpublished predecessor tile's aggregate
+    (common.h lb_prefix_rc).  In-order dispatch makes that path rare, so
+    TNP_LB_SPIN=0 forces it on every unpublished predecessor: the per-step
+    states must stay bitwise the reference's."""
+    from tropical._engine import engine_for
+    d = load("synth32")
+    net = product_net(d, cuda)
+    runs = []
+    for spin in (None, "0"):
+        if spin is not None:
+            monkeypatch.setenv("TNP_LB_SPIN", spin)
+        eng = engine_for(net)
+        eng.lattice(keep_all=True)
+        runs.append(engine_steps(eng))
+    assert runs[0] == runs[1]
+    for g, V, E, s in zip(runs[1], d["step_V"], d["step_E"], d["step_sha"]):
+        assert (g[0], g[1], g[2]) == (V, E, s)
+
+
 @pytest.mark.parametrize("force", [True, False])
 def test_subpoly_step_rewrites_caller_edges(cuda, force):
     """subpoly.py:209-212: a splitting step rewrites the caller's edges[:, 1]

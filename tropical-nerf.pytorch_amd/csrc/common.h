@@ -133,6 +133,7 @@ struct TnpLB {
   uint64_t* st;
   uint64_t tbase;
   uint32_t epoch;
+  int32_t spin;  // lb_prefix_rc polls before recomputing; < 0: the kernel's default
 };
 
 __device__ __forceinline__ int64_t lb_tile(const TnpLB& lb, int64_t* slot) {
@@ -205,6 +206,7 @@ __device__ __forceinline__ int64_t lb_prefix_rc(const TnpLB& lb, int64_t tile, i
                                                 int64_t* slot, F&& tile_agg, int spin = 64) {
   constexpr uint64_t VMASK = (1ull << 40) - 1ull;
   const uint64_t tag = (uint64_t)(lb.epoch & 0x3FFFFFu) << 40;
+  if (lb.spin >= 0) spin = lb.spin;
   if (threadIdx.x < 64) {
     int64_t prefix = 0;
     if (tile == 0) {

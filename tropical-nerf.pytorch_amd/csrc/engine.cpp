@@ -182,6 +182,7 @@ struct tnp_engine {
   Buf lb[2];
   uint64_t lb_tickets[2] = {0, 0};
   uint32_t lb_epoch[2] = {0, 0};
+  int32_t lb_spin = -1;  // TNP_LB_SPIN: ticket-free look-back polls (0 forces the recompute path)
   Buf fscr[12];
   Buf fscr2[32];
   Buf sents;                // bucket-ordered packed entries before the in-bucket grouping
@@ -275,6 +276,7 @@ static int lb_begin(tnp_engine* e, int64_t tiles, hipStream_t s, TnpLB* out, int
   out->st = static_cast<uint64_t*>(b.p) + 1;
   out->tbase = e->lb_tickets[w];
   out->epoch = e->lb_epoch[w];
+  out->spin = e->lb_spin;
   if (ticketed) e->lb_tickets[w] += (uint64_t)tiles;
   return 0;
 }
@@ -406,6 +408,7 @@ extern "C" int tnp_engine_create(tnp_engine** out, int device) {
   e->device = device;
   if (const char* lim = getenv("TNP_MAX_PAIR_TESTS")) e->max_pair_tests = atoll(lim);
   if (const char* rc = getenv("TNP_RADIX_CELLS")) e->radix_cells = atoi(rc) != 0;
+  if (const char* sp = getenv("TNP_LB_SPIN")) e->lb_spin = atoi(sp);
   if (hipHostMalloc((void**)&e->h_ctr, CTR_N * sizeof(int64_t), hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc((void**)&e->h_map, 32 * sizeof(int64_t), hipHostMallocMapped | hipHostMallocCoherent) !=
           hipSuccess ||

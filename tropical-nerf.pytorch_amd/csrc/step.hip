@@ -59,6 +59,9 @@ constexpr int STILE = TNP_BLOCK * SIPT;
 #define TNP_LIPT 16  // 16: half the look-back tickets of 8 (one returning atomic per tile on one word)
 #endif
 constexpr int LIPT = TNP_LIPT;
+#ifndef TNP_SPLIT_SPIN  // look-back polls before recomputing (0: recompute at once; tests)
+#define TNP_SPLIT_SPIN 64
+#endif
 #ifndef TNP_PRUNE_SPIN
 #define TNP_PRUNE_SPIN 1024
 #endif
@@ -126,7 +129,7 @@ k_split_lb(int32_t* __restrict__ edges, int64_t E, int64_t ntiles, const uint8_t
     }
     return tnp::wave_sum((int64_t)c);
   };
-  const int64_t prefix = tnp::lb_prefix_rc(lb, tile, agg, &slot, tile_agg);
+  const int64_t prefix = tnp::lb_prefix_rc(lb, tile, agg, &slot, tile_agg, TNP_SPLIT_SPIN);
   int64_t run = prefix;
 #pragma unroll
   for (int k = 0; k < SI; ++k) {
