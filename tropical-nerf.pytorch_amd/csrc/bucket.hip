@@ -36,7 +36,10 @@
 
 namespace {
 
-constexpr int BK_IPT = 8;  // members per thread in the member passes
+#ifndef TNP_BK_IPT
+#define TNP_BK_IPT 4
+#endif
+constexpr int BK_IPT = TNP_BK_IPT;  // members per thread in the member passes
 // grids up to this many workgroups finish their scans in the last workgroup
 // (one launch less); larger ones pay more in every workgroup's tail
 // (measured at 128^3: 4,913 buckets +0.26 ms per pass) and scan in a launch
@@ -493,8 +496,11 @@ __device__ __forceinline__ void group_bucket(const BGeom& G, int b, int64_t base
   }
 }
 
+#ifndef TNP_BG_MINB
+#define TNP_BG_MINB 1
+#endif
 template <int SH>
-__global__ void __launch_bounds__(TNP_BLOCK)
+__global__ void __launch_bounds__(TNP_BLOCK, TNP_BG_MINB)
 k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __restrict__ ekv,
                const ulonglong2* __restrict__ pz, CellEnt* __restrict__ ents,
                int32_t* __restrict__ lcell, int32_t* __restrict__ lent, int32_t* __restrict__ ln,

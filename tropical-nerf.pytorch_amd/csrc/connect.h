@@ -77,7 +77,10 @@ __device__ __forceinline__ void add_pair_stats(int64_t a, int64_t r, int64_t x, 
 // is read once from memory per window; emitted keys go through a per-wave LDS
 // buffer, one global append per WKEYS.
 // ---------------------------------------------------------------------------
-constexpr int WKEYS = 384;
+#ifndef TNP_WKEYS
+#define TNP_WKEYS 384
+#endif
+constexpr int WKEYS = TNP_WKEYS;
 
 
 __device__ __forceinline__ void lds_fence() {
