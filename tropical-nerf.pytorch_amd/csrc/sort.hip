@@ -8,11 +8,19 @@
 #include "common.h"
 #include "step.h"
 
+// rocPRIM sorts up to 1 M keys by block sort + merge passes (a dozen launches
+// for 2 M keys); the connecting-edge keys go to onesweep above this size
+#ifndef TNP_SORT_MERGE_LIMIT
+#define TNP_SORT_MERGE_LIMIT (256 * 1024)
+#endif
+using KeySortCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                              rocprim::default_config, TNP_SORT_MERGE_LIMIT>;
+
 size_t sort_scratch_bytes(int64_t n, int bits) {
   size_t bytes = 0;
   rocprim::double_buffer<uint64_t> db(nullptr, nullptr);
-  if (rocprim::radix_sort_keys(nullptr, bytes, db, (size_t)std::max<int64_t>(n, 1), 0u,
-                               (unsigned)bits) != hipSuccess)
+  if (rocprim::radix_sort_keys<KeySortCfg>(nullptr, bytes, db, (size_t)std::max<int64_t>(n, 1), 0u,
+                                           (unsigned)bits) != hipSuccess)
     return 0;
   return bytes;
 }
@@ -23,7 +31,7 @@ int sort_keys_u64(uint64_t* a, uint64_t* b, int64_t n, int bits, void* scratch, 
   if (n <= 1) return 0;
   rocprim::double_buffer<uint64_t> db(a, b);
   size_t bytes = scratch_bytes;
-  TNP_CHECK(rocprim::radix_sort_keys(scratch, bytes, db, (size_t)n, 0u, (unsigned)bits, s));
+  TNP_CHECK(rocprim::radix_sort_keys<KeySortCfg>(scratch, bytes, db, (size_t)n, 0u, (unsigned)bits, s));
   *out = db.current();
   return 0;
 }
