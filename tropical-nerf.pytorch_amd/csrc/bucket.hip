@@ -45,6 +45,7 @@ constexpr int BK_IPT = TNP_BK_IPT;  // members per thread in the member passes
 // (measured at 128^3: 4,913 buckets +0.26 ms per pass) and scan in a launch
 // of their own
 constexpr unsigned FUSE_MAX_BLOCKS = 512;
+static_assert(FUSE_MAX_BLOCKS <= 512, "engine.cpp sizes the parts buffer for at least 512 workgroups");
 
 // member m of a step: the S new vertices are slots V + m (no list needed),
 // the hit vertices follow in members[S..]
@@ -613,6 +614,10 @@ int bucket_geometry(int n_marks, int* sh, int* NBd, int* NB) {
   return 0;
 }
 
+int64_t bucket_member_blocks(int64_t M) {
+  const int64_t per = (int64_t)TNP_BLOCK * BK_IPT;
+  return std::max<int64_t>((M + per - 1) / per, 1);
+}
 int launch_bucket_entries(const int32_t* members, int64_t S, int64_t V, int64_t M, const uint64_t* keys,
                           const uint64_t* zero, int idx, int n_marks, int32_t* bcount, int32_t* bcur,
                           int64_t* bbase, int64_t* part, uint64_t* ekv, bool clean, uint8_t* live,
@@ -627,8 +632,7 @@ int launch_bucket_entries(const int32_t* members, int64_t S, int64_t V, int64_t 
     TNP_CHECK(hipMemsetAsync(bcount, 0, NB * sizeof(int32_t), s));
     TNP_CHECK(hipMemsetAsync(bcur, 0, NB * sizeof(int32_t), s));
   }
-  const int64_t per = (int64_t)TNP_BLOCK * BK_IPT;
-  const unsigned nblk = (unsigned)std::max<int64_t>((M + per - 1) / per, 1);
+  const unsigned nblk = (unsigned)bucket_member_blocks(M);
   // the live-flag zeroing rides along: a step with few members still gets
   // enough workgroups for it (64 B per thread; the extra ones count nothing)
   unsigned grid = nblk;

@@ -978,7 +978,10 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     if (buf_ensure(e->bk[4], NB * sizeof(int64_t), s)) return -1;        // pairs
     if (buf_ensure(e->bk[5], (NB + 1) * sizeof(int64_t), s)) return -1;  // pair-cell offsets
     if (buf_ensure(e->bk[6], (NB + 1) * sizeof(int64_t), s)) return -1;  // pair offsets
-    if (buf_ensure(e->bk[7], (std::max<int64_t>(M / 2048, 512) + 2) * sizeof(int64_t), s)) return -1;  // block parts
+    // block parts: one per workgroup of the member passes (the grid is at least
+    // FUSE_MAX_BLOCKS = 512 when the live-flag zeroing rides along)
+    if (buf_ensure(e->bk[7], (std::max<int64_t>(bucket_member_blocks(M), 512) + 2) * sizeof(int64_t), s))
+      return -1;
     for (int k = 8; k < 11; ++k)
       if (buf_ensure(e->bk[k], RC * sizeof(int32_t), s)) return -1;  // per-bucket pair-cell areas
     if (buf_ensure(e->bk[11], RC * sizeof(int64_t), s)) return -1;

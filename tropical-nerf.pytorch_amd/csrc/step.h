@@ -199,6 +199,9 @@ struct NewOverride {
   uint64_t* zero;
   uint64_t* pz;
 };
+// workgroups of the member passes over M members (>= 1): the per-block parts buffer
+// of launch_bucket_entries needs max(this, 512) entries
+int64_t bucket_member_blocks(int64_t M);
 int launch_bucket_entries(const int32_t* members, int64_t S, int64_t V, int64_t M, const uint64_t* grid,
                           const uint64_t* zero, int idx, int n_marks, int32_t* bcount, int32_t* bcur,
                           int64_t* bbase, int64_t* part, uint64_t* ekv, bool clean, uint8_t* live,
