@@ -284,7 +284,7 @@ static int lb_begin(tnp_engine* e, int64_t tiles, hipStream_t s, TnpLB* out, int
 static int scan_counts(tnp_engine* e, const int32_t* in, int64_t* out, int64_t n, int slot,
                        hipStream_t s) {
   TnpLB lb;
-  if (n > 0 && lb_begin(e, scan_tiles(n), s, &lb)) return -1;
+  if (n > 0 && lb_begin(e, scan_tiles(n), s, &lb, 0, false)) return -1;
   TIMED("scan", 12.0 * n, scan_i32_to_i64(in, out, n, P<int64_t>(e->ctr) + slot, lb, s));
   return 0;
 }

@@ -10,15 +10,16 @@ namespace {
 constexpr int IPT = 32;
 constexpr int TILE = TNP_BLOCK * IPT;
 
-// single pass: tile = ticket, thread t owns IPT consecutive elements (local
-// serial scan), block scan of the thread sums, decoupled look-back for the
-// tile's offset; the last tile writes the total.
+// single pass: tile = blockIdx (ticket-free look-back, common.h
+// lb_prefix_rc), thread t owns IPT consecutive elements (local serial scan),
+// block scan of the thread sums, decoupled look-back for the tile's offset;
+// the last tile writes the total.
 __global__ void __launch_bounds__(TNP_BLOCK)
 k_scan_lb(const int32_t* __restrict__ in, int64_t n, int64_t ntiles, int64_t* __restrict__ out,
           int64_t* __restrict__ total, TnpLB lb) {
   __shared__ int64_t lds[TNP_WAVES];
   __shared__ int64_t slot;
-  const int64_t tile = tnp::lb_tile(lb, &slot);
+  const int64_t tile = blockIdx.x;
   int64_t base = tile * TILE + (int64_t)threadIdx.x * IPT;
   int32_t v[IPT];
   int64_t s = 0;
@@ -45,7 +46,14 @@ k_scan_lb(const int32_t* __restrict__ in, int64_t n, int64_t ntiles, int64_t* __
   for (int k = 0; k < IPT; ++k) s += v[k];
   int64_t tot;
   int64_t ex = tnp::block_scan_excl(s, lds, tot);
-  const int64_t prefix = tnp::lb_prefix(lb, tile, tot, &slot);
+  // a predecessor tile not yet published: its sum, one wave
+  auto tile_agg = [&](int64_t t) -> int64_t {
+    const int64_t b0 = t * TILE, b1 = b0 + TILE < n ? b0 + TILE : n;
+    int64_t c = 0;
+    for (int64_t j = b0 + tnp::lane(); j < b1; j += 64) c += in[j];
+    return tnp::wave_sum(c);
+  };
+  const int64_t prefix = tnp::lb_prefix_rc(lb, tile, tot, &slot, tile_agg);
   ex += prefix;
 #pragma unroll
   for (int k = 0; k < IPT; ++k) {
