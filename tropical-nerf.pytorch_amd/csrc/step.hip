@@ -50,7 +50,10 @@ constexpr int TILE = TNP_BLOCK * IPT;   // tile of a compaction pass
 // before any is used
 // split / hit passes: 32 items per thread on large inputs (more loads in
 // flight), 8 on small ones (more tiles to spread over the CUs)
-constexpr int SIPT_BIG = 32, SIPT_SMALL = 8;
+#ifndef TNP_SIPT_BIG
+#define TNP_SIPT_BIG 32
+#endif
+constexpr int SIPT_BIG = TNP_SIPT_BIG, SIPT_SMALL = 8;
 constexpr int64_t SIPT_BIG_FROM = 1 << 20;
 __host__ __device__ constexpr int split_ipt(int64_t n) { return n >= SIPT_BIG_FROM ? SIPT_BIG : SIPT_SMALL; }
 constexpr int SIPT = 16;  // the radix path's run-start pass
