@@ -390,7 +390,7 @@ __device__ __forceinline__ void group_bucket(const BGeom& G, int b, int64_t base
                                              int32_t* __restrict__ ln, int64_t* __restrict__ lpoff,
                                              int64_t* __restrict__ bnpc, int64_t* __restrict__ bnpairs,
                                              int64_t* __restrict__ bspairs, int64_t* __restrict__ ctr,
-                                             int* cnt, int* cur, int64_t* lds) {
+                                             int* cnt, int* cur, int64_t* lds, int64_t* lds3) {
   constexpr int LC = 1 << (3 * SH);
   for (int i = threadIdx.x; i < LC; i += TNP_BLOCK) cnt[i] = 0;
   __syncthreads();
@@ -468,10 +468,33 @@ __device__ __forceinline__ void group_bucket(const BGeom& G, int b, int64_t base
     }
   }
   if (__ballot(big) && tnp::lane() == 0) atomicOr((unsigned long long*)&ctr[CTR_BIG], 1ull);
-  int64_t tpc, tp, tsp;
-  int64_t opc = tnp::block_scan_excl((int64_t)npc, lds, tpc);
-  int64_t op = tnp::block_scan_excl(np, lds, tp);
-  tnp::block_scan_excl(nsp, lds, tsp);
+  // the three scans share one barrier pair (lds3: 3 * TNP_WAVES)
+  int64_t tpc = 0, tp = 0, tsp = 0;
+  int64_t opc = 0, op = 0;
+  {
+    const int64_t i0 = tnp::wave_scan_incl((int64_t)npc), i1 = tnp::wave_scan_incl(np),
+                  i2 = tnp::wave_scan_incl(nsp);
+    if (tnp::lane() == 63) {
+      lds3[tnp::wave()] = i0;
+      lds3[TNP_WAVES + tnp::wave()] = i1;
+      lds3[2 * TNP_WAVES + tnp::wave()] = i2;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < TNP_WAVES; ++w) {
+      const int64_t c0 = lds3[w], c1 = lds3[TNP_WAVES + w], c2 = lds3[2 * TNP_WAVES + w];
+      if (w < tnp::wave()) {
+        opc += c0;
+        op += c1;
+      }
+      tpc += c0;
+      tp += c1;
+      tsp += c2;
+    }
+    __syncthreads();
+    opc += i0 - npc;
+    op += i1 - np;
+  }
   const int64_t area = base / 2;
   const int m_ = (1 << G.sh) - 1;
   const int bz = b % G.NBd, by = (b / G.NBd) % G.NBd, bx = b / (G.NBd * G.NBd);
@@ -512,6 +535,7 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
   __shared__ int cnt[LC];
   __shared__ int cur[LC];
   __shared__ int64_t lds[TNP_WAVES];
+  __shared__ int64_t lds3[3 * TNP_WAVES];
   __shared__ int last;
   __shared__ WinLds W;
   const int b = blockIdx.x;
@@ -537,7 +561,7 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
     }
   } else {
     group_bucket<SH>(G, b, base, n, ekv, pz, ents, lcell, lent, ln, lpoff, bnpc, bnpairs, bspairs, ctr, cnt,
-                     cur, lds);
+                     cur, lds, lds3);
     if (wa.keys) {
       // the window pass over this bucket's records, right behind their
       // stores (the workgroup's own stores: visible after the barrier)
