@@ -158,16 +158,29 @@ class Collective:
         return a.max(axis=0)
 
 
-def cpu_baseline(G: int, slab: int, seed: int, threads: int):
-    """The oracle (PyTorch-CPU restatement of the reference, same op sequence)
-    on a bounded sample of the SAME workload: the x-slab of mark planes
-    [0, slab] of the G^3 lattice of the same net, every hyperplane step."""
+def cpu_threads() -> int:
+    """Host threads for the CPU baseline: the usable cores
+    (sched_getaffinity), capped by the job's CPU share when the launcher
+    states one (OMP_NUM_THREADS: the GPU box gives one GPU's job 16 of the
+    host's cores; sched_getaffinity there lists the whole machine)."""
+    n = len(os.sched_getaffinity(0))
+    share = os.environ.get("OMP_NUM_THREADS")
+    if share and share.isdigit() and int(share) > 0:
+        n = min(n, int(share))
+    return max(1, n)
+
+
+def cpu_baseline(G: int, seed: int, threads: int):
+    """The oracle (PyTorch-CPU restatement of the reference, same op sequence,
+    pinned to the reference's goldens) on the whole G^3 lattice of the
+    synthetic net of this seed (N = 64 when the budget is
+    short), every hyperplane step."""
     import oracle.subdivide as od
     from tropical.synthetic import slab_lattice
     torch.set_num_threads(threads)
     cfg, p = synthetic_params(G, seed)
     ref = od.load_params(od.RefNet(**cfg), p)
-    V, E = slab_lattice(ref.enc.marks.numpy(), 0, slab)
+    V, E = slab_lattice(ref.enc.marks.numpy(), 0, G - 1)
     V, E = torch.from_numpy(V), torch.from_numpy(E)
     stats = {}
     t0 = time.perf_counter()
@@ -176,6 +189,64 @@ def cpu_baseline(G: int, slab: int, seed: int, threads: int):
     dt = time.perf_counter() - t0
     S = sum(s["S"] for s in stats["steps"])
     return S / dt, S, dt
+
+
+def gpu_same_workload(G: int, seed: int, dev, reps: int = 5):
+    """The engine on the CPU baseline's workload (the whole G^3 lattice of
+    the same net): splits per pass and the median pass time."""
+    from tropical._engine import engine_for
+    net = make_net(G, dev, seed)
+    eng = engine_for(net)
+    eng.set_owned()
+    eng.set_shards(1)
+    ts, S = [], 0
+    for i in range(reps + 1):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        stats = []
+        eng.lattice()
+        eng.run_steps(stats)
+        torch.cuda.synchronize(dev)
+        if i:  # the first pass warms the engine's buffers
+            ts.append(time.perf_counter() - t0)
+        S = sum(s["S"] for s in stats)
+    return S, float(np.median(ts))
+
+
+def reference_full_workload(G: int, seed: int):
+    """The reference ITSELF on the exact benchmarked workload (128^3, seed 6),
+    timed once when tests/golden/make_golden.py produced the bench128 golden
+    in the build container (8-core Intel Xeon, torch CPU): its splits and
+    seconds.  None for other workloads."""
+    from golden_io import GOLDEN
+    path = os.path.join(GOLDEN, "bench128.npz")
+    if G != 128 or seed != 6 or not os.path.isfile(path):
+        return None
+    with np.load(path, allow_pickle=False) as z:
+        return float(z["ref_seconds"])
+
+
+# kernels of the PMC profile that are not part of a pass (export / stitch /
+# the first pass's buffer growth), left out of the whole-pass counter total
+PMC_NOT_PER_PASS = ("k_gather_vertices", "k_remap_edges", "k_scan_lb", "k_i32_to_i64", "k_widen_flags",
+                    "at", "__amd_rocclr_copyBuffer", "__amd_rocclr_copyBufferRectAligned")
+
+
+def pmc_pass_bytes(marks: int, seed: int):
+    """Sum of the committed PMC HBM bytes (2 FETCH_SIZE + WRITE_SIZE, per
+    launch x launches) over the kernels of one pass, divided by the passes
+    the profiled run made (k_forward: the lattice's full forward, once per
+    pass).  None without a profile of this workload."""
+    if marks != 128 or seed != 6 or not os.path.isfile(PMC_TABLE):
+        return None
+    with open(PMC_TABLE) as f:
+        ks = json.load(f)["kernels"]
+    passes = ks.get("k_forward", {}).get("launches")
+    if not passes:
+        return None
+    tot = sum(v["traffic_bytes_per_launch"] * v["launches"] for k, v in ks.items()
+              if k not in PMC_NOT_PER_PASS and "traffic_bytes_per_launch" in v)
+    return tot / passes
 
 
 def small_net_check(dev, force: bool = True):
@@ -282,9 +353,10 @@ def main():
     # 12 contain regions of 1e5-1e7 vertices (seed 8: 5.5e13 in-region pairs)
     # that the reference's CPU path could not materialise (tools/seed_scan.py)
     ap.add_argument("--seed", type=int, default=6)
-    # the CPU baseline's sample: the x-slab of mark planes [0, N] of the
-    # benchmarked lattice (same net, same cell density), ~20 s of CPU work
-    ap.add_argument("--cpu-slab", type=int, default=int(os.environ.get("TNP_CPU_SLAB", 3)))
+    # the CPU baseline's sample: the whole lattice of this many
+    # marks per axis, same seed (64: ~1 min of CPU work; 128 is the benchmarked
+    # workload itself, ~18 min)
+    ap.add_argument("--cpu-marks", type=int, default=int(os.environ.get("TNP_CPU_MARKS", 64)))
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
 
@@ -445,7 +517,15 @@ def main():
                     # the whole hyperplane loop against the same peak: SURVEY
                     # §8d's per-step model (bench.algorithmic_bytes) / pass time
                     "whole_loop_gbs": round(loop_gbs, 1),
-                    "whole_loop_frac": round(loop_gbs / (HBM_PEAK_GBS * world), 4)}
+                    "whole_loop_frac": round(loop_gbs / (HBM_PEAK_GBS * world), 4),
+                    # the same pass against the counters: sum of the PMC HBM
+                    # bytes of every kernel of one pass / pass time / peak
+                    # (MALL hits included: an upper bound on HBM traffic)
+                    "counter_bytes_per_pass": None, "counter_frac": None}
+            pb = pmc_pass_bytes(G, args.seed) if world == 1 else None
+            if pb is not None:
+                roof["counter_bytes_per_pass"] = int(pb)
+                roof["counter_frac"] = round(pb / (dt_max / args.steps) / 1e9 / HBM_PEAK_GBS, 4)
         if roof and world == 1:
             row = pmc_row(dom, G, args.seed)
             if row and "SQ_INSTS_VALU" in row:
@@ -487,15 +567,35 @@ def main():
         if stitched:
             out["final_complex" if world == 1 else "stitched_complex"] = stitched
         if not args.no_cpu and world == 1:
-            thr = max(1, min(16, len(os.sched_getaffinity(0))))
-            cps, S_cpu, t_cpu = cpu_baseline(G, args.cpu_slab, args.seed, thr)
+            thr = cpu_threads()
+            Gc = args.cpu_marks
+            cps, S_cpu, t_cpu = cpu_baseline(Gc, args.seed, thr)
+            S_g, t_g = gpu_same_workload(Gc, args.seed, dev)
+            if S_g != S_cpu:
+                raise SystemExit(f"CPU baseline workload: {S_cpu} splits on the host, {S_g} on the GPU")
             out["cpu_baseline"] = {
                 "value": round(cps, 1), "unit": "edges/s", "cores": thr, "kind": "port",
                 "cpu": cpu_model(),
-                "sample": f"oracle (PyTorch-CPU restatement of the reference, pinned to its goldens) on "
-                          f"the x-slab of mark planes [0, {args.cpu_slab}] of this {G}^3 seed-{args.seed} "
-                          f"lattice (same net): {S_cpu} splits in {t_cpu:.1f}s"}
-            out["gpu_over_cpu"] = round(value / cps, 1)
+                "threads_rule": "usable cores (sched_getaffinity), capped by the job's CPU share "
+                                "(OMP_NUM_THREADS)",
+                "sample": f"oracle (PyTorch-CPU restatement of the reference, pinned to its goldens) on the "
+                          f"whole {Gc}^3 lattice of the seed-{args.seed} synthetic net, all hyperplane "
+                          f"steps (BASELINE.md §3): {S_cpu} splits in {t_cpu:.1f}s",
+                # the GPU on the SAME workload, so the ratio compares equal work
+                "gpu_same_sample": {"edges_subdivided": int(S_g), "seconds": round(t_g, 5),
+                                    "edges_per_s": round(S_g / t_g, 1)},
+                "gpu_over_cpu_same_sample": round((S_g / t_g) / cps, 1)}
+            ref_s = reference_full_workload(G, args.seed)
+            if ref_s is not None:
+                # the reference itself on the benchmarked workload (all of it)
+                out["cpu_baseline"]["reference_full_workload"] = {
+                    "value": round(per_pass / ref_s, 1), "unit": "edges/s", "kind": "reference",
+                    "seconds": round(ref_s, 1), "edges_subdivided": int(per_pass), "cores": 8,
+                    "cpu": "8-core Intel Xeon (the build container, not this host)",
+                    "sample": f"the reference's subpoly_ loop on the full {G}^3 seed-{args.seed} lattice, "
+                              "timed by tests/golden/make_golden.py when it produced the bench128 golden",
+                    "gpu_over_reference": round(value / (per_pass / ref_s), 1)}
+            engine_for(net)  # restore
         if not args.no_cpu and world == 1:
             out["small_net"] = small_net_check(dev, force=True)
             out["small_net_curve"] = small_net_check(dev, force=False)

@@ -63,6 +63,9 @@ typedef struct tnp_step_stats {
 
 const char* tnp_last_error(void);
 int tnp_abi_version(void);
+/* Hash of the sources the library was built from (csrc/build_id.sh); the
+ * Python binding refuses a library whose id differs from its tree's. */
+const char* tnp_build_id(void);
 int tnp_device_count(int* n);
 
 /* ---- stateless net ops -------------------------------------------------- */
@@ -189,8 +192,9 @@ int tnp_engine_faces_export(tnp_engine* eng, int64_t* d_tri, float* d_faces,
  * Single-device only (the descent's stop criterion is global). */
 int tnp_engine_set_curve(tnp_engine* eng, int on);
 
-/* Multi-GPU x-slabs with a halo of HALO (= 2) cells each side (tropical/
- * distributed.py): this shard OWNS the mark planes
+/* Multi-GPU x-slabs, each extracted with a halo of cells on either side
+ * (tropical/distributed.py; the halo width is the caller's, checked by
+ * halo_check): this shard OWNS the mark planes
  * (lo, hi] (lo == 0: [0, hi]) and the cells between them; new vertices
  * outside (halo work, also computed by the neighbour that owns them) are
  * counted in tnp_step_stats.S_dup so the global split count counts each
@@ -230,9 +234,11 @@ int tnp_shm_allreduce(tnp_shm* shm, const int64_t* in, int n, int op, int64_t* o
 /* ---- SDF training (train.py:169-224, dataset.py:80-96; csrc/train.hip) --
  * Gradient of one batch's loss (train.py:181-201) for the n points d_x
  * (n x 3 in [-1, 1]^3) with target distances d_gt (n):
- *   L = mean |clamp(sdf(x)) - clamp(gt)| + eik_w (||J||_F - 1)^2 / n,
+ *   L = mean |clamp(sdf(x)) - clamp(gt)| + eik_w (||J||_F - 1)^2 / eik_batch,
  * clamp to [-clamp_t, clamp_t], sdf = tanh(o1 - o0) (model.py:84-87),
- * J = d sdf / d x (n x 3) -- the L1 and eikonal terms; the weight-norm term
+ * J = d sdf / d x (n x 3) -- the L1 and eikonal terms (eik_batch: the
+ * reference's BATCH_SIZE constant, train.py:197, which equals n except for a
+ * partial last batch; <= 0 takes n); the weight-norm term
  * (train.py:200-201) involves only the fc weights and is the caller's.  The
  * eikonal term's parameter gradient (the reference's double backward) is
  * written out in closed form.  ACCUMULATES into d_grad_table (the table's
@@ -241,7 +247,8 @@ int tnp_shm_allreduce(tnp_shm* shm, const int64_t* in, int n, int op, int64_t* o
  * the call) receives sum |clamp(sdf) - clamp(gt)| and sum ||J_i||^2.  Float
  * atomics: the summation order is not fixed.  3-layer nets, 16 hidden. */
 int tnp_sdf_train_grad(const tnp_net* net, const float* d_x, const float* d_gt, int64_t n, float clamp_t,
-                       float eik_w, float* d_grad_table, float* d_grad_weights, double* d_stats, void* stream);
+                       float eik_w, int64_t eik_batch, float* d_grad_table, float* d_grad_weights,
+                       double* d_stats, void* stream);
 
 /* Signed distance of n points d_p (n x 3) to a closed triangle mesh (d_V
  * nV x 3 fp32, d_F nF x 3 int32, indices in [0, nV)): replaces

@@ -24,6 +24,15 @@ int tnp_debug_ops(const float* d_a, const float* d_b, const float* d_c, int64_t 
 int tnp_engine_faces_debug(tnp_engine* eng, float* d_scores, int64_t cap, int64_t* F,
                            int64_t* width, void* stream);
 
+/* Debug: the ticket-free look-back of the split, prune and count scans
+ * (csrc/common.h lb_prefix_rc).  set_lb_spin: polls of an unpublished
+ * predecessor tile before the waiting wave recomputes its aggregate (< 0: the
+ * kernels' defaults, 0: recompute every unpublished predecessor -- the path
+ * in-order dispatch makes rare).  lb_recomputes: recomputes since the last
+ * reset (reset=1 zeroes the counter after reading it). */
+int tnp_engine_debug_set_lb_spin(tnp_engine* eng, int spin);
+int tnp_engine_debug_lb_recomputes(tnp_engine* eng, int64_t* n, int reset, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

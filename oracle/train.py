@@ -53,7 +53,7 @@ def encode_diff(x01: torch.Tensor, params: torch.Tensor, meta, F: int = 2) -> to
     return torch.cat(cols, 1)
 
 
-def train_loss_grads(table, weights, meta, x, gt, clamp_t=0.2, eik_w=1e-2):
+def train_loss_grads(table, weights, meta, x, gt, clamp_t=0.2, eik_w=1e-2, batch_size=None):
     """(l1, eik, grads) of one batch: the L1 and eikonal terms of
     train.py:181-197 and their gradients w.r.t. the table and the fc
     parameters [W0, b0, W1, b1, W2, b2] (the weight-norm term,
@@ -75,7 +75,8 @@ def train_loss_grads(table, weights, meta, x, gt, clamp_t=0.2, eik_w=1e-2):
     y = sdf(x)
     l1 = (torch.clamp(y, -clamp_t, clamp_t) - torch.clamp(gt, -clamp_t, clamp_t)).abs().mean()
     J = torch.autograd.grad(y.sum(), x, create_graph=True)[0]
-    eik = eik_w * (J.norm(p=2) - 1).pow(2) / x.shape[0]
+    # train.py:197 divides by the BATCH_SIZE constant (the L1 mean by the actual batch)
+    eik = eik_w * (J.norm(p=2) - 1).pow(2) / (x.shape[0] if batch_size is None else batch_size)
     grads = torch.autograd.grad(l1 + eik, [tab] + ws)
     return l1.detach(), eik.detach(), grads
 

@@ -61,3 +61,24 @@ def test_product_never_imports_oracle():
                 txt = open(os.path.join(dirpath, f)).read()
                 assert "oracle" not in re.sub(r'""".*?"""', "", txt, flags=re.S).replace(
                     "# oracle", ""), f
+
+
+def test_build_id_rules_agree():
+    """csrc/build_id.sh (compiled into the library) and tropical/_buildid.py
+    (the loader's check) hash the same sources the same way."""
+    import subprocess
+    from tropical._buildid import CSRC, build_id
+    sh = subprocess.run(["sh", os.path.join(CSRC, "build_id.sh")], capture_output=True, text=True, check=True)
+    assert sh.stdout.strip() == build_id()
+
+
+def test_stale_library_is_refused(monkeypatch):
+    """A prebuilt library whose sources differ from the tree's (tnp_build_id)
+    must not load: the GPU box runs whatever .so travels with the tree."""
+    from tropical import _buildid, _hip
+    good = _hip.lib()
+    assert good.tnp_build_id().decode() == _buildid.build_id()
+    monkeypatch.setattr(_hip, "_lib", None)
+    monkeypatch.setattr(_buildid, "build_id", lambda: "0000000000000000")
+    with pytest.raises(RuntimeError, match="stale"):
+        _hip.lib()

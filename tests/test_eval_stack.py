@@ -57,7 +57,7 @@ def test_ply_round_trip(tmp_path):
     V = np.random.RandomState(1).rand(10, 3)
     F = np.random.RandomState(2).randint(0, 10, (7, 3))
     Mesh(V, F).export(str(tmp_path / "m.ply"))
-    m = load_ply(str(tmp_path / "m.ply"))
+    m = load_ply(str(tmp_path / "m.ply"), process=False)
     np.testing.assert_array_equal(m.vertices, V.astype(np.float32))
     np.testing.assert_array_equal(m.faces, F)
 

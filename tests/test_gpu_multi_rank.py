@@ -12,7 +12,11 @@ fingerprints; N > 1 parity is up to numbering):
   reference itself;
 * Stanford-style nets (BASELINE config 4): subpoly_sharded -- skeleton on the
   reference's 128-mark tiles, slabs of equal skeleton-edge load -- on the
-  201-mark large net and the small net.
+  201-mark large net (2, 3 and the config's 8 ranks) and the small net;
+* BASELINE config 5 at full size: the 256^3 seed-6 synthetic lattice cut
+  into 8 x-slabs must stitch to exactly the complex the unsharded engine
+  extracts on one GPU (counts + order-free fingerprints).
+Lattice shards use the halo search of bench.py (HALOS, halo_check).
 """
 import os
 import socket
@@ -35,6 +39,29 @@ def _free_port():
     return port
 
 
+def _sharded_lattice(net, rank, world, coll, stats):
+    """This rank's x-slab of the net's full lattice, with the narrowest halo
+    of HALOS that halo_check accepts (bench.py's N > 1 path)."""
+    from tropical import distributed as D
+    from tropical._engine import engine_for
+    n = int(net.enc.marks.shape[0])
+    cuts = D.slab_cuts(n, world)
+    eng = engine_for(net)
+    eng.set_owned(cuts[rank], cuts[rank + 1])
+    eng.set_shards(world)
+    marks = net.enc.marks.cpu()
+    for k, h in enumerate(D.HALOS):
+        st = []
+        eng.lattice(*D.slab_marks(cuts, rank, h))
+        eng.run_steps(st, coll)
+        Vl, El, _ = eng.export()
+        Vl, El = Vl.cpu(), El.cpu()
+        if D.halo_check(Vl, El, marks, cuts, raise_=k == len(D.HALOS) - 1) is not None:
+            break
+    stats.extend(st)
+    return cuts, Vl, El
+
+
 def _worker(rank, world, port, outdir, case, mode):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
@@ -43,25 +70,28 @@ def _worker(rank, world, port, outdir, case, mode):
         import bench
         from helpers import product_net
         from tropical import distributed as D
-        from tropical._engine import engine_for
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)
-        d = load(case)
-        net = product_net(d, dev)
         coll = bench.Collective(torch.device("cpu"))
         stats = []
+        if mode == "bench":  # the synthetic bench net of `case` = (marks, seed)
+            G, seed = case
+            net = bench.make_net(G, dev, seed)
+            cuts, Vl, El = _sharded_lattice(net, rank, world, coll, stats)
+            own = D.owner_of(Vl, net.enc.marks.cpu(), cuts) == rank
+            owner = D.owner_of(Vl, net.enc.marks.cpu(), cuts)
+            keep = torch.maximum(owner[El[:, 0]], owner[El[:, 1]]) == rank
+            hv, he = D.complex_hash(Vl, El, own, keep)
+            splits = sum(s["S"] - s["S_dup"] for s in stats)
+            tot = torch.tensor([int(own.sum()), int(keep.sum()), hv, he, splits], dtype=torch.int64)
+            dist.all_reduce(tot)
+            if rank == 0:
+                np.savez(os.path.join(outdir, "out.npz"), tot=tot.numpy(), cuts=np.array(cuts))
+            return
+        d = load(case)
+        net = product_net(d, dev)
         if mode == "lattice":
-            n = int(d["lattice_n"])
-            cuts = D.slab_cuts(n, world)
-            x0, x1 = D.slab_marks(cuts, rank)
-            eng = engine_for(net)
-            eng.set_owned(cuts[rank], cuts[rank + 1])
-            eng.set_shards(world)
-            eng.lattice(x0, x1)
-            eng.run_steps(stats, coll)
-            Vl, El, _ = eng.export()
-            Vl, El = Vl.cpu(), El.cpu()
-            D.halo_check(Vl, El, net.enc.marks.cpu(), cuts)
+            cuts, Vl, El = _sharded_lattice(net, rank, world, coll, stats)
             owned, first, gE, own, keep = D.stitch(Vl, El, net.enc.marks.cpu(), cuts, masks=True)
         else:
             eng, owned, first, gE, cuts = D.subpoly_sharded(net, 1.2, allreduce=coll, stats=stats)
@@ -94,6 +124,8 @@ def _unsharded(cuda, case, mode):
     d = load(case)
     net = product_net(d, cuda)
     eng = engine_for(net)
+    eng.set_owned()
+    eng.set_shards(1)
     if mode == "lattice":
         eng.lattice()
     else:
@@ -105,7 +137,7 @@ def _unsharded(cuda, case, mode):
     return d, V, E, (V.shape[0], E.shape[0], hv, he, sum(s["S"] for s in stats))
 
 
-@pytest.mark.parametrize("case,world", [("synth32h", 2), ("synth32h", 3), ("synth64h", 2)])
+@pytest.mark.parametrize("case,world", [("synth32h", 2), ("synth32h", 3), ("synth64h", 2), ("synth64h", 8)])
 def test_sharded_lattice_engine(cuda, tmp_path, case, world):
     d, V, E, want = _unsharded(cuda, case, "lattice")
     assert (want[0], want[1]) == tuple(int(x) for x in d["pre_VE"])
@@ -117,10 +149,38 @@ def test_sharded_lattice_engine(cuda, tmp_path, case, world):
     assert z["E"].min() >= 0 and z["E"].max() < want[0]
 
 
-@pytest.mark.parametrize("case,world", [("large_sphere", 2), ("large_sphere", 3), ("small_sphere", 2)])
+@pytest.mark.parametrize("case,world", [("large_sphere", 2), ("large_sphere", 3), ("large_sphere", 8),
+                                        ("small_sphere", 2)])
 def test_sharded_stanford_net(cuda, tmp_path, case, world):
     d, V, E, want = _unsharded(cuda, case, "skeleton")
     z = _run(tmp_path, case, "skeleton", world)
     assert tuple(int(x) for x in z["tot"]) == want
     cuts = z["cuts"].tolist()
     assert cuts[0] == 0 and cuts[-1] == len(d["marks"]) - 1 and len(cuts) == world + 1
+
+
+@pytest.mark.timeout(600)
+def test_lattice256_eight_slabs_stitch_to_the_unsharded_complex(cuda, tmp_path):
+    """BASELINE config 5 at its full size (the 8-GPU weak-scaling lattice of
+    bench.py --gpus 8): the 256^3 seed-6 synthetic lattice cut into 8 x-slabs
+    (8 gloo ranks sharing this GPU, halo search as bench.py) must hold exactly
+    the complex the unsharded engine extracts on one GPU -- same vertex and
+    edge counts, same order-free fingerprints -- and count every split once."""
+    import bench
+    from tropical.distributed import complex_hash
+    from tropical._engine import engine_for
+    net = bench.make_net(256, cuda, 6)
+    eng = engine_for(net)
+    eng.set_owned()
+    eng.set_shards(1)
+    eng.lattice()
+    stats = []
+    eng.run_steps(stats)
+    V, E, _ = eng.export()
+    hv, he = complex_hash(V, E)
+    want = (V.shape[0], E.shape[0], hv, he, sum(s["S"] for s in stats))
+    del V, E
+    torch.cuda.empty_cache()
+    z = _run(tmp_path, (256, 6), "bench", 8)
+    assert tuple(int(x) for x in z["tot"]) == want
+    assert len(z["cuts"]) == 9

@@ -233,22 +233,27 @@ def test_tied_levels_layout(cuda, monkeypatch):
     assert runs[0][-1][:2] == (int(d["step_V"][-1]), int(d["step_E"][-1]))
 
 
-def test_lookback_recompute_path(cuda, monkeypatch):
+def test_lookback_recompute_path(cuda):
     """The split and the prune number tiles by blockIdx and, after a bounded
     wait, recompute an unpublished predecessor tile's aggregate
-    (common.h lb_prefix_rc).  In-order dispatch makes that path rare, so
-    TNP_LB_SPIN=0 forces it on every unpublished predecessor: the per-step
-    states must stay bitwise the reference's."""
+    (common.h lb_prefix_rc).  In-order dispatch makes that path rare, so a
+    poll count of 0 forces it on every unpublished predecessor: the
+    recompute must really run (its counter moves) and the per-step states
+    must stay bitwise the reference's."""
     from tropical._engine import engine_for
     d = load("synth32")
     net = product_net(d, cuda)
-    runs = []
-    for spin in (None, "0"):
-        if spin is not None:
-            monkeypatch.setenv("TNP_LB_SPIN", spin)
-        eng = engine_for(net)
-        eng.lattice(keep_all=True)
-        runs.append(engine_steps(eng))
+    runs, recomputes = [], []
+    eng = engine_for(net)
+    try:
+        for spin in (-1, 0):
+            eng.debug_lb(spin)
+            eng.lattice(keep_all=True)
+            runs.append(engine_steps(eng))
+            recomputes.append(eng.debug_lb())
+    finally:
+        eng.debug_lb(-1)
+    assert recomputes[1] > 0, recomputes
     assert runs[0] == runs[1]
     for g, V, E, s in zip(runs[1], d["step_V"], d["step_E"], d["step_sha"]):
         assert (g[0], g[1], g[2]) == (V, E, s)

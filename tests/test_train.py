@@ -73,6 +73,26 @@ def test_ply_reader_layouts(tmp_path):
     assert np.array_equal(m.vertices, V) and m.faces.tolist() == F
 
 
+def test_ply_reader_merges_duplicate_vertices(tmp_path):
+    """trimesh.load's process=True (dataset.py:39-67): exactly-equal
+    positions merge, unreferenced vertices go, first-occurrence order stays
+    and faces are remapped (a scan's duplicated vertices would otherwise
+    change the dataset's sampling distribution)."""
+    from tropical.utils.mesh import Mesh, load_ply, merge_vertices
+    V = np.array([[0, 0, 0], [1, 0, 0], [9, 9, 9], [0, 1, 0], [1, 0, 0], [-0.0, 0, 1], [0, 0, 1]],
+                 dtype=np.float64)
+    F = np.array([[0, 1, 3], [0, 4, 5], [3, 4, 6]])
+    mv, mf = merge_vertices(V, F)
+    assert mv.tolist() == [[0, 0, 0], [1, 0, 0], [0, 1, 0], [0, 0, 1]]
+    assert mf.tolist() == [[0, 1, 2], [0, 1, 3], [2, 1, 3]]
+    assert np.array_equal(mv[mf], V[F])  # every face keeps its corner positions
+    Mesh(V, F).export(str(tmp_path / "d.ply"))
+    m = load_ply(str(tmp_path / "d.ply"))
+    assert m.vertices.tolist() == mv.tolist() and m.faces.tolist() == mf.tolist()
+    raw = load_ply(str(tmp_path / "d.ply"), process=False)
+    assert raw.vertices.shape == (7, 3) and raw.faces.tolist() == F.tolist()
+
+
 def test_oracle_gradients_match_finite_differences():
     """The oracle's double backward (the reference's create_graph=True path)
     against central differences of its own loss, float64."""
@@ -137,11 +157,13 @@ def test_train_grads_match_oracle(cuda, cfg):
     n = 777
     x = (torch.rand(n, 3, generator=g) * 2 - 1) * 0.95
     gt = (torch.rand(n, generator=g) * 2 - 1) * 0.3
+    # the eikonal term divides by the reference's BATCH_SIZE (1000, train.py:197),
+    # the L1 mean by the actual (here partial) batch of 777 points
     tr = SDFTrainer(net)
     l1, eik = tr.data_grads(x.to(cuda), gt.to(cuda))
     ws = [t.detach().cpu() for lin in net.fc for t in (lin.weight, lin.bias)]
     rl1, reik, ref = train_loss_grads(net.enc.module.params.detach().cpu(), ws, net.enc.meta, x, gt,
-                                      eik_w=EIK_W)
+                                      eik_w=EIK_W, batch_size=1000)
     assert abs(float(l1) - float(rl1)) <= 1e-5 * max(1.0, float(rl1))
     assert abs(float(eik) - float(reik)) <= 1e-4 * max(1e-3, float(reik))
     got = [tr.g_table.cpu()]

@@ -134,6 +134,7 @@ struct TnpLB {
   uint64_t tbase;
   uint32_t epoch;
   int32_t spin;  // lb_prefix_rc polls before recomputing; < 0: the kernel's default
+  unsigned long long* rc;  // nullable: lb_prefix_rc counts its recomputes here (diagnostics)
 };
 
 __device__ __forceinline__ int64_t lb_tile(const TnpLB& lb, int64_t* slot) {
@@ -242,6 +243,7 @@ __device__ __forceinline__ int64_t lb_prefix_rc(const TnpLB& lb, int64_t tile, i
           const int64_t v = tile_agg(w - l);
           if (lane() == l) {
             val = v;
+            if (lb.rc) atomicAdd(lb.rc, 1ull);
             // publish it as that tile's aggregate unless its owner has since
             // published (so later waiters need not recompute it again)
             atomicCAS((unsigned long long*)&lb.st[w - l], (unsigned long long)word,

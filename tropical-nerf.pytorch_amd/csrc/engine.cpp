@@ -154,6 +154,11 @@ struct tnp_engine {
   // preserves ascending ids), so every id-ordered result is unchanged;
   // compact_now() renumbers once, before anything exports or reads ids.
   bool dirty = false;
+  // a complex is loaded and consistent: a failed split / finish (an error
+  // the reference raises mid-step, or a device failure) leaves the edges and
+  // live flags half-updated, so the engine refuses to go on until a complex
+  // is loaded again (tnp_engine_load / lattice / skeleton)
+  bool valid = false;
   int64_t V_live = 0;
   Buf live;  // live-slot flags (uint8) of the lazily compacted vertex set
   // step scratch
@@ -183,6 +188,7 @@ struct tnp_engine {
   uint64_t lb_tickets[2] = {0, 0};
   uint32_t lb_epoch[2] = {0, 0};
   int32_t lb_spin = -1;  // TNP_LB_SPIN: ticket-free look-back polls (0 forces the recompute path)
+  Buf lbrc;              // look-back recompute counter (tnp_engine_debug_lb_recomputes)
   Buf fscr[12];
   Buf fscr2[32];
   Buf sents;                // bucket-ordered packed entries before the in-bucket grouping
@@ -277,6 +283,11 @@ static int lb_begin(tnp_engine* e, int64_t tiles, hipStream_t s, TnpLB* out, int
   out->tbase = e->lb_tickets[w];
   out->epoch = e->lb_epoch[w];
   out->spin = e->lb_spin;
+  if (!e->lbrc.p) {
+    if (buf_ensure(e->lbrc, sizeof(uint64_t), s)) return -1;
+    TNP_CHECK(hipMemsetAsync(e->lbrc.p, 0, sizeof(uint64_t), s));
+  }
+  out->rc = static_cast<unsigned long long*>(e->lbrc.p);
   if (ticketed) e->lb_tickets[w] += (uint64_t)tiles;
   return 0;
 }
@@ -337,6 +348,7 @@ static int set_alive(tnp_engine* e, int64_t from, int64_t n, hipStream_t s) {
 // a freshly loaded complex: every slot live, ids dense, edge masks to compute
 static int reset_live(tnp_engine* e, hipStream_t s, bool edges_changed = true) {
   if (edges_changed) e->masks_valid = false;
+  e->valid = true;
   e->dirty = false;
   e->V_live = e->V;
   return set_alive(e, 0, e->V, s);
@@ -399,6 +411,13 @@ static int compact_now(tnp_engine* e, hipStream_t s) {
   return reset_live(e, s, false);  // same edges, same order: masks stay valid
 }
 
+static int require_valid(const tnp_engine* e, const char* what) {
+  if (e->valid) return 0;
+  tnp_set_error("%s: no consistent complex (none loaded, or a failed step left it half-updated); "
+                "load one first (tnp_engine_load / lattice / skeleton)", what);
+  return -1;
+}
+
 // ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
@@ -439,7 +458,7 @@ extern "C" void tnp_engine_destroy(tnp_engine* e) {
                  &e->ent_v, &e->ents, &e->pcell, &e->ptoff, &e->bcell,
                  &e->ckeys_a, &e->ckeys_b, &e->sort_scr, &e->flags, &e->used, &e->nid,
                  &e->ctr, &e->tri, &e->faces, &e->lb[0], &e->lb[1], &e->edm, &e->eef,
-                 &e->edm_alt, &e->eef_alt, &e->live, &e->tied_table, &e->xs};
+                 &e->edm_alt, &e->eef_alt, &e->live, &e->tied_table, &e->xs, &e->lbrc};
   for (Buf* b : bufs) buf_free(*b, s);
   for (Buf& b : e->fscr) buf_free(b, s);
   for (Buf& b : e->fscr2) buf_free(b, s);
@@ -547,11 +566,11 @@ extern "C" int tnp_sdf_grad(const tnp_net* n, const float* xyz, int64_t N, float
 }
 
 extern "C" int tnp_sdf_train_grad(const tnp_net* n, const float* xyz, const float* gt, int64_t N, float clamp_t,
-                                  float eik_w, float* d_grad_table, float* d_grad_weights, double* d_stats,
-                                  void* stream) {
+                                  float eik_w, int64_t eik_batch, float* d_grad_table, float* d_grad_weights,
+                                  double* d_stats, void* stream) {
   if (check_net(n)) return -1;
   if (N < 0 || !d_grad_table || !d_grad_weights || !d_stats) { tnp_set_error("sdf_train_grad: bad arguments"); return -1; }
-  return launch_train_grad(to_dev(n), xyz, gt, N, clamp_t, eik_w, d_grad_table, d_grad_weights, d_stats,
+  return launch_train_grad(to_dev(n), xyz, gt, N, clamp_t, eik_w, eik_batch > 0 ? eik_batch : N, d_grad_table, d_grad_weights, d_stats,
                            (hipStream_t)stream);
 }
 
@@ -609,6 +628,7 @@ extern "C" int tnp_engine_sizes(tnp_engine* e, int64_t* V, int64_t* E) {
 extern "C" int tnp_engine_active_planes(tnp_engine* e, int from, uint64_t* mask, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   TNP_CHECK(hipSetDevice(e->device));
+  if (require_valid(e, "active_planes")) return -1;
   if (buf_ensure(e->ctr, CTR_N * sizeof(int64_t), s)) return -1;
   TNP_CHECK(hipMemsetAsync(P<int64_t>(e->ctr) + CTR_ACTIVE, 0, sizeof(int64_t), s));
   // the per-edge masks are (re)computed here and the OR of their first split
@@ -785,6 +805,8 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
     tnp_set_error("plane %d not cached (valid from %d)", idx, e->valid_from);
     return -1;
   }
+  if (require_valid(e, "split")) return -1;
+  e->valid = false;  // until this split has completed
   const float eps = e->net.eps;
   const float* col = P<float>(e->cur.pre) + (int64_t)idx * e->cur.cap;
   TNP_CHECK(hipMemsetAsync(e->ctr.p, 0, CTR_N * sizeof(int64_t), s));
@@ -887,6 +909,7 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
   *S_out = S;
   e->pend_idx = idx;
   e->pend_S = S;
+  e->valid = true;
   return 0;
 }
 
@@ -895,7 +918,9 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   hipStream_t s = (hipStream_t)stream;
   TNP_CHECK(hipSetDevice(e->device));
   if (e->pend_idx != idx) { tnp_set_error("finish(%d) without split(%d)", idx, idx); return -1; }
+  if (require_valid(e, "finish")) return -1;
   e->pend_idx = -1;
+  e->valid = false;  // until this step has completed
   const bool hits_done = e->pend_hits;
   e->pend_hits = false;
   const float eps = e->net.eps;
@@ -1256,6 +1281,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     st->S_dup = e->pend_dup;
     st->T = T;
   }
+  e->valid = true;
   return 0;
 }
 
@@ -1263,6 +1289,7 @@ extern "C" int tnp_engine_export(tnp_engine* e, float* d_xyz, int64_t* d_edges, 
                                  void* stream) {
   hipStream_t s = (hipStream_t)stream;
   TNP_CHECK(hipSetDevice(e->device));
+  if (require_valid(e, "export")) return -1;
   if (compact_now(e, s)) return -1;
   if (d_xyz && e->V > 0)
     TNP_CHECK(hipMemcpyAsync(d_xyz, e->cur.xyz.p, e->V * 3 * sizeof(float), hipMemcpyDeviceToDevice, s));
@@ -1285,6 +1312,7 @@ extern "C" int tnp_engine_export(tnp_engine* e, float* d_xyz, int64_t* d_edges, 
 extern "C" int tnp_engine_surface(tnp_engine* e, void* stream, int64_t* V_out, int64_t* E_out) {
   hipStream_t s = (hipStream_t)stream;
   TNP_CHECK(hipSetDevice(e->device));
+  if (require_valid(e, "surface")) return -1;
   if (compact_now(e, s)) return -1;
   const int64_t V = e->V, E = e->E;
   VSet& c = e->cur;
@@ -1572,6 +1600,7 @@ enum { FS_TABLE, FS_CNT, FS_KC, FS_KF, FS_MEMOFF, FS_RID, FS_MEM, FS_CUR, FS_ROF
 extern "C" int tnp_engine_faces(tnp_engine* e, void* stream, int64_t* n_tri, int64_t* n_faces) {
   hipStream_t s = (hipStream_t)stream;
   TNP_CHECK(hipSetDevice(e->device));
+  if (require_valid(e, "faces")) return -1;
   if (compact_now(e, s)) return -1;
   static_assert(FS_N <= 32, "face scratch slots");
   Buf* fs = e->fscr2;
@@ -1772,6 +1801,27 @@ extern "C" int tnp_engine_kernel_stat(tnp_engine* e, int i, char* name, int cap,
   *ms = e->kt_ms[i];
   *launches = e->kt_n[i];
   *bytes = e->kt_bytes[i];
+  return 0;
+}
+
+// diagnostics of the ticket-free look-back (common.h lb_prefix_rc): the poll
+// count before a waiting wave recomputes an unpublished predecessor (< 0: the
+// kernels' defaults; 0 forces the recompute on every unpublished one), and
+// the number of recomputes since the last reset
+extern "C" int tnp_engine_debug_set_lb_spin(tnp_engine* e, int spin) {
+  e->lb_spin = spin;
+  return 0;
+}
+extern "C" int tnp_engine_debug_lb_recomputes(tnp_engine* e, int64_t* n, int reset, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  TNP_CHECK(hipSetDevice(e->device));
+  *n = 0;
+  if (!e->lbrc.p) return 0;
+  uint64_t v = 0;
+  TNP_CHECK(hipMemcpyAsync(&v, e->lbrc.p, sizeof(v), hipMemcpyDeviceToHost, s));
+  TNP_CHECK(hipStreamSynchronize(s));
+  if (reset) TNP_CHECK(hipMemsetAsync(e->lbrc.p, 0, sizeof(uint64_t), s));
+  *n = (int64_t)v;
   return 0;
 }
 

@@ -5,11 +5,11 @@
 // Loss of one batch of n points x (train.py:181-201, Net.sdf = tanh(o1 - o0),
 // model.py:84-87):
 //   L1  = mean_i |clamp(y_i) - clamp(gt_i)|,   clamp to [-T, T] (T = 0.2)
-//   Eik = w_e (||J||_F - 1)^2 / n,   J_i = d y_i / d x_i   (w_e = 1e-2)
+//   Eik = w_e (||J||_F - 1)^2 / B,   J_i = d y_i / d x_i   (w_e = 1e-2, B = BATCH_SIZE)
 // (the weight-norm term needs only the fc weights: the caller's).  The
 // reference gets dEik/dtheta by double backward (autograd.grad with
 // create_graph through tcnn); here it is written out.  With z = o1 - o0,
-// g = dz/dx, y = tanh z, v_i = dEik/dJ_i = w_e 2 (||J|| - 1) / (n ||J||) J_i:
+// g = dz/dx, y = tanh z, v_i = dEik/dJ_i = w_e 2 (||J|| - 1) / (B ||J||) J_i:
 //   v.J = (1 - y^2) q,  q = v.g = u . a,
 //   u = dz/de (the encoding's output), a = (1/2) sum_c T_c (grad w_c . v)
 // -- q is the derivative of z along the direction a in feature space, so
@@ -197,7 +197,7 @@ __device__ __forceinline__ void acc_param(float* lds_g, int p, float v) {
 template <int LV, int H>
 __global__ void __launch_bounds__(TNP_BLOCK)
 k_train_grads(NetDev net, const float* __restrict__ xyz, const float* __restrict__ gt, int64_t n, float T,
-              float eik_w, const double* __restrict__ stats, float* __restrict__ g_table,
+              float eik_w, int64_t eik_batch, const double* __restrict__ stats, float* __restrict__ g_table,
               float* __restrict__ g_w) {
   constexpr int IN = 2 * LV;
   constexpr int NW = NetShape<LV, H, 3>::NW;
@@ -214,9 +214,10 @@ k_train_grads(NetDev net, const float* __restrict__ xyz, const float* __restrict
   if (live) load_point(xyz, i, x);
   Pass<LV, H> p;
   p.run(net, w, x);
-  // v_i = c J_i, c = w_e 2 (||J|| - 1) / (n ||J||)   (torch: a zero norm has a zero gradient)
+  // v_i = c J_i, c = w_e 2 (||J|| - 1) / (B ||J||), B = BATCH_SIZE (train.py:197;
+  // the L1 mean below divides by the actual n)   (torch: a zero norm has a zero gradient)
   const double nj = sqrt(stats[1]);
-  const float c = nj > 0.0 ? (float)(eik_w * 2.0 * (nj - 1.0) / ((double)n * nj)) : 0.f;
+  const float c = nj > 0.0 ? (float)(eik_w * 2.0 * (nj - 1.0) / ((double)eik_batch * nj)) : 0.f;
   const float ty = 1.f - p.y * p.y;
   float v[3];
 #pragma unroll
@@ -453,7 +454,7 @@ __global__ void k_fill_u32(uint32_t* __restrict__ p, int64_t n, uint32_t v) {
   }
 
 int launch_train_grad(const NetDev& net, const float* xyz, const float* gt, int64_t n, float clamp_t, float eik_w,
-                      float* g_table, float* g_w, double* stats, hipStream_t s) {
+                      int64_t eik_batch, float* g_table, float* g_w, double* stats, hipStream_t s) {
   if (!net_supported(net) || net.tied) { tnp_set_error("train: unsupported net shape"); return -1; }
   TNP_CHECK(hipMemsetAsync(stats, 0, 2 * sizeof(double), s));
   if (n <= 0) return 0;
@@ -461,7 +462,7 @@ int launch_train_grad(const NetDev& net, const float* xyz, const float* gt, int6
     hipLaunchKernelGGL((k_train_norms<L_, 16>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net, xyz, gt, n, clamp_t,
                        stats);
     hipLaunchKernelGGL((k_train_grads<L_, 16>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net, xyz, gt, n, clamp_t,
-                       eik_w, stats, g_table, g_w);
+                       eik_w, eik_batch, stats, g_table, g_w);
   });
   TNP_CHECK(hipGetLastError());
   return 0;

@@ -120,6 +120,19 @@ class Engine:
             out[name.value.decode()] = {"ms": ms.value, "launches": nl.value, "bytes": by.value}
         return out
 
+    def debug_lb(self, spin: int = None, reset: bool = True) -> int:
+        """Diagnostics of the ticket-free look-back (common.h lb_prefix_rc):
+        spin != None sets the polls before a recompute (0: always recompute,
+        -1: the kernels' defaults); returns the recomputes counted since the
+        last reset."""
+        if spin is not None:
+            _hip.check(_hip.lib().tnp_engine_debug_set_lb_spin(self.h, int(spin)),
+                       "tnp_engine_debug_set_lb_spin")
+        n = C.c_int64()
+        _hip.check(_hip.lib().tnp_engine_debug_lb_recomputes(self.h, C.byref(n), int(reset), self._s),
+                   "tnp_engine_debug_lb_recomputes")
+        return n.value
+
     # -- steps ---------------------------------------------------------------
     def active_planes(self, start: int = 0) -> int:
         m = C.c_uint64()

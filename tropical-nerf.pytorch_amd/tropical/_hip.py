@@ -51,13 +51,14 @@ _NETP = C.POINTER(TnpNet)
 SIGNATURES = {
     "tnp_last_error": (C.c_char_p, []),
     "tnp_abi_version": (C.c_int, []),
+    "tnp_build_id": (C.c_char_p, []),
     "tnp_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "tnp_forward": (C.c_int, [_NETP, _VP, _I64, _VP, _I64, _VP, _VP]),
     "tnp_encode": (C.c_int, [_NETP, _VP, _I64, _VP, _VP]),
     "tnp_forward_grouped": (C.c_int, [_NETP, _VP, _I64, _VP, _I64, _VP, _VP]),
     "tnp_region": (C.c_int, [_NETP, _VP, _VP, _I64, _I64, _F, _VP, _VP, _VP]),
     "tnp_sdf_grad": (C.c_int, [_NETP, _VP, _I64, _VP, _VP, _VP]),
-    "tnp_sdf_train_grad": (C.c_int, [_NETP, _VP, _VP, _I64, _F, _F, _VP, _VP, _VP, _VP]),
+    "tnp_sdf_train_grad": (C.c_int, [_NETP, _VP, _VP, _I64, _F, _F, _I64, _VP, _VP, _VP, _VP]),
     "tnp_mesh_signed_distance": (C.c_int, [_VP, _I64, _VP, _I64, _VP, _I64, _VP, _VP, _VP]),
     "tnp_engine_create": (C.c_int, [C.POINTER(_VP), C.c_int]),
     "tnp_engine_destroy": (None, [_VP]),
@@ -84,6 +85,8 @@ SIGNATURES = {
     "tnp_engine_set_shards": (C.c_int, [_VP, C.c_int]),
     "tnp_debug_ops": (C.c_int, [_VP, _VP, _VP, C.c_int64, _VP, _VP]),
     "tnp_engine_faces_debug": (C.c_int, [_VP, _VP, C.c_int64, _P64, _P64, _VP]),
+    "tnp_engine_debug_set_lb_spin": (C.c_int, [_VP, C.c_int]),
+    "tnp_engine_debug_lb_recomputes": (C.c_int, [_VP, _P64, C.c_int, _VP]),
     "tnp_engine_kernel_timer": (C.c_int, [_VP, C.c_int, _VP, _P32]),
     "tnp_mc_count": (C.c_int, [_VP, C.c_int, C.c_int, C.c_int, _F, _VP, _VP, _VP, _P64, _P64, _VP]),
     "tnp_mc_emit": (C.c_int, [_VP, C.c_int, C.c_int, C.c_int, _F, _VP, _VP, _VP, _VP, _VP, _VP]),
@@ -113,6 +116,12 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
+        from ._buildid import build_id
+        want, got = build_id(), L.tnp_build_id().decode()
+        if want is not None and got != want:
+            raise RuntimeError(
+                f"tropical HIP library {_LIB_PATH} is stale: built from sources {got}, the tree's "
+                f"are {want} (rebuild: `make -C tropical-nerf.pytorch_amd/csrc` or __graft_entry__.build())")
         _lib = L
     return _lib
 

@@ -19,6 +19,7 @@ from .. import _hip
 
 CLAMP = 0.2      # train.py:184-185 (minT, maxT)
 EIK_W = 1e-2     # train.py:197
+BATCH_SIZE = 1000  # train.py:66: the eikonal term's divisor (train.py:197), whatever the batch length
 WN_W = 1e-1      # train.py:200
 
 
@@ -30,10 +31,11 @@ class SDFTrainer:
     """Adam(lr) + CosineAnnealingLR(T_max) over ``net.parameters()``
     (train.py:86-90); ``step(x, gt)`` is one iteration of train.py:177-205."""
 
-    def __init__(self, net, lr: float = 1e-3, T_max: float = 500.0):
+    def __init__(self, net, lr: float = 1e-3, T_max: float = 500.0, batch_size: int = BATCH_SIZE):
         if net.num_layers != 3 or net.num_hidden != 16:
             raise NotImplementedError("SDF training is built for the reference's 3-layer, 16-hidden nets")
         self.net = net
+        self.batch_size = int(batch_size)
         self.opt = torch.optim.Adam(net.parameters(), lr=lr)
         self.sched = torch.optim.lr_scheduler.CosineAnnealingLR(self.opt, T_max)
         dev = net.device()
@@ -55,13 +57,14 @@ class SDFTrainer:
         self.g_w.zero_()
         s, keep = net.tnp_desc()
         _hip.check(_hip.lib().tnp_sdf_train_grad(
-            ctypes.byref(s), _hip.ptr(x), _hip.ptr(gt), x.shape[0], CLAMP, EIK_W, _hip.ptr(self.g_table),
+            ctypes.byref(s), _hip.ptr(x), _hip.ptr(gt), x.shape[0], CLAMP, EIK_W, self.batch_size,
+            _hip.ptr(self.g_table),
             _hip.ptr(self.g_w), _hip.ptr(self.stats), ctypes.c_void_p(_hip.stream_ptr(x.device))),
             "tnp_sdf_train_grad")
         del keep
         n = max(x.shape[0], 1)
-        l1 = self.stats[0] / n
-        eik = EIK_W * (self.stats[1].sqrt() - 1) ** 2 / n
+        l1 = self.stats[0] / n  # nn.L1Loss: the mean over the actual batch
+        eik = EIK_W * (self.stats[1].sqrt() - 1) ** 2 / self.batch_size
         return l1.float(), eik.float()
 
     def step(self, x, gt):

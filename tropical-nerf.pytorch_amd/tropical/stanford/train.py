@@ -167,7 +167,7 @@ def train_sdf(net, args, path: str):
           f"guarantee the convergence of training nor a reliable SDF.", flush=True)
     training_data = StanfordDataset(args.dataset, mesh=args.mesh)
     loader = torch.utils.data.DataLoader(training_data, batch_size=BATCH_SIZE, shuffle=True)
-    trainer = SDFTrainer(net, lr=1e-3, T_max=epochs * len(training_data) / BATCH_SIZE)
+    trainer = SDFTrainer(net, lr=1e-3, T_max=epochs * len(training_data) / BATCH_SIZE, batch_size=BATCH_SIZE)
     result = None
     for epoch in range(epochs):
         running_loss = torch.zeros((), device=net.device())

@@ -36,12 +36,38 @@ _PLY_TYPES = {"char": "i1", "int8": "i1", "uchar": "u1", "uint8": "u1", "short":
               "float": "f4", "float32": "f4", "double": "f8", "float64": "f8"}
 
 
-def load_ply(path: str) -> Mesh:
+def merge_vertices(verts: np.ndarray, tris: np.ndarray, digits: int = 8):
+    """trimesh's process=True vertex merge (the default of the trimesh.load
+    calls in dataset.py:39-67): vertices equal after rounding to `digits`
+    decimals (trimesh's merge tolerance, 1e-8) become one, vertices no face
+    references are dropped (a mesh with faces), first-occurrence order is
+    kept and the faces are remapped.  trimesh is absent here, so the exact
+    rounding rule is restated, not pinned against it."""
+    verts = np.asarray(verts, dtype=np.float64)
+    tris = np.asarray(tris, dtype=np.int64).reshape(-1, 3)
+    keep = np.ones(len(verts), dtype=bool)
+    if len(tris):
+        keep[:] = False
+        keep[tris.reshape(-1)] = True
+    idx = np.nonzero(keep)[0]
+    key = np.round(verts[idx], digits) + 0.0  # + 0.0: -0.0 and 0.0 merge
+    _, first, inv = np.unique(key, axis=0, return_index=True, return_inverse=True)
+    order = np.argsort(first, kind="stable")  # groups in first-occurrence order
+    rank = np.empty_like(order)
+    rank[order] = np.arange(len(order))
+    remap = np.full(len(verts), -1, dtype=np.int64)
+    remap[idx] = rank[inv.reshape(-1)]
+    return verts[idx[first[order]]], remap[tris] if len(tris) else tris
+
+
+def load_ply(path: str, process: bool = True) -> Mesh:
     """PLY reader for the meshes the training data comes from (the
     trimesh.load calls of dataset.py:39-67): ascii or binary (either
     endianness), any extra vertex properties (the Stanford scans carry
     confidence / intensity), faces as index lists (polygons fan-triangulated).
-    Elements other than vertex and face are skipped."""
+    Elements other than vertex and face are skipped.  process=True (trimesh's
+    default): duplicate vertices merged and unreferenced ones dropped
+    (merge_vertices), so the dataset samples the same vertex list."""
     with open(path, "rb") as f:
         data = f.read()
     end = data.index(b"end_header") + len(b"end_header")
@@ -127,4 +153,7 @@ def load_ply(path: str) -> Mesh:
     if verts is None:
         raise ValueError(f"{path}: no vertex element")
     tris = [(f[0], f[i], f[i + 1]) for f in faces for i in range(1, len(f) - 1)]
-    return Mesh(verts, np.array(tris, dtype=np.int64).reshape(-1, 3))
+    tris = np.array(tris, dtype=np.int64).reshape(-1, 3)
+    if process:
+        verts, tris = merge_vertices(verts, tris)
+    return Mesh(verts, tris)
