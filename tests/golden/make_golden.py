@@ -101,6 +101,18 @@ CASES = {
     # the bench headline workload (bench.py: 128^3 lattice, seed 6, amp 0.1,
     # uncentred): per-step hashes + order-free final fingerprints
     "bench128": ("lattice", None, ("rand_uncentered", 6, 0.1), (128, 19)),
+    # net shapes beyond 3 layers x 16 hidden x {2,4} levels (the reference's
+    # Net is generic, model.py:19-50; subpoly loops num_layers-1 x num_hidden,
+    # subpoly.py:60-69): BASELINE config 3's "deeper MLP" (4 layers, K = 49
+    # planes), a 32-wide 2-layer net, a 3-level 8-wide net (odd level count:
+    # MKL's zero-padded schedules), an 8-level net, and lattices of them
+    "small4l_sphere": ("subpoly", dict(SMALL, num_layers=4), ("fit", sphere, 17), None),
+    "small4l_sphere_curve": ("curve", dict(SMALL, num_layers=4), ("same", "small4l_sphere"), None),
+    "h32_torus": ("subpoly", dict(SMALL, num_layers=2, num_hidden=32), ("fit", torus, 19), None),
+    "h8l3_sphere": ("subpoly", dict(SMALL, num_hidden=8, levels=3, r_max=24), ("fit", sphere, 23), None),
+    "lv8_rand": ("subpoly", dict(SMALL, levels=8, r_max=48, T=15), ("rand", 29, 0.05), None),
+    "synth24_l4h8": ("lattice", None, ("rand", 31, 0.1), (24, 19, dict(num_layers=4, num_hidden=8))),
+    "synth20_h32": ("lattice", None, ("rand", 37, 0.1), (20, 19, dict(num_layers=2, num_hidden=32))),
 }
 # table params above this many floats are stored as the generator spec
 # (tropical/synthetic.py random_params) instead of the values
@@ -139,8 +151,8 @@ def run_case(name):
     kind, cfg, wspec, n = CASES[name]
     T = 19
     if kind == "lattice":
-        n, T = (n, 19) if isinstance(n, int) else n
-        cfg = syn.net_config_for_lattice(n, T)
+        n, T, over = (n, 19, {}) if isinstance(n, int) else (tuple(n) + ({},))[:3]
+        cfg = dict(syn.net_config_for_lattice(n, T), **over)
     net = model.Net(**cfg)
     params = build_params(cfg, wspec, net)
     net.load_state_dict({k: torch.from_numpy(v.astype(np.float32)) for k, v in params.items()})
@@ -153,7 +165,8 @@ def run_case(name):
         # centred output bias is stored as a value
         out["gen"] = np.array([wspec[1], wspec[2], n_table], dtype=np.float64)
         if wspec[0] == "rand":
-            out["p:fc.2.bias"] = params["fc.2.bias"]
+            last = f"fc.{len(net.fc) - 1}.bias"
+            out["p:" + last] = params[last]
     else:
         for k, v in params.items():
             out["p:" + k] = v
