@@ -167,10 +167,15 @@ k_bucket_count(const int32_t* __restrict__ members, int64_t S, int64_t V, int64_
       l4[i] = make_uint4(0, 0, 0, 0);
     if (blockIdx.x == 0 && threadIdx.x < (nlive & 15)) live[(n16 << 4) + threadIdx.x] = 0;
   }
-  for (int i = threadIdx.x; i < NB; i += TNP_BLOCK) hist[i] = 0;
-  __syncthreads();
   const uint64_t below = (idx >= 64) ? ~0ull : ((1ull << idx) - 1ull);
   const int64_t base = (int64_t)blockIdx.x * TNP_BLOCK * BK_IPT;
+  // workgroups past the members only zero live flags: no histogram to clear
+  // or flush (a near-empty step's grid is sized by the live-flag zeroing)
+  const bool counts = base < M;
+  if (counts) {
+    for (int i = threadIdx.x; i < NB; i += TNP_BLOCK) hist[i] = 0;
+    __syncthreads();
+  }
   int64_t aug = 0;
   bool k0 = false;
   // every item's loads in flight before any is used
@@ -226,9 +231,11 @@ k_bucket_count(const int32_t* __restrict__ members, int64_t S, int64_t V, int64_
     k0 |= kz == 0;
   }
   if (__ballot(k0) && tnp::lane() == 0) atomicOr((unsigned long long*)&ctr[CTR_K0], 1ull);
-  __syncthreads();
-  for (int i = threadIdx.x; i < NB; i += TNP_BLOCK)
-    if (hist[i]) atomicAdd(&bcount[i], hist[i]);
+  if (counts) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < NB; i += TNP_BLOCK)
+      if (hist[i]) atomicAdd(&bcount[i], hist[i]);
+  }
   int64_t tot;
   tnp::block_scan_excl(aug, lds, tot);
   if (threadIdx.x == 0) tnp::st_agent(part + blockIdx.x, tot);

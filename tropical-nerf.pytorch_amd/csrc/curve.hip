@@ -738,73 +738,95 @@ __device__ __forceinline__ float mm1_16(const float* x, const float* W, int ld, 
 // pre-activations of planes j0, j1 at u (preprocessed) and d(d0^2 + d1^2)/du
 // exactly as torch autograd computes it on CPU for a G-row batch
 // (subpoly_debug.py:143-148): forward with MKL's G-row schedules, backward
-// through AddmmBackward (mm(grad, W): sequential fma; 1-row layer-2 tree),
-// threshold_backward, and the encoding's input gradient (oracle/encoding.py
-// _GridFn.backward op order).
-template <int LV, int H>
+// through AddmmBackward (mm(grad, W): sequential fma; the 1-row tree of a
+// 16 x 16 layer), threshold_backward, and the encoding's input gradient
+// (oracle/encoding.py _GridFn.backward op order).  NL - 1 hidden layers of
+// H = 16 (the shapes whose backward schedules are verified).
+template <int LV, int H, int NL>
 __device__ __forceinline__ void plane_pair_grad(const NetDev& net, const float* w, const float u[3],
                                                 int j0, int j1, int mh, int mo, bool one_row,
                                                 float& d0, float& d1, float gu[3]) {
   constexpr int IN = 2 * LV;
-  float f[IN], a1[H], h1[H], a2[H], h2[H], o[2];
+  constexpr int NH = NL - 1;
+  float f[IN], a[NH][H], h[H], o[2];
   encode<LV>(net, u, f);
-  const float* W0 = w;
-  const float* W1 = W0 + H * IN + H;
-  const float* W2 = W1 + H * H + H;
-  linear_mode<IN, H>(W0, W0 + H * IN, f, a1, mh);
+  const float* Wl[NH];
+  Wl[0] = w;
 #pragma unroll
-  for (int j = 0; j < H; ++j) h1[j] = fmaxf(a1[j], 0.f);
-  linear_mode<H, H>(W1, W1 + H * H, h1, a2, mh);
+  for (int l = 1; l < NH; ++l) Wl[l] = Wl[l - 1] + (l == 1 ? H * IN + H : H * H + H);
+  const float* WL = Wl[NH - 1] + (NH == 1 ? H * IN + H : H * H + H);
+  linear_mode<IN, H>(Wl[0], Wl[0] + H * IN, f, a[0], mh);
 #pragma unroll
-  for (int j = 0; j < H; ++j) h2[j] = fmaxf(a2[j], 0.f);
-  linear_mode<H, 2>(W2, W2 + 2 * H, h2, o, mo);
+  for (int j = 0; j < H; ++j) h[j] = fmaxf(a[0][j], 0.f);
+#pragma unroll
+  for (int l = 1; l < NH; ++l) {
+    linear_mode<H, H>(Wl[l], Wl[l] + H * H, h, a[l], mh);
+#pragma unroll
+    for (int j = 0; j < H; ++j) h[j] = fmaxf(a[l][j], 0.f);
+  }
+  linear_mode<H, 2>(WL, WL + 2 * H, h, o, mo);
   float last = __fsub_rn(o[1], o[0]);
-  d0 = j0 < H ? a1[j0] : (j0 < 2 * H ? a2[j0 - H] : last);
-  d1 = j1 < H ? a1[j1] : (j1 < 2 * H ? a2[j1 - H] : last);
-  // seeds of y = d0^2 + d1^2 on the gathered pre-activations (2 d, exact)
-  float g1[H], g2[H], go = 0.f;
+  d0 = last;
+  d1 = last;
 #pragma unroll
-  for (int j = 0; j < H; ++j) g1[j] = g2[j] = 0.f;
+  for (int l = 0; l < NH; ++l)
+#pragma unroll
+    for (int k = 0; k < H; ++k) {
+      if (j0 == l * H + k) d0 = a[l][k];
+      if (j1 == l * H + k) d1 = a[l][k];
+    }
+  // seeds of y = d0^2 + d1^2 on the gathered pre-activations (2 d, exact)
+  float g[NH][H], go = 0.f;
+#pragma unroll
+  for (int l = 0; l < NH; ++l)
+#pragma unroll
+    for (int k = 0; k < H; ++k) g[l][k] = 0.f;
   const int js[2] = {j0, j1};
   const float ds[2] = {d0, d1};
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    float g = __fmul_rn(2.f, ds[s]);
+    float gs = __fmul_rn(2.f, ds[s]);
     int j = js[s];
 #pragma unroll
+    for (int l = 0; l < NH; ++l)
+#pragma unroll
+      for (int k = 0; k < H; ++k)
+        if (j == l * H + k) g[l][k] = __fadd_rn(g[l][k], gs);
+    if (j == NH * H) go = __fadd_rn(go, gs);
+  }
+  // last layer (o1 - o0): mm([-go, go], W), K = 2 sequential fma; ReLU
+#pragma unroll
+  for (int k = 0; k < H; ++k) {
+    float v = __fmaf_rn(go, WL[H + k], __fmul_rn(-go, WL[k]));
+    if (a[NH - 1][k] > 0.f) g[NH - 1][k] = __fadd_rn(g[NH - 1][k], v);
+  }
+  // hidden H x H layers, top down: mm(g_a, W) ; ReLU
+#pragma unroll
+  for (int l = NH - 1; l >= 1; --l) {
+    float gp[H];
+#pragma unroll
     for (int k = 0; k < H; ++k) {
-      if (j == k) g1[k] = __fadd_rn(g1[k], g);
-      if (j == H + k) g2[k] = __fadd_rn(g2[k], g);
+      float v;
+      if (one_row) {
+        v = mm1_16(g[l], Wl[l], H, k);
+      } else {
+        v = 0.f;
+#pragma unroll
+        for (int j = 0; j < H; ++j) v = __fmaf_rn(g[l][j], Wl[l][j * H + k], v);
+      }
+      gp[k] = a[l - 1][k] > 0.f ? __fadd_rn(g[l - 1][k], v) : g[l - 1][k];
     }
-    if (j == 2 * H) go = __fadd_rn(go, g);
-  }
-  // layer 3 (o1 - o0): mm([-go, go], W2), K = 2 sequential fma; ReLU 2
 #pragma unroll
-  for (int k = 0; k < H; ++k) {
-    float v = __fmaf_rn(go, W2[H + k], __fmul_rn(-go, W2[k]));
-    if (a2[k] > 0.f) g2[k] = __fadd_rn(g2[k], v);
+    for (int k = 0; k < H; ++k) g[l - 1][k] = gp[k];
   }
-  // layer 2: mm(g_a2, W1) ; ReLU 1
-  float ga1[H];
-#pragma unroll
-  for (int k = 0; k < H; ++k) {
-    float v;
-    if (one_row) {
-      v = mm1_16(g2, W1, H, k);
-    } else {
-      v = 0.f;
-#pragma unroll
-      for (int j = 0; j < H; ++j) v = __fmaf_rn(g2[j], W1[j * H + k], v);
-    }
-    ga1[k] = a1[k] > 0.f ? __fadd_rn(g1[k], v) : g1[k];
-  }
-  // layer 1: mm(g_a1, W0), sequential fma
+  // first layer: mm(g_a0, W0), sequential fma
+  const float* W0 = Wl[0];
   float df[IN];
 #pragma unroll
   for (int m = 0; m < IN; ++m) {
     float v = 0.f;
 #pragma unroll
-    for (int k = 0; k < H; ++k) v = __fmaf_rn(ga1[k], W0[k * IN + m], v);
+    for (int k = 0; k < H; ++k) v = __fmaf_rn(g[0][k], W0[k * IN + m], v);
     df[m] = v;
   }
   // encoding input gradient: per level, per corner, per dim
@@ -814,13 +836,13 @@ __device__ __forceinline__ void plane_pair_grad(const NetDev& net, const float* 
   for (int l = 0; l < LV; ++l) {
     const float sc = net.scales[l];
     float t[3];
-    uint32_t g[3];
+    uint32_t gi[3];
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
       float pos = __fadd_rn(__fmul_rn(u[d], sc), 0.5f);
       float fl = floorf(pos);
       t[d] = __fsub_rn(pos, fl);
-      g[d] = (uint32_t)(int)fl;
+      gi[d] = (uint32_t)(int)fl;
     }
     const uint32_t res = (uint32_t)net.res[l];
 #pragma unroll
@@ -831,7 +853,7 @@ __device__ __forceinline__ void plane_pair_grad(const NetDev& net, const float* 
       for (int d = 0; d < 3; ++d) {
         bool up = (c >> d) & 1;
         fc[d] = up ? t[d] : __fsub_rn(1.f, t[d]);
-        gc[d] = g[d] + (up ? 1u : 0u);
+        gc[d] = gi[d] + (up ? 1u : 0u);
       }
       uint32_t id = net.dense[l] ? (gc[0] + gc[1] * res + gc[2] * (res * res))
                                  : (gc[0] ^ (gc[1] * P1) ^ (gc[2] * P2));
@@ -853,7 +875,7 @@ __device__ __forceinline__ void plane_pair_grad(const NetDev& net, const float* 
 // deal_with_gradient_descent (subpoly_debug.py:121-165), one thread per row.
 // record != 0: AND this row's per-iteration "both residuals <= eps" bits into
 // conv[0..7] (iteration i -> bit i) so the host finds the common stop.
-template <int LV, int H>
+template <int LV, int H, int NL>
 __global__ void __launch_bounds__(TNP_BLOCK)
 k_descend(NetDev net, int64_t G, const int32_t* __restrict__ glist,
           const int32_t* __restrict__ crow, const int32_t* __restrict__ sa,
@@ -861,7 +883,7 @@ k_descend(NetDev net, int64_t G, const int32_t* __restrict__ glist,
           const int32_t* __restrict__ plane, int idx, float eps, int iters, int record,
           float* __restrict__ ints, float* __restrict__ d0s, float* __restrict__ d1s,
           unsigned long long* __restrict__ conv) {
-  constexpr int NW = NetShape<LV, H, 3>::NW;
+  constexpr int NW = NetShape<LV, H, NL>::NW;
   __shared__ float w[NW];
   for (int i = threadIdx.x; i < NW; i += blockDim.x) w[i] = net.weights[i];
   __syncthreads();
@@ -877,7 +899,7 @@ k_descend(NetDev net, int64_t G, const int32_t* __restrict__ glist,
     x[d] = ints[3 * b + d];
   }
   const int j0 = plane[b];
-  const int mh = lin_mode(G, false), mo = lin_mode(G, true);
+  const int mh = lin_mode<H, H>(G), mo = lin_mode<H, 2>(G);  // (H = 16: layer 0's mode too)
   uint64_t bits[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   float d0 = 1.f, d1 = 1.f;
   for (int it = 0; it < iters; ++it) {
@@ -885,7 +907,7 @@ k_descend(NetDev net, int64_t G, const int32_t* __restrict__ glist,
 #pragma unroll
     for (int d = 0; d < 3; ++d)
       u[d] = __fmul_rn(__fadd_rn(__fadd_rn(e0[d], __fmul_rn(x[d], de[d])), 1.0f), 0.5f);  // x/2 == x*0.5
-    plane_pair_grad<LV, H>(net, w, u, j0, idx, mh, mo, G == 1, d0, d1, gu);
+    plane_pair_grad<LV, H, NL>(net, w, u, j0, idx, mh, mo, G == 1, d0, d1, gu);
     float gx[3], nn = 0.f;
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
@@ -919,9 +941,9 @@ __device__ __forceinline__ float lane_f(float v, int l) {
 // table entry is gathered once per iteration and reused by the backward
 // pass) and lane j < H neuron j of each layer; every sum keeps the
 // single-thread order above -- corner sums, sequential fma chains, the
-// 1-row layer-2 tree -- over operands broadcast with v_readlane, so the
+// 1-row 16 x 16 tree -- over operands broadcast with v_readlane, so the
 // result is bitwise that of k_descend.
-template <int LV, int H>
+template <int LV, int H, int NL>
 __global__ void __launch_bounds__(64)
 k_descend_wave(NetDev net, int64_t G, const int32_t* __restrict__ glist,
                const int32_t* __restrict__ crow, const int32_t* __restrict__ sa,
@@ -931,7 +953,8 @@ k_descend_wave(NetDev net, int64_t G, const int32_t* __restrict__ glist,
                unsigned long long* __restrict__ conv) {
   static_assert(LV * 8 <= 64 && H <= 64, "one wave holds every corner and neuron");
   constexpr int IN = 2 * LV;
-  constexpr int NW = NetShape<LV, H, 3>::NW;
+  constexpr int NH = NL - 1;
+  constexpr int NW = NetShape<LV, H, NL>::NW;
   __shared__ float w[NW];
   for (int i = threadIdx.x; i < NW; i += blockDim.x) w[i] = net.weights[i];
   __syncthreads();
@@ -948,7 +971,7 @@ k_descend_wave(NetDev net, int64_t G, const int32_t* __restrict__ glist,
     x[d] = ints[3 * b + d];
   }
   const int j0 = plane[b];
-  const int mh = lin_mode(G, false), mo = lin_mode(G, true);
+  const int mh = lin_mode<H, H>(G), mo = lin_mode<H, 2>(G);  // (H = 16: layer 0's mode too)
   const bool one_row = G == 1;
   // lane roles
   const int nj = lane & (H - 1);                      // neuron
@@ -964,9 +987,11 @@ k_descend_wave(NetDev net, int64_t G, const int32_t* __restrict__ glist,
       size = net.sizes[l];
       dense = net.dense[l] != 0;
     }
-  const float* W0 = w;
-  const float* W1 = W0 + H * IN + H;
-  const float* W2 = W1 + H * H + H;
+  const float* Wl[NH];
+  Wl[0] = w;
+#pragma unroll
+  for (int l = 1; l < NH; ++l) Wl[l] = Wl[l - 1] + (l == 1 ? H * IN + H : H * H + H);
+  const float* WL = Wl[NH - 1] + (NH == 1 ? H * IN + H : H * H + H);
   uint64_t word = 0;  // convergence bits of iterations [64 k, 64 k + 64)
   float d0 = 1.f, d1 = 1.f;
   for (int it = 0; it < iters; ++it) {
@@ -1008,49 +1033,64 @@ k_descend_wave(NetDev net, int64_t G, const int32_t* __restrict__ glist,
       f[2 * l] = a0;
       f[2 * l + 1] = a1;
     }
-    // forward, neuron nj per lane
-    const float a1 = neuron_mode<IN, H>(W0, W0 + H * IN, f, nj, mh);
-    float h1[H];
+    // forward, neuron nj per lane; a[l]: this lane's neuron of hidden layer l
+    float a[NH];
+    float hh[H];
+    a[0] = neuron_mode<IN, H>(Wl[0], Wl[0] + H * IN, f, nj, mh);
 #pragma unroll
-    for (int j = 0; j < H; ++j) h1[j] = fmaxf(lane_f(a1, j), 0.f);
-    const float a2 = neuron_mode<H, H>(W1, W1 + H * H, h1, nj, mh);
-    float h2[H];
+    for (int l = 1; l < NH; ++l) {
 #pragma unroll
-    for (int j = 0; j < H; ++j) h2[j] = fmaxf(lane_f(a2, j), 0.f);
-    const float o = neuron_mode<H, 2>(W2, W2 + 2 * H, h2, lane & 1, mo);
+      for (int j = 0; j < H; ++j) hh[j] = fmaxf(lane_f(a[l - 1], j), 0.f);
+      a[l] = neuron_mode<H, H>(Wl[l], Wl[l] + H * H, hh, nj, mh);
+    }
+#pragma unroll
+    for (int j = 0; j < H; ++j) hh[j] = fmaxf(lane_f(a[NH - 1], j), 0.f);
+    const float o = neuron_mode<H, 2>(WL, WL + 2 * H, hh, lane & 1, mo);
     const float last = __fsub_rn(lane_f(o, 1), lane_f(o, 0));
-    d0 = j0 < H ? lane_f(a1, j0) : (j0 < 2 * H ? lane_f(a2, j0 - H) : last);
-    d1 = idx < H ? lane_f(a1, idx) : (idx < 2 * H ? lane_f(a2, idx - H) : last);
+    d0 = last;
+    d1 = last;
+#pragma unroll
+    for (int l = 0; l < NH; ++l) {
+      if (j0 >= l * H && j0 < (l + 1) * H) d0 = lane_f(a[l], j0 - l * H);
+      if (idx >= l * H && idx < (l + 1) * H) d1 = lane_f(a[l], idx - l * H);
+    }
     // backward: seeds of d0^2 + d1^2, neuron nj per lane
-    float g1 = 0.f, g2 = 0.f, go = 0.f;
+    float gl[NH], go = 0.f;
+#pragma unroll
+    for (int l = 0; l < NH; ++l) gl[l] = 0.f;
     {
       const int js[2] = {j0, idx};
       const float ds[2] = {d0, d1};
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const float gs = __fmul_rn(2.f, ds[s]);
-        if (js[s] == nj) g1 = __fadd_rn(g1, gs);
-        if (js[s] == H + nj) g2 = __fadd_rn(g2, gs);
-        if (js[s] == 2 * H) go = __fadd_rn(go, gs);
+#pragma unroll
+        for (int l = 0; l < NH; ++l)
+          if (js[s] == l * H + nj) gl[l] = __fadd_rn(gl[l], gs);
+        if (js[s] == NH * H) go = __fadd_rn(go, gs);
       }
     }
-    const float v3 = __fmaf_rn(go, W2[H + nj], __fmul_rn(-go, W2[nj]));
-    if (a2 > 0.f) g2 = __fadd_rn(g2, v3);
-    float g2u[H];
+    const float v3 = __fmaf_rn(go, WL[H + nj], __fmul_rn(-go, WL[nj]));
+    if (a[NH - 1] > 0.f) gl[NH - 1] = __fadd_rn(gl[NH - 1], v3);
 #pragma unroll
-    for (int j = 0; j < H; ++j) g2u[j] = lane_f(g2, j);
-    float v2;
-    if (one_row) {
-      v2 = mm1_16(g2u, W1, H, nj);
-    } else {
-      v2 = 0.f;
+    for (int l = NH - 1; l >= 1; --l) {
+      float gu_[H];
 #pragma unroll
-      for (int j = 0; j < H; ++j) v2 = __fmaf_rn(g2u[j], W1[j * H + nj], v2);
+      for (int j = 0; j < H; ++j) gu_[j] = lane_f(gl[l], j);
+      float v2;
+      if (one_row) {
+        v2 = mm1_16(gu_, Wl[l], H, nj);
+      } else {
+        v2 = 0.f;
+#pragma unroll
+        for (int j = 0; j < H; ++j) v2 = __fmaf_rn(gu_[j], Wl[l][j * H + nj], v2);
+      }
+      gl[l - 1] = a[l - 1] > 0.f ? __fadd_rn(gl[l - 1], v2) : gl[l - 1];
     }
-    const float ga1 = a1 > 0.f ? __fadd_rn(g1, v2) : g1;
     float ga1u[H];
 #pragma unroll
-    for (int k = 0; k < H; ++k) ga1u[k] = lane_f(ga1, k);
+    for (int k = 0; k < H; ++k) ga1u[k] = lane_f(gl[0], k);
+    const float* W0 = Wl[0];
     const int m = lane & (IN - 1);
     float dfm = 0.f;
 #pragma unroll
@@ -1172,13 +1212,6 @@ __global__ void k_compact_splits(int64_t S, int K, const int32_t* __restrict__ k
   edges[2 * (int64_t)eidx[r] + 1] = (int32_t)(V + n);
 }
 
-#define TNP_DISPATCH(LV, BODY)                                      \
-  switch (LV) {                                                     \
-    case 2: { constexpr int L_ = 2; BODY; break; }                  \
-    case 4: { constexpr int L_ = 4; BODY; break; }                  \
-    default: tnp_set_error("n_levels=%d not instantiated", LV); return -1; \
-  }
-
 }  // namespace
 
 int launch_curve_flags(const int32_t* sa, const int32_t* sb, int64_t S, const float* xyz, float eps,
@@ -1235,18 +1268,36 @@ int launch_descend(const NetDev& net, int64_t G, const int32_t* glist, const int
                    unsigned long long* conv, hipStream_t s) {
   if (G <= 0) return 0;
   if (!net_supported(net)) { tnp_set_error("unsupported net shape"); return -1; }
+  if (net.num_hidden != 16 || (net.n_levels != 2 && net.n_levels != 4)) {
+    // the descent reproduces autograd's CPU backward schedules (AddmmBackward,
+    // subpoly_debug.py:143-148), reverse-engineered for 16-hidden nets of 2 or
+    // 4 levels (the 1-row 16 x 16 tree; sequential fma into 4 / 8 features)
+    tnp_set_error("curve path: the gradient-descent fallback (subpoly_debug.py:121-165) is built for 16-hidden "
+                  "nets of 2 or 4 levels (this net: %d hidden, %d levels)", net.num_hidden, net.n_levels);
+    return -1;
+  }
   if (iters > 512) { tnp_set_error("descend: at most 512 iterations"); return -1; }
   // TNP_DESCEND_THREAD=1: the one-thread-per-row kernel (tests compare both)
   const char* pt = getenv("TNP_DESCEND_THREAD");
   const bool per_thread = pt && pt[0] == '1';
-  TNP_DISPATCH(net.n_levels, {
-    if (per_thread)
-      hipLaunchKernelGGL((k_descend<L_, 16>), dim3(tnp_grid(G)), dim3(TNP_BLOCK), 0, s, net, G, glist,
-                         crow, sa, sb, xyz, plane, idx, eps, iters, record, ints, d0s, d1s, conv);
-    else
-      hipLaunchKernelGGL((k_descend_wave<L_, 16>), dim3((unsigned)G), dim3(64), 0, s, net, G, glist,
-                         crow, sa, sb, xyz, plane, idx, eps, iters, record, ints, d0s, d1s, conv);
-  });
+#define TNP_DESCEND(L_, NL_)                                                                                \
+  if (per_thread)                                                                                            \
+    hipLaunchKernelGGL((k_descend<L_, 16, NL_>), dim3(tnp_grid(G)), dim3(TNP_BLOCK), 0, s, net, G, glist,   \
+                       crow, sa, sb, xyz, plane, idx, eps, iters, record, ints, d0s, d1s, conv);             \
+  else                                                                                                       \
+    hipLaunchKernelGGL((k_descend_wave<L_, 16, NL_>), dim3((unsigned)G), dim3(64), 0, s, net, G, glist,    \
+                       crow, sa, sb, xyz, plane, idx, eps, iters, record, ints, d0s, d1s, conv);
+  const int key = net.n_levels * 8 + net.num_layers;
+  switch (key) {
+    case 2 * 8 + 2: TNP_DESCEND(2, 2) break;
+    case 2 * 8 + 3: TNP_DESCEND(2, 3) break;
+    case 2 * 8 + 4: TNP_DESCEND(2, 4) break;
+    case 4 * 8 + 2: TNP_DESCEND(4, 2) break;
+    case 4 * 8 + 3: TNP_DESCEND(4, 3) break;
+    case 4 * 8 + 4: TNP_DESCEND(4, 4) break;
+    default: tnp_set_error("descend: net shape not instantiated"); return -1;
+  }
+#undef TNP_DESCEND
   TNP_CHECK(hipGetLastError());
   return 0;
 }

@@ -1609,8 +1609,8 @@ extern "C" int tnp_engine_faces(tnp_engine* e, void* stream, int64_t* n_tri, int
   e->n_tri = e->n_faces = 0;
   *n_tri = *n_faces = 0;
   if (V == 0) return 0;
-  if (e->net.n_marks + 2 >= 1024 || K - 1 > 34) {
-    tnp_set_error("faces: region key needs n_marks+2 < 1024 and <= 34 planes");
+  if (e->net.n_marks + 2 >= 1024) {
+    tnp_set_error("faces: region keys hold n_marks + 2 < 1024 cells per axis");
     return -1;
   }
   const uint64_t pmask = (K - 1 >= 64) ? ~0ull : ((1ull << (K - 1)) - 1ull);
@@ -1627,12 +1627,14 @@ extern "C" int tnp_engine_faces(tnp_engine* e, void* stream, int64_t* n_tri, int
   if (e->h_ctr[CTR_AUX] > 30) { tnp_set_error("faces: a vertex lies on %lld planes", (long long)e->h_ctr[CTR_AUX]); return -1; }
   int64_t cap = 1024;
   while (cap < 2 * A) cap <<= 1;
-  if (buf_ensure(fs[FS_TABLE], cap * 8, s) || buf_ensure(fs[FS_CNT], cap * 4, s) ||
+  // region table: cap sign words + cap cell words (faces.hip probe_insert)
+  if (buf_ensure(fs[FS_TABLE], cap * 16, s) || buf_ensure(fs[FS_CNT], cap * 4, s) ||
       buf_ensure(fs[FS_KC], cap * 4, s) || buf_ensure(fs[FS_KF], cap * 4, s) ||
       buf_ensure(fs[FS_MEMOFF], cap * 8, s) || buf_ensure(fs[FS_RID], cap * 8, s) ||
       buf_ensure(fs[FS_CUR], cap * 4, s))
     return -1;
-  TNP_CHECK(hipMemsetAsync(fs[FS_TABLE].p, 0xFF, cap * 8, s));
+  TNP_CHECK(hipMemsetAsync(fs[FS_TABLE].p, 0xFF, cap * 8, s));                                // EMPTY signs
+  TNP_CHECK(hipMemsetAsync(static_cast<char*>(fs[FS_TABLE].p) + cap * 8, 0, cap * 8, s));    // NO_CELL
   TNP_CHECK(hipMemsetAsync(fs[FS_CNT].p, 0, cap * 4, s));
   TNP_CHECK(hipMemsetAsync(fs[FS_CUR].p, 0, cap * 4, s));
   if (launch_face_insert(V, grid, pos, zero, pmask, P<uint64_t>(fs[FS_TABLE]), (uint64_t)cap - 1,

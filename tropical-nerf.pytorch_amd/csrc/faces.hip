@@ -4,9 +4,11 @@
 //  F1 regions  : every surface vertex with k zeros among (3 grid + K-1 plane)
 //                sign columns spans 2^k sign-resolved regions
 //                (regions_to_vertices, subpoly.py:281-340).  Each (cell,
-//                signs) key is hashed into an open-addressing table (u64
-//                CAS); the slot is the region id.  Only ids are hashed --
-//                no output order comes from the table.
+//                signs) key -- two words: the 30-bit cell, the plane signs
+//                (up to 62 planes) -- is hashed into an open-addressing
+//                table (the signs word claimed by CAS, the cell word
+//                published behind it); the slot is the region id.  Only ids
+//                are hashed -- no output order comes from the table.
 //  F2 rows     : regions with >= 3 members (mean_points_with_valid) keep
 //                their member list sorted by (k, vertex id) = the stable
 //                argsort order of r_idx_as_tensor (subpoly.py:357).
@@ -61,9 +63,17 @@ __device__ __forceinline__ VKey vkey(uint64_t g, uint64_t pos, uint64_t zero, ui
   return r;
 }
 
+// a region key: cell word (3 x 10-bit cell coordinates + 2, never 0) and the
+// plane-sign word (bit j: plane j positive; planes < K - 1 <= 62, so never
+// all ones)
+struct RKey {
+  uint64_t cell, signs;
+};
+constexpr uint64_t NO_CELL = 0ull;
+
 // augmented key of pattern p (torch.cartesian_prod order: the first zero
 // column is the most significant pattern bit; 0 -> -1, 1 -> +1)
-__device__ __forceinline__ uint64_t aug_key(const VKey& v, uint32_t p) {
+__device__ __forceinline__ RKey aug_key(const VKey& v, uint32_t p) {
   int cell[3] = {v.off[0], v.off[1], v.off[2]};
   int j = 0;
   for (int i = 0; i < v.nzg; ++i, ++j) {
@@ -76,8 +86,8 @@ __device__ __forceinline__ uint64_t aug_key(const VKey& v, uint32_t p) {
     int b = (p >> (v.k - 1 - j)) & 1;
     if (b) signs |= 1ull << pl;
   }
-  return ((uint64_t)(cell[0] + 2) << 54) | ((uint64_t)(cell[1] + 2) << 44) |
-         ((uint64_t)(cell[2] + 2) << 34) | signs;
+  return RKey{((uint64_t)(cell[0] + 2) << 20) | ((uint64_t)(cell[1] + 2) << 10) | (uint64_t)(cell[2] + 2),
+              signs};
 }
 
 __global__ void k_face_count(int64_t V, const uint64_t* __restrict__ grid, const uint64_t* __restrict__ pos,
@@ -99,19 +109,43 @@ __global__ void k_face_count(int64_t V, const uint64_t* __restrict__ grid, const
   }
 }
 
-__device__ __forceinline__ uint64_t probe_insert(uint64_t* table, uint64_t mask, uint64_t key) {
-  uint64_t h = mix64(key) & mask;
+// table: [cap] sign words (EMPTY: free) then [cap] cell words (NO_CELL: not
+// yet published).  A slot is claimed by CAS on its sign word and the
+// claiming lane publishes the cell word in the same loop round; a lane that
+// found the same sign word reads the cell word once per round (no inner
+// wait: every lane advances one step per round, so a lane never waits on a
+// store its own wave has not yet issued).
+__device__ __forceinline__ uint64_t rkey_hash(const RKey& k) { return mix64(k.signs ^ mix64(k.cell)); }
+
+__device__ __forceinline__ uint64_t probe_insert(uint64_t* table, uint64_t mask, RKey key) {
+  uint64_t* cells = table + mask + 1;
+  uint64_t h = rkey_hash(key) & mask;
+  bool polling = false;  // slot h holds our signs; its cell word was not published yet
   while (true) {
-    uint64_t prev = atomicCAS((unsigned long long*)&table[h], (unsigned long long)EMPTY,
-                              (unsigned long long)key);
-    if (prev == EMPTY || prev == key) return h;
+    if (!polling) {
+      const uint64_t prev = atomicCAS((unsigned long long*)&table[h], (unsigned long long)EMPTY,
+                                      (unsigned long long)key.signs);
+      if (prev == EMPTY) {
+        tnp::st_agent(cells + h, key.cell);
+        return h;
+      }
+      if (prev != key.signs) {
+        h = (h + 1) & mask;
+        continue;
+      }
+    }
+    const uint64_t c = tnp::ld_agent(cells + h);
+    polling = c == NO_CELL;
+    if (polling) continue;
+    if (c == key.cell) return h;
     h = (h + 1) & mask;
   }
 }
 
-__device__ __forceinline__ uint64_t probe_find(const uint64_t* table, uint64_t mask, uint64_t key) {
-  uint64_t h = mix64(key) & mask;
-  while (table[h] != key) h = (h + 1) & mask;
+__device__ __forceinline__ uint64_t probe_find(const uint64_t* table, uint64_t mask, RKey key) {
+  const uint64_t* cells = table + mask + 1;
+  uint64_t h = rkey_hash(key) & mask;
+  while (table[h] != key.signs || cells[h] != key.cell) h = (h + 1) & mask;
   return h;
 }
 

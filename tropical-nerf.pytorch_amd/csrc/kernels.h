@@ -31,6 +31,55 @@ struct NetDev {
 static inline int net_K(const NetDev& n) { return (n.num_layers - 1) * n.num_hidden + 1; }
 int net_supported(const NetDev& n);  // 1 if an instantiation exists
 
+// ---- net_lv.hip: the kernels of one level count (one translation unit per
+// level count 2..8, -DTNP_LV; explicit specializations, dispatched by the
+// launch_* functions of net.hip / skeleton.hip) ----
+template <int LV>
+int lv_forward(const NetDev& net, const float* xyz, int64_t n, float* pre, int64_t ld, int group, hipStream_t s,
+               float* out2, uint64_t* pos, uint64_t* zero, uint64_t* grid, uint64_t* pz);
+template <int LV>
+int lv_forward_new(const NetDev& net, const float* xyz, int64_t n, float* pre, int64_t ld, int64_t V,
+                   int keep_from, const int32_t* sa, const int32_t* sb, int idx, int own_lo, int own_hi,
+                   uint64_t* pos, uint64_t* zero, uint64_t* grid, uint64_t* shared, int64_t* ctr, uint64_t* pz,
+                   const float* col, hipStream_t s);
+template <int LV>
+int lv_sdf_grad(const NetDev& net, const float* xyz, int64_t n, float* sdf, float* grad, hipStream_t s);
+template <int LV>
+int lv_skel_eval(const NetDev& net, int i0, int j0, int k0, int n0, int n1, int n2, float* dist,
+                 unsigned int* gmax_bits, hipStream_t s);
+template <int LV>
+int lv_encode(const NetDev& net, const float* x01, int64_t n, float* out, hipStream_t s);
+#define TNP_LV_DECLARE(L)                                                                                   \
+  template <> int lv_forward<L>(const NetDev&, const float*, int64_t, float*, int64_t, int, hipStream_t, float*, \
+                                uint64_t*, uint64_t*, uint64_t*, uint64_t*);                                  \
+  template <> int lv_forward_new<L>(const NetDev&, const float*, int64_t, float*, int64_t, int64_t, int,        \
+                                    const int32_t*, const int32_t*, int, int, int, uint64_t*, uint64_t*,      \
+                                    uint64_t*, uint64_t*, int64_t*, uint64_t*, const float*, hipStream_t);    \
+  template <> int lv_sdf_grad<L>(const NetDev&, const float*, int64_t, float*, float*, hipStream_t);           \
+  template <> int lv_skel_eval<L>(const NetDev&, int, int, int, int, int, int, float*, unsigned int*,         \
+                                  hipStream_t);                                                               \
+  template <> int lv_encode<L>(const NetDev&, const float*, int64_t, float*, hipStream_t);
+TNP_LV_DECLARE(2)
+TNP_LV_DECLARE(3)
+TNP_LV_DECLARE(4)
+TNP_LV_DECLARE(5)
+TNP_LV_DECLARE(6)
+TNP_LV_DECLARE(7)
+TNP_LV_DECLARE(8)
+#undef TNP_LV_DECLARE
+// the level-count dispatch of the lv_* functions: BODY sees constexpr L_
+#define TNP_LV_SWITCH(LV, BODY)                                                     \
+  switch (LV) {                                                                     \
+    case 2: { constexpr int L_ = 2; BODY; break; }                                  \
+    case 3: { constexpr int L_ = 3; BODY; break; }                                  \
+    case 4: { constexpr int L_ = 4; BODY; break; }                                  \
+    case 5: { constexpr int L_ = 5; BODY; break; }                                  \
+    case 6: { constexpr int L_ = 6; BODY; break; }                                  \
+    case 7: { constexpr int L_ = 7; BODY; break; }                                  \
+    case 8: { constexpr int L_ = 8; BODY; break; }                                  \
+    default: tnp_set_error("n_levels=%d not instantiated (2..8)", (int)(LV)); return -1; \
+  }
+
 // ---- net.hip ----
 // pre plane-major [K][ld]; rows [0, n)
 // pos/zero/grid/pz (group 1 only): the packed keys of k_keys written by the

@@ -171,44 +171,58 @@ __device__ __forceinline__ uint64_t grid_word(const float* marks, int M, float e
 
 // SDF = tanh(o1 - o0) and d SDF / d x (input gradient through ReLU masks and
 // the trilinear encoding; floor() has zero gradient so the cell on the right
-// is used on grid lines, as autograd through tcnn does).  w: packed weights.
-template <int LV, int H>
+// is used on grid lines, as autograd through tcnn does).  w: packed weights
+// of an NL-layer net (NL - 1 hidden layers of H).
+template <int LV, int H, int NL>
 __device__ __forceinline__ float sdf_grad(const NetDev& net, const float* w, const float x[3],
                                           float* grad) {
   constexpr int IN = 2 * LV;
-  float f[IN], a1[H], h1[H], a2[H], h2[H], o[2];
+  constexpr int NH = NL - 1;  // hidden layers
+  float f[IN], a[NH][H], h[H], o[2];
   encode<LV>(net, x, f);
-  const float* W0 = w;
-  const float* W1 = W0 + H * IN + H;
-  const float* W2 = W1 + H * H + H;
-  linear<IN, H>(W0, W0 + H * IN, f, a1);
+  const float* Wl[NH];
+  Wl[0] = w;
 #pragma unroll
-  for (int j = 0; j < H; ++j) h1[j] = fmaxf(a1[j], 0.f);
-  linear<H, H>(W1, W1 + H * H, h1, a2);
+  for (int l = 1; l < NH; ++l) Wl[l] = Wl[l - 1] + (l == 1 ? H * IN + H : H * H + H);
+  const float* WL = Wl[NH - 1] + (NH == 1 ? H * IN + H : H * H + H);
+  linear<IN, H>(Wl[0], Wl[0] + H * IN, f, a[0]);
 #pragma unroll
-  for (int j = 0; j < H; ++j) h2[j] = fmaxf(a2[j], 0.f);
-  linear<H, 2>(W2, W2 + 2 * H, h2, o);
+  for (int j = 0; j < H; ++j) h[j] = fmaxf(a[0][j], 0.f);
+#pragma unroll
+  for (int l = 1; l < NH; ++l) {
+    linear<H, H>(Wl[l], Wl[l] + H * H, h, a[l]);
+#pragma unroll
+    for (int j = 0; j < H; ++j) h[j] = fmaxf(a[l][j], 0.f);
+  }
+  linear<H, 2>(WL, WL + 2 * H, h, o);
   float y = tanhf(o[1] - o[0]);
   if (grad == nullptr) return y;
   float gz = 1.f - y * y;
-  float d2[H], d1[H], df[IN];
+  float d[H], df[IN];
 #pragma unroll
   for (int j = 0; j < H; ++j) {
-    float v = gz * W2[H + j] - gz * W2[j];
-    d2[j] = a2[j] > 0.f ? v : 0.f;
+    float v = gz * WL[H + j] - gz * WL[j];
+    d[j] = a[NH - 1][j] > 0.f ? v : 0.f;
   }
 #pragma unroll
-  for (int k = 0; k < H; ++k) {
-    float v = 0.f;
+  for (int l = NH - 1; l >= 1; --l) {
+    float dp[H];
 #pragma unroll
-    for (int j = 0; j < H; ++j) v += d2[j] * W1[j * H + k];
-    d1[k] = a1[k] > 0.f ? v : 0.f;
+    for (int k = 0; k < H; ++k) {
+      float v = 0.f;
+#pragma unroll
+      for (int j = 0; j < H; ++j) v += d[j] * Wl[l][j * H + k];
+      dp[k] = a[l - 1][k] > 0.f ? v : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < H; ++k) d[k] = dp[k];
   }
+  const float* W0 = Wl[0];
 #pragma unroll
   for (int m = 0; m < IN; ++m) {
     float v = 0.f;
 #pragma unroll
-    for (int k = 0; k < H; ++k) v += d1[k] * W0[k * IN + m];
+    for (int k = 0; k < H; ++k) v += d[k] * W0[k * IN + m];
     df[m] = v;
   }
   float gx[3] = {0.f, 0.f, 0.f};
@@ -254,13 +268,20 @@ __device__ __forceinline__ float sdf_grad(const NetDev& net, const float* w, con
 
 // Batch-size-dependent summation schedules of x86 MKL sgemm (what
 // torch.nn.Linear computes on CPU in the reference), reverse-engineered
-// bitwise (oracle/subdivide.py::linear_seqfma, tools/mkl_order_probe.py):
+// bitwise for every layer shape of the supported nets (IN = 2 x levels or
+// H inputs, OUT = H or 2 outputs; oracle/subdivide.py::linear_seqfma,
+// tools/mkl_order_probe.py).  With p_k = x_k*W_jk rounded and the lanes of a
+// WD-wide vector (WD = next power of two >= IN, zero-padded; 16 lanes a
+// register: inputs 16..31 are fma'd onto lanes 0..15 first):
 //   SEQ   acc = 0; acc = fma(x_k, W_jk, acc); acc + b_j
-//   ONE   (a 1-row call) lanes {0, fma(x1,W_j1,x0*W_j0), x2*W_j2, ...},
-//         halving fold, + b_j; the 2-output layer adds x0*W_j0 after the
-//         fold of {0, x1*W_j1, x2*W_j2, ...}
-//   FOLD  (2-output layer, 2..15 rows) halving fold of x_k*W_jk, + b_j
+//   ONE   (a 1-row call) lanes {0, fma(x1,W_j1,p0), p2, ...}, halving fold,
+//         + b_j; the 2-output layer adds p0 after the fold of {0, p1, p2, ...}
+//   FOLD  (2-output layer, 2..15 rows; 8-output layer of <= 8 inputs, 2..7
+//         rows) halving fold of the p_k, + b_j; 32 inputs: lane i = p_i +
+//         p_{i+16} on even rows, fma(x_{i+16}, W, p_i) on odd rows
 enum LinMode { LIN_SEQ = 0, LIN_ONE = 1, LIN_FOLD = 2 };
+
+__host__ __device__ constexpr int next_pow2(int k) { return k <= 1 ? 1 : 2 * next_pow2((k + 1) / 2); }
 
 template <int IN>
 __device__ __forceinline__ float fold_lanes(float* l) {
@@ -272,49 +293,71 @@ __device__ __forceinline__ float fold_lanes(float* l) {
   return l[0];
 }
 
-// output j of linear_mode<IN, OUT> (the same ops, one output)
+// output j of linear_mode<IN, OUT> (the same ops, one output); row: the
+// row's index in the call (its parity picks the 32-input FOLD variant)
 template <int IN, int OUT>
 __device__ __forceinline__ float neuron_mode(const float* __restrict__ W, const float* __restrict__ b,
-                                             const float* in, int j, int mode) {
+                                             const float* in, int j, int mode, int64_t row = 0) {
   if (mode == LIN_SEQ) {
     float acc = 0.f;
 #pragma unroll
     for (int k = 0; k < IN; ++k) acc = __fmaf_rn(in[k], W[j * IN + k], acc);
     return __fadd_rn(acc, b[j]);
   }
-  float l[IN];
-#pragma unroll
-  for (int k = 0; k < IN; ++k) l[k] = __fmul_rn(in[k], W[j * IN + k]);
+  constexpr int WD = next_pow2(IN);
+  constexpr int LN = WD < 16 ? WD : 16;
+  static_assert(WD <= 32, "layers of at most 32 inputs");
+  // (a 32-input layer with more than 2 outputs -- 32-wide hidden layers --
+  // is compiled but never run: TNP_NET_SHAPES has no such shape, and MKL's
+  // 1-row schedule for it is not verified)
+  const float* Wj = W + j * IN;
+  float l[LN];
   float r;
   if (mode == LIN_FOLD) {
-    r = fold_lanes<IN>(l);
-  } else if (OUT == 2) {
-    float p0 = l[0];
-    l[0] = 0.f;
-    r = __fadd_rn(p0, fold_lanes<IN>(l));
+    if constexpr (WD <= 16) {
+#pragma unroll
+      for (int k = 0; k < WD; ++k) l[k] = k < IN ? __fmul_rn(in[k], Wj[k]) : 0.f;
+    } else {
+      const bool odd = row & 1;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float p = __fmul_rn(in[i], Wj[i]);
+        l[i] = odd ? __fmaf_rn(in[i + 16], Wj[i + 16], p) : __fadd_rn(p, __fmul_rn(in[i + 16], Wj[i + 16]));
+      }
+    }
+    r = fold_lanes<LN>(l);
   } else {
-    l[1] = __fmaf_rn(in[1], W[j * IN + 1], l[0]);
-    l[0] = 0.f;
-    r = fold_lanes<IN>(l);
+    float base[WD];
+#pragma unroll
+    for (int k = 0; k < WD; ++k) base[k] = k < IN ? __fmul_rn(in[k], Wj[k]) : 0.f;
+    const float p0 = base[0];
+    if (OUT != 2) base[1] = __fmaf_rn(in[1], Wj[1], p0);
+    base[0] = 0.f;
+#pragma unroll
+    for (int i = 0; i < LN; ++i) l[i] = (WD > 16 && i + 16 < IN) ? __fmaf_rn(in[i + 16], Wj[i + 16], base[i]) : base[i];
+    r = fold_lanes<LN>(l);
+    if (OUT == 2) r = __fadd_rn(p0, r);
   }
   return __fadd_rn(r, b[j]);
 }
 
 template <int IN, int OUT>
 __device__ __forceinline__ void linear_mode(const float* __restrict__ W, const float* __restrict__ b,
-                                            const float* in, float* out, int mode) {
+                                            const float* in, float* out, int mode, int64_t row = 0) {
   if (mode == LIN_SEQ) {
     linear<IN, OUT>(W, b, in, out);
     return;
   }
 #pragma unroll
-  for (int j = 0; j < OUT; ++j) out[j] = neuron_mode<IN, OUT>(W, b, in, j, mode);
+  for (int j = 0; j < OUT; ++j) out[j] = neuron_mode<IN, OUT>(W, b, in, j, mode, row);
 }
 
-// per-layer mode for a call on n rows (hidden layers: OUT = H, last: OUT = 2)
-__device__ __forceinline__ int lin_mode(int64_t n, bool last) {
+// the schedule of an n-row call of an IN -> OUT layer
+template <int IN, int OUT>
+__host__ __device__ __forceinline__ int lin_mode(int64_t n) {
   if (n == 1) return LIN_ONE;
-  if (last && n <= 15) return LIN_FOLD;
+  if (n >= 16) return LIN_SEQ;
+  if (OUT == 2 || (OUT == 8 && IN <= 8 && n <= 7)) return LIN_FOLD;
   return LIN_SEQ;
 }
 
@@ -323,5 +366,10 @@ struct NetShape {
   static constexpr int IN = 2 * LV;
   static constexpr int NW = H * IN + H + (NL - 2) * (H * H + H) + 2 * H + 2;
 };
+
+// the net shapes with kernels: levels 2..8 (one translation unit each,
+// net_lv.hip), (hidden, layers) below -- K = (layers - 1) hidden + 1 <= 63
+// planes fit the 64-bit sign keys
+#define TNP_NET_SHAPES(X) X(8, 2) X(8, 3) X(8, 4) X(16, 2) X(16, 3) X(16, 4) X(32, 2)
 
 }  // namespace tnpnet

@@ -1,0 +1,368 @@
+// The net kernels of ONE level count (compiled once per level count,
+// -DTNP_LV=2..8, so the shape instantiations build in parallel): the fused
+// hash-grid encoding + ReLU MLP forward, the forward of a step's new
+// vertices with its epilogue, the SDF with its input gradient, the raw
+// encoding and the skeleton's tile evaluation, for every (hidden, layers)
+// shape of TNP_NET_SHAPES.
+//
+// Reference semantics:
+//   Net.forward(x, gather=True)   tropical/stanford/model.py:52-76 (any
+//                                 num_layers / num_hidden, model.py:19-50)
+//   TropicalHashGrid.forward      tropical/tropical.py:46-47 -> tcnn Grid/Hash
+//   Net.sdf / Net.normal          model.py:84-88, 105-123
+//   skeleton max_grad             tropical.py:188-197
+//
+// Bitwise contract with the PyTorch-CPU path: net.hip header; every Linear
+// layer follows the MKL schedule of its shape and row count (net_device.h
+// lin_mode / linear_mode).  Compiled with -ffp-contract=off.
+#include "common.h"
+#include "kernels.h"
+#include "net_device.h"
+#include "step.h"
+
+#ifndef TNP_LV
+#error "net_lv.hip is compiled once per level count: -DTNP_LV=<2..8>"
+#endif
+
+using namespace tnpnet;
+
+namespace {
+
+constexpr int LVC = TNP_LV;
+
+// GROUPED: rows come in groups of 8 consecutive lanes (box corners); a
+// hidden unit is active for the whole group iff corner 0 or corner 7 has a
+// pre-activation > eps (model.py:67-70), else ReLU.
+template <int LV, int H, int NL, bool GROUPED>
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_forward(NetDev net, const float* __restrict__ xyz, int64_t n, float* __restrict__ pre,
+          int64_t ld, float* __restrict__ out2, uint64_t* __restrict__ kpos, uint64_t* __restrict__ kzero,
+          uint64_t* __restrict__ kgrid, ulonglong2* __restrict__ kpz) {
+  constexpr int IN = 2 * LV;
+  constexpr int NW = NetShape<LV, H, NL>::NW;
+  __shared__ float w[NW];
+  __shared__ float mk[GROUPED ? 1 : TNP_MAX_MARKS];  // the marks for the grid words (keys)
+  for (int i = threadIdx.x; i < NW; i += blockDim.x) w[i] = net.weights[i];
+  if (!GROUPED && kpos)
+    for (int i = threadIdx.x; i < net.n_marks; i += blockDim.x) mk[i] = net.marks[i];
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = i < n;
+  float x[3] = {0.f, 0.f, 0.f};
+  if (live) load_point(xyz, i, x);
+  float h[H > IN ? H : IN];
+  float a[H];
+  encode<LV>(net, x, h);
+  const float* W = w;
+  int p = 0;
+  const int m0 = lin_mode<IN, H>(n), mh = lin_mode<H, H>(n), mo = lin_mode<H, 2>(n);
+  uint64_t ps = 0, zs = 0;  // packed eps-sign keys (k_keys), when kpos is given
+#pragma unroll
+  for (int layer = 0; layer < NL - 1; ++layer) {
+    if (layer == 0) {
+      linear_mode<IN, H>(W, W + H * IN, h, a, m0, i);
+      W += H * IN + H;
+    } else {
+      linear_mode<H, H>(W, W + H * H, h, a, mh, i);
+      W += H * H + H;
+    }
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+      ps |= (uint64_t)(a[j] > net.eps) << (p + j);
+      zs |= (uint64_t)(fabsf(a[j]) <= net.eps) << (p + j);
+      if (live && pre) pre[(int64_t)(p + j) * ld + i] = a[j];
+      if (GROUPED) {
+        const int base = (threadIdx.x & 63) & ~7;
+        float a_first = __shfl(a[j], base, 64);
+        float a_last = __shfl(a[j], base + 7, 64);
+        bool on = (a_first > net.eps) || (a_last > net.eps);
+        h[j] = __fmul_rn(a[j], on ? 1.0f : 0.0f);
+      } else {
+        h[j] = fmaxf(a[j], 0.0f);
+      }
+    }
+    p += H;
+  }
+  float o[2];
+  linear_mode<H, 2>(W, W + 2 * H, h, o, mo, i);
+  const float v = __fsub_rn(o[1], o[0]);
+  if (live && pre) pre[(int64_t)p * ld + i] = v;
+  if (live && out2) {
+    out2[2 * i] = o[0];
+    out2[2 * i + 1] = o[1];
+  }
+  if (!GROUPED && live && kpos) {  // the keys of k_keys, from the values in registers
+    ps |= (uint64_t)(v > net.eps) << p;
+    zs |= (uint64_t)(fabsf(v) <= net.eps) << p;
+    kpos[i] = ps;
+    kzero[i] = zs;
+    kpz[i] = make_ulonglong2(ps, zs);
+    kgrid[i] = grid_word(mk, net.n_marks, net.eps, x);
+  }
+}
+
+// Forward of the S new vertices of a flat step with the step's epilogue
+// fused (replaces forward -> fail_check -> keys -> finalize_new): the
+// pre-activations of planes >= keep_from go straight into the cache
+// (plane-major, slot V + r), the packed pos/zero/grid keys are written as if
+// no override applies, and the failover predicate of subpoly_debug.py:35-49
+// (a new vertex off one of its shared planes by more than eps) is ORed into
+// ctr[CTR_FAIL]; shared[r] keeps the plane set for k_override_new.  Values
+// and the MKL row-count schedule are those of k_forward (same n = S).
+template <int LV, int H, int NL>
+__global__ void __launch_bounds__(TNP_BLOCK, 4)
+k_forward_new(NetDev net, const float* xyz, int64_t n, float* __restrict__ pre,
+              int64_t ld, int64_t V, int keep_from, const int32_t* __restrict__ sa,
+              const int32_t* __restrict__ sb, int idx, int own_lo, int own_hi, uint64_t* pos,
+              uint64_t* zero, uint64_t* __restrict__ grid, uint64_t* __restrict__ shared,
+              int64_t* __restrict__ ctr, ulonglong2* __restrict__ pz, const float* __restrict__ scol) {
+  constexpr int IN = 2 * LV;
+  constexpr int NW = NetShape<LV, H, NL>::NW;
+  __shared__ float w[NW];
+  __shared__ float mk[TNP_MAX_MARKS];
+  for (int i = threadIdx.x; i < NW; i += blockDim.x) w[i] = net.weights[i];
+  for (int i = threadIdx.x; i < net.n_marks; i += blockDim.x) mk[i] = net.marks[i];
+  __syncthreads();
+  // XCD-contiguous chunks of the (edge-ordered, spatially coherent) splits:
+  // the hash-table lines one XCD's splits touch then mostly fit its L2
+  const int64_t i = tnp::xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+  const bool live = i < n;
+  const float eps = net.eps;
+  float x[3] = {0.f, 0.f, 0.f};
+  uint64_t m = 0;
+  if (live) {
+    const int a = sa[i], b = sb[i];
+    // every gather the endpoints need, issued before the first store (the
+    // coordinate store could alias zero[] for the compiler)
+    const uint64_t za = zero[a], zb = zero[b];
+    if (scol) {
+      // the split point itself (k_new_vertices, subpoly.py:113-117, 180), fused:
+      // d = d/eps; w = |d0| / |d1 - d0|; v = e0*(1-w) + e1*w
+      const float* base = xyz - 3 * V;  // xyz points at slot V
+      const float c0 = scol[a], c1 = scol[b];
+      float ea[3], eb[3];
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        ea[d] = base[3 * (int64_t)a + d];
+        eb[d] = base[3 * (int64_t)b + d];
+      }
+      const float d0 = __fdiv_rn(c0, eps), d1 = __fdiv_rn(c1, eps);
+      const float w = __fdiv_rn(fabsf(d0), fabsf(__fsub_rn(d1, d0)));
+      const float om = __fsub_rn(1.0f, w);
+      float* out = const_cast<float*>(xyz) + 3 * i;
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        const float v = __fadd_rn(__fmul_rn(ea[d], om), __fmul_rn(eb[d], w));
+        out[d] = v;
+        x[d] = __fmul_rn(__fadd_rn(v, 1.0f), 0.5f);  // Net.preprocess, as load_point (x/2 == x*0.5 exactly)
+      }
+    } else {
+      load_point(xyz, i, x);
+    }
+    const uint64_t below = (idx >= 64) ? ~0ull : ((1ull << idx) - 1ull);
+    m = (za & zb & below) | (1ull << idx);
+  }
+  float h[H > IN ? H : IN];
+  float a[H];
+  encode<LV>(net, x, h);
+  const float* W = w;
+  int p = 0;
+  uint64_t ps = 0, zs = 0;
+  bool bad = false;
+  const int m0 = lin_mode<IN, H>(n), mh = lin_mode<H, H>(n), mo = lin_mode<H, 2>(n);
+  float* col = pre + V + i;
+#pragma unroll
+  for (int layer = 0; layer < NL - 1; ++layer) {
+    if (layer == 0) {
+      linear_mode<IN, H>(W, W + H * IN, h, a, m0, i);
+      W += H * IN + H;
+    } else {
+      linear_mode<H, H>(W, W + H * H, h, a, mh, i);
+      W += H * H + H;
+    }
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+      const float v = a[j];
+      if (live && p + j >= keep_from) col[(int64_t)(p + j) * ld] = v;
+      ps |= (uint64_t)(v > eps) << (p + j);
+      zs |= (uint64_t)(fabsf(v) <= eps) << (p + j);
+      bad |= ((m >> (p + j)) & 1) && fabsf(v) > eps;
+      h[j] = fmaxf(v, 0.0f);
+    }
+    p += H;
+  }
+  float o[2];
+  linear_mode<H, 2>(W, W + 2 * H, h, o, mo, i);
+  const float v = __fsub_rn(o[1], o[0]);
+  if (live) {
+    if (p >= keep_from) col[(int64_t)p * ld] = v;
+    ps |= (uint64_t)(v > eps) << p;
+    zs |= (uint64_t)(fabsf(v) <= eps) << p;
+    bad |= ((m >> p) & 1) && fabsf(v) > eps;
+    pos[V + i] = ps;
+    zero[V + i] = zs;
+    pz[V + i] = make_ulonglong2(ps, zs);
+    shared[i] = m;
+  }
+  // full lower_bound over the marks in LDS: cheaper than gathering the
+  // endpoints' grid words to narrow it (measured at 128^3: 1.02 -> 0.90 ms
+  // per pass for this kernel)
+  const uint64_t g = grid_word(mk, net.n_marks, eps, x);
+  if (live) grid[V + i] = g;
+  if (__ballot(live && bad) && tnp::lane() == 0) tnp::or_sticky(&ctr[CTR_FAIL], 1ull);
+  if (own_lo <= own_hi) {
+    // x-slab ownership of the new vertex: on mark plane p -> owned iff
+    // own_lo < p <= own_hi (plane 0 by the first shard); in the cell above
+    // mark c -> owned iff own_lo <= c < own_hi
+    const int c = tnp::grid_off(g, 0);
+    const bool owned = tnp::grid_zero(g, 0) ? ((c > own_lo || (own_lo == 0 && c == 0)) && c <= own_hi)
+                                            : (c >= own_lo && c < own_hi);
+    const uint64_t halo = __ballot(live && !owned);
+    if (halo && tnp::lane() == 0)
+      atomicAdd((unsigned long long*)&ctr[CTR_DUP], (unsigned long long)__popcll(halo));
+  }
+}
+
+// TropicalHashGrid.forward: raw encoding of x already in [0,1]^3 -> [n][2L]
+template <int LV>
+__global__ void k_encode(NetDev net, const float* __restrict__ x01, int64_t n, float* __restrict__ out) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float x[3] = {x01[3 * i], x01[3 * i + 1], x01[3 * i + 2]};
+  float f[2 * LV];
+  encode<LV>(net, x, f);
+#pragma unroll
+  for (int k = 0; k < 2 * LV; ++k) out[i * 2 * LV + k] = f[k];
+}
+
+// SDF = tanh(o1 - o0) and its input gradient (Net.sdf / Net.normal).
+template <int LV, int H, int NL>
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_sdf_grad(NetDev net, const float* __restrict__ xyz, int64_t n, float* __restrict__ sdf,
+           float* __restrict__ grad) {
+  constexpr int NW = NetShape<LV, H, NL>::NW;
+  __shared__ float w[NW];
+  for (int i = threadIdx.x; i < NW; i += blockDim.x) w[i] = net.weights[i];
+  __syncthreads();
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float x[3];
+  load_point(xyz, i, x);
+  float g[3];
+  float y = sdf_grad<LV, H, NL>(net, w, x, grad ? g : nullptr);
+  sdf[i] = y;
+  if (grad)
+    for (int d = 0; d < 3; ++d) grad[3 * i + d] = g[d];
+}
+
+// skeleton tile (tropical.py:186-197): |sdf| at every tile lattice point +
+// the tile's max |grad sdf| (skeleton.hip has the rest)
+template <int LV, int H, int NL>
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_skel_eval(NetDev net, int i0, int j0, int k0, int n0, int n1, int n2,
+            float* __restrict__ dist, unsigned int* __restrict__ gmax_bits) {
+  constexpr int NW = NetShape<LV, H, NL>::NW;
+  __shared__ float w[NW];
+  for (int i = threadIdx.x; i < NW; i += blockDim.x) w[i] = net.weights[i];
+  __syncthreads();
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t n = (int64_t)n0 * n1 * n2;
+  float gn = 0.f;
+  if (t < n) {
+    int k = (int)(t % n2), j = (int)((t / n2) % n1), i = (int)(t / ((int64_t)n1 * n2));
+    int ix[3] = {i0 + i, j0 + j, k0 + k};
+    float x[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      // vertex = marks*2-1 (preprocess_inverse), then preprocess (x+1)/2
+      float v = __fsub_rn(__fmul_rn(net.marks[ix[d]], 2.0f), 1.0f);
+      x[d] = __fmul_rn(__fadd_rn(v, 1.0f), 0.5f);  // x/2 == x*0.5 exactly
+    }
+    float g[3];
+    float y = sdf_grad<LV, H, NL>(net, w, x, g);
+    dist[t] = fabsf(y);
+    gn = sqrtf(g[0] * g[0] + g[1] * g[1] + g[2] * g[2]);
+  }
+  // non-negative floats order like their bit patterns
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) gn = fmaxf(gn, __shfl_xor(gn, o, 64));
+  if (tnp::lane() == 0) atomicMax(gmax_bits, __float_as_uint(gn));
+}
+
+}  // namespace
+
+// (hidden, layers) dispatch inside one level count
+#define TNP_SHAPE_CASE(H_, NL_)                              \
+  case H_ * 16 + NL_: {                                      \
+    constexpr int H = H_, NL = NL_;                          \
+    TNP_SHAPE_BODY;                                          \
+    break;                                                   \
+  }
+#define TNP_SHAPE_SWITCH(net)                                                                       \
+  switch ((net).num_hidden * 16 + (net).num_layers) {                                              \
+    TNP_NET_SHAPES(TNP_SHAPE_CASE)                                                                   \
+    default:                                                                                         \
+      tnp_set_error("net shape (hidden=%d, layers=%d) not instantiated", (net).num_hidden, (net).num_layers); \
+      return -1;                                                                                     \
+  }
+
+template <>
+int lv_forward<LVC>(const NetDev& net, const float* xyz, int64_t n, float* pre, int64_t ld, int group,
+                    hipStream_t s, float* out2, uint64_t* pos, uint64_t* zero, uint64_t* grid, uint64_t* pz) {
+#define TNP_SHAPE_BODY                                                                                          \
+  if (group == 8)                                                                                               \
+    hipLaunchKernelGGL((k_forward<LVC, H, NL, true>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net, xyz, n, pre, \
+                       ld, out2, nullptr, nullptr, nullptr, nullptr);                                           \
+  else                                                                                                          \
+    hipLaunchKernelGGL((k_forward<LVC, H, NL, false>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net, xyz, n,    \
+                       pre, ld, out2, pos, zero, grid, reinterpret_cast<ulonglong2*>(pz));
+  TNP_SHAPE_SWITCH(net)
+#undef TNP_SHAPE_BODY
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+
+template <>
+int lv_forward_new<LVC>(const NetDev& net, const float* xyz, int64_t n, float* pre, int64_t ld, int64_t V,
+                        int keep_from, const int32_t* sa, const int32_t* sb, int idx, int own_lo, int own_hi,
+                        uint64_t* pos, uint64_t* zero, uint64_t* grid, uint64_t* shared, int64_t* ctr, uint64_t* pz,
+                        const float* col, hipStream_t s) {
+#define TNP_SHAPE_BODY                                                                                   \
+  hipLaunchKernelGGL((k_forward_new<LVC, H, NL>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net, xyz, n, pre, \
+                     ld, V, keep_from, sa, sb, idx, own_lo, own_hi, pos, zero, grid, shared, ctr,            \
+                     reinterpret_cast<ulonglong2*>(pz), col);
+  TNP_SHAPE_SWITCH(net)
+#undef TNP_SHAPE_BODY
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+
+template <>
+int lv_sdf_grad<LVC>(const NetDev& net, const float* xyz, int64_t n, float* sdf, float* grad, hipStream_t s) {
+#define TNP_SHAPE_BODY \
+  hipLaunchKernelGGL((k_sdf_grad<LVC, H, NL>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net, xyz, n, sdf, grad);
+  TNP_SHAPE_SWITCH(net)
+#undef TNP_SHAPE_BODY
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+
+template <>
+int lv_skel_eval<LVC>(const NetDev& net, int i0, int j0, int k0, int n0, int n1, int n2, float* dist,
+                      unsigned int* gmax_bits, hipStream_t s) {
+  const int64_t n = (int64_t)n0 * n1 * n2;
+#define TNP_SHAPE_BODY                                                                                         \
+  hipLaunchKernelGGL((k_skel_eval<LVC, H, NL>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net, i0, j0, k0, n0, \
+                     n1, n2, dist, gmax_bits);
+  TNP_SHAPE_SWITCH(net)
+#undef TNP_SHAPE_BODY
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+
+template <>
+int lv_encode<LVC>(const NetDev& net, const float* x01, int64_t n, float* out, hipStream_t s) {
+  hipLaunchKernelGGL((k_encode<LVC>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net, x01, n, out);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}

@@ -26,37 +26,7 @@ namespace {
 constexpr int IPT = 8;
 constexpr int TILE = TNP_BLOCK * IPT;
 
-template <int LV, int H>
-__global__ void __launch_bounds__(TNP_BLOCK)
-k_skel_eval(NetDev net, int i0, int j0, int k0, int n0, int n1, int n2,
-            float* __restrict__ dist, unsigned int* __restrict__ gmax_bits) {
-  constexpr int NW = NetShape<LV, H, 3>::NW;
-  __shared__ float w[NW];
-  for (int i = threadIdx.x; i < NW; i += blockDim.x) w[i] = net.weights[i];
-  __syncthreads();
-  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  int64_t n = (int64_t)n0 * n1 * n2;
-  float gn = 0.f;
-  if (t < n) {
-    int k = (int)(t % n2), j = (int)((t / n2) % n1), i = (int)(t / ((int64_t)n1 * n2));
-    int ix[3] = {i0 + i, j0 + j, k0 + k};
-    float x[3];
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-      // vertex = marks*2-1 (preprocess_inverse), then preprocess (x+1)/2
-      float v = __fsub_rn(__fmul_rn(net.marks[ix[d]], 2.0f), 1.0f);
-      x[d] = __fmul_rn(__fadd_rn(v, 1.0f), 0.5f);  // x/2 == x*0.5 exactly
-    }
-    float g[3];
-    float y = sdf_grad<LV, H>(net, w, x, g);
-    dist[t] = fabsf(y);
-    gn = sqrtf(g[0] * g[0] + g[1] * g[1] + g[2] * g[2]);
-  }
-  // non-negative floats order like their bit patterns
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) gn = fmaxf(gn, __shfl_xor(gn, o, 64));
-  if (tnp::lane() == 0) atomicMax(gmax_bits, __float_as_uint(gn));
-}
+// k_skel_eval (|sdf| + the tile max |grad sdf|) lives in net_lv.hip
 
 struct TileGeom {
   int i0, j0, k0, n0, n1, n2, L;
@@ -189,13 +159,7 @@ int launch_skel_eval(const NetDev& net, int i0, int j0, int k0, int n0, int n1, 
   int64_t n = (int64_t)n0 * n1 * n2;
   if (n <= 0) return 0;
   if (!net_supported(net)) { tnp_set_error("unsupported net shape"); return -1; }
-  if (net.n_levels == 4)
-    hipLaunchKernelGGL((k_skel_eval<4, 16>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net, i0, j0,
-                       k0, n0, n1, n2, dist, gmax_bits);
-  else
-    hipLaunchKernelGGL((k_skel_eval<2, 16>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net, i0, j0,
-                       k0, n0, n1, n2, dist, gmax_bits);
-  TNP_CHECK(hipGetLastError());
+  TNP_LV_SWITCH(net.n_levels, return lv_skel_eval<L_>(net, i0, j0, k0, n0, n1, n2, dist, gmax_bits, s));
   return 0;
 }
 

@@ -455,7 +455,11 @@ __global__ void k_fill_u32(uint32_t* __restrict__ p, int64_t n, uint32_t v) {
 
 int launch_train_grad(const NetDev& net, const float* xyz, const float* gt, int64_t n, float clamp_t, float eik_w,
                       int64_t eik_batch, float* g_table, float* g_w, double* stats, hipStream_t s) {
-  if (!net_supported(net) || net.tied) { tnp_set_error("train: unsupported net shape"); return -1; }
+  if (!net_supported(net) || net.tied || net.num_hidden != 16 || net.num_layers != 3) {
+    tnp_set_error("train: the closed-form gradient is written for 3-layer, 16-hidden nets (this net: %d layers, "
+                  "%d hidden, %d levels)", net.num_layers, net.num_hidden, net.n_levels);
+    return -1;
+  }
   TNP_CHECK(hipMemsetAsync(stats, 0, 2 * sizeof(double), s));
   if (n <= 0) return 0;
   TNP_TRAIN_DISPATCH(net.n_levels, {
