@@ -103,6 +103,7 @@ struct VSet {
   Buf xyz, pre, pos, zero, grid;
   Buf pz;  // (pos, zero) interleaved, 16 B per vertex: one gather for both
   int64_t cap = 0;  // rows; pre leading dimension == cap
+  int K = 0;        // planes the pre buffer holds (the engine is reused across nets)
 };
 
 struct KRec {
@@ -302,11 +303,13 @@ static int scan_counts(tnp_engine* e, const int32_t* in, int64_t* out, int64_t n
 
 // grow a vertex set to `rows` keeping [0, keep_rows)
 static int vset_ensure(tnp_engine* e, VSet& v, int64_t rows, int64_t keep_rows, hipStream_t s) {
-  if (rows <= v.cap) return 0;
+  if (rows <= v.cap && v.K == e->K) return 0;
+  if (v.K != e->K) keep_rows = 0;  // another net: nothing of the old set is kept
   int64_t nc = std::max<int64_t>(rows, v.cap + v.cap / 2);
   nc = (nc + 255) / 256 * 256;
   VSet n;
   n.cap = nc;
+  n.K = e->K;
   if (buf_ensure(n.xyz, nc * 3 * sizeof(float), s)) return -1;
   if (buf_ensure(n.pre, (size_t)nc * e->K * sizeof(float), s)) return -1;
   if (buf_ensure(n.pos, nc * sizeof(uint64_t), s)) return -1;
@@ -535,7 +538,14 @@ extern "C" int tnp_engine_set_net(tnp_engine* e, const tnp_net* n) {
     e->net.table = P<float>(e->tied_table);
     e->net.tied = 1;
   }
-  e->K = net_K(e->net);
+  const int K = net_K(e->net);
+  if (e->has_net && K != e->K) {
+    // the resident complex's cache has the old net's planes (vset_ensure
+    // reallocates the vertex sets for the new K): load a complex again
+    e->valid = false;
+    e->pend_idx = -1;
+  }
+  e->K = K;
   e->has_net = true;
   return 0;
 }
