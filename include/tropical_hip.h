@@ -192,6 +192,12 @@ int tnp_engine_faces_export(tnp_engine* eng, int64_t* d_tri, float* d_faces,
  * Single-device only (the descent's stop criterion is global). */
 int tnp_engine_set_curve(tnp_engine* eng, int on);
 
+/* Curve path: subpoly_(..., strict=...) (subpoly.py:198-203).  1 (default):
+ * debug.strict_check drops splits that miss their planes
+ * (subpoly_debug.py:234-271); 0: every split stays (the reference then only
+ * prints a diagnostic). */
+int tnp_engine_set_strict(tnp_engine* eng, int on);
+
 /* Multi-GPU x-slabs, each extracted with a halo of cells on either side
  * (tropical/distributed.py; the halo width is the caller's, checked by
  * halo_check): this shard OWNS the mark planes

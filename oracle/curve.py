@@ -141,7 +141,7 @@ def descend(net, ends, x, plane, idx, eps, iters=500, step=1e-2):
     return x.detach(), d0.detach(), d1.detach(), i
 
 
-def curve_vertices(V, E, split, cache, rgn, net, idx, eps, stats=None):
+def curve_vertices(V, E, split, cache, rgn, net, idx, eps, stats=None, off=None):
     """subpoly.py:120-177, 204-207: new vertices of the split edges with the
     trilinear correction on non-axis-aligned edges.  Returns
     (v_new S x 3, c mask S, ints B x 3, d_new B x 2)."""
@@ -156,6 +156,16 @@ def curve_vertices(V, E, split, cache, rgn, net, idx, eps, stats=None):
     corners = corner_points(ends[c]).view(-1, 3)
     dc = torch.cat(net(corners, gather=True, group=8)[1], dim=-1)
     dc = dc.view(-1, 8, dc.shape[-1])
+    if off is not None:
+        # check_new_vertices_on_two_planes (subpoly.py:134-135,
+        # subpoly_debug.py:96-104): fewer than two shared zero columns -> the
+        # reference's diagnostic print raises (Tensor has no .astype)
+        ar, ao = rgn[E][split][c], off[E][split][c]
+        chk = (ar[:, 0] == 0) & (ar[:, 1] == 0)
+        chk[:, :3] &= ao[:, 0] == ao[:, 1]
+        if bool((chk.sum(-1) < 2).any()):
+            raise AttributeError(f"curve path, plane {idx}: a split edge's endpoints share fewer than two "
+                                 "zero columns (reference subpoly_debug.py:96-104 fails on Tensor.astype)")
     er = rgn[E][split][c][:, :, 3:]
     both_zero = (er[:, 0] == 0) & (er[:, 1] == 0)
     plane = last_nonzero(both_zero[:, :idx])

@@ -113,6 +113,10 @@ CASES = {
     "lv8_rand": ("subpoly", dict(SMALL, levels=8, r_max=48, T=15), ("rand", 29, 0.05), None),
     "synth24_l4h8": ("lattice", None, ("rand", 31, 0.1), (24, 19, dict(num_layers=4, num_hidden=8))),
     "synth20_h32": ("lattice", None, ("rand", 37, 0.1), (20, 19, dict(num_layers=2, num_hidden=32))),
+    # the curve branch with strict=False (subpoly_(..., strict=False),
+    # subpoly.py:198-203): every split stays, no strict_check -- driven step
+    # by step through subpoly_ from the skeleton (subpoly() never passes it)
+    "small_torus_curve_loose": ("curve_loose", SMALL, ("same", "small_torus"), None),
 }
 # table params above this many floats are stored as the generator spec
 # (tropical/synthetic.py random_params) instead of the values
@@ -187,7 +191,7 @@ def run_case(name):
         return v, e, o
 
     sp.subpoly_ = wrapped
-    force = kind != "curve"
+    force = kind not in ("curve", "curve_loose")
     if not force:
         sp.check_new_vertices_on_surface = _surface_check
         out["patched"] = np.array("check_new_vertices_on_surface -> diagnostic print")
@@ -222,8 +226,8 @@ def run_case(name):
                 if isinstance(m, sys.modules["tropical"].TropicalHashGrid):
                     V0, E0 = m.skeleton(net)
                     break
-            out["skel_V"] = V0.numpy()
-            out["skel_E"] = E0.numpy()
+            out["skel_V"] = V0.numpy().copy()
+            out["skel_E"] = E0.numpy().copy()  # (subpoly_ rewrites its edges argument in place)
             # duplicate edges from the 127-stride tile overlap (tropical.py:176-181)
             out["skel_dups"] = np.int64(E0.shape[0] - np.unique(E0.numpy(), axis=0).shape[0])
             if not force:
@@ -235,10 +239,29 @@ def run_case(name):
                     return orig_ex(vertices, edges, net_, eps, outputs)
 
                 sp.extract_skeleton = grab
-            faces, Vs, fwi = sp.subpoly(net, 3, 1.2, 1e-4, force=force)
+            if kind == "curve_loose":
+                # subpoly.py:58-86 with strict=False in every subpoly_ call;
+                # the reference may fail part-way (its diagnostics): record where
+                V, E, o = V0.clone(), E0.clone(), None
+                try:
+                    for l in range(net.num_layers - 1):
+                        for h in range(net.num_hidden):
+                            cur = l * net.num_hidden + h
+                            V, E, o = sp.subpoly_(V, E, net, l, h, 1e-4, o, force=False, strict=False)
+                    cur = (net.num_layers - 1) * net.num_hidden
+                    V, E, o = sp.subpoly_(V, E, net, net.num_layers - 2, net.num_hidden, 1e-4, o,
+                                          force=False, strict=False)
+                    Vs, Es, used = sp.extract_skeleton(V, E, net, 1e-4, o)
+                    faces, fwi = sp.extract_faces(Vs, Es, net, o[used], 1e-4)
+                except AttributeError as ex:
+                    out["raises_at"] = np.int64(cur)
+                    out["raises"] = np.array(f"{type(ex).__name__}: {ex}")
+                    Vs, faces, fwi = torch.zeros(0, 3), [], []
+            else:
+                faces, Vs, fwi = sp.subpoly(net, 3, 1.2, 1e-4, force=force)
             if not force:
                 sp.extract_skeleton = orig_ex
-                if last["V"].shape[0] <= 50_000:  # small enough to commit in full
+                if "V" in last and last["V"].shape[0] <= 50_000:  # small enough to commit in full
                     out["pre_V"], out["pre_E"] = last["V"], last["E"].astype(np.int32)
             out["surf_V"] = Vs.numpy()
     sp.subpoly_ = orig

@@ -527,8 +527,66 @@ __device__ __forceinline__ void group_bucket(const BGeom& G, int b, int64_t base
   }
 }
 
+// Packed windows of one bucket (one wave builds the list): greedy over the
+// bucket's cells in local-cell order, a window takes whole consecutive
+// cells while they fit in 64 records and none holds more than WCELL members
+// (those are k_connect's; they only end windows).  cnt[c] / cur[c]: member
+// count and end offset of cell c (group_bucket's LDS); the list (start |
+// end << 16, bucket-relative) overwrites cnt[0..nwin) -- a window is
+// written only after every count it could overwrite was read.  Returns the
+// window count (valid in lane 0).  n must be < 65536.
+template <int LC>
+__device__ __forceinline__ int build_windows(int* cnt, const int* cur) {
+  const int L = tnp::lane();
+  int nwin = 0;
+  int so = -1;  // start offset of the open window (-1: none)
+  for (int c0 = 0; c0 < LC; c0 += 64) {
+    const int c = c0 + L;
+    const int len = cnt[c], end = cur[c];
+    const int start = end - len;
+    const bool big = len > WCELL;
+    __builtin_amdgcn_wave_barrier();
+    int lo = 0;  // first lane of this chunk not yet placed in a window
+    while (lo < 64) {
+      const uint64_t rest = ~0ull << lo;
+      if (so < 0) {
+        // open a window at the first non-empty small cell from lane lo
+        const uint64_t cand = __ballot(len > 0 && !big) & rest;
+        if (!cand) break;
+        const int f = __builtin_ctzll(cand);
+        so = __shfl(start, f, 64);
+        lo = f;
+        continue;
+      }
+      // the window [so, ...) closes before the first cell that does not fit
+      // or is big
+      const uint64_t stop = __ballot((len > 0) && (big || end > so + 64)) & rest;
+      if (!stop) break;  // every remaining cell of the chunk fits: carry on
+      const int f = __builtin_ctzll(stop);
+      const int eo = __shfl(start, f, 64);  // the window ends where cell f starts
+      if (eo > so) {
+        if (L == 0) cnt[nwin] = so | (eo << 16);
+        ++nwin;
+      }
+      so = -1;
+      lo = __shfl(big ? 1 : 0, f, 64) ? f + 1 : f;  // a big cell is skipped
+    }
+  }
+  if (so >= 0) {
+    const int eo = cur[LC - 1];
+    if (eo > so) {
+      if (L == 0) cnt[nwin] = so | (eo << 16);
+      ++nwin;
+    }
+  }
+  return nwin;
+}
+
 #ifndef TNP_BG_MINB
 #define TNP_BG_MINB 1
+#endif
+#ifndef TNP_PACKED_WIN  // 0: the 32-stride window pass (A/B variant)
+#define TNP_PACKED_WIN 1
 #endif
 template <int SH>
 __global__ void __launch_bounds__(TNP_BLOCK, TNP_BG_MINB)
@@ -544,6 +602,7 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
   __shared__ int64_t lds[TNP_WAVES];
   __shared__ int64_t lds3[3 * TNP_WAVES];
   __shared__ int last;
+  __shared__ int nwin_s;
   __shared__ WinLds W;
   const int b = blockIdx.x;
   const int64_t base = bbase[b];
@@ -575,8 +634,19 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
       __syncthreads();
       WinAcc a;
       const uint64_t below = (wa.idx >= 64) ? ~0ull : ((1ull << wa.idx) - 1ull);
-      window_pass(ents, base, base + n, tnp::wave(), TNP_WAVES, below, wa.nb, wa.fmask, wa.keys, wa.cap, wa.xs,
-                  ctr, W, a);
+      if (TNP_PACKED_WIN && n < 65536) {
+        // packed windows of whole cells (wave 0 builds the list in cnt[])
+        if (tnp::wave() == 0) {
+          const int nw = build_windows<LC>(cnt, cur);
+          if (tnp::lane() == 0) nwin_s = nw;
+        }
+        __syncthreads();
+        window_pass_packed(ents, base, reinterpret_cast<const uint32_t*>(cnt), nwin_s, tnp::wave(), TNP_WAVES,
+                           below, wa.nb, wa.fmask, wa.keys, wa.cap, wa.xs, ctr, W, a);
+      } else {
+        window_pass(ents, base, base + n, tnp::wave(), TNP_WAVES, below, wa.nb, wa.fmask, wa.keys, wa.cap,
+                    wa.xs, ctr, W, a);
+      }
       window_flush(wa.keys, wa.cap, wa.xs, ctr, W, a);
       add_pair_stats(a.n_compat, a.n_reg, a.n_conn, lds, wa.xs, ctr);
     }

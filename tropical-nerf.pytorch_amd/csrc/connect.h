@@ -119,6 +119,12 @@ __device__ __forceinline__ void window_flush(uint64_t* __restrict__ keys, int64_
   a.kn = 0;
 }
 
+// the pair tests of one staged window (W.st[wave][0..63]): lane L initiates
+// `rounds` tests, against the next `rounds` records of its cell
+__device__ __forceinline__ void window_tests(int rounds, uint64_t below, int nb, uint64_t fmask,
+                                             uint64_t* __restrict__ keys, int64_t cap, int64_t* __restrict__ xs,
+                                             int64_t* __restrict__ ctr, WinLds& W, WinAcc& a);
+
 // windows w = w0, w0 + dw, ... of the records [lo, hi); one wave each
 __device__ __forceinline__ void window_pass(const CellEnt* __restrict__ ent, int64_t lo, int64_t hi,
                                             int64_t w0, int64_t dw, uint64_t below, int nb, uint64_t fmask,
@@ -147,7 +153,50 @@ __device__ __forceinline__ void window_pass(const CellEnt* __restrict__ ent, int
     const uint64_t bm = __ballot(L == 63 || nxt != r.tag);
     const int last = L + __builtin_ctzll(bm >> L);
     const bool init = valid && L < WSTRIDE && !(r.tag & 0x80000000u);
-    const int rounds = init ? last - L : 0;
+    window_tests(init ? last - L : 0, below, nb, fmask, keys, cap, xs, ctr, W, a);
+  }
+}
+
+// Packed windows (the bucket path): window k holds the WHOLE cells
+// [s_k, e_k) (at most 64 records, cells of <= WCELL members, chosen by the
+// grouping kernel), so every record is staged once and every record
+// initiates -- half the windows of the 32-stride pass above.
+__device__ __forceinline__ void window_pass_packed(const CellEnt* __restrict__ ent, int64_t base,
+                                                   const uint32_t* __restrict__ wl, int nwin, int w0, int dw,
+                                                   uint64_t below, int nb, uint64_t fmask,
+                                                   uint64_t* __restrict__ keys, int64_t cap,
+                                                   int64_t* __restrict__ xs, int64_t* __restrict__ ctr,
+                                                   WinLds& W, WinAcc& a) {
+  const int wv = tnp::wave(), L = tnp::lane();
+  for (int w = w0; w < nwin; w += dw) {
+    const uint32_t se = wl[w];
+    const int s = (int)(se & 0xFFFFu), n = (int)(se >> 16) - s;
+    const bool valid = L < n;
+    CellEnt r;
+    if (valid) {
+      r = ent[base + s + L];
+    } else {
+      r.p = r.z = 0;
+      r.v = 0;
+      r.f = 0;
+      r.tag = 0xFFFFFFFFu;  // no cell: matches nothing, never initiates
+      r.pad = 0;
+    }
+    W.st[wv][L] = r;
+    lds_fence();
+    const uint32_t nxt = __shfl_down(r.tag, 1, 64);
+    const uint64_t bm = __ballot(L == 63 || nxt != r.tag);
+    const int last = L + __builtin_ctzll(bm >> L);
+    const bool init = valid && !(r.tag & 0x80000000u);  // (windows hold no big cell; defensive)
+    window_tests(init ? last - L : 0, below, nb, fmask, keys, cap, xs, ctr, W, a);
+  }
+}
+
+__device__ __forceinline__ void window_tests(int rounds, uint64_t below, int nb, uint64_t fmask,
+                                             uint64_t* __restrict__ keys, int64_t cap, int64_t* __restrict__ xs,
+                                             int64_t* __restrict__ ctr, WinLds& W, WinAcc& a) {
+  const int wv = tnp::wave(), L = tnp::lane();
+  {
     // flatten the window's (initiator, partner) tests over the lanes: test t
     // belongs to the last initiator j with exc[j] <= t, partner j + 1 + t - exc[j]
     const int incl = tnp::wave_scan_incl(rounds);

@@ -59,8 +59,8 @@ __global__ void k_curve_rows(const int32_t* __restrict__ cflag, const int64_t* _
 __global__ void k_curve_corners(const int32_t* __restrict__ crow, int64_t B,
                                 const int32_t* __restrict__ sa, const int32_t* __restrict__ sb,
                                 const float* __restrict__ xyz, const uint64_t* __restrict__ zero,
-                                int idx, float* __restrict__ corners, int32_t* __restrict__ plane,
-                                int64_t* __restrict__ ctr) {
+                                const uint64_t* __restrict__ grid, int idx, float* __restrict__ corners,
+                                int32_t* __restrict__ plane, int64_t* __restrict__ ctr) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= 8 * B) return;
   int64_t b = t >> 3;
@@ -78,6 +78,16 @@ __global__ void k_curve_corners(const int32_t* __restrict__ crow, int64_t B,
     uint64_t m = zero[e[0]] & zero[e[1]] & below;
     plane[b] = m ? 63 - __builtin_clzll(m) : 0;
     if (!m) atomicOr((unsigned long long*)&ctr[CTR_NOPLANE], 1ull);
+    // check_new_vertices_on_two_planes (subpoly.py:134-135, subpoly_debug.py:
+    // 96-104): the endpoints share fewer than two zero columns (every plane,
+    // plus grid axes with both on the same mark) -> the reference's
+    // diagnostic print fails (AttributeError: Tensor.astype)
+    const uint64_t ga = grid[e[0]], gb = grid[e[1]];
+    int shared = __popcll(zero[e[0]] & zero[e[1]]);
+#pragma unroll
+    for (int d = 0; d < 3; ++d)
+      shared += tnp::grid_zero(ga, d) && tnp::grid_zero(gb, d) && tnp::grid_off(ga, d) == tnp::grid_off(gb, d);
+    if (shared < 2) atomicOr((unsigned long long*)&ctr[CTR_NOPLANE], 2ull);
   }
 }
 
@@ -1175,7 +1185,7 @@ __global__ void k_curve_apply(int64_t B, const int32_t* __restrict__ crow,
 // strict_check (subpoly_debug.py:234-271) after the override
 __global__ void k_strict_keep(int64_t S, const int32_t* __restrict__ cinfo,
                               const float* __restrict__ stage, int idx, int override_,
-                              const uint64_t* __restrict__ shared, float eps, int tight,
+                              const uint64_t* __restrict__ shared, float eps, int tight, int strict,
                               int32_t* __restrict__ keep) {
   int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= S) return;
@@ -1184,7 +1194,7 @@ __global__ void k_strict_keep(int64_t S, const int32_t* __restrict__ cinfo,
   bool k = fabsf(chk) < eps;
   int ci = cinfo[r];
   if (ci & 1) k = k && !(ci & 2) && (!tight || (ci & 4));
-  keep[r] = k;
+  keep[r] = strict ? k : 1;  // strict=False: every split stays (subpoly.py:198-202)
 }
 
 // surviving splits -> consecutive new ids in edge order; the split edge's
@@ -1230,11 +1240,11 @@ int launch_curve_rows(const int32_t* cflag, const int64_t* coff, int64_t S, int3
   return 0;
 }
 int launch_curve_corners(const int32_t* crow, int64_t B, const int32_t* sa, const int32_t* sb,
-                         const float* xyz, const uint64_t* zero, int idx, float* corners,
+                         const float* xyz, const uint64_t* zero, const uint64_t* grid, int idx, float* corners,
                          int32_t* plane, int64_t* ctr, hipStream_t s) {
   if (B <= 0) return 0;
   hipLaunchKernelGGL(k_curve_corners, dim3(tnp_grid(8 * B)), dim3(TNP_BLOCK), 0, s, crow, B, sa, sb,
-                     xyz, zero, idx, corners, plane, ctr);
+                     xyz, zero, grid, idx, corners, plane, ctr);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
@@ -1311,10 +1321,10 @@ int launch_curve_apply(int64_t B, const int32_t* crow, const int32_t* sa, const 
   return 0;
 }
 int launch_strict_keep(int64_t S, const int32_t* cinfo, const float* stage, int idx, int override_,
-                       const uint64_t* shared, float eps, int tight, int32_t* keep, hipStream_t s) {
+                       const uint64_t* shared, float eps, int tight, int strict, int32_t* keep, hipStream_t s) {
   if (S <= 0) return 0;
   hipLaunchKernelGGL(k_strict_keep, dim3(tnp_grid(S)), dim3(TNP_BLOCK), 0, s, S, cinfo, stage, idx,
-                     override_, shared, eps, tight, keep);
+                     override_, shared, eps, tight, strict, keep);
   TNP_CHECK(hipGetLastError());
   return 0;
 }

@@ -123,6 +123,7 @@ struct tnp_engine {
   int device = 0;
   int own_lo = 1, own_hi = 0;  // owned mark planes (lo, hi]; lo > hi: all
   int curve = 0;          // 1: subpoly_(force=False) semantics
+  int strict = 1;         // curve path: subpoly_(strict=...) -- 0 keeps every split (subpoly.py:198-202)
   int shards = 1;         // >1: one x-slab of a sharded complex
   int pend_tight = 0;
   int gd_iters = 500;     // subpoly_debug.py:141
@@ -690,7 +691,7 @@ static int curve_correct(tnp_engine* e, int idx, int64_t S, hipStream_t s) {
   float* d1s = P<float>(cv[CV_D1]);
   if (launch_curve_rows(P<int32_t>(cv[CV_CFLAG]), P<int64_t>(cv[CV_COFF]), S, crow, s)) return -1;
   TIMED("curve_corners", 8.0 * B * 12 + 24.0 * B,
-        launch_curve_corners(crow, B, sa, sb, xyz, P<uint64_t>(e->cur.zero), idx,
+        launch_curve_corners(crow, B, sa, sb, xyz, P<uint64_t>(e->cur.zero), P<uint64_t>(e->cur.grid), idx,
                              P<float>(cv[CV_CORNERS]), plane, ctr, s));
   TIMED("curve_forward", 8.0 * B * (12 + 4.0 * K),
         launch_forward(e->net, P<float>(cv[CV_CORNERS]), 8 * B, P<float>(cv[CV_STAGE_C]), 8 * B, 8, s));
@@ -703,6 +704,12 @@ static int curve_correct(tnp_engine* e, int idx, int64_t S, hipStream_t s) {
                         P<int32_t>(cv[CV_GG]), P<int32_t>(cv[CV_GD]), s)) return -1;
   if (scan_counts(e, P<int32_t>(cv[CV_GD]), P<int64_t>(cv[CV_GOFF]), B, CTR_G, s)) return -1;
   if (read_ctr(e, s)) return -1;
+  if (e->h_ctr[CTR_NOPLANE] & 2) {
+    tnp_set_error("curve path, plane %d: a split edge's endpoints share fewer than two zero columns (the "
+                  "reference's check_new_vertices_on_two_planes then fails: AttributeError, "
+                  "subpoly_debug.py:96-104)", idx);
+    return -1;
+  }
   if (e->h_ctr[CTR_NOPLANE]) {
     tnp_set_error("curve path: a split edge shares no plane below %d (the reference prints it and "
                   "exit()s, subpoly.py:141-148)", idx);
@@ -751,7 +758,7 @@ static int curve_filter(tnp_engine* e, int idx, int override_, hipStream_t s, in
   if (buf_ensure(cv[CV_KEEP], S * sizeof(int32_t), s)) return -1;
   if (buf_ensure(cv[CV_NID], S * sizeof(int64_t), s)) return -1;
   if (launch_strict_keep(S, P<int32_t>(cv[CV_CINFO]), P<float>(e->stage), idx, override_,
-                         P<uint64_t>(e->shared), e->net.eps, e->pend_tight, P<int32_t>(cv[CV_KEEP]), s))
+                         P<uint64_t>(e->shared), e->net.eps, e->pend_tight, e->strict, P<int32_t>(cv[CV_KEEP]), s))
     return -1;
   if (scan_counts(e, P<int32_t>(cv[CV_KEEP]), P<int64_t>(cv[CV_NID]), S, CTR_KEEP, s)) return -1;
   if (read_ctr(e, s)) return -1;
@@ -805,6 +812,11 @@ extern "C" int tnp_engine_set_shards(tnp_engine* e, int world) {
 
 extern "C" int tnp_engine_set_curve(tnp_engine* e, int on) {
   e->curve = on ? 1 : 0;
+  return 0;
+}
+
+extern "C" int tnp_engine_set_strict(tnp_engine* e, int on) {
+  e->strict = on ? 1 : 0;
   return 0;
 }
 

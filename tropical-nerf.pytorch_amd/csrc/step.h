@@ -301,7 +301,7 @@ int launch_curve_flags(const int32_t* sa, const int32_t* sb, int64_t S, const fl
 int launch_curve_rows(const int32_t* cflag, const int64_t* coff, int64_t S, int32_t* crow,
                       hipStream_t s);
 int launch_curve_corners(const int32_t* crow, int64_t B, const int32_t* sa, const int32_t* sb,
-                         const float* xyz, const uint64_t* zero, int idx, float* corners,
+                         const float* xyz, const uint64_t* zero, const uint64_t* grid, int idx, float* corners,
                          int32_t* plane, int64_t* ctr, hipStream_t s);
 int launch_curve_solve(int64_t B, const float* stage_c, int64_t ldc, const int32_t* plane, int idx,
                        const int32_t* crow, const int32_t* sa, const int32_t* sb, const float* xyz,
@@ -319,7 +319,7 @@ int launch_curve_apply(int64_t B, const int32_t* crow, const int32_t* sa, const 
                        float* xyz, int64_t V, const float* ints, const float* d0s, const int32_t* gg,
                        float eps, int32_t* cinfo, int64_t* ctr, hipStream_t s);
 int launch_strict_keep(int64_t S, const int32_t* cinfo, const float* stage, int idx, int override_,
-                       const uint64_t* shared, float eps, int tight, int32_t* keep, hipStream_t s);
+                       const uint64_t* shared, float eps, int tight, int strict, int32_t* keep, hipStream_t s);
 int launch_compact_splits(int64_t S, int K, const int32_t* keep, const int64_t* nid,
                           const int32_t* eidx, int64_t V, const int32_t* sa, const int32_t* sb,
                           const uint64_t* shared, const float* stage, const float* xyz,

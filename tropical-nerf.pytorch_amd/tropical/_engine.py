@@ -96,6 +96,12 @@ class Engine:
         self.curve = bool(on)
         return self
 
+    def set_strict(self, on: bool):
+        """Curve path: subpoly_(strict=on) (subpoly.py:198-203); False keeps
+        every split (no strict_check)."""
+        _hip.check(_hip.lib().tnp_engine_set_strict(self.h, int(on)), "tnp_engine_set_strict")
+        return self
+
     def set_shards(self, world: int):
         _hip.check(_hip.lib().tnp_engine_set_shards(self.h, int(world)), "tnp_engine_set_shards")
         return self
@@ -221,4 +227,4 @@ def engine_for(net) -> Engine:
     if eng is None:
         eng = Engine(torch.device("cuda", key))
         _ENGINES[key] = eng
-    return eng.set_net(net).set_curve(False)
+    return eng.set_net(net).set_curve(False).set_strict(True)

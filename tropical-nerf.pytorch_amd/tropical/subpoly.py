@@ -80,15 +80,14 @@ def subpoly_lattice(net, x0: int = 0, x1: int = -1, stats: list = None, faces: b
 def subpoly_(vertices, edges, net, l, h, eps, outputs_=None, pruning=True, strict=True,
              force=False):
     """One hyperplane step (subpoly.py:90-279); ``force=False`` is the curve
-    branch (strict filter on, as the reference's default ``strict=True``).
+    branch, with the strict filter when ``strict`` (the reference's default;
+    strict=False keeps every split, subpoly.py:198-203).
 
     Like the reference, a step that splits rewrites the caller's ``edges``
     in place: the second endpoint of every split edge becomes its new vertex
     (``masked_scatter_``, subpoly.py:209-212)."""
     _check_eps(net, eps)
-    if not force and not strict:
-        raise NotImplementedError("subpoly_(force=False, strict=False) is not on the extraction path")
-    eng = engine_for(net).set_curve(not force)
+    eng = engine_for(net).set_curve(not force).set_strict(strict)
     eng.load(vertices, edges, outputs_, keep_all=True)
     idx = l * net.num_hidden + h
     S, fail = eng.split(idx)
