@@ -256,6 +256,14 @@ int tnp_sdf_train_grad(const tnp_net* net, const float* d_x, const float* d_gt, 
                        float eik_w, int64_t eik_batch, float* d_grad_table, float* d_grad_weights,
                        double* d_stats, void* stream);
 
+/* Autograd through Net.sdf (model.py:84-88): the vector-Jacobian product
+ * sum_i d_gout[i] * d sdf(x_i) / d theta, ACCUMULATED into d_grad_table (the
+ * table's own layout) and d_grad_weights (the packed weight layout) -- the
+ * backward of a caller's net.sdf(x) w.r.t. the parameters (the input
+ * gradient is tnp_sdf_grad's).  Float atomics; 3-layer, 16-hidden nets. */
+int tnp_sdf_vjp(const tnp_net* net, const float* d_x, const float* d_gout, int64_t n, float* d_grad_table,
+                float* d_grad_weights, void* stream);
+
 /* Signed distance of n points d_p (n x 3) to a closed triangle mesh (d_V
  * nV x 3 fp32, d_F nF x 3 int32, indices in [0, nV)): replaces
  * cubvh.cuBVH(V, F).signed_distance (dataset.py:77, 92).  Exact distance to

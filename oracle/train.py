@@ -53,6 +53,19 @@ def encode_diff(x01: torch.Tensor, params: torch.Tensor, meta, F: int = 2) -> to
     return torch.cat(cols, 1)
 
 
+def sdf64(table, weights, meta, x):
+    """Net.sdf (model.py:84-88) in float64 with autograd through the
+    encoding (encode_diff), the MLP and tanh: the checker of the product's
+    autograd (tnp_sdf_grad / tnp_sdf_vjp)."""
+    h = encode_diff((x + 1) / 2, table, meta)
+    n = len(weights) // 2
+    for i in range(n):
+        h = torch.nn.functional.linear(h, weights[2 * i], weights[2 * i + 1])
+        if i < n - 1:
+            h = torch.relu(h)
+    return torch.tanh(h[:, 1] - h[:, 0])
+
+
 def train_loss_grads(table, weights, meta, x, gt, clamp_t=0.2, eik_w=1e-2, batch_size=None):
     """(l1, eik, grads) of one batch: the L1 and eikonal terms of
     train.py:181-197 and their gradients w.r.t. the table and the fc

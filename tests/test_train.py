@@ -211,3 +211,43 @@ def test_train_entry_point_fits_a_sphere(cuda, tmp_path, capsys):
     m = load_ply(str(tmp_path / "meshes" / "bunny" / "our_mesh_small_45.ply"))
     r = np.linalg.norm(m.vertices * R, axis=1)  # back to the normalised frame (radius 1)
     assert len(r) > 100 and abs(np.median(r) - 1.0) < 0.05 and np.percentile(np.abs(r - 1), 95) < 0.12
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [dict(levels=4, r_min=2, r_max=32, T=19), dict(levels=4, r_min=8, r_max=128, T=14)])
+def test_sdf_autograd_matches_oracle(cuda, cfg):
+    """net.sdf(x) is differentiable as the reference's (model.py:84-88,
+    autograd through tcnn there): (g * sdf).sum().backward() fills x.grad and
+    every parameter's .grad (encoding table, fc weights and biases), checked
+    against float64 autograd of the same net; double backward refuses."""
+    from oracle.train import sdf64
+    net = _small_net(**cfg).to(cuda)
+    gen = torch.Generator().manual_seed(3)
+    n = 513
+    x = ((torch.rand(n, 3, generator=gen) * 2 - 1) * 0.9)
+    g = torch.rand(n, generator=gen) * 2 - 1
+    xg = x.to(cuda).requires_grad_(True)
+    y = net.sdf(xg)
+    assert y.shape == (n, 1) and y.requires_grad
+    (y[:, 0] * g.to(cuda)).sum().backward()
+    tab = net.enc.module.params.detach().cpu().double().requires_grad_(True)
+    ws = [t.detach().cpu().double().requires_grad_(True) for lin in net.fc for t in (lin.weight, lin.bias)]
+    xd = x.double().requires_grad_(True)
+    yd = sdf64(tab, ws, net.enc.meta, xd)
+    assert torch.allclose(y[:, 0].detach().cpu().double(), yd.detach(), atol=1e-5)
+    (yd * g.double()).sum().backward()
+    got = [xg.grad, net.enc.module.params.grad] + [t.grad for lin in net.fc for t in (lin.weight, lin.bias)]
+    want = [xd.grad, tab.grad] + [t.grad for t in ws]
+    for name, a, b in zip(["x", "table", "W0", "b0", "W1", "b1", "W2", "b2"], got, want):
+        assert a is not None, name
+        err = float((a.detach().cpu().double() - b).abs().max())
+        assert err <= 2e-4 * float(b.abs().max()) + 1e-7, (name, err)
+    # x only (parameters frozen): the input gradient alone
+    for p in net.parameters():
+        p.requires_grad_(False)
+    x2 = x.to(cuda).requires_grad_(True)
+    net.sdf(x2).sum().backward()
+    assert x2.grad is not None and torch.isfinite(x2.grad).all()
+    with pytest.raises(NotImplementedError, match="double backward"):
+        x3 = x.to(cuda).requires_grad_(True)
+        torch.autograd.grad(net.sdf(x3).sum(), x3, create_graph=True)[0].sum().backward()

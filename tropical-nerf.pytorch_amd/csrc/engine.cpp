@@ -585,6 +585,13 @@ extern "C" int tnp_sdf_train_grad(const tnp_net* n, const float* xyz, const floa
                            (hipStream_t)stream);
 }
 
+extern "C" int tnp_sdf_vjp(const tnp_net* n, const float* xyz, const float* gout, int64_t N, float* d_grad_table,
+                           float* d_grad_weights, void* stream) {
+  if (check_net(n)) return -1;
+  if (N < 0 || !gout || !d_grad_table || !d_grad_weights) { tnp_set_error("sdf_vjp: bad arguments"); return -1; }
+  return launch_sdf_vjp(to_dev(n), xyz, gout, N, d_grad_table, d_grad_weights, (hipStream_t)stream);
+}
+
 extern "C" int tnp_mesh_signed_distance(const float* d_V, int64_t nV, const int32_t* d_F, int64_t nF,
                                         const float* d_p, int64_t n, float* d_work, float* d_dist, void* stream) {
   if (n < 0) { tnp_set_error("mesh_signed_distance: n < 0"); return -1; }

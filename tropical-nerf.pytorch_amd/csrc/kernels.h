@@ -109,6 +109,10 @@ int launch_region(const NetDev& net, const float* xyz, const float* pre, int64_t
 // SDF training gradients of one batch (train.py:181-201); stats: 2 doubles
 int launch_train_grad(const NetDev& net, const float* xyz, const float* gt, int64_t n, float clamp_t, float eik_w,
                       int64_t eik_batch, float* g_table, float* g_w, double* stats, hipStream_t s);
+// sum_i gout_i d sdf_i / d theta accumulated into g_table / g_w (autograd
+// through Net.sdf; 3-layer, 16-hidden nets)
+int launch_sdf_vjp(const NetDev& net, const float* xyz, const float* gout, int64_t n, float* g_table, float* g_w,
+                   hipStream_t s);
 // mesh signed distance (dataset.py:92); work: 2 n floats
 int launch_mesh_sd(const float* V, int64_t nV, const int32_t* F, int64_t nF, const float* P, int64_t n, float* work,
                    float* out, hipStream_t s);

@@ -198,7 +198,7 @@ template <int LV, int H>
 __global__ void __launch_bounds__(TNP_BLOCK)
 k_train_grads(NetDev net, const float* __restrict__ xyz, const float* __restrict__ gt, int64_t n, float T,
               float eik_w, int64_t eik_batch, const double* __restrict__ stats, float* __restrict__ g_table,
-              float* __restrict__ g_w) {
+              float* __restrict__ g_w, const float* __restrict__ gout) {
   constexpr int IN = 2 * LV;
   constexpr int NW = NetShape<LV, H, 3>::NW;
   __shared__ float w[NW];
@@ -216,7 +216,9 @@ k_train_grads(NetDev net, const float* __restrict__ xyz, const float* __restrict
   p.run(net, w, x);
   // v_i = c J_i, c = w_e 2 (||J|| - 1) / (B ||J||), B = BATCH_SIZE (train.py:197;
   // the L1 mean below divides by the actual n)   (torch: a zero norm has a zero gradient)
-  const double nj = sqrt(stats[1]);
+  // gout != null: the vector-Jacobian product sum_i gout_i d sdf_i / d theta
+  // instead (autograd through Net.sdf): kappa = gout (1 - y^2), mu = 0
+  const double nj = gout ? 0.0 : sqrt(stats[1]);
   const float c = nj > 0.0 ? (float)(eik_w * 2.0 * (nj - 1.0) / ((double)eik_batch * nj)) : 0.f;
   const float ty = 1.f - p.y * p.y;
   float v[3];
@@ -224,12 +226,12 @@ k_train_grads(NetDev net, const float* __restrict__ xyz, const float* __restrict
   for (int d = 0; d < 3; ++d) v[d] = c * ty * p.gz[d];
   const float q = v[0] * p.gz[0] + v[1] * p.gz[1] + v[2] * p.gz[2];
   float rho = 0.f;
-  if (live && p.y >= -T && p.y <= T) {
+  if (!gout && live && p.y >= -T && p.y <= T) {
     const float r = clampf(p.y, T) - clampf(gt[i], T);
     rho = (r > 0.f ? 1.f : (r < 0.f ? -1.f : 0.f)) / (float)n;
   }
-  const float kappa = live ? ty * (rho - 2.f * p.y * q) : 0.f;
-  const float mu = live ? ty : 0.f;
+  const float kappa = !live ? 0.f : (gout ? ty * gout[i] : ty * (rho - 2.f * p.y * q));
+  const float mu = (live && !gout) ? ty : 0.f;
   // direction a = (1/2) sum_c T_c (grad w_c . v), and the table terms
   const float2* tab = reinterpret_cast<const float2*>(net.table);
   float a[IN];
@@ -466,7 +468,23 @@ int launch_train_grad(const NetDev& net, const float* xyz, const float* gt, int6
     hipLaunchKernelGGL((k_train_norms<L_, 16>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net, xyz, gt, n, clamp_t,
                        stats);
     hipLaunchKernelGGL((k_train_grads<L_, 16>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net, xyz, gt, n, clamp_t,
-                       eik_w, eik_batch, stats, g_table, g_w);
+                       eik_w, eik_batch, stats, g_table, g_w, nullptr);
+  });
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int launch_sdf_vjp(const NetDev& net, const float* xyz, const float* gout, int64_t n, float* g_table, float* g_w,
+                   hipStream_t s) {
+  if (!net_supported(net) || net.tied || net.num_hidden != 16 || net.num_layers != 3) {
+    tnp_set_error("sdf_vjp: the parameter gradient is written for 3-layer, 16-hidden nets (this net: %d layers, "
+                  "%d hidden, %d levels)", net.num_layers, net.num_hidden, net.n_levels);
+    return -1;
+  }
+  if (n <= 0) return 0;
+  TNP_TRAIN_DISPATCH(net.n_levels, {
+    hipLaunchKernelGGL((k_train_grads<L_, 16>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net, xyz, nullptr, n, 0.f,
+                       0.f, (int64_t)1, nullptr, g_table, g_w, gout);
   });
   TNP_CHECK(hipGetLastError());
   return 0;

@@ -7,9 +7,17 @@ Same constructor, attributes (``enc``, ``fc``, ``num_layers``,
 (``forward(x, gather, group)``, ``preprocess``, ``preprocess_inverse``,
 ``sdf``, ``region``, ``normal``).  Every evaluation is a fused HIP kernel
 (encoding + MLP, csrc/net.hip) on the net's ROCm device; the forward is
-bitwise equal to the reference's PyTorch-CPU evaluation.  These ops carry
-no autograd graph: training takes its gradients in closed form from
-``tropical.stanford.sdf_train.SDFTrainer`` (csrc/train.hip).
+bitwise equal to the reference's PyTorch-CPU evaluation.
+
+Autograd: ``sdf`` is differentiable like the reference's (model.py:84-88,
+through tcnn there) -- w.r.t. its input (the analytic input gradient of
+``tnp_sdf_grad``) and w.r.t. the parameters (``tnp_sdf_vjp``: the encoding
+table and the fc weights; 3-layer, 16-hidden nets), so a caller's
+``net.sdf(x).sum().backward()`` fills ``x.grad`` and the parameters'
+``.grad``.  Double backward (the eikonal term's ``create_graph=True``,
+train.py:196) is taken in closed form by
+``tropical.stanford.sdf_train.SDFTrainer`` instead.  ``forward`` / ``region``
+/ ``normal`` return values without a graph, as the extraction uses them.
 """
 from __future__ import annotations
 
@@ -21,6 +29,46 @@ from torch import Tensor
 
 from .. import _hip
 from ..tropical import TropicalHashGrid
+
+
+class _SDF(torch.autograd.Function):
+    """Net.sdf with its backward: d sdf / d x from tnp_sdf_grad (computed in
+    the forward's kernel), d sdf / d theta as one tnp_sdf_vjp call."""
+
+    @staticmethod
+    def forward(ctx, net, x, table, *weights):
+        y, J = net._sdf_eval(x, want_grad=bool(ctx.needs_input_grad[1]))
+        ctx.net = net
+        ctx.save_for_backward(x, J)
+        return y.unsqueeze(-1)
+
+    @staticmethod
+    def backward(ctx, gy):
+        if torch.is_grad_enabled():
+            raise NotImplementedError(
+                "double backward through Net.sdf (the reference's eikonal term, train.py:196): "
+                "tropical.stanford.sdf_train.SDFTrainer takes it in closed form")
+        net = ctx.net
+        x, J = ctx.saved_tensors
+        g = gy.detach().reshape(-1).float().contiguous()
+        gx = (g[:, None] * J).to(x.dtype) if ctx.needs_input_grad[1] else None
+        grads = [None] * (len(ctx.needs_input_grad) - 2)
+        if any(ctx.needs_input_grad[2:]):
+            params = [net.enc.module.params] + [t for lin in net.fc for t in (lin.weight, lin.bias)]
+            g_table = torch.zeros(params[0].numel(), device=x.device)
+            g_w = torch.zeros(sum(t.numel() for t in params[1:]), device=x.device)
+            s, keep = net.tnp_desc()
+            xs = x.detach().float().contiguous()
+            _hip.check(_hip.lib().tnp_sdf_vjp(ctypes.byref(s), _hip.ptr(xs), _hip.ptr(g), xs.shape[0],
+                                              _hip.ptr(g_table), _hip.ptr(g_w),
+                                              ctypes.c_void_p(_hip.stream_ptr(x.device))), "tnp_sdf_vjp")
+            del keep
+            grads[0] = g_table.view_as(params[0]).to(params[0].dtype)
+            off = 0
+            for k, t in enumerate(params[1:]):
+                grads[1 + k] = g_w[off:off + t.numel()].view_as(t).to(t.dtype)
+                off += t.numel()
+        return (None, gx, *grads)
 
 
 class Net(nn.Module):
@@ -92,15 +140,26 @@ class Net(nn.Module):
     def preprocess_inverse(self, x):
         return x * (self.scale * 2) - self.scale
 
-    def sdf(self, x):
+    def _sdf_eval(self, x, want_grad: bool = False):
+        """(sdf [n], d sdf / d x [n, 3] or None) from one tnp_sdf_grad call."""
         _hip.require_cuda(x, "Net.sdf")
         s, keep = self.tnp_desc()
         x = x.detach().float().contiguous()
         y = torch.empty(x.shape[0], device=x.device)
+        J = torch.empty(x.shape[0], 3, device=x.device) if want_grad else None
         _hip.check(_hip.lib().tnp_sdf_grad(ctypes.byref(s), _hip.ptr(x), x.shape[0], _hip.ptr(y),
-                                           None, ctypes.c_void_p(_hip.stream_ptr(x.device))),
+                                           _hip.ptr(J), ctypes.c_void_p(_hip.stream_ptr(x.device))),
                    "tnp_sdf_grad")
-        return y.unsqueeze(-1)
+        del keep
+        return y, J
+
+    def sdf(self, x):
+        """tanh(o1 - o0) (model.py:84-88); differentiable w.r.t. x and the
+        parameters under grad mode (module docstring)."""
+        params = [self.enc.module.params] + [t for lin in self.fc for t in (lin.weight, lin.bias)]
+        if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in params)):
+            return _SDF.apply(self, x, *params)
+        return self._sdf_eval(x)[0].unsqueeze(-1)
 
     def region(self, vertices: Tensor, output: Tensor = None, eps=None):
         eps = self.eps if eps is None else eps
