@@ -157,6 +157,17 @@ int tnp_engine_split(tnp_engine* eng, int idx, void* stream, int64_t* S,
 int tnp_engine_finish(tnp_engine* eng, int idx, int prune, int override,
                       void* stream, tnp_step_stats* stats);
 
+/* The whole hyperplane loop of subpoly.py:58-69 on one device: active
+ * planes, then per active plane tnp_engine_split + tnp_engine_finish (prune
+ * on every plane but the last), empty steps skipped (subpoly.py:110), the
+ * next-active mask folded in after each pruning step -- the loop a host
+ * driver would run, without a host round trip per step.  stats[0 ..
+ * max_stats) receive the completed steps' stats, *n_steps their count.  Not
+ * for a sharded engine (tnp_engine_set_shards > 1: its global decisions
+ * fall between split and finish). */
+int tnp_engine_run_steps(tnp_engine* eng, void* stream, tnp_step_stats* stats, int max_stats,
+                         int* n_steps);
+
 int tnp_engine_sizes(tnp_engine* eng, int64_t* V, int64_t* E);
 
 /* Curve path: after tnp_engine_finish, the strict filter's keep flags
@@ -206,6 +217,14 @@ int tnp_engine_set_strict(tnp_engine* eng, int on);
  * counted in tnp_step_stats.S_dup so the global split count counts each
  * split once.  lo > hi (default) = everything owned.  Flat path only. */
 int tnp_engine_set_owned(tnp_engine* eng, int lo, int hi);
+
+/* The loaded complex lies between the x mark planes x0 and x1 (an x-slab
+ * with its halo): the step's spatial buckets then cover only those cells.
+ * tnp_engine_lattice sets it, tnp_engine_load / _skeleton reset it to the
+ * whole grid (x1 < x0).  A vertex outside fails the step with an error.
+ * Performance only: the results do not depend on it.  No reference
+ * counterpart (multi-GPU sharding). */
+int tnp_engine_set_xspan(tnp_engine* eng, int x0, int x1);
 
 /* world > 1: this engine holds one x-slab of a complex sharded over `world`
  * devices.  A step the other shards split may leave this one without any

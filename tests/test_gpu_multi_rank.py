@@ -184,3 +184,32 @@ def test_lattice256_eight_slabs_stitch_to_the_unsharded_complex(cuda, tmp_path):
     z = _run(tmp_path, (256, 6), "bench", 8)
     assert tuple(int(x) for x in z["tot"]) == want
     assert len(z["cuts"]) == 9
+
+
+def test_slab_buckets_do_not_change_the_result(cuda):
+    """The spatial buckets of an x-slab cover only its cells (lattice() sets
+    the x span; an 8-rank 256^3 slab: 5 x 33 x 33 buckets of 8^3 cells
+    instead of 17^3 of 16^3).  Geometry is performance only: the slab's
+    complex with the narrow buckets equals the one with the whole grid's,
+    and a vertex outside the span fails loudly instead of being dropped."""
+    from helpers import product_net
+    from tropical.distributed import complex_hash
+    from tropical._engine import engine_for
+    net = product_net(load("synth64h"), cuda)
+    eng = engine_for(net)
+    eng.set_owned()
+    eng.set_shards(2)  # a slab may hold no connecting pair on some step
+    got = []
+    for narrow in (True, False):
+        eng.lattice(20, 41)
+        if not narrow:
+            eng.set_xspan()  # the whole grid
+        eng.run_steps([])
+        V, E, _ = eng.export()
+        got.append((V.shape[0], E.shape[0]) + complex_hash(V, E))
+    assert got[0] == got[1]
+    eng.lattice(20, 41)
+    eng.set_xspan(30, 41)
+    with pytest.raises(RuntimeError, match="outside the x mark planes"):
+        eng.run_steps([])
+    eng.set_shards(1)

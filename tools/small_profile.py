@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Bunny-scale latency breakdown of the drop-in subpoly() on one GPU.
 
-    python tools/small_profile.py [reps]
+    python tools/small_profile.py [reps] [flat|curve]
 
 For the committed stand-in small nets (small_sphere flat, small_sphere_curve
 curve-approx on): median wall time of each phase (skeleton, the hyperplane
@@ -25,12 +25,15 @@ import torch  # noqa: E402
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+    only = sys.argv[2] if len(sys.argv) > 2 else None  # "flat" | "curve"
     from golden_io import load
     from helpers import product_net
     import tropical.subpoly as sp
     from tropical._engine import engine_for
     dev = torch.device("cuda", 0)
     for name, force in (("small_sphere", True), ("small_sphere_curve", False)):
+        if only and only != ("flat" if force else "curve"):
+            continue
         d = load(name)
         net = product_net(d, dev)
         ph = {"skeleton": [], "loop": [], "finish": [], "total": []}

@@ -29,6 +29,7 @@
 // deterministic.  Traffic per entry: 8 B scatter write + 8 B read + 24 B key
 // gather + 32 B record write, against ~70 B for three 8-bit radix passes.
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 #include "step.h"
@@ -53,11 +54,7 @@ __device__ __forceinline__ int member_of(const int32_t* members, int64_t S, int6
   return m < S ? (int)(V + m) : members[m];
 }
 
-struct BGeom {
-  int NC;   // cell coordinates (+2) per axis: [0, NC)
-  int sh;   // log2 of the bucket edge in cells
-  int NBd;  // buckets per axis
-};
+using BGeom = BucketGeom;
 
 // the window pass the grouping kernel runs over each bucket (keys == null:
 // none; the engine then launches k_connect_win)
@@ -102,12 +99,18 @@ __device__ __forceinline__ void span_of(uint64_t g, int lo[3], int n[3]) {
 }
 
 __device__ __forceinline__ int bucket_of(const BGeom& G, int cx, int cy, int cz) {
-  return ((cx >> G.sh) * G.NBd + (cy >> G.sh)) * G.NBd + (cz >> G.sh);
+  return (((cx - G.xorg) >> G.sh) * G.NBd + (cy >> G.sh)) * G.NBd + (cz >> G.sh);
 }
 
 __device__ __forceinline__ int local_of(const BGeom& G, int cx, int cy, int cz) {
   const int m = (1 << G.sh) - 1;
-  return ((cx & m) << (2 * G.sh)) | ((cy & m) << G.sh) | (cz & m);
+  return (((cx - G.xorg) & m) << (2 * G.sh)) | ((cy & m) << G.sh) | (cz & m);
+}
+
+// every cell of the span inside the buckets' x range (else the member is
+// skipped and flagged: the complex left the slab the engine was told of)
+__device__ __forceinline__ bool span_inside(const BGeom& G, const int lo[3], const int n[3]) {
+  return (unsigned)(lo[0] - G.xorg) <= (unsigned)(G.xn - n[0]);
 }
 
 // exclusive scan of n counts another workgroup of this launch handed over
@@ -157,7 +160,7 @@ k_bucket_count(const int32_t* __restrict__ members, int64_t S, int64_t V, int64_
                int32_t* __restrict__ bcount, int64_t* __restrict__ part, int64_t* __restrict__ bbase,
                uint8_t* __restrict__ live, int64_t nlive, int fuse, Override ov,
                int64_t* __restrict__ ctr) {
-  __shared__ int hist[BUCKET_MAX];
+  extern __shared__ int hist[];  // NB bins (dynamic: the geometry's count)
   __shared__ int64_t lds[TNP_WAVES];
   __shared__ int last;
   if (live) {
@@ -218,11 +221,16 @@ k_bucket_count(const int32_t* __restrict__ members, int64_t S, int64_t V, int64_
       zz[k] = z;
     }
   }
+  bool outside = false;
 #pragma unroll
   for (int k = 0; k < BK_IPT; ++k) {
     if (vv[k] < 0) continue;
     int lo[3], n[3];
     span_of(gg[k], lo, n);
+    if (!span_inside(G, lo, n)) {
+      outside = true;
+      continue;
+    }
     for (int i = 0; i < n[0]; ++i)
       for (int j = 0; j < n[1]; ++j)
         for (int q = 0; q < n[2]; ++q) atomicAdd(&hist[bucket_of(G, lo[0] + i, lo[1] + j, lo[2] + q)], 1);
@@ -231,6 +239,7 @@ k_bucket_count(const int32_t* __restrict__ members, int64_t S, int64_t V, int64_
     k0 |= kz == 0;
   }
   if (__ballot(k0) && tnp::lane() == 0) atomicOr((unsigned long long*)&ctr[CTR_K0], 1ull);
+  if (__ballot(outside) && tnp::lane() == 0) atomicOr((unsigned long long*)&ctr[CTR_K0], 2ull);
   if (counts) {
     __syncthreads();
     for (int i = threadIdx.x; i < NB; i += TNP_BLOCK)
@@ -285,8 +294,8 @@ k_bucket_scatter(const int32_t* __restrict__ members, int64_t S, int64_t V, int6
                  const uint64_t* __restrict__ grid,
                  BGeom G, int NB, const int64_t* __restrict__ bbase, int32_t* __restrict__ bcur,
                  uint64_t* __restrict__ ekv) {
-  __shared__ int hist[BUCKET_MAX];
-  __shared__ int rel[BUCKET_MAX];
+  extern __shared__ int hist[];  // NB bins, then rel[NB] (dynamic)
+  int* const rel = hist + NB;
   for (int i = threadIdx.x; i < NB; i += TNP_BLOCK) hist[i] = 0;
   __syncthreads();
   const int64_t base = (int64_t)blockIdx.x * TNP_BLOCK * BK_IPT;
@@ -304,6 +313,10 @@ k_bucket_scatter(const int32_t* __restrict__ members, int64_t S, int64_t V, int6
     if (vv[k] < 0) continue;
     int lo[3], n[3];
     span_of(gg[k], lo, n);
+    if (!span_inside(G, lo, n)) {  // flagged by the count pass
+      vv[k] = -1;
+      continue;
+    }
     for (int i = 0; i < n[0]; ++i)
       for (int j = 0; j < n[1]; ++j)
         for (int q = 0; q < n[2]; ++q) atomicAdd(&hist[bucket_of(G, lo[0] + i, lo[1] + j, lo[2] + q)], 1);
@@ -508,7 +521,7 @@ __device__ __forceinline__ void group_bucket(const BGeom& G, int b, int64_t base
   for (int i = c0; i < c0 + per && i < LC; ++i) {
     const int m = cnt[i];
     if (m > WCELL && m <= 65535) {
-      const int cx = (bx << G.sh) | (i >> (2 * G.sh));
+      const int cx = G.xorg + ((bx << G.sh) | (i >> (2 * G.sh)));
       const int cy = (by << G.sh) | ((i >> G.sh) & m_);
       const int cz = (bz << G.sh) | (i & m_);
       // agent-scope stores: the fused last workgroup gathers them (tnp::last_block)
@@ -702,17 +715,25 @@ k_pair_gather(const int64_t* __restrict__ bbase, const int64_t* __restrict__ bnp
 
 }  // namespace
 
-int bucket_geometry(int n_marks, int* sh, int* NBd, int* NB) {
+int bucket_geometry(int n_marks, int x0, int x1, BucketGeom* g) {
   const int NC = n_marks + 2;
-  int s = 3;
-  while (s < 5 && NC > 17 * (1 << s)) ++s;  // k_bucket_group is built for 3 and 4
-  if ((1 << (3 * s)) > BUCKET_LOCAL_MAX) return -1;
-  const int nbd = (NC + (1 << s) - 1) >> s;
-  if (nbd * nbd * nbd > BUCKET_MAX) return -1;
-  *sh = s;
-  *NBd = nbd;
-  *NB = nbd * nbd * nbd;
-  return 0;
+  // cells of a complex inside the x mark planes [x0, x1]: offsets x0 - 1
+  // (a vertex within eps of plane x0 spans the cell below) to x1, i.e. cell
+  // coordinates x0 + 1 .. x1 + 2; one more on each side
+  const int xlo = std::max(0, x0), xhi = std::min(NC - 1, x1 + 3);
+  static const int s_env = [] {  // TNP_BUCKET_SH=3|4: force the bucket edge (experiments)
+    const char* v = getenv("TNP_BUCKET_SH");
+    return v ? atoi(v) : 0;
+  }();
+  for (int s = (s_env == 4 ? 4 : 3); s <= 4; ++s) {
+    const int nbd = (NC + (1 << s) - 1) >> s;
+    const int nbx = (xhi - xlo + 1 + (1 << s) - 1) >> s;
+    const int64_t nb = (int64_t)nbx * nbd * nbd;
+    if (nb > BUCKET_MAX) continue;
+    *g = BucketGeom{NC, s, nbd, nbx, xlo, nbx << s, (int)nb};
+    return 0;
+  }
+  return -1;
 }
 
 int64_t bucket_member_blocks(int64_t M) {
@@ -720,15 +741,10 @@ int64_t bucket_member_blocks(int64_t M) {
   return std::max<int64_t>((M + per - 1) / per, 1);
 }
 int launch_bucket_entries(const int32_t* members, int64_t S, int64_t V, int64_t M, const uint64_t* keys,
-                          const uint64_t* zero, int idx, int n_marks, int32_t* bcount, int32_t* bcur,
+                          const uint64_t* zero, int idx, const BucketGeom& G, int32_t* bcount, int32_t* bcur,
                           int64_t* bbase, int64_t* part, uint64_t* ekv, bool clean, uint8_t* live,
                           int64_t nlive, const NewOverride* ovr, int64_t* ctr, hipStream_t s) {
-  int sh, NBd, NB;
-  if (bucket_geometry(n_marks, &sh, &NBd, &NB)) {
-    tnp_set_error("bucket geometry: %d marks", n_marks);
-    return -1;
-  }
-  const BGeom G{n_marks + 2, sh, NBd};
+  const int NB = G.NB;
   if (!clean) {  // else: zeroed by the previous step's k_pair_gather
     TNP_CHECK(hipMemsetAsync(bcount, 0, NB * sizeof(int32_t), s));
     TNP_CHECK(hipMemsetAsync(bcur, 0, NB * sizeof(int32_t), s));
@@ -746,31 +762,26 @@ int launch_bucket_entries(const int32_t* members, int64_t S, int64_t V, int64_t 
   if (ovr)
     ov = Override{ovr->flag, ovr->shared, ovr->pre, ovr->ld, ovr->keep_from, ovr->pos, ovr->zero,
                   reinterpret_cast<ulonglong2*>(ovr->pz)};
-  hipLaunchKernelGGL(k_bucket_count, dim3(grid), dim3(TNP_BLOCK), 0, s, members, S, V, M, keys, zero, idx,
+  hipLaunchKernelGGL(k_bucket_count, dim3(grid), dim3(TNP_BLOCK), NB * sizeof(int), s, members, S, V, M, keys, zero, idx,
                      G, NB, bcount, part, bbase, live, nlive, fuse, ov, ctr);
   if (!fuse)
     hipLaunchKernelGGL(k_scan_sets, dim3(1, 1), dim3(TNP_BLOCK), 0, s, ScanSet{bcount, 0, bbase, CTR_T},
                        ScanSet{}, ScanSet{}, NB, part, (int64_t)grid, (int)CTR_A, ctr);
   if (M > 0)
-    hipLaunchKernelGGL(k_bucket_scatter, dim3(nblk), dim3(TNP_BLOCK), 0, s, members, S, V, M, keys, G, NB,
+    hipLaunchKernelGGL(k_bucket_scatter, dim3(nblk), dim3(TNP_BLOCK), 2 * NB * sizeof(int), s, members, S, V, M, keys, G, NB,
                        bbase, bcur, ekv);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
 
-int launch_bucket_pairs(int n_marks, const int64_t* bbase, const uint64_t* ekv, const uint64_t* pz,
+int launch_bucket_pairs(const BucketGeom& G, const int64_t* bbase, const uint64_t* ekv, const uint64_t* pz,
                         CellEnt* ents, int32_t* lcell,
                         int32_t* lent, int32_t* ln, int64_t* lpoff, int64_t* bnpc, int64_t* bnpairs,
                         int64_t* bspairs, int64_t* spoff, int64_t* pcoff, int64_t* pairoff,
                         int32_t* pcell, int32_t* pent, int32_t* pn, int64_t* ptoff, int32_t* bcell,
                         int64_t bcap, int32_t* bcount, int32_t* bcur, const ConnectWin* win, int64_t* ctr,
                         hipStream_t s) {
-  int sh, NBd, NB;
-  if (bucket_geometry(n_marks, &sh, &NBd, &NB)) {
-    tnp_set_error("bucket geometry: %d marks", n_marks);
-    return -1;
-  }
-  const BGeom G{n_marks + 2, sh, NBd};
+  const int NB = G.NB, sh = G.sh;
   const int fuse = NB <= FUSE_MAX_BLOCKS;
   const PairLists pl{pcell, pent, pn, ptoff, bcell, bcap, connect_chunk_pairs(), bcount, bcur};
   WinArgs wa{0, 0, 0ull, nullptr, 0, nullptr};

@@ -122,6 +122,9 @@ enum {
 struct tnp_engine {
   int device = 0;
   int own_lo = 1, own_hi = 0;  // owned mark planes (lo, hi]; lo > hi: all
+  // x mark planes the complex lies within (the spatial buckets cover only
+  // those cells); xs1 < xs0: all
+  int xs0 = 0, xs1 = -1;
   int curve = 0;          // 1: subpoly_(force=False) semantics
   int strict = 1;         // curve path: subpoly_(strict=...) -- 0 keeps every split (subpoly.py:198-202)
   int shards = 1;         // >1: one x-slab of a sharded complex
@@ -142,12 +145,17 @@ struct tnp_engine {
   // which the endpoint keys differ, ef = the first plane >= mask_from that
   // splits the edge (EDGE_NOSPLIT: none); valid when masks_valid
   Buf edm, eef, edm_alt, eef_alt;
+  Buf lzpart;  // the lazy prune's per-workgroup kept counts
   Buf xs;                // per-XCD shards of the connect phase (step.h XS_*)
   bool xs_clean = false;
   bool masks_valid = false;
   int mask_from = 0;       // plane the stored first split planes start at
   uint64_t act_bits = 0;   // OR of the edges' first split planes (bit p: plane p splits an edge)
   int64_t V = 0, E = 0;
+  // E counts edge SLOTS: the pruning deletes lazily (EDGE_DEAD bytes, edges
+  // keep their slots) and compacts only when most slots are dead or before
+  // an export; E_live is the reference's edge count
+  int64_t E_live = 0;
   int keep_all = 0;
   int valid_from = 0;  // pre planes [valid_from, K) are valid for every vertex
   // Lazy compaction: during the hot loop vertex ids are SLOTS (V = slots in
@@ -196,6 +204,7 @@ struct tnp_engine {
   Buf sents;                // bucket-ordered packed entries before the in-bucket grouping
   Buf bk[14];               // bucket.hip scratch (per-bucket counts, bases, pair-cell areas)
   bool radix_cells = false; // TNP_RADIX_CELLS=1: the radix-sort bucketing path
+  bool lazy_edges = true;   // TNP_LAZY_EDGES=0: every pruning step compacts the edge list
   bool bk_clean = false;    // bucket counters (bk[0], bk[1]) are zero
   Buf cv[CV_N];
 };
@@ -305,8 +314,11 @@ static int scan_counts(tnp_engine* e, const int32_t* in, int64_t* out, int64_t n
 // grow a vertex set to `rows` keeping [0, keep_rows)
 static int vset_ensure(tnp_engine* e, VSet& v, int64_t rows, int64_t keep_rows, hipStream_t s) {
   if (rows <= v.cap && v.K == e->K) return 0;
-  if (v.K != e->K) keep_rows = 0;  // another net: nothing of the old set is kept
-  int64_t nc = std::max<int64_t>(rows, v.cap + v.cap / 2);
+  // another net: nothing of the old set is kept, and its capacity is no
+  // growth history (alternating nets must not compound the 1.5x)
+  const bool same = v.K == e->K;
+  if (!same) keep_rows = 0;
+  int64_t nc = same ? std::max<int64_t>(rows, v.cap + v.cap / 2) : rows;
   nc = (nc + 255) / 256 * 256;
   VSet n;
   n.cap = nc;
@@ -366,7 +378,7 @@ static int compute_masks(tnp_engine* e, int from, int64_t* ctr, hipStream_t s) {
   if (buf_ensure(e->eef, E1 * sizeof(uint8_t), s)) return -1;
   TIMED("edge_masks", 42.0 * e->E,
         launch_edge_masks(P<int32_t>(e->edges), e->E, P<uint64_t>(e->cur.pz), P<uint8_t>(e->edm),
-                          P<uint8_t>(e->eef), from, e->K - 1, ctr, s));
+                          P<uint8_t>(e->eef), from, e->K - 1, e->E != e->E_live, ctr, s));
   e->masks_valid = true;
   e->mask_from = from;
   return 0;
@@ -384,10 +396,39 @@ static int ensure_masks(tnp_engine* e, int idx, hipStream_t s) {
   return compute_masks(e, idx, P<int64_t>(e->ctr), s) ? -1 : 1;
 }
 
+// drop the lazily deleted edges, live ones in order (the compacting prune
+// keeping every live edge: idx = -1)
+static int compact_edges(tnp_engine* e, hipStream_t s) {
+  if (e->E == e->E_live) return 0;
+  const int64_t E = e->E, E1 = std::max<int64_t>(E, 1);
+  if (buf_ensure(e->edges_alt, E1 * 2 * sizeof(int32_t), s)) return -1;
+  if (buf_ensure(e->edm_alt, E1 * sizeof(uint8_t), s)) return -1;
+  if (buf_ensure(e->eef_alt, E1 * sizeof(uint8_t), s)) return -1;
+  TnpLB lb;
+  if (lb_begin(e, lb_tiles(E), s, &lb, 0, false)) return -1;
+  TIMED("compact_edges", 12.0 * E,
+        launch_prune_lb(P<int32_t>(e->edges), E, nullptr, 0, e->V, nullptr, 0, 0, -1, e->K - 1,
+                        P<uint64_t>(e->cur.pz), P<uint8_t>(e->edm), P<uint8_t>(e->eef), P<int32_t>(e->edges_alt),
+                        P<uint8_t>(e->edm_alt), P<uint8_t>(e->eef_alt), P<uint8_t>(e->live), false,
+                        P<int64_t>(e->ctr), lb, s));
+  std::swap(e->edges, e->edges_alt);
+  std::swap(e->edm, e->edm_alt);
+  std::swap(e->eef, e->eef_alt);
+  if (read_ctr(e, s)) return -1;
+  if (e->h_ctr[CTR_E] != e->E_live) {
+    tnp_set_error("edge compaction: %lld live edges, %lld expected", (long long)e->h_ctr[CTR_E],
+                  (long long)e->E_live);
+    return -1;
+  }
+  e->E = e->E_live;
+  return 0;
+}
+
 // renumber the live slots densely (the reference's per-step compaction,
 // subpoly.py:266-277, done once): scan of the live flags, gather of the
 // vertex rows (planes >= valid_from), edge remap
 static int compact_now(tnp_engine* e, hipStream_t s) {
+  if (compact_edges(e, s)) return -1;
   if (!e->dirty) return 0;
   const int64_t NV = e->V;
   if (buf_ensure(e->nid, std::max<int64_t>(NV, 1) * sizeof(int64_t), s)) return -1;
@@ -431,6 +472,7 @@ extern "C" int tnp_engine_create(tnp_engine** out, int device) {
   e->device = device;
   if (const char* lim = getenv("TNP_MAX_PAIR_TESTS")) e->max_pair_tests = atoll(lim);
   if (const char* rc = getenv("TNP_RADIX_CELLS")) e->radix_cells = atoi(rc) != 0;
+  if (const char* lz = getenv("TNP_LAZY_EDGES")) e->lazy_edges = atoi(lz) != 0;
   if (const char* sp = getenv("TNP_LB_SPIN")) e->lb_spin = atoi(sp);
   if (hipHostMalloc((void**)&e->h_ctr, CTR_N * sizeof(int64_t), hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc((void**)&e->h_map, 32 * sizeof(int64_t), hipHostMallocMapped | hipHostMallocCoherent) !=
@@ -462,7 +504,7 @@ extern "C" void tnp_engine_destroy(tnp_engine* e) {
                  &e->ent_v, &e->ents, &e->pcell, &e->ptoff, &e->bcell,
                  &e->ckeys_a, &e->ckeys_b, &e->sort_scr, &e->flags, &e->used, &e->nid,
                  &e->ctr, &e->tri, &e->faces, &e->lb[0], &e->lb[1], &e->edm, &e->eef,
-                 &e->edm_alt, &e->eef_alt, &e->live, &e->tied_table, &e->xs, &e->lbrc};
+                 &e->edm_alt, &e->eef_alt, &e->live, &e->tied_table, &e->xs, &e->lbrc, &e->lzpart};
   for (Buf* b : bufs) buf_free(*b, s);
   for (Buf& b : e->fscr) buf_free(b, s);
   for (Buf& b : e->fscr2) buf_free(b, s);
@@ -605,6 +647,7 @@ static int set_edges_i64(tnp_engine* e, const int64_t* d_edges, int64_t E, hipSt
                        P<int32_t>(e->edges), 2 * E);
   TNP_CHECK(hipGetLastError());
   e->E = E;
+  e->E_live = E;
   return 0;
 }
 
@@ -613,6 +656,8 @@ extern "C" int tnp_engine_load(tnp_engine* e, const float* d_xyz, int64_t V, con
   hipStream_t s = (hipStream_t)stream;
   if (!e->has_net) { tnp_set_error("engine has no net"); return -1; }
   TNP_CHECK(hipSetDevice(e->device));
+  e->xs0 = 0;  // anywhere (tnp_engine_set_xspan narrows it)
+  e->xs1 = -1;
   if (buf_ensure(e->ctr, CTR_N * sizeof(int64_t), s)) return -1;
   if (vset_ensure(e, e->cur, std::max<int64_t>(V, 1), 0, s)) return -1;
   if (V > 0)
@@ -639,7 +684,7 @@ extern "C" int tnp_engine_load(tnp_engine* e, const float* d_xyz, int64_t V, con
 
 extern "C" int tnp_engine_sizes(tnp_engine* e, int64_t* V, int64_t* E) {
   *V = e->V_live;
-  *E = e->E;
+  *E = e->E_live;
   return 0;
 }
 
@@ -968,8 +1013,10 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   uint64_t* zero = P<uint64_t>(c.zero);
   uint64_t* grid = P<uint64_t>(c.grid);
 
-  int bsh = 0, bnd = 0, NB = 0;
-  const bool buckets = !e->radix_cells && bucket_geometry(e->net.n_marks, &bsh, &bnd, &NB) == 0;
+  BucketGeom bg{};
+  const int gx0 = e->xs1 >= e->xs0 ? e->xs0 : 0, gx1 = e->xs1 >= e->xs0 ? e->xs1 : e->net.n_marks - 1;
+  const bool buckets = !e->radix_cells && bucket_geometry(e->net.n_marks, gx0, gx1, &bg) == 0;
+  const int NB = buckets ? bg.NB : 0;
   // 1. override + keys of the new vertices (flat bucket path: the override
   //    runs inside the bucket count, below)
   if (e->pend_fused && buckets) {
@@ -1048,7 +1095,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     NewOverride nov{override_, P<uint64_t>(e->shared), P<float>(c.pre), c.cap, e->valid_from, pos, zero,
                     P<uint64_t>(c.pz)};
     TIMED("bucket_entries", 16.0 * M,  // + 8 B per entry, set once T is known
-          launch_bucket_entries(P<int32_t>(e->members), S, V, M, grid, zero, idx, e->net.n_marks,
+          launch_bucket_entries(P<int32_t>(e->members), S, V, M, grid, zero, idx, bg,
                                 P<int32_t>(e->bk[0]), P<int32_t>(e->bk[1]), P<int64_t>(e->bk[2]),
                                 P<int64_t>(e->bk[7]), P<uint64_t>(e->sents), e->bk_clean,
                                 prune ? P<uint8_t>(e->live) : nullptr, NV, e->pend_fused ? &nov : nullptr,
@@ -1148,7 +1195,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
       if (buf_ensure(e->bcell, bcap * sizeof(int32_t), s)) return -1;
       const ConnectWin cw{idx, nb, cfmask, P<uint64_t>(e->ckeys_a), cap, xs};
       TIMED("bucket_group", 0.0,
-            launch_bucket_pairs(e->net.n_marks, P<int64_t>(e->bk[2]), P<uint64_t>(e->sents),
+            launch_bucket_pairs(bg, P<int64_t>(e->bk[2]), P<uint64_t>(e->sents),
                                 P<uint64_t>(c.pz), P<CellEnt>(e->ents),
                                 P<int32_t>(e->bk[8]), P<int32_t>(e->bk[9]), P<int32_t>(e->bk[10]),
                                 P<int64_t>(e->bk[11]), P<int64_t>(e->bk[3]), P<int64_t>(e->bk[4]),
@@ -1175,6 +1222,11 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     }
     if (read_ctr(e, s)) return -1;
     if (buckets) {
+      if (e->h_ctr[CTR_K0] & 2) {
+        tnp_set_error("plane %d: a vertex outside the x mark planes [%d, %d] the engine was given "
+                      "(tnp_engine_set_xspan)", idx, gx0, gx1);
+        return -1;
+      }
       if (e->h_ctr[CTR_K0]) {
         // the reference builds torch.cartesian_prod() of zero tensors (subpoly.py:317)
         tnp_set_error("meshgrid expects a non-empty TensorList (a region row without zeros, plane %d)",
@@ -1235,14 +1287,18 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
 
   // 5. pruning over [edges; e_new; c_new] + vertex compaction
   const int64_t N = E + S + X;
+  const int64_t E_live_in = e->E_live;
   int64_t nt = step_tiles(N);
   if (buf_ensure(e->blk, (nt + 1) * sizeof(int32_t), s)) return -1;
   if (buf_ensure(e->blkoff, (nt + 1) * sizeof(int64_t), s)) return -1;
-  if (buf_ensure(e->edges_alt, std::max<int64_t>(N, 1) * 2 * sizeof(int32_t), s)) return -1;
   // ctr[CTR_ACTIVE] and ctr[CTR_V] are still zero from the split's reset
   const int32_t* eg = P<int32_t>(e->edges);
-  int64_t V2 = NV, E2 = N;
+  int64_t V2 = NV, E2 = N, E2_live = N;
   int next_valid = e->valid_from;
+  // lazy edge deletion (k_prune_lazy) unless the list is mostly dead edges
+  // already: then the compacting prune drops them (and this step's)
+  const bool lazy = prune && e->lazy_edges && (E - E_live_in) <= E_live_in;
+  bool swap_edges = true;
   if (prune) {
     // live flags recomputed from the kept edges; no vertex moves (lazy
     // compaction): the distinct flagged count is the reference's V'
@@ -1254,31 +1310,73 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     // (curve path: recomputed after the rewiring, first split planes above idx)
     if (!e->masks_valid && compute_masks(e, idx + 1, nullptr, s)) return -1;
     const int64_t N1 = std::max<int64_t>(N, 1);
-    if (buf_ensure(e->edm_alt, N1 * sizeof(uint8_t), s)) return -1;
-    if (buf_ensure(e->eef_alt, N1 * sizeof(uint8_t), s)) return -1;
-    TnpLB lb;
-    if (lb_begin(e, lb_tiles(N), s, &lb, 0, false)) return -1;
-    // old edges: 8 B ids + 1 B high plane + 1 B first split plane read; e_new /
-    // c_new: 4 / 8 B ids + 32 B endpoint keys; kept edges: 10 B written + 2 B flags
-    TIMED("prune", 10.0 * E + 36.0 * S + 40.0 * X,
-          launch_prune_lb(eg, E, P<int32_t>(e->sb), S, V, e->ckeys, nb, X, idx, K - 1,
-                          P<uint64_t>(c.pz), P<uint8_t>(e->edm), P<uint8_t>(e->eef),
-                          P<int32_t>(e->edges_alt), P<uint8_t>(e->edm_alt), P<uint8_t>(e->eef_alt),
-                          P<uint8_t>(e->live), count_in_prune, ctr, lb, s));
-    std::swap(e->edm, e->edm_alt);
-    std::swap(e->eef, e->eef_alt);
-    if (!count_in_prune)
-      TIMED("count_live", 1.0 * NV, launch_count_flags(P<uint8_t>(e->live), NV, ctr, CTR_V, s));
+    if (lazy) {
+      // in place: the slots grow to N (kept contents), nothing is compacted
+      if (buf_ensure(e->edges, N1 * 2 * sizeof(int32_t), s, true)) return -1;
+      if (buf_ensure(e->edm, N1 * sizeof(uint8_t), s, true)) return -1;
+      if (buf_ensure(e->eef, N1 * sizeof(uint8_t), s, true)) return -1;
+      if (buf_ensure(e->lzpart, PRUNE_LAZY_MAX_BLOCKS * sizeof(int64_t), s)) return -1;
+      // old edges: 1 B high plane (+ 1 B first split plane, 8 B ids when
+      // kept); e_new / c_new: 4 / 8 B ids + 32 B endpoint keys, 10 B written
+      TIMED("prune", 1.0 * E + 36.0 * S + 40.0 * X,
+            launch_prune_lazy(P<int32_t>(e->edges), E, P<int32_t>(e->sb), S, V, e->ckeys, nb, X, idx, K - 1,
+                              P<uint64_t>(c.pz), P<uint8_t>(e->edm), P<uint8_t>(e->eef), P<uint8_t>(e->live),
+                              P<int64_t>(e->lzpart), ctr, s));
+      TIMED("count_live", 1.0 * NV,
+            launch_count_flags(P<uint8_t>(e->live), NV, ctr, CTR_V, s, P<int64_t>(e->lzpart),
+                               prune_lazy_blocks(N), CTR_E));
+      swap_edges = false;
+    } else {
+      if (buf_ensure(e->edges_alt, N1 * 2 * sizeof(int32_t), s)) return -1;
+      if (buf_ensure(e->edm_alt, N1 * sizeof(uint8_t), s)) return -1;
+      if (buf_ensure(e->eef_alt, N1 * sizeof(uint8_t), s)) return -1;
+      TnpLB lb;
+      if (lb_begin(e, lb_tiles(N), s, &lb, 0, false)) return -1;
+      // old edges: 8 B ids + 1 B high plane + 1 B first split plane read; e_new /
+      // c_new: 4 / 8 B ids + 32 B endpoint keys; kept edges: 10 B written + 2 B flags
+      TIMED("prune", 10.0 * E + 36.0 * S + 40.0 * X,
+            launch_prune_lb(eg, E, P<int32_t>(e->sb), S, V, e->ckeys, nb, X, idx, K - 1,
+                            P<uint64_t>(c.pz), P<uint8_t>(e->edm), P<uint8_t>(e->eef),
+                            P<int32_t>(e->edges_alt), P<uint8_t>(e->edm_alt), P<uint8_t>(e->eef_alt),
+                            P<uint8_t>(e->live), count_in_prune, ctr, lb, s));
+      std::swap(e->edm, e->edm_alt);
+      std::swap(e->eef, e->eef_alt);
+      if (!count_in_prune)
+        TIMED("count_live", 1.0 * NV, launch_count_flags(P<uint8_t>(e->live), NV, ctr, CTR_V, s));
+    }
     next_valid = e->keep_all ? 0 : std::min(idx + 1, K - 1);
     if (read_ctr(e, s)) return -1;
-    ktimer_set_bytes(e, "prune", 10.0 * E + 36.0 * S + 40.0 * X + 12.0 * e->h_ctr[CTR_E]);
-    E2 = e->h_ctr[CTR_E];
+    E2_live = e->h_ctr[CTR_E];
+    E2 = lazy ? N : E2_live;
+    ktimer_set_bytes(e, "prune", lazy ? 1.0 * E + 36.0 * S + 40.0 * X + 9.0 * E2_live
+                                      : 10.0 * E + 36.0 * S + 40.0 * X + 12.0 * E2_live);
     V2 = e->h_ctr[CTR_V];
     // the kept edges' first split planes are above idx now
     e->mask_from = idx + 1;
     e->act_bits = (uint64_t)e->h_ctr[CTR_ACTIVE];
     e->dirty = true;
+  } else if (E != E_live_in) {
+    // the last plane (no pruning) behind lazily deleted edges: the
+    // concatenation drops them (the compacting prune keeping every live edge)
+    const int64_t N1 = std::max<int64_t>(N, 1);
+    if (buf_ensure(e->edges_alt, N1 * 2 * sizeof(int32_t), s)) return -1;
+    if (buf_ensure(e->edm_alt, N1 * sizeof(uint8_t), s)) return -1;
+    if (buf_ensure(e->eef_alt, N1 * sizeof(uint8_t), s)) return -1;
+    TnpLB lb;
+    if (lb_begin(e, lb_tiles(N), s, &lb, 0, false)) return -1;
+    if (launch_prune_lb(eg, E, P<int32_t>(e->sb), S, V, e->ckeys, nb, X, -1, K - 1, P<uint64_t>(c.pz),
+                        P<uint8_t>(e->edm), P<uint8_t>(e->eef), P<int32_t>(e->edges_alt),
+                        P<uint8_t>(e->edm_alt), P<uint8_t>(e->eef_alt), P<uint8_t>(e->live), false, ctr, lb, s))
+      return -1;
+    std::swap(e->edm, e->edm_alt);
+    std::swap(e->eef, e->eef_alt);
+    if (set_alive(e, V, S, s)) return -1;
+    V2 = e->V_live + S;
+    e->masks_valid = false;
+    if (read_ctr(e, s)) return -1;
+    E2 = E2_live = e->h_ctr[CTR_E];
   } else {
+    if (buf_ensure(e->edges_alt, std::max<int64_t>(N, 1) * 2 * sizeof(int32_t), s)) return -1;
     if (launch_prune(true, eg, E, P<int32_t>(e->sb), S, V, e->ckeys, nb, X, idx, 0, K - 1, pos, zero, nullptr, nullptr,
                      P<int32_t>(e->edges_alt), nullptr, ctr, s))
       return -1;
@@ -1287,21 +1385,22 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     e->masks_valid = false;  // the concatenated edge list carries no masks
     if (read_ctr(e, s)) return -1;
   }
-  std::swap(e->edges, e->edges_alt);
+  if (swap_edges) std::swap(e->edges, e->edges_alt);
   const int64_t V_in_live = e->V_live;
   e->V = NV;  // slots
   e->V_live = V2;
   e->E = E2;
+  e->E_live = E2_live;
   e->valid_from = next_valid;
   if (st) {
     st->idx = idx;
     st->V_in = V_in_live;
-    st->E_in = E;
+    st->E_in = E_live_in;
     st->S = S;
     st->H = H;
     st->X = e->h_ctr[CTR_X];  // all connecting edges (X kept ones were appended)
     st->V_out = V2;
-    st->E_out = E2;
+    st->E_out = E2_live;
     st->A = e->h_ctr[CTR_A];
     st->P = e->h_ctr[CTR_P];
     st->pair_tests = e->h_ctr[CTR_TESTS] + e->h_ctr[CTR_SPAIRS];
@@ -1311,6 +1410,35 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     st->T = T;
   }
   e->valid = true;
+  return 0;
+}
+
+// the hyperplane loop of subpoly.py:58-69 on one device, in the library:
+// the same split / finish calls the Python driver makes per step, without a
+// host-language round trip per step (bunny-scale steps are tens of us)
+extern "C" int tnp_engine_run_steps(tnp_engine* e, void* stream, tnp_step_stats* stats, int max_stats,
+                                    int* n_steps) {
+  *n_steps = 0;
+  if (e->shards > 1) {
+    tnp_set_error("run_steps: a sharded engine takes its global decisions between split and finish");
+    return -1;
+  }
+  uint64_t mask = 0;
+  if (tnp_engine_active_planes(e, 0, &mask, stream)) return -1;
+  const int K = e->K;
+  for (int idx = 0; idx < K; ++idx) {
+    if (!((mask >> idx) & 1ull)) continue;
+    int64_t S = 0;
+    int32_t fail = 0;
+    if (tnp_engine_split(e, idx, stream, &S, &fail)) return -1;
+    if (S == 0) continue;
+    const int prune = idx < K - 1;  // the last plane never prunes
+    tnp_step_stats st{};
+    if (tnp_engine_finish(e, idx, prune, fail, stream, &st)) return -1;
+    if (*n_steps < max_stats) stats[*n_steps] = st;
+    ++*n_steps;
+    if (prune) mask = (mask & ((2ull << idx) - 1ull)) | st.next_active;
+  }
   return 0;
 }
 
@@ -1357,6 +1485,7 @@ extern "C" int tnp_engine_surface(tnp_engine* e, void* stream, int64_t* V_out, i
   if (e->h_ctr[CTR_AUX] < 3) {
     e->V = 0;
     e->E = 0;
+    e->E_live = 0;
     *V_out = 0;
     *E_out = 0;
     return reset_live(e, s);
@@ -1390,6 +1519,7 @@ extern "C" int tnp_engine_surface(tnp_engine* e, void* stream, int64_t* V_out, i
   std::swap(e->edges, e->edges_alt);
   e->V = V2;
   e->E = E2;
+  e->E_live = E2;
   *V_out = V2;
   *E_out = E2;
   return reset_live(e, s);
@@ -1447,6 +1577,8 @@ extern "C" int tnp_engine_lattice(tnp_engine* e, int x0, int x1, int keep_all, v
   const int N = e->net.n_marks;
   if (x0 < 0 || x1 >= N || x1 < x0) { tnp_set_error("bad slab [%d, %d] of %d marks", x0, x1, N); return -1; }
   const int nx = x1 - x0 + 1;
+  e->xs0 = x0;
+  e->xs1 = x1;
   const int64_t V = (int64_t)nx * N * N;
   const int64_t E = (int64_t)(nx - 1) * N * N + 2LL * nx * (N - 1) * N;
   if (V >= (1LL << 31) || E >= (1LL << 31)) { tnp_set_error("lattice too large for int32 ids"); return -1; }
@@ -1465,6 +1597,7 @@ extern "C" int tnp_engine_lattice(tnp_engine* e, int x0, int x1, int keep_all, v
                        P<uint64_t>(e->cur.pz)));
   e->V = V;
   e->E = E;
+  e->E_live = E;
   e->keep_all = keep_all;
   e->valid_from = 0;
   e->pend_idx = -1;
@@ -1507,6 +1640,7 @@ static int load_hypercube(tnp_engine* e, float size, hipStream_t s) {
   TNP_CHECK(hipStreamSynchronize(s));  // host vectors go out of scope
   e->V = 8;
   e->E = (int64_t)ed.size() / 2;
+  e->E_live = (int64_t)ed.size() / 2;
   return 0;
 }
 
@@ -1521,6 +1655,8 @@ extern "C" int tnp_engine_skeleton_mode(tnp_engine* e, int unit, float size, int
   if (!e->has_net) { tnp_set_error("engine has no net"); return -1; }
   if (unit < 2) { tnp_set_error("unit must be >= 2"); return -1; }
   TNP_CHECK(hipSetDevice(e->device));
+  e->xs0 = 0;  // the whole grid
+  e->xs1 = -1;
   const int L = e->net.n_marks;
   if ((int64_t)L * L * L >= (1LL << 31)) { tnp_set_error("too many marks for int32 ids"); return -1; }
   std::vector<float> mk(L);
@@ -1606,6 +1742,7 @@ extern "C" int tnp_engine_skeleton_mode(tnp_engine* e, int unit, float size, int
     std::swap(e->edges, e->edges_alt);
     e->V = V;
     e->E = total;
+    e->E_live = total;
   }
   if (launch_forward(e->net, P<float>(e->cur.xyz), e->V, P<float>(e->cur.pre), e->cur.cap, 1, s, nullptr,
                      P<uint64_t>(e->cur.pos), P<uint64_t>(e->cur.zero), P<uint64_t>(e->cur.grid),
@@ -1784,6 +1921,16 @@ extern "C" int tnp_engine_faces_export(tnp_engine* e, int64_t* d_tri, float* d_f
 extern "C" int tnp_engine_set_owned(tnp_engine* e, int lo, int hi) {
   e->own_lo = lo;
   e->own_hi = hi;
+  return 0;
+}
+
+extern "C" int tnp_engine_set_xspan(tnp_engine* e, int x0, int x1) {
+  if (x1 >= x0 && (x0 < 0 || (e->has_net && x1 >= e->net.n_marks))) {
+    tnp_set_error("bad x span [%d, %d]", x0, x1);
+    return -1;
+  }
+  e->xs0 = x0;
+  e->xs1 = x1;
   return 0;
 }
 

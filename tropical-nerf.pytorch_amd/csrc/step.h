@@ -57,7 +57,7 @@ int launch_split_lb(int32_t* edges, int64_t E, const uint8_t* ef, uint8_t* dm, i
 // splits the edge (EDGE_NOSPLIT: none); ctr != null: OR of those first
 // planes -> CTR_ACTIVE
 int launch_edge_masks(const int32_t* edges, int64_t E, const uint64_t* pz, uint8_t* dm,
-                      uint8_t* ef, int from, int last_plane, int64_t* ctr, hipStream_t s);
+                      uint8_t* sm, int from, int last_plane, bool keep_dead, int64_t* ctr, hipStream_t s);
 int launch_new_vertices(const int32_t* sa, const int32_t* sb, int64_t S, const float* col,
                         float eps, float* xyz, int64_t V, hipStream_t s);
 int launch_fail_check(const int32_t* sa, const int32_t* sb, int64_t S, int idx,
@@ -165,7 +165,20 @@ int launch_prune_lb(const int32_t* edges, int64_t E, const int32_t* sb, int64_t 
 // count_live: the distinct live endpoints are counted into ctr[CTR_V] on the
 // way (word atomics; for small complexes, instead of launch_count_flags)
 // ctr[slot] += number of set byte flags in f[0, n) (16-B aligned f, 0/1 bytes)
-int launch_count_flags(const uint8_t* f, int64_t n, int64_t* ctr, int slot, hipStream_t s);
+// part != null: also ctr[pslot] = sum of part[0, nparts) (the lazy prune's
+// per-workgroup kept counts)
+int launch_count_flags(const uint8_t* f, int64_t n, int64_t* ctr, int slot, hipStream_t s,
+                       const int64_t* part = nullptr, int nparts = 0, int pslot = 0);
+// lazy pruning of step idx over [edges; e_new; c_new] (N = E + S + X slots):
+// old edges stay in place (removed ones marked EDGE_DEAD, rewired ones get
+// their bytes), e_new / c_new written to slots E.. (edges, dm, ef need N
+// entries); used flags; per-workgroup kept counts -> part (fold them with
+// launch_count_flags), next-active planes -> ctr[CTR_ACTIVE]
+constexpr int PRUNE_LAZY_MAX_BLOCKS = 1024;
+int prune_lazy_blocks(int64_t N);
+int launch_prune_lazy(int32_t* edges, int64_t E, const int32_t* sb, int64_t S, int64_t V, const uint64_t* ckeys,
+                      int nb, int64_t X, int idx, int last_plane, const uint64_t* pz, uint8_t* dm, uint8_t* ef,
+                      uint8_t* used, int64_t* part, int64_t* ctr, hipStream_t s);
 // the counter block -> a host-mapped mirror, then the sequence word at [31]
 // (the host spins on it instead of a copy + stream synchronise)
 int launch_publish(const int64_t* ctr, int64_t* host, int64_t seq, hipStream_t s);
@@ -173,13 +186,28 @@ int launch_widen_flags(const uint8_t* f, int64_t n, int32_t* out, hipStream_t s)
 // planes the pruning of step idx compares (idx .. last_plane)
 uint64_t prune_mask(int idx, int last_plane);
 // ---- bucket.hip: members grouped by grid cell in spatial buckets ----------
-constexpr int BUCKET_MAX = 4913;        // buckets (17^3)
+constexpr int BUCKET_MAX = 6144;        // buckets (17^3 lattice; 5 x 33 x 33 slab)
 constexpr int BUCKET_LOCAL_MAX = 4096;  // cells per bucket (16^3)
-// bucket edge 2^sh cells, NBd buckets per axis, NB in total; -1: the grid is
-// too fine for the bucket path (the radix-sort path takes it)
-int bucket_geometry(int n_marks, int* sh, int* NBd, int* NB);
+// The buckets cover the cells (+2 coordinates) [0, NC) along y and z and
+// [xorg, xorg + xn) along x: an x-slab of a sharded complex buckets only its
+// own cells (an 8-rank 256^3 slab: 5 x 33 x 33 buckets of 8^3 cells instead
+// of 17^3 buckets of 16^3, 82 % of them empty)
+struct BucketGeom {
+  int NC;    // cell coordinates per axis (n_marks + 2)
+  int sh;    // log2 of the bucket edge in cells
+  int NBd;   // buckets along y and z
+  int NBx;   // buckets along x
+  int xorg;  // first cell coordinate along x
+  int xn;    // cells along x the buckets cover (NBx << sh)
+  int NB;    // NBx * NBd * NBd
+};
+// the smallest bucket edge (2^3 or 2^4 cells) whose bucket count fits
+// BUCKET_MAX for a complex inside the x mark planes [x0, x1]; -1: the grid
+// is too fine for the bucket path (the radix-sort path takes it)
+int bucket_geometry(int n_marks, int x0, int x1, BucketGeom* g);
 // members -> (local cell, vertex) entries in bucket ranges; A -> ctr[CTR_A],
-// T -> ctr[CTR_T], k=0 rows -> ctr[CTR_K0].  bcount/bcur: NB int32,
+// T -> ctr[CTR_T], k=0 rows -> ctr[CTR_K0] bit 0, a member outside the
+// geometry's x range -> bit 1 (skipped; the host raises).  bcount/bcur: NB int32,
 // bbase: NB + 1, part: ceil(M / 2048) + 1 int64; ekey/ev: 8 M capacity
 // ekv: the entries in bucket order, packed (local cell << 40 | cell flags
 // << 32 | vertex) (8 M capacity)
@@ -203,7 +231,7 @@ struct NewOverride {
 // of launch_bucket_entries needs max(this, 512) entries
 int64_t bucket_member_blocks(int64_t M);
 int launch_bucket_entries(const int32_t* members, int64_t S, int64_t V, int64_t M, const uint64_t* grid,
-                          const uint64_t* zero, int idx, int n_marks, int32_t* bcount, int32_t* bcur,
+                          const uint64_t* zero, int idx, const BucketGeom& g, int32_t* bcount, int32_t* bcur,
                           int64_t* bbase, int64_t* part, uint64_t* ekv, bool clean, uint8_t* live,
                           int64_t nlive, const NewOverride* ovr, int64_t* ctr, hipStream_t s);
 // per bucket: cell-contiguous CellEnt records (ents, entry positions), the
@@ -247,7 +275,7 @@ struct ConnectWin {
   int64_t cap;
   int64_t* xs;
 };
-int launch_bucket_pairs(int n_marks, const int64_t* bbase, const uint64_t* ekv, const uint64_t* pz,
+int launch_bucket_pairs(const BucketGeom& g, const int64_t* bbase, const uint64_t* ekv, const uint64_t* pz,
                         CellEnt* ents, int32_t* lcell,
                         int32_t* lent, int32_t* ln, int64_t* lpoff, int64_t* bnpc, int64_t* bnpairs,
                         int64_t* bspairs, int64_t* spoff, int64_t* pcoff, int64_t* pairoff,

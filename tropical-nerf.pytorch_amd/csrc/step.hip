@@ -40,6 +40,11 @@ __device__ __forceinline__ uint8_t high_plane(uint64_t dm) {
 // whose planes come from the new keys, so one byte per edge carries every
 // future split test (instead of the 64-bit mask of all its split planes)
 constexpr uint8_t EDGE_NOSPLIT = 0xFF;
+// lazily deleted edge (high-plane byte; its first split plane is
+// EDGE_NOSPLIT): the pruning of a step marks the edges it removes instead of
+// compacting the list (k_prune_lazy); every edge pass skips them and the
+// compacting passes drop them
+constexpr uint8_t EDGE_DEAD = 0xFE;
 __device__ __forceinline__ uint8_t first_plane(uint64_t m) {
   return (uint8_t)(m ? __builtin_ctzll(m) : EDGE_NOSPLIT);
 }
@@ -949,7 +954,7 @@ k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, int idx, uint64_t amask,
 #pragma unroll
   for (int k = 0; k < LIPT; ++k) {
     const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
-    const bool f = (i <= last) && ((int)d[k] > idx);
+    const bool f = (i <= last) && ((int)d[k] > idx) && d[k] != EDGE_DEAD;
     // (an old edge's first split plane is above idx: else it would have split)
     if (f && m[k] != EDGE_NOSPLIT) act |= 1ull << m[k];
     bal[k] = __ballot(f);
@@ -973,7 +978,7 @@ k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, int idx, uint64_t amask,
         const ulonglong2 ka = pz[ea], kb = pz[eb];
         dd = high_plane((ka.x ^ kb.x) | (ka.y ^ kb.y));
       }
-      c += (int)dd > idx;
+      c += (int)dd > idx && dd != EDGE_DEAD;
     }
     return tnp::wave_sum((int64_t)c);
   };
@@ -1028,17 +1033,112 @@ k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, int idx, uint64_t amask,
   }
 }
 
+// Lazy pruning (no compaction).  The old edges stay in their slots: a
+// removed one is marked EDGE_DEAD, a rewired one (EDGE_STALE) gets its
+// recomputed bytes, a kept one is not rewritten; e_new / c_new go behind
+// them to slots E + r (removed ones marked dead).  The live edges so keep
+// the order of the reference's `edges[p_idx]` (subpoly.py:246-263) with no
+// look-back and no rewrite of the kept edges: a step that splits few edges
+// but removes many costs one byte per old edge plus the kept edges' endpoint
+// reads (live flags).  Kept count per workgroup -> part[blockIdx.x] (folded
+// by the counting pass, launch_count_flags), next-active mask -> ctr.
+constexpr int LZ_IPT = 4;
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_prune_lazy(EdgeSrc src, int64_t N, int idx, uint64_t amask, const ulonglong2* __restrict__ pz,
+             int32_t* __restrict__ edges, uint8_t* __restrict__ dm, uint8_t* __restrict__ ef,
+             uint8_t* __restrict__ used, int64_t* __restrict__ part, int64_t* __restrict__ ctr) {
+  __shared__ int64_t lds[TNP_WAVES];
+  __shared__ uint64_t acts[TNP_WAVES];
+  int2* const e2 = reinterpret_cast<int2*>(edges);
+  const uint64_t lo_mask = (1ull << src.nb) - 1ull;
+  const int64_t ES = src.E + src.S;
+  int64_t kept = 0;
+  uint64_t act = 0;
+  for (int64_t t0 = (int64_t)blockIdx.x * TNP_BLOCK * LZ_IPT; t0 < N;
+       t0 += (int64_t)gridDim.x * TNP_BLOCK * LZ_IPT) {
+    uint32_t d[LZ_IPT], m[LZ_IPT];
+    int a[LZ_IPT], b[LZ_IPT];
+    bool need[LZ_IPT];  // endpoints needed (kept or stale old edge, or a new edge)
+#pragma unroll
+    for (int k = 0; k < LZ_IPT; ++k) {
+      const int64_t i = t0 + (int64_t)k * TNP_BLOCK + threadIdx.x;
+      d[k] = i < src.E ? dm[i] : (i < N ? EDGE_STALE : EDGE_DEAD);
+      m[k] = i < src.E ? ef[i] : EDGE_NOSPLIT;
+    }
+#pragma unroll
+    for (int k = 0; k < LZ_IPT; ++k) {
+      const int64_t i = t0 + (int64_t)k * TNP_BLOCK + threadIdx.x;
+      need[k] = d[k] == EDGE_STALE || (d[k] != EDGE_DEAD && (int)d[k] > idx);
+      a[k] = b[k] = 0;
+      if (!need[k]) continue;
+      if (i < src.E) {
+        const int2 ab = e2[i];
+        a[k] = ab.x;
+        b[k] = ab.y;
+      } else if (i < ES) {
+        a[k] = src.sb[i - src.E];
+        b[k] = (int)(src.V + (i - src.E));
+      } else {
+        const uint64_t key = src.ckeys[i - ES];
+        a[k] = (int)(key >> src.nb);
+        b[k] = (int)(key & lo_mask);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < LZ_IPT; ++k) {
+      const int64_t i = t0 + (int64_t)k * TNP_BLOCK + threadIdx.x;
+      if (i >= N) continue;
+      const bool stale = d[k] == EDGE_STALE;
+      if (stale) {  // rewired or new: bytes from the endpoint keys
+        const ulonglong2 ka = pz[a[k]], kb = pz[b[k]];
+        d[k] = high_plane((ka.x ^ kb.x) | (ka.y ^ kb.y));
+        m[k] = first_plane((ka.x ^ kb.x) & ~ka.y & ~kb.y & amask);
+      }
+      const bool keep = need[k] && (int)d[k] > idx;
+      if (i >= src.E) e2[i] = make_int2(a[k], b[k]);
+      if (i >= src.E || stale || (!keep && d[k] != EDGE_DEAD)) {
+        dm[i] = keep ? (uint8_t)d[k] : EDGE_DEAD;
+        ef[i] = keep ? (uint8_t)m[k] : EDGE_NOSPLIT;
+      }
+      if (keep) {
+        used[a[k]] = 1;
+        used[b[k]] = 1;
+        ++kept;
+        if (m[k] != EDGE_NOSPLIT) act |= 1ull << m[k];
+      }
+    }
+  }
+  kept = tnp::wave_sum(kept);
+  act = tnp::wave_or(act);
+  if (tnp::lane() == 0) {
+    lds[tnp::wave()] = kept;
+    acts[tnp::wave()] = act;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t k = 0;
+    uint64_t t = 0;
+    for (int w = 0; w < TNP_WAVES; ++w) {
+      k += lds[w];
+      t |= acts[w];
+    }
+    part[blockIdx.x] = k;
+    tnp::or_sticky(&ctr[CTR_ACTIVE], t);
+  }
+}
+
 // masks of every edge from the endpoint keys (after a load, or when the
 // curve path rewired edges); OR of the split masks on planes of amask into
 // ctr[CTR_ACTIVE] when ctr != null
 __global__ void __launch_bounds__(TNP_BLOCK)
 k_edge_masks(const int32_t* __restrict__ edges, int64_t E, const ulonglong2* __restrict__ pz,
              uint8_t* __restrict__ dm, uint8_t* __restrict__ ef, uint64_t amask,
-             int64_t* __restrict__ ctr) {
+             int keep_dead, int64_t* __restrict__ ctr) {
   __shared__ uint64_t lds[TNP_WAVES];
   uint64_t act = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < E;
        i += (int64_t)gridDim.x * blockDim.x) {
+    if (keep_dead && dm[i] == EDGE_DEAD) continue;  // stays deleted
     const int2 ab = reinterpret_cast<const int2*>(edges)[i];
     const ulonglong2 ka = pz[ab.x], kb = pz[ab.y];
     const uint8_t f = first_plane((ka.x ^ kb.x) & ~ka.y & ~kb.y & amask);
@@ -1059,8 +1159,22 @@ k_edge_masks(const int32_t* __restrict__ edges, int64_t E, const ulonglong2* __r
 
 // number of set byte flags -> ctr[slot] (+=, one atomic per block)
 __global__ void __launch_bounds__(TNP_BLOCK)
-k_count_flags(const uint8_t* __restrict__ f, int64_t n, int64_t* __restrict__ ctr, int slot) {
+k_count_flags(const uint8_t* __restrict__ f, int64_t n, int64_t* __restrict__ ctr, int slot,
+              const int64_t* __restrict__ part, int nparts, int pslot) {
   __shared__ int lds[TNP_WAVES];
+  __shared__ int64_t lds64[TNP_WAVES];
+  if (part && blockIdx.x == 0) {  // the lazy prune's per-workgroup kept counts
+    int64_t p = 0;
+    for (int i = threadIdx.x; i < nparts; i += TNP_BLOCK) p += part[i];
+    p = tnp::wave_sum(p);
+    if (tnp::lane() == 0) lds64[tnp::wave()] = p;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int64_t t = 0;
+      for (int w = 0; w < TNP_WAVES; ++w) t += lds64[w];
+      ctr[pslot] = t;
+    }
+  }
   int c = 0;
   const int64_t i0 = ((int64_t)blockIdx.x * TNP_BLOCK + threadIdx.x) * 16;
   const int64_t stride = (int64_t)gridDim.x * TNP_BLOCK * 16;
@@ -1353,6 +1467,23 @@ int launch_prune_lb(const int32_t* edges, int64_t E, const int32_t* sb, int64_t 
   TNP_CHECK(hipGetLastError());
   return 0;
 }
+int prune_lazy_blocks(int64_t N) {
+  return (int)std::max<int64_t>(1, std::min<int64_t>(PRUNE_LAZY_MAX_BLOCKS,
+                                                     (N + TNP_BLOCK * LZ_IPT - 1) / (TNP_BLOCK * LZ_IPT)));
+}
+int launch_prune_lazy(int32_t* edges, int64_t E, const int32_t* sb, int64_t S, int64_t V, const uint64_t* ckeys,
+                      int nb, int64_t X, int idx, int last_plane, const uint64_t* pz, uint8_t* dm, uint8_t* ef,
+                      uint8_t* used, int64_t* part, int64_t* ctr, hipStream_t s) {
+  EdgeSrc src{edges, E, sb, S, V, ckeys, nb, X};
+  const int64_t N = E + S + X;
+  uint64_t amask = (idx + 1 >= 64) ? 0ull : (~0ull << (idx + 1));
+  if (last_plane < 63) amask &= (1ull << (last_plane + 1)) - 1ull;
+  const int g = prune_lazy_blocks(N);
+  hipLaunchKernelGGL(k_prune_lazy, dim3(g), dim3(TNP_BLOCK), 0, s, src, N, idx, amask,
+                     reinterpret_cast<const ulonglong2*>(pz), edges, dm, ef, used, part, ctr);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
 int launch_widen_flags(const uint8_t* f, int64_t n, int32_t* out, hipStream_t s) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(k_widen_flags, dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, f, n, out);
@@ -1365,23 +1496,25 @@ int launch_publish(const int64_t* ctr, int64_t* host, int64_t seq, hipStream_t s
   return 0;
 }
 
-int launch_count_flags(const uint8_t* f, int64_t n, int64_t* ctr, int slot, hipStream_t s) {
-  if (n <= 0) return 0;
+int launch_count_flags(const uint8_t* f, int64_t n, int64_t* ctr, int slot, hipStream_t s,
+                       const int64_t* part, int nparts, int pslot) {
+  if (n <= 0 && !part) return 0;
   // one device-scope atomic per workgroup on one word: they serialise at
   // ~11 ns each (MI355X_MICROARCH.md fan-in), so few workgroups that loop
-  const unsigned g = (unsigned)std::min<int64_t>(256, (n + 16 * TNP_BLOCK - 1) / (16 * TNP_BLOCK));
-  hipLaunchKernelGGL(k_count_flags, dim3(g), dim3(TNP_BLOCK), 0, s, f, n, ctr, slot);
+  const unsigned g = (unsigned)std::max<int64_t>(
+      1, std::min<int64_t>(256, (n + 16 * TNP_BLOCK - 1) / (16 * TNP_BLOCK)));
+  hipLaunchKernelGGL(k_count_flags, dim3(g), dim3(TNP_BLOCK), 0, s, f, n, ctr, slot, part, nparts, pslot);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
 int launch_edge_masks(const int32_t* edges, int64_t E, const uint64_t* pz, uint8_t* dm,
-                      uint8_t* sm, int from, int last_plane, int64_t* ctr, hipStream_t s) {
+                      uint8_t* sm, int from, int last_plane, bool keep_dead, int64_t* ctr, hipStream_t s) {
   if (E <= 0) return 0;
   uint64_t amask = (from >= 64) ? 0ull : (~0ull << from);
   if (last_plane < 63) amask &= (1ull << (last_plane + 1)) - 1ull;
   const unsigned g = (unsigned)std::min<int64_t>(4096, tnp_grid(E));
   hipLaunchKernelGGL(k_edge_masks, dim3(g), dim3(TNP_BLOCK), 0, s, edges, E,
-                     reinterpret_cast<const ulonglong2*>(pz), dm, sm, amask, ctr);
+                     reinterpret_cast<const ulonglong2*>(pz), dm, sm, amask, keep_dead ? 1 : 0, ctr);
   TNP_CHECK(hipGetLastError());
   return 0;
 }

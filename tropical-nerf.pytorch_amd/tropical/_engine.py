@@ -28,6 +28,7 @@ class Engine:
             _hip.check(_hip.lib().tnp_engine_create(C.byref(h), idx), "tnp_engine_create")
         self.h = h
         self._keep = None
+        self._sharded = False
         self.K = None
         self._fin = weakref.finalize(self, _hip.lib().tnp_engine_destroy, h)
 
@@ -104,12 +105,20 @@ class Engine:
 
     def set_shards(self, world: int):
         _hip.check(_hip.lib().tnp_engine_set_shards(self.h, int(world)), "tnp_engine_set_shards")
+        self._sharded = int(world) > 1
         return self
 
     def set_owned(self, lo: int = 1, hi: int = 0):
         """This shard owns mark planes (lo, hi] and the cells between
         (lo > hi: everything); splits outside are reported as S_dup."""
         _hip.check(_hip.lib().tnp_engine_set_owned(self.h, int(lo), int(hi)), "tnp_engine_set_owned")
+
+    def set_xspan(self, x0: int = 0, x1: int = -1):
+        """The loaded complex lies between x mark planes x0 and x1 (a slab
+        with its halo; x1 < x0: anywhere): the step's spatial buckets cover
+        only those cells.  lattice() sets it, load()/skeleton() reset it."""
+        _hip.check(_hip.lib().tnp_engine_set_xspan(self.h, int(x0), int(x1)), "tnp_engine_set_xspan")
+        return self
 
     def kernel_timer(self, on: bool):
         """on=True: start HIP-event timing of every engine launch; on=False:
@@ -191,6 +200,15 @@ class Engine:
         if allreduce is not None and getattr(self, "curve", False):
             raise NotImplementedError("curve path (force=False) is single-device: the descent's "
                                       "stop criterion is global (subpoly_debug.py:141)")
+        if allreduce is None and not self._sharded:
+            # one device: the loop runs in the library (tnp_engine_run_steps)
+            buf = (_hip.TnpStepStats * max(self.K, 1))()
+            n = C.c_int32()
+            _hip.check(_hip.lib().tnp_engine_run_steps(self.h, self._s, buf, len(buf), C.byref(n)),
+                       "tnp_engine_run_steps")
+            if stats is not None:
+                stats.extend(buf[i].as_dict() for i in range(min(n.value, len(buf))))
+            return stats
         mask = self.active_planes(0)
         if allreduce is not None:
             mask = int(allreduce(np.array([mask], dtype=np.uint64), "or")[0])

@@ -82,6 +82,8 @@ SIGNATURES = {
     "tnp_engine_faces": (C.c_int, [_VP, _VP, _P64, _P64]),
     "tnp_engine_faces_export": (C.c_int, [_VP, _VP, _VP, _VP]),
     "tnp_engine_set_owned": (C.c_int, [_VP, C.c_int, C.c_int]),
+    "tnp_engine_set_xspan": (C.c_int, [_VP, C.c_int, C.c_int]),
+    "tnp_engine_run_steps": (C.c_int, [_VP, _VP, C.POINTER(TnpStepStats), C.c_int, _P32]),
     "tnp_engine_set_curve": (C.c_int, [_VP, C.c_int]),
     "tnp_engine_set_strict": (C.c_int, [_VP, C.c_int]),
     "tnp_engine_set_shards": (C.c_int, [_VP, C.c_int]),

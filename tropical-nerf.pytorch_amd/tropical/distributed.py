@@ -363,6 +363,7 @@ def subpoly_sharded(net, size: float = 1.2, group=None, allreduce=None, stats: l
         x0, x1 = slab_marks(cuts, rank, h)
         vs, es = slab_restrict(v, e, marks, x0, x1, net.eps)
         eng.load(vs, es)
+        eng.set_xspan(x0, x1)
         eng.set_owned(cuts[rank], cuts[rank + 1])
         st = []
         eng.run_steps(st, allreduce)

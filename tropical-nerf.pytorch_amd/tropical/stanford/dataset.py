@@ -10,6 +10,10 @@ from the (10x repeated) vertices plus uniform jitter of width 0.4
 (dataset.py:80-90).  The signed distances are the HIP kernel's
 (``mesh_signed_distance``, replacing cubvh); the samples stay on the host
 as in the reference.
+
+Attribution: the normalisation and the resampling rule restate
+seonghunn/tropical-nerf.pytorch (tropical/stanford/dataset.py:69-96),
+licensed CC BY-SA 4.0; the training distribution has to match it.
 """
 from __future__ import annotations
 

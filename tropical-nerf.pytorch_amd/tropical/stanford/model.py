@@ -93,11 +93,19 @@ class Net(nn.Module):
 
     # -- C ABI descriptor ----------------------------------------------------
     def tnp_desc(self):
-        """(tnp_net struct, keep-alive tensors) for the current parameters."""
+        """(tnp_net struct, keep-alive tensors) for the current parameters,
+        rebuilt only when a parameter changed (in-place updates bump its
+        version counter; a new tensor changes its storage)."""
         dev = self.device()
         if dev.type != "cuda":
             raise RuntimeError("Net: move the net to a ROCm GPU (.cuda()); the tropical HIP "
                                "path has no CPU fallback")
+        params = [self.enc.module.params] + [t for lin in self.fc for t in (lin.weight, lin.bias)]
+        sig = (self.num_layers, self.num_hidden, float(self.eps),
+               tuple((t.data_ptr(), t._version, t.dtype) for t in params), self.enc.marks.data_ptr())
+        cached = getattr(self, "_tnp_cache", None)
+        if cached is not None and cached[0] == sig:
+            return cached[1]
         s = _hip.TnpNet()
         self.enc.tnp_fields(s)
         s.num_layers, s.num_hidden, s.eps = self.num_layers, self.num_hidden, float(self.eps)
@@ -106,6 +114,7 @@ class Net(nn.Module):
                        for t in (lin.weight, lin.bias)]).contiguous()
         marks = self.enc.marks.to(dev).contiguous()
         s.d_table, s.d_weights, s.d_marks = table.data_ptr(), w.data_ptr(), marks.data_ptr()
+        self._tnp_cache = (sig, (s, (table, w, marks)))
         return s, (table, w, marks)
 
     # -- evaluation ----------------------------------------------------------
