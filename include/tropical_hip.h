@@ -218,6 +218,17 @@ int tnp_engine_set_strict(tnp_engine* eng, int on);
  * split once.  lo > hi (default) = everything owned.  Flat path only. */
 int tnp_engine_set_owned(tnp_engine* eng, int lo, int hi);
 
+/* subpoly(net, d, size, eps) / subpoly_(..., eps, ...) with eps != Net.eps
+ * (subpoly.py:24, 90): the following steps take the sign test, split point,
+ * hit vertices and failover predicate at `eps` (subpoly.py:98-117, 233;
+ * subpoly_debug.py:43), extract_skeleton and extract_faces too
+ * (subpoly.py:556-606), while the region keys of the pair tests and the
+ * pruning stay at Net.eps (Net.region without eps, subpoly.py:118, 184,
+ * 256).  In this mode every cached plane is kept (first split planes come
+ * from the plane values) and the pruning deletes edges lazily.  tnp_engine_set_net
+ * resets it to Net.eps. */
+int tnp_engine_set_eps(tnp_engine* eng, float eps);
+
 /* The loaded complex lies between the x mark planes x0 and x1 (an x-slab
  * with its halo): the step's spatial buckets then cover only those cells.
  * tnp_engine_lattice sets it, tnp_engine_load / _skeleton reset it to the

@@ -26,6 +26,11 @@ def cases(kind=None):
     return out
 
 
+def golden_eps(d) -> float:
+    """The eps argument the golden's subpoly calls used (make_golden.py EPS)."""
+    return float(d["eps"]) if "eps" in d else 1e-4
+
+
 def load(name: str) -> dict:
     with np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False) as z:
         d = {k: z[k] for k in z.files}

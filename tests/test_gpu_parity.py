@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 import torch
 
-from golden_io import cases, load, sha
+from golden_io import cases, golden_eps, load, sha
 from helpers import engine_steps, oracle_net, product_net
 
 pytestmark = pytest.mark.gpu
@@ -186,6 +186,7 @@ def test_subpoly_steps_bitwise(cuda, name):
     eng.skeleton(128, 1.2)
     v0, e0, _ = eng.export()
     eng.load(v0, e0, keep_all=True)
+    eng.set_eps(golden_eps(d))  # subpoly's eps argument (the eps goldens: != net.eps)
     got = engine_steps(eng)
     for i, (g, V, E, s) in enumerate(zip(got, d["step_V"], d["step_E"], d["step_sha"])):
         assert (g[0], g[1]) == (V, E), f"step {i}: V/E {g[:2]} != {(V, E)}"
@@ -195,12 +196,14 @@ def test_subpoly_steps_bitwise(cuda, name):
 
 @pytest.mark.parametrize("name", cases("subpoly"))
 def test_subpoly_dropin(cuda, name, capsys):
-    """The drop-in call surface: subpoly(net, 3, 1.2, force=True)."""
+    """The drop-in call surface: subpoly(net, 3, 1.2, eps, force=True) (eps:
+    the golden's argument -- Net's 1e-4, or another value for the eps
+    goldens, where the reference mixes the argument and Net.eps)."""
     import tropical.subpoly as sp
     d = load(name)
     net = product_net(d, cuda)
     stats = []
-    faces, verts, fwi = sp.subpoly(net, 3, 1.2, force=True, stats=stats)
+    faces, verts, fwi = sp.subpoly(net, 3, 1.2, golden_eps(d), force=True, stats=stats)
     out = capsys.readouterr().out
     assert "# of vertices and edges = " in out and " faces, " in out
     assert verts.shape[0] == int(d["n_surf"][0])
@@ -225,6 +228,38 @@ def test_subpoly_step_dropin(cuda):
         l, h = divmod(int(idx), net.num_hidden)
         V, E, o = sp.subpoly_(V, E, net, l, h, 1e-4, o, force=True)
         assert sha(V.cpu().numpy(), E.cpu().numpy(), o.cpu().numpy()) == str(d["step_sha"][step])
+
+
+@pytest.mark.parametrize("name", [n for n in ("small_sphere_eps3", "small_torus_eps05") if n in cases()])
+def test_subpoly_step_dropin_other_eps(cuda, name):
+    """subpoly_(..., eps, ...) one call at a time from the skeleton with eps
+    != net.eps (3e-4 / 5e-5 against Net's 1e-4): sign test, split point,
+    hits and failover at the argument, regions and pruning at net.eps --
+    every step's state hash equals the reference's, then extract_skeleton
+    and extract_faces at the argument give its surface and faces."""
+    import tropical.subpoly as sp
+    from tropical._engine import engine_for
+    d = load(name)
+    eps = golden_eps(d)
+    assert eps != 1e-4
+    net = product_net(d, cuda)
+    eng = engine_for(net)
+    eng.skeleton(128, 1.2)
+    V, E, _ = eng.export()
+    o = None
+    # subpoly.py:60-69: every (l, h), then the output plane (l = L-2, h = H)
+    calls = [(l, h) for l in range(net.num_layers - 1) for h in range(net.num_hidden)]
+    calls.append((net.num_layers - 2, net.num_hidden))
+    for step, (l, h) in enumerate(calls):
+        V, E, o = sp.subpoly_(V, E, net, l, h, eps, o, force=True)
+        assert sha(V.cpu().numpy(), E.cpu().numpy().astype(np.int64), o.cpu().numpy()) == \
+            str(d["step_sha"][step]), f"step {step}"
+    assert len(calls) == len(d["step_sha"])
+    Vs, Es, used = sp.extract_skeleton(V, E, net, eps, o)
+    assert sha(Vs.cpu().numpy()) == str(d["sha_surf"])
+    faces, fwi = sp.extract_faces(Vs, Es, net, o[used], eps)
+    assert sha(np.asarray(fwi, dtype=np.int64)) == str(d["sha_tri"])
+    assert sha(np.asarray(faces, dtype=np.float32)) == str(d["sha_faces"])
 
 
 def test_tied_levels_layout(cuda, monkeypatch):

@@ -30,6 +30,7 @@
 // gather + 32 B record write, against ~70 B for three 8-bit radix passes.
 #include <algorithm>
 #include <cstdlib>
+#include <cstdio>
 
 #include "common.h"
 #include "step.h"
@@ -55,6 +56,23 @@ __device__ __forceinline__ int member_of(const int32_t* members, int64_t S, int6
 }
 
 using BGeom = BucketGeom;
+
+// TNP_BG_PHASES=1 (diagnostic builds, tools/build_variant.sh): per-phase
+// shader-clock totals of k_bucket_group, printed per launch to stderr
+#ifndef TNP_BG_PHASES
+#define TNP_BG_PHASES 0
+#endif
+#if TNP_BG_PHASES
+__device__ unsigned long long g_bg_ph[8 * 8];
+#define BG_PH(k) \
+  do {           \
+    if (threadIdx.x == 0) tph[k] = __builtin_readcyclecounter(); \
+  } while (0)
+#else
+#define BG_PH(k) \
+  do {           \
+  } while (0)
+#endif
 
 // the window pass the grouping kernel runs over each bucket (keys == null:
 // none; the engine then launches k_connect_win)
@@ -410,7 +428,9 @@ __device__ __forceinline__ void group_bucket(const BGeom& G, int b, int64_t base
                                              int32_t* __restrict__ ln, int64_t* __restrict__ lpoff,
                                              int64_t* __restrict__ bnpc, int64_t* __restrict__ bnpairs,
                                              int64_t* __restrict__ bspairs, int64_t* __restrict__ ctr,
-                                             int* cnt, int* cur, int64_t* lds, int64_t* lds3) {
+                                             int* cnt, int* cur, int64_t* lds, int64_t* lds3,
+                                             unsigned long long* tph) {
+  (void)tph;
   constexpr int LC = 1 << (3 * SH);
   for (int i = threadIdx.x; i < LC; i += TNP_BLOCK) cnt[i] = 0;
   __syncthreads();
@@ -427,6 +447,7 @@ __device__ __forceinline__ void group_bucket(const BGeom& G, int b, int64_t base
       if (w[k] != ~0ull) atomicAdd(&cnt[(int)(w[k] >> 40)], 1);
   }
   __syncthreads();
+  BG_PH(1);
   // exclusive scan of cnt into cur (contiguous chunk per thread)
   constexpr int per = LC / TNP_BLOCK > 0 ? LC / TNP_BLOCK : 1;
   const int c0 = threadIdx.x * per;
@@ -439,6 +460,7 @@ __device__ __forceinline__ void group_bucket(const BGeom& G, int b, int64_t base
     run += cnt[i];
   }
   __syncthreads();
+  BG_PH(2);
   // records, cell-contiguous: the member keys gathered here (the members of
   // one bucket are spatially close: their slots cluster)
   for (int64_t e0 = 0; e0 < n; e0 += TNP_BLOCK * GIPT) {
@@ -472,6 +494,7 @@ __device__ __forceinline__ void group_bucket(const BGeom& G, int b, int64_t base
     }
   }
   __syncthreads();
+  BG_PH(3);
   // pair cells above WCELL members in local-cell order (cur[i] now = end
   // of cell i); the pairs of the smaller cells are the window pass's
   int npc = 0;
@@ -639,8 +662,11 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
       ents[base] = r;
     }
   } else {
+    unsigned long long tph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    BG_PH(0);
     group_bucket<SH>(G, b, base, n, ekv, pz, ents, lcell, lent, ln, lpoff, bnpc, bnpairs, bspairs, ctr, cnt,
-                     cur, lds, lds3);
+                     cur, lds, lds3, tph);
+    BG_PH(4);
     if (wa.keys) {
       // the window pass over this bucket's records, right behind their
       // stores (the workgroup's own stores: visible after the barrier)
@@ -654,15 +680,24 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
           if (tnp::lane() == 0) nwin_s = nw;
         }
         __syncthreads();
+        BG_PH(5);
         window_pass_packed(ents, base, reinterpret_cast<const uint32_t*>(cnt), nwin_s, tnp::wave(), TNP_WAVES,
                            below, wa.nb, wa.fmask, wa.keys, wa.cap, wa.xs, ctr, W, a);
       } else {
         window_pass(ents, base, base + n, tnp::wave(), TNP_WAVES, below, wa.nb, wa.fmask, wa.keys, wa.cap,
                     wa.xs, ctr, W, a);
       }
+      BG_PH(6);
       window_flush(wa.keys, wa.cap, wa.xs, ctr, W, a);
       add_pair_stats(a.n_compat, a.n_reg, a.n_conn, lds, wa.xs, ctr);
+      BG_PH(7);
     }
+#if TNP_BG_PHASES
+    if (threadIdx.x == 0)
+      for (int k = 0; k < 7; ++k)
+        if (tph[k + 1] > tph[k] && tph[k])
+          atomicAdd(&g_bg_ph[k * 8 + (blockIdx.x & 7)], tph[k + 1] - tph[k]);
+#endif
   }
   if (!fuse || !tnp::last_block(&ctr[CTR_TK1], &last)) return;
   // every bucket's pair-cell / pair totals -> global offsets (k_pair_gather)
@@ -794,6 +829,20 @@ int launch_bucket_pairs(const BucketGeom& G, const int64_t* bbase, const uint64_
     hipLaunchKernelGGL(k_bucket_group<4>, dim3(NB), dim3(TNP_BLOCK), 0, s, G, bbase, ekv,
                        reinterpret_cast<const ulonglong2*>(pz), ents, lcell, lent, ln, lpoff, bnpc, bnpairs,
                        bspairs, pcoff, pairoff, spoff, fuse, wa, pl, ctr);
+#if TNP_BG_PHASES
+  {
+    unsigned long long h[64];
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_bg_ph), sizeof(h));
+    unsigned long long t[7] = {0, 0, 0, 0, 0, 0, 0};
+    for (int k = 0; k < 7; ++k)
+      for (int x = 0; x < 8; ++x) t[k] += h[k * 8 + x];
+    fprintf(stderr, "bg_phases count %llu scan %llu records %llu paircells %llu windows %llu pass %llu flush %llu\n",
+            t[0], t[1], t[2], t[3], t[4], t[5], t[6]);
+    for (auto& v : h) v = 0;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_bg_ph), h, sizeof(h));
+  }
+#endif
   if (!fuse)
     hipLaunchKernelGGL(k_scan_sets, dim3(1, 3), dim3(TNP_BLOCK), 0, s, ScanSet{bnpc, 1, pcoff, CTR_R},
                        ScanSet{bnpairs, 1, pairoff, CTR_TESTS}, ScanSet{bspairs, 1, spoff, CTR_SPAIRS}, NB,

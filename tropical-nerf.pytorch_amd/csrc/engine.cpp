@@ -146,6 +146,7 @@ struct tnp_engine {
   // splits the edge (EDGE_NOSPLIT: none); valid when masks_valid
   Buf edm, eef, edm_alt, eef_alt;
   Buf lzpart;  // the lazy prune's per-workgroup kept counts
+  Buf kse[3];  // split-eps faces: pos / zero / grid keys at subpoly's eps
   Buf xs;                // per-XCD shards of the connect phase (step.h XS_*)
   bool xs_clean = false;
   bool masks_valid = false;
@@ -370,6 +371,9 @@ static int reset_live(tnp_engine* e, hipStream_t s, bool edges_changed = true) {
   return set_alive(e, 0, e->V, s);
 }
 
+// split-eps mode: subpoly's eps argument differs from Net.eps (tnp_engine_set_eps)
+static bool eps2(const tnp_engine* e) { return e->net.eps_s != e->net.eps; }
+
 // per-edge high plane and first split plane (>= from) from the endpoint
 // keys; ctr != null: the OR of the first split planes -> ctr[CTR_ACTIVE]
 static int compute_masks(tnp_engine* e, int from, int64_t* ctr, hipStream_t s) {
@@ -379,6 +383,18 @@ static int compute_masks(tnp_engine* e, int from, int64_t* ctr, hipStream_t s) {
   TIMED("edge_masks", 42.0 * e->E,
         launch_edge_masks(P<int32_t>(e->edges), e->E, P<uint64_t>(e->cur.pz), P<uint8_t>(e->edm),
                           P<uint8_t>(e->eef), from, e->K - 1, e->E != e->E_live, ctr, s));
+  if (eps2(e)) {
+    // first split planes at subpoly's eps from the cached planes (the mode
+    // keeps them all): they replace the Net.eps ones and their OR
+    if (e->valid_from > from) {
+      tnp_set_error("split-eps masks from plane %d: planes below %d were dropped", from, e->valid_from);
+      return -1;
+    }
+    if (ctr) TNP_CHECK(hipMemsetAsync(ctr + CTR_ACTIVE, 0, sizeof(int64_t), s));
+    TIMED("edge_masks", 8.0 * e->E,
+          launch_ef_cache(P<int32_t>(e->edges), e->E, P<uint8_t>(e->edm), P<uint8_t>(e->eef),
+                          P<float>(e->cur.pre), e->cur.cap, from, e->K, e->net.eps_s, ctr, s));
+  }
   e->masks_valid = true;
   e->mask_from = from;
   return 0;
@@ -504,7 +520,7 @@ extern "C" void tnp_engine_destroy(tnp_engine* e) {
                  &e->ent_v, &e->ents, &e->pcell, &e->ptoff, &e->bcell,
                  &e->ckeys_a, &e->ckeys_b, &e->sort_scr, &e->flags, &e->used, &e->nid,
                  &e->ctr, &e->tri, &e->faces, &e->lb[0], &e->lb[1], &e->edm, &e->eef,
-                 &e->edm_alt, &e->eef_alt, &e->live, &e->tied_table, &e->xs, &e->lbrc, &e->lzpart};
+                 &e->edm_alt, &e->eef_alt, &e->live, &e->tied_table, &e->xs, &e->lbrc, &e->lzpart, &e->kse[0], &e->kse[1], &e->kse[2]};
   for (Buf* b : bufs) buf_free(*b, s);
   for (Buf& b : e->fscr) buf_free(b, s);
   for (Buf& b : e->fscr2) buf_free(b, s);
@@ -536,6 +552,7 @@ static NetDev to_dev(const tnp_net* n) {
   d.num_hidden = n->num_hidden;
   d.n_marks = n->n_marks;
   d.eps = n->eps;
+  d.eps_s = n->eps;
   return d;
 }
 
@@ -709,7 +726,7 @@ extern "C" int tnp_engine_active_planes(tnp_engine* e, int from, uint64_t* mask,
 // gradient-descent fallback; leaves per-split strict-filter inputs in cinfo.
 // ---------------------------------------------------------------------------
 static int curve_correct(tnp_engine* e, int idx, int64_t S, hipStream_t s) {
-  const float eps = e->net.eps;
+  const float eps = e->net.eps_s;  // subpoly_'s eps (subpoly.py:120-177)
   const int K = e->K;
   Buf* cv = e->cv;
   int64_t* ctr = P<int64_t>(e->ctr);
@@ -810,7 +827,7 @@ static int curve_filter(tnp_engine* e, int idx, int override_, hipStream_t s, in
   if (buf_ensure(cv[CV_KEEP], S * sizeof(int32_t), s)) return -1;
   if (buf_ensure(cv[CV_NID], S * sizeof(int64_t), s)) return -1;
   if (launch_strict_keep(S, P<int32_t>(cv[CV_CINFO]), P<float>(e->stage), idx, override_,
-                         P<uint64_t>(e->shared), e->net.eps, e->pend_tight, e->strict, P<int32_t>(cv[CV_KEEP]), s))
+                         P<uint64_t>(e->shared), e->net.eps_s, e->pend_tight, e->strict, P<int32_t>(cv[CV_KEEP]), s))
     return -1;
   if (scan_counts(e, P<int32_t>(cv[CV_KEEP]), P<int64_t>(cv[CV_NID]), S, CTR_KEEP, s)) return -1;
   if (read_ctr(e, s)) return -1;
@@ -881,7 +898,7 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
   }
   if (require_valid(e, "split")) return -1;
   e->valid = false;  // until this split has completed
-  const float eps = e->net.eps;
+  const float eps = e->net.eps_s;  // subpoly_'s eps: hits, split point, failover
   const float* col = P<float>(e->cur.pre) + (int64_t)idx * e->cur.cap;
   TNP_CHECK(hipMemsetAsync(e->ctr.p, 0, CTR_N * sizeof(int64_t), s));
   int64_t S = 0;
@@ -1038,7 +1055,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     if (!buckets && launch_new_members(P<int32_t>(e->members), S, V, s)) return -1;
   } else {
     TIMED("hits", 5.0 * V + 4.0 * S,
-          launch_hits(col, P<uint8_t>(e->live), V, eps, P<int32_t>(e->members), S, ctr, s));
+          launch_hits(col, P<uint8_t>(e->live), V, e->net.eps_s, P<int32_t>(e->members), S, ctr, s));
   }
 
   // 3. bucket members by grid cell (dense cell grid over the marks): one
@@ -1297,7 +1314,9 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   int next_valid = e->valid_from;
   // lazy edge deletion (k_prune_lazy) unless the list is mostly dead edges
   // already: then the compacting prune drops them (and this step's)
-  const bool lazy = prune && e->lazy_edges && (E - E_live_in) <= E_live_in;
+  // (split-eps mode: always lazy -- its first split planes are recomputed
+  // over the edge slots in place, k_ef_cache)
+  const bool lazy = prune && (eps2(e) || (e->lazy_edges && (E - E_live_in) <= E_live_in));
   bool swap_edges = true;
   if (prune) {
     // live flags recomputed from the kept edges; no vertex moves (lazy
@@ -1322,6 +1341,12 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
             launch_prune_lazy(P<int32_t>(e->edges), E, P<int32_t>(e->sb), S, V, e->ckeys, nb, X, idx, K - 1,
                               P<uint64_t>(c.pz), P<uint8_t>(e->edm), P<uint8_t>(e->eef), P<uint8_t>(e->live),
                               P<int64_t>(e->lzpart), ctr, s));
+      if (eps2(e)) {  // the first split planes at subpoly's eps, and their OR
+        TNP_CHECK(hipMemsetAsync(ctr + CTR_ACTIVE, 0, sizeof(int64_t), s));
+        TIMED("edge_masks", 8.0 * N,
+              launch_ef_cache(P<int32_t>(e->edges), N, P<uint8_t>(e->edm), P<uint8_t>(e->eef), P<float>(c.pre),
+                              c.cap, idx + 1, K, e->net.eps_s, ctr, s));
+      }
       TIMED("count_live", 1.0 * NV,
             launch_count_flags(P<uint8_t>(e->live), NV, ctr, CTR_V, s, P<int64_t>(e->lzpart),
                                prune_lazy_blocks(N), CTR_E));
@@ -1344,7 +1369,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
       if (!count_in_prune)
         TIMED("count_live", 1.0 * NV, launch_count_flags(P<uint8_t>(e->live), NV, ctr, CTR_V, s));
     }
-    next_valid = e->keep_all ? 0 : std::min(idx + 1, K - 1);
+    next_valid = (e->keep_all || eps2(e)) ? 0 : std::min(idx + 1, K - 1);
     if (read_ctr(e, s)) return -1;
     E2_live = e->h_ctr[CTR_E];
     E2 = lazy ? N : E2_live;
@@ -1362,6 +1387,8 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     if (buf_ensure(e->edges_alt, N1 * 2 * sizeof(int32_t), s)) return -1;
     if (buf_ensure(e->edm_alt, N1 * sizeof(uint8_t), s)) return -1;
     if (buf_ensure(e->eef_alt, N1 * sizeof(uint8_t), s)) return -1;
+    // (the live flags grow to the new slots first: the pass marks endpoints)
+    if (set_alive(e, V, S, s)) return -1;
     TnpLB lb;
     if (lb_begin(e, lb_tiles(N), s, &lb, 0, false)) return -1;
     if (launch_prune_lb(eg, E, P<int32_t>(e->sb), S, V, e->ckeys, nb, X, -1, K - 1, P<uint64_t>(c.pz),
@@ -1370,7 +1397,6 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
       return -1;
     std::swap(e->edm, e->edm_alt);
     std::swap(e->eef, e->eef_alt);
-    if (set_alive(e, V, S, s)) return -1;
     V2 = e->V_live + S;
     e->masks_valid = false;
     if (read_ctr(e, s)) return -1;
@@ -1479,7 +1505,7 @@ extern "C" int tnp_engine_surface(tnp_engine* e, void* stream, int64_t* V_out, i
   if (buf_ensure(e->nid, std::max<int64_t>(V, 1) * sizeof(int64_t), s)) return -1;
   TNP_CHECK(hipMemsetAsync(e->ctr.p, 0, CTR_N * sizeof(int64_t), s));
   int32_t* on = P<int32_t>(e->flags);
-  if (launch_surface_flags(P<float>(c.xyz), col, V, e->net.eps, on, s)) return -1;
+  if (launch_surface_flags(P<float>(c.xyz), col, V, e->net.eps_s, on, s)) return -1;
   if (scan_counts(e, on, P<int64_t>(e->nid), V, CTR_AUX, s)) return -1;
   if (read_ctr(e, s)) return -1;
   if (e->h_ctr[CTR_AUX] < 3) {
@@ -1785,6 +1811,21 @@ extern "C" int tnp_engine_faces(tnp_engine* e, void* stream, int64_t* n_tri, int
   const uint64_t* zero = P<uint64_t>(e->cur.zero);
   const uint64_t* grid = P<uint64_t>(e->cur.grid);
   const float* xyz = P<float>(e->cur.xyz);
+  if (eps2(e)) {
+    // extract_faces takes the regions at subpoly's eps (net.region(vertices,
+    // outputs, eps), subpoly.py:606): keys of every plane from the cache
+    if (e->valid_from != 0) { tnp_set_error("split-eps faces: cached planes were dropped"); return -1; }
+    for (int k = 0; k < 3; ++k)
+      if (buf_ensure(e->kse[k], V * sizeof(uint64_t), s)) return -1;
+    NetDev ns = e->net;
+    ns.eps = ns.eps_s;
+    if (launch_keys(ns, xyz, P<float>(e->cur.pre), e->cur.cap, V, K, P<uint64_t>(e->kse[0]),
+                    P<uint64_t>(e->kse[1]), P<uint64_t>(e->kse[2]), s))
+      return -1;
+    pos = P<uint64_t>(e->kse[0]);
+    zero = P<uint64_t>(e->kse[1]);
+    grid = P<uint64_t>(e->kse[2]);
+  }
   TNP_CHECK(hipMemsetAsync(ctr, 0, CTR_N * sizeof(int64_t), s));
   // F1: augmented-row count and region hash table
   if (launch_face_count(V, grid, pos, zero, pmask, ctr + CTR_AUX - 1, s)) return -1;
@@ -1921,6 +1962,16 @@ extern "C" int tnp_engine_faces_export(tnp_engine* e, int64_t* d_tri, float* d_f
 extern "C" int tnp_engine_set_owned(tnp_engine* e, int lo, int hi) {
   e->own_lo = lo;
   e->own_hi = hi;
+  return 0;
+}
+
+extern "C" int tnp_engine_set_eps(tnp_engine* e, float eps) {
+  if (!e->has_net) { tnp_set_error("engine has no net"); return -1; }
+  if (!(eps > 0.f)) { tnp_set_error("eps must be positive (got %g)", (double)eps); return -1; }
+  if (eps != e->net.eps_s) {
+    e->net.eps_s = eps;
+    e->masks_valid = false;  // first split planes at the new eps
+  }
   return 0;
 }
 

@@ -21,6 +21,10 @@ struct NetDev {
   const float* marks;
   int32_t n_levels, num_layers, num_hidden, n_marks;
   float eps;
+  // the eps argument of subpoly / subpoly_ (subpoly.py:24, 90): the steps'
+  // sign test, split point and failover predicate use it, Net.region (the
+  // keys) uses eps; equal unless tnp_engine_set_eps says otherwise
+  float eps_s;
   // 1: every level has the same scale/res/size/dense, so one set of corner
   // weights and hash indices serves all levels, and `table` is the engine's
   // level-interleaved copy: entry idx of level l at float2 (idx * L + l) --

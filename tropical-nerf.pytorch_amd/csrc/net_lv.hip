@@ -127,7 +127,8 @@ k_forward_new(NetDev net, const float* xyz, int64_t n, float* __restrict__ pre,
   // the hash-table lines one XCD's splits touch then mostly fit its L2
   const int64_t i = tnp::xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   const bool live = i < n;
-  const float eps = net.eps;
+  const float eps = net.eps;      // Net.region: the keys
+  const float eps_s = net.eps_s;  // subpoly_'s eps: split point, failover
   float x[3] = {0.f, 0.f, 0.f};
   uint64_t m = 0;
   if (live) {
@@ -146,7 +147,7 @@ k_forward_new(NetDev net, const float* xyz, int64_t n, float* __restrict__ pre,
         ea[d] = base[3 * (int64_t)a + d];
         eb[d] = base[3 * (int64_t)b + d];
       }
-      const float d0 = __fdiv_rn(c0, eps), d1 = __fdiv_rn(c1, eps);
+      const float d0 = __fdiv_rn(c0, eps_s), d1 = __fdiv_rn(c1, eps_s);
       const float w = __fdiv_rn(fabsf(d0), fabsf(__fsub_rn(d1, d0)));
       const float om = __fsub_rn(1.0f, w);
       float* out = const_cast<float*>(xyz) + 3 * i;
@@ -186,7 +187,7 @@ k_forward_new(NetDev net, const float* xyz, int64_t n, float* __restrict__ pre,
       if (live && p + j >= keep_from) col[(int64_t)(p + j) * ld] = v;
       ps |= (uint64_t)(v > eps) << (p + j);
       zs |= (uint64_t)(fabsf(v) <= eps) << (p + j);
-      bad |= ((m >> (p + j)) & 1) && fabsf(v) > eps;
+      bad |= ((m >> (p + j)) & 1) && fabsf(v) > eps_s;
       h[j] = fmaxf(v, 0.0f);
     }
     p += H;
@@ -198,7 +199,7 @@ k_forward_new(NetDev net, const float* xyz, int64_t n, float* __restrict__ pre,
     if (p >= keep_from) col[(int64_t)p * ld] = v;
     ps |= (uint64_t)(v > eps) << p;
     zs |= (uint64_t)(fabsf(v) <= eps) << p;
-    bad |= ((m >> p) & 1) && fabsf(v) > eps;
+    bad |= ((m >> p) & 1) && fabsf(v) > eps_s;
     pos[V + i] = ps;
     zero[V + i] = zs;
     pz[V + i] = make_ulonglong2(ps, zs);

@@ -174,6 +174,11 @@ int launch_count_flags(const uint8_t* f, int64_t n, int64_t* ctr, int slot, hipS
 // their bytes), e_new / c_new written to slots E.. (edges, dm, ef need N
 // entries); used flags; per-workgroup kept counts -> part (fold them with
 // launch_count_flags), next-active planes -> ctr[CTR_ACTIVE]
+// split-eps mode: first split planes >= from of the live edges at eps_s from
+// the cached planes (pre plane-major, leading dimension ld, every plane
+// cached); OR -> ctr[CTR_ACTIVE] when ctr != null
+int launch_ef_cache(const int32_t* edges, int64_t E, const uint8_t* dm, uint8_t* ef, const float* pre, int64_t ld,
+                    int from, int K, float eps_s, int64_t* ctr, hipStream_t s);
 constexpr int PRUNE_LAZY_MAX_BLOCKS = 1024;
 int prune_lazy_blocks(int64_t N);
 int launch_prune_lazy(int32_t* edges, int64_t E, const int32_t* sb, int64_t S, int64_t V, const uint64_t* ckeys,

@@ -1127,6 +1127,43 @@ k_prune_lazy(EdgeSrc src, int64_t N, int idx, uint64_t amask, const ulonglong2* 
   }
 }
 
+// Split-eps mode (subpoly's eps argument != Net.eps, subpoly.py:24): the
+// first split plane >= from of every live edge at the step's eps -- the
+// sign test of subpoly.py:104-105 on the cached plane values of both
+// endpoints (the mode keeps every plane cached) -- instead of the one the
+// Net.eps keys give; OR of them -> ctr[CTR_ACTIVE] when ctr != null
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_ef_cache(const int32_t* __restrict__ edges, int64_t E, const uint8_t* __restrict__ dm,
+           uint8_t* __restrict__ ef, const float* __restrict__ pre, int64_t ld, int from, int K,
+           float eps_s, int64_t* __restrict__ ctr) {
+  __shared__ uint64_t lds[TNP_WAVES];
+  uint64_t act = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < E;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    if (dm[i] == EDGE_DEAD) continue;
+    const int2 ab = reinterpret_cast<const int2*>(edges)[i];
+    uint8_t f = EDGE_NOSPLIT;
+    for (int p = from; p < K; ++p) {
+      const float d0 = pre[(int64_t)p * ld + ab.x], d1 = pre[(int64_t)p * ld + ab.y];
+      if ((__fmul_rn(d0, d1) < 0.f) && (fabsf(d0) > eps_s) && (fabsf(d1) > eps_s)) {
+        f = (uint8_t)p;
+        break;
+      }
+    }
+    ef[i] = f;
+    if (f != EDGE_NOSPLIT) act |= 1ull << f;
+  }
+  if (!ctr) return;
+  act = tnp::wave_or(act);
+  if (tnp::lane() == 0) lds[tnp::wave()] = act;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t t = 0;
+    for (int w = 0; w < TNP_WAVES; ++w) t |= lds[w];
+    tnp::or_sticky(&ctr[CTR_ACTIVE], t);
+  }
+}
+
 // masks of every edge from the endpoint keys (after a load, or when the
 // curve path rewired edges); OR of the split masks on planes of amask into
 // ctr[CTR_ACTIVE] when ctr != null
@@ -1481,6 +1518,14 @@ int launch_prune_lazy(int32_t* edges, int64_t E, const int32_t* sb, int64_t S, i
   const int g = prune_lazy_blocks(N);
   hipLaunchKernelGGL(k_prune_lazy, dim3(g), dim3(TNP_BLOCK), 0, s, src, N, idx, amask,
                      reinterpret_cast<const ulonglong2*>(pz), edges, dm, ef, used, part, ctr);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_ef_cache(const int32_t* edges, int64_t E, const uint8_t* dm, uint8_t* ef, const float* pre, int64_t ld,
+                    int from, int K, float eps_s, int64_t* ctr, hipStream_t s) {
+  if (E <= 0) return 0;
+  const unsigned g = (unsigned)std::min<int64_t>(4096, tnp_grid(E));
+  hipLaunchKernelGGL(k_ef_cache, dim3(g), dim3(TNP_BLOCK), 0, s, edges, E, dm, ef, pre, ld, from, K, eps_s, ctr);
   TNP_CHECK(hipGetLastError());
   return 0;
 }

@@ -40,6 +40,7 @@ class Engine:
         s, keep = net.tnp_desc()
         self._keep = (s, keep)  # the engine reads these device buffers later
         self.K = net.K
+        self.net_eps = float(net.eps)
         self.num_hidden = net.num_hidden
         self.num_layers = net.num_layers
         _hip.check(_hip.lib().tnp_engine_set_net(self.h, C.byref(s)), "tnp_engine_set_net")
@@ -112,6 +113,14 @@ class Engine:
         """This shard owns mark planes (lo, hi] and the cells between
         (lo > hi: everything); splits outside are reported as S_dup."""
         _hip.check(_hip.lib().tnp_engine_set_owned(self.h, int(lo), int(hi)), "tnp_engine_set_owned")
+
+    def set_eps(self, eps: float = None):
+        """subpoly's eps argument (None: Net.eps): the steps' sign test, split
+        point, hits and failover, the surface and the faces take it; the
+        region keys stay at Net.eps (subpoly.py:24, 90, 556-606)."""
+        e = self.net_eps if eps is None else float(eps)
+        _hip.check(_hip.lib().tnp_engine_set_eps(self.h, C.c_float(e)), "tnp_engine_set_eps")
+        return self
 
     def set_xspan(self, x0: int = 0, x1: int = -1):
         """The loaded complex lies between x mark planes x0 and x1 (a slab
@@ -204,10 +213,10 @@ class Engine:
             # one device: the loop runs in the library (tnp_engine_run_steps)
             buf = (_hip.TnpStepStats * max(self.K, 1))()
             n = C.c_int32()
-            _hip.check(_hip.lib().tnp_engine_run_steps(self.h, self._s, buf, len(buf), C.byref(n)),
-                       "tnp_engine_run_steps")
-            if stats is not None:
+            rc = _hip.lib().tnp_engine_run_steps(self.h, self._s, buf, len(buf), C.byref(n))
+            if stats is not None:  # the completed steps, also when a later one failed
                 stats.extend(buf[i].as_dict() for i in range(min(n.value, len(buf))))
+            _hip.check(rc, "tnp_engine_run_steps")
             return stats
         mask = self.active_planes(0)
         if allreduce is not None:

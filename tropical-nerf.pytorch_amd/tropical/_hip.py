@@ -83,6 +83,7 @@ SIGNATURES = {
     "tnp_engine_faces_export": (C.c_int, [_VP, _VP, _VP, _VP]),
     "tnp_engine_set_owned": (C.c_int, [_VP, C.c_int, C.c_int]),
     "tnp_engine_set_xspan": (C.c_int, [_VP, C.c_int, C.c_int]),
+    "tnp_engine_set_eps": (C.c_int, [_VP, C.c_float]),
     "tnp_engine_run_steps": (C.c_int, [_VP, _VP, C.POINTER(TnpStepStats), C.c_int, _P32]),
     "tnp_engine_set_curve": (C.c_int, [_VP, C.c_int]),
     "tnp_engine_set_strict": (C.c_int, [_VP, C.c_int]),

@@ -19,11 +19,13 @@ from torch import Tensor
 from ._engine import engine_for
 
 
-def _check_eps(net, eps):
-    if eps is not None and float(eps) != float(net.eps):
-        raise NotImplementedError(
-            f"eps={eps} differs from net.eps={net.eps}; the reference mixes both "
-            "(subpoly_ uses eps, Net.region uses net.eps) -- construct Net(eps=...) instead")
+def _eps(net, eps):
+    """subpoly's eps argument (None: Net.eps).  The reference mixes both:
+    the steps' sign test, split point, hits and failover, extract_skeleton
+    and extract_faces take the argument, Net.region (the pair tests and the
+    pruning) net.eps (subpoly.py:24, 90-279, 556-606); the engine does the
+    same (tnp_engine_set_eps)."""
+    return float(net.eps) if eps is None else float(eps)
 
 
 def _faces_to_numpy(tri: Tensor, faces: Tensor):
@@ -40,10 +42,9 @@ def subpoly(net, d: int, size: float, eps: float = 1e-4, force: bool = False,
     Returns ``(faces float np F x 3 x 3, vertices V x 3 on net.device(),
     faces_with_indices int64 np F x 3)``; ``stats`` (optional list) receives
     one counter dict per active step."""
-    _check_eps(net, eps)
     if d != 3:
         raise NotImplementedError("d must be 3 (the reference's hash grid is 3-D)")
-    eng = engine_for(net).set_curve(not force)
+    eng = engine_for(net).set_curve(not force).set_eps(_eps(net, eps))
     eng.skeleton(unit=128, size=size)
     eng.run_steps(stats)
     return _finish(eng, net)
@@ -86,8 +87,7 @@ def subpoly_(vertices, edges, net, l, h, eps, outputs_=None, pruning=True, stric
     Like the reference, a step that splits rewrites the caller's ``edges``
     in place: the second endpoint of every split edge becomes its new vertex
     (``masked_scatter_``, subpoly.py:209-212)."""
-    _check_eps(net, eps)
-    eng = engine_for(net).set_curve(not force).set_strict(strict)
+    eng = engine_for(net).set_curve(not force).set_strict(strict).set_eps(_eps(net, eps))
     eng.load(vertices, edges, outputs_, keep_all=True)
     idx = l * net.num_hidden + h
     S, fail = eng.split(idx)
@@ -112,7 +112,7 @@ def subpoly_(vertices, edges, net, l, h, eps, outputs_=None, pruning=True, stric
 
 def extract_skeleton(vertices, edges, net, eps, outputs=None):
     """subpoly.py:556-581; returns (vertices, edges, v_idx)."""
-    _check_eps(net, eps)
+    eps = _eps(net, eps)
     on = (outputs[:, -1].abs() < eps) if outputs is not None else (net.sdf(vertices)[:, 0].abs() < eps)
     v = net.preprocess(vertices)
     on[(v > 1).sum(dim=-1) > 0] = False
@@ -125,11 +125,11 @@ def extract_skeleton(vertices, edges, net, eps, outputs=None):
 
 
 def extract_faces(vertices, edges, net, outputs=None, eps=None):
-    """subpoly.py:584-652 on the device engine."""
-    _check_eps(net, eps)
+    """subpoly.py:584-652 on the device engine (regions at ``eps``,
+    subpoly.py:606)."""
     if vertices.shape[0] == 0:
         return [], []
-    eng = engine_for(net)
+    eng = engine_for(net).set_eps(_eps(net, eps))
     eng.load(vertices, edges, outputs, keep_all=True)
     tri, fc = eng.faces()
     return _faces_to_numpy(tri, fc)
