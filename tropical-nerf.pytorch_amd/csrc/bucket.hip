@@ -618,6 +618,193 @@ __device__ __forceinline__ int build_windows(int* cnt, const int* cur) {
   return nwin;
 }
 
+// A small bucket (2..64 entries, the bunny-scale nets' buckets hold tens):
+// ONE wave groups it and tests all its pairs in a single window, with no
+// barrier and no trip of the records through memory.  The wave ranks its
+// entries by (local cell, lane) with v_readlane (the records land
+// cell-contiguous in the window's LDS slot), and every same-cell pair --
+// also of a cell above WCELL members, at most 64 * 63 / 2 tests -- is tested
+// once by window_tests; the bucket lists no pair cell for k_connect.
+#ifndef TNP_SMALL_BUCKET
+#define TNP_SMALL_BUCKET 1
+#endif
+template <int SH>
+__device__ __forceinline__ void group_small(int b, int64_t base, int n, const uint64_t* __restrict__ ekv,
+                                            const ulonglong2* __restrict__ pz, const WinArgs& wa, uint64_t below,
+                                            int64_t* __restrict__ bnpc, int64_t* __restrict__ bnpairs,
+                                            int64_t* __restrict__ bspairs, int64_t* __restrict__ ctr, WinLds& W) {
+  constexpr int LC = 1 << (3 * SH);
+  const int L = tnp::lane();
+  const bool valid = L < n;
+  const uint64_t w = valid ? ekv[base + L] : 0ull;
+  const ulonglong2 k = pz[valid ? (uint32_t)w : 0u];
+  const uint32_t lc = valid ? (uint32_t)(w >> 40) : (uint32_t)LC;  // invalid lanes rank last
+  const uint32_t key = (lc << 6) | (uint32_t)L;
+  int rank = 0;
+  for (int q = 0; q < 64; ++q) rank += (uint32_t)__builtin_amdgcn_readlane((int)key, q) < key;
+  CellEnt r;
+  r.p = valid ? k.x : 0ull;
+  r.z = valid ? k.y : 0ull;
+  r.v = valid ? (int32_t)(uint32_t)w : 0;
+  r.f = valid ? ((uint32_t)(w >> 32) & 63u) : 0u;
+  r.tag = valid ? (uint32_t)b * (uint32_t)LC + lc : 0xFFFFFFFFu;  // invalid: matches nothing
+  r.pad = 0;
+  const int wv = tnp::wave();
+  W.st[wv][rank] = r;
+  lds_fence();
+  // lane L now takes position L of the window
+  const uint32_t tag = W.st[wv][L].tag;
+  const uint32_t nxt = __shfl_down(tag, 1, 64);
+  const uint64_t bm = __ballot(L == 63 || nxt != tag);
+  const int last = L + __builtin_ctzll(bm >> L);
+  const uint32_t prv = __shfl_up(tag, 1, 64);
+  const bool first = L < n && (L == 0 || prv != tag);
+  const int64_t m = first ? (int64_t)(last - L + 1) : 0;  // this cell's members (at its first position)
+  const int64_t pairs = tnp::wave_sum(m * (m - 1) / 2);
+  WinAcc a;
+  window_tests(L < n ? last - L : 0, below, wa.nb, wa.fmask, wa.keys, wa.cap, wa.xs, ctr, W, a);
+  window_flush(wa.keys, wa.cap, wa.xs, ctr, W, a);
+  const int64_t c = tnp::wave_sum(a.n_compat), g = tnp::wave_sum(a.n_reg), x = tnp::wave_sum(a.n_conn);
+  if (L == 0) {
+    if (c) atomicAdd((unsigned long long*)sink_word(wa.xs, ctr, XS_COMPAT), (unsigned long long)c);
+    if (g) atomicAdd((unsigned long long*)sink_word(wa.xs, ctr, XS_P), (unsigned long long)g);
+    if (x) atomicAdd((unsigned long long*)sink_word(wa.xs, ctr, XS_X), (unsigned long long)x);
+    tnp::st_agent(bnpc + b, (int64_t)0);
+    tnp::st_agent(bnpairs + b, (int64_t)0);
+    tnp::st_agent(bspairs + b, pairs);
+  }
+}
+
+// The same windows built by the whole workgroup (sh = 3).  The greedy
+// packing is a chain c0 -> J(c0) -> ... over window-opening cells: a window
+// opened at cell c closes before the first non-empty cell after c that is
+// big or ends beyond s_c + 64 (a binary search over the cells' end
+// offsets), and the next one opens there (after a big cell: at the next
+// non-empty cell of <= WCELL members).  With every cell's J known, the
+// chain is enumerated by pointer doubling (J^(2^k) tables) -- the serial
+// walk of one wave (build_windows) was ~26 % of the grouping kernel's
+// workgroup time at 128^3.  Bit for bit the windows of build_windows.
+// scratch: (NJ + 3) * (LC + 1) uint16 + 8 int of LDS not otherwise in use.
+#ifndef TNP_PAR_WIN
+#define TNP_PAR_WIN 1
+#endif
+constexpr int PW_NJ = 10;  // J^(2^k), k < PW_NJ: chains of up to 1024 windows
+// below this many entries the serial walk is shorter than the builder's
+// fixed ~40 barrier-separated steps (bunny-scale buckets hold ~100)
+constexpr int PW_MIN = 512;
+template <int LC>
+__device__ __forceinline__ int build_windows_par(int* cnt, const int* cur, uint16_t* scratch) {
+  static_assert(LC + 1 <= 65535 && LC <= (1 << PW_NJ), "cell indices in 16 bits, chains in the tables");
+  constexpr int W1 = LC + 1;  // cell index LC: none
+  uint16_t* opn = scratch;    // first non-empty cell of <= WCELL members at or after c
+  uint16_t* nbg = opn + W1;   // first big cell at or after c
+  uint16_t* wend = nbg + W1;  // end offset of the window opened at c
+  uint16_t* J = wend + W1;    // J[k * W1 + c] = J^(2^k)(c)
+  int* red = reinterpret_cast<int*>(J + PW_NJ * W1 + (PW_NJ * W1 + 3 * W1) % 2);  // 8 ints
+  const int t = threadIdx.x, L = tnp::lane(), wv = tnp::wave();
+  constexpr int per = LC / TNP_BLOCK > 0 ? LC / TNP_BLOCK : 1;
+  const int c0 = t * per;
+  // (1) suffix minima: per-thread chunk, then over the lanes, then the waves
+  int mo = LC, mb = LC;
+  for (int i = c0 + per - 1; i >= c0; --i) {
+    if (i >= LC) continue;
+    const int m = cnt[i];
+    if (m > 0 && m <= WCELL) mo = i;
+    if (m > WCELL) mb = i;
+  }
+  int so = mo, sb = mb;  // minima over lanes >= L of this wave
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int a = __shfl_down(so, d, 64), b = __shfl_down(sb, d, 64);
+    if (L + d < 64) {
+      so = min(so, a);
+      sb = min(sb, b);
+    }
+  }
+  if (L == 0) {
+    red[wv] = so;
+    red[TNP_WAVES + wv] = sb;
+  }
+  __syncthreads();
+  // carry: the minima of the chunks after this thread's
+  int co = __shfl_down(so, 1, 64), cb = __shfl_down(sb, 1, 64);
+  if (L == 63) co = cb = LC;
+  for (int w = wv + 1; w < TNP_WAVES; ++w) {
+    co = min(co, red[w]);
+    cb = min(cb, red[TNP_WAVES + w]);
+  }
+  for (int i = c0 + per - 1; i >= c0; --i) {
+    if (i >= LC) continue;
+    const int m = cnt[i];
+    if (m > 0 && m <= WCELL) co = i;
+    if (m > WCELL) cb = i;
+    opn[i] = (uint16_t)co;
+    nbg[i] = (uint16_t)cb;
+  }
+  if (t == 0) {
+    opn[LC] = LC;
+    nbg[LC] = LC;
+  }
+  __syncthreads();
+  // (2) J and the window end of every window-opening cell
+  const int total = cur[LC - 1];
+  for (int i = c0; i < c0 + per && i < LC; ++i) {
+    const int m = cnt[i];
+    int j = LC, e = total;
+    if (m > 0 && m <= WCELL) {
+      const int lim = cur[i] - m + 64;  // the window [s, s + 64)
+      int lo = i + 1, hi = LC;  // first cell after i ending beyond it (ends never decrease)
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (cur[mid] > lim) hi = mid;
+        else lo = mid + 1;
+      }
+      const int stop = min(lo, (int)nbg[i + 1]);
+      if (stop < LC) {
+        e = cur[stop] - cnt[stop];  // the window ends where the stopping cell starts
+        j = cnt[stop] > WCELL ? opn[stop + 1] : stop;
+      }
+    }
+    J[i] = (uint16_t)j;
+    wend[i] = (uint16_t)e;
+  }
+  if (t == 0) J[LC] = LC;
+  __syncthreads();
+  for (int k = 1; k < PW_NJ; ++k) {
+    const uint16_t* A = J + (k - 1) * W1;
+    uint16_t* B = J + k * W1;
+    for (int i = t; i < W1; i += TNP_BLOCK) B[i] = A[A[i]];
+    __syncthreads();
+  }
+  // (3) window w opens at J^w(opn[0])
+  const int first = opn[0];
+  constexpr int NR = (1 << PW_NJ) / TNP_BLOCK;
+  uint32_t ent[NR];
+  int n = 0;
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    const int w = t + r * TNP_BLOCK;
+    int c = first;
+#pragma unroll
+    for (int k = 0; k < PW_NJ; ++k)
+      if (((w >> k) & 1) && c < LC) c = J[k * W1 + c];
+    ent[r] = c < LC ? ((uint32_t)(cur[c] - cnt[c]) | ((uint32_t)wend[c] << 16)) : 0xFFFFFFFFu;
+    if (c < LC) n = w + 1;
+  }
+  // (windows are a prefix of w: the count is the largest valid w + 1)
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) n = max(n, __shfl_xor(n, d, 64));
+  __syncthreads();  // every read of cnt[] is done: the list overwrites it
+  if (L == 0) red[wv] = n;
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+    if (ent[r] != 0xFFFFFFFFu) cnt[t + r * TNP_BLOCK] = (int)ent[r];
+  __syncthreads();
+  int nw = 0;
+  for (int w = 0; w < TNP_WAVES; ++w) nw = max(nw, red[w]);
+  return nw;
+}
+
 #ifndef TNP_BG_MINB
 #define TNP_BG_MINB 1
 #endif
@@ -661,6 +848,11 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
       r.pad = 0;
       ents[base] = r;
     }
+  } else if (TNP_SMALL_BUCKET && wa.keys && n <= 64) {
+    if (tnp::wave() == 0) {
+      const uint64_t below = (wa.idx >= 64) ? ~0ull : ((1ull << wa.idx) - 1ull);
+      group_small<SH>(b, base, (int)n, ekv, pz, wa, below, bnpc, bnpairs, bspairs, ctr, W);
+    }
   } else {
     unsigned long long tph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     BG_PH(0);
@@ -674,8 +866,20 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
       WinAcc a;
       const uint64_t below = (wa.idx >= 64) ? ~0ull : ((1ull << wa.idx) - 1ull);
       if (TNP_PACKED_WIN && n < 65536) {
-        // packed windows of whole cells (wave 0 builds the list in cnt[])
-        if (tnp::wave() == 0) {
+        // packed windows of whole cells (the list overwrites cnt[]): built by
+        // the whole workgroup for 8^3-cell buckets (their scratch fits the
+        // window pass's LDS, unused until the pass), by wave 0 for 16^3
+        bool par = false;
+        if constexpr (TNP_PAR_WIN && LC == 512) {
+          static_assert(sizeof(WinLds) >= (PW_NJ + 3) * (LC + 1) * sizeof(uint16_t) + 12 * sizeof(int),
+                        "window-builder scratch");
+          par = n >= PW_MIN;
+          if (par) {
+            const int nw = build_windows_par<LC>(cnt, cur, reinterpret_cast<uint16_t*>(&W));
+            if (threadIdx.x == 0) nwin_s = nw;
+          }
+        }
+        if (!par && tnp::wave() == 0) {
           const int nw = build_windows<LC>(cnt, cur);
           if (tnp::lane() == 0) nwin_s = nw;
         }

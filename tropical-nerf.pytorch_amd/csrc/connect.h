@@ -206,50 +206,77 @@ __device__ __forceinline__ void window_tests(int rounds, uint64_t below, int nb,
     if (table)  // each initiator lists its own tests (a few, mostly)
       for (int r = 0, t = incl - rounds; r < rounds; ++r, ++t) W.own[wv][t] = (uint16_t)(L | ((L + 1 + r) << 8));
     lds_fence();
-    for (int t0 = 0; t0 < total; t0 += 64) {
-      if (a.kn + 64 > WKEYS) window_flush(keys, cap, xs, ctr, W, a);
-      const int t = t0 + L;
-      bool em = false;
-      uint64_t key = 0;
-      if (t < total) {
-        int j, i;
-        if (table) {
-          const uint32_t o = W.own[wv][t];
-          j = (int)(o & 0xFFu);
-          i = (int)(o >> 8);
-        } else {
-          int lo2 = 0, hi2 = 62;
+    // test t -> (initiator j, partner i)
+    auto pair_of = [&](int t, int& j, int& i) {
+      if (table) {
+        const uint32_t o = W.own[wv][t];
+        j = (int)(o & 0xFFu);
+        i = (int)(o >> 8);
+      } else {
+        int lo2 = 0, hi2 = 62;
 #pragma unroll
-          for (int it = 0; it < 6; ++it) {
-            const int mid = (lo2 + hi2 + 1) >> 1;
-            if (W.exc[wv][mid] <= t) lo2 = mid;
-            else hi2 = mid - 1;
-          }
-          j = lo2;
-          i = j + 1 + (t - W.exc[wv][j]);
+        for (int it = 0; it < 6; ++it) {
+          const int mid = (lo2 + hi2 + 1) >> 1;
+          if (W.exc[wv][mid] <= t) lo2 = mid;
+          else hi2 = mid - 1;
         }
-        const CellEnt u = W.st[wv][j];
-        const CellEnt q = W.st[wv][i];
-        // pair_test without branches: both records are read once, every
-        // predicate is a select (branches here cost exec-mask juggling and a
-        // second dependent LDS round trip per test)
-        const uint64_t d = (u.p ^ q.p) & ~u.z & ~q.z & below;
-        const uint32_t af = u.f & q.f;
-        const uint32_t sp = af & (af >> 3) & 7u;
-        const uint64_t zz = u.z & q.z & below;
-        const bool compat = (((u.f | q.f) & 7u) == 7u) & (d == 0);
-        const bool emit = compat & ((sp != 0) | (zz != 0));
-        a.n_compat += compat;
-        a.n_reg += compat ? ((int64_t)1 << (__popc(sp) + __popcll(zz))) : 0;
-        a.n_conn += emit;
-        // the step's pruning drops it anyway (keep_edge): never appended
-        em = emit & ((fmask == 0) | ((((u.p ^ q.p) | (u.z ^ q.z)) & fmask) != 0));
-        const uint32_t vu = (uint32_t)u.v, vv = (uint32_t)q.v;
-        key = ((uint64_t)min(vu, vv) << nb) | max(vu, vv);
+        j = lo2;
+        i = j + 1 + (t - W.exc[wv][j]);
       }
+    };
+    // pair_test without branches: both records are read once, every
+    // predicate is a select (branches here cost exec-mask juggling and a
+    // second dependent LDS round trip per test); live == false counts nothing
+    auto test = [&](const CellEnt& u, const CellEnt& q, bool live, uint64_t& key) -> bool {
+      const uint64_t d = (u.p ^ q.p) & ~u.z & ~q.z & below;
+      const uint32_t af = u.f & q.f;
+      const uint32_t sp = af & (af >> 3) & 7u;
+      const uint64_t zz = u.z & q.z & below;
+      const bool compat = live & (((u.f | q.f) & 7u) == 7u) & (d == 0);
+      const bool emit = compat & ((sp != 0) | (zz != 0));
+      a.n_compat += compat;
+      a.n_reg += compat ? ((int64_t)1 << (__popc(sp) + __popcll(zz))) : 0;
+      a.n_conn += emit;
+      const uint32_t vu = (uint32_t)u.v, vv = (uint32_t)q.v;
+      key = ((uint64_t)min(vu, vv) << nb) | max(vu, vv);
+      // the step's pruning drops it anyway (keep_edge): never appended
+      return emit & ((fmask == 0) | ((((u.p ^ q.p) | (u.z ^ q.z)) & fmask) != 0));
+    };
+    auto append = [&](bool em, uint64_t key) {
       const uint64_t eb = __ballot(em);
       if (em) W.kb[wv][a.kn + tnp::mbcnt(eb)] = key;
       a.kn += __popcll(eb);
+    };
+    int t0 = 0;
+    // two batches of 64 tests per round while both hold tests: their LDS
+    // reads in flight together (the chain own[] -> records -> test is
+    // latency-bound one batch at a time)
+    for (; t0 + 64 < total; t0 += 128) {
+      if (a.kn + 128 > WKEYS) window_flush(keys, cap, xs, ctr, W, a);
+      const int ta = t0 + L, tb = t0 + 64 + L;
+      const bool lb = tb < total;
+      int ja, ia, jb, ib;
+      pair_of(ta, ja, ia);
+      pair_of(lb ? tb : ta, jb, ib);
+      const CellEnt ua = W.st[wv][ja], qa = W.st[wv][ia];
+      const CellEnt ub = W.st[wv][jb], qb = W.st[wv][ib];
+      uint64_t ka, kb;
+      const bool ema = test(ua, qa, true, ka);
+      const bool emb = test(ub, qb, lb, kb);
+      append(ema, ka);
+      append(emb, kb);
+    }
+    for (; t0 < total; t0 += 64) {
+      if (a.kn + 64 > WKEYS) window_flush(keys, cap, xs, ctr, W, a);
+      const int t = t0 + L;
+      const bool live = t < total;
+      int j = 0, i = 0;
+      pair_of(live ? t : 0, j, i);
+      const CellEnt u = W.st[wv][j];
+      const CellEnt q = W.st[wv][i];
+      uint64_t key;
+      const bool em = test(u, q, live, key);
+      append(em, key);
     }
     lds_fence();
   }
