@@ -158,6 +158,11 @@ class Collective:
         return a.max(axis=0)
 
 
+def log(msg: str) -> None:
+    """Progress on stderr (the JSON line alone goes to stdout)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def cpu_threads() -> int:
     """Host threads for the CPU baseline: the usable cores
     (sched_getaffinity), capped by the job's CPU share when the launcher
@@ -354,9 +359,10 @@ def main():
     # that the reference's CPU path could not materialise (tools/seed_scan.py)
     ap.add_argument("--seed", type=int, default=6)
     # the CPU baseline's sample: the whole lattice of this many
-    # marks per axis, same seed (64: ~1 min of CPU work; 128 is the benchmarked
-    # workload itself, ~18 min)
-    ap.add_argument("--cpu-marks", type=int, default=int(os.environ.get("TNP_CPU_MARKS", 64)))
+    # marks per axis, same seed (48: ~8 s of CPU work on the GPU box's 16-core
+    # share, so the default run finishes in a few minutes; 64 took over three
+    # minutes there; 128 is the benchmarked workload itself, ~18 min)
+    ap.add_argument("--cpu-marks", type=int, default=int(os.environ.get("TNP_CPU_MARKS", 48)))
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
 
@@ -429,6 +435,7 @@ def main():
             torch.distributed.barrier()
         torch.cuda.synchronize(dev)
 
+    log(f"rank {rank}: {G}^3 lattice, {args.warmup} warmup + {args.steps} timed passes")
     for _ in range(args.warmup):
         one_pass()
     barrier()
@@ -569,7 +576,9 @@ def main():
         if not args.no_cpu and world == 1:
             thr = cpu_threads()
             Gc = args.cpu_marks
+            log(f"CPU baseline: the oracle on the {Gc}^3 lattice, {thr} threads")
             cps, S_cpu, t_cpu = cpu_baseline(Gc, args.seed, thr)
+            log(f"CPU baseline: {S_cpu} splits in {t_cpu:.1f} s")
             S_g, t_g = gpu_same_workload(Gc, args.seed, dev)
             if S_g != S_cpu:
                 raise SystemExit(f"CPU baseline workload: {S_cpu} splits on the host, {S_g} on the GPU")
@@ -597,6 +606,7 @@ def main():
                     "gpu_over_reference": round(value / (per_pass / ref_s), 1)}
             engine_for(net)  # restore
         if not args.no_cpu and world == 1:
+            log("bunny-scale and large-net legs")
             out["small_net"] = small_net_check(dev, force=True)
             out["small_net_curve"] = small_net_check(dev, force=False)
             out["large_net"] = large_net_check(dev)
