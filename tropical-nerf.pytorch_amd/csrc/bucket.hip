@@ -84,7 +84,7 @@ struct WinArgs {
   int64_t* xs;  // per-XCD shards of the appends and pair statistics (step.h); null: ctr
 };
 
-// the global pair-cell lists the fused last workgroup fills
+// the global pair-cell list (k_connect's) and the bucket counters
 struct PairLists {
   int32_t *pcell, *pent, *pn;
   int64_t* ptoff;
@@ -394,29 +394,19 @@ k_bucket_scatter(const int32_t* __restrict__ members, int64_t S, int64_t V, int6
 #endif
 constexpr int GIPT = TNP_GIPT;
 
-// pair cell i of a bucket (its area slot a, global slot o, the bucket's
-// first pair po) into the global lists and k_connect's chunk table; handed:
-// the lists come from other workgroups of the running launch (sc1 loads)
-__device__ __forceinline__ void gather_pair_cell(int64_t a, int64_t o, int64_t po,
-                                                 const int32_t* __restrict__ lcell,
-                                                 const int32_t* __restrict__ lent,
-                                                 const int32_t* __restrict__ ln,
-                                                 const int64_t* __restrict__ lpoff, int32_t* __restrict__ pcell,
-                                                 int32_t* __restrict__ pent, int32_t* __restrict__ pn,
-                                                 int64_t* __restrict__ ptoff, int32_t* __restrict__ bcell,
-                                                 int64_t bcap, int64_t chunk, int64_t* __restrict__ ctr,
-                                                 bool handed) {
-  const int m = handed ? tnp::ld_agent(ln + a) : ln[a];
-  const int64_t lo = po + (handed ? tnp::ld_agent(lpoff + a) : lpoff[a]);
-  pcell[o] = handed ? tnp::ld_agent(lcell + a) : lcell[a];
-  pent[o] = handed ? tnp::ld_agent(lent + a) : lent[a];
-  pn[o] = m;
-  ptoff[o] = lo;
+// pair cell o of the global list (cell id, first entry, m members, first
+// pair lo) and its chunks in k_connect's chunk table
+__device__ __forceinline__ void put_pair_cell(int64_t o, int64_t lo, int32_t cell, int32_t ent, int m,
+                                              const PairLists& pl, int64_t* __restrict__ ctr) {
+  pl.pcell[o] = cell;
+  pl.pent[o] = ent;
+  pl.pn[o] = m;
+  pl.ptoff[o] = lo;
   // k_connect's chunk table (k_chunk_cells): chunk q starts in pair cell o
   const int64_t n = (int64_t)m * (m - 1) / 2;
-  const int64_t b0 = (lo + chunk - 1) / chunk, b1 = (lo + n + chunk - 1) / chunk;
-  if (b1 > bcap) atomicOr((unsigned long long*)&ctr[CTR_BOVF], 1ull);
-  for (int64_t q = b0; q < b1 && q < bcap; ++q) bcell[q] = (int32_t)o;
+  const int64_t b0 = (lo + pl.chunk - 1) / pl.chunk, b1 = (lo + n + pl.chunk - 1) / pl.chunk;
+  if (b1 > pl.bcap) atomicOr((unsigned long long*)&ctr[CTR_BOVF], 1ull);
+  for (int64_t q = b0; q < b1 && q < pl.bcap; ++q) pl.bcell[q] = (int32_t)o;
 }
 
 // the grouping of one bucket of n >= 2 entries (k_bucket_group)
@@ -424,12 +414,9 @@ template <int SH>
 __device__ __forceinline__ void group_bucket(const BGeom& G, int b, int64_t base, int64_t n,
                                              const uint64_t* __restrict__ ekv,
                                              const ulonglong2* __restrict__ pz, CellEnt* __restrict__ ents,
-                                             int32_t* __restrict__ lcell, int32_t* __restrict__ lent,
-                                             int32_t* __restrict__ ln, int64_t* __restrict__ lpoff,
-                                             int64_t* __restrict__ bnpc, int64_t* __restrict__ bnpairs,
-                                             int64_t* __restrict__ bspairs, int64_t* __restrict__ ctr,
-                                             int* cnt, int* cur, int64_t* lds, int64_t* lds3,
-                                             unsigned long long* tph) {
+                                             const PairLists& pl, int64_t* __restrict__ xs,
+                                             int64_t* __restrict__ ctr, int* cnt, int* cur, int64_t* lds,
+                                             int64_t* lds3, int64_t* s_pk, unsigned long long* tph) {
   (void)tph;
   constexpr int LC = 1 << (3 * SH);
   for (int i = threadIdx.x; i < LC; i += TNP_BLOCK) cnt[i] = 0;
@@ -538,7 +525,22 @@ __device__ __forceinline__ void group_bucket(const BGeom& G, int b, int64_t base
     opc += i0 - npc;
     op += i1 - np;
   }
-  const int64_t area = base / 2;
+  // the bucket's cells and pairs in the global list: one atomic reserves
+  // both (same order), then every thread writes its cells
+  if (threadIdx.x == 0) {
+    int64_t pk = 0;
+    if (tpc) {
+      pk = (int64_t)atomicAdd((unsigned long long*)&ctr[CTR_PCK], (unsigned long long)(tp << 24 | tpc));
+      if ((pk & (PCK_CELLS - 1)) + tpc >= PCK_CELLS) atomicOr((unsigned long long*)&ctr[CTR_BIG], 1ull);
+    }
+    *s_pk = pk;
+    if (tsp) atomicAdd((unsigned long long*)sink_word(xs, ctr, XS_SP), (unsigned long long)tsp);
+  }
+  if (tpc == 0) return;  // (block-uniform)
+  __syncthreads();
+  const int64_t o0 = (*s_pk & (PCK_CELLS - 1)) + opc, p0 = (*s_pk >> 24) + op;
+  opc = 0;
+  op = 0;
   const int m_ = (1 << G.sh) - 1;
   const int bz = b % G.NBd, by = (b / G.NBd) % G.NBd, bx = b / (G.NBd * G.NBd);
   for (int i = c0; i < c0 + per && i < LC; ++i) {
@@ -547,19 +549,11 @@ __device__ __forceinline__ void group_bucket(const BGeom& G, int b, int64_t base
       const int cx = G.xorg + ((bx << G.sh) | (i >> (2 * G.sh)));
       const int cy = (by << G.sh) | ((i >> G.sh) & m_);
       const int cz = (bz << G.sh) | (i & m_);
-      // agent-scope stores: the fused last workgroup gathers them (tnp::last_block)
-      tnp::st_agent(lcell + area + opc, (int32_t)((cx * G.NC + cy) * G.NC + cz));
-      tnp::st_agent(lent + area + opc, (int32_t)(base + cur[i] - m));
-      tnp::st_agent(ln + area + opc, (int32_t)m);
-      tnp::st_agent(lpoff + area + opc, op);
+      put_pair_cell(o0 + opc, p0 + op, (int32_t)((cx * G.NC + cy) * G.NC + cz), (int32_t)(base + cur[i] - m), m,
+                    pl, ctr);
       ++opc;
       op += (int64_t)m * (m - 1) / 2;
     }
-  }
-  if (threadIdx.x == 0) {
-    tnp::st_agent(bnpc + b, tpc);
-    tnp::st_agent(bnpairs + b, tp);
-    tnp::st_agent(bspairs + b, tsp);
   }
 }
 
@@ -631,8 +625,7 @@ __device__ __forceinline__ int build_windows(int* cnt, const int* cur) {
 template <int SH>
 __device__ __forceinline__ void group_small(int b, int64_t base, int n, const uint64_t* __restrict__ ekv,
                                             const ulonglong2* __restrict__ pz, const WinArgs& wa, uint64_t below,
-                                            int64_t* __restrict__ bnpc, int64_t* __restrict__ bnpairs,
-                                            int64_t* __restrict__ bspairs, int64_t* __restrict__ ctr, WinLds& W) {
+                                            int64_t* __restrict__ ctr, WinLds& W) {
   constexpr int LC = 1 << (3 * SH);
   const int L = tnp::lane();
   const bool valid = L < n;
@@ -669,9 +662,7 @@ __device__ __forceinline__ void group_small(int b, int64_t base, int n, const ui
     if (c) atomicAdd((unsigned long long*)sink_word(wa.xs, ctr, XS_COMPAT), (unsigned long long)c);
     if (g) atomicAdd((unsigned long long*)sink_word(wa.xs, ctr, XS_P), (unsigned long long)g);
     if (x) atomicAdd((unsigned long long*)sink_word(wa.xs, ctr, XS_X), (unsigned long long)x);
-    tnp::st_agent(bnpc + b, (int64_t)0);
-    tnp::st_agent(bnpairs + b, (int64_t)0);
-    tnp::st_agent(bspairs + b, pairs);
+    if (pairs) atomicAdd((unsigned long long*)sink_word(wa.xs, ctr, XS_SP), (unsigned long long)pairs);
   }
 }
 
@@ -814,28 +805,24 @@ __device__ __forceinline__ int build_windows_par(int* cnt, const int* cur, uint1
 template <int SH>
 __global__ void __launch_bounds__(TNP_BLOCK, TNP_BG_MINB)
 k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __restrict__ ekv,
-               const ulonglong2* __restrict__ pz, CellEnt* __restrict__ ents,
-               int32_t* __restrict__ lcell, int32_t* __restrict__ lent, int32_t* __restrict__ ln,
-               int64_t* __restrict__ lpoff, int64_t* __restrict__ bnpc, int64_t* __restrict__ bnpairs,
-               int64_t* __restrict__ bspairs, int64_t* __restrict__ pcoff, int64_t* __restrict__ pairoff,
-               int64_t* __restrict__ spoff, int fuse, WinArgs wa, PairLists pl, int64_t* __restrict__ ctr) {
+               const ulonglong2* __restrict__ pz, CellEnt* __restrict__ ents, WinArgs wa, PairLists pl,
+               int64_t* __restrict__ ctr) {
   constexpr int LC = 1 << (3 * SH);
   __shared__ int cnt[LC];
   __shared__ int cur[LC];
   __shared__ int64_t lds[TNP_WAVES];
   __shared__ int64_t lds3[3 * TNP_WAVES];
-  __shared__ int last;
+  __shared__ int64_t s_pk;
   __shared__ int nwin_s;
   __shared__ WinLds W;
   const int b = blockIdx.x;
   const int64_t base = bbase[b];
   const int64_t n = bbase[b + 1] - base;
+  if (threadIdx.x == 0) {  // the bucket counters are clean for the next step (read by the member passes)
+    pl.bcount[b] = 0;
+    pl.bcur[b] = 0;
+  }
   if (n < 2) {
-    if (threadIdx.x == 0) {
-      tnp::st_agent(bnpc + b, (int64_t)0);
-      tnp::st_agent(bnpairs + b, (int64_t)0);
-      tnp::st_agent(bspairs + b, (int64_t)0);
-    }
     if (n == 1 && threadIdx.x == 0) {  // a lone entry: a record the window pass can read
       const uint64_t w = ekv[base];
       const ulonglong2 k = pz[(uint32_t)w];
@@ -851,13 +838,12 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
   } else if (TNP_SMALL_BUCKET && wa.keys && n <= 64) {
     if (tnp::wave() == 0) {
       const uint64_t below = (wa.idx >= 64) ? ~0ull : ((1ull << wa.idx) - 1ull);
-      group_small<SH>(b, base, (int)n, ekv, pz, wa, below, bnpc, bnpairs, bspairs, ctr, W);
+      group_small<SH>(b, base, (int)n, ekv, pz, wa, below, ctr, W);
     }
   } else {
     unsigned long long tph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     BG_PH(0);
-    group_bucket<SH>(G, b, base, n, ekv, pz, ents, lcell, lent, ln, lpoff, bnpc, bnpairs, bspairs, ctr, cnt,
-                     cur, lds, lds3, tph);
+    group_bucket<SH>(G, b, base, n, ekv, pz, ents, pl, wa.xs, ctr, cnt, cur, lds, lds3, &s_pk, tph);
     BG_PH(4);
     if (wa.keys) {
       // the window pass over this bucket's records, right behind their
@@ -903,53 +889,6 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
           atomicAdd(&g_bg_ph[k * 8 + (blockIdx.x & 7)], tph[k + 1] - tph[k]);
 #endif
   }
-  if (!fuse || !tnp::last_block(&ctr[CTR_TK1], &last)) return;
-  // every bucket's pair-cell / pair totals -> global offsets (k_pair_gather)
-  const int NB = (int)gridDim.x;
-  const int64_t R = scan_handed(bnpc, NB, pcoff, lds);
-  const int64_t TT = scan_handed(bnpairs, NB, pairoff, lds);
-  const int64_t SP = scan_handed(bspairs, NB, spoff, lds);
-  if (threadIdx.x == 0) {
-    ctr[CTR_R] = R;
-    ctr[CTR_TESTS] = TT;
-    ctr[CTR_SPAIRS] = SP;
-  }
-  __syncthreads();  // pcoff / pairoff: this workgroup's stores
-  // the pair-cell gather (k_pair_gather's work), a thread per bucket, and the
-  // bucket counters cleaned for the next step
-  for (int bb = threadIdx.x; bb < NB; bb += TNP_BLOCK) {
-    pl.bcount[bb] = 0;
-    pl.bcur[bb] = 0;
-    const int cnt = (int)tnp::ld_agent(bnpc + bb);
-    const int64_t area = bbase[bb] / 2, o = pcoff[bb], po = pairoff[bb];
-    for (int i = 0; i < cnt; ++i)
-      gather_pair_cell(area + i, o + i, po, lcell, lent, ln, lpoff, pl.pcell, pl.pent, pl.pn, pl.ptoff, pl.bcell,
-                       pl.bcap, pl.chunk, ctr, true);
-  }
-}
-
-// (6) the global pair-cell list k_connect walks: bucket order, then local
-// cell order (k_pair_gather: a workgroup per bucket; the fused last
-// workgroup of k_bucket_group: a thread per bucket)
-__global__ void __launch_bounds__(TNP_BLOCK)
-k_pair_gather(const int64_t* __restrict__ bbase, const int64_t* __restrict__ bnpc,
-              const int64_t* __restrict__ pcoff, const int64_t* __restrict__ pairoff,
-              const int32_t* __restrict__ lcell, const int32_t* __restrict__ lent,
-              const int32_t* __restrict__ ln, const int64_t* __restrict__ lpoff,
-              int32_t* __restrict__ pcell, int32_t* __restrict__ pent, int32_t* __restrict__ pn,
-              int64_t* __restrict__ ptoff, int32_t* __restrict__ bcell, int64_t bcap, int64_t chunk,
-              int32_t* __restrict__ bcount, int32_t* __restrict__ bcur, int64_t* __restrict__ ctr) {
-  const int b = blockIdx.x;
-  if (threadIdx.x == 0) {  // the bucket counters are clean for the next step
-    bcount[b] = 0;
-    bcur[b] = 0;
-  }
-  const int cnt = (int)bnpc[b];
-  if (cnt == 0) return;
-  const int64_t area = bbase[b] / 2, o = pcoff[b], po = pairoff[b];
-  for (int i = threadIdx.x; i < cnt; i += TNP_BLOCK)
-    gather_pair_cell(area + i, o + i, po, lcell, lent, ln, lpoff, pcell, pent, pn, ptoff, bcell, bcap, chunk,
-                     ctr, false);
 }
 
 }  // namespace
@@ -984,7 +923,7 @@ int launch_bucket_entries(const int32_t* members, int64_t S, int64_t V, int64_t 
                           int64_t* bbase, int64_t* part, uint64_t* ekv, bool clean, uint8_t* live,
                           int64_t nlive, const NewOverride* ovr, int64_t* ctr, hipStream_t s) {
   const int NB = G.NB;
-  if (!clean) {  // else: zeroed by the previous step's k_pair_gather
+  if (!clean) {  // else: zeroed by the previous step's grouping kernel
     TNP_CHECK(hipMemsetAsync(bcount, 0, NB * sizeof(int32_t), s));
     TNP_CHECK(hipMemsetAsync(bcur, 0, NB * sizeof(int32_t), s));
   }
@@ -1014,25 +953,19 @@ int launch_bucket_entries(const int32_t* members, int64_t S, int64_t V, int64_t 
 }
 
 int launch_bucket_pairs(const BucketGeom& G, const int64_t* bbase, const uint64_t* ekv, const uint64_t* pz,
-                        CellEnt* ents, int32_t* lcell,
-                        int32_t* lent, int32_t* ln, int64_t* lpoff, int64_t* bnpc, int64_t* bnpairs,
-                        int64_t* bspairs, int64_t* spoff, int64_t* pcoff, int64_t* pairoff,
-                        int32_t* pcell, int32_t* pent, int32_t* pn, int64_t* ptoff, int32_t* bcell,
+                        CellEnt* ents, int32_t* pcell, int32_t* pent, int32_t* pn, int64_t* ptoff, int32_t* bcell,
                         int64_t bcap, int32_t* bcount, int32_t* bcur, const ConnectWin* win, int64_t* ctr,
                         hipStream_t s) {
   const int NB = G.NB, sh = G.sh;
-  const int fuse = NB <= FUSE_MAX_BLOCKS;
   const PairLists pl{pcell, pent, pn, ptoff, bcell, bcap, connect_chunk_pairs(), bcount, bcur};
   WinArgs wa{0, 0, 0ull, nullptr, 0, nullptr};
   if (win) wa = WinArgs{win->idx, win->nb, win->fmask, win->keys, win->cap, win->xs};
   if (sh == 3)
     hipLaunchKernelGGL(k_bucket_group<3>, dim3(NB), dim3(TNP_BLOCK), 0, s, G, bbase, ekv,
-                       reinterpret_cast<const ulonglong2*>(pz), ents, lcell, lent, ln, lpoff, bnpc, bnpairs,
-                       bspairs, pcoff, pairoff, spoff, fuse, wa, pl, ctr);
+                       reinterpret_cast<const ulonglong2*>(pz), ents, wa, pl, ctr);
   else
     hipLaunchKernelGGL(k_bucket_group<4>, dim3(NB), dim3(TNP_BLOCK), 0, s, G, bbase, ekv,
-                       reinterpret_cast<const ulonglong2*>(pz), ents, lcell, lent, ln, lpoff, bnpc, bnpairs,
-                       bspairs, pcoff, pairoff, spoff, fuse, wa, pl, ctr);
+                       reinterpret_cast<const ulonglong2*>(pz), ents, wa, pl, ctr);
 #if TNP_BG_PHASES
   {
     unsigned long long h[64];
@@ -1047,13 +980,6 @@ int launch_bucket_pairs(const BucketGeom& G, const int64_t* bbase, const uint64_
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_bg_ph), h, sizeof(h));
   }
 #endif
-  if (!fuse)
-    hipLaunchKernelGGL(k_scan_sets, dim3(1, 3), dim3(TNP_BLOCK), 0, s, ScanSet{bnpc, 1, pcoff, CTR_R},
-                       ScanSet{bnpairs, 1, pairoff, CTR_TESTS}, ScanSet{bspairs, 1, spoff, CTR_SPAIRS}, NB,
-                       nullptr, (int64_t)0, 0, ctr);
-  if (!fuse)
-    hipLaunchKernelGGL(k_pair_gather, dim3(NB), dim3(TNP_BLOCK), 0, s, bbase, bnpc, pcoff, pairoff, lcell, lent,
-                       ln, lpoff, pcell, pent, pn, ptoff, bcell, bcap, connect_chunk_pairs(), bcount, bcur, ctr);
   TNP_CHECK(hipGetLastError());
   return 0;
 }

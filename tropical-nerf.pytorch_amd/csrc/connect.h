@@ -46,7 +46,7 @@ __device__ __forceinline__ PairTest pair_test(uint64_t below, uint32_t fu, uint6
 // the shards into ctr) or the counter block itself (small grids: a few
 // hundred workgroups, no fold or concatenation launches)
 __device__ __forceinline__ int64_t* sink_word(int64_t* xs, int64_t* ctr, int stat) {
-  constexpr int slot[4] = {CTR_XK, CTR_COMPAT, CTR_P, CTR_X};
+  constexpr int slot[5] = {CTR_XK, CTR_COMPAT, CTR_P, CTR_X, CTR_SPAIRS};
   return xs ? &xs[xs_word(stat, blockIdx.x % XS_N)] : &ctr[slot[stat]];
 }
 

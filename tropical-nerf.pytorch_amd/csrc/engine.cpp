@@ -1092,19 +1092,10 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     if (buf_ensure(e->bk[1], NB * sizeof(int32_t), s)) return -1;        // cursors
     if (e->bk[0].p != bk0 || e->bk[1].p != bk1) e->bk_clean = false;     // fresh memory
     if (buf_ensure(e->bk[2], (NB + 1) * sizeof(int64_t), s)) return -1;  // bases
-    if (buf_ensure(e->bk[3], NB * sizeof(int64_t), s)) return -1;        // pair cells
-    if (buf_ensure(e->bk[4], NB * sizeof(int64_t), s)) return -1;        // pairs
-    if (buf_ensure(e->bk[5], (NB + 1) * sizeof(int64_t), s)) return -1;  // pair-cell offsets
-    if (buf_ensure(e->bk[6], (NB + 1) * sizeof(int64_t), s)) return -1;  // pair offsets
     // block parts: one per workgroup of the member passes (the grid is at least
     // FUSE_MAX_BLOCKS = 512 when the live-flag zeroing rides along)
     if (buf_ensure(e->bk[7], (std::max<int64_t>(bucket_member_blocks(M), 512) + 2) * sizeof(int64_t), s))
       return -1;
-    for (int k = 8; k < 11; ++k)
-      if (buf_ensure(e->bk[k], RC * sizeof(int32_t), s)) return -1;  // per-bucket pair-cell areas
-    if (buf_ensure(e->bk[11], RC * sizeof(int64_t), s)) return -1;
-    if (buf_ensure(e->bk[12], NB * sizeof(int64_t), s)) return -1;        // window-pass pairs
-    if (buf_ensure(e->bk[13], (NB + 1) * sizeof(int64_t), s)) return -1;
     if (buf_ensure(e->sents, TB * sizeof(uint64_t), s)) return -1;
     // a pruning step recomputes the live flags: zeroed by the bucket count
     // (after the hit pass read them), re-marked by the prune
@@ -1200,7 +1191,8 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
       TNP_CHECK(hipMemsetAsync(ctr + CTR_XK, 0, sizeof(int64_t), s));
       TNP_CHECK(hipMemsetAsync(ctr + CTR_P, 0, 2 * sizeof(int64_t), s));  // CTR_P, CTR_COMPAT
       TNP_CHECK(hipMemsetAsync(ctr + CTR_BOVF, 0, sizeof(int64_t), s));
-      TNP_CHECK(hipMemsetAsync(ctr + CTR_TK1, 0, sizeof(int64_t), s));
+      TNP_CHECK(hipMemsetAsync(ctr + CTR_PCK, 0, sizeof(int64_t), s));
+      TNP_CHECK(hipMemsetAsync(ctr + CTR_SPAIRS, 0, sizeof(int64_t), s));
     }
     // the shards are left zero by k_keys_finish; cleared here after an
     // aborted step or on fresh memory
@@ -1213,11 +1205,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
       const ConnectWin cw{idx, nb, cfmask, P<uint64_t>(e->ckeys_a), cap, xs};
       TIMED("bucket_group", 0.0,
             launch_bucket_pairs(bg, P<int64_t>(e->bk[2]), P<uint64_t>(e->sents),
-                                P<uint64_t>(c.pz), P<CellEnt>(e->ents),
-                                P<int32_t>(e->bk[8]), P<int32_t>(e->bk[9]), P<int32_t>(e->bk[10]),
-                                P<int64_t>(e->bk[11]), P<int64_t>(e->bk[3]), P<int64_t>(e->bk[4]),
-                                P<int64_t>(e->bk[12]), P<int64_t>(e->bk[13]),
-                                P<int64_t>(e->bk[5]), P<int64_t>(e->bk[6]), P<int32_t>(e->pcell),
+                                P<uint64_t>(c.pz), P<CellEnt>(e->ents), P<int32_t>(e->pcell),
                                 P<int32_t>(e->pent), P<int32_t>(e->pcn), P<int64_t>(e->ptoff),
                                 P<int32_t>(e->bcell), bcap, P<int32_t>(e->bk[0]), P<int32_t>(e->bk[1]),
                                 &cw, ctr, s));
@@ -1239,6 +1227,9 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     }
     if (read_ctr(e, s)) return -1;
     if (buckets) {
+      // the atomically allocated pair-cell list: cells | pairs << 24
+      e->h_ctr[CTR_R] = e->h_ctr[CTR_PCK] & (PCK_CELLS - 1);
+      e->h_ctr[CTR_TESTS] = e->h_ctr[CTR_PCK] >> 24;
       if (e->h_ctr[CTR_K0] & 2) {
         tnp_set_error("plane %d: a vertex outside the x mark planes [%d, %d] the engine was given "
                       "(tnp_engine_set_xspan)", idx, gx0, gx1);
@@ -1429,7 +1420,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     st->E_out = E2_live;
     st->A = e->h_ctr[CTR_A];
     st->P = e->h_ctr[CTR_P];
-    st->pair_tests = e->h_ctr[CTR_TESTS] + e->h_ctr[CTR_SPAIRS];
+    st->pair_tests = (e->h_ctr[CTR_PCK] ? (e->h_ctr[CTR_PCK] >> 24) : e->h_ctr[CTR_TESTS]) + e->h_ctr[CTR_SPAIRS];
     st->override_applied = override_ < 0 ? (e->h_ctr[CTR_FAIL] != 0) : override_;
     st->next_active = (uint64_t)e->h_ctr[CTR_ACTIVE];
     st->S_dup = e->pend_dup;

@@ -33,8 +33,8 @@ enum {
   CTR_R = 25,       // cells with at least one member pair
   CTR_RUNS = 26,    // occupied cells (runs of equal keys in the sorted entries)
   CTR_SPAIRS = 27,  // member pairs of the cells the window pass tests (<= WCELL members)
-  CTR_TK0 = 28,     // last-workgroup tickets (tnp::last_block) of the fused
-  CTR_TK1 = 29,     //   bucket count / bucket group launches
+  CTR_TK0 = 28,     // last-workgroup ticket (tnp::last_block) of the fused bucket count
+  CTR_PCK = 29,     // bucket path: pair cells (bits 0..23) | their pairs << 24, allocated by atomics
   CTR_MISSED = 30,  // split: an edge whose first split plane lies below the step (masks to redo)
   CTR_N = 31        // <= 31: the host-mapped mirror keeps its sequence word at [31]
 };
@@ -239,16 +239,18 @@ int launch_bucket_entries(const int32_t* members, int64_t S, int64_t V, int64_t 
                           const uint64_t* zero, int idx, const BucketGeom& g, int32_t* bcount, int32_t* bcur,
                           int64_t* bbase, int64_t* part, uint64_t* ekv, bool clean, uint8_t* live,
                           int64_t nlive, const NewOverride* ovr, int64_t* ctr, hipStream_t s);
-// per bucket: cell-contiguous CellEnt records (ents, entry positions), the
-// pair cells; then the global pair-cell list (pcell, pent, pn, ptoff; R ->
-// ctr[CTR_R], pairs -> ctr[CTR_TESTS]) that launch_connect walks.
-// lcell/lent/ln/lpoff: 4 M + 1 capacity; bnpc/bnpairs: NB; pcoff/pairoff: NB + 1
-// Cells above WCELL members go to the pair-cell list (and k_connect's chunk
-// table bcell, bcap chunks, overflow -> CTR_BOVF); the pairs of the others
-// -> ctr[CTR_SPAIRS] (bspairs/spoff: NB / NB + 1 int64 scratch).  Leaves
-// bcount/bcur zeroed for the next step.
+// per bucket: cell-contiguous CellEnt records (ents, entry positions) and
+// the bucket's cells above WCELL members, appended to the global pair-cell
+// list (pcell, pent, pn, ptoff) that launch_connect walks: a workgroup
+// reserves its cells and their pairs with ONE atomic on ctr[CTR_PCK] (cells
+// | pairs << 24: cell slots and pair offsets in the same order, which the
+// chunk walk needs; the list order is otherwise free -- the emitted keys are
+// sorted), and fills k_connect's chunk table bcell (bcap chunks, overflow ->
+// CTR_BOVF).  The pairs of the smaller cells -> ctr[CTR_SPAIRS].  Leaves
+// bcount/bcur zeroed for the next step.  launch_connect unpacks CTR_PCK;
+// the host reads R = CTR_PCK & 0xFFFFFF, pairs = CTR_PCK >> 24.
 // win != null: the grouping kernel also runs the window pass (launch_connect_win's
-// work) over each bucket's records; uses ctr[CTR_TK1] on small grids
+// work) over each bucket's records
 // Per-XCD shards of the connect phase's appends and pair statistics.  One
 // device-scope atomic per workgroup (or per wave flush) on ONE word
 // serialises at ~11 ns (MI355X_MICROARCH.md fan-in: ~88 per microsecond);
@@ -261,7 +263,7 @@ int launch_bucket_entries(const int32_t* members, int64_t S, int64_t V, int64_t 
 #endif
 constexpr int XS_N = TNP_XS_N;  // shards (<= 63: k_keys_finish folds them in one wave)
 constexpr int XS_LINE = 16;  // int64 words per counter line
-enum { XS_KEYS = 0, XS_COMPAT = 1, XS_P = 2, XS_X = 3, XS_STATS = 4 };
+enum { XS_KEYS = 0, XS_COMPAT = 1, XS_P = 2, XS_X = 3, XS_SP = 4, XS_STATS = 5 };
 __host__ __device__ constexpr int xs_word(int stat, int shard) { return (stat * XS_N + shard) * XS_LINE; }
 constexpr int XS_OFF = XS_STATS * XS_N * XS_LINE;  // + [0, XS_N]: region output offsets
 constexpr int XS_WORDS = XS_OFF + 64 + 1;  // + the XS_N + 1 offsets
@@ -281,12 +283,10 @@ struct ConnectWin {
   int64_t* xs;
 };
 int launch_bucket_pairs(const BucketGeom& g, const int64_t* bbase, const uint64_t* ekv, const uint64_t* pz,
-                        CellEnt* ents, int32_t* lcell,
-                        int32_t* lent, int32_t* ln, int64_t* lpoff, int64_t* bnpc, int64_t* bnpairs,
-                        int64_t* bspairs, int64_t* spoff, int64_t* pcoff, int64_t* pairoff,
-                        int32_t* pcell, int32_t* pent, int32_t* pn, int64_t* ptoff, int32_t* bcell,
+                        CellEnt* ents, int32_t* pcell, int32_t* pent, int32_t* pn, int64_t* ptoff, int32_t* bcell,
                         int64_t bcap, int32_t* bcount, int32_t* bcur, const ConnectWin* win, int64_t* ctr,
                         hipStream_t s);
+constexpr int64_t PCK_CELLS = 1 << 24;  // CTR_PCK: cell count field
 // pair indices per k_connect chunk (its bcell table granularity)
 int64_t connect_chunk_pairs();
 // window pass over the cell-contiguous entries (count ctr[CTR_T]): every

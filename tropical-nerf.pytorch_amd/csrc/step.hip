@@ -609,8 +609,11 @@ k_connect(const int64_t* __restrict__ ptoff, const int32_t* __restrict__ pcell,
   __shared__ int32_t s_off[CONNECT_CELLS];  // first pair of the cell - chunk start
   __shared__ int32_t s_n[CONNECT_CELLS];
   __shared__ int32_t s_ent[CONNECT_CELLS];  // first entry of the cell
-  const int64_t TT = ctr[CTR_TESTS];
-  const int64_t R = ctr[CTR_R];
+  // the bucket path's atomically allocated list (cells | pairs << 24), else
+  // the radix path's scans
+  const int64_t pk = ctr[CTR_PCK];
+  const int64_t TT = pk ? (pk >> 24) : ctr[CTR_TESTS];
+  const int64_t R = pk ? (pk & (PCK_CELLS - 1)) : ctr[CTR_R];
   if (TT > max_tests || ctr[CTR_BOVF] || ctr[CTR_BIG]) return;
   const int64_t nblk = (TT + CCH - 1) / CCH;
   const uint64_t below = (idx >= 64) ? ~0ull : ((1ull << idx) - 1ull);
@@ -762,14 +765,15 @@ __global__ void k_keys_finish(int64_t* __restrict__ xs, int64_t cap, int64_t* __
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
   const int64_t total = __shfl(incl, 63, 64);
-  int64_t st[3];
+  int64_t st[4];
 #pragma unroll
-  for (int q = 0; q < 3; ++q) st[q] = tnp::wave_sum(L < XS_N ? xs[xs_word(XS_COMPAT + q, L)] : (int64_t)0);
+  for (int q = 0; q < 4; ++q) st[q] = tnp::wave_sum(L < XS_N ? xs[xs_word(XS_COMPAT + q, L)] : (int64_t)0);
   if (L == 0) {
     ctr[CTR_XK] = mx > rc ? mx * XS_N : total;  // overflow: the capacity every region needs
     ctr[CTR_COMPAT] = st[0];
     ctr[CTR_P] = st[1];
     ctr[CTR_X] = st[2];
+    if (st[3]) ctr[CTR_SPAIRS] = st[3];  // (the bucket path's window-pass pairs)
   }
   for (int q = L; q < XS_N * XS_STATS; q += 64) xs[xs_word(q / XS_N, q % XS_N)] = 0;
 }
