@@ -82,7 +82,29 @@ struct WinArgs {
   uint64_t* keys;
   int64_t cap;
   int64_t* xs;  // per-XCD shards of the appends and pair statistics (step.h); null: ctr
+  // small grids (no shards): per-bucket pair statistics [NB][4] (compatible
+  // pairs, shared regions, connecting edges, window-pass pairs), plain
+  // stores that k_connect's first workgroup sums -- instead of 4 atomics per
+  // bucket on the counter block's words (~11 ns each, serialised)
+  int64_t* bstat;
 };
+
+// a bucket's pair statistics -> its bstat row, or the counter block / shards
+__device__ __forceinline__ void bucket_stats_out(const WinArgs& wa, int b, int64_t c, int64_t g, int64_t x,
+                                                 int64_t sp, int64_t* __restrict__ ctr) {
+  if (wa.bstat) {
+    int64_t* r = wa.bstat + 4 * (int64_t)b;
+    r[0] = c;
+    r[1] = g;
+    r[2] = x;
+    r[3] = sp;
+    return;
+  }
+  if (c) atomicAdd((unsigned long long*)sink_word(wa.xs, ctr, XS_COMPAT), (unsigned long long)c);
+  if (g) atomicAdd((unsigned long long*)sink_word(wa.xs, ctr, XS_P), (unsigned long long)g);
+  if (x) atomicAdd((unsigned long long*)sink_word(wa.xs, ctr, XS_X), (unsigned long long)x);
+  if (sp) atomicAdd((unsigned long long*)sink_word(wa.xs, ctr, XS_SP), (unsigned long long)sp);
+}
 
 // the global pair-cell list (k_connect's) and the bucket counters
 struct PairLists {
@@ -278,6 +300,157 @@ k_bucket_count(const int32_t* __restrict__ members, int64_t S, int64_t V, int64_
   }
 }
 
+// (1') bunny-scale steps: the member passes of a step with few members in
+// ONE workgroup -- counts, the bucket scan and the scatter through LDS: no
+// global bucket counters, no second launch and no last-workgroup hand-off
+// (the two-launch path costs ~19 us per step at bunny scale, most of it
+// global-atomic and hand-off latency)
+constexpr int SB_THREADS = 1024;
+constexpr int SB_IPT = 8;
+constexpr int SB_WAVES = SB_THREADS / 64;
+constexpr int64_t SB_MAX_M = (int64_t)SB_THREADS * SB_IPT;  // members
+constexpr int64_t SB_MAX_LIVE = 1 << 18;                      // live-flag bytes it zeroes
+constexpr int SB_PER = (BUCKET_MAX + SB_THREADS - 1) / SB_THREADS;
+
+__device__ __forceinline__ int64_t sb_scan_excl(int64_t v, int64_t* lds, int64_t& total) {
+  const int64_t inc = tnp::wave_scan_incl(v);
+  if (tnp::lane() == 63) lds[threadIdx.x >> 6] = inc;
+  __syncthreads();
+  int64_t off = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < SB_WAVES; ++i) {
+    const int64_t c = lds[i];
+    off += (i < (int)(threadIdx.x >> 6)) ? c : 0;
+    tot += c;
+  }
+  __syncthreads();
+  total = tot;
+  return off + inc - v;
+}
+
+__global__ void __launch_bounds__(SB_THREADS)
+k_bucket_small(const int32_t* __restrict__ members, int64_t S, int64_t V, int64_t M,
+               const uint64_t* __restrict__ grid, const uint64_t* __restrict__ zero, int idx, BGeom G, int NB,
+               int64_t* __restrict__ bbase, uint64_t* __restrict__ ekv, uint8_t* __restrict__ live,
+               int64_t nlive, Override ov, int64_t* __restrict__ ctr) {
+  extern __shared__ int hist[];  // NB bins
+  __shared__ int64_t lds[SB_WAVES];
+  const int t = threadIdx.x;
+  if (live) {  // the next live-flag set (k_bucket_count's zeroing)
+    const int64_t n16 = nlive >> 4;
+    uint4* l4 = reinterpret_cast<uint4*>(live);
+    for (int64_t i = t; i < n16; i += SB_THREADS) l4[i] = make_uint4(0, 0, 0, 0);
+    if (t < (nlive & 15)) live[(n16 << 4) + t] = 0;
+  }
+  for (int i = t; i < NB; i += SB_THREADS) hist[i] = 0;
+  const uint64_t below = (idx >= 64) ? ~0ull : ((1ull << idx) - 1ull);
+  int vv[SB_IPT];
+  uint64_t gg[SB_IPT], zz[SB_IPT];
+#pragma unroll
+  for (int k = 0; k < SB_IPT; ++k) {
+    const int64_t m = (int64_t)k * SB_THREADS + t;
+    vv[k] = m < M ? member_of(members, S, V, m) : -1;
+  }
+#pragma unroll
+  for (int k = 0; k < SB_IPT; ++k) {
+    const int v = vv[k] >= 0 ? vv[k] : 0;
+    gg[k] = grid[v];
+    zz[k] = zero[v];
+  }
+  if (ov.shared && (ov.flag < 0 ? ctr[CTR_FAIL] != 0 : ov.flag != 0)) {
+    // the new vertices' failover override (as k_bucket_count)
+    uint64_t sh[SB_IPT], ps[SB_IPT];
+#pragma unroll
+    for (int k = 0; k < SB_IPT; ++k) {
+      const int64_t m = (int64_t)k * SB_THREADS + t;
+      const int64_t mc = m < S ? m : 0;
+      sh[k] = ov.shared[mc];
+      ps[k] = ov.pos[V + mc];
+    }
+#pragma unroll
+    for (int k = 0; k < SB_IPT; ++k) {
+      const int64_t m = (int64_t)k * SB_THREADS + t;
+      if (m >= S) continue;
+      for (uint64_t q = sh[k]; q; q &= q - 1) {
+        const int p = __builtin_ctzll(q);
+        if (p >= ov.keep_from) ov.pre[(int64_t)p * ov.ld + V + m] = 0.f;
+      }
+      const uint64_t pp = ps[k] & ~sh[k], z = zz[k] | sh[k];
+      ov.pos[V + m] = pp;
+      ov.zero[V + m] = z;
+      ov.pz[V + m] = make_ulonglong2(pp, z);
+      zz[k] = z;
+    }
+  }
+  __syncthreads();  // hist zeroed
+  int64_t aug = 0;
+  bool k0 = false, outside = false;
+#pragma unroll
+  for (int k = 0; k < SB_IPT; ++k) {
+    if (vv[k] < 0) continue;
+    int lo[3], n[3];
+    span_of(gg[k], lo, n);
+    if (!span_inside(G, lo, n)) {
+      outside = true;
+      vv[k] = -1;
+      continue;
+    }
+    for (int i = 0; i < n[0]; ++i)
+      for (int j = 0; j < n[1]; ++j)
+        for (int q = 0; q < n[2]; ++q) atomicAdd(&hist[bucket_of(G, lo[0] + i, lo[1] + j, lo[2] + q)], 1);
+    const int kz = __popcll(zz[k] & below) + (n[0] - 1) + (n[1] - 1) + (n[2] - 1);
+    aug += 1ll << kz;
+    k0 |= kz == 0;
+  }
+  if (__ballot(k0) && tnp::lane() == 0) atomicOr((unsigned long long*)&ctr[CTR_K0], 1ull);
+  if (__ballot(outside) && tnp::lane() == 0) atomicOr((unsigned long long*)&ctr[CTR_K0], 2ull);
+  __syncthreads();  // counts complete
+  // bucket bases: a contiguous chunk of bins per thread
+  {
+    const int b0 = t * SB_PER;
+    int c[SB_PER];
+    int64_t s = 0;
+#pragma unroll
+    for (int k = 0; k < SB_PER; ++k) {
+      c[k] = b0 + k < NB ? hist[b0 + k] : 0;
+      s += c[k];
+    }
+    int64_t T;
+    int64_t run = sb_scan_excl(s, lds, T);
+#pragma unroll
+    for (int k = 0; k < SB_PER; ++k) {
+      if (b0 + k < NB) {
+        bbase[b0 + k] = run;
+        hist[b0 + k] = (int)run;  // cursor
+      }
+      run += c[k];
+    }
+    if (t == 0) {
+      bbase[NB] = T;
+      ctr[CTR_T] = T;
+    }
+  }
+  int64_t atot;
+  sb_scan_excl(aug, lds, atot);  // (its barriers also publish the cursors)
+  if (t == 0) ctr[CTR_A] = atot;
+#pragma unroll
+  for (int k = 0; k < SB_IPT; ++k) {
+    if (vv[k] < 0) continue;
+    int lo[3], n[3];
+    span_of(gg[k], lo, n);
+    for (int i = 0; i < n[0]; ++i)
+      for (int j = 0; j < n[1]; ++j)
+        for (int q = 0; q < n[2]; ++q) {
+          const int cx = lo[0] + i, cy = lo[1] + j, cz = lo[2] + q;
+          const int pos = atomicAdd(&hist[bucket_of(G, cx, cy, cz)], 1);
+          const uint32_t f = (uint32_t)(i == 0) | ((uint32_t)(j == 0) << 1) | ((uint32_t)(q == 0) << 2) |
+                             ((uint32_t)(n[0] - 1) << 3) | ((uint32_t)(n[1] - 1) << 4) |
+                             ((uint32_t)(n[2] - 1) << 5);
+          ekv[pos] = ((uint64_t)local_of(G, cx, cy, cz) << 40) | ((uint64_t)f << 32) | (uint32_t)vv[k];
+        }
+  }
+}
+
 // (2) the same scans as a launch of their own, for grids too large for the
 // last-workgroup hand-off to pay (every workgroup's tail then waits for its
 // stores and a contended ticket): blockIdx.y picks (cnt, out, slot) set y;
@@ -414,9 +587,9 @@ template <int SH>
 __device__ __forceinline__ void group_bucket(const BGeom& G, int b, int64_t base, int64_t n,
                                              const uint64_t* __restrict__ ekv,
                                              const ulonglong2* __restrict__ pz, CellEnt* __restrict__ ents,
-                                             const PairLists& pl, int64_t* __restrict__ xs,
-                                             int64_t* __restrict__ ctr, int* cnt, int* cur, int64_t* lds,
-                                             int64_t* lds3, int64_t* s_pk, unsigned long long* tph) {
+                                             const PairLists& pl, int64_t* __restrict__ ctr, int* cnt,
+                                             int* cur, int64_t* lds, int64_t* lds3, int64_t* s_pk,
+                                             int64_t* s_sp, unsigned long long* tph) {
   (void)tph;
   constexpr int LC = 1 << (3 * SH);
   for (int i = threadIdx.x; i < LC; i += TNP_BLOCK) cnt[i] = 0;
@@ -534,7 +707,7 @@ __device__ __forceinline__ void group_bucket(const BGeom& G, int b, int64_t base
       if ((pk & (PCK_CELLS - 1)) + tpc >= PCK_CELLS) atomicOr((unsigned long long*)&ctr[CTR_BIG], 1ull);
     }
     *s_pk = pk;
-    if (tsp) atomicAdd((unsigned long long*)sink_word(xs, ctr, XS_SP), (unsigned long long)tsp);
+    *s_sp = tsp;  // (reported with the window pass's statistics)
   }
   if (tpc == 0) return;  // (block-uniform)
   __syncthreads();
@@ -658,12 +831,7 @@ __device__ __forceinline__ void group_small(int b, int64_t base, int n, const ui
   window_tests(L < n ? last - L : 0, below, wa.nb, wa.fmask, wa.keys, wa.cap, wa.xs, ctr, W, a);
   window_flush(wa.keys, wa.cap, wa.xs, ctr, W, a);
   const int64_t c = tnp::wave_sum(a.n_compat), g = tnp::wave_sum(a.n_reg), x = tnp::wave_sum(a.n_conn);
-  if (L == 0) {
-    if (c) atomicAdd((unsigned long long*)sink_word(wa.xs, ctr, XS_COMPAT), (unsigned long long)c);
-    if (g) atomicAdd((unsigned long long*)sink_word(wa.xs, ctr, XS_P), (unsigned long long)g);
-    if (x) atomicAdd((unsigned long long*)sink_word(wa.xs, ctr, XS_X), (unsigned long long)x);
-    if (pairs) atomicAdd((unsigned long long*)sink_word(wa.xs, ctr, XS_SP), (unsigned long long)pairs);
-  }
+  if (L == 0) bucket_stats_out(wa, b, c, g, x, pairs, ctr);
 }
 
 // The same windows built by the whole workgroup (sh = 3).  The greedy
@@ -812,7 +980,7 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
   __shared__ int cur[LC];
   __shared__ int64_t lds[TNP_WAVES];
   __shared__ int64_t lds3[3 * TNP_WAVES];
-  __shared__ int64_t s_pk;
+  __shared__ int64_t s_pk, s_sp;
   __shared__ int nwin_s;
   __shared__ WinLds W;
   const int b = blockIdx.x;
@@ -823,6 +991,7 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
     pl.bcur[b] = 0;
   }
   if (n < 2) {
+    if (threadIdx.x == 0 && wa.bstat) bucket_stats_out(wa, b, 0, 0, 0, 0, ctr);
     if (n == 1 && threadIdx.x == 0) {  // a lone entry: a record the window pass can read
       const uint64_t w = ekv[base];
       const ulonglong2 k = pz[(uint32_t)w];
@@ -843,7 +1012,7 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
   } else {
     unsigned long long tph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     BG_PH(0);
-    group_bucket<SH>(G, b, base, n, ekv, pz, ents, pl, wa.xs, ctr, cnt, cur, lds, lds3, &s_pk, tph);
+    group_bucket<SH>(G, b, base, n, ekv, pz, ents, pl, ctr, cnt, cur, lds, lds3, &s_pk, &s_sp, tph);
     BG_PH(4);
     if (wa.keys) {
       // the window pass over this bucket's records, right behind their
@@ -879,7 +1048,11 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
       }
       BG_PH(6);
       window_flush(wa.keys, wa.cap, wa.xs, ctr, W, a);
-      add_pair_stats(a.n_compat, a.n_reg, a.n_conn, lds, wa.xs, ctr);
+      int64_t tc, tr, tx;
+      tnp::block_scan_excl(a.n_compat, lds, tc);
+      tnp::block_scan_excl(a.n_reg, lds, tr);
+      tnp::block_scan_excl(a.n_conn, lds, tx);
+      if (threadIdx.x == 0) bucket_stats_out(wa, b, tc, tr, tx, s_sp, ctr);
       BG_PH(7);
     }
 #if TNP_BG_PHASES
@@ -923,6 +1096,21 @@ int launch_bucket_entries(const int32_t* members, int64_t S, int64_t V, int64_t 
                           int64_t* bbase, int64_t* part, uint64_t* ekv, bool clean, uint8_t* live,
                           int64_t nlive, const NewOverride* ovr, int64_t* ctr, hipStream_t s) {
   const int NB = G.NB;
+  Override ov{0, nullptr, nullptr, 0, 0, nullptr, nullptr, nullptr};
+  if (ovr)
+    ov = Override{ovr->flag, ovr->shared, ovr->pre, ovr->ld, ovr->keep_from, ovr->pos, ovr->zero,
+                  reinterpret_cast<ulonglong2*>(ovr->pz)};
+  static const bool s_small = [] {  // TNP_SMALL_ENTRIES=0: always the two-launch path (A/B)
+    const char* v = getenv("TNP_SMALL_ENTRIES");
+    return !(v && v[0] == '0');
+  }();
+  if (s_small && M <= SB_MAX_M && (!live || nlive <= SB_MAX_LIVE)) {
+    // bcount / bcur stay untouched (the grouping kernel zeroes them anyway)
+    hipLaunchKernelGGL(k_bucket_small, dim3(1), dim3(SB_THREADS), NB * sizeof(int), s, members, S, V, M, keys, zero,
+                       idx, G, NB, bbase, ekv, live, nlive, ov, ctr);
+    TNP_CHECK(hipGetLastError());
+    return 0;
+  }
   if (!clean) {  // else: zeroed by the previous step's grouping kernel
     TNP_CHECK(hipMemsetAsync(bcount, 0, NB * sizeof(int32_t), s));
     TNP_CHECK(hipMemsetAsync(bcur, 0, NB * sizeof(int32_t), s));
@@ -936,10 +1124,6 @@ int launch_bucket_entries(const int32_t* members, int64_t S, int64_t V, int64_t 
     grid = std::max<unsigned>(nblk, (unsigned)std::min<int64_t>(nz, FUSE_MAX_BLOCKS));
   }
   const int fuse = grid <= FUSE_MAX_BLOCKS;
-  Override ov{0, nullptr, nullptr, 0, 0, nullptr, nullptr, nullptr};
-  if (ovr)
-    ov = Override{ovr->flag, ovr->shared, ovr->pre, ovr->ld, ovr->keep_from, ovr->pos, ovr->zero,
-                  reinterpret_cast<ulonglong2*>(ovr->pz)};
   hipLaunchKernelGGL(k_bucket_count, dim3(grid), dim3(TNP_BLOCK), NB * sizeof(int), s, members, S, V, M, keys, zero, idx,
                      G, NB, bcount, part, bbase, live, nlive, fuse, ov, ctr);
   if (!fuse)
@@ -958,8 +1142,8 @@ int launch_bucket_pairs(const BucketGeom& G, const int64_t* bbase, const uint64_
                         hipStream_t s) {
   const int NB = G.NB, sh = G.sh;
   const PairLists pl{pcell, pent, pn, ptoff, bcell, bcap, connect_chunk_pairs(), bcount, bcur};
-  WinArgs wa{0, 0, 0ull, nullptr, 0, nullptr};
-  if (win) wa = WinArgs{win->idx, win->nb, win->fmask, win->keys, win->cap, win->xs};
+  WinArgs wa{0, 0, 0ull, nullptr, 0, nullptr, nullptr};
+  if (win) wa = WinArgs{win->idx, win->nb, win->fmask, win->keys, win->cap, win->xs, win->bstat};
   if (sh == 3)
     hipLaunchKernelGGL(k_bucket_group<3>, dim3(NB), dim3(TNP_BLOCK), 0, s, G, bbase, ekv,
                        reinterpret_cast<const ulonglong2*>(pz), ents, wa, pl, ctr);

@@ -1180,6 +1180,10 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   const bool shard = !buckets || NB > 512;
   if (shard && buf_ensure(e->xs, XS_WORDS * sizeof(int64_t), s)) return -1;
   int64_t* const xs = shard ? P<int64_t>(e->xs) : nullptr;
+  // small bucket grids: per-bucket statistics rows (plain stores) that the
+  // connect kernel sums, instead of counter-block atomics from every bucket
+  if (buckets && !shard && buf_ensure(e->bk[3], (int64_t)NB * 4 * sizeof(int64_t), s)) return -1;
+  int64_t* const bstat = (buckets && !shard) ? P<int64_t>(e->bk[3]) : nullptr;
   int64_t cap = std::max<int64_t>(e->ckeys_a.bytes / sizeof(uint64_t), 4 * M + 1024);
   cap = (cap + XS_N - 1) / XS_N * XS_N;
   int64_t X = 0, TT = 0;
@@ -1202,7 +1206,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
       // in-bucket grouping + the window pass over each bucket (cells of <=
       // WCELL members) + pair-cell lists and k_connect's chunk table (bcap)
       if (buf_ensure(e->bcell, bcap * sizeof(int32_t), s)) return -1;
-      const ConnectWin cw{idx, nb, cfmask, P<uint64_t>(e->ckeys_a), cap, xs};
+      const ConnectWin cw{idx, nb, cfmask, P<uint64_t>(e->ckeys_a), cap, xs, bstat};
       TIMED("bucket_group", 0.0,
             launch_bucket_pairs(bg, P<int64_t>(e->bk[2]), P<uint64_t>(e->sents),
                                 P<uint64_t>(c.pz), P<CellEnt>(e->ents), P<int32_t>(e->pcell),
@@ -1220,7 +1224,8 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     TIMED("connect", 0.0,
           launch_connect(P<int64_t>(e->ptoff), P<int32_t>(e->pcell), P<int32_t>(e->pcn),
                          P<int32_t>(e->pent), NC, e->max_pair_tests, P<int32_t>(e->bcell),
-                         P<CellEnt>(e->ents), idx, nb, cfmask, P<uint64_t>(e->ckeys_a), cap, xs, ctr, s));
+                         P<CellEnt>(e->ents), idx, nb, cfmask, P<uint64_t>(e->ckeys_a), cap, xs, ctr, s,
+                         bstat, NB));
     if (shard) {
       if (launch_keys_finish(xs, cap, ctr, s)) return -1;
       e->xs_clean = true;

@@ -153,7 +153,8 @@ int launch_chunk_cells(const int64_t* ptoff, const int32_t* pn, int64_t rcap, in
 int launch_connect(const int64_t* ptoff, const int32_t* pcell, const int32_t* pn,
                    const int32_t* pent, int NC, int64_t max_tests, const int32_t* bcell,
                    const CellEnt* ent, int idx, int nb, uint64_t fmask, uint64_t* keys,
-                   int64_t cap, int64_t* xs, int64_t* ctr, hipStream_t s);
+                   int64_t cap, int64_t* xs, int64_t* ctr, hipStream_t s, const int64_t* bstat = nullptr,
+                   int nbstat = 0);
 // single-pass pruning over [edges; e_new; c_new] (lb_tiles(E + S + X)
 // look-back tiles): kept edges in order -> out, used flags (zeroed by the
 // caller), ctr[CTR_E], ctr[CTR_ACTIVE]
@@ -281,6 +282,7 @@ struct ConnectWin {
   uint64_t* keys;
   int64_t cap;
   int64_t* xs;
+  int64_t* bstat;  // small grids (xs == null): per-bucket statistics [NB][4] that launch_connect sums
 };
 int launch_bucket_pairs(const BucketGeom& g, const int64_t* bbase, const uint64_t* ekv, const uint64_t* pz,
                         CellEnt* ents, int32_t* pcell, int32_t* pent, int32_t* pn, int64_t* ptoff, int32_t* bcell,

@@ -603,9 +603,24 @@ k_connect(const int64_t* __restrict__ ptoff, const int32_t* __restrict__ pcell,
           const int32_t* __restrict__ pn, const int32_t* __restrict__ pent, int NC,
           int64_t max_tests, const int32_t* __restrict__ bcell, const CellEnt* __restrict__ ent,
           int idx, int nb, uint64_t fmask, uint64_t* __restrict__ keys, int64_t cap,
-          int64_t* __restrict__ xs, int64_t* __restrict__ ctr) {
+          int64_t* __restrict__ xs, int64_t* __restrict__ ctr, const int64_t* __restrict__ bstat,
+          int nbstat) {
   __shared__ int64_t lds[TNP_WAVES];
   __shared__ int64_t s_base;
+  if (bstat && blockIdx.x == 0) {
+    // the grouping kernel's per-bucket statistics (small grids) -> ctr
+    int64_t v[4] = {0, 0, 0, 0};
+    for (int i = threadIdx.x; i < nbstat; i += TNP_BLOCK)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] += bstat[4 * (int64_t)i + q];
+    constexpr int slot[4] = {CTR_COMPAT, CTR_P, CTR_X, CTR_SPAIRS};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      int64_t tot;
+      tnp::block_scan_excl(v[q], lds, tot);
+      if (threadIdx.x == 0 && tot) atomicAdd((unsigned long long*)&ctr[slot[q]], (unsigned long long)tot);
+    }
+  }
   __shared__ int32_t s_off[CONNECT_CELLS];  // first pair of the cell - chunk start
   __shared__ int32_t s_n[CONNECT_CELLS];
   __shared__ int32_t s_ent[CONNECT_CELLS];  // first entry of the cell
@@ -1434,11 +1449,11 @@ int launch_chunk_cells(const int64_t* ptoff, const int32_t* pn, int64_t rcap, in
 int launch_connect(const int64_t* ptoff, const int32_t* pcell, const int32_t* pn,
                    const int32_t* pent, int NC, int64_t max_tests, const int32_t* bcell,
                    const CellEnt* ent, int idx, int nb, uint64_t fmask, uint64_t* keys,
-                   int64_t cap, int64_t* xs, int64_t* ctr, hipStream_t s) {
+                   int64_t cap, int64_t* xs, int64_t* ctr, hipStream_t s, const int64_t* bstat, int nbstat) {
   static_assert(CONNECT_CELLS >= CCH + 2, "chunk cell window");
   const int grid = connect_grid_size();
   hipLaunchKernelGGL(k_connect, dim3(grid), dim3(TNP_BLOCK), 0, s, ptoff, pcell, pn,
-                     pent, NC, max_tests, bcell, ent, idx, nb, fmask, keys, cap, xs, ctr);
+                     pent, NC, max_tests, bcell, ent, idx, nb, fmask, keys, cap, xs, ctr, bstat, nbstat);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
