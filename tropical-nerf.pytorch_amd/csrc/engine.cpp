@@ -188,6 +188,7 @@ struct tnp_engine {
   int pend_idx = -1;
   int64_t pend_S = 0, pend_dup = 0;
   bool pend_hits = false;   // the pending split also found the plane's hit vertices
+  int64_t pend_hoff = -1;   // ... at members[pend_hoff] (the split's E; -1: after the S new members)
   bool pend_fused = false;  // the pending split ran k_forward_new (flat path)
   // faces output
   Buf tri, faces;
@@ -209,6 +210,11 @@ struct tnp_engine {
   bool bk_clean = false;    // bucket counters (bk[0], bk[1]) are zero
   Buf cv[CV_N];
 };
+
+// the counter block is cleared as 32 words: a 248-byte memset takes two fill
+// dispatches (aligned body + tail), 256 bytes one
+constexpr size_t CTR_CLEAR_BYTES = 32 * sizeof(int64_t);
+static_assert(CTR_N <= 32, "counter block");
 
 // counter readback: k_publish writes the block into host-mapped memory and
 // the host spins on its sequence word (measured on MI355X: 9.9 us per round
@@ -369,6 +375,13 @@ static int reset_live(tnp_engine* e, hipStream_t s, bool edges_changed = true) {
   e->dirty = false;
   e->V_live = e->V;
   return set_alive(e, 0, e->V, s);
+}
+
+// the cell grouping runs on spatial buckets (bucket.hip) unless the grid is
+// too fine for them or TNP_RADIX_CELLS=1; *bg: their geometry
+static bool uses_buckets(const tnp_engine* e, BucketGeom* bg) {
+  const int gx0 = e->xs1 >= e->xs0 ? e->xs0 : 0, gx1 = e->xs1 >= e->xs0 ? e->xs1 : e->net.n_marks - 1;
+  return !e->radix_cells && bucket_geometry(e->net.n_marks, gx0, gx1, bg) == 0;
 }
 
 // split-eps mode: subpoly's eps argument differs from Net.eps (tnp_engine_set_eps)
@@ -675,7 +688,7 @@ extern "C" int tnp_engine_load(tnp_engine* e, const float* d_xyz, int64_t V, con
   TNP_CHECK(hipSetDevice(e->device));
   e->xs0 = 0;  // anywhere (tnp_engine_set_xspan narrows it)
   e->xs1 = -1;
-  if (buf_ensure(e->ctr, CTR_N * sizeof(int64_t), s)) return -1;
+  if (buf_ensure(e->ctr, CTR_CLEAR_BYTES, s)) return -1;
   if (vset_ensure(e, e->cur, std::max<int64_t>(V, 1), 0, s)) return -1;
   if (V > 0)
     TNP_CHECK(hipMemcpyAsync(e->cur.xyz.p, d_xyz, V * 3 * sizeof(float), hipMemcpyDeviceToDevice, s));
@@ -709,7 +722,7 @@ extern "C" int tnp_engine_active_planes(tnp_engine* e, int from, uint64_t* mask,
   hipStream_t s = (hipStream_t)stream;
   TNP_CHECK(hipSetDevice(e->device));
   if (require_valid(e, "active_planes")) return -1;
-  if (buf_ensure(e->ctr, CTR_N * sizeof(int64_t), s)) return -1;
+  if (buf_ensure(e->ctr, CTR_CLEAR_BYTES, s)) return -1;
   TNP_CHECK(hipMemsetAsync(P<int64_t>(e->ctr) + CTR_ACTIVE, 0, sizeof(int64_t), s));
   // the per-edge masks are (re)computed here and the OR of their first split
   // planes taken in the same pass: the planes the next steps must visit
@@ -900,7 +913,7 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
   e->valid = false;  // until this split has completed
   const float eps = e->net.eps_s;  // subpoly_'s eps: hits, split point, failover
   const float* col = P<float>(e->cur.pre) + (int64_t)idx * e->cur.cap;
-  TNP_CHECK(hipMemsetAsync(e->ctr.p, 0, CTR_N * sizeof(int64_t), s));
+  TNP_CHECK(hipMemsetAsync(e->ctr.p, 0, CTR_CLEAR_BYTES, s));
   int64_t S = 0;
   e->pend_hits = false;
   if (e->E > 0) {
@@ -912,22 +925,30 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
     if (fresh < 0) return -1;
     TnpLB lb;
     if (lb_begin(e, split_tiles(e->E), s, &lb, 0, false)) return -1;
-    // algorithmic bytes: 1 B first split plane per edge; per split 8 B
-    // endpoints, 4 B rewired id, 1 B stale mask (set once S is known)
-    TIMED("split", 1.0 * e->E,
+    // flat path: the plane's hit vertices are found with the split (they
+    // read only the cached column and the live flags), so one readback
+    // returns S and H.  The bucket path reads them at members[E, E + H)
+    // (S <= E) and they ride in the split's own dispatch; the radix path
+    // wants them after the S new members (members[S, S + H)): launched
+    // behind the split, which writes S
+    BucketGeom bgs{};
+    const bool flat_hits = !e->curve && e->V > 0;
+    const bool fused_hits = flat_hits && uses_buckets(e, &bgs);
+    if (flat_hits && buf_ensure(e->members, (e->E + e->V) * sizeof(int32_t), s)) return -1;
+    const HitArgs ha{col, P<uint8_t>(e->live), e->V, eps, P<int32_t>(e->members) + e->E};
+    // algorithmic bytes: 1 B first split plane per edge (+ 5 B per vertex
+    // slot for fused hits); per split 8 B endpoints, 4 B rewired id, 1 B
+    // stale mask (set once S is known)
+    TIMED("split", 1.0 * e->E + (fused_hits ? 5.0 * e->V : 0.0),
           launch_split_lb(P<int32_t>(e->edges), e->E, P<uint8_t>(e->eef), P<uint8_t>(e->edm), idx,
                           e->V, P<int32_t>(e->sa), P<int32_t>(e->sb), P<int64_t>(e->ctr),
-                          e->curve ? P<int32_t>(e->cv[CV_EIDX]) : nullptr, lb, s));
-    if (!e->curve && e->V > 0) {
-      // flat path: the plane's hit vertices right behind the split (they read
-      // only the cached column and the live flags), so one readback returns
-      // S and H; members holds [V, V+S) ++ hits, S <= E
-      if (buf_ensure(e->members, (e->E + e->V) * sizeof(int32_t), s)) return -1;
+                          e->curve ? P<int32_t>(e->cv[CV_EIDX]) : nullptr, lb, s, fused_hits ? &ha : nullptr));
+    if (flat_hits && !fused_hits)
       TIMED("hits", 5.0 * e->V,
             launch_hits(col, P<uint8_t>(e->live), e->V, eps, P<int32_t>(e->members), -1,
                         P<int64_t>(e->ctr), s));
-      e->pend_hits = true;
-    }
+    e->pend_hits = flat_hits;
+    e->pend_hoff = fused_hits ? e->E : -1;
     if (read_ctr(e, s)) return -1;
     S = e->h_ctr[CTR_S];
     if (fresh) e->act_bits = (uint64_t)e->h_ctr[CTR_ACTIVE];
@@ -935,7 +956,7 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
       tnp_set_error("plane %d: an edge's first split plane lies below the step (stale edge masks)", idx);
       return -1;
     }
-    ktimer_set_bytes(e, "split", 1.0 * e->E + 13.0 * S);
+    ktimer_set_bytes(e, "split", 1.0 * e->E + 13.0 * S + (e->pend_hoff >= 0 ? 5.0 * e->V : 0.0));
   }
   *fail = 0;
   if (e->V + S >= (int64_t)INT32_MAX) {
@@ -1013,6 +1034,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   e->pend_idx = -1;
   e->valid = false;  // until this step has completed
   const bool hits_done = e->pend_hits;
+  const int64_t hoff = hits_done ? e->pend_hoff : -1;
   e->pend_hits = false;
   const float eps = e->net.eps;
   const int K = e->K;
@@ -1032,7 +1054,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
 
   BucketGeom bg{};
   const int gx0 = e->xs1 >= e->xs0 ? e->xs0 : 0, gx1 = e->xs1 >= e->xs0 ? e->xs1 : e->net.n_marks - 1;
-  const bool buckets = !e->radix_cells && bucket_geometry(e->net.n_marks, gx0, gx1, &bg) == 0;
+  const bool buckets = uses_buckets(e, &bg);
   const int NB = buckets ? bg.NB : 0;
   // 1. override + keys of the new vertices (flat bucket path: the override
   //    runs inside the bucket count, below)
@@ -1103,7 +1125,8 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     NewOverride nov{override_, P<uint64_t>(e->shared), P<float>(c.pre), c.cap, e->valid_from, pos, zero,
                     P<uint64_t>(c.pz)};
     TIMED("bucket_entries", 16.0 * M,  // + 8 B per entry, set once T is known
-          launch_bucket_entries(P<int32_t>(e->members), S, V, M, grid, zero, idx, bg,
+          // (member m >= S is members[m]: the hits sit at hoff >= S when the split found them)
+          launch_bucket_entries(P<int32_t>(e->members) + (hoff >= 0 ? hoff - S : 0), S, V, M, grid, zero, idx, bg,
                                 P<int32_t>(e->bk[0]), P<int32_t>(e->bk[1]), P<int64_t>(e->bk[2]),
                                 P<int64_t>(e->bk[7]), P<uint64_t>(e->sents), e->bk_clean,
                                 prune ? P<uint8_t>(e->live) : nullptr, NV, e->pend_fused ? &nov : nullptr,
@@ -1499,7 +1522,7 @@ extern "C" int tnp_engine_surface(tnp_engine* e, void* stream, int64_t* V_out, i
   if (buf_ensure(e->used, std::max<int64_t>(V, 1) * sizeof(int32_t), s)) return -1;
   if (buf_ensure(e->flags, std::max<int64_t>(V, 1) * sizeof(int32_t), s)) return -1;
   if (buf_ensure(e->nid, std::max<int64_t>(V, 1) * sizeof(int64_t), s)) return -1;
-  TNP_CHECK(hipMemsetAsync(e->ctr.p, 0, CTR_N * sizeof(int64_t), s));
+  TNP_CHECK(hipMemsetAsync(e->ctr.p, 0, CTR_CLEAR_BYTES, s));
   int32_t* on = P<int32_t>(e->flags);
   if (launch_surface_flags(P<float>(c.xyz), col, V, e->net.eps_s, on, s)) return -1;
   if (scan_counts(e, on, P<int64_t>(e->nid), V, CTR_AUX, s)) return -1;
@@ -1604,7 +1627,7 @@ extern "C" int tnp_engine_lattice(tnp_engine* e, int x0, int x1, int keep_all, v
   const int64_t V = (int64_t)nx * N * N;
   const int64_t E = (int64_t)(nx - 1) * N * N + 2LL * nx * (N - 1) * N;
   if (V >= (1LL << 31) || E >= (1LL << 31)) { tnp_set_error("lattice too large for int32 ids"); return -1; }
-  if (buf_ensure(e->ctr, CTR_N * sizeof(int64_t), s)) return -1;
+  if (buf_ensure(e->ctr, CTR_CLEAR_BYTES, s)) return -1;
   if (vset_ensure(e, e->cur, V, 0, s)) return -1;
   if (buf_ensure(e->edges, std::max<int64_t>(E, 1) * 2 * sizeof(int32_t), s)) return -1;
   hipLaunchKernelGGL(k_lattice_vertices, dim3(tnp_grid(V)), dim3(TNP_BLOCK), 0, s, e->net.marks, N,
@@ -1686,7 +1709,7 @@ extern "C" int tnp_engine_skeleton_mode(tnp_engine* e, int unit, float size, int
   TNP_CHECK(hipStreamSynchronize(s));
   float dmax = -INFINITY;  // torch.diff(marks).max().item()
   for (int i = 0; i + 1 < L; ++i) dmax = std::max(dmax, mk[i + 1] - mk[i]);
-  if (buf_ensure(e->ctr, CTR_N * sizeof(int64_t), s)) return -1;
+  if (buf_ensure(e->ctr, CTR_CLEAR_BYTES, s)) return -1;
   const int64_t LLL = (int64_t)L * L * L;
   if (buf_ensure(e->used, LLL * sizeof(int32_t), s)) return -1;
   if (buf_ensure(e->nid, LLL * sizeof(int64_t), s)) return -1;
@@ -1822,7 +1845,7 @@ extern "C" int tnp_engine_faces(tnp_engine* e, void* stream, int64_t* n_tri, int
     zero = P<uint64_t>(e->kse[1]);
     grid = P<uint64_t>(e->kse[2]);
   }
-  TNP_CHECK(hipMemsetAsync(ctr, 0, CTR_N * sizeof(int64_t), s));
+  TNP_CHECK(hipMemsetAsync(ctr, 0, CTR_CLEAR_BYTES, s));
   // F1: augmented-row count and region hash table
   if (launch_face_count(V, grid, pos, zero, pmask, ctr + CTR_AUX - 1, s)) return -1;
   if (read_ctr(e, s)) return -1;

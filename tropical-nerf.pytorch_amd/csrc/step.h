@@ -49,9 +49,19 @@ int64_t run_tiles(int64_t n);    // tiles of the radix path's run-start pass
 // than the caller's step order: redo them from idx); sa/sb (and eidx if
 // given) need capacity E; without eidx the split edges are rewired in place
 // and their masks marked stale
+// hits != null: the plane's hit vertices in the same dispatch (workgroups
+// past the split tiles): live slots v < hits->V with |col[v]| < eps ->
+// hits->out[0, ctr[CTR_H]) (no dependence on S)
+struct HitArgs {
+  const float* col;
+  const uint8_t* alive;
+  int64_t V;
+  float eps;
+  int32_t* out;
+};
 int launch_split_lb(int32_t* edges, int64_t E, const uint8_t* ef, uint8_t* dm, int idx, int64_t V,
                     int32_t* sa, int32_t* sb, int64_t* ctr, int32_t* eidx, const TnpLB& lb,
-                    hipStream_t s);
+                    hipStream_t s, const HitArgs* hits = nullptr);
 // per-edge masks from the endpoint keys (pz): dm = 1 + highest plane where
 // the keys differ (0: none), ef = the first plane in [from, last_plane] that
 // splits the edge (EDGE_NOSPLIT: none); ctr != null: OR of those first

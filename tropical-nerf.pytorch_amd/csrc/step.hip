@@ -75,6 +75,14 @@ constexpr int LIPT = TNP_LIPT;
 #endif
 constexpr int LTILE = TNP_BLOCK * LIPT;
 
+constexpr int HIPT = 16;                    // slots per thread per chunk
+constexpr int HCHUNK = TNP_BLOCK * HIPT;    // slots per chunk
+constexpr int HBUF = 2 * HCHUNK;            // LDS hit buffer (a chunk always fits after a flush)
+constexpr int HIT_GRID = 512;
+
+__device__ __forceinline__ void hit_body(int64_t bid, int64_t nblk, const float* __restrict__ col,
+                                         const uint8_t* __restrict__ alive, int64_t V, float eps,
+                                         int32_t* __restrict__ out, int64_t* __restrict__ ctr);
 // ---------------------------------------------------------------------------
 // split test: subpoly.py:102-105
 // ---------------------------------------------------------------------------
@@ -94,7 +102,15 @@ template <int SI>
 __global__ void __launch_bounds__(TNP_BLOCK)
 k_split_lb(int32_t* __restrict__ edges, int64_t E, int64_t ntiles, const uint8_t* __restrict__ ef,
            uint8_t* __restrict__ dm, int idx, int64_t V, int32_t* __restrict__ sa,
-           int32_t* __restrict__ sb, int64_t* __restrict__ ctr, int32_t* __restrict__ eidx, TnpLB lb) {
+           int32_t* __restrict__ sb, int64_t* __restrict__ ctr, int32_t* __restrict__ eidx, TnpLB lb,
+           HitArgs ha) {
+  if ((int64_t)blockIdx.x >= ntiles) {
+    // the plane's hit vertices (k_hit_append's work) in the same dispatch:
+    // workgroups past the split tiles (they wait on nothing)
+    hit_body((int64_t)blockIdx.x - ntiles, (int64_t)gridDim.x - ntiles, ha.col, ha.alive, ha.V, ha.eps, ha.out,
+             ctr);
+    return;
+  }
   __shared__ int cnt[SI][TNP_WAVES];
   __shared__ int64_t slot;
   const int64_t tile = blockIdx.x;  // ticket-free look-back (lb_prefix_rc)
@@ -244,19 +260,14 @@ __global__ void k_finalize_new(int64_t S, int K, int override_, const uint64_t* 
 // per flush: no tickets, no look-back (one returning atomic per workgroup on
 // one word serialises chip-wide).  alive: the live-slot flags of the lazily
 // compacted vertex set.
-constexpr int HIPT = 16;                    // slots per thread per chunk
-constexpr int HCHUNK = TNP_BLOCK * HIPT;    // slots per chunk
-constexpr int HBUF = 2 * HCHUNK;            // LDS hit buffer (a chunk always fits after a flush)
-constexpr int HIT_GRID = 512;
 
-__global__ void __launch_bounds__(TNP_BLOCK)
-k_hit_append(const float* __restrict__ col, const uint8_t* __restrict__ alive, int64_t V, float eps,
-             int32_t* __restrict__ members, int64_t S_arg, int64_t* __restrict__ ctr) {
+// one hit worker (block bid of nblk): hits appended to out[ctr[CTR_H]++]
+__device__ __forceinline__ void hit_body(int64_t bid, int64_t nblk, const float* __restrict__ col,
+                                         const uint8_t* __restrict__ alive, int64_t V, float eps,
+                                         int32_t* __restrict__ out, int64_t* __restrict__ ctr) {
   __shared__ int32_t hb[HBUF];
   __shared__ int hn;
   __shared__ int64_t hbase;
-  // S_arg < 0: launched right behind the split, whose count is on the device
-  const int64_t S = S_arg < 0 ? ctr[CTR_S] : S_arg;
   if (threadIdx.x == 0) hn = 0;
   __syncthreads();
   auto flush = [&]() {
@@ -264,12 +275,12 @@ k_hit_append(const float* __restrict__ col, const uint8_t* __restrict__ alive, i
     if (n == 0) return;
     if (threadIdx.x == 0) hbase = (int64_t)atomicAdd((unsigned long long*)&ctr[CTR_H], (unsigned long long)n);
     __syncthreads();
-    for (int q = threadIdx.x; q < n; q += TNP_BLOCK) members[S + hbase + q] = hb[q];
+    for (int q = threadIdx.x; q < n; q += TNP_BLOCK) out[hbase + q] = hb[q];
     __syncthreads();
     if (threadIdx.x == 0) hn = 0;
     __syncthreads();
   };
-  for (int64_t base = (int64_t)blockIdx.x * HCHUNK; base < V; base += (int64_t)gridDim.x * HCHUNK) {
+  for (int64_t base = bid * HCHUNK; base < V; base += nblk * HCHUNK) {
     float c[HIPT];
     uint8_t al[HIPT];
 #pragma unroll
@@ -296,6 +307,14 @@ k_hit_append(const float* __restrict__ col, const uint8_t* __restrict__ alive, i
   }
   __syncthreads();
   flush();
+}
+
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_hit_append(const float* __restrict__ col, const uint8_t* __restrict__ alive, int64_t V, float eps,
+             int32_t* __restrict__ members, int64_t S_arg, int64_t* __restrict__ ctr) {
+  // S_arg < 0: launched right behind the split, whose count is on the device
+  const int64_t S = S_arg < 0 ? ctr[CTR_S] : S_arg;
+  hit_body(blockIdx.x, gridDim.x, col, alive, V, eps, members + S, ctr);
 }
 
 __global__ void k_new_members(int32_t* __restrict__ members, int64_t S, int64_t V) {
@@ -1314,14 +1333,21 @@ int64_t run_tiles(int64_t n) { return (n + STILE - 1) / STILE; }
 
 int launch_split_lb(int32_t* edges, int64_t E, const uint8_t* sm, uint8_t* dm, int idx, int64_t V,
                     int32_t* sa, int32_t* sb, int64_t* ctr, int32_t* eidx, const TnpLB& lb,
-                    hipStream_t s) {
+                    hipStream_t s, const HitArgs* hits) {
   const int64_t tiles = split_tiles(E);
+  HitArgs ha{nullptr, nullptr, 0, 0.f, nullptr};
+  int64_t hg = 0;
+  if (hits && hits->V > 0) {
+    ha = *hits;
+    hg = std::min<int64_t>(HIT_GRID, (hits->V + HCHUNK - 1) / HCHUNK);
+  }
+  const unsigned grid = (unsigned)(tiles + hg);
   if (split_ipt(E) == SIPT_BIG)
-    hipLaunchKernelGGL(k_split_lb<SIPT_BIG>, dim3((unsigned)tiles), dim3(TNP_BLOCK), 0, s, edges, E, tiles, sm,
-                       dm, idx, V, sa, sb, ctr, eidx, lb);
+    hipLaunchKernelGGL(k_split_lb<SIPT_BIG>, dim3(grid), dim3(TNP_BLOCK), 0, s, edges, E, tiles, sm,
+                       dm, idx, V, sa, sb, ctr, eidx, lb, ha);
   else
-    hipLaunchKernelGGL(k_split_lb<SIPT_SMALL>, dim3((unsigned)tiles), dim3(TNP_BLOCK), 0, s, edges, E, tiles,
-                       sm, dm, idx, V, sa, sb, ctr, eidx, lb);
+    hipLaunchKernelGGL(k_split_lb<SIPT_SMALL>, dim3(grid), dim3(TNP_BLOCK), 0, s, edges, E, tiles,
+                       sm, dm, idx, V, sa, sb, ctr, eidx, lb, ha);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
