@@ -364,7 +364,8 @@ static int keys_for(tnp_engine* e, VSet& v, int64_t from, int64_t n, hipStream_t
 // live flags of slots [from, from + n) := 1 (kept capacity: earlier flags stay)
 static int set_alive(tnp_engine* e, int64_t from, int64_t n, hipStream_t s) {
   if (buf_ensure(e->live, std::max<int64_t>(from + n, 16), s, true)) return -1;
-  if (n > 0) TNP_CHECK(hipMemsetAsync(P<uint8_t>(e->live) + from, 1, n, s));
+  const FillOp f{P<uint8_t>(e->live) + from, (uint64_t)std::max<int64_t>(n, 0), 1};
+  if (launch_fill(&f, 1, s)) return -1;
   return 0;
 }
 
@@ -749,7 +750,8 @@ static int curve_correct(tnp_engine* e, int idx, int64_t S, hipStream_t s) {
   if (buf_ensure(cv[CV_CFLAG], S * sizeof(int32_t), s)) return -1;
   if (buf_ensure(cv[CV_COFF], S * sizeof(int64_t), s)) return -1;
   if (buf_ensure(cv[CV_CINFO], S * sizeof(int32_t), s)) return -1;
-  TNP_CHECK(hipMemsetAsync(cv[CV_CINFO].p, 0, S * sizeof(int32_t), s));
+  const FillOp f{cv[CV_CINFO].p, (uint64_t)S * sizeof(int32_t), 0};
+  if (launch_fill(&f, 1, s)) return -1;
   TIMED("curve_flags", 32.0 * S,
         launch_curve_flags(sa, sb, S, xyz, eps, P<int32_t>(cv[CV_CFLAG]), s));
   if (scan_counts(e, P<int32_t>(cv[CV_CFLAG]), P<int64_t>(cv[CV_COFF]), S, CTR_B, s)) return -1;
@@ -1539,7 +1541,8 @@ extern "C" int tnp_engine_surface(tnp_engine* e, void* stream, int64_t* V_out, i
   if (buf_ensure(e->blk, (nt + 1) * sizeof(int32_t), s)) return -1;
   if (buf_ensure(e->blkoff, (nt + 1) * sizeof(int64_t), s)) return -1;
   if (buf_ensure(e->edges_alt, std::max<int64_t>(E, 1) * 2 * sizeof(int32_t), s)) return -1;
-  TNP_CHECK(hipMemsetAsync(e->used.p, 0, V * sizeof(int32_t), s));
+  const FillOp fu{e->used.p, (uint64_t)V * sizeof(int32_t), 0};
+  if (launch_fill(&fu, 1, s)) return -1;
   if (launch_surface_edges(P<int32_t>(e->edges), E, on, P<int32_t>(e->blk), nullptr, 0, nullptr,
                            nullptr, s))
     return -1;
@@ -1713,7 +1716,8 @@ extern "C" int tnp_engine_skeleton_mode(tnp_engine* e, int unit, float size, int
   const int64_t LLL = (int64_t)L * L * L;
   if (buf_ensure(e->used, LLL * sizeof(int32_t), s)) return -1;
   if (buf_ensure(e->nid, LLL * sizeof(int64_t), s)) return -1;
-  TNP_CHECK(hipMemsetAsync(e->used.p, 0, LLL * sizeof(int32_t), s));
+  const FillOp fu{e->used.p, (uint64_t)LLL * sizeof(int32_t), 0};
+  if (launch_fill(&fu, 1, s)) return -1;
   if (mode != TNP_SKELETON_DISTANCE && mode != TNP_SKELETON_SIGN) {
     tnp_set_error("skeleton mode %d (0: distance, 1: sign)", mode);
     return -1;
@@ -1859,16 +1863,22 @@ extern "C" int tnp_engine_faces(tnp_engine* e, void* stream, int64_t* n_tri, int
       buf_ensure(fs[FS_MEMOFF], cap * 8, s) || buf_ensure(fs[FS_RID], cap * 8, s) ||
       buf_ensure(fs[FS_CUR], cap * 4, s))
     return -1;
-  TNP_CHECK(hipMemsetAsync(fs[FS_TABLE].p, 0xFF, cap * 8, s));                                // EMPTY signs
-  TNP_CHECK(hipMemsetAsync(static_cast<char*>(fs[FS_TABLE].p) + cap * 8, 0, cap * 8, s));    // NO_CELL
-  TNP_CHECK(hipMemsetAsync(fs[FS_CNT].p, 0, cap * 4, s));
-  TNP_CHECK(hipMemsetAsync(fs[FS_CUR].p, 0, cap * 4, s));
+  {  // EMPTY signs, NO_CELL, counts, cursors: one dispatch
+    const FillOp f[4] = {{fs[FS_TABLE].p, (uint64_t)cap * 8, 0xFF},
+                         {static_cast<char*>(fs[FS_TABLE].p) + cap * 8, (uint64_t)cap * 8, 0},
+                         {fs[FS_CNT].p, (uint64_t)cap * 4, 0},
+                         {fs[FS_CUR].p, (uint64_t)cap * 4, 0}};
+    if (launch_fill(f, 4, s)) return -1;
+  }
   if (launch_face_insert(V, grid, pos, zero, pmask, P<uint64_t>(fs[FS_TABLE]), (uint64_t)cap - 1,
                          P<int32_t>(fs[FS_CNT]), s))
     return -1;
   if (launch_keep_counts(P<int32_t>(fs[FS_CNT]), cap, P<int32_t>(fs[FS_KC]), P<int32_t>(fs[FS_KF]), s)) return -1;
   // padded width of r_idx_as_tensor = the largest region over ALL regions
-  TNP_CHECK(hipMemsetAsync(ctr + CTR_COMPAT, 0, sizeof(int64_t), s));
+  {
+    const FillOp f{ctr + CTR_COMPAT, sizeof(int64_t), 0};
+    if (launch_fill(&f, 1, s)) return -1;
+  }
   if (launch_max_i32(P<int32_t>(fs[FS_CNT]), cap, ctr + CTR_COMPAT, s)) return -1;
   if (scan_counts(e, P<int32_t>(fs[FS_KC]), P<int64_t>(fs[FS_MEMOFF]), cap, CTR_T, s)) return -1;
   if (scan_counts(e, P<int32_t>(fs[FS_KF]), P<int64_t>(fs[FS_RID]), cap, CTR_X, s)) return -1;
@@ -1897,8 +1907,10 @@ extern "C" int tnp_engine_faces(tnp_engine* e, void* stream, int64_t* n_tri, int
       buf_ensure(fs[FS_BCUR], V * 4, s) || buf_ensure(fs[FS_ROWS], R * 4, s) ||
       buf_ensure(fs[FS_KEEP], R * 4, s) || buf_ensure(fs[FS_KOFF], R * 8, s))
     return -1;
-  TNP_CHECK(hipMemsetAsync(fs[FS_BCNT].p, 0, V * 4, s));
-  TNP_CHECK(hipMemsetAsync(fs[FS_BCUR].p, 0, V * 4, s));
+  {
+    const FillOp f[2] = {{fs[FS_BCNT].p, (uint64_t)V * 4, 0}, {fs[FS_BCUR].p, (uint64_t)V * 4, 0}};
+    if (launch_fill(f, 2, s)) return -1;
+  }
   const uint64_t* mem = P<uint64_t>(fs[FS_MEM]);
   const int64_t* roff = P<int64_t>(fs[FS_ROFF]);
   const int32_t* rcnt = P<int32_t>(fs[FS_RCNT]);
@@ -1932,7 +1944,10 @@ extern "C" int tnp_engine_faces(tnp_engine* e, void* stream, int64_t* n_tri, int
                        fs[FS_KEY].p, P<int32_t>(fs[FS_ORDV]), P<int32_t>(fs[FS_CALL]),
                        P<int32_t>(fs[FS_CNZ]), s))
     return -1;
-  TNP_CHECK(hipMemsetAsync(ctr + CTR_TRI, 0, 2 * sizeof(int64_t), s));
+  {
+    const FillOp f{ctr + CTR_TRI, 2 * sizeof(int64_t), 0};
+    if (launch_fill(&f, 1, s)) return -1;
+  }
   if (launch_max_i32(P<int32_t>(fs[FS_CALL]), F, ctr + CTR_TRI, s)) return -1;
   if (launch_max_i32(P<int32_t>(fs[FS_CNZ]), F, ctr + CTR_FACES, s)) return -1;
   if (read_ctr(e, s)) return -1;

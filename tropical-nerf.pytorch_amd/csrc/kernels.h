@@ -133,3 +133,13 @@ int launch_keys(const NetDev& net, const float* xyz, const float* pre, int64_t l
 int scan_i32_to_i64(const int32_t* in, int64_t* out, int64_t n, int64_t* total, const TnpLB& lb,
                     hipStream_t s);
 int64_t scan_tiles(int64_t n);
+// Batched fill: up to FILL_MAX byte ranges set to a byte value in ONE
+// dispatch (hipMemsetAsync takes one fill dispatch per range, two when the
+// size is not 16-B aligned -- at bunny scale every dispatch costs ~4 us)
+struct FillOp {
+  void* p;
+  uint64_t n;     // bytes
+  uint32_t byte;  // value
+};
+constexpr int FILL_MAX = 4;
+int launch_fill(const FillOp* ops, int n, hipStream_t s);

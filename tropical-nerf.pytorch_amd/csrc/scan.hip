@@ -2,6 +2,8 @@
 // counts -> int64 offsets.  HBM-bound: 4 B read + 8 B written per element.
 // Used for every order-preserving compaction keyed by counts (cell buckets,
 // pair buckets, vertex renumbering).
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -64,6 +66,27 @@ k_scan_lb(const int32_t* __restrict__ in, int64_t n, int64_t ntiles, int64_t* __
   if (total && tile == ntiles - 1 && threadIdx.x == 0) *total = prefix + tot;
 }
 
+struct FillOps {
+  FillOp op[FILL_MAX];
+};
+// blockIdx.y: the range; 16-B stores over the aligned body, bytes at the ends
+__global__ void __launch_bounds__(TNP_BLOCK) k_fill(FillOps f) {
+  const FillOp& o = f.op[blockIdx.y];
+  uint8_t* p = static_cast<uint8_t*>(o.p);
+  const uint64_t n = o.n;
+  const uint32_t b = o.byte & 0xFFu;
+  const uint32_t w = b * 0x01010101u;
+  const uint64_t h0 = (16 - (reinterpret_cast<uintptr_t>(p) & 15)) & 15;
+  const uint64_t head = h0 < n ? h0 : n;
+  const uint64_t nb = (n - head) >> 4;  // 16-B words
+  const uint64_t tail0 = head + (nb << 4);
+  const uint64_t t = (uint64_t)blockIdx.x * TNP_BLOCK + threadIdx.x;
+  if (t < head) p[t] = (uint8_t)b;
+  if (t < n - tail0) p[tail0 + t] = (uint8_t)b;
+  uint4* q = reinterpret_cast<uint4*>(p + head);
+  for (uint64_t i = t; i < nb; i += (uint64_t)gridDim.x * TNP_BLOCK) q[i] = make_uint4(w, w, w, w);
+}
+
 }  // namespace
 
 int64_t scan_tiles(int64_t n) { return (n + TILE - 1) / TILE; }
@@ -77,6 +100,24 @@ int scan_i32_to_i64(const int32_t* in, int64_t* out, int64_t n, int64_t* total, 
   int64_t tiles = scan_tiles(n);
   hipLaunchKernelGGL(k_scan_lb, dim3((unsigned)tiles), dim3(TNP_BLOCK), 0, s, in, n, tiles, out,
                      total, lb);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int launch_fill(const FillOp* ops, int n, hipStream_t s) {
+  FillOps f{};
+  uint64_t mx = 0;
+  int k = 0;
+  for (int i = 0; i < n; ++i) {
+    if (!ops[i].p || ops[i].n == 0) continue;
+    if (k == FILL_MAX) { tnp_set_error("launch_fill: more than %d ranges", FILL_MAX); return -1; }
+    f.op[k++] = ops[i];
+    mx = std::max<uint64_t>(mx, ops[i].n);
+  }
+  if (k == 0) return 0;
+  const uint64_t words = (mx + 15) / 16;
+  const unsigned gx = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(2048, (words + TNP_BLOCK - 1) / TNP_BLOCK));
+  hipLaunchKernelGGL(k_fill, dim3(gx, k), dim3(TNP_BLOCK), 0, s, f);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
