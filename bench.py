@@ -148,13 +148,17 @@ class Collective:
     def __call__(self, vec: np.ndarray, op: str):
         if self.shm is not None:
             return self.shm(vec, op)
-        words = np.ascontiguousarray(vec.astype(np.uint64 if op == "or" else np.int64)).view(np.int64)
+        words = np.ascontiguousarray(vec.astype(np.uint64 if op in ("or", "and") else np.int64)).view(np.int64)
         t = torch.from_numpy(words.copy()).to(self.device)
         out = torch.empty(self.world * t.numel(), dtype=torch.int64, device=self.device)
         self.dist.all_gather_into_tensor(out, t)
         a = out.cpu().numpy().reshape(self.world, -1)
         if op == "or":
             return np.bitwise_or.reduce(a.view(np.uint64), axis=0).astype(vec.dtype)
+        if op == "and":
+            return np.bitwise_and.reduce(a.view(np.uint64), axis=0).astype(vec.dtype)
+        if op == "sum":
+            return a.sum(axis=0)
         return a.max(axis=0)
 
 

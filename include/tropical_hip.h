@@ -200,8 +200,24 @@ int tnp_engine_faces_export(tnp_engine* eng, int64_t* d_tri, float* d_faces,
  * edges move to the intersection of the two trilinear level sets (largest
  * real root in [0,1] of the xz-plane quartic, gradient-descent fallback) and
  * the strict filter drops splits that miss their planes.  0: flat (default).
- * Single-device only (the descent's stop criterion is global). */
+ * On x-slab shards the branch takes its whole-complex decisions through
+ * the collective of tnp_engine_set_collective. */
 int tnp_engine_set_curve(tnp_engine* eng, int on);
+
+/* Collective for the decisions a sharded engine takes inside a step (the
+ * curve branch: the curve rows' and descent rows' global counts, which pick
+ * MKL's row-count schedules, the descent's stop iteration -- an AND over
+ * the shards' per-iteration convergence words, subpoly_debug.py:141 -- and
+ * the strict filter's "some kept c row misses its plane" flag,
+ * subpoly_debug.py:253-257).  fn reduces n int64 words in place over the
+ * shards (op: TNP_COLL_SUM, _MAX, _AND, _OR bitwise) and returns 0; the
+ * engine calls it only with tnp_engine_set_shards(n > 1), every shard the
+ * same calls in the same order.  fn == NULL: none (the branch then refuses
+ * n > 1 shards).  Binds to the host language's all-reduce (the Python
+ * driver: torch.distributed, tropical/_engine.py run_steps). */
+enum { TNP_COLL_SUM = 0, TNP_COLL_MAX = 1, TNP_COLL_AND = 2, TNP_COLL_OR = 3 };
+typedef int (*tnp_collective_fn)(int64_t* vec, int n, int op, void* ctx);
+int tnp_engine_set_collective(tnp_engine* eng, tnp_collective_fn fn, void* ctx);
 
 /* Curve path: subpoly_(..., strict=...) (subpoly.py:198-203).  1 (default):
  * debug.strict_check drops splits that miss their planes
@@ -259,9 +275,10 @@ int tnp_engine_kernel_stat(tnp_engine* eng, int i, char* name, int cap, double* 
  * arrives on an atomic counter and spins until all have (no library
  * collective, no device copies).  Rank 0 creates the segment (create=1)
  * before the others open it; it can be unlinked once all have.  allreduce
- * op: TNP_SHM_MAX, TNP_SHM_OR (bitwise, 64-bit masks) or TNP_SHM_SUM. */
+ * op: TNP_SHM_MAX, TNP_SHM_OR (bitwise, 64-bit masks), TNP_SHM_SUM or
+ * TNP_SHM_AND (bitwise). */
 typedef struct tnp_shm tnp_shm;
-enum { TNP_SHM_MAX = 0, TNP_SHM_OR = 1, TNP_SHM_SUM = 2 };
+enum { TNP_SHM_MAX = 0, TNP_SHM_OR = 1, TNP_SHM_SUM = 2, TNP_SHM_AND = 3 };
 int tnp_shm_open(const char* name, int rank, int world, int create, tnp_shm** out);
 int tnp_shm_unlink(const char* name);
 void tnp_shm_close(tnp_shm* shm);

@@ -93,8 +93,10 @@ def _worker(rank, world, port, outdir, case, mode):
         if mode == "lattice":
             cuts, Vl, El = _sharded_lattice(net, rank, world, coll, stats)
             owned, first, gE, own, keep = D.stitch(Vl, El, net.enc.marks.cpu(), cuts, masks=True)
-        else:
-            eng, owned, first, gE, cuts = D.subpoly_sharded(net, 1.2, allreduce=coll, stats=stats)
+        else:  # "skeleton" (flat) or "curve" (force=False: the curve branch's decisions go
+            # through the engine's collective callback)
+            eng, owned, first, gE, cuts = D.subpoly_sharded(net, 1.2, allreduce=coll, stats=stats,
+                                                            force=mode != "curve")
             Vl, El, _ = eng.export()
             Vl, El = Vl.cpu(), El.cpu()
             own = D.owner_of(Vl, net.enc.marks.cpu(), cuts) == rank
@@ -126,6 +128,7 @@ def _unsharded(cuda, case, mode):
     eng = engine_for(net)
     eng.set_owned()
     eng.set_shards(1)
+    eng.set_curve(mode == "curve")
     if mode == "lattice":
         eng.lattice()
     else:
@@ -133,6 +136,7 @@ def _unsharded(cuda, case, mode):
     stats = []
     eng.run_steps(stats)
     V, E, _ = eng.export()
+    eng.set_curve(False)
     hv, he = complex_hash(V, E)
     return d, V, E, (V.shape[0], E.shape[0], hv, he, sum(s["S"] for s in stats))
 
@@ -157,6 +161,22 @@ def test_sharded_stanford_net(cuda, tmp_path, case, world):
     assert tuple(int(x) for x in z["tot"]) == want
     cuts = z["cuts"].tolist()
     assert cuts[0] == 0 and cuts[-1] == len(d["marks"]) - 1 and len(cuts) == world + 1
+
+
+@pytest.mark.parametrize("case,world", [("small_sphere_curve", 2), ("small_sphere_curve", 3),
+                                        ("small_torus_curve", 2)])
+def test_sharded_curve_branch(cuda, tmp_path, case, world):
+    """The curve branch (force=False) on x-slabs: the per-step decisions the
+    reference takes over the whole batch -- the curve rows' and descent rows'
+    counts (MKL's row-count schedules), the descent's stop iteration (an AND
+    of the shards' convergence words, subpoly_debug.py:141) and the strict
+    filter's flag (subpoly_debug.py:253-257) -- go through the engine's
+    collective callback (tnp_engine_set_collective); the stitched complex must
+    equal the unsharded curve run's."""
+    d, V, E, want = _unsharded(cuda, case, "curve")
+    z = _run(tmp_path, case, "curve", world)
+    assert tuple(int(x) for x in z["tot"]) == want
+    assert z["V"].shape[0] == want[0] and z["E"].shape[0] == want[1]
 
 
 @pytest.mark.timeout(600)

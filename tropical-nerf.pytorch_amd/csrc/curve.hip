@@ -909,7 +909,8 @@ k_descend(NetDev net, int64_t G, const int32_t* __restrict__ glist,
     x[d] = ints[3 * b + d];
   }
   const int j0 = plane[b];
-  const int mh = lin_mode<H, H>(G), mo = lin_mode<H, 2>(G);  // (H = 16: layer 0's mode too)
+  const int64_t Gs = net.sched_rows > 0 ? net.sched_rows : G;  // the schedule's row count (sharded: global)
+  const int mh = lin_mode<H, H>(Gs), mo = lin_mode<H, 2>(Gs);  // (H = 16: layer 0's mode too)
   uint64_t bits[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   float d0 = 1.f, d1 = 1.f;
   for (int it = 0; it < iters; ++it) {
@@ -981,7 +982,8 @@ k_descend_wave(NetDev net, int64_t G, const int32_t* __restrict__ glist,
     x[d] = ints[3 * b + d];
   }
   const int j0 = plane[b];
-  const int mh = lin_mode<H, H>(G), mo = lin_mode<H, 2>(G);  // (H = 16: layer 0's mode too)
+  const int64_t Gs = net.sched_rows > 0 ? net.sched_rows : G;  // the schedule's row count (sharded: global)
+  const int mh = lin_mode<H, H>(Gs), mo = lin_mode<H, 2>(Gs);  // (H = 16: layer 0's mode too)
   const bool one_row = G == 1;
   // lane roles
   const int nj = lane & (H - 1);                      // neuron

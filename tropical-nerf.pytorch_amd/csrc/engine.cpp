@@ -129,6 +129,8 @@ struct tnp_engine {
   int strict = 1;         // curve path: subpoly_(strict=...) -- 0 keeps every split (subpoly.py:198-202)
   int shards = 1;         // >1: one x-slab of a sharded complex
   int pend_tight = 0;
+  tnp_collective_fn coll_fn = nullptr;  // a sharded step's in-step decisions (tnp_engine_set_collective)
+  void* coll_ctx = nullptr;
   int gd_iters = 500;     // subpoly_debug.py:141
   int64_t max_pair_tests = 20000000000LL;
   bool kt_on = false;
@@ -739,6 +741,27 @@ extern "C" int tnp_engine_active_planes(tnp_engine* e, int from, uint64_t* mask,
 // of non-axis-aligned split edges to the trilinear intersection, with the
 // gradient-descent fallback; leaves per-split strict-filter inputs in cinfo.
 // ---------------------------------------------------------------------------
+// the shards' reduction of n words (tnp_engine_set_collective); one shard: none
+static int coll(tnp_engine* e, int64_t* v, int n, int op) {
+  if (e->shards <= 1) return 0;
+  if (!e->coll_fn) {
+    tnp_set_error("curve path on %d shards: no collective for its whole-complex decisions "
+                  "(tnp_engine_set_collective)", e->shards);
+    return -1;
+  }
+  if (e->coll_fn(v, n, op, e->coll_ctx) != 0) {
+    tnp_set_error("the shards' collective failed");
+    return -1;
+  }
+  return 0;
+}
+
+// curve path, phase 1 (subpoly.py:120-177, subpoly_debug.py:121-165).  On
+// shards (e->shards > 1) every shard calls it for every split step, S == 0
+// included, and takes the batch's decisions with the others: the curve rows'
+// and descent rows' totals (MKL's row-count schedules of the corner, point
+// and descent launches follow the whole batch) and the descent's stop (the
+// AND of the shards' per-iteration convergence words).
 static int curve_correct(tnp_engine* e, int idx, int64_t S, hipStream_t s) {
   const float eps = e->net.eps_s;  // subpoly_'s eps (subpoly.py:120-177)
   const int K = e->K;
@@ -747,17 +770,31 @@ static int curve_correct(tnp_engine* e, int idx, int64_t S, hipStream_t s) {
   const int32_t* sa = P<int32_t>(e->sa);
   const int32_t* sb = P<int32_t>(e->sb);
   float* xyz = P<float>(e->cur.xyz);
-  if (buf_ensure(cv[CV_CFLAG], S * sizeof(int32_t), s)) return -1;
-  if (buf_ensure(cv[CV_COFF], S * sizeof(int64_t), s)) return -1;
-  if (buf_ensure(cv[CV_CINFO], S * sizeof(int32_t), s)) return -1;
-  const FillOp f{cv[CV_CINFO].p, (uint64_t)S * sizeof(int32_t), 0};
-  if (launch_fill(&f, 1, s)) return -1;
-  TIMED("curve_flags", 32.0 * S,
-        launch_curve_flags(sa, sb, S, xyz, eps, P<int32_t>(cv[CV_CFLAG]), s));
-  if (scan_counts(e, P<int32_t>(cv[CV_CFLAG]), P<int64_t>(cv[CV_COFF]), S, CTR_B, s)) return -1;
-  if (read_ctr(e, s)) return -1;
-  const int64_t B = e->h_ctr[CTR_B];
-  if (B == 0) return 0;
+  int64_t B = 0;
+  if (S > 0) {
+    if (buf_ensure(cv[CV_CFLAG], S * sizeof(int32_t), s)) return -1;
+    if (buf_ensure(cv[CV_COFF], S * sizeof(int64_t), s)) return -1;
+    if (buf_ensure(cv[CV_CINFO], S * sizeof(int32_t), s)) return -1;
+    const FillOp f{cv[CV_CINFO].p, (uint64_t)S * sizeof(int32_t), 0};
+    if (launch_fill(&f, 1, s)) return -1;
+    TIMED("curve_flags", 32.0 * S,
+          launch_curve_flags(sa, sb, S, xyz, eps, P<int32_t>(cv[CV_CFLAG]), s));
+    if (scan_counts(e, P<int32_t>(cv[CV_CFLAG]), P<int64_t>(cv[CV_COFF]), S, CTR_B, s)) return -1;
+    if (read_ctr(e, s)) return -1;
+    B = e->h_ctr[CTR_B];
+  }
+  const bool sh = e->shards > 1;
+  int64_t Bg = B;  // the batch's curve rows (r_edges, subpoly.py:120)
+  if (coll(e, &Bg, 1, TNP_COLL_SUM)) return -1;
+  if (Bg == 0) return 0;
+  NetDev ns = e->net;  // sharded: the schedules of the whole batch
+  int64_t G = 0;
+  int32_t* crow = nullptr;
+  int32_t* plane = nullptr;
+  float* ints = nullptr;
+  float* d0s = nullptr;
+  float* d1s = nullptr;
+  if (B > 0) {
   if (buf_ensure(cv[CV_CROW], B * sizeof(int32_t), s)) return -1;
   if (buf_ensure(cv[CV_CORNERS], 24 * B * sizeof(float), s)) return -1;
   if (buf_ensure(cv[CV_PLANE], B * sizeof(int32_t), s)) return -1;
@@ -768,22 +805,24 @@ static int curve_correct(tnp_engine* e, int idx, int64_t S, hipStream_t s) {
   if (buf_ensure(cv[CV_STAGE_P], (size_t)B * K * sizeof(float), s)) return -1;
   for (int k : {CV_D0, CV_D1, CV_GG, CV_GD}) if (buf_ensure(cv[k], B * 4, s)) return -1;
   if (buf_ensure(cv[CV_GOFF], B * sizeof(int64_t), s)) return -1;
-  int32_t* crow = P<int32_t>(cv[CV_CROW]);
-  int32_t* plane = P<int32_t>(cv[CV_PLANE]);
-  float* ints = P<float>(cv[CV_INTS]);
-  float* d0s = P<float>(cv[CV_D0]);
-  float* d1s = P<float>(cv[CV_D1]);
+  crow = P<int32_t>(cv[CV_CROW]);
+  plane = P<int32_t>(cv[CV_PLANE]);
+  ints = P<float>(cv[CV_INTS]);
+  d0s = P<float>(cv[CV_D0]);
+  d1s = P<float>(cv[CV_D1]);
   if (launch_curve_rows(P<int32_t>(cv[CV_CFLAG]), P<int64_t>(cv[CV_COFF]), S, crow, s)) return -1;
   TIMED("curve_corners", 8.0 * B * 12 + 24.0 * B,
         launch_curve_corners(crow, B, sa, sb, xyz, P<uint64_t>(e->cur.zero), P<uint64_t>(e->cur.grid), idx,
                              P<float>(cv[CV_CORNERS]), plane, ctr, s));
+  if (sh) ns.sched_rows = 8 * Bg;
   TIMED("curve_forward", 8.0 * B * (12 + 4.0 * K),
-        launch_forward(e->net, P<float>(cv[CV_CORNERS]), 8 * B, P<float>(cv[CV_STAGE_C]), 8 * B, 8, s));
+        launch_forward(ns, P<float>(cv[CV_CORNERS]), 8 * B, P<float>(cv[CV_STAGE_C]), 8 * B, 8, s));
   TIMED("curve_solve", 64.0 * B + 24.0 * B,
         launch_curve_solve(B, P<float>(cv[CV_STAGE_C]), 8 * B, plane, idx, crow, sa, sb, xyz, ints,
                            P<float>(cv[CV_PTS]), s));
+  if (sh) ns.sched_rows = Bg;
   TIMED("curve_forward", B * (12 + 4.0 * K),
-        launch_forward(e->net, P<float>(cv[CV_PTS]), B, P<float>(cv[CV_STAGE_P]), B, 1, s));
+        launch_forward(ns, P<float>(cv[CV_PTS]), B, P<float>(cv[CV_STAGE_P]), B, 1, s));
   if (launch_curve_dnew(B, P<float>(cv[CV_STAGE_P]), B, plane, idx, ints, eps, d0s, d1s,
                         P<int32_t>(cv[CV_GG]), P<int32_t>(cv[CV_GD]), s)) return -1;
   if (scan_counts(e, P<int32_t>(cv[CV_GD]), P<int64_t>(cv[CV_GOFF]), B, CTR_G, s)) return -1;
@@ -799,35 +838,47 @@ static int curve_correct(tnp_engine* e, int idx, int64_t S, hipStream_t s) {
                   "exit()s, subpoly.py:141-148)", idx);
     return -1;
   }
-  const int64_t G = e->h_ctr[CTR_G];
-  if (G > 0) {
-    if (buf_ensure(cv[CV_GLIST], G * sizeof(int32_t), s)) return -1;
-    if (buf_ensure(cv[CV_CONV], 8 * sizeof(uint64_t), s)) return -1;
-    int32_t* glist = P<int32_t>(cv[CV_GLIST]);
-    unsigned long long* conv = P<unsigned long long>(cv[CV_CONV]);
-    if (launch_gd_rows(P<int32_t>(cv[CV_GD]), P<int64_t>(cv[CV_GOFF]), B, glist, s)) return -1;
-    TNP_CHECK(hipMemcpyAsync(cv[CV_INTS0].p, ints, 3 * B * sizeof(float), hipMemcpyDeviceToDevice, s));
-    TNP_CHECK(hipMemsetAsync(conv, 0xFF, 8 * sizeof(uint64_t), s));
-    TIMED("descend", 0.0,
-          launch_descend(e->net, G, glist, crow, sa, sb, xyz, plane, idx, eps, e->gd_iters, 1, ints,
-                         d0s, d1s, conv, s));
-    uint64_t h_conv[8];
-    TNP_CHECK(hipMemcpyAsync(h_conv, conv, sizeof(h_conv), hipMemcpyDeviceToHost, s));
-    TNP_CHECK(hipStreamSynchronize(s));
+  G = e->h_ctr[CTR_G];
+  }  // B > 0
+  int64_t Gg = G;  // the batch's descent rows
+  if (coll(e, &Gg, 1, TNP_COLL_SUM)) return -1;
+  if (Gg > 0) {
+    if (sh) ns.sched_rows = Gg;
+    uint64_t h_conv[8] = {~0ull, ~0ull, ~0ull, ~0ull, ~0ull, ~0ull, ~0ull, ~0ull};  // (no rows: converged)
+    int32_t* glist = nullptr;
+    unsigned long long* conv = nullptr;
+    if (G > 0) {
+      if (buf_ensure(cv[CV_GLIST], G * sizeof(int32_t), s)) return -1;
+      if (buf_ensure(cv[CV_CONV], 8 * sizeof(uint64_t), s)) return -1;
+      glist = P<int32_t>(cv[CV_GLIST]);
+      conv = P<unsigned long long>(cv[CV_CONV]);
+      if (launch_gd_rows(P<int32_t>(cv[CV_GD]), P<int64_t>(cv[CV_GOFF]), B, glist, s)) return -1;
+      TNP_CHECK(hipMemcpyAsync(cv[CV_INTS0].p, ints, 3 * B * sizeof(float), hipMemcpyDeviceToDevice, s));
+      TNP_CHECK(hipMemsetAsync(conv, 0xFF, 8 * sizeof(uint64_t), s));
+      TIMED("descend", 0.0,
+            launch_descend(ns, G, glist, crow, sa, sb, xyz, plane, idx, eps, e->gd_iters, 1, ints,
+                           d0s, d1s, conv, s));
+      TNP_CHECK(hipMemcpyAsync(h_conv, conv, sizeof(h_conv), hipMemcpyDeviceToHost, s));
+      TNP_CHECK(hipStreamSynchronize(s));
+    }
+    // the loop of subpoly_debug.py:141 stops when EVERY row of the batch met
+    // both planes: the AND of the shards' per-iteration words
+    if (coll(e, reinterpret_cast<int64_t*>(h_conv), 8, TNP_COLL_AND)) return -1;
     int stop = -1;  // first iteration after which every row met both planes
     for (int i = 0; i < e->gd_iters && stop < 0; ++i)
       if ((h_conv[i >> 6] >> (i & 63)) & 1) stop = i;
-    if (stop >= 0 && stop + 1 < e->gd_iters) {
-      // the loop of subpoly_debug.py:141 ends after iteration `stop`: replay
+    if (G > 0 && stop >= 0 && stop + 1 < e->gd_iters) {
+      // the loop ends after iteration `stop`: replay
       TNP_CHECK(hipMemcpyAsync(ints, cv[CV_INTS0].p, 3 * B * sizeof(float), hipMemcpyDeviceToDevice, s));
       TIMED("descend", 0.0,
-            launch_descend(e->net, G, glist, crow, sa, sb, xyz, plane, idx, eps, stop + 1, 0, ints,
+            launch_descend(ns, G, glist, crow, sa, sb, xyz, plane, idx, eps, stop + 1, 0, ints,
                            d0s, d1s, conv, s));
     }
   }
-  TIMED("curve_apply", 60.0 * B,
-        launch_curve_apply(B, crow, sa, sb, xyz, e->V, ints, d0s, P<int32_t>(cv[CV_GG]), eps,
-                           P<int32_t>(cv[CV_CINFO]), ctr, s));
+  if (B > 0)
+    TIMED("curve_apply", 60.0 * B,
+          launch_curve_apply(B, crow, sa, sb, xyz, e->V, ints, d0s, P<int32_t>(cv[CV_GG]), eps,
+                             P<int32_t>(cv[CV_CINFO]), ctr, s));
   return 0;
 }
 
@@ -904,6 +955,12 @@ extern "C" int tnp_engine_set_strict(tnp_engine* e, int on) {
   return 0;
 }
 
+extern "C" int tnp_engine_set_collective(tnp_engine* e, tnp_collective_fn fn, void* ctx) {
+  e->coll_fn = fn;
+  e->coll_ctx = ctx;
+  return 0;
+}
+
 extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S_out, int32_t* fail) {
   hipStream_t s = (hipStream_t)stream;
   TNP_CHECK(hipSetDevice(e->device));
@@ -968,6 +1025,13 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
                   (long long)e->V, (long long)S);
     return -1;
   }
+  // curve branch on shards: the new vertices' forward follows the schedule
+  // of the whole batch (the shards' total split count), and every shard
+  // joins the branch's decisions (curve_correct) whatever its own count
+  const bool ccoll = e->curve && e->shards > 1;
+  int64_t Sg = S;
+  if (ccoll && coll(e, &Sg, 1, TNP_COLL_SUM)) return -1;
+  if (ccoll && S == 0 && Sg > 0 && curve_correct(e, idx, 0, s)) return -1;
   if (S > 0) {
     if (vset_ensure(e, e->cur, e->V + S, e->V, s)) return -1;
     col = P<float>(e->cur.pre) + (int64_t)idx * e->cur.cap;  // may have moved
@@ -998,8 +1062,10 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
                                col, s));
     } else {
       if (buf_ensure(e->stage, (size_t)S * e->K * sizeof(float), s)) return -1;
+      NetDev nf = e->net;
+      if (ccoll) nf.sched_rows = Sg;
       TIMED("forward", (12.0 + 4.0 * e->K) * S,
-            launch_forward(e->net, P<float>(e->cur.xyz) + 3 * e->V, S, P<float>(e->stage), S, 1, s));
+            launch_forward(nf, P<float>(e->cur.xyz) + 3 * e->V, S, P<float>(e->stage), S, 1, s));
       TIMED("fail_check", 40.0 * S,
             launch_fail_check(P<int32_t>(e->sa), P<int32_t>(e->sb), S, idx, P<uint64_t>(e->cur.zero),
                               P<float>(e->stage), eps, P<uint64_t>(e->shared), P<int64_t>(e->ctr), s));
@@ -1020,6 +1086,11 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
   }
   e->pend_dup = S > 0 ? e->h_ctr[CTR_DUP] : 0;
   e->pend_tight = (S > 0 && e->curve) ? (int)e->h_ctr[CTR_TIGHT] : 0;
+  if (ccoll && Sg > 0) {  // the strict filter's flag is the batch's (subpoly_debug.py:253-257)
+    int64_t t = e->pend_tight;
+    if (coll(e, &t, 1, TNP_COLL_OR)) return -1;
+    e->pend_tight = t != 0;
+  }
   *S_out = S;
   e->pend_idx = idx;
   e->pend_S = S;
@@ -1044,6 +1115,11 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   if (e->curve) {
     if (curve_filter(e, idx, override_, s, &S_kept)) return -1;
     e->masks_valid = false;  // the filter rewired the kept split edges
+    // the kept splits another shard owns (read back with the connect
+    // counters; the split's CTR_DUP count is the flat path's)
+    TNP_CHECK(hipMemsetAsync(P<int64_t>(e->ctr) + CTR_DUP, 0, sizeof(int64_t), s));
+    if (launch_count_unowned(P<uint64_t>(e->cur.grid) + e->V, S_kept, e->own_lo, e->own_hi, P<int64_t>(e->ctr), s))
+      return -1;
   }
   const int64_t V = e->V, E = e->E, S = S_kept;
   const int64_t NV = V + S;
@@ -1453,7 +1529,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     st->pair_tests = (e->h_ctr[CTR_PCK] ? (e->h_ctr[CTR_PCK] >> 24) : e->h_ctr[CTR_TESTS]) + e->h_ctr[CTR_SPAIRS];
     st->override_applied = override_ < 0 ? (e->h_ctr[CTR_FAIL] != 0) : override_;
     st->next_active = (uint64_t)e->h_ctr[CTR_ACTIVE];
-    st->S_dup = e->pend_dup;
+    st->S_dup = e->curve ? e->h_ctr[CTR_DUP] : e->pend_dup;
     st->T = T;
   }
   e->valid = true;

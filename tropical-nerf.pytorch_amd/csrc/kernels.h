@@ -30,6 +30,9 @@ struct NetDev {
   // level-interleaved copy: entry idx of level l at float2 (idx * L + l) --
   // one 16-B gather per corner instead of L 8-B gathers in L cache lines
   int32_t tied;
+  // > 0: the row count whose MKL schedule the forward / descent launches
+  // follow (a sharded batch: the shards' total), else each launch's own
+  int64_t sched_rows;
 };
 
 static inline int net_K(const NetDev& n) { return (n.num_layers - 1) * n.num_hidden + 1; }

@@ -55,7 +55,8 @@ k_forward(NetDev net, const float* __restrict__ xyz, int64_t n, float* __restric
   encode<LV>(net, x, h);
   const float* W = w;
   int p = 0;
-  const int m0 = lin_mode<IN, H>(n), mh = lin_mode<H, H>(n), mo = lin_mode<H, 2>(n);
+  const int64_t ns = net.sched_rows > 0 ? net.sched_rows : n;  // the schedule's row count
+  const int m0 = lin_mode<IN, H>(ns), mh = lin_mode<H, H>(ns), mo = lin_mode<H, 2>(ns);
   uint64_t ps = 0, zs = 0;  // packed eps-sign keys (k_keys), when kpos is given
 #pragma unroll
   for (int layer = 0; layer < NL - 1; ++layer) {

@@ -95,7 +95,7 @@ extern "C" void tnp_shm_close(tnp_shm* s) {
 }
 
 extern "C" int tnp_shm_allreduce(tnp_shm* s, const int64_t* in, int n, int op, int64_t* out) {
-  if (n < 1 || n > SHM_WORDS || (op != TNP_SHM_MAX && op != TNP_SHM_OR && op != TNP_SHM_SUM)) {
+  if (n < 1 || n > SHM_WORDS || (op != TNP_SHM_MAX && op != TNP_SHM_OR && op != TNP_SHM_SUM && op != TNP_SHM_AND)) {
     tnp_set_error("tnp_shm_allreduce: %d words (max %d), op %d", n, SHM_WORDS, op);
     return -1;
   }
@@ -119,7 +119,7 @@ extern "C" int tnp_shm_allreduce(tnp_shm* s, const int64_t* in, int n, int op, i
     int64_t v = bank[k];
     for (int r = 1; r < s->world; ++r) {
       const int64_t w = bank[(size_t)r * SHM_WORDS + k];
-      v = op == TNP_SHM_MAX ? (w > v ? w : v) : op == TNP_SHM_OR ? (v | w) : v + w;
+      v = op == TNP_SHM_MAX ? (w > v ? w : v) : op == TNP_SHM_OR ? (v | w) : op == TNP_SHM_AND ? (v & w) : v + w;
     }
     out[k] = v;
   }

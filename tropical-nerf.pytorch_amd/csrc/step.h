@@ -83,6 +83,8 @@ int launch_finalize_new(int64_t S, int K, int override_, const uint64_t* shared,
 int launch_hits(const float* col, const uint8_t* alive, int64_t V, float eps, int32_t* members,
                 int64_t S, int64_t* ctr, hipStream_t s);
 int launch_new_members(int32_t* members, int64_t S, int64_t V, hipStream_t s);
+// new vertices (grid words) outside the owned x range (lo, hi] -> ctr[CTR_DUP] (lo > hi: nothing)
+int launch_count_unowned(const uint64_t* grid, int64_t n, int own_lo, int own_hi, int64_t* ctr, hipStream_t s);
 // sort-based cell bucketing: span counts (+ A), (cell, member) entries,
 // segment bounds of the cell-sorted entries, per-cell counts, key copies
 // M = capacity (S + V); the live member count S + ctr[CTR_H] is read on

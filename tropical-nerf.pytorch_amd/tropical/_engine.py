@@ -16,6 +16,32 @@ import torch
 from . import _hip
 
 
+
+# tnp_collective_fn (include/tropical_hip.h): ops TNP_COLL_SUM / _MAX / _AND / _OR
+_COLL_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_int64), C.c_int, C.c_int, C.c_void_p)
+_COLL_OPS = {0: "sum", 1: "max", 2: "and", 3: "or"}
+
+
+def _collective_callback(allreduce):
+    """The engine's collective as a C callback over the host-language
+    ``allreduce(vec, op)``; the returned object must stay alive while the
+    engine may call it."""
+    def fn(ptr, n, op, ctx):
+        try:
+            name = _COLL_OPS[op]
+            v = np.ctypeslib.as_array(ptr, shape=(n,))
+            if name in ("and", "or"):
+                r = np.asarray(allreduce(v.copy().view(np.uint64), name), dtype=np.uint64).view(np.int64)
+            else:
+                r = np.asarray(allreduce(v.copy(), name), dtype=np.int64)
+            v[:] = r
+            return 0
+        except Exception:  # noqa: BLE001 -- reported by the engine as a failed collective
+            import traceback
+            traceback.print_exc()
+            return 1
+    return _COLL_FN(fn)
+
 class Engine:
     def __init__(self, device: torch.device):
         self.device = torch.device(device)
@@ -207,8 +233,20 @@ class Engine:
         the split count, the override predicate and the active mask global."""
         K, H = self.K, self.num_hidden
         if allreduce is not None and getattr(self, "curve", False):
-            raise NotImplementedError("curve path (force=False) is single-device: the descent's "
-                                      "stop criterion is global (subpoly_debug.py:141)")
+            # the curve branch's in-step decisions (curve rows, descent rows,
+            # the descent's stop, the strict filter's flag) go through the
+            # same collective, called back from the engine
+            cb = _collective_callback(allreduce)
+            _hip.check(_hip.lib().tnp_engine_set_collective(self.h, C.cast(cb, C.c_void_p), None),
+                       "tnp_engine_set_collective")
+            try:
+                return self._run_steps_host(stats, allreduce)
+            finally:
+                _hip.lib().tnp_engine_set_collective(self.h, None, None)
+        return self._run_steps_host(stats, allreduce)
+
+    def _run_steps_host(self, stats, allreduce):
+        K = self.K
         if allreduce is None and not self._sharded:
             # one device: the loop runs in the library (tnp_engine_run_steps)
             buf = (_hip.TnpStepStats * max(self.K, 1))()

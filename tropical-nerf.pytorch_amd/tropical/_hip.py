@@ -87,6 +87,7 @@ SIGNATURES = {
     "tnp_engine_run_steps": (C.c_int, [_VP, _VP, C.POINTER(TnpStepStats), C.c_int, _P32]),
     "tnp_engine_set_curve": (C.c_int, [_VP, C.c_int]),
     "tnp_engine_set_strict": (C.c_int, [_VP, C.c_int]),
+    "tnp_engine_set_collective": (C.c_int, [_VP, _VP, _VP]),
     "tnp_engine_set_shards": (C.c_int, [_VP, C.c_int]),
     "tnp_debug_ops": (C.c_int, [_VP, _VP, _VP, C.c_int64, _VP, _VP]),
     "tnp_engine_faces_debug": (C.c_int, [_VP, _VP, C.c_int64, _P64, _P64, _VP]),

@@ -59,9 +59,10 @@ class ShmCollective:
     the ranks of ONE node through host shared memory (csrc/shm.cpp,
     tnp_shm_*): every rank writes its <= 8 words and spins on one atomic
     counter -- no library collective, no device copies.  Same results as an
-    all_gather + host reduction: "max" (int64), "or" (64-bit masks), "sum"."""
+    all_gather + host reduction: "max" (int64), "or" / "and" (64-bit masks),
+    "sum"."""
 
-    OPS = {"max": 0, "or": 1, "sum": 2}
+    OPS = {"max": 0, "or": 1, "sum": 2, "and": 3}
 
     def __init__(self, group=None):
         import ctypes as C
@@ -90,12 +91,13 @@ class ShmCollective:
         from . import _hip
         vec = np.asarray(vec)
         n = vec.size
-        words = np.ascontiguousarray(vec.astype(np.uint64 if op == "or" else np.int64)).view(np.int64)
+        bits = op in ("or", "and")
+        words = np.ascontiguousarray(vec.astype(np.uint64 if bits else np.int64)).view(np.int64)
         self._in[:n] = words
         _hip.check(self._lib.tnp_shm_allreduce(self.h, self._in.ctypes.data, n, self.OPS[op],
                                                self._out.ctypes.data), "tnp_shm_allreduce")
         res = self._out[:n].copy()
-        return res.view(np.uint64).astype(vec.dtype) if op == "or" else res
+        return res.view(np.uint64).astype(vec.dtype) if bits else res
 
     def close(self):
         if self.h:
@@ -331,7 +333,7 @@ def gather_complex(owned: Tensor, first: int, gedges: Tensor, dst: int = 0, grou
 
 
 def subpoly_sharded(net, size: float = 1.2, group=None, allreduce=None, stats: list = None,
-                    halo: int = None):
+                    halo: int = None, force: bool = True):
     """The hot loop of subpoly() (subpoly.py:45-69) sharded over the ranks of
     `group` (one GPU each): the skeleton (tropical.py:158-225, computed whole
     on every rank -- a few lattice passes), x-slabs of equal skeleton-edge
@@ -340,11 +342,13 @@ def subpoly_sharded(net, size: float = 1.2, group=None, allreduce=None, stats: l
     halo_check and stitch; while halo_check sees a difference, the slabs are
     redone with the next width of HALOS (halo=None), or it raises (a fixed
     halo).  Returns (engine, owned vertices, first global id, global edges,
-    cuts): the engine still holds this rank's slab complex."""
+    cuts): the engine still holds this rank's slab complex.  force=False:
+    the curve branch, its in-step decisions through the same allreduce."""
     from ._engine import engine_for
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     eng = engine_for(net)
     eng.set_shards(world)
+    eng.set_curve(not force)
     V0, E0 = eng.skeleton(unit=128, size=size)
     v, e, _ = eng.export()
     marks = net.enc.marks.to(v.device)
