@@ -113,6 +113,7 @@ struct PairLists {
   int32_t* bcell;
   int64_t bcap, chunk;
   int32_t *bcount, *bcur;
+  int32_t* perm;  // LDS-record path: every bucket's entries in cell order (entry indices; null: off)
 };
 
 // the new vertices' failover override, applied by the bucket count
@@ -589,7 +590,7 @@ __device__ __forceinline__ void group_bucket(const BGeom& G, int b, int64_t base
                                              const ulonglong2* __restrict__ pz, CellEnt* __restrict__ ents,
                                              const PairLists& pl, int64_t* __restrict__ ctr, int* cnt,
                                              int* cur, int64_t* lds, int64_t* lds3, int64_t* s_pk,
-                                             int64_t* s_sp, unsigned long long* tph) {
+                                             int64_t* s_sp, unsigned long long* tph, int32_t* perm) {
   (void)tph;
   constexpr int LC = 1 << (3 * SH);
   for (int i = threadIdx.x; i < LC; i += TNP_BLOCK) cnt[i] = 0;
@@ -622,7 +623,9 @@ __device__ __forceinline__ void group_bucket(const BGeom& G, int b, int64_t base
   __syncthreads();
   BG_PH(2);
   // records, cell-contiguous: the member keys gathered here (the members of
-  // one bucket are spatially close: their slots cluster)
+  // one bucket are spatially close: their slots cluster).  perm != null
+  // (the LDS-record path): the entries' cell order goes to perm[] instead,
+  // records are written only for the cells k_connect takes
   for (int64_t e0 = 0; e0 < n; e0 += TNP_BLOCK * GIPT) {
     uint64_t w[GIPT];
     int pos[GIPT];
@@ -635,12 +638,17 @@ __device__ __forceinline__ void group_bucket(const BGeom& G, int b, int64_t base
 #pragma unroll
     for (int k = 0; k < GIPT; ++k) {
       pos[k] = w[k] != ~0ull ? atomicAdd(&cur[(int)(w[k] >> 40)], 1) : 0;
-      k2[k] = pz[w[k] != ~0ull ? (uint32_t)w[k] : 0u];
+      const bool rec = w[k] != ~0ull && (!perm || cnt[(int)(w[k] >> 40)] > WCELL);
+      k2[k] = pz[rec ? (uint32_t)w[k] : 0u];
     }
 #pragma unroll
     for (int k = 0; k < GIPT; ++k) {
       if (w[k] == ~0ull) continue;
       const int lc = (int)(w[k] >> 40);
+      if (perm) {
+        perm[pos[k]] = (int32_t)(e0 + k * TNP_BLOCK + threadIdx.x);
+        if (cnt[lc] <= WCELL) continue;
+      }
       CellEnt r;
       r.p = k2[k].x;
       r.z = k2[k].y;
@@ -828,7 +836,7 @@ __device__ __forceinline__ void group_small(int b, int64_t base, int n, const ui
   const int64_t m = first ? (int64_t)(last - L + 1) : 0;  // this cell's members (at its first position)
   const int64_t pairs = tnp::wave_sum(m * (m - 1) / 2);
   WinAcc a;
-  window_tests(L < n ? last - L : 0, below, wa.nb, wa.fmask, wa.keys, wa.cap, wa.xs, ctr, W, a);
+  window_tests(W.st[wv], L < n ? last - L : 0, below, wa.nb, wa.fmask, wa.keys, wa.cap, wa.xs, ctr, W, a);
   window_flush(wa.keys, wa.cap, wa.xs, ctr, W, a);
   const int64_t c = tnp::wave_sum(a.n_compat), g = tnp::wave_sum(a.n_reg), x = tnp::wave_sum(a.n_conn);
   if (L == 0) bucket_stats_out(wa, b, c, g, x, pairs, ctr);
@@ -964,14 +972,32 @@ __device__ __forceinline__ int build_windows_par(int* cnt, const int* cur, uint1
   return nw;
 }
 
+// 8^3-cell buckets: 5 workgroups per CU (LDS allows 5; the LDS-record
+// path's pipeline registers would otherwise cost one: 105 VGPRs -> 4 waves
+// per SIMD, bucket_group 0.92 vs 1.04 ms per 128^3 pass at 5)
 #ifndef TNP_BG_MINB
-#define TNP_BG_MINB 1
+#define TNP_BG_MINB 5
 #endif
 #ifndef TNP_PACKED_WIN  // 0: the 32-stride window pass (A/B variant)
 #define TNP_PACKED_WIN 1
 #endif
+// LDS-record path (pl.perm != null): a bucket's records never go through
+// memory -- its cell order goes to pl.perm (4 B per entry), chunks of
+// TNP_LREC_CH record positions (+ 64 for the windows that start near a
+// chunk's end) are gathered into LDS (over the window stage and behind it)
+// and the windows starting in the chunk are tested there.  Only the cells
+// above WCELL members (k_connect's) get records in memory.
+#ifndef TNP_LREC_CH
+#define TNP_LREC_CH 192  // (256 records: the window stage's own LDS, occupancy unchanged)
+#endif
+constexpr int LREC_N = TNP_LREC_CH + 64;
+constexpr size_t WL_ST = offsetof(WinLds, st);
+constexpr size_t WL_RAW = WL_ST + (sizeof(WinLds) - WL_ST > LREC_N * sizeof(CellEnt) ? sizeof(WinLds) - WL_ST
+                                                                                     : LREC_N * sizeof(CellEnt));
+constexpr int LREC_R = (LREC_N + TNP_BLOCK - 1) / TNP_BLOCK;  // records per thread per chunk
+
 template <int SH>
-__global__ void __launch_bounds__(TNP_BLOCK, TNP_BG_MINB)
+__global__ void __launch_bounds__(TNP_BLOCK, SH == 3 ? TNP_BG_MINB : 1)
 k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __restrict__ ekv,
                const ulonglong2* __restrict__ pz, CellEnt* __restrict__ ents, WinArgs wa, PairLists pl,
                int64_t* __restrict__ ctr) {
@@ -982,7 +1008,10 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
   __shared__ int64_t lds3[3 * TNP_WAVES];
   __shared__ int64_t s_pk, s_sp;
   __shared__ int nwin_s;
-  __shared__ WinLds W;
+  constexpr bool LREC = TNP_PACKED_WIN;
+  __shared__ __attribute__((aligned(32))) unsigned char wraw[LREC ? WL_RAW : sizeof(WinLds)];
+  WinLds& W = *reinterpret_cast<WinLds*>(wraw);
+  CellEnt* const lrec = reinterpret_cast<CellEnt*>(wraw + WL_ST);
   const int b = blockIdx.x;
   const int64_t base = bbase[b];
   const int64_t n = bbase[b + 1] - base;
@@ -1012,7 +1041,10 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
   } else {
     unsigned long long tph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     BG_PH(0);
-    group_bucket<SH>(G, b, base, n, ekv, pz, ents, pl, ctr, cnt, cur, lds, lds3, &s_pk, &s_sp, tph);
+    // (a bucket of one chunk gains nothing from it: bunny-scale buckets)
+    const bool in_lds = LREC && wa.keys && pl.perm && n > LREC_N && n < 65536;
+    int32_t* const perm = in_lds ? pl.perm + base : nullptr;
+    group_bucket<SH>(G, b, base, n, ekv, pz, ents, pl, ctr, cnt, cur, lds, lds3, &s_pk, &s_sp, tph, perm);
     BG_PH(4);
     if (wa.keys) {
       // the window pass over this bucket's records, right behind their
@@ -1040,8 +1072,78 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
         }
         __syncthreads();
         BG_PH(5);
-        window_pass_packed(ents, base, reinterpret_cast<const uint32_t*>(cnt), nwin_s, tnp::wave(), TNP_WAVES,
-                           below, wa.nb, wa.fmask, wa.keys, wa.cap, wa.xs, ctr, W, a);
+        if (in_lds) {
+          // chunks of TNP_LREC_CH record positions: gather (perm -> entry ->
+          // member keys) into LDS, then test the windows that start there.
+          // Software-pipelined: the cell order of chunk j + 3, the entry
+          // words of chunk j + 2 and the member keys of chunk j + 1 are in
+          // flight while chunk j is tested
+          const uint64_t* kv = ekv + base;
+          const int nn = (int)n;
+          constexpr int CH = TNP_LREC_CH;
+          int kw = tnp::wave();  // this wave's next window (windows kw, kw + TNP_WAVES, ...)
+          int ia[LREC_R], ib[LREC_R];
+          uint64_t wa0[LREC_R], wb[LREC_R];
+          ulonglong2 ka[LREC_R], kb[LREC_R];
+          auto in_chunk = [&](int q0, int r) {
+            const int q = q0 + r * TNP_BLOCK + threadIdx.x;
+            return q < q0 + LREC_N && q < nn;
+          };
+          auto load_i = [&](int q0, int (&ix)[LREC_R]) {
+#pragma unroll
+            for (int r = 0; r < LREC_R; ++r) ix[r] = in_chunk(q0, r) ? perm[q0 + r * TNP_BLOCK + threadIdx.x] : -1;
+          };
+          auto load_w = [&](const int (&ix)[LREC_R], uint64_t (&w)[LREC_R]) {
+#pragma unroll
+            for (int r = 0; r < LREC_R; ++r) w[r] = ix[r] >= 0 ? kv[ix[r]] : 0ull;
+          };
+          auto load_k = [&](const uint64_t (&w)[LREC_R], ulonglong2 (&k)[LREC_R]) {
+#pragma unroll
+            for (int r = 0; r < LREC_R; ++r) k[r] = pz[(uint32_t)w[r]];
+          };
+          load_i(0, ia);
+          load_w(ia, wa0);
+          load_k(wa0, ka);
+          if (CH < nn) {
+            load_i(CH, ia);
+            load_w(ia, wb);
+          }
+          if (2 * CH < nn) load_i(2 * CH, ib);
+          for (int p0 = 0; p0 < nn; p0 += CH) {
+            const int p1 = min(nn, p0 + LREC_N);
+#pragma unroll
+            for (int r = 0; r < LREC_R; ++r) {
+              const int q = p0 + r * TNP_BLOCK + threadIdx.x;
+              if (q >= p1) continue;
+              CellEnt e;
+              e.p = ka[r].x;
+              e.z = ka[r].y;
+              e.v = (int32_t)(uint32_t)wa0[r];
+              e.f = (uint32_t)(wa0[r] >> 32) & 63u;
+              e.tag = (uint32_t)b * (uint32_t)LC + (uint32_t)(wa0[r] >> 40);
+              e.pad = 0;
+              lrec[q - p0] = e;
+            }
+            __syncthreads();
+            // next chunks: keys of j + 1, entry words of j + 2, order of j + 3
+            uint64_t wc[LREC_R];
+            if (p0 + CH < nn) load_k(wb, kb);
+            if (p0 + 2 * CH < nn) load_w(ib, wc);
+            if (p0 + 3 * CH < nn) load_i(p0 + 3 * CH, ib);
+            window_pass_lds(lrec, p0, p0 + CH, reinterpret_cast<const uint32_t*>(cnt), nwin_s, &kw, TNP_WAVES,
+                            below, wa.nb, wa.fmask, wa.keys, wa.cap, wa.xs, ctr, W, a);
+            __syncthreads();  // (the next chunk overwrites the records)
+#pragma unroll
+            for (int r = 0; r < LREC_R; ++r) {
+              wa0[r] = wb[r];
+              ka[r] = kb[r];
+              wb[r] = wc[r];
+            }
+          }
+        } else {
+          window_pass_packed(ents, base, reinterpret_cast<const uint32_t*>(cnt), nwin_s, tnp::wave(), TNP_WAVES,
+                             below, wa.nb, wa.fmask, wa.keys, wa.cap, wa.xs, ctr, W, a);
+        }
       } else {
         window_pass(ents, base, base + n, tnp::wave(), TNP_WAVES, below, wa.nb, wa.fmask, wa.keys, wa.cap,
                     wa.xs, ctr, W, a);
@@ -1139,9 +1241,9 @@ int launch_bucket_entries(const int32_t* members, int64_t S, int64_t V, int64_t 
 int launch_bucket_pairs(const BucketGeom& G, const int64_t* bbase, const uint64_t* ekv, const uint64_t* pz,
                         CellEnt* ents, int32_t* pcell, int32_t* pent, int32_t* pn, int64_t* ptoff, int32_t* bcell,
                         int64_t bcap, int32_t* bcount, int32_t* bcur, const ConnectWin* win, int64_t* ctr,
-                        hipStream_t s) {
+                        hipStream_t s, int32_t* perm) {
   const int NB = G.NB, sh = G.sh;
-  const PairLists pl{pcell, pent, pn, ptoff, bcell, bcap, connect_chunk_pairs(), bcount, bcur};
+  const PairLists pl{pcell, pent, pn, ptoff, bcell, bcap, connect_chunk_pairs(), bcount, bcur, perm};
   WinArgs wa{0, 0, 0ull, nullptr, 0, nullptr, nullptr};
   if (win) wa = WinArgs{win->idx, win->nb, win->fmask, win->keys, win->cap, win->xs, win->bstat};
   if (sh == 3)

@@ -89,11 +89,13 @@ __device__ __forceinline__ void lds_fence() {
 
 constexpr int WOWN = 512;  // tests of one window resolved by table (more: binary search)
 
+// st last: the grouping kernel's LDS-record path lays its record chunk over
+// st and the space behind it (bucket.hip k_bucket_group)
 struct WinLds {
-  CellEnt st[TNP_WAVES][64];
   int exc[TNP_WAVES][64];
   uint16_t own[TNP_WAVES][WOWN];  // test t -> initiator | partner << 8
   uint64_t kb[TNP_WAVES][WKEYS];
+  CellEnt st[TNP_WAVES][64];
 };
 struct WinAcc {
   int kn = 0;  // wave-uniform fill of this wave's key buffer
@@ -119,9 +121,9 @@ __device__ __forceinline__ void window_flush(uint64_t* __restrict__ keys, int64_
   a.kn = 0;
 }
 
-// the pair tests of one staged window (W.st[wave][0..63]): lane L initiates
+// the pair tests of one staged window (st[0..63], LDS): lane L initiates
 // `rounds` tests, against the next `rounds` records of its cell
-__device__ __forceinline__ void window_tests(int rounds, uint64_t below, int nb, uint64_t fmask,
+__device__ __forceinline__ void window_tests(const CellEnt* st, int rounds, uint64_t below, int nb, uint64_t fmask,
                                              uint64_t* __restrict__ keys, int64_t cap, int64_t* __restrict__ xs,
                                              int64_t* __restrict__ ctr, WinLds& W, WinAcc& a);
 
@@ -153,7 +155,7 @@ __device__ __forceinline__ void window_pass(const CellEnt* __restrict__ ent, int
     const uint64_t bm = __ballot(L == 63 || nxt != r.tag);
     const int last = L + __builtin_ctzll(bm >> L);
     const bool init = valid && L < WSTRIDE && !(r.tag & 0x80000000u);
-    window_tests(init ? last - L : 0, below, nb, fmask, keys, cap, xs, ctr, W, a);
+    window_tests(W.st[wv], init ? last - L : 0, below, nb, fmask, keys, cap, xs, ctr, W, a);
   }
 }
 
@@ -188,11 +190,34 @@ __device__ __forceinline__ void window_pass_packed(const CellEnt* __restrict__ e
     const uint64_t bm = __ballot(L == 63 || nxt != r.tag);
     const int last = L + __builtin_ctzll(bm >> L);
     const bool init = valid && !(r.tag & 0x80000000u);  // (windows hold no big cell; defensive)
-    window_tests(init ? last - L : 0, below, nb, fmask, keys, cap, xs, ctr, W, a);
+    window_tests(W.st[wv], init ? last - L : 0, below, nb, fmask, keys, cap, xs, ctr, W, a);
   }
 }
 
-__device__ __forceinline__ void window_tests(int rounds, uint64_t below, int nb, uint64_t fmask,
+// Packed windows over records already in LDS (the grouping kernel's record
+// chunk: rec[p - p0] holds the bucket's record p): the windows of wl[] from
+// this wave's cursor *k (windows k, k + dw, ...) that start before p_end
+__device__ __forceinline__ void window_pass_lds(const CellEnt* rec, int p0, int p_end, const uint32_t* wl, int nwin,
+                                                int* k, int dw, uint64_t below, int nb, uint64_t fmask,
+                                                uint64_t* __restrict__ keys, int64_t cap,
+                                                int64_t* __restrict__ xs, int64_t* __restrict__ ctr,
+                                                WinLds& W, WinAcc& a) {
+  const int L = tnp::lane();
+  for (; *k < nwin; *k += dw) {
+    const uint32_t se = wl[*k];
+    const int s = (int)(se & 0xFFFFu), n = (int)(se >> 16) - s;
+    if (s >= p_end) break;
+    const CellEnt* st = rec + (s - p0);
+    const bool valid = L < n;
+    const uint32_t tag = valid ? st[L].tag : 0xFFFFFFFFu;
+    const uint32_t nxt = __shfl_down(tag, 1, 64);
+    const uint64_t bm = __ballot(L >= n - 1 || nxt != tag);  // (the window holds whole cells)
+    const int last = L + __builtin_ctzll(bm >> L);
+    window_tests(st, valid ? last - L : 0, below, nb, fmask, keys, cap, xs, ctr, W, a);
+  }
+}
+
+__device__ __forceinline__ void window_tests(const CellEnt* st, int rounds, uint64_t below, int nb, uint64_t fmask,
                                              uint64_t* __restrict__ keys, int64_t cap, int64_t* __restrict__ xs,
                                              int64_t* __restrict__ ctr, WinLds& W, WinAcc& a) {
   const int wv = tnp::wave(), L = tnp::lane();
@@ -258,8 +283,8 @@ __device__ __forceinline__ void window_tests(int rounds, uint64_t below, int nb,
       int ja, ia, jb, ib;
       pair_of(ta, ja, ia);
       pair_of(lb ? tb : ta, jb, ib);
-      const CellEnt ua = W.st[wv][ja], qa = W.st[wv][ia];
-      const CellEnt ub = W.st[wv][jb], qb = W.st[wv][ib];
+      const CellEnt ua = st[ja], qa = st[ia];
+      const CellEnt ub = st[jb], qb = st[ib];
       uint64_t ka, kb;
       const bool ema = test(ua, qa, true, ka);
       const bool emb = test(ub, qb, lb, kb);
@@ -272,8 +297,8 @@ __device__ __forceinline__ void window_tests(int rounds, uint64_t below, int nb,
       const bool live = t < total;
       int j = 0, i = 0;
       pair_of(live ? t : 0, j, i);
-      const CellEnt u = W.st[wv][j];
-      const CellEnt q = W.st[wv][i];
+      const CellEnt u = st[j];
+      const CellEnt q = st[i];
       uint64_t key;
       const bool em = test(u, q, live, key);
       append(em, key);

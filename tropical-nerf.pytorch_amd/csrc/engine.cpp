@@ -209,6 +209,7 @@ struct tnp_engine {
   Buf bk[14];               // bucket.hip scratch (per-bucket counts, bases, pair-cell areas)
   bool radix_cells = false; // TNP_RADIX_CELLS=1: the radix-sort bucketing path
   bool lazy_edges = true;   // TNP_LAZY_EDGES=0: every pruning step compacts the edge list
+  bool lds_records = true;  // TNP_LDS_RECORDS=0: the grouping's records go through memory
   bool bk_clean = false;    // bucket counters (bk[0], bk[1]) are zero
   Buf cv[CV_N];
 };
@@ -505,6 +506,7 @@ extern "C" int tnp_engine_create(tnp_engine** out, int device) {
   if (const char* lim = getenv("TNP_MAX_PAIR_TESTS")) e->max_pair_tests = atoll(lim);
   if (const char* rc = getenv("TNP_RADIX_CELLS")) e->radix_cells = atoi(rc) != 0;
   if (const char* lz = getenv("TNP_LAZY_EDGES")) e->lazy_edges = atoi(lz) != 0;
+  if (const char* lr = getenv("TNP_LDS_RECORDS")) e->lds_records = atoi(lr) != 0;
   if (const char* sp = getenv("TNP_LB_SPIN")) e->lb_spin = atoi(sp);
   if (hipHostMalloc((void**)&e->h_ctr, CTR_N * sizeof(int64_t), hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc((void**)&e->h_map, 32 * sizeof(int64_t), hipHostMallocMapped | hipHostMallocCoherent) !=
@@ -1308,12 +1310,15 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
       // WCELL members) + pair-cell lists and k_connect's chunk table (bcap)
       if (buf_ensure(e->bcell, bcap * sizeof(int32_t), s)) return -1;
       const ConnectWin cw{idx, nb, cfmask, P<uint64_t>(e->ckeys_a), cap, xs, bstat};
+      // the LDS-record path's cell-order scratch (TNP_LDS_RECORDS=0: off)
+      const bool lrec = e->lds_records;
+      if (lrec && buf_ensure(e->bk[4], TB * sizeof(int32_t), s)) return -1;
       TIMED("bucket_group", 0.0,
             launch_bucket_pairs(bg, P<int64_t>(e->bk[2]), P<uint64_t>(e->sents),
                                 P<uint64_t>(c.pz), P<CellEnt>(e->ents), P<int32_t>(e->pcell),
                                 P<int32_t>(e->pent), P<int32_t>(e->pcn), P<int64_t>(e->ptoff),
                                 P<int32_t>(e->bcell), bcap, P<int32_t>(e->bk[0]), P<int32_t>(e->bk[1]),
-                                &cw, ctr, s));
+                                &cw, ctr, s, lrec ? P<int32_t>(e->bk[4]) : nullptr));
       e->bk_clean = true;
     } else if (!chunks_ok) {
       if (buf_ensure(e->bcell, bcap * sizeof(int32_t), s)) return -1;
@@ -1354,8 +1359,11 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
       // every record (once, algorithmically) and writes the kept keys
       ktimer_set_bytes(e, "bucket_entries", 16.0 * M + 8.0 * T);
       // the window pass re-reads the records the same workgroup just wrote
-      // (cache traffic): its compulsory bytes are the kept keys
-      ktimer_set_bytes(e, "bucket_group", 56.0 * T + 8.0 * e->h_ctr[CTR_XK]);
+      // (cache traffic): its compulsory bytes are the kept keys.  LDS-record
+      // path: 8 B entry word + 16 B member keys + 4 + 4 B cell order (written,
+      // read back) per entry, records in memory only for k_connect's cells
+      // (not counted: an understatement)
+      ktimer_set_bytes(e, "bucket_group", (e->lds_records ? 32.0 : 56.0) * T + 8.0 * e->h_ctr[CTR_XK]);
     }
     TT = e->h_ctr[CTR_TESTS];
     X = e->h_ctr[CTR_XK];

@@ -299,7 +299,7 @@ struct ConnectWin {
 int launch_bucket_pairs(const BucketGeom& g, const int64_t* bbase, const uint64_t* ekv, const uint64_t* pz,
                         CellEnt* ents, int32_t* pcell, int32_t* pent, int32_t* pn, int64_t* ptoff, int32_t* bcell,
                         int64_t bcap, int32_t* bcount, int32_t* bcur, const ConnectWin* win, int64_t* ctr,
-                        hipStream_t s);
+                        hipStream_t s, int32_t* perm = nullptr);  // perm: T int32 scratch (LDS-record path; null: off)
 constexpr int64_t PCK_CELLS = 1 << 24;  // CTR_PCK: cell count field
 // pair indices per k_connect chunk (its bcell table granularity)
 int64_t connect_chunk_pairs();
