@@ -1439,7 +1439,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
       if (buf_ensure(e->edges, N1 * 2 * sizeof(int32_t), s, true)) return -1;
       if (buf_ensure(e->edm, N1 * sizeof(uint8_t), s, true)) return -1;
       if (buf_ensure(e->eef, N1 * sizeof(uint8_t), s, true)) return -1;
-      if (buf_ensure(e->lzpart, PRUNE_LAZY_MAX_BLOCKS * sizeof(int64_t), s)) return -1;
+      if (buf_ensure(e->lzpart, prune_lazy_blocks(N) * sizeof(int64_t), s)) return -1;
       // old edges: 1 B high plane (+ 1 B first split plane, 8 B ids when
       // kept); e_new / c_new: 4 / 8 B ids + 32 B endpoint keys, 10 B written
       TIMED("prune", 1.0 * E + 36.0 * S + 40.0 * X,

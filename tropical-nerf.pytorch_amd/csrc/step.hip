@@ -1574,8 +1574,12 @@ int launch_prune_lb(const int32_t* edges, int64_t E, const int32_t* sb, int64_t 
   return 0;
 }
 int prune_lazy_blocks(int64_t N) {
-  return (int)std::max<int64_t>(1, std::min<int64_t>(PRUNE_LAZY_MAX_BLOCKS,
-                                                     (N + TNP_BLOCK * LZ_IPT - 1) / (TNP_BLOCK * LZ_IPT)));
+  static const int64_t s_max = [] {  // TNP_PL_BLOCKS: the grid cap (experiments)
+    const char* v = getenv("TNP_PL_BLOCKS");
+    const int64_t b = v ? atoll(v) : PRUNE_LAZY_MAX_BLOCKS;
+    return b > 0 ? b : (int64_t)PRUNE_LAZY_MAX_BLOCKS;
+  }();
+  return (int)std::max<int64_t>(1, std::min<int64_t>(s_max, (N + TNP_BLOCK * LZ_IPT - 1) / (TNP_BLOCK * LZ_IPT)));
 }
 int launch_prune_lazy(int32_t* edges, int64_t E, const int32_t* sb, int64_t S, int64_t V, const uint64_t* ckeys,
                       int nb, int64_t X, int idx, int last_plane, const uint64_t* pz, uint8_t* dm, uint8_t* ef,
