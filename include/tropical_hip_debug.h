@@ -33,6 +33,11 @@ int tnp_engine_faces_debug(tnp_engine* eng, float* d_scores, int64_t cap, int64_
 int tnp_engine_debug_set_lb_spin(tnp_engine* eng, int spin);
 int tnp_engine_debug_lb_recomputes(tnp_engine* eng, int64_t* n, int reset, void* stream);
 
+/* Debug: the grouping kernel's LDS-record path (csrc/bucket.hip
+ * k_bucket_group; on by default, TNP_LDS_RECORDS=0 at engine creation turns
+ * it off): on = 0 sends every bucket's records through memory, as before. */
+int tnp_engine_debug_set_lds_records(tnp_engine* eng, int on);
+
 #ifdef __cplusplus
 }
 #endif

@@ -306,6 +306,30 @@ def test_lookback_recompute_path(cuda):
         assert (g[0], g[1], g[2]) == (V, E, s)
 
 
+@pytest.mark.parametrize("name", ["synth32", "synth64h"])
+def test_lds_record_path(cuda, name):
+    """The grouping kernel keeps the records of buckets above one chunk in
+    LDS (csrc/bucket.hip k_bucket_group: cell order in memory, 192-position
+    chunks gathered three deep); every step state must be bitwise the same
+    with the path off (records through memory) and equal to the reference's
+    step records (synth64h: buckets of thousands of entries, many chunks)."""
+    from tropical._engine import engine_for
+    d = load(name)
+    net = product_net(d, cuda)
+    eng = engine_for(net)
+    runs = []
+    try:
+        for on in (True, False):
+            eng.debug_lds_records(on)
+            eng.lattice(keep_all=True)
+            runs.append(engine_steps(eng))
+    finally:
+        eng.debug_lds_records(True)
+    assert runs[0] == runs[1]
+    for g, V, E, s in zip(runs[0], d["step_V"], d["step_E"], d["step_sha"]):
+        assert (g[0], g[1], g[2]) == (V, E, s)
+
+
 @pytest.mark.parametrize("force", [True, False])
 def test_subpoly_step_rewrites_caller_edges(cuda, force):
     """subpoly.py:209-212: a splitting step rewrites the caller's edges[:, 1]

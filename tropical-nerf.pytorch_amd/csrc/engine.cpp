@@ -2159,6 +2159,10 @@ extern "C" int tnp_engine_debug_set_lb_spin(tnp_engine* e, int spin) {
   e->lb_spin = spin;
   return 0;
 }
+extern "C" int tnp_engine_debug_set_lds_records(tnp_engine* e, int on) {
+  e->lds_records = on != 0;
+  return 0;
+}
 extern "C" int tnp_engine_debug_lb_recomputes(tnp_engine* e, int64_t* n, int reset, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   TNP_CHECK(hipSetDevice(e->device));

@@ -170,6 +170,13 @@ class Engine:
             out[name.value.decode()] = {"ms": ms.value, "launches": nl.value, "bytes": by.value}
         return out
 
+    def debug_lds_records(self, on: bool):
+        """The grouping kernel's LDS-record path on / off (csrc/bucket.hip;
+        off: every bucket's records go through memory)."""
+        _hip.check(_hip.lib().tnp_engine_debug_set_lds_records(self.h, int(bool(on))),
+                   "tnp_engine_debug_set_lds_records")
+        return self
+
     def debug_lb(self, spin: int = None, reset: bool = True) -> int:
         """Diagnostics of the ticket-free look-back (common.h lb_prefix_rc):
         spin != None sets the polls before a recompute (0: always recompute,

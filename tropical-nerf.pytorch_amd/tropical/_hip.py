@@ -92,6 +92,7 @@ SIGNATURES = {
     "tnp_debug_ops": (C.c_int, [_VP, _VP, _VP, C.c_int64, _VP, _VP]),
     "tnp_engine_faces_debug": (C.c_int, [_VP, _VP, C.c_int64, _P64, _P64, _VP]),
     "tnp_engine_debug_set_lb_spin": (C.c_int, [_VP, C.c_int]),
+    "tnp_engine_debug_set_lds_records": (C.c_int, [_VP, C.c_int]),
     "tnp_engine_debug_lb_recomputes": (C.c_int, [_VP, _P64, C.c_int, _VP]),
     "tnp_engine_kernel_timer": (C.c_int, [_VP, C.c_int, _VP, _P32]),
     "tnp_mc_count": (C.c_int, [_VP, C.c_int, C.c_int, C.c_int, _F, _VP, _VP, _VP, _P64, _P64, _VP]),
