@@ -109,10 +109,12 @@ class Engine:
         _hip.check(_hip.lib().tnp_engine_sizes(self.h, C.byref(V), C.byref(E)), "tnp_engine_sizes")
         return V.value, E.value
 
-    def export(self, pre: bool = False):
+    def export(self, pre: bool = False, edges: bool = True):
+        """(vertices [V, 3], edges [E, 2] int64 or None when edges=False,
+        cache [V, K] when pre) of the compacted complex."""
         V, E = self.sizes()
         verts = torch.empty(V, 3, device=self.device)
-        edges = torch.empty(E, 2, dtype=torch.int64, device=self.device)
+        edges = torch.empty(E, 2, dtype=torch.int64, device=self.device) if edges else None
         cache = torch.empty(V, self.K, device=self.device) if pre else None
         _hip.check(_hip.lib().tnp_engine_export(self.h, _hip.ptr(verts), _hip.ptr(edges),
                                                 _hip.ptr(cache), self._s), "tnp_engine_export")

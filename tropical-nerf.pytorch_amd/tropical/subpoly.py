@@ -59,7 +59,7 @@ def _finish(eng, net):
     if sV == 0:
         print("0 faces", end=", ")
         return [], torch.zeros(0, dtype=torch.int64, device=eng.device), []
-    verts, _, _ = eng.export()
+    verts, _, _ = eng.export(edges=False)  # (the faces need no edge list)
     tri, fc = eng.faces()
     faces, fwi = _faces_to_numpy(tri, fc)
     print(f"{len(faces)} faces", end=", ")
