@@ -557,6 +557,97 @@ k_bucket_scatter(const int32_t* __restrict__ members, int64_t S, int64_t V, int6
   }
 }
 
+// (3') sub geometries: each 16^3-cell bucket's entries regrouped by octant
+// (8^3 cells), the group buckets 8 b + o.  One workgroup per bucket; each
+// wave takes a contiguous quarter of the bucket's entries and walks it twice:
+// octant counts (wave ballots, counts in scalar registers), then placement
+// at wave-private cursors (the waves' octant counts scanned in LDS) -- no
+// atomics.  The order inside an octant is free (as inside a bucket: nothing
+// downstream depends on it)
+constexpr int RF_U = 8;          // entries per lane in flight
+constexpr int RF_THREADS = 1024;  // 16 waves per bucket: short serial walks (each iteration waits on HBM)
+constexpr int RF_WAVES = RF_THREADS / 64;
+__device__ __forceinline__ int refine_octant(uint64_t w) {
+  const uint32_t lc = (uint32_t)(w >> 40);  // 16^3 local cell: x bits 8..11, y 4..7, z 0..3
+  return (int)(((lc >> 9) & 4u) | ((lc >> 6) & 2u) | ((lc >> 3) & 1u));
+}
+__global__ void __launch_bounds__(RF_THREADS)
+k_bucket_refine(int NB, const int64_t* __restrict__ bbase, const uint64_t* __restrict__ ekv,
+                int64_t* __restrict__ bbase2, uint64_t* __restrict__ ekv2, int32_t* __restrict__ bcount,
+                int32_t* __restrict__ bcur) {
+  __shared__ int64_t wc[RF_WAVES][8];
+  const int b = blockIdx.x, t = threadIdx.x, L = tnp::lane(), wv = tnp::wave();
+  const int64_t base = bbase[b], n = bbase[b + 1] - base;
+  if (t == 0) {  // the member passes' counters, clean for the next step
+    bcount[b] = 0;
+    bcur[b] = 0;
+    if (b == NB - 1) bbase2[8 * (int64_t)NB] = bbase[NB];
+  }
+  const int64_t r0 = base + n * wv / RF_WAVES, r1 = base + n * (wv + 1) / RF_WAVES;
+  int64_t c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int64_t e0 = r0; e0 < r1; e0 += 64 * RF_U) {
+    uint64_t w[RF_U];
+#pragma unroll
+    for (int k = 0; k < RF_U; ++k) {
+      const int64_t e = e0 + 64 * k + L;
+      w[k] = e < r1 ? ekv[e] : ~0ull;
+    }
+#pragma unroll
+    for (int k = 0; k < RF_U; ++k) {
+      const int o = w[k] != ~0ull ? refine_octant(w[k]) : 8;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) c[q] += __popcll(__ballot(o == q));
+    }
+  }
+  if (L == 0)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) wc[wv][q] = c[q];
+  __syncthreads();
+  // this wave's cursors: the bucket base, the earlier octants, the earlier
+  // waves' share of this octant
+  int64_t cur[8];
+  {
+    int64_t off = base;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      int64_t tot = 0, before = 0;
+#pragma unroll
+      for (int w = 0; w < RF_WAVES; ++w) {
+        tot += wc[w][q];
+        before += w < wv ? wc[w][q] : 0;
+      }
+      if (wv == 0 && L == q) bbase2[8 * (int64_t)b + q] = off;
+      cur[q] = off + before;
+      off += tot;
+    }
+  }
+  for (int64_t e0 = r0; e0 < r1; e0 += 64 * RF_U) {
+    uint64_t w[RF_U];
+#pragma unroll
+    for (int k = 0; k < RF_U; ++k) {
+      const int64_t e = e0 + 64 * k + L;
+      w[k] = e < r1 ? ekv[e] : ~0ull;
+    }
+#pragma unroll
+    for (int k = 0; k < RF_U; ++k) {
+      const bool live = w[k] != ~0ull;
+      const int o = live ? refine_octant(w[k]) : 8;
+      int64_t pos = 0;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const uint64_t m = __ballot(o == q);
+        if (o == q) pos = cur[q] + tnp::mbcnt(m);
+        cur[q] += __popcll(m);
+      }
+      if (live) {
+        const uint32_t lc = (uint32_t)(w[k] >> 40);
+        const uint64_t l3 = ((lc >> 2) & 0x1C0u) | ((lc >> 1) & 0x38u) | (lc & 7u);
+        ekv2[pos] = (l3 << 40) | (w[k] & 0xFFFFFFFFFFull);
+      }
+    }
+  }
+}
+
 // (4) one block per bucket: counting sort by local cell in LDS, records,
 // the bucket's pair cells.  Pair-cell lists are written to the bucket's own
 // area [bbase / 2, bbase / 2 + n / 2] (a pair cell holds >= 2 entries).
@@ -581,6 +672,21 @@ __device__ __forceinline__ void put_pair_cell(int64_t o, int64_t lo, int32_t cel
   const int64_t b0 = (lo + pl.chunk - 1) / pl.chunk, b1 = (lo + n + pl.chunk - 1) / pl.chunk;
   if (b1 > pl.bcap) atomicOr((unsigned long long*)&ctr[CTR_BOVF], 1ull);
   for (int64_t q = b0; q < b1 && q < pl.bcap; ++q) pl.bcell[q] = (int32_t)o;
+}
+
+// the first cell (+2 coordinates) of group bucket b: a member-pass bucket,
+// or (sub geometries) octant b & 7 of member-pass bucket b >> 3
+__device__ __forceinline__ void group_origin(const BGeom& G, int b, int& ox, int& oy, int& oz) {
+  const int B = G.sub ? b >> 3 : b;
+  const int bz = B % G.NBd, by = (B / G.NBd) % G.NBd, bx = B / (G.NBd * G.NBd);
+  ox = G.xorg + (bx << G.sh);
+  oy = by << G.sh;
+  oz = bz << G.sh;
+  if (G.sub) {
+    ox += ((b >> 2) & 1) << 3;
+    oy += ((b >> 1) & 1) << 3;
+    oz += (b & 1) << 3;
+  }
 }
 
 // the grouping of one bucket of n >= 2 entries (k_bucket_group)
@@ -722,14 +828,15 @@ __device__ __forceinline__ void group_bucket(const BGeom& G, int b, int64_t base
   const int64_t o0 = (*s_pk & (PCK_CELLS - 1)) + opc, p0 = (*s_pk >> 24) + op;
   opc = 0;
   op = 0;
-  const int m_ = (1 << G.sh) - 1;
-  const int bz = b % G.NBd, by = (b / G.NBd) % G.NBd, bx = b / (G.NBd * G.NBd);
+  constexpr int m_ = (1 << SH) - 1;
+  int ox, oy, oz;
+  group_origin(G, b, ox, oy, oz);
   for (int i = c0; i < c0 + per && i < LC; ++i) {
     const int m = cnt[i];
     if (m > WCELL && m <= 65535) {
-      const int cx = G.xorg + ((bx << G.sh) | (i >> (2 * G.sh)));
-      const int cy = (by << G.sh) | ((i >> G.sh) & m_);
-      const int cz = (bz << G.sh) | (i & m_);
+      const int cx = ox + (i >> (2 * SH));
+      const int cy = oy + ((i >> SH) & m_);
+      const int cz = oz + (i & m_);
       put_pair_cell(o0 + opc, p0 + op, (int32_t)((cx * G.NC + cy) * G.NC + cz), (int32_t)(base + cur[i] - m), m,
                     pl, ctr);
       ++opc;
@@ -1015,8 +1122,8 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
   const int b = blockIdx.x;
   const int64_t base = bbase[b];
   const int64_t n = bbase[b + 1] - base;
-  if (threadIdx.x == 0) {  // the bucket counters are clean for the next step (read by the member passes)
-    pl.bcount[b] = 0;
+  if (threadIdx.x == 0 && !G.sub) {  // the bucket counters are clean for the next step (read by the member
+    pl.bcount[b] = 0;                 // passes; sub geometries: the refine pass zeroes them)
     pl.bcur[b] = 0;
   }
   if (n < 2) {
@@ -1178,12 +1285,19 @@ int bucket_geometry(int n_marks, int x0, int x1, BucketGeom* g) {
     const char* v = getenv("TNP_BUCKET_SH");
     return v ? atoi(v) : 0;
   }();
-  for (int s = (s_env == 4 ? 4 : 3); s <= 4; ++s) {
+  static const int s_sub = [] {  // TNP_BUCKET_SUB=0: never two-level, 1: always (experiments)
+    const char* v = getenv("TNP_BUCKET_SUB");
+    return v ? atoi(v) : -1;
+  }();
+  for (int s = (s_env == 4 || s_sub == 1 ? 4 : 3); s <= 4; ++s) {
     const int nbd = (NC + (1 << s) - 1) >> s;
     const int nbx = (xhi - xlo + 1 + (1 << s) - 1) >> s;
     const int64_t nb = (int64_t)nbx * nbd * nbd;
     if (nb > BUCKET_MAX) continue;
-    *g = BucketGeom{NC, s, nbd, nbx, xlo, nbx << s, (int)nb};
+    // 16^3-cell member buckets are refined into 8^3-cell group buckets
+    // unless TNP_BUCKET_SH=4 asks for the 16^3-cell grouping kernel
+    const int sub = s == 4 && s_env != 4 && s_sub != 0;
+    *g = BucketGeom{NC, s, nbd, nbx, xlo, nbx << s, (int)nb, sub, sub ? 8 * (int)nb : (int)nb};
     return 0;
   }
   return -1;
@@ -1238,11 +1352,23 @@ int launch_bucket_entries(const int32_t* members, int64_t S, int64_t V, int64_t 
   return 0;
 }
 
+int launch_bucket_refine(const BucketGeom& G, const int64_t* bbase, const uint64_t* ekv, int64_t* bbase2,
+                         uint64_t* ekv2, int32_t* bcount, int32_t* bcur, hipStream_t s) {
+  if (!G.sub || G.sh != 4) {
+    tnp_set_error("bucket refine: not a two-level geometry");
+    return -1;
+  }
+  hipLaunchKernelGGL(k_bucket_refine, dim3(G.NB), dim3(RF_THREADS), 0, s, G.NB, bbase, ekv, bbase2, ekv2, bcount,
+                     bcur);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+
 int launch_bucket_pairs(const BucketGeom& G, const int64_t* bbase, const uint64_t* ekv, const uint64_t* pz,
                         CellEnt* ents, int32_t* pcell, int32_t* pent, int32_t* pn, int64_t* ptoff, int32_t* bcell,
                         int64_t bcap, int32_t* bcount, int32_t* bcur, const ConnectWin* win, int64_t* ctr,
                         hipStream_t s, int32_t* perm) {
-  const int NB = G.NB, sh = G.sh;
+  const int NB = G.NG, sh = G.sub ? 3 : G.sh;
   const PairLists pl{pcell, pent, pn, ptoff, bcell, bcap, connect_chunk_pairs(), bcount, bcur, perm};
   WinArgs wa{0, 0, 0ull, nullptr, 0, nullptr, nullptr};
   if (win) wa = WinArgs{win->idx, win->nb, win->fmask, win->keys, win->cap, win->xs, win->bstat};

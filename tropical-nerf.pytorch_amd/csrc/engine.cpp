@@ -206,6 +206,7 @@ struct tnp_engine {
   Buf fscr[12];
   Buf fscr2[32];
   Buf sents;                // bucket-ordered packed entries before the in-bucket grouping
+  Buf sents2;               // ... regrouped by octant (two-level bucket geometries, bk[8]: their bases)
   Buf bk[14];               // bucket.hip scratch (per-bucket counts, bases, pair-cell areas)
   bool radix_cells = false; // TNP_RADIX_CELLS=1: the radix-sort bucketing path
   bool lazy_edges = true;   // TNP_LAZY_EDGES=0: every pruning step compacts the edge list
@@ -544,6 +545,7 @@ extern "C" void tnp_engine_destroy(tnp_engine* e) {
   for (Buf& b : e->fscr2) buf_free(b, s);
   for (Buf& b : e->bk) buf_free(b, s);
   buf_free(e->sents, s);
+  buf_free(e->sents2, s);
   for (Buf& b : e->cv) buf_free(b, s);
   for (Buf* b : {&e->spcnt, &e->spoff, &e->part, &e->ekey_a, &e->ekey_b, &e->eval_b,
                  &e->sort_scr2})
@@ -1212,6 +1214,15 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
                                 prune ? P<uint8_t>(e->live) : nullptr, NV, e->pend_fused ? &nov : nullptr,
                                 ctr, s));
     e->bk_clean = false;  // until the grouping's pair-cell gather has reset the counters
+    if (bg.sub) {
+      // two-level geometry: the 16^3-cell buckets split into their 8^3-cell
+      // octants (the grouping's buckets); the refine resets the counters
+      if (buf_ensure(e->bk[8], ((int64_t)bg.NG + 1) * sizeof(int64_t), s)) return -1;
+      if (buf_ensure(e->sents2, TB * sizeof(uint64_t), s)) return -1;
+      TIMED("bucket_refine", 24.0 * M,  // 8 B read twice + 8 B written per entry (set once T is known)
+            launch_bucket_refine(bg, P<int64_t>(e->bk[2]), P<uint64_t>(e->sents), P<int64_t>(e->bk[8]),
+                                 P<uint64_t>(e->sents2), P<int32_t>(e->bk[0]), P<int32_t>(e->bk[1]), s));
+    }
   } else {
     // radix-sort path (grids finer than the bucket geometry, TNP_RADIX_CELLS=1)
     if (buf_ensure(e->spcnt, std::max<int64_t>(M, 1) * sizeof(int32_t), s)) return -1;
@@ -1280,12 +1291,13 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   const uint64_t cfmask = prune ? prune_mask(idx, K - 1) : 0ull;
   // the kept keys go to XS_N per-XCD regions of cap / XS_N keys (step.h) on
   // grids of many bucket workgroups; small grids count in ctr directly
-  const bool shard = !buckets || NB > 512;
+  const int NG = buckets ? bg.NG : 0;  // grouping workgroups
+  const bool shard = !buckets || NG > 512;
   if (shard && buf_ensure(e->xs, XS_WORDS * sizeof(int64_t), s)) return -1;
   int64_t* const xs = shard ? P<int64_t>(e->xs) : nullptr;
   // small bucket grids: per-bucket statistics rows (plain stores) that the
   // connect kernel sums, instead of counter-block atomics from every bucket
-  if (buckets && !shard && buf_ensure(e->bk[3], (int64_t)NB * 4 * sizeof(int64_t), s)) return -1;
+  if (buckets && !shard && buf_ensure(e->bk[3], (int64_t)NG * 4 * sizeof(int64_t), s)) return -1;
   int64_t* const bstat = (buckets && !shard) ? P<int64_t>(e->bk[3]) : nullptr;
   int64_t cap = std::max<int64_t>(e->ckeys_a.bytes / sizeof(uint64_t), 4 * M + 1024);
   cap = (cap + XS_N - 1) / XS_N * XS_N;
@@ -1314,7 +1326,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
       const bool lrec = e->lds_records;
       if (lrec && buf_ensure(e->bk[4], TB * sizeof(int32_t), s)) return -1;
       TIMED("bucket_group", 0.0,
-            launch_bucket_pairs(bg, P<int64_t>(e->bk[2]), P<uint64_t>(e->sents),
+            launch_bucket_pairs(bg, P<int64_t>(e->bk[bg.sub ? 8 : 2]), P<uint64_t>(bg.sub ? e->sents2 : e->sents),
                                 P<uint64_t>(c.pz), P<CellEnt>(e->ents), P<int32_t>(e->pcell),
                                 P<int32_t>(e->pent), P<int32_t>(e->pcn), P<int64_t>(e->ptoff),
                                 P<int32_t>(e->bcell), bcap, P<int32_t>(e->bk[0]), P<int32_t>(e->bk[1]),
@@ -1331,7 +1343,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
           launch_connect(P<int64_t>(e->ptoff), P<int32_t>(e->pcell), P<int32_t>(e->pcn),
                          P<int32_t>(e->pent), NC, e->max_pair_tests, P<int32_t>(e->bcell),
                          P<CellEnt>(e->ents), idx, nb, cfmask, P<uint64_t>(e->ckeys_a), cap, xs, ctr, s,
-                         bstat, NB));
+                         bstat, NG));
     if (shard) {
       if (launch_keys_finish(xs, cap, ctr, s)) return -1;
       e->xs_clean = true;
@@ -1358,6 +1370,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
       // 16 B of member keys and writes the 32 B record; the window pass reads
       // every record (once, algorithmically) and writes the kept keys
       ktimer_set_bytes(e, "bucket_entries", 16.0 * M + 8.0 * T);
+      if (bg.sub) ktimer_set_bytes(e, "bucket_refine", 24.0 * T);
       // the window pass re-reads the records the same workgroup just wrote
       // (cache traffic): its compulsory bytes are the kept keys.  LDS-record
       // path: 8 B entry word + 16 B member keys + 4 + 4 B cell order (written,

@@ -204,7 +204,7 @@ int launch_widen_flags(const uint8_t* f, int64_t n, int32_t* out, hipStream_t s)
 // planes the pruning of step idx compares (idx .. last_plane)
 uint64_t prune_mask(int idx, int last_plane);
 // ---- bucket.hip: members grouped by grid cell in spatial buckets ----------
-constexpr int BUCKET_MAX = 6144;        // buckets (17^3 lattice; 5 x 33 x 33 slab)
+constexpr int BUCKET_MAX = 6144;        // member-pass buckets (17^3 lattice; 5 x 33 x 33 slab)
 constexpr int BUCKET_LOCAL_MAX = 4096;  // cells per bucket (16^3)
 // The buckets cover the cells (+2 coordinates) [0, NC) along y and z and
 // [xorg, xorg + xn) along x: an x-slab of a sharded complex buckets only its
@@ -212,17 +212,33 @@ constexpr int BUCKET_LOCAL_MAX = 4096;  // cells per bucket (16^3)
 // of 17^3 buckets of 16^3, 82 % of them empty)
 struct BucketGeom {
   int NC;    // cell coordinates per axis (n_marks + 2)
-  int sh;    // log2 of the bucket edge in cells
+  int sh;    // log2 of the bucket edge in cells (the member passes' buckets)
   int NBd;   // buckets along y and z
   int NBx;   // buckets along x
   int xorg;  // first cell coordinate along x
   int xn;    // cells along x the buckets cover (NBx << sh)
   int NB;    // NBx * NBd * NBd
+  // 1: two-level buckets.  The member passes bucket by 16^3 cells (sh = 4,
+  // NB <= BUCKET_MAX bins in their LDS histograms); launch_bucket_refine
+  // splits every bucket into its 8 octants of 8^3 cells, and the grouping
+  // runs over those NG = 8 NB sub-buckets (group bucket 8 b + o) with the
+  // 8^3-cell kernel -- grids above 17^3 buckets of 8^3 (~134 marks) keep
+  // the small buckets the grouping is tuned for
+  int sub;
+  int NG;  // group buckets: NB, or 8 NB when sub
 };
-// the smallest bucket edge (2^3 or 2^4 cells) whose bucket count fits
-// BUCKET_MAX for a complex inside the x mark planes [x0, x1]; -1: the grid
-// is too fine for the bucket path (the radix-sort path takes it)
+// the bucket geometry for a complex inside the x mark planes [x0, x1]:
+// 8^3-cell buckets when their count fits BUCKET_MAX, else 16^3-cell member
+// buckets refined into 8^3-cell group buckets (sub); -1: the grid is too
+// fine for the bucket path (the radix-sort path takes it)
 int bucket_geometry(int n_marks, int x0, int x1, BucketGeom* g);
+// sub geometries: every 16^3-cell bucket's entries (bbase / ekv, the member
+// passes' output) regrouped by octant into ekv2, bases of the 8 NB group
+// buckets -> bbase2 [8 NB + 1]; entries keep their cell flags and vertex,
+// their local cell becomes the 9-bit one of the octant.  Zeroes the member
+// passes' bucket counters bcount / bcur for the next step
+int launch_bucket_refine(const BucketGeom& g, const int64_t* bbase, const uint64_t* ekv, int64_t* bbase2,
+                         uint64_t* ekv2, int32_t* bcount, int32_t* bcur, hipStream_t s);
 // members -> (local cell, vertex) entries in bucket ranges; A -> ctr[CTR_A],
 // T -> ctr[CTR_T], k=0 rows -> ctr[CTR_K0] bit 0, a member outside the
 // geometry's x range -> bit 1 (skipped; the host raises).  bcount/bcur: NB int32,

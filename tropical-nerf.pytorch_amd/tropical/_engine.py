@@ -301,4 +301,10 @@ def engine_for(net) -> Engine:
     if eng is None:
         eng = Engine(torch.device("cuda", key))
         _ENGINES[key] = eng
+    # every per-run setting back to the single-device default: a sharded run
+    # (subpoly_sharded, a bench rank) leaves shards, the owned range and the
+    # bucket x span behind on the cached engine otherwise
+    eng.set_shards(1)
+    eng.set_owned()
+    eng.set_xspan()
     return eng.set_net(net).set_curve(False).set_strict(True)

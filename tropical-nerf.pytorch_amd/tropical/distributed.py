@@ -333,7 +333,7 @@ def gather_complex(owned: Tensor, first: int, gedges: Tensor, dst: int = 0, grou
 
 
 def subpoly_sharded(net, size: float = 1.2, group=None, allreduce=None, stats: list = None,
-                    halo: int = None, force: bool = True):
+                    halo: int = None, force: bool = True, eps: float = 1e-4):
     """The hot loop of subpoly() (subpoly.py:45-69) sharded over the ranks of
     `group` (one GPU each): the skeleton (tropical.py:158-225, computed whole
     on every rank -- a few lattice passes), x-slabs of equal skeleton-edge
@@ -343,12 +343,15 @@ def subpoly_sharded(net, size: float = 1.2, group=None, allreduce=None, stats: l
     redone with the next width of HALOS (halo=None), or it raises (a fixed
     halo).  Returns (engine, owned vertices, first global id, global edges,
     cuts): the engine still holds this rank's slab complex.  force=False:
-    the curve branch, its in-step decisions through the same allreduce."""
+    the curve branch, its in-step decisions through the same allreduce.
+    eps: subpoly's eps argument (None: Net.eps), as in subpoly()."""
     from ._engine import engine_for
+    from .subpoly import _eps
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     eng = engine_for(net)
     eng.set_shards(world)
     eng.set_curve(not force)
+    eng.set_eps(_eps(net, eps))
     V0, E0 = eng.skeleton(unit=128, size=size)
     v, e, _ = eng.export()
     marks = net.enc.marks.to(v.device)

@@ -39,6 +39,10 @@ class _SDF(torch.autograd.Function):
     def forward(ctx, net, x, table, *weights):
         y, J = net._sdf_eval(x, want_grad=bool(ctx.needs_input_grad[1]))
         ctx.net = net
+        # the parameters' versions at forward time: the backward's VJP reads
+        # the parameters as they are then, so an in-place change in between
+        # must fail as autograd's saved-tensor check would
+        ctx.versions = tuple(t._version for t in (table,) + weights)
         ctx.save_for_backward(x, J)
         return y.unsqueeze(-1)
 
@@ -50,11 +54,15 @@ class _SDF(torch.autograd.Function):
                 "tropical.stanford.sdf_train.SDFTrainer takes it in closed form")
         net = ctx.net
         x, J = ctx.saved_tensors
+        now = tuple(t._version for t in net._params())
+        if any(ctx.needs_input_grad[2:]) and now != ctx.versions:
+            raise RuntimeError("Net.sdf backward: a parameter was modified in place after the forward "
+                               "(its version changed); the gradient would be taken at other weights")
         g = gy.detach().reshape(-1).float().contiguous()
         gx = (g[:, None] * J).to(x.dtype) if ctx.needs_input_grad[1] else None
         grads = [None] * (len(ctx.needs_input_grad) - 2)
         if any(ctx.needs_input_grad[2:]):
-            params = [net.enc.module.params] + [t for lin in net.fc for t in (lin.weight, lin.bias)]
+            params = net._params()
             g_table = torch.zeros(params[0].numel(), device=x.device)
             g_w = torch.zeros(sum(t.numel() for t in params[1:]), device=x.device)
             s, keep = net.tnp_desc()
@@ -83,6 +91,52 @@ class Net(nn.Module):
         self.num_nodes = [levels * 2] + [num_hidden] * (num_layers - 1) + [2]
         self.fc = nn.ModuleList(nn.Linear(a, b) for a, b in
                                 zip(self.num_nodes[:-1], self.num_nodes[1:]))
+        self._flatten_fc()
+
+    def _params(self):
+        return [self.enc.module.params] + [t for lin in self.fc for t in (lin.weight, lin.bias)]
+
+    def _flatten_fc(self):
+        """Every fc weight and bias becomes a view of ONE flat buffer, in the
+        C ABI's order (W0, b0, W1, b1, ...): the kernels read that buffer
+        directly, so any in-place change -- including through ``p.data``,
+        which bumps no version counter -- is what they see, with no copy to
+        go stale (tnp_desc)."""
+        ts = [t for lin in self.fc for t in (lin.weight, lin.bias)]
+        if len({(t.device, t.dtype) for t in ts}) != 1:
+            self._fc_flat = None
+            return
+        flat = torch.empty(sum(t.numel() for t in ts), dtype=ts[0].dtype, device=ts[0].device)
+        off = 0
+        with torch.no_grad():
+            for t in ts:
+                n = t.numel()
+                flat[off:off + n].copy_(t.reshape(-1))
+                t.data = flat[off:off + n].view_as(t)
+                off += n
+        self._fc_flat = flat
+
+    def _apply(self, fn, *args, **kwargs):
+        # .to() / .cuda() / .float() give every parameter new storage
+        out = super()._apply(fn, *args, **kwargs)
+        self._flatten_fc()
+        return out
+
+    def _fc_buffer(self):
+        """The flat fp32 weight buffer the kernels read: the parameters' own
+        storage when they are still views of it, else a fresh copy."""
+        flat = getattr(self, "_fc_flat", None)
+        ts = [t for lin in self.fc for t in (lin.weight, lin.bias)]
+        if flat is not None and flat.dtype == torch.float32:
+            off, ok = 0, True
+            for t in ts:
+                if t.data_ptr() != flat.data_ptr() + 4 * off or not t.is_contiguous():
+                    ok = False
+                    break
+                off += t.numel()
+            if ok:
+                return flat
+        return torch.cat([t.detach().float().reshape(-1) for t in ts]).contiguous()
 
     @property
     def K(self) -> int:
@@ -93,14 +147,16 @@ class Net(nn.Module):
 
     # -- C ABI descriptor ----------------------------------------------------
     def tnp_desc(self):
-        """(tnp_net struct, keep-alive tensors) for the current parameters,
-        rebuilt only when a parameter changed (in-place updates bump its
-        version counter; a new tensor changes its storage)."""
+        """(tnp_net struct, keep-alive tensors) for the current parameters.
+        The kernels read the parameters' own storage (the table, and the fc
+        weights' flat buffer, _flatten_fc), so edits in place are always
+        seen; the descriptor is rebuilt when a parameter got new storage (or,
+        for parameters that no longer share the flat buffer, a new version)."""
         dev = self.device()
         if dev.type != "cuda":
             raise RuntimeError("Net: move the net to a ROCm GPU (.cuda()); the tropical HIP "
                                "path has no CPU fallback")
-        params = [self.enc.module.params] + [t for lin in self.fc for t in (lin.weight, lin.bias)]
+        params = self._params()
         sig = (self.num_layers, self.num_hidden, float(self.eps),
                tuple((t.data_ptr(), t._version, t.dtype) for t in params), self.enc.marks.data_ptr())
         cached = getattr(self, "_tnp_cache", None)
@@ -110,8 +166,7 @@ class Net(nn.Module):
         self.enc.tnp_fields(s)
         s.num_layers, s.num_hidden, s.eps = self.num_layers, self.num_hidden, float(self.eps)
         table = self.enc.module.params.detach().float().contiguous()
-        w = torch.cat([t.detach().float().reshape(-1) for lin in self.fc
-                       for t in (lin.weight, lin.bias)]).contiguous()
+        w = self._fc_buffer()
         marks = self.enc.marks.to(dev).contiguous()
         s.d_table, s.d_weights, s.d_marks = table.data_ptr(), w.data_ptr(), marks.data_ptr()
         self._tnp_cache = (sig, (s, (table, w, marks)))
@@ -165,7 +220,7 @@ class Net(nn.Module):
     def sdf(self, x):
         """tanh(o1 - o0) (model.py:84-88); differentiable w.r.t. x and the
         parameters under grad mode (module docstring)."""
-        params = [self.enc.module.params] + [t for lin in self.fc for t in (lin.weight, lin.bias)]
+        params = self._params()
         if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in params)):
             return _SDF.apply(self, x, *params)
         return self._sdf_eval(x)[0].unsqueeze(-1)
