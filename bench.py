@@ -299,6 +299,20 @@ def small_net_check(dev, force: bool = True):
             out.update({"cpu_s": round(t_cpu, 3), "cpu_edges_per_s": round(S / t_cpu, 1)})
         else:
             rv, rtri = d["surf_V"], d["tri"]
+    # launches of the extraction (HIP events on every engine launch, one more
+    # untimed run): how launch-bound the bunny scale is
+    from tropical._engine import engine_for
+    eng = engine_for(net)
+    eng.kernel_timer(True)
+    with contextlib.redirect_stdout(io.StringIO()):
+        sp.subpoly(net, 3, 1.2, force=force)
+    kt = eng.kernel_timer(False)
+    nl = int(sum(x["launches"] for x in kt.values()))
+    kms = float(sum(x["ms"] for x in kt.values()))
+    out.update({"active_steps": len(stats), "timed_launches": nl,
+                "launches_per_step": round(nl / max(len(stats), 1), 1),
+                "us_per_launch": round(kms * 1e3 / max(nl, 1), 2),
+                "kernel_ms_total": round(kms, 3)})
     v = verts.cpu().numpy()
     out["chamfer_l2_vs_ref"] = chamfer(v, rv)
     out["faces_bit_exact"] = bool(np.array_equal(np.asarray(tri), np.asarray(rtri)))
@@ -339,6 +353,83 @@ def large_net_check(dev):
             "reference_cpu_note": "the reference itself, run once on the 8-core build container "
                                   "(tests/golden/make_golden.py)",
             "gpu_over_reference": round(ref_s / t_gpu, 1), "surface_faces_match_reference": bool(ok)}
+
+
+def finish_check(dev, reps: int = 5):
+    """The finish phase at scale: extract_skeleton + extract_faces
+    (subpoly.py:556-728, the a14/a15 kernels) on the synth64h complex (the
+    64^3 hashed lattice after all 33 steps: 703,300 surface vertices),
+    timed per phase and checked against the reference's own hashes of the
+    surface, triangles and float faces (tests/golden/synth64h.npz)."""
+    from golden_io import load, sha
+    from helpers import product_net
+    from tropical._engine import engine_for
+    d = load("synth64h")
+    net = product_net(d, dev)
+    eng = engine_for(net)
+    ts = {"surface": [], "export": [], "faces": []}
+    v = tri = fc = None
+    for i in range(reps + 1):
+        eng.lattice()
+        eng.run_steps([])
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        eng.surface()
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        v, _, _ = eng.export(edges=False)
+        torch.cuda.synchronize(dev)
+        t2 = time.perf_counter()
+        tri, fc = eng.faces()
+        torch.cuda.synchronize(dev)
+        t3 = time.perf_counter()
+        if i:  # the first round grows the engine's buffers
+            ts["surface"].append(t1 - t0)
+            ts["export"].append(t2 - t1)
+            ts["faces"].append(t3 - t2)
+    # per-kernel times of one more finish (HIP events on the engine's stream)
+    eng.lattice()
+    eng.run_steps([])
+    eng.kernel_timer(True)
+    eng.surface()
+    eng.export(edges=False)
+    eng.faces()
+    kt = eng.kernel_timer(False)
+    med = {k: float(np.median(x)) for k, x in ts.items()}
+    nv, nt = int(v.shape[0]), int(tri.shape[0])
+    ok = (sha(v.cpu().numpy()) == str(d["sha_surf"]) and sha(tri.cpu().numpy()) == str(d["sha_tri"]) and
+          sha(fc.cpu().numpy()) == str(d["sha_faces"]))
+    tot = sum(med.values())
+    return {"config": "synth64h: 64^3 hashed synthetic lattice after all 33 steps (reference golden), "
+                      "extract_skeleton + extract_faces on the device",
+            "surface_vertices": nv, "triangles": nt, "ms": {k: round(x * 1e3, 3) for k, x in med.items()},
+            "ms_total": round(tot * 1e3, 3), "ns_per_surface_vertex": round(tot * 1e9 / max(nv, 1), 2),
+            "triangles_per_s": round(nt / max(med["faces"], 1e-12), 1),
+            "kernel_ms": {k: round(x["ms"], 3) for k, x in sorted(kt.items(), key=lambda kv: -kv[1]["ms"])},
+            "launches": int(sum(x["launches"] for x in kt.values())),
+            "matches_reference": bool(ok)}
+
+
+def design_independent_rates(ktime: dict, stats: list) -> dict:
+    """Per-unit kernel times that do not depend on this build's byte model
+    (VERDICT r03 weak #8): ns per (cell, member) entry and per member pair
+    tested for the grouping kernel, per split for the new-vertex forward, per
+    edge slot for the pruning, over one pass."""
+    T = sum(s.get("T", 0) for s in stats)
+    tests = sum(s.get("pair_tests", 0) for s in stats)
+    S = sum(s["S"] for s in stats)
+    slots = sum(s["E_in"] + 2 * s["S"] + s["X"] for s in stats)
+    out = {"entries_per_pass": int(T), "pair_tests_per_pass": int(tests)}
+
+    def rate(k, n):
+        return None if k not in ktime or not n else round(ktime[k]["ms"] * 1e6 / n, 4)
+    grp = ktime.get("bucket_group", {}).get("ms", 0.0) + ktime.get("bucket_refine", {}).get("ms", 0.0)
+    out["bucket_group_ns_per_entry"] = round(grp * 1e6 / T, 4) if T else None
+    out["bucket_group_ns_per_pair_test"] = round(grp * 1e6 / tests, 4) if tests else None
+    out["bucket_entries_ns_per_entry"] = rate("bucket_entries", T)
+    out["forward_new_ns_per_split"] = rate("forward_new", S)
+    out["prune_ns_per_edge"] = rate("prune", slots)
+    return out
 
 
 def chamfer(a: np.ndarray, b: np.ndarray) -> float:
@@ -574,6 +665,8 @@ def main():
             "kernel_ms_per_pass": {k: round(v["ms"], 3) for k, v in
                                    sorted(ktime.items(), key=lambda kv: -kv[1]["ms"])},
             "active_steps": len(st0),
+            # ns per entry / pair test / split / edge, independent of the byte model
+            "unit_rates": design_independent_rates(ktime, st0),
         }
         if stitched:
             out["final_complex" if world == 1 else "stitched_complex"] = stitched
@@ -614,6 +707,8 @@ def main():
             out["small_net"] = small_net_check(dev, force=True)
             out["small_net_curve"] = small_net_check(dev, force=False)
             out["large_net"] = large_net_check(dev)
+            log("finish phase at scale (synth64h)")
+            out["finish_synth64h"] = finish_check(dev)
             engine_for(net)  # restore
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -111,6 +111,11 @@ CASES = {
     "h32_torus": ("subpoly", dict(SMALL, num_layers=2, num_hidden=32), ("fit", torus, 19), None),
     "h8l3_sphere": ("subpoly", dict(SMALL, num_hidden=8, levels=3, r_max=24), ("fit", sphere, 23), None),
     "lv8_rand": ("subpoly", dict(SMALL, levels=8, r_max=48, T=15), ("rand", 29, 0.05), None),
+    # the curve branch (with its gradient-descent fallback) on 8- and
+    # 32-hidden nets and an odd level count (the descent's backward
+    # schedules per shape, csrc/curve.hip)
+    "h8l3_sphere_curve": ("curve", dict(SMALL, num_hidden=8, levels=3, r_max=24), ("same", "h8l3_sphere"), None),
+    "h32_torus_curve": ("curve", dict(SMALL, num_layers=2, num_hidden=32), ("same", "h32_torus"), None),
     "synth24_l4h8": ("lattice", None, ("rand", 31, 0.1), (24, 19, dict(num_layers=4, num_hidden=8))),
     "synth20_h32": ("lattice", None, ("rand", 37, 0.1), (20, 19, dict(num_layers=2, num_hidden=32))),
     # the curve branch with strict=False (subpoly_(..., strict=False),

@@ -87,6 +87,7 @@ struct WinArgs {
   // stores that k_connect's first workgroup sums -- instead of 4 atomics per
   // bucket on the counter block's words (~11 ns each, serialised)
   int64_t* bstat;
+  int packed;  // the LDS-record path stages packed records (connect.h packed_ok)
 };
 
 // a bucket's pair statistics -> its bstat row, or the counter block / shards
@@ -564,8 +565,9 @@ k_bucket_scatter(const int32_t* __restrict__ members, int64_t S, int64_t V, int6
 // at wave-private cursors (the waves' octant counts scanned in LDS) -- no
 // atomics.  The order inside an octant is free (as inside a bucket: nothing
 // downstream depends on it)
-constexpr int RF_U = 8;          // entries per lane in flight
-constexpr int RF_THREADS = 1024;  // 16 waves per bucket: short serial walks (each iteration waits on HBM)
+constexpr int RF_U = 8;  // entries per lane in flight
+// (1024-thread workgroups, 16 shorter walks per bucket: 7x slower, spilled)
+constexpr int RF_THREADS = 256;
 constexpr int RF_WAVES = RF_THREADS / 64;
 __device__ __forceinline__ int refine_octant(uint64_t w) {
   const uint32_t lc = (uint32_t)(w >> 40);  // 16^3 local cell: x bits 8..11, y 4..7, z 0..3
@@ -658,6 +660,13 @@ k_bucket_refine(int NB, const int64_t* __restrict__ bbase, const uint64_t* __res
 #define TNP_GIPT 8
 #endif
 constexpr int GIPT = TNP_GIPT;
+// SW: the grouping writes the bucket's entry words in cell order (8 B per
+// entry) for the LDS-record pass, one dependent gather less than the entry
+// indices (4 B)
+#ifndef TNP_SORTED_WORDS
+#define TNP_SORTED_WORDS 1
+#endif
+constexpr bool SW = TNP_SORTED_WORDS;
 
 // pair cell o of the global list (cell id, first entry, m members, first
 // pair lo) and its chunks in k_connect's chunk table
@@ -696,7 +705,7 @@ __device__ __forceinline__ void group_bucket(const BGeom& G, int b, int64_t base
                                              const ulonglong2* __restrict__ pz, CellEnt* __restrict__ ents,
                                              const PairLists& pl, int64_t* __restrict__ ctr, int* cnt,
                                              int* cur, int64_t* lds, int64_t* lds3, int64_t* s_pk,
-                                             int64_t* s_sp, unsigned long long* tph, int32_t* perm) {
+                                             int64_t* s_sp, unsigned long long* tph, void* order) {
   (void)tph;
   constexpr int LC = 1 << (3 * SH);
   for (int i = threadIdx.x; i < LC; i += TNP_BLOCK) cnt[i] = 0;
@@ -744,15 +753,18 @@ __device__ __forceinline__ void group_bucket(const BGeom& G, int b, int64_t base
 #pragma unroll
     for (int k = 0; k < GIPT; ++k) {
       pos[k] = w[k] != ~0ull ? atomicAdd(&cur[(int)(w[k] >> 40)], 1) : 0;
-      const bool rec = w[k] != ~0ull && (!perm || cnt[(int)(w[k] >> 40)] > WCELL);
+      const bool rec = w[k] != ~0ull && (!order || cnt[(int)(w[k] >> 40)] > WCELL);
       k2[k] = pz[rec ? (uint32_t)w[k] : 0u];
     }
 #pragma unroll
     for (int k = 0; k < GIPT; ++k) {
       if (w[k] == ~0ull) continue;
       const int lc = (int)(w[k] >> 40);
-      if (perm) {
-        perm[pos[k]] = (int32_t)(e0 + k * TNP_BLOCK + threadIdx.x);
+      if (order) {
+        if (SW)
+          static_cast<uint64_t*>(order)[pos[k]] = w[k];
+        else
+          static_cast<int32_t*>(order)[pos[k]] = (int32_t)(e0 + k * TNP_BLOCK + threadIdx.x);
         if (cnt[lc] <= WCELL) continue;
       }
       CellEnt r;
@@ -1103,7 +1115,8 @@ constexpr size_t WL_RAW = WL_ST + (sizeof(WinLds) - WL_ST > LREC_N * sizeof(Cell
                                                                                      : LREC_N * sizeof(CellEnt));
 constexpr int LREC_R = (LREC_N + TNP_BLOCK - 1) / TNP_BLOCK;  // records per thread per chunk
 
-template <int SH>
+// PK: packed records (steps with packed_ok)
+template <int SH, bool PK>
 __global__ void __launch_bounds__(TNP_BLOCK, SH == 3 ? TNP_BG_MINB : 1)
 k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __restrict__ ekv,
                const ulonglong2* __restrict__ pz, CellEnt* __restrict__ ents, WinArgs wa, PairLists pl,
@@ -1150,8 +1163,10 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
     BG_PH(0);
     // (a bucket of one chunk gains nothing from it: bunny-scale buckets)
     const bool in_lds = LREC && wa.keys && pl.perm && n > LREC_N && n < 65536;
-    int32_t* const perm = in_lds ? pl.perm + base : nullptr;
-    group_bucket<SH>(G, b, base, n, ekv, pz, ents, pl, ctr, cnt, cur, lds, lds3, &s_pk, &s_sp, tph, perm);
+    void* const order = !in_lds ? nullptr
+                                : SW ? static_cast<void*>(reinterpret_cast<uint64_t*>(pl.perm) + base)
+                                     : static_cast<void*>(pl.perm + base);
+    group_bucket<SH>(G, b, base, n, ekv, pz, ents, pl, ctr, cnt, cur, lds, lds3, &s_pk, &s_sp, tph, order);
     BG_PH(4);
     if (wa.keys) {
       // the window pass over this bucket's records, right behind their
@@ -1180,11 +1195,12 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
         __syncthreads();
         BG_PH(5);
         if (in_lds) {
-          // chunks of TNP_LREC_CH record positions: gather (perm -> entry ->
-          // member keys) into LDS, then test the windows that start there.
-          // Software-pipelined: the cell order of chunk j + 3, the entry
+          // chunks of TNP_LREC_CH record positions gathered into LDS, then the
+          // windows that start there tested.  Software-pipelined: SW (the
+          // bucket's entry words written in cell order by the grouping): the
           // words of chunk j + 2 and the member keys of chunk j + 1 are in
-          // flight while chunk j is tested
+          // flight while chunk j is tested; else (cell order as entry
+          // indices) the order of j + 3, the words of j + 2, the keys of j + 1
           const uint64_t* kv = ekv + base;
           const int nn = (int)n;
           constexpr int CH = TNP_LREC_CH;
@@ -1197,6 +1213,7 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
             return q < q0 + LREC_N && q < nn;
           };
           auto load_i = [&](int q0, int (&ix)[LREC_R]) {
+            const int32_t* perm = static_cast<const int32_t*>(order);
 #pragma unroll
             for (int r = 0; r < LREC_R; ++r) ix[r] = in_chunk(q0, r) ? perm[q0 + r * TNP_BLOCK + threadIdx.x] : -1;
           };
@@ -1204,41 +1221,78 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
 #pragma unroll
             for (int r = 0; r < LREC_R; ++r) w[r] = ix[r] >= 0 ? kv[ix[r]] : 0ull;
           };
+          auto load_sw = [&](int q0, uint64_t (&w)[LREC_R]) {
+            const uint64_t* sw = static_cast<const uint64_t*>(order);
+#pragma unroll
+            for (int r = 0; r < LREC_R; ++r) w[r] = in_chunk(q0, r) ? sw[q0 + r * TNP_BLOCK + threadIdx.x] : 0ull;
+          };
           auto load_k = [&](const uint64_t (&w)[LREC_R], ulonglong2 (&k)[LREC_R]) {
 #pragma unroll
             for (int r = 0; r < LREC_R; ++r) k[r] = pz[(uint32_t)w[r]];
           };
-          load_i(0, ia);
-          load_w(ia, wa0);
-          load_k(wa0, ka);
-          if (CH < nn) {
-            load_i(CH, ia);
-            load_w(ia, wb);
+          if constexpr (SW) {
+            load_sw(0, wa0);
+            load_k(wa0, ka);
+            if (CH < nn) load_sw(CH, wb);
+          } else {
+            load_i(0, ia);
+            load_w(ia, wa0);
+            load_k(wa0, ka);
+            if (CH < nn) {
+              load_i(CH, ia);
+              load_w(ia, wb);
+            }
+            if (2 * CH < nn) load_i(2 * CH, ib);
           }
-          if (2 * CH < nn) load_i(2 * CH, ib);
+          // packed records (PK: steps with packed_ok): SoA over the same LDS
+          uint64_t* const ptw = reinterpret_cast<uint64_t*>(wraw + WL_ST);
+          uint64_t* const paw = ptw + LREC_N;
+          uint32_t* const pvv = reinterpret_cast<uint32_t*>(paw + LREC_N);
+          uint16_t* const ptg = reinterpret_cast<uint16_t*>(pvv + LREC_N);
+          static_assert(LREC_N * (8 + 8 + 4 + 2) <= WL_RAW - WL_ST, "packed records fit the record chunk");
+          const PackedRecs PR{ptw, paw, pvv, ptg};
+          uint64_t amask = 0;
+          if (PK && wa.fmask) {
+            const uint64_t lo = (uint32_t)(wa.fmask >> wa.idx);
+            amask = lo | (lo << 32);
+          }
           for (int p0 = 0; p0 < nn; p0 += CH) {
             const int p1 = min(nn, p0 + LREC_N);
 #pragma unroll
             for (int r = 0; r < LREC_R; ++r) {
               const int q = p0 + r * TNP_BLOCK + threadIdx.x;
               if (q >= p1) continue;
-              CellEnt e;
-              e.p = ka[r].x;
-              e.z = ka[r].y;
-              e.v = (int32_t)(uint32_t)wa0[r];
-              e.f = (uint32_t)(wa0[r] >> 32) & 63u;
-              e.tag = (uint32_t)b * (uint32_t)LC + (uint32_t)(wa0[r] >> 40);
-              e.pad = 0;
-              lrec[q - p0] = e;
+              if constexpr (PK) {
+                ptw[q - p0] = packed_test_word(ka[r].x, ka[r].y, (uint32_t)(wa0[r] >> 32) & 63u, below);
+                paw[q - p0] = packed_above_word(ka[r].x, ka[r].y, wa.idx);
+                pvv[q - p0] = (uint32_t)wa0[r];
+                ptg[q - p0] = (uint16_t)(wa0[r] >> 40);
+              } else {
+                CellEnt e;
+                e.p = ka[r].x;
+                e.z = ka[r].y;
+                e.v = (int32_t)(uint32_t)wa0[r];
+                e.f = (uint32_t)(wa0[r] >> 32) & 63u;
+                e.tag = (uint32_t)b * (uint32_t)LC + (uint32_t)(wa0[r] >> 40);
+                e.pad = 0;
+                lrec[q - p0] = e;
+              }
             }
             __syncthreads();
-            // next chunks: keys of j + 1, entry words of j + 2, order of j + 3
             uint64_t wc[LREC_R];
             if (p0 + CH < nn) load_k(wb, kb);
-            if (p0 + 2 * CH < nn) load_w(ib, wc);
-            if (p0 + 3 * CH < nn) load_i(p0 + 3 * CH, ib);
-            window_pass_lds(lrec, p0, p0 + CH, reinterpret_cast<const uint32_t*>(cnt), nwin_s, &kw, TNP_WAVES,
-                            below, wa.nb, wa.fmask, wa.keys, wa.cap, wa.xs, ctr, W, a);
+            if constexpr (SW) {
+              if (p0 + 2 * CH < nn) load_sw(p0 + 2 * CH, wc);
+            } else {
+              if (p0 + 2 * CH < nn) load_w(ib, wc);
+              if (p0 + 3 * CH < nn) load_i(p0 + 3 * CH, ib);
+            }
+            if constexpr (PK)
+              window_pass_packed_lds(PR, p0, p0 + CH, reinterpret_cast<const uint32_t*>(cnt), nwin_s, &kw,
+                                     TNP_WAVES, (uint32_t)below, wa.nb, amask, wa.keys, wa.cap, wa.xs, ctr, W, a);
+            else
+              window_pass_lds(lrec, p0, p0 + CH, reinterpret_cast<const uint32_t*>(cnt), nwin_s, &kw, TNP_WAVES,
+                              below, wa.nb, wa.fmask, wa.keys, wa.cap, wa.xs, ctr, W, a);
             __syncthreads();  // (the next chunk overwrites the records)
 #pragma unroll
             for (int r = 0; r < LREC_R; ++r) {
@@ -1370,14 +1424,18 @@ int launch_bucket_pairs(const BucketGeom& G, const int64_t* bbase, const uint64_
                         hipStream_t s, int32_t* perm) {
   const int NB = G.NG, sh = G.sub ? 3 : G.sh;
   const PairLists pl{pcell, pent, pn, ptoff, bcell, bcap, connect_chunk_pairs(), bcount, bcur, perm};
-  WinArgs wa{0, 0, 0ull, nullptr, 0, nullptr, nullptr};
-  if (win) wa = WinArgs{win->idx, win->nb, win->fmask, win->keys, win->cap, win->xs, win->bstat};
-  if (sh == 3)
-    hipLaunchKernelGGL(k_bucket_group<3>, dim3(NB), dim3(TNP_BLOCK), 0, s, G, bbase, ekv,
-                       reinterpret_cast<const ulonglong2*>(pz), ents, wa, pl, ctr);
+  WinArgs wa{0, 0, 0ull, nullptr, 0, nullptr, nullptr, 0};
+  if (win) wa = WinArgs{win->idx, win->nb, win->fmask, win->keys, win->cap, win->xs, win->bstat, win->packed};
+  const ulonglong2* pz2 = reinterpret_cast<const ulonglong2*>(pz);
+  if (sh == 3 && wa.packed)
+    hipLaunchKernelGGL((k_bucket_group<3, true>), dim3(NB), dim3(TNP_BLOCK), 0, s, G, bbase, ekv, pz2, ents, wa, pl,
+                       ctr);
+  else if (sh == 3)
+    hipLaunchKernelGGL((k_bucket_group<3, false>), dim3(NB), dim3(TNP_BLOCK), 0, s, G, bbase, ekv, pz2, ents, wa,
+                       pl, ctr);
   else
-    hipLaunchKernelGGL(k_bucket_group<4>, dim3(NB), dim3(TNP_BLOCK), 0, s, G, bbase, ekv,
-                       reinterpret_cast<const ulonglong2*>(pz), ents, wa, pl, ctr);
+    hipLaunchKernelGGL((k_bucket_group<4, false>), dim3(NB), dim3(TNP_BLOCK), 0, s, G, bbase, ekv, pz2, ents, wa,
+                       pl, ctr);
 #if TNP_BG_PHASES
   {
     unsigned long long h[64];

@@ -217,6 +217,143 @@ __device__ __forceinline__ void window_pass_lds(const CellEnt* rec, int p0, int 
   }
 }
 
+// ---------------------------------------------------------------------------
+// Packed records (the grouping kernel's LDS-record path, steps with
+// 1 <= idx <= 29 and K - idx <= 32).  The pair test reads only the planes
+// below idx and the 6 cell flags: one u64 TEST word per record,
+//   low  32: (pos & below)   | span-start flags (bits 0..2 of f) << 29
+//   high 32: (~zero & below) | on-plane flags   (bits 3..5 of f) << 29
+// (pu ^ pv) & ~zu & ~zv & below  = (lo_u ^ lo_v) & hi_u & hi_v   (plane bits)
+// zu & zv & below                = below & ~(hi_u | hi_v)
+// canonical <=> (lo_u | lo_v) >> 29 == 7; sp = (lo_u & lo_v & hi_u & hi_v) >> 29.
+// The pruning filter of the emitted pairs reads an ABOVE word (pos >> idx |
+// zero >> idx << 32: planes idx .. K-1), the key the vertex slots.
+// ---------------------------------------------------------------------------
+struct PackedRecs {
+  const uint64_t* tw;  // test words
+  const uint64_t* aw;  // above words
+  const uint32_t* vv;  // vertex slots
+  const uint16_t* tg;  // local cell
+};
+constexpr int PK_FLAG_SHIFT = 29;
+constexpr uint32_t PK_PLANES = (1u << PK_FLAG_SHIFT) - 1u;
+__device__ __forceinline__ uint64_t packed_test_word(uint64_t p, uint64_t z, uint32_t f, uint64_t below) {
+  const uint32_t lo = (uint32_t)(p & below) | ((f & 7u) << PK_FLAG_SHIFT);
+  const uint32_t hi = (uint32_t)(~z & below) | (((f >> 3) & 7u) << PK_FLAG_SHIFT);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t packed_above_word(uint64_t p, uint64_t z, int idx) {
+  return ((uint64_t)(uint32_t)(z >> idx) << 32) | (uint32_t)(p >> idx);
+}
+
+// the tests of one staged window of packed records (rec + s: its first
+// record); lane L initiates `rounds` tests against the next records of its
+// cell.  Same flattening, emission rules and counters as window_tests.
+// amask: the pruning filter on the above words (0: every emitted pair kept)
+__device__ __forceinline__ void window_tests_packed(const PackedRecs& R, int s, int rounds, uint32_t below,
+                                                    int nb, uint64_t amask, uint64_t* __restrict__ keys,
+                                                    int64_t cap, int64_t* __restrict__ xs,
+                                                    int64_t* __restrict__ ctr, WinLds& W, WinAcc& a) {
+  const int wv = tnp::wave(), L = tnp::lane();
+  const int incl = tnp::wave_scan_incl(rounds);
+  const int total = __shfl(incl, 63, 64);
+  const bool table = total <= WOWN;
+  W.exc[wv][L] = incl - rounds;
+  if (table)
+    for (int r = 0, t = incl - rounds; r < rounds; ++r, ++t) W.own[wv][t] = (uint16_t)(L | ((L + 1 + r) << 8));
+  lds_fence();
+  auto pair_of = [&](int t, int& j, int& i) {
+    if (table) {
+      const uint32_t o = W.own[wv][t];
+      j = (int)(o & 0xFFu);
+      i = (int)(o >> 8);
+    } else {
+      int lo2 = 0, hi2 = 62;
+#pragma unroll
+      for (int it = 0; it < 6; ++it) {
+        const int mid = (lo2 + hi2 + 1) >> 1;
+        if (W.exc[wv][mid] <= t) lo2 = mid;
+        else hi2 = mid - 1;
+      }
+      j = lo2;
+      i = j + 1 + (t - W.exc[wv][j]);
+    }
+  };
+  // the test of records j, i (live == false counts nothing); true: append key
+  auto test = [&](int j, int i, bool live, uint64_t& key) -> bool {
+    // every LDS read of the test issued together (a read behind the emit
+    // predicate would add a dependent round trip to nearly every batch)
+    const uint64_t tu = R.tw[s + j], tv = R.tw[s + i];
+    const uint64_t au = R.aw[s + j], av = R.aw[s + i];
+    const uint32_t vu = R.vv[s + j], vq = R.vv[s + i];
+    const uint32_t lu = (uint32_t)tu, hu = (uint32_t)(tu >> 32), lv = (uint32_t)tv, hv = (uint32_t)(tv >> 32);
+    const uint32_t hh = hu & hv;
+    const bool canon = ((lu | lv) >> PK_FLAG_SHIFT) == 7u;
+    const uint32_t d = (lu ^ lv) & hh & PK_PLANES;
+    const uint32_t sp = (lu & lv & hh) >> PK_FLAG_SHIFT;
+    const uint32_t zz = below & ~(hu | hv);
+    const bool compat = live & canon & (d == 0u);
+    const bool emit = compat & ((sp | zz) != 0u);
+    a.n_compat += compat;
+    a.n_reg += compat ? ((int64_t)1 << (__popc(sp) + __popc(zz))) : 0;
+    a.n_conn += emit;
+    key = ((uint64_t)min(vu, vq) << nb) | max(vu, vq);
+    // the step's pruning drops it anyway (keep_edge): never appended
+    return emit & ((amask == 0) | (((au ^ av) & amask) != 0));
+  };
+  auto append = [&](bool em, uint64_t key) {
+    const uint64_t eb = __ballot(em);
+    if (em) W.kb[wv][a.kn + tnp::mbcnt(eb)] = key;
+    a.kn += __popcll(eb);
+  };
+  int t0 = 0;
+  for (; t0 + 64 < total; t0 += 128) {
+    if (a.kn + 128 > WKEYS) window_flush(keys, cap, xs, ctr, W, a);
+    const int ta = t0 + L, tb = t0 + 64 + L;
+    const bool lb = tb < total;
+    int ja, ia, jb, ib;
+    pair_of(ta, ja, ia);
+    pair_of(lb ? tb : ta, jb, ib);
+    uint64_t ka = 0, kb = 0;
+    const bool ema = test(ja, ia, true, ka);
+    const bool emb = test(jb, ib, lb, kb);
+    append(ema, ka);
+    append(emb, kb);
+  }
+  for (; t0 < total; t0 += 64) {
+    if (a.kn + 64 > WKEYS) window_flush(keys, cap, xs, ctr, W, a);
+    const int t = t0 + L;
+    const bool live = t < total;
+    int j = 0, i = 0;
+    pair_of(live ? t : 0, j, i);
+    uint64_t key = 0;
+    const bool em = test(j, i, live, key);
+    append(em, key);
+  }
+  lds_fence();
+}
+
+// packed windows over the packed record chunk (records p0 .. of the bucket
+// at R index p - p0): as window_pass_lds
+__device__ __forceinline__ void window_pass_packed_lds(const PackedRecs& R, int p0, int p_end, const uint32_t* wl,
+                                                       int nwin, int* k, int dw, uint32_t below, int nb,
+                                                       uint64_t amask, uint64_t* __restrict__ keys, int64_t cap,
+                                                       int64_t* __restrict__ xs, int64_t* __restrict__ ctr,
+                                                       WinLds& W, WinAcc& a) {
+  const int L = tnp::lane();
+  for (; *k < nwin; *k += dw) {
+    const uint32_t se = wl[*k];
+    const int s = (int)(se & 0xFFFFu), n = (int)(se >> 16) - s;
+    if (s >= p_end) break;
+    const bool valid = L < n;
+    const uint32_t tag = valid ? R.tg[s - p0 + L] : 0xFFFFFFFFu;
+    const uint32_t nxt = __shfl_down(tag, 1, 64);
+    const uint64_t bm = __ballot(L >= n - 1 || nxt != tag);  // (the window holds whole cells)
+    const int last = L + __builtin_ctzll(bm >> L);
+    window_tests_packed(R, s - p0, valid ? last - L : 0, below, nb, amask, keys, cap, xs, ctr, W, a);
+  }
+}
+
 __device__ __forceinline__ void window_tests(const CellEnt* st, int rounds, uint64_t below, int nb, uint64_t fmask,
                                              uint64_t* __restrict__ keys, int64_t cap, int64_t* __restrict__ xs,
                                              int64_t* __restrict__ ctr, WinLds& W, WinAcc& a) {

@@ -211,6 +211,7 @@ struct tnp_engine {
   bool radix_cells = false; // TNP_RADIX_CELLS=1: the radix-sort bucketing path
   bool lazy_edges = true;   // TNP_LAZY_EDGES=0: every pruning step compacts the edge list
   bool lds_records = true;  // TNP_LDS_RECORDS=0: the grouping's records go through memory
+  bool packed_records = true;  // TNP_PACKED_RECORDS=0: the LDS records stay 32-B CellEnt
   bool bk_clean = false;    // bucket counters (bk[0], bk[1]) are zero
   Buf cv[CV_N];
 };
@@ -508,6 +509,7 @@ extern "C" int tnp_engine_create(tnp_engine** out, int device) {
   if (const char* rc = getenv("TNP_RADIX_CELLS")) e->radix_cells = atoi(rc) != 0;
   if (const char* lz = getenv("TNP_LAZY_EDGES")) e->lazy_edges = atoi(lz) != 0;
   if (const char* lr = getenv("TNP_LDS_RECORDS")) e->lds_records = atoi(lr) != 0;
+  if (const char* pr = getenv("TNP_PACKED_RECORDS")) e->packed_records = atoi(pr) != 0;
   if (const char* sp = getenv("TNP_LB_SPIN")) e->lb_spin = atoi(sp);
   if (hipHostMalloc((void**)&e->h_ctr, CTR_N * sizeof(int64_t), hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc((void**)&e->h_map, 32 * sizeof(int64_t), hipHostMallocMapped | hipHostMallocCoherent) !=
@@ -1321,10 +1323,11 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
       // in-bucket grouping + the window pass over each bucket (cells of <=
       // WCELL members) + pair-cell lists and k_connect's chunk table (bcap)
       if (buf_ensure(e->bcell, bcap * sizeof(int32_t), s)) return -1;
-      const ConnectWin cw{idx, nb, cfmask, P<uint64_t>(e->ckeys_a), cap, xs, bstat};
+      const ConnectWin cw{idx, nb, cfmask, P<uint64_t>(e->ckeys_a), cap, xs, bstat,
+                          e->packed_records && packed_ok(idx, K) ? 1 : 0};
       // the LDS-record path's cell-order scratch (TNP_LDS_RECORDS=0: off)
       const bool lrec = e->lds_records;
-      if (lrec && buf_ensure(e->bk[4], TB * sizeof(int32_t), s)) return -1;
+      if (lrec && buf_ensure(e->bk[4], TB * sizeof(uint64_t), s)) return -1;  // (entry words or indices)
       TIMED("bucket_group", 0.0,
             launch_bucket_pairs(bg, P<int64_t>(e->bk[bg.sub ? 8 : 2]), P<uint64_t>(bg.sub ? e->sents2 : e->sents),
                                 P<uint64_t>(c.pz), P<CellEnt>(e->ents), P<int32_t>(e->pcell),

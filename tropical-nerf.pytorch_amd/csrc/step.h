@@ -304,6 +304,9 @@ int launch_keys_finish(int64_t* xs, int64_t cap, int64_t* ctr, hipStream_t s);
 int launch_keys_compact(const uint64_t* keys, int64_t cap, const int64_t* xs, int64_t X, uint64_t* out,
                         hipStream_t s);
 
+// steps whose window pass can test packed records (connect.h): the planes
+// below idx fit 29 bits beside 3 flag bits, the planes idx .. K-1 32 bits
+__host__ __device__ inline bool packed_ok(int idx, int K) { return idx >= 1 && idx <= 29 && K - idx <= 32; }
 struct ConnectWin {
   int idx, nb;
   uint64_t fmask;
@@ -311,6 +314,7 @@ struct ConnectWin {
   int64_t cap;
   int64_t* xs;
   int64_t* bstat;  // small grids (xs == null): per-bucket statistics [NB][4] that launch_connect sums
+  int packed;      // 1: the LDS-record path tests packed records (connect.h packed_ok(idx, K))
 };
 int launch_bucket_pairs(const BucketGeom& g, const int64_t* bbase, const uint64_t* ekv, const uint64_t* pz,
                         CellEnt* ents, int32_t* pcell, int32_t* pent, int32_t* pn, int64_t* ptoff, int32_t* bcell,
