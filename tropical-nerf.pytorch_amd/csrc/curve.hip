@@ -731,432 +731,6 @@ __global__ void k_gd_rows(const int32_t* __restrict__ gd, const int64_t* __restr
   if (b < B && gd[b]) glist[goff[b]] = (int32_t)b;
 }
 
-// x86 MKL's 1-row sgemm (1x16 @ 16x16, the gradient through layer 2 when
-// a single row descends): this summation tree with these fused products
-// (tools probe, bitwise against torch.mm on CPU)
-__device__ __forceinline__ float mm1_16(const float* x, const float* W, int ld, int k) {
-  auto pr = [&](int a, int b) {  // fma(x_a, w_a, x_b * w_b)
-    return __fmaf_rn(x[a], W[a * ld + k], __fmul_rn(x[b], W[b * ld + k]));
-  };
-  float v = __fadd_rn(__fadd_rn(pr(0, 2), pr(1, 3)), __fadd_rn(pr(4, 6), pr(5, 7)));
-  v = __fmaf_rn(x[14], W[14 * ld + k], v);
-  v = __fmaf_rn(x[12], W[12 * ld + k], v);
-  v = __fadd_rn(v, pr(13, 15));
-  return __fadd_rn(v, __fadd_rn(pr(8, 10), pr(9, 11)));
-}
-
-// pre-activations of planes j0, j1 at u (preprocessed) and d(d0^2 + d1^2)/du
-// exactly as torch autograd computes it on CPU for a G-row batch
-// (subpoly_debug.py:143-148): forward with MKL's G-row schedules, backward
-// through AddmmBackward (mm(grad, W): sequential fma; the 1-row tree of a
-// 16 x 16 layer), threshold_backward, and the encoding's input gradient
-// (oracle/encoding.py _GridFn.backward op order).  NL - 1 hidden layers of
-// H = 16 (the shapes whose backward schedules are verified).
-template <int LV, int H, int NL>
-__device__ __forceinline__ void plane_pair_grad(const NetDev& net, const float* w, const float u[3],
-                                                int j0, int j1, int mh, int mo, bool one_row,
-                                                float& d0, float& d1, float gu[3]) {
-  constexpr int IN = 2 * LV;
-  constexpr int NH = NL - 1;
-  float f[IN], a[NH][H], h[H], o[2];
-  encode<LV>(net, u, f);
-  const float* Wl[NH];
-  Wl[0] = w;
-#pragma unroll
-  for (int l = 1; l < NH; ++l) Wl[l] = Wl[l - 1] + (l == 1 ? H * IN + H : H * H + H);
-  const float* WL = Wl[NH - 1] + (NH == 1 ? H * IN + H : H * H + H);
-  linear_mode<IN, H>(Wl[0], Wl[0] + H * IN, f, a[0], mh);
-#pragma unroll
-  for (int j = 0; j < H; ++j) h[j] = fmaxf(a[0][j], 0.f);
-#pragma unroll
-  for (int l = 1; l < NH; ++l) {
-    linear_mode<H, H>(Wl[l], Wl[l] + H * H, h, a[l], mh);
-#pragma unroll
-    for (int j = 0; j < H; ++j) h[j] = fmaxf(a[l][j], 0.f);
-  }
-  linear_mode<H, 2>(WL, WL + 2 * H, h, o, mo);
-  float last = __fsub_rn(o[1], o[0]);
-  d0 = last;
-  d1 = last;
-#pragma unroll
-  for (int l = 0; l < NH; ++l)
-#pragma unroll
-    for (int k = 0; k < H; ++k) {
-      if (j0 == l * H + k) d0 = a[l][k];
-      if (j1 == l * H + k) d1 = a[l][k];
-    }
-  // seeds of y = d0^2 + d1^2 on the gathered pre-activations (2 d, exact)
-  float g[NH][H], go = 0.f;
-#pragma unroll
-  for (int l = 0; l < NH; ++l)
-#pragma unroll
-    for (int k = 0; k < H; ++k) g[l][k] = 0.f;
-  const int js[2] = {j0, j1};
-  const float ds[2] = {d0, d1};
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    float gs = __fmul_rn(2.f, ds[s]);
-    int j = js[s];
-#pragma unroll
-    for (int l = 0; l < NH; ++l)
-#pragma unroll
-      for (int k = 0; k < H; ++k)
-        if (j == l * H + k) g[l][k] = __fadd_rn(g[l][k], gs);
-    if (j == NH * H) go = __fadd_rn(go, gs);
-  }
-  // last layer (o1 - o0): mm([-go, go], W), K = 2 sequential fma; ReLU
-#pragma unroll
-  for (int k = 0; k < H; ++k) {
-    float v = __fmaf_rn(go, WL[H + k], __fmul_rn(-go, WL[k]));
-    if (a[NH - 1][k] > 0.f) g[NH - 1][k] = __fadd_rn(g[NH - 1][k], v);
-  }
-  // hidden H x H layers, top down: mm(g_a, W) ; ReLU
-#pragma unroll
-  for (int l = NH - 1; l >= 1; --l) {
-    float gp[H];
-#pragma unroll
-    for (int k = 0; k < H; ++k) {
-      float v;
-      if (one_row) {
-        v = mm1_16(g[l], Wl[l], H, k);
-      } else {
-        v = 0.f;
-#pragma unroll
-        for (int j = 0; j < H; ++j) v = __fmaf_rn(g[l][j], Wl[l][j * H + k], v);
-      }
-      gp[k] = a[l - 1][k] > 0.f ? __fadd_rn(g[l - 1][k], v) : g[l - 1][k];
-    }
-#pragma unroll
-    for (int k = 0; k < H; ++k) g[l - 1][k] = gp[k];
-  }
-  // first layer: mm(g_a0, W0), sequential fma
-  const float* W0 = Wl[0];
-  float df[IN];
-#pragma unroll
-  for (int m = 0; m < IN; ++m) {
-    float v = 0.f;
-#pragma unroll
-    for (int k = 0; k < H; ++k) v = __fmaf_rn(g[0][k], W0[k * IN + m], v);
-    df[m] = v;
-  }
-  // encoding input gradient: per level, per corner, per dim
-  //   gx_d += (((sgn * f_e0) * f_e1) * dv) * scale,  dv = val . g_feat
-  float gx[3] = {0.f, 0.f, 0.f};
-#pragma unroll
-  for (int l = 0; l < LV; ++l) {
-    const float sc = net.scales[l];
-    float t[3];
-    uint32_t gi[3];
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-      float pos = __fadd_rn(__fmul_rn(u[d], sc), 0.5f);
-      float fl = floorf(pos);
-      t[d] = __fsub_rn(pos, fl);
-      gi[d] = (uint32_t)(int)fl;
-    }
-    const uint32_t res = (uint32_t)net.res[l];
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      float fc[3];
-      uint32_t gc[3];
-#pragma unroll
-      for (int d = 0; d < 3; ++d) {
-        bool up = (c >> d) & 1;
-        fc[d] = up ? t[d] : __fsub_rn(1.f, t[d]);
-        gc[d] = gi[d] + (up ? 1u : 0u);
-      }
-      uint32_t id = net.dense[l] ? (gc[0] + gc[1] * res + gc[2] * (res * res))
-                                 : (gc[0] ^ (gc[1] * P1) ^ (gc[2] * P2));
-      id = wrap_index(id, net.sizes[l]);
-      float2 v = table_entry(net, l, id);
-      float dv = __fadd_rn(__fmul_rn(v.x, df[2 * l]), __fmul_rn(v.y, df[2 * l + 1]));
-#pragma unroll
-      for (int d = 0; d < 3; ++d) {
-        float sg = ((c >> d) & 1) ? 1.f : -1.f;
-        float fa = fc[d == 0 ? 1 : 0], fb = fc[d == 2 ? 1 : 2];
-        gx[d] = __fadd_rn(gx[d], __fmul_rn(__fmul_rn(__fmul_rn(__fmul_rn(sg, fa), fb), dv), sc));
-      }
-    }
-  }
-#pragma unroll
-  for (int d = 0; d < 3; ++d) gu[d] = gx[d];
-}
-
-// deal_with_gradient_descent (subpoly_debug.py:121-165), one thread per row.
-// record != 0: AND this row's per-iteration "both residuals <= eps" bits into
-// conv[0..7] (iteration i -> bit i) so the host finds the common stop.
-template <int LV, int H, int NL>
-__global__ void __launch_bounds__(TNP_BLOCK)
-k_descend(NetDev net, int64_t G, const int32_t* __restrict__ glist,
-          const int32_t* __restrict__ crow, const int32_t* __restrict__ sa,
-          const int32_t* __restrict__ sb, const float* __restrict__ xyz,
-          const int32_t* __restrict__ plane, int idx, float eps, int iters, int record,
-          float* __restrict__ ints, float* __restrict__ d0s, float* __restrict__ d1s,
-          unsigned long long* __restrict__ conv) {
-  constexpr int NW = NetShape<LV, H, NL>::NW;
-  __shared__ float w[NW];
-  for (int i = threadIdx.x; i < NW; i += blockDim.x) w[i] = net.weights[i];
-  __syncthreads();
-  int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= G) return;
-  int b = glist[g];
-  int r = crow[b];
-  float e0[3], de[3], x[3];
-#pragma unroll
-  for (int d = 0; d < 3; ++d) {
-    e0[d] = xyz[3 * (int64_t)sa[r] + d];
-    de[d] = __fsub_rn(xyz[3 * (int64_t)sb[r] + d], e0[d]);
-    x[d] = ints[3 * b + d];
-  }
-  const int j0 = plane[b];
-  const int64_t Gs = net.sched_rows > 0 ? net.sched_rows : G;  // the schedule's row count (sharded: global)
-  const int mh = lin_mode<H, H>(Gs), mo = lin_mode<H, 2>(Gs);  // (H = 16: layer 0's mode too)
-  uint64_t bits[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  float d0 = 1.f, d1 = 1.f;
-  for (int it = 0; it < iters; ++it) {
-    float u[3], gu[3];
-#pragma unroll
-    for (int d = 0; d < 3; ++d)
-      u[d] = __fmul_rn(__fadd_rn(__fadd_rn(e0[d], __fmul_rn(x[d], de[d])), 1.0f), 0.5f);  // x/2 == x*0.5
-    plane_pair_grad<LV, H, NL>(net, w, u, j0, idx, mh, mo, G == 1, d0, d1, gu);
-    float gx[3], nn = 0.f;
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-      gx[d] = __fmul_rn(__fmul_rn(gu[d], 0.5f), de[d]);
-      nn = __fmaf_rn(gx[d], gx[d], nn);
-    }
-    float den = fmaxf(__fsqrt_rn(nn), 1e-12f);
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-      float v = __fsub_rn(x[d], __fmul_rn(1e-2f, __fdiv_rn(gx[d], den)));
-      x[d] = fminf(fmaxf(v, 0.f), 1.f);
-    }
-    if (record && fabsf(d0) <= eps && fabsf(d1) <= eps) bits[it >> 6] |= 1ull << (it & 63);
-  }
-  if (record)
-    for (int k = 0; k < 8; ++k) atomicAnd(&conv[k], (unsigned long long)bits[k]);
-#pragma unroll
-  for (int d = 0; d < 3; ++d) ints[3 * b + d] = x[d];
-  d0s[b] = d0;
-  d1s[b] = d1;
-}
-
-__device__ __forceinline__ float lane_f(float v, int l) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
-}
-
-// The same descent with ONE WAVE PER ROW: the 500 iterations are strictly
-// sequential, so a row's latency per iteration is the whole cost (one thread
-// per row left a lone wave issuing ~4k dependent instructions per
-// iteration).  Here lane q holds hash-grid corner q & 7 of level q >> 3 (its
-// table entry is gathered once per iteration and reused by the backward
-// pass) and lane j < H neuron j of each layer; every sum keeps the
-// single-thread order above -- corner sums, sequential fma chains, the
-// 1-row 16 x 16 tree -- over operands broadcast with v_readlane, so the
-// result is bitwise that of k_descend.
-template <int LV, int H, int NL>
-__global__ void __launch_bounds__(64)
-k_descend_wave(NetDev net, int64_t G, const int32_t* __restrict__ glist,
-               const int32_t* __restrict__ crow, const int32_t* __restrict__ sa,
-               const int32_t* __restrict__ sb, const float* __restrict__ xyz,
-               const int32_t* __restrict__ plane, int idx, float eps, int iters, int record,
-               float* __restrict__ ints, float* __restrict__ d0s, float* __restrict__ d1s,
-               unsigned long long* __restrict__ conv) {
-  static_assert(LV * 8 <= 64 && H <= 64, "one wave holds every corner and neuron");
-  constexpr int IN = 2 * LV;
-  constexpr int NH = NL - 1;
-  constexpr int NW = NetShape<LV, H, NL>::NW;
-  __shared__ float w[NW];
-  for (int i = threadIdx.x; i < NW; i += blockDim.x) w[i] = net.weights[i];
-  __syncthreads();
-  const int64_t g = blockIdx.x;
-  if (g >= G) return;
-  const int lane = threadIdx.x;
-  const int b = glist[g];
-  const int r = crow[b];
-  float e0[3], de[3], x[3];
-#pragma unroll
-  for (int d = 0; d < 3; ++d) {
-    e0[d] = xyz[3 * (int64_t)sa[r] + d];
-    de[d] = __fsub_rn(xyz[3 * (int64_t)sb[r] + d], e0[d]);
-    x[d] = ints[3 * b + d];
-  }
-  const int j0 = plane[b];
-  const int64_t Gs = net.sched_rows > 0 ? net.sched_rows : G;  // the schedule's row count (sharded: global)
-  const int mh = lin_mode<H, H>(Gs), mo = lin_mode<H, 2>(Gs);  // (H = 16: layer 0's mode too)
-  const bool one_row = G == 1;
-  // lane roles
-  const int nj = lane & (H - 1);                      // neuron
-  const int lc = min(lane >> 3, LV - 1), c = lane & 7;  // corner c of level lc
-  float sc = 0.f;
-  uint32_t res = 0, size = 1;
-  bool dense = false;
-#pragma unroll
-  for (int l = 0; l < LV; ++l)
-    if (l == lc) {
-      sc = net.scales[l];
-      res = (uint32_t)net.res[l];
-      size = net.sizes[l];
-      dense = net.dense[l] != 0;
-    }
-  const float* Wl[NH];
-  Wl[0] = w;
-#pragma unroll
-  for (int l = 1; l < NH; ++l) Wl[l] = Wl[l - 1] + (l == 1 ? H * IN + H : H * H + H);
-  const float* WL = Wl[NH - 1] + (NH == 1 ? H * IN + H : H * H + H);
-  uint64_t word = 0;  // convergence bits of iterations [64 k, 64 k + 64)
-  float d0 = 1.f, d1 = 1.f;
-  for (int it = 0; it < iters; ++it) {
-    float u[3];
-#pragma unroll
-    for (int d = 0; d < 3; ++d)
-      u[d] = __fmul_rn(__fadd_rn(__fadd_rn(e0[d], __fmul_rn(x[d], de[d])), 1.0f), 0.5f);  // x/2 == x*0.5
-    // this lane's corner (encode's op order)
-    float t[3];
-    uint32_t gc[3];
-    float wc = 1.0f;
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-      const float pos = __fadd_rn(__fmul_rn(u[d], sc), 0.5f);
-      const float fl = floorf(pos);
-      t[d] = __fsub_rn(pos, fl);
-      const uint32_t gi = (uint32_t)(int)fl;
-      if ((c >> d) & 1) {
-        wc = __fmul_rn(wc, t[d]);
-        gc[d] = gi + 1u;
-      } else {
-        wc = __fmul_rn(wc, __fsub_rn(1.0f, t[d]));
-        gc[d] = gi;
-      }
-    }
-    uint32_t id = dense ? (gc[0] + gc[1] * res + gc[2] * (res * res)) : (gc[0] ^ (gc[1] * P1) ^ (gc[2] * P2));
-    id = wrap_index(id, size);
-    const float2 v = table_entry(net, lc, id);
-    const float px = __fmul_rn(wc, v.x), py = __fmul_rn(wc, v.y);
-    float f[IN];
-#pragma unroll
-    for (int l = 0; l < LV; ++l) {
-      float a0 = 0.f, a1 = 0.f;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        a0 = __fadd_rn(a0, lane_f(px, 8 * l + k));
-        a1 = __fadd_rn(a1, lane_f(py, 8 * l + k));
-      }
-      f[2 * l] = a0;
-      f[2 * l + 1] = a1;
-    }
-    // forward, neuron nj per lane; a[l]: this lane's neuron of hidden layer l
-    float a[NH];
-    float hh[H];
-    a[0] = neuron_mode<IN, H>(Wl[0], Wl[0] + H * IN, f, nj, mh);
-#pragma unroll
-    for (int l = 1; l < NH; ++l) {
-#pragma unroll
-      for (int j = 0; j < H; ++j) hh[j] = fmaxf(lane_f(a[l - 1], j), 0.f);
-      a[l] = neuron_mode<H, H>(Wl[l], Wl[l] + H * H, hh, nj, mh);
-    }
-#pragma unroll
-    for (int j = 0; j < H; ++j) hh[j] = fmaxf(lane_f(a[NH - 1], j), 0.f);
-    const float o = neuron_mode<H, 2>(WL, WL + 2 * H, hh, lane & 1, mo);
-    const float last = __fsub_rn(lane_f(o, 1), lane_f(o, 0));
-    d0 = last;
-    d1 = last;
-#pragma unroll
-    for (int l = 0; l < NH; ++l) {
-      if (j0 >= l * H && j0 < (l + 1) * H) d0 = lane_f(a[l], j0 - l * H);
-      if (idx >= l * H && idx < (l + 1) * H) d1 = lane_f(a[l], idx - l * H);
-    }
-    // backward: seeds of d0^2 + d1^2, neuron nj per lane
-    float gl[NH], go = 0.f;
-#pragma unroll
-    for (int l = 0; l < NH; ++l) gl[l] = 0.f;
-    {
-      const int js[2] = {j0, idx};
-      const float ds[2] = {d0, d1};
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const float gs = __fmul_rn(2.f, ds[s]);
-#pragma unroll
-        for (int l = 0; l < NH; ++l)
-          if (js[s] == l * H + nj) gl[l] = __fadd_rn(gl[l], gs);
-        if (js[s] == NH * H) go = __fadd_rn(go, gs);
-      }
-    }
-    const float v3 = __fmaf_rn(go, WL[H + nj], __fmul_rn(-go, WL[nj]));
-    if (a[NH - 1] > 0.f) gl[NH - 1] = __fadd_rn(gl[NH - 1], v3);
-#pragma unroll
-    for (int l = NH - 1; l >= 1; --l) {
-      float gu_[H];
-#pragma unroll
-      for (int j = 0; j < H; ++j) gu_[j] = lane_f(gl[l], j);
-      float v2;
-      if (one_row) {
-        v2 = mm1_16(gu_, Wl[l], H, nj);
-      } else {
-        v2 = 0.f;
-#pragma unroll
-        for (int j = 0; j < H; ++j) v2 = __fmaf_rn(gu_[j], Wl[l][j * H + nj], v2);
-      }
-      gl[l - 1] = a[l - 1] > 0.f ? __fadd_rn(gl[l - 1], v2) : gl[l - 1];
-    }
-    float ga1u[H];
-#pragma unroll
-    for (int k = 0; k < H; ++k) ga1u[k] = lane_f(gl[0], k);
-    const float* W0 = Wl[0];
-    const int m = lane & (IN - 1);
-    float dfm = 0.f;
-#pragma unroll
-    for (int k = 0; k < H; ++k) dfm = __fmaf_rn(ga1u[k], W0[k * IN + m], dfm);
-    // encoding input gradient, this lane's corner; sums in (level, corner) order
-    float dfa = 0.f, dfb = 0.f;
-#pragma unroll
-    for (int l = 0; l < LV; ++l) {
-      const float pa = lane_f(dfm, 2 * l), pb = lane_f(dfm, 2 * l + 1);
-      if (l == lc) {
-        dfa = pa;
-        dfb = pb;
-      }
-    }
-    const float dv = __fadd_rn(__fmul_rn(v.x, dfa), __fmul_rn(v.y, dfb));
-    float fc[3];
-#pragma unroll
-    for (int d = 0; d < 3; ++d) fc[d] = ((c >> d) & 1) ? t[d] : __fsub_rn(1.f, t[d]);
-    float term[3];
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-      const float sg = ((c >> d) & 1) ? 1.f : -1.f;
-      const float fa = fc[d == 0 ? 1 : 0], fb = fc[d == 2 ? 1 : 2];
-      term[d] = __fmul_rn(__fmul_rn(__fmul_rn(__fmul_rn(sg, fa), fb), dv), sc);
-    }
-    float gx[3], nn = 0.f;
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-      float acc = 0.f;
-#pragma unroll
-      for (int q = 0; q < 8 * LV; ++q) acc = __fadd_rn(acc, lane_f(term[d], q));
-      gx[d] = __fmul_rn(__fmul_rn(acc, 0.5f), de[d]);
-      nn = __fmaf_rn(gx[d], gx[d], nn);
-    }
-    const float den = fmaxf(__fsqrt_rn(nn), 1e-12f);
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-      const float vv = __fsub_rn(x[d], __fmul_rn(1e-2f, __fdiv_rn(gx[d], den)));
-      x[d] = fminf(fmaxf(vv, 0.f), 1.f);
-    }
-    if (record && fabsf(d0) <= eps && fabsf(d1) <= eps) word |= 1ull << (it & 63);
-    if ((it & 63) == 63 || it == iters - 1) {
-      if (record && lane == 0) atomicAnd(&conv[it >> 6], (unsigned long long)word);
-      word = 0;
-    }
-  }
-  if (lane == 0) {
-#pragma unroll
-    for (int d = 0; d < 3; ++d) ints[3 * b + d] = x[d];
-    d0s[b] = d0;
-    d1s[b] = d1;
-  }
-}
-
 // v = e0 + t (e1 - e0) for c rows (subpoly.py:204-207) and the per-split
 // strict-filter inputs: cinfo bit0 c row, bit1 gg, bit2 |d0| < eps; the
 // global "some kept c row has |d0| > eps" flag (subpoly_debug.py:253-257).
@@ -1280,37 +854,12 @@ int launch_descend(const NetDev& net, int64_t G, const int32_t* glist, const int
                    unsigned long long* conv, hipStream_t s) {
   if (G <= 0) return 0;
   if (!net_supported(net)) { tnp_set_error("unsupported net shape"); return -1; }
-  if (net.num_hidden != 16 || (net.n_levels != 2 && net.n_levels != 4)) {
-    // the descent reproduces autograd's CPU backward schedules (AddmmBackward,
-    // subpoly_debug.py:143-148), reverse-engineered for 16-hidden nets of 2 or
-    // 4 levels (the 1-row 16 x 16 tree; sequential fma into 4 / 8 features)
-    tnp_set_error("curve path: the gradient-descent fallback (subpoly_debug.py:121-165) is built for 16-hidden "
-                  "nets of 2 or 4 levels (this net: %d hidden, %d levels)", net.num_hidden, net.n_levels);
-    return -1;
-  }
   if (iters > 512) { tnp_set_error("descend: at most 512 iterations"); return -1; }
   // TNP_DESCEND_THREAD=1: the one-thread-per-row kernel (tests compare both)
   const char* pt = getenv("TNP_DESCEND_THREAD");
   const bool per_thread = pt && pt[0] == '1';
-#define TNP_DESCEND(L_, NL_)                                                                                \
-  if (per_thread)                                                                                            \
-    hipLaunchKernelGGL((k_descend<L_, 16, NL_>), dim3(tnp_grid(G)), dim3(TNP_BLOCK), 0, s, net, G, glist,   \
-                       crow, sa, sb, xyz, plane, idx, eps, iters, record, ints, d0s, d1s, conv);             \
-  else                                                                                                       \
-    hipLaunchKernelGGL((k_descend_wave<L_, 16, NL_>), dim3((unsigned)G), dim3(64), 0, s, net, G, glist,    \
-                       crow, sa, sb, xyz, plane, idx, eps, iters, record, ints, d0s, d1s, conv);
-  const int key = net.n_levels * 8 + net.num_layers;
-  switch (key) {
-    case 2 * 8 + 2: TNP_DESCEND(2, 2) break;
-    case 2 * 8 + 3: TNP_DESCEND(2, 3) break;
-    case 2 * 8 + 4: TNP_DESCEND(2, 4) break;
-    case 4 * 8 + 2: TNP_DESCEND(4, 2) break;
-    case 4 * 8 + 3: TNP_DESCEND(4, 3) break;
-    case 4 * 8 + 4: TNP_DESCEND(4, 4) break;
-    default: tnp_set_error("descend: net shape not instantiated"); return -1;
-  }
-#undef TNP_DESCEND
-  TNP_CHECK(hipGetLastError());
+  TNP_LV_SWITCH(net.n_levels, return lv_descend<L_>(net, G, glist, crow, sa, sb, xyz, plane, idx, eps, iters, record,
+                                                     ints, d0s, d1s, conv, per_thread, s));
   return 0;
 }
 int launch_curve_apply(int64_t B, const int32_t* crow, const int32_t* sa, const int32_t* sb,

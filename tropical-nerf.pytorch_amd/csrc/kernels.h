@@ -56,6 +56,12 @@ int lv_skel_eval(const NetDev& net, int i0, int j0, int k0, int n0, int n1, int 
                  unsigned int* gmax_bits, hipStream_t s);
 template <int LV>
 int lv_encode(const NetDev& net, const float* x01, int64_t n, float* out, hipStream_t s);
+// the curve branch's gradient descent (descend.h) for every shape of this
+// level count; per_thread: one thread per row (else one wave per row)
+template <int LV>
+int lv_descend(const NetDev& net, int64_t G, const int32_t* glist, const int32_t* crow, const int32_t* sa,
+               const int32_t* sb, const float* xyz, const int32_t* plane, int idx, float eps, int iters, int record,
+               float* ints, float* d0s, float* d1s, unsigned long long* conv, bool per_thread, hipStream_t s);
 #define TNP_LV_DECLARE(L)                                                                                   \
   template <> int lv_forward<L>(const NetDev&, const float*, int64_t, float*, int64_t, int, hipStream_t, float*, \
                                 uint64_t*, uint64_t*, uint64_t*, uint64_t*);                                  \
@@ -65,7 +71,10 @@ int lv_encode(const NetDev& net, const float* x01, int64_t n, float* out, hipStr
   template <> int lv_sdf_grad<L>(const NetDev&, const float*, int64_t, float*, float*, hipStream_t);           \
   template <> int lv_skel_eval<L>(const NetDev&, int, int, int, int, int, int, float*, unsigned int*,         \
                                   hipStream_t);                                                               \
-  template <> int lv_encode<L>(const NetDev&, const float*, int64_t, float*, hipStream_t);
+  template <> int lv_encode<L>(const NetDev&, const float*, int64_t, float*, hipStream_t);                    \
+  template <> int lv_descend<L>(const NetDev&, int64_t, const int32_t*, const int32_t*, const int32_t*,        \
+                                const int32_t*, const float*, const int32_t*, int, float, int, int, float*,    \
+                                float*, float*, unsigned long long*, bool, hipStream_t);
 TNP_LV_DECLARE(2)
 TNP_LV_DECLARE(3)
 TNP_LV_DECLARE(4)

@@ -19,6 +19,7 @@
 #include "kernels.h"
 #include "net_device.h"
 #include "step.h"
+#include "descend.h"
 
 #ifndef TNP_LV
 #error "net_lv.hip is compiled once per level count: -DTNP_LV=<2..8>"
@@ -356,6 +357,24 @@ int lv_skel_eval<LVC>(const NetDev& net, int i0, int j0, int k0, int n0, int n1,
 #define TNP_SHAPE_BODY                                                                                         \
   hipLaunchKernelGGL((k_skel_eval<LVC, H, NL>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net, i0, j0, k0, n0, \
                      n1, n2, dist, gmax_bits);
+  TNP_SHAPE_SWITCH(net)
+#undef TNP_SHAPE_BODY
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+
+template <>
+int lv_descend<LVC>(const NetDev& net, int64_t G, const int32_t* glist, const int32_t* crow, const int32_t* sa,
+                    const int32_t* sb, const float* xyz, const int32_t* plane, int idx, float eps, int iters,
+                    int record, float* ints, float* d0s, float* d1s, unsigned long long* conv, bool per_thread,
+                    hipStream_t s) {
+#define TNP_SHAPE_BODY                                                                                           \
+  if (per_thread)                                                                                                \
+    hipLaunchKernelGGL((k_descend<LVC, H, NL>), dim3(tnp_grid(G)), dim3(TNP_BLOCK), 0, s, net, G, glist, crow, sa, \
+                       sb, xyz, plane, idx, eps, iters, record, ints, d0s, d1s, conv);                          \
+  else                                                                                                           \
+    hipLaunchKernelGGL((k_descend_wave<LVC, H, NL>), dim3((unsigned)G), dim3(64), 0, s, net, G, glist, crow, sa, \
+                       sb, xyz, plane, idx, eps, iters, record, ints, d0s, d1s, conv);
   TNP_SHAPE_SWITCH(net)
 #undef TNP_SHAPE_BODY
   TNP_CHECK(hipGetLastError());
