@@ -32,10 +32,10 @@ extern "C" {
  * order.  table: the flat `enc.module.params` (tcnn layout
  * params[(offset_l + index) * 2 + f]). */
 typedef struct tnp_net {
-  int32_t n_levels;   /* L  (2 or 4 are instantiated) */
+  int32_t n_levels;   /* L  (2..8 are instantiated) */
   int32_t n_features; /* F  (must be 2) */
-  int32_t num_layers; /* 3 */
-  int32_t num_hidden; /* 16 */
+  int32_t num_layers; /* with num_hidden, one of the instantiated shapes */
+  int32_t num_hidden; /* (layers, hidden): (2..4, 8) (2..4, 16) (2, 32) -- K <= 63 planes */
   int32_t n_marks;    /* len(TropicalHashGrid.marks) */
   float eps;          /* Net.eps (model.py:20) */
   float scales[TNP_MAX_LEVELS];    /* fp32 exp2(l*log2 b)*N_min - 1 */
@@ -298,7 +298,7 @@ int tnp_shm_allreduce(tnp_shm* shm, const int64_t* in, int n, int op, int64_t* o
  * own layout, params[(offset_l + idx) * 2 + f]) and d_grad_weights (the
  * packed weight layout of tnp_net); d_stats (2 doubles, device, zeroed by
  * the call) receives sum |clamp(sdf) - clamp(gt)| and sum ||J_i||^2.  Float
- * atomics: the summation order is not fixed.  3-layer nets, 16 hidden. */
+ * atomics: the summation order is not fixed.  Every instantiated net shape. */
 int tnp_sdf_train_grad(const tnp_net* net, const float* d_x, const float* d_gt, int64_t n, float clamp_t,
                        float eik_w, int64_t eik_batch, float* d_grad_table, float* d_grad_weights,
                        double* d_stats, void* stream);
@@ -307,9 +307,26 @@ int tnp_sdf_train_grad(const tnp_net* net, const float* d_x, const float* d_gt, 
  * sum_i d_gout[i] * d sdf(x_i) / d theta, ACCUMULATED into d_grad_table (the
  * table's own layout) and d_grad_weights (the packed weight layout) -- the
  * backward of a caller's net.sdf(x) w.r.t. the parameters (the input
- * gradient is tnp_sdf_grad's).  Float atomics; 3-layer, 16-hidden nets. */
+ * gradient is tnp_sdf_grad's).  Float atomics; every instantiated net shape. */
 int tnp_sdf_vjp(const tnp_net* net, const float* d_x, const float* d_gout, int64_t n, float* d_grad_table,
                 float* d_grad_weights, void* stream);
+
+/* Autograd through Net.normal(create_graph=True) (model.py:105-123: J =
+ * d sdf / d x with a graph): the VJP sum_i d_gJ[i] . d J_i / d theta,
+ * ACCUMULATED into d_grad_table / d_grad_weights, and (d_grad_x != null)
+ * d_gJ[i] . d J_i / d x_i -- the Hessian of sdf along d_gJ[i] -- ACCUMULATED
+ * into d_grad_x (n x 3).  Replaces the reference's double backward through
+ * tcnn (train.py:196).  Float atomics. */
+int tnp_normal_vjp(const tnp_net* net, const float* d_x, const float* d_gJ, int64_t n, float* d_grad_table,
+                   float* d_grad_weights, float* d_grad_x, void* stream);
+
+/* Autograd through Net.forward(x, gather=True) (model.py:52-76): upstream
+ * gradients of the gathered planes (d_gpre, plane-major [K][ld] as
+ * tnp_forward writes them: every hidden pre-activation, then o1 - o0) and
+ * of the output (d_gout, n x 2); either may be null.  ACCUMULATES into
+ * d_grad_table, d_grad_weights and (when given) d_grad_x (n x 3). */
+int tnp_forward_vjp(const tnp_net* net, const float* d_x, int64_t n, const float* d_gpre, int64_t ld,
+                    const float* d_gout, float* d_grad_table, float* d_grad_weights, float* d_grad_x, void* stream);
 
 /* Signed distance of n points d_p (n x 3) to a closed triangle mesh (d_V
  * nV x 3 fp32, d_F nF x 3 int32, indices in [0, nV)): replaces

@@ -116,6 +116,9 @@ CASES = {
     # schedules per shape, csrc/curve.hip)
     "h8l3_sphere_curve": ("curve", dict(SMALL, num_hidden=8, levels=3, r_max=24), ("same", "h8l3_sphere"), None),
     "h32_torus_curve": ("curve", dict(SMALL, num_layers=2, num_hidden=32), ("same", "h32_torus"), None),
+    # random weights: rows that need the gradient-descent fallback
+    "h8l3_rand_curve": ("curve", dict(SMALL, num_hidden=8, levels=3, r_max=24), ("rand", 41, 0.05), None),
+    "h32_rand_curve": ("curve", dict(SMALL, num_layers=2, num_hidden=32), ("rand", 43, 0.05), None),
     "synth24_l4h8": ("lattice", None, ("rand", 31, 0.1), (24, 19, dict(num_layers=4, num_hidden=8))),
     "synth20_h32": ("lattice", None, ("rand", 37, 0.1), (20, 19, dict(num_layers=2, num_hidden=32))),
     # the curve branch with strict=False (subpoly_(..., strict=False),

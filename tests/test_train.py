@@ -39,10 +39,10 @@ def icosphere(level: int = 3, r: float = 1.0):
     return np.array(V) * r, np.array(F, dtype=np.int64)
 
 
-def _small_net(levels=4, r_min=2, r_max=32, T=19, seed=0, amp=0.1):
+def _small_net(levels=4, r_min=2, r_max=32, T=19, seed=0, amp=0.1, num_layers=3, num_hidden=16):
     from tropical.stanford.model import Net
     torch.manual_seed(seed)
-    net = Net(num_layers=3, num_hidden=16, levels=levels, r_min=r_min, r_max=r_max, T=T)
+    net = Net(num_layers=num_layers, num_hidden=num_hidden, levels=levels, r_min=r_min, r_max=r_max, T=T)
     with torch.no_grad():
         net.enc.module.params.uniform_(-amp, amp)
     return net
@@ -146,9 +146,25 @@ def test_oracle_signed_distance_on_a_sphere():
 
 # ---------------------------------------------------------------- GPU -----
 
+# every instantiated shape family: 3 x 16 (the reference's nets), 2 x 32 with
+# 3 levels, 4 x 8 with 5 levels, 4 x 16 with 8 hashed levels
+SHAPES = [dict(levels=4, r_min=2, r_max=32, T=19),     # small: dense levels
+          dict(levels=4, r_min=8, r_max=128, T=14),    # hashed levels
+          dict(levels=3, r_min=2, r_max=24, T=19, num_layers=2, num_hidden=32),
+          dict(levels=5, r_min=2, r_max=32, T=19, num_layers=4, num_hidden=8),
+          dict(levels=8, r_min=4, r_max=64, T=13, num_layers=4, num_hidden=16)]
+
+
+def _fc(net):
+    return [t.detach().cpu() for lin in net.fc for t in (lin.weight, lin.bias)]
+
+
+def _names(net):
+    return ["table"] + [f"{k}{i}" for i in range(len(net.fc)) for k in ("W", "b")]
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg", [dict(levels=4, r_min=2, r_max=32, T=19),     # small: dense levels
-                                 dict(levels=4, r_min=8, r_max=128, T=14)])   # hashed levels
+@pytest.mark.parametrize("cfg", SHAPES)
 def test_train_grads_match_oracle(cuda, cfg):
     from oracle.train import train_loss_grads
     from tropical.stanford.sdf_train import EIK_W, SDFTrainer
@@ -171,7 +187,7 @@ def test_train_grads_match_oracle(cuda, cfg):
     for t in ws:
         got.append(tr.g_w[off:off + t.numel()].view_as(t).cpu())
         off += t.numel()
-    for name, a, b in zip(["table", "W0", "b0", "W1", "b1", "W2", "b2"], got, ref):
+    for name, a, b in zip(_names(net), got, ref):
         scale = float(b.abs().max())
         err = float((a.double() - b).abs().max())
         assert err <= 2e-4 * scale + 1e-9, (name, err, scale)
@@ -214,12 +230,12 @@ def test_train_entry_point_fits_a_sphere(cuda, tmp_path, capsys):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg", [dict(levels=4, r_min=2, r_max=32, T=19), dict(levels=4, r_min=8, r_max=128, T=14)])
+@pytest.mark.parametrize("cfg", SHAPES)
 def test_sdf_autograd_matches_oracle(cuda, cfg):
     """net.sdf(x) is differentiable as the reference's (model.py:84-88,
     autograd through tcnn there): (g * sdf).sum().backward() fills x.grad and
     every parameter's .grad (encoding table, fc weights and biases), checked
-    against float64 autograd of the same net; double backward refuses."""
+    against float64 autograd of the same net."""
     from oracle.train import sdf64
     net = _small_net(**cfg).to(cuda)
     gen = torch.Generator().manual_seed(3)
@@ -238,7 +254,7 @@ def test_sdf_autograd_matches_oracle(cuda, cfg):
     (yd * g.double()).sum().backward()
     got = [xg.grad, net.enc.module.params.grad] + [t.grad for lin in net.fc for t in (lin.weight, lin.bias)]
     want = [xd.grad, tab.grad] + [t.grad for t in ws]
-    for name, a, b in zip(["x", "table", "W0", "b0", "W1", "b1", "W2", "b2"], got, want):
+    for name, a, b in zip(["x"] + _names(net), got, want):
         assert a is not None, name
         err = float((a.detach().cpu().double() - b).abs().max())
         assert err <= 2e-4 * float(b.abs().max()) + 1e-7, (name, err)
@@ -248,6 +264,87 @@ def test_sdf_autograd_matches_oracle(cuda, cfg):
     x2 = x.to(cuda).requires_grad_(True)
     net.sdf(x2).sum().backward()
     assert x2.grad is not None and torch.isfinite(x2.grad).all()
-    with pytest.raises(NotImplementedError, match="double backward"):
-        x3 = x.to(cuda).requires_grad_(True)
-        torch.autograd.grad(net.sdf(x3).sum(), x3, create_graph=True)[0].sum().backward()
+
+
+def _double_backward_ref(net, x, gJ):
+    """float64 autograd: J = d sdf / d x with a graph, then (gJ . J).sum()
+    backward -- the reference's double backward (train.py:196)."""
+    from oracle.train import sdf64
+    tab = net.enc.module.params.detach().cpu().double().requires_grad_(True)
+    ws = [t.double().requires_grad_(True) for t in _fc(net)]
+    xd = x.double().requires_grad_(True)
+    yd = sdf64(tab, ws, net.enc.meta, xd)
+    J = torch.autograd.grad(yd.sum(), xd, create_graph=True)[0]
+    (J * gJ.double()).sum().backward()
+    return J.detach(), [xd.grad, tab.grad] + [t.grad for t in ws]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [SHAPES[0], SHAPES[1], SHAPES[3]])
+@pytest.mark.parametrize("route", ["normal", "autograd"])
+def test_double_backward_matches_oracle(cuda, cfg, route):
+    """The reference's create_graph=True: Net.normal(x, create_graph=True)
+    (model.py:105-123) and torch.autograd.grad(net.sdf(x).sum(), x,
+    create_graph=True) return J with a graph; (gJ . J).sum().backward() then
+    fills the parameters' gradients and x's (the Hessian of sdf along gJ),
+    checked against float64 autograd's double backward."""
+    net = _small_net(**cfg).to(cuda)
+    gen = torch.Generator().manual_seed(5)
+    n = 401
+    x = (torch.rand(n, 3, generator=gen) * 2 - 1) * 0.9
+    gJ = torch.rand(n, 3, generator=gen) * 2 - 1
+    xg = x.to(cuda).requires_grad_(True)
+    if route == "normal":
+        J = net.normal(xg, create_graph=True)
+    else:
+        J = torch.autograd.grad(net.sdf(xg).sum(), xg, create_graph=True)[0]
+    assert J.requires_grad
+    Jref, want = _double_backward_ref(net, x, gJ)
+    assert float((J.detach().cpu().double() - Jref).abs().max()) <= 2e-4 * float(Jref.abs().max())
+    (J * gJ.to(cuda)).sum().backward()
+    got = [xg.grad, net.enc.module.params.grad] + [t.grad for lin in net.fc for t in (lin.weight, lin.bias)]
+    for name, a, b in zip(["x"] + _names(net), got, want):
+        assert a is not None, name
+        err = float((a.detach().cpu().double() - b).abs().max())
+        assert err <= 5e-4 * float(b.abs().max()) + 1e-7, (name, err, float(b.abs().max()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [SHAPES[0], SHAPES[2], SHAPES[4]])
+def test_forward_autograd_matches_oracle(cuda, cfg):
+    """Net.forward(x, gather=True) is differentiable as the reference's
+    (model.py:52-76): a loss over the output and every gathered plane
+    backpropagates to x, the table and the fc parameters (tnp_forward_vjp),
+    checked against float64 autograd of the same forward."""
+    from oracle.train import encode_diff
+    net = _small_net(**cfg).to(cuda)
+    gen = torch.Generator().manual_seed(7)
+    n = 333
+    x = (torch.rand(n, 3, generator=gen) * 2 - 1) * 0.9
+    xg = x.to(cuda).requires_grad_(True)
+    out, inputs = net(xg, gather=True)
+    K = net.K
+    gpl = torch.rand(n, K, generator=gen) * 2 - 1
+    go = torch.rand(n, 2, generator=gen) * 2 - 1
+    loss = (out * go.to(cuda)).sum() + (torch.cat(inputs, dim=-1) * gpl.to(cuda)).sum()
+    loss.backward()
+    tab = net.enc.module.params.detach().cpu().double().requires_grad_(True)
+    ws = [t.double().requires_grad_(True) for t in _fc(net)]
+    xd = x.double().requires_grad_(True)
+    h = encode_diff((xd + 1) / 2, tab, net.enc.meta)
+    planes = []
+    for i in range(len(ws) // 2):
+        h = torch.nn.functional.linear(h, ws[2 * i], ws[2 * i + 1])
+        if i < len(ws) // 2 - 1:
+            planes.append(h)
+            h = torch.relu(h)
+    planes.append(h[:, 1:] - h[:, :1])
+    ref = (h * go.double()).sum() + (torch.cat(planes, dim=-1) * gpl.double()).sum()
+    ref.backward()
+    assert torch.allclose(out.detach().cpu().double(), h.detach(), atol=1e-5)
+    got = [xg.grad, net.enc.module.params.grad] + [t.grad for lin in net.fc for t in (lin.weight, lin.bias)]
+    want = [xd.grad, tab.grad] + [t.grad for t in ws]
+    for name, a, b in zip(["x"] + _names(net), got, want):
+        assert a is not None, name
+        err = float((a.detach().cpu().double() - b).abs().max())
+        assert err <= 2e-4 * float(b.abs().max()) + 1e-7, (name, err)

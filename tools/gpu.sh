@@ -16,6 +16,7 @@
 #   small[:lib]        tools/small_profile.py (bunny-scale latency)
 #   finish[:lib]       tools/finish_profile.py
 #   prof[:G]           rocprofv3 --kernel-trace --stats of a short bench
+#   proffinish         rocprofv3 --kernel-trace --stats of tools/finish64.py
 #   pmc:<counters>     one rocprofv3 --pmc pass (counters comma-separated) of a short bench
 #   env:<VAR=val>      export a variable for the following steps
 # Logs: gpurun_out/<tag>_<n>_<step>.log, summary gpurun_out/<tag>_session.log
@@ -55,6 +56,8 @@ for step in "$@"; do
     sp) run 300 0 env "$(lib "$a2")" python -u tools/step_profile.py "${a1:-128}" 6 ;;
     small) run 300 0 env "$(lib "$a1")" python -u tools/small_profile.py ;;
     finish) run 300 0 env "$(lib "$a1")" python -u tools/finish_profile.py ;;
+    proffinish) run 600 0 rocprofv3 --kernel-trace --stats -d "gpurun_out/${tag}_proffinish" -o run --output-format csv \
+            -- python tools/finish64.py ;;
     prof) run 600 0 rocprofv3 --kernel-trace --stats -d "gpurun_out/${tag}_prof${a1:-128}" -o run --output-format csv \
             -- python bench.py --marks "${a1:-128}" --steps 2 --warmup 1 --no-cpu ;;
     pmc) run 120 0 rocprofv3 --pmc ${a1//,/ } -d "gpurun_out/${tag}_pmc_${a1//,/_}" -o run --output-format csv \

@@ -673,6 +673,25 @@ extern "C" int tnp_sdf_vjp(const tnp_net* n, const float* xyz, const float* gout
   return launch_sdf_vjp(to_dev(n), xyz, gout, N, d_grad_table, d_grad_weights, (hipStream_t)stream);
 }
 
+extern "C" int tnp_normal_vjp(const tnp_net* n, const float* xyz, const float* gJ, int64_t N, float* d_grad_table,
+                              float* d_grad_weights, float* d_grad_x, void* stream) {
+  if (check_net(n)) return -1;
+  if (N < 0 || !gJ || !d_grad_table || !d_grad_weights) { tnp_set_error("normal_vjp: bad arguments"); return -1; }
+  return launch_normal_vjp(to_dev(n), xyz, gJ, N, d_grad_table, d_grad_weights, d_grad_x, (hipStream_t)stream);
+}
+
+extern "C" int tnp_forward_vjp(const tnp_net* n, const float* xyz, int64_t N, const float* d_gpre, int64_t ld,
+                               const float* d_gout, float* d_grad_table, float* d_grad_weights, float* d_grad_x,
+                               void* stream) {
+  if (check_net(n)) return -1;
+  if (N < 0 || (!d_gpre && !d_gout) || (d_gpre && ld < N) || !d_grad_table || !d_grad_weights) {
+    tnp_set_error("forward_vjp: bad arguments");
+    return -1;
+  }
+  return launch_forward_vjp(to_dev(n), xyz, N, d_gpre, ld, d_gout, d_grad_table, d_grad_weights, d_grad_x,
+                            (hipStream_t)stream);
+}
+
 extern "C" int tnp_mesh_signed_distance(const float* d_V, int64_t nV, const int32_t* d_F, int64_t nF,
                                         const float* d_p, int64_t n, float* d_work, float* d_dist, void* stream) {
   if (n < 0) { tnp_set_error("mesh_signed_distance: n < 0"); return -1; }

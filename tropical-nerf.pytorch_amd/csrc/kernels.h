@@ -56,6 +56,15 @@ int lv_skel_eval(const NetDev& net, int i0, int j0, int k0, int n0, int n1, int 
                  unsigned int* gmax_bits, hipStream_t s);
 template <int LV>
 int lv_encode(const NetDev& net, const float* x01, int64_t n, float* out, hipStream_t s);
+// parameter gradients (train_net.h k_train_grads): training (gout, gJ null;
+// stats zeroed by the caller), the sdf VJP (gout), the normal VJP (gJ, g_x)
+template <int LV>
+int lv_train(const NetDev& net, const float* xyz, const float* gt, int64_t n, float T, float eik_w, int64_t eik_batch,
+             double* stats, float* g_table, float* g_w, const float* gout, const float* gJ, float* g_x, hipStream_t s);
+// VJP of the forward's gathered planes / output (train_net.h k_forward_vjp)
+template <int LV>
+int lv_forward_vjp(const NetDev& net, const float* xyz, int64_t n, const float* gpl, int64_t ld, const float* gout2,
+                   float* g_table, float* g_w, float* g_x, hipStream_t s);
 // the curve branch's gradient descent (descend.h) for every shape of this
 // level count; per_thread: one thread per row (else one wave per row)
 template <int LV>
@@ -72,6 +81,10 @@ int lv_descend(const NetDev& net, int64_t G, const int32_t* glist, const int32_t
   template <> int lv_skel_eval<L>(const NetDev&, int, int, int, int, int, int, float*, unsigned int*,         \
                                   hipStream_t);                                                               \
   template <> int lv_encode<L>(const NetDev&, const float*, int64_t, float*, hipStream_t);                    \
+  template <> int lv_train<L>(const NetDev&, const float*, const float*, int64_t, float, float, int64_t, double*, \
+                              float*, float*, const float*, const float*, float*, hipStream_t);                  \
+  template <> int lv_forward_vjp<L>(const NetDev&, const float*, int64_t, const float*, int64_t, const float*,   \
+                                    float*, float*, float*, hipStream_t);                                         \
   template <> int lv_descend<L>(const NetDev&, int64_t, const int32_t*, const int32_t*, const int32_t*,        \
                                 const int32_t*, const float*, const int32_t*, int, float, int, int, float*,    \
                                 float*, float*, unsigned long long*, bool, hipStream_t);
@@ -126,9 +139,17 @@ int launch_region(const NetDev& net, const float* xyz, const float* pre, int64_t
 int launch_train_grad(const NetDev& net, const float* xyz, const float* gt, int64_t n, float clamp_t, float eik_w,
                       int64_t eik_batch, float* g_table, float* g_w, double* stats, hipStream_t s);
 // sum_i gout_i d sdf_i / d theta accumulated into g_table / g_w (autograd
-// through Net.sdf; 3-layer, 16-hidden nets)
+// through Net.sdf)
 int launch_sdf_vjp(const NetDev& net, const float* xyz, const float* gout, int64_t n, float* g_table, float* g_w,
                    hipStream_t s);
+// sum_i gJ_i . d J_i / d theta (and d / d x_i into g_x when given), J = d sdf / d x
+// (autograd through Net.normal(create_graph=True))
+int launch_normal_vjp(const NetDev& net, const float* xyz, const float* gJ, int64_t n, float* g_table, float* g_w,
+                      float* g_x, hipStream_t s);
+// VJP of Net.forward(x, gather=True): upstream of the gathered planes (gpl
+// plane-major [K][ld]) and of the output (gout2 [n][2]); either may be null
+int launch_forward_vjp(const NetDev& net, const float* xyz, int64_t n, const float* gpl, int64_t ld,
+                       const float* gout2, float* g_table, float* g_w, float* g_x, hipStream_t s);
 // mesh signed distance (dataset.py:92); work: 2 n floats
 int launch_mesh_sd(const float* V, int64_t nV, const int32_t* F, int64_t nF, const float* P, int64_t n, float* work,
                    float* out, hipStream_t s);

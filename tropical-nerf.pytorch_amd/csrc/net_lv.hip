@@ -20,6 +20,7 @@
 #include "net_device.h"
 #include "step.h"
 #include "descend.h"
+#include "train_net.h"
 
 #ifndef TNP_LV
 #error "net_lv.hip is compiled once per level count: -DTNP_LV=<2..8>"
@@ -357,6 +358,35 @@ int lv_skel_eval<LVC>(const NetDev& net, int i0, int j0, int k0, int n0, int n1,
 #define TNP_SHAPE_BODY                                                                                         \
   hipLaunchKernelGGL((k_skel_eval<LVC, H, NL>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net, i0, j0, k0, n0, \
                      n1, n2, dist, gmax_bits);
+  TNP_SHAPE_SWITCH(net)
+#undef TNP_SHAPE_BODY
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+
+template <>
+int lv_train<LVC>(const NetDev& net, const float* xyz, const float* gt, int64_t n, float T, float eik_w,
+                  int64_t eik_batch, double* stats, float* g_table, float* g_w, const float* gout, const float* gJ,
+                  float* g_x, hipStream_t s) {
+  const bool train = !gout && !gJ;
+#define TNP_SHAPE_BODY                                                                                            \
+  if (train)                                                                                                      \
+    hipLaunchKernelGGL((k_train_norms<LVC, H, NL>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net, xyz, gt, n, T,  \
+                       stats);                                                                                    \
+  hipLaunchKernelGGL((k_train_grads<LVC, H, NL>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net, xyz, gt, n, T,    \
+                     eik_w, eik_batch, stats, g_table, g_w, gout, gJ, g_x);
+  TNP_SHAPE_SWITCH(net)
+#undef TNP_SHAPE_BODY
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+
+template <>
+int lv_forward_vjp<LVC>(const NetDev& net, const float* xyz, int64_t n, const float* gpl, int64_t ld,
+                        const float* gout2, float* g_table, float* g_w, float* g_x, hipStream_t s) {
+#define TNP_SHAPE_BODY                                                                                           \
+  hipLaunchKernelGGL((k_forward_vjp<LVC, H, NL>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net, xyz, n, gpl, ld, \
+                     gout2, g_table, g_w, g_x);
   TNP_SHAPE_SWITCH(net)
 #undef TNP_SHAPE_BODY
   TNP_CHECK(hipGetLastError());

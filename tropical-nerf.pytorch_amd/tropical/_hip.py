@@ -61,6 +61,8 @@ SIGNATURES = {
     "tnp_sdf_train_grad": (C.c_int, [_NETP, _VP, _VP, _I64, _F, _F, _I64, _VP, _VP, _VP, _VP]),
     "tnp_mesh_signed_distance": (C.c_int, [_VP, _I64, _VP, _I64, _VP, _I64, _VP, _VP, _VP]),
     "tnp_sdf_vjp": (C.c_int, [_NETP, _VP, _VP, _I64, _VP, _VP, _VP]),
+    "tnp_normal_vjp": (C.c_int, [_NETP, _VP, _VP, _I64, _VP, _VP, _VP, _VP]),
+    "tnp_forward_vjp": (C.c_int, [_NETP, _VP, _I64, _VP, _I64, _VP, _VP, _VP, _VP, _VP]),
     "tnp_engine_create": (C.c_int, [C.POINTER(_VP), C.c_int]),
     "tnp_engine_destroy": (None, [_VP]),
     "tnp_engine_set_net": (C.c_int, [_VP, _NETP]),

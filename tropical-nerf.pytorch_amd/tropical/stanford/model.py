@@ -9,15 +9,16 @@ Same constructor, attributes (``enc``, ``fc``, ``num_layers``,
 (encoding + MLP, csrc/net.hip) on the net's ROCm device; the forward is
 bitwise equal to the reference's PyTorch-CPU evaluation.
 
-Autograd: ``sdf`` is differentiable like the reference's (model.py:84-88,
-through tcnn there) -- w.r.t. its input (the analytic input gradient of
-``tnp_sdf_grad``) and w.r.t. the parameters (``tnp_sdf_vjp``: the encoding
-table and the fc weights; 3-layer, 16-hidden nets), so a caller's
-``net.sdf(x).sum().backward()`` fills ``x.grad`` and the parameters'
-``.grad``.  Double backward (the eikonal term's ``create_graph=True``,
-train.py:196) is taken in closed form by
-``tropical.stanford.sdf_train.SDFTrainer`` instead.  ``forward`` / ``region``
-/ ``normal`` return values without a graph, as the extraction uses them.
+Autograd, as the reference's (autograd through tcnn and nn.Linear there):
+``sdf`` is differentiable w.r.t. its input (the analytic input gradient of
+``tnp_sdf_grad``) and the parameters (``tnp_sdf_vjp``: the encoding table
+and the fc weights); ``forward(x, gather)`` w.r.t. both through every
+gathered plane and the output (``tnp_forward_vjp``); ``normal(...,
+create_graph=True)`` returns J with a graph whose backward -- the
+reference's double backward, the eikonal term of train.py:196 -- is
+``tnp_normal_vjp`` (parameters, and the Hessian along the upstream for the
+points).  Every instantiated net shape.  ``region`` and ``normal`` without
+``create_graph`` return values without a graph, as the extraction uses them.
 """
 from __future__ import annotations
 
@@ -48,35 +49,146 @@ class _SDF(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gy):
-        if torch.is_grad_enabled():
-            raise NotImplementedError(
-                "double backward through Net.sdf (the reference's eikonal term, train.py:196): "
-                "tropical.stanford.sdf_train.SDFTrainer takes it in closed form")
         net = ctx.net
         x, J = ctx.saved_tensors
         now = tuple(t._version for t in net._params())
         if any(ctx.needs_input_grad[2:]) and now != ctx.versions:
             raise RuntimeError("Net.sdf backward: a parameter was modified in place after the forward "
                                "(its version changed); the gradient would be taken at other weights")
+        if torch.is_grad_enabled() and ctx.needs_input_grad[1]:
+            # create_graph=True (the reference's Net.normal / eikonal term,
+            # train.py:196): the input gradient g * J with a graph through
+            # _Normal (whose backward is the double backward); the parameter
+            # gradients are returned as values (their own derivatives are not
+            # tracked -- autograd.grad(..., x, create_graph=True) discards them)
+            Jg, _ = _Normal.apply(net, x, *net._params())
+            gx = gy.reshape(-1, 1).to(Jg.dtype) * Jg
+            with torch.no_grad():
+                grads = _SDF._param_vjp(ctx, net, x, gy)
+            return (None, gx.to(x.dtype), *grads)
         g = gy.detach().reshape(-1).float().contiguous()
         gx = (g[:, None] * J).to(x.dtype) if ctx.needs_input_grad[1] else None
+        return (None, gx, *_SDF._param_vjp(ctx, net, x, gy))
+
+    @staticmethod
+    def _param_vjp(ctx, net, x, gy):
         grads = [None] * (len(ctx.needs_input_grad) - 2)
-        if any(ctx.needs_input_grad[2:]):
-            params = net._params()
-            g_table = torch.zeros(params[0].numel(), device=x.device)
-            g_w = torch.zeros(sum(t.numel() for t in params[1:]), device=x.device)
-            s, keep = net.tnp_desc()
-            xs = x.detach().float().contiguous()
-            _hip.check(_hip.lib().tnp_sdf_vjp(ctypes.byref(s), _hip.ptr(xs), _hip.ptr(g), xs.shape[0],
-                                              _hip.ptr(g_table), _hip.ptr(g_w),
-                                              ctypes.c_void_p(_hip.stream_ptr(x.device))), "tnp_sdf_vjp")
-            del keep
-            grads[0] = g_table.view_as(params[0]).to(params[0].dtype)
-            off = 0
-            for k, t in enumerate(params[1:]):
-                grads[1 + k] = g_w[off:off + t.numel()].view_as(t).to(t.dtype)
-                off += t.numel()
-        return (None, gx, *grads)
+        if not any(ctx.needs_input_grad[2:]):
+            return grads
+        g = gy.detach().reshape(-1).float().contiguous()
+        params = net._params()
+        g_table = torch.zeros(params[0].numel(), device=x.device)
+        g_w = torch.zeros(sum(t.numel() for t in params[1:]), device=x.device)
+        s, keep = net.tnp_desc()
+        xs = x.detach().float().contiguous()
+        _hip.check(_hip.lib().tnp_sdf_vjp(ctypes.byref(s), _hip.ptr(xs), _hip.ptr(g), xs.shape[0],
+                                          _hip.ptr(g_table), _hip.ptr(g_w),
+                                          ctypes.c_void_p(_hip.stream_ptr(x.device))), "tnp_sdf_vjp")
+        del keep
+        return _param_grads(net, g_table, g_w, ctx.needs_input_grad[2:])
+
+
+def _param_grads(net, g_table, g_w, needs):
+    """Split the C ABI's packed gradients over the parameters (table, then
+    fc.{i}.weight / bias); None where no gradient is needed."""
+    params = net._params()
+    out = [None] * len(params)
+    if needs[0]:
+        out[0] = g_table.view_as(params[0]).to(params[0].dtype)
+    off = 0
+    for k, t in enumerate(params[1:]):
+        if needs[1 + k]:
+            out[1 + k] = g_w[off:off + t.numel()].view_as(t).to(t.dtype)
+        off += t.numel()
+    return out
+
+
+class _Forward(torch.autograd.Function):
+    """Net.forward with its backward (the reference's is autograd through tcnn
+    and nn.Linear, model.py:52-76): outputs the gathered planes (plane-major
+    [K, n], as tnp_forward writes them) and the output [n, 2]; the backward
+    is one tnp_forward_vjp call (table, fc parameters and the points)."""
+
+    @staticmethod
+    def forward(ctx, net, x, table, *weights):
+        pre, out = net._forward_planes(x, 1, want_out=True)
+        ctx.net = net
+        ctx.versions = tuple(t._version for t in (table,) + weights)
+        ctx.save_for_backward(x)
+        return pre, out
+
+    @staticmethod
+    def backward(ctx, g_pre, g_out):
+        if torch.is_grad_enabled():
+            raise NotImplementedError("double backward through Net.forward")
+        net = ctx.net
+        (x,) = ctx.saved_tensors
+        if any(ctx.needs_input_grad[2:]) and tuple(t._version for t in net._params()) != ctx.versions:
+            raise RuntimeError("Net.forward backward: a parameter was modified in place after the forward")
+        n = x.shape[0]
+        gp = None if g_pre is None else g_pre.detach().float().contiguous()
+        go = None if g_out is None else g_out.detach().float().contiguous()
+        params = net._params()
+        g_table = torch.zeros(params[0].numel(), device=x.device)
+        g_w = torch.zeros(sum(t.numel() for t in params[1:]), device=x.device)
+        gx = torch.zeros(n, 3, device=x.device) if ctx.needs_input_grad[1] else None
+        if gp is None and go is None:
+            return (None, None, *([None] * len(params)))
+        s, keep = net.tnp_desc()
+        xs = x.detach().float().contiguous()
+        _hip.check(_hip.lib().tnp_forward_vjp(ctypes.byref(s), _hip.ptr(xs), n, _hip.ptr(gp), n, _hip.ptr(go),
+                                              _hip.ptr(g_table), _hip.ptr(g_w), _hip.ptr(gx),
+                                              ctypes.c_void_p(_hip.stream_ptr(x.device))), "tnp_forward_vjp")
+        del keep
+        grads = _param_grads(net, g_table, g_w, ctx.needs_input_grad[2:])
+        return (None, None if gx is None else gx.to(x.dtype), *grads)
+
+
+class _Normal(torch.autograd.Function):
+    """Net.normal(create_graph=True): J = d sdf / d x as a differentiable
+    output (the reference's autograd.grad(..., create_graph=True) through
+    tcnn, model.py:105-123); its backward -- the reference's double
+    backward -- is one tnp_normal_vjp call (the parameters' gradient of
+    gJ . J and the Hessian of sdf along gJ for the points)."""
+
+    @staticmethod
+    def forward(ctx, net, x, table, *weights):
+        y, J = net._sdf_eval(x, want_grad=True)
+        ctx.net = net
+        ctx.versions = tuple(t._version for t in (table,) + weights)
+        ctx.save_for_backward(x)
+        return J, y.unsqueeze(-1)
+
+    @staticmethod
+    def backward(ctx, gJ, gy):
+        if torch.is_grad_enabled():
+            raise NotImplementedError("third-order derivatives through Net.normal")
+        net = ctx.net
+        (x,) = ctx.saved_tensors
+        if any(ctx.needs_input_grad[2:]) and tuple(t._version for t in net._params()) != ctx.versions:
+            raise RuntimeError("Net.normal backward: a parameter was modified in place after the forward")
+        n = x.shape[0]
+        params = net._params()
+        g_table = torch.zeros(params[0].numel(), device=x.device)
+        g_w = torch.zeros(sum(t.numel() for t in params[1:]), device=x.device)
+        gx = torch.zeros(n, 3, device=x.device) if ctx.needs_input_grad[1] else None
+        s, keep = net.tnp_desc()
+        xs = x.detach().float().contiguous()
+        stream = ctypes.c_void_p(_hip.stream_ptr(x.device))
+        if gJ is not None:
+            g = gJ.detach().float().contiguous()
+            _hip.check(_hip.lib().tnp_normal_vjp(ctypes.byref(s), _hip.ptr(xs), _hip.ptr(g), n, _hip.ptr(g_table),
+                                                 _hip.ptr(g_w), _hip.ptr(gx), stream), "tnp_normal_vjp")
+        if gy is not None:  # the returned y (return_y=True): Net.sdf's backward
+            g1 = gy.detach().reshape(-1).float().contiguous()
+            _hip.check(_hip.lib().tnp_sdf_vjp(ctypes.byref(s), _hip.ptr(xs), _hip.ptr(g1), n, _hip.ptr(g_table),
+                                              _hip.ptr(g_w), stream), "tnp_sdf_vjp")
+            if gx is not None:
+                _, J = net._sdf_eval(x, want_grad=True)
+                gx += g1[:, None] * J
+        del keep
+        grads = _param_grads(net, g_table, g_w, ctx.needs_input_grad[2:])
+        return (None, None if gx is None else gx.to(x.dtype), *grads)
 
 
 class Net(nn.Module):
@@ -189,7 +301,13 @@ class Net(nn.Module):
         return pre, out2
 
     def forward(self, x, gather: bool = False, group: int = 1):
-        pre, out = self._forward_planes(x, group, want_out=True)
+        params = self._params()
+        if (group == 1 and torch.is_grad_enabled()
+                and (x.requires_grad or any(p.requires_grad for p in params))):
+            # differentiable as the reference's (autograd through tcnn and nn.Linear)
+            pre, out = _Forward.apply(self, x, *params)
+        else:
+            pre, out = self._forward_planes(x, group, want_out=True)
         if not gather:
             return out
         H = self.num_hidden
@@ -249,6 +367,14 @@ class Net(nn.Module):
             raise NotImplementedError("Net.normal: per-neuron gradients (the reference's "
                                       "l/h branch references an undefined global)")
         _hip.require_cuda(vertices, "Net.normal")
+        if create_graph:
+            # J with a graph (the reference's create_graph=True): differentiable
+            # w.r.t. the parameters and the points (_Normal's double backward)
+            if not vertices.requires_grad:
+                vertices.requires_grad_(True)
+            with torch.enable_grad():
+                J, y = _Normal.apply(self, vertices, *self._params())
+            return (J, y) if return_y else J
         s, keep = self.tnp_desc()
         x = vertices.detach().float().contiguous()
         y = torch.empty(x.shape[0], device=x.device)

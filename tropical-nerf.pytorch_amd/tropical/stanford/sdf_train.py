@@ -32,8 +32,6 @@ class SDFTrainer:
     (train.py:86-90); ``step(x, gt)`` is one iteration of train.py:177-205."""
 
     def __init__(self, net, lr: float = 1e-3, T_max: float = 500.0, batch_size: int = BATCH_SIZE):
-        if net.num_layers != 3 or net.num_hidden != 16:
-            raise NotImplementedError("SDF training is built for the reference's 3-layer, 16-hidden nets")
         self.net = net
         self.batch_size = int(batch_size)
         self.opt = torch.optim.Adam(net.parameters(), lr=lr)
