@@ -38,6 +38,16 @@ int tnp_engine_debug_lb_recomputes(tnp_engine* eng, int64_t* n, int reset, void*
  * it off): on = 0 sends every bucket's records through memory, as before. */
 int tnp_engine_debug_set_lds_records(tnp_engine* eng, int on);
 
+/* Debug: the curve branch's gradient-descent fallback (descend.h, the
+ * engine's launch) on n arbitrary rows: row r descends along the edge
+ * d_ends[r] (e0 xyz, e1 xyz) from the box parameters d_x[r] (in/out) on
+ * plane pair (d_plane[r], idx) for exactly `iters` iterations (<= 512);
+ * d_d0 / d_d1: the distances evaluated before the last update.  The batch
+ * is the n rows (MKL row-count schedules).  per_thread: the one-thread-per-
+ * row kernel.  Checked against the oracle's descend (oracle/curve.py). */
+int tnp_debug_descend(const tnp_net* net, const float* d_ends, float* d_x, const int32_t* d_plane, int64_t n,
+                      int idx, float eps, int iters, float* d_d0, float* d_d1, int per_thread, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

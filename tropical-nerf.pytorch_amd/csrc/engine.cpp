@@ -2211,6 +2211,48 @@ extern "C" int tnp_engine_debug_lb_recomputes(tnp_engine* e, int64_t* n, int res
   return 0;
 }
 
+// debugging aid: the gradient-descent fallback on arbitrary rows
+// (tropical_hip_debug.h; checked against the oracle's descent)
+extern "C" int tnp_debug_descend(const tnp_net* n, const float* d_ends, float* d_x, const int32_t* d_plane,
+                                 int64_t N, int idx, float eps, int iters, float* d_d0, float* d_d1, int per_thread,
+                                 void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (check_net(n)) return -1;
+  if (N <= 0) return 0;
+  if (N > (1 << 20)) { tnp_set_error("debug_descend: at most 2^20 rows"); return -1; }
+  NetDev net = to_dev(n);
+  // the engine's operands for rows of a made-up complex: vertices 2r, 2r + 1
+  // are the ends of split r, which is curve row r and descending row r
+  std::vector<int32_t> h(4 * N);
+  for (int64_t r = 0; r < N; ++r) {
+    h[r] = (int32_t)(2 * r);          // sa
+    h[N + r] = (int32_t)(2 * r + 1);  // sb
+    h[2 * N + r] = (int32_t)r;        // crow
+    h[3 * N + r] = (int32_t)r;        // glist
+  }
+  int32_t* d = nullptr;
+  unsigned long long* conv = nullptr;
+  TNP_CHECK(hipMalloc(&d, 4 * N * sizeof(int32_t)));
+  TNP_CHECK(hipMalloc(&conv, 8 * sizeof(unsigned long long)));
+  int rc = hipMemcpyAsync(d, h.data(), 4 * N * sizeof(int32_t), hipMemcpyHostToDevice, s) == hipSuccess ? 0 : -1;
+  if (rc == 0) {
+    const char* prev = getenv("TNP_DESCEND_THREAD");
+    std::string keep = prev ? prev : "";
+    setenv("TNP_DESCEND_THREAD", per_thread ? "1" : "0", 1);
+    rc = launch_descend(net, N, d + 3 * N, d + 2 * N, d, d + N, d_ends, d_plane, idx, eps, iters, 0, d_x, d_d0,
+                        d_d1, conv, s);
+    if (prev) setenv("TNP_DESCEND_THREAD", keep.c_str(), 1);
+    else unsetenv("TNP_DESCEND_THREAD");
+  }
+  if (hipStreamSynchronize(s) != hipSuccess && rc == 0) {
+    tnp_set_error("debug_descend: stream synchronise failed");
+    rc = -1;
+  }
+  (void)hipFree(d);
+  (void)hipFree(conv);
+  return rc;
+}
+
 // debugging aid: the padded angular scores of the last tnp_engine_faces call
 // (F x width fp32, final-row order); returns F and width
 extern "C" int tnp_engine_faces_debug(tnp_engine* e, float* d_scores, int64_t cap, int64_t* F, int64_t* width,

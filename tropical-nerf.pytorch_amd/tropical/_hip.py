@@ -92,6 +92,8 @@ SIGNATURES = {
     "tnp_engine_set_collective": (C.c_int, [_VP, _VP, _VP]),
     "tnp_engine_set_shards": (C.c_int, [_VP, C.c_int]),
     "tnp_debug_ops": (C.c_int, [_VP, _VP, _VP, C.c_int64, _VP, _VP]),
+    "tnp_debug_descend": (C.c_int, [_NETP, _VP, _VP, _VP, C.c_int64, C.c_int, C.c_float, C.c_int, _VP, _VP,
+                                    C.c_int, _VP]),
     "tnp_engine_faces_debug": (C.c_int, [_VP, _VP, C.c_int64, _P64, _P64, _VP]),
     "tnp_engine_debug_set_lb_spin": (C.c_int, [_VP, C.c_int]),
     "tnp_engine_debug_set_lds_records": (C.c_int, [_VP, C.c_int]),

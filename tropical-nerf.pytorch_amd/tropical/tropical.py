@@ -43,7 +43,11 @@ def compute_marks(L: int, n_min: int, b: float, scale: float = 1.0, eps: float =
 
     Same float64 cell size / fp32 ``arange`` construction and the same
     sequential merge of marks closer than eps, so the marks are bitwise the
-    reference's."""
+    reference's.
+
+    Attribution: this construction restates seonghunn/tropical-nerf.pytorch
+    (tropical/tropical.py:49-79, Copyright (c) 2024-present NAVER Cloud Corp.),
+    licensed CC BY-SA 4.0; the marks have to be the reference's bit for bit."""
     cand = []
     for l in range(L):
         n_cells = np.exp2(l * np.log2(b)) * n_min - 1.0
