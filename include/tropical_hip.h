@@ -214,7 +214,11 @@ int tnp_engine_set_curve(tnp_engine* eng, int on);
  * engine calls it only with tnp_engine_set_shards(n > 1), every shard the
  * same calls in the same order.  fn == NULL: none (the branch then refuses
  * n > 1 shards).  Binds to the host language's all-reduce (the Python
- * driver: torch.distributed, tropical/_engine.py run_steps). */
+ * driver: torch.distributed, tropical/_engine.py run_steps).  Every call
+ * carries one word more than the decision it takes: the shard's failure
+ * flag, so a shard that fails between two collectives still joins the next
+ * one and every shard returns -1 from that same call (none waits on a
+ * collective its peer never reaches). */
 enum { TNP_COLL_SUM = 0, TNP_COLL_MAX = 1, TNP_COLL_AND = 2, TNP_COLL_OR = 3 };
 typedef int (*tnp_collective_fn)(int64_t* vec, int n, int op, void* ctx);
 int tnp_engine_set_collective(tnp_engine* eng, tnp_collective_fn fn, void* ctx);
@@ -271,7 +275,7 @@ int tnp_engine_kernel_stat(tnp_engine* eng, int i, char* name, int cap, double* 
  * The per-step global decisions of the sharded loop (subpoly.py:110 "does
  * anything split", subpoly_debug.py:43-49 the failover override, and the OR
  * of the ranks' next-active plane masks) between the processes of ONE node
- * through a POSIX shared-memory segment: every rank writes <= 8 int64 words,
+ * through a POSIX shared-memory segment: every rank writes <= 16 int64 words,
  * arrives on an atomic counter and spins until all have (no library
  * collective, no device copies).  Rank 0 creates the segment (create=1)
  * before the others open it; it can be unlinked once all have.  allreduce

@@ -20,6 +20,9 @@ def cases(kind=None):
     out = []
     for f in sorted(os.listdir(GOLDEN)):
         if f.endswith(".npz"):
+            with np.load(os.path.join(GOLDEN, f), allow_pickle=False) as z:
+                if "kind" not in z.files:  # not a subpoly case (descend_cases.npz)
+                    continue
             d = load(f[:-4])
             if kind is None or str(d["kind"]) == kind:
                 out.append(f[:-4])

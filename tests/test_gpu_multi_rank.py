@@ -1,4 +1,4 @@
-"""GPU, 2-3 ranks sharing one MI355X over gloo: the sharded HIP engine.
+"""GPU, 2-8 ranks sharing one MI355X over gloo: the sharded HIP engine.
 
 Each rank runs the device engine on its x-slab (plus halo) with the
 reference's whole-complex decisions taken through bench.Collective; the
@@ -107,9 +107,23 @@ def _worker(rank, world, port, outdir, case, mode):
         tot = torch.tensor([owned.shape[0], gE.shape[0], hv, he, splits], dtype=torch.int64)
         dist.all_reduce(tot)
         SV, SE = D.gather_complex(owned.cpu(), first, gE.cpu())
+        # then a plain single-device subpoly(force=False) in the same process:
+        # engine_for must hand it an engine without the sharded run's shard
+        # count, owned range and x span
+        import contextlib
+        import io
+        from golden_io import sha
+        import tropical.subpoly as sp
+        single_ok = torch.tensor([1])
+        if mode != "lattice":  # (the lattice goldens hold the full-lattice surface, not subpoly's)
+            with contextlib.redirect_stdout(io.StringIO()):
+                _, verts, fwi = sp.subpoly(net, 3, 1.2, force=mode != "curve")
+            single_ok[0] = int(verts.shape[0] == int(d["n_surf"][0]) and
+                               sha(np.asarray(fwi, dtype=np.int64)) == str(d["sha_tri"]))
+        dist.all_reduce(single_ok, op=dist.ReduceOp.MIN)
         if rank == 0:
             np.savez(os.path.join(outdir, "out.npz"), tot=tot.numpy(), V=SV.numpy(), E=SE.numpy(),
-                     cuts=np.array(cuts))
+                     cuts=np.array(cuts), single_ok=single_ok.numpy())
     finally:
         dist.destroy_process_group()
 
@@ -177,6 +191,8 @@ def test_sharded_curve_branch(cuda, tmp_path, case, world):
     z = _run(tmp_path, case, "curve", world)
     assert tuple(int(x) for x in z["tot"]) == want
     assert z["V"].shape[0] == want[0] and z["E"].shape[0] == want[1]
+    # a single-device subpoly(force=False) after the sharded run, same process
+    assert int(z["single_ok"][0]) == 1
 
 
 @pytest.mark.timeout(600)

@@ -131,6 +131,7 @@ struct tnp_engine {
   int pend_tight = 0;
   tnp_collective_fn coll_fn = nullptr;  // a sharded step's in-step decisions (tnp_engine_set_collective)
   void* coll_ctx = nullptr;
+  bool coll_err = false;  // this shard failed: the next collective says so (coll_fail)
   int gd_iters = 500;     // subpoly_debug.py:141
   int64_t max_pair_tests = 20000000000LL;
   bool kt_on = false;
@@ -766,7 +767,12 @@ extern "C" int tnp_engine_active_planes(tnp_engine* e, int from, uint64_t* mask,
 // of non-axis-aligned split edges to the trilinear intersection, with the
 // gradient-descent fallback; leaves per-split strict-filter inputs in cinfo.
 // ---------------------------------------------------------------------------
-// the shards' reduction of n words (tnp_engine_set_collective); one shard: none
+// the shards' reduction of n words (tnp_engine_set_collective); one shard:
+// none.  Every call carries one more word, this shard's failure flag
+// (coll_fail), reduced with the same op: a shard that failed between two
+// collectives joins the next one with the flag set, and every shard then
+// fails at that same call -- none is left blocked in a collective its peer
+// never reaches.
 static int coll(tnp_engine* e, int64_t* v, int n, int op) {
   if (e->shards <= 1) return 0;
   if (!e->coll_fn) {
@@ -774,11 +780,33 @@ static int coll(tnp_engine* e, int64_t* v, int n, int op) {
                   "(tnp_engine_set_collective)", e->shards);
     return -1;
   }
-  if (e->coll_fn(v, n, op, e->coll_ctx) != 0) {
+  const bool all_ones = op == TNP_COLL_AND;  // AND: "no failure" is all ones
+  std::vector<int64_t> w(v, v + n);
+  w.push_back(e->coll_err ? (all_ones ? 0 : 1) : (all_ones ? -1 : 0));
+  if (e->coll_fn(w.data(), n + 1, op, e->coll_ctx) != 0) {
     tnp_set_error("the shards' collective failed");
     return -1;
   }
+  if (all_ones ? w[n] != -1 : w[n] != 0) {
+    if (!e->coll_err) tnp_set_error("a peer shard failed in this sharded step (its own error names the cause)");
+    e->coll_err = false;
+    return -1;
+  }
+  std::copy(w.begin(), w.begin() + n, v);
   return 0;
+}
+
+// this shard failed before the step's next collective (n words, op): join
+// it with the failure flag set, keep this shard's own error message
+static int coll_fail(tnp_engine* e, int n, int op) {
+  if (e->shards <= 1 || !e->coll_fn) return -1;
+  const std::string msg = g_err;
+  std::vector<int64_t> v(n, op == TNP_COLL_AND ? -1 : 0);
+  e->coll_err = true;
+  (void)coll(e, v.data(), n, op);
+  e->coll_err = false;
+  g_err = msg;
+  return -1;
 }
 
 // curve path, phase 1 (subpoly.py:120-177, subpoly_debug.py:121-165).  On
@@ -795,7 +823,10 @@ static int curve_correct(tnp_engine* e, int idx, int64_t S, hipStream_t s) {
   const int32_t* sa = P<int32_t>(e->sa);
   const int32_t* sb = P<int32_t>(e->sb);
   float* xyz = P<float>(e->cur.xyz);
+  // (sharded: a segment that fails joins the step's next collective with the
+  // failure flag, coll_fail, so every shard stops at the same call)
   int64_t B = 0;
+  auto seg_flags = [&]() -> int {
   if (S > 0) {
     if (buf_ensure(cv[CV_CFLAG], S * sizeof(int32_t), s)) return -1;
     if (buf_ensure(cv[CV_COFF], S * sizeof(int64_t), s)) return -1;
@@ -808,6 +839,9 @@ static int curve_correct(tnp_engine* e, int idx, int64_t S, hipStream_t s) {
     if (read_ctr(e, s)) return -1;
     B = e->h_ctr[CTR_B];
   }
+  return 0;
+  };
+  if (seg_flags()) return coll_fail(e, 1, TNP_COLL_SUM);
   const bool sh = e->shards > 1;
   int64_t Bg = B;  // the batch's curve rows (r_edges, subpoly.py:120)
   if (coll(e, &Bg, 1, TNP_COLL_SUM)) return -1;
@@ -819,6 +853,7 @@ static int curve_correct(tnp_engine* e, int idx, int64_t S, hipStream_t s) {
   float* ints = nullptr;
   float* d0s = nullptr;
   float* d1s = nullptr;
+  auto seg_rows = [&]() -> int {
   if (B > 0) {
   if (buf_ensure(cv[CV_CROW], B * sizeof(int32_t), s)) return -1;
   if (buf_ensure(cv[CV_CORNERS], 24 * B * sizeof(float), s)) return -1;
@@ -865,6 +900,9 @@ static int curve_correct(tnp_engine* e, int idx, int64_t S, hipStream_t s) {
   }
   G = e->h_ctr[CTR_G];
   }  // B > 0
+  return 0;
+  };
+  if (seg_rows()) return coll_fail(e, 1, TNP_COLL_SUM);
   int64_t Gg = G;  // the batch's descent rows
   if (coll(e, &Gg, 1, TNP_COLL_SUM)) return -1;
   if (Gg > 0) {
@@ -872,6 +910,7 @@ static int curve_correct(tnp_engine* e, int idx, int64_t S, hipStream_t s) {
     uint64_t h_conv[8] = {~0ull, ~0ull, ~0ull, ~0ull, ~0ull, ~0ull, ~0ull, ~0ull};  // (no rows: converged)
     int32_t* glist = nullptr;
     unsigned long long* conv = nullptr;
+    auto seg_desc = [&]() -> int {
     if (G > 0) {
       if (buf_ensure(cv[CV_GLIST], G * sizeof(int32_t), s)) return -1;
       if (buf_ensure(cv[CV_CONV], 8 * sizeof(uint64_t), s)) return -1;
@@ -886,12 +925,17 @@ static int curve_correct(tnp_engine* e, int idx, int64_t S, hipStream_t s) {
       TNP_CHECK(hipMemcpyAsync(h_conv, conv, sizeof(h_conv), hipMemcpyDeviceToHost, s));
       TNP_CHECK(hipStreamSynchronize(s));
     }
+    return 0;
+    };
+    if (seg_desc()) return coll_fail(e, 8, TNP_COLL_AND);
     // the loop of subpoly_debug.py:141 stops when EVERY row of the batch met
     // both planes: the AND of the shards' per-iteration words
     if (coll(e, reinterpret_cast<int64_t*>(h_conv), 8, TNP_COLL_AND)) return -1;
-    int stop = -1;  // first iteration after which every row met both planes
+    int stop = -1;  // first iteration after which every row met both planes (the replay below
+                    // fails towards the step's next collective, the strict flag's OR)
     for (int i = 0; i < e->gd_iters && stop < 0; ++i)
       if ((h_conv[i >> 6] >> (i & 63)) & 1) stop = i;
+    auto seg_replay = [&]() -> int {
     if (G > 0 && stop >= 0 && stop + 1 < e->gd_iters) {
       // the loop ends after iteration `stop`: replay
       TNP_CHECK(hipMemcpyAsync(ints, cv[CV_INTS0].p, 3 * B * sizeof(float), hipMemcpyDeviceToDevice, s));
@@ -899,11 +943,18 @@ static int curve_correct(tnp_engine* e, int idx, int64_t S, hipStream_t s) {
             launch_descend(ns, G, glist, crow, sa, sb, xyz, plane, idx, eps, stop + 1, 0, ints,
                            d0s, d1s, conv, s));
     }
+    return 0;
+    };
+    if (seg_replay()) return coll_fail(e, 1, TNP_COLL_OR);
   }
+  auto seg_apply = [&]() -> int {
   if (B > 0)
     TIMED("curve_apply", 60.0 * B,
           launch_curve_apply(B, crow, sa, sb, xyz, e->V, ints, d0s, P<int32_t>(cv[CV_GG]), eps,
                              P<int32_t>(cv[CV_CINFO]), ctr, s));
+  return 0;
+  };
+  if (seg_apply()) return coll_fail(e, 1, TNP_COLL_OR);
   return 0;
 }
 
@@ -997,9 +1048,16 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
   e->valid = false;  // until this split has completed
   const float eps = e->net.eps_s;  // subpoly_'s eps: hits, split point, failover
   const float* col = P<float>(e->cur.pre) + (int64_t)idx * e->cur.cap;
-  TNP_CHECK(hipMemsetAsync(e->ctr.p, 0, CTR_CLEAR_BYTES, s));
+  // curve branch on shards: the new vertices' forward follows the schedule
+  // of the whole batch (the shards' total split count), and every shard
+  // joins the branch's decisions (curve_correct) whatever its own count; a
+  // shard failing between two of the step's collectives joins the next one
+  // with its failure flag (coll_fail)
+  const bool ccoll = e->curve && e->shards > 1;
   int64_t S = 0;
   e->pend_hits = false;
+  auto seg_split = [&]() -> int {
+  TNP_CHECK(hipMemsetAsync(e->ctr.p, 0, CTR_CLEAR_BYTES, s));
   if (e->E > 0) {
     // single pass; the id buffers hold the upper bound E (capacity is kept)
     if (buf_ensure(e->sa, e->E * sizeof(int32_t), s)) return -1;
@@ -1042,7 +1100,6 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
     }
     ktimer_set_bytes(e, "split", 1.0 * e->E + 13.0 * S + (e->pend_hoff >= 0 ? 5.0 * e->V : 0.0));
   }
-  *fail = 0;
   if (e->V + S >= (int64_t)INT32_MAX) {
     // slots (dead ones included: compaction is lazy) are int32 ids in sa/sb,
     // members, edges and the packed pair keys
@@ -1050,22 +1107,27 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
                   (long long)e->V, (long long)S);
     return -1;
   }
-  // curve branch on shards: the new vertices' forward follows the schedule
-  // of the whole batch (the shards' total split count), and every shard
-  // joins the branch's decisions (curve_correct) whatever its own count
-  const bool ccoll = e->curve && e->shards > 1;
+  return 0;
+  };
+  if (seg_split()) return ccoll ? coll_fail(e, 1, TNP_COLL_SUM) : -1;
+  *fail = 0;
   int64_t Sg = S;
   if (ccoll && coll(e, &Sg, 1, TNP_COLL_SUM)) return -1;
   if (ccoll && S == 0 && Sg > 0 && curve_correct(e, idx, 0, s)) return -1;
   if (S > 0) {
+    auto seg_new = [&]() -> int {
     if (vset_ensure(e, e->cur, e->V + S, e->V, s)) return -1;
     col = P<float>(e->cur.pre) + (int64_t)idx * e->cur.cap;  // may have moved
-    if (e->curve) {
+    if (e->curve)
       TIMED("new_vertices", 52.0 * S,
             launch_new_vertices(P<int32_t>(e->sa), P<int32_t>(e->sb), S, col, eps, P<float>(e->cur.xyz),
                                 e->V, s));
-      if (curve_correct(e, idx, S, s)) return -1;
-    }
+    return 0;
+    };
+    // (the curve branch's next collective: curve_correct's first)
+    if (seg_new()) return ccoll ? coll_fail(e, 1, TNP_COLL_SUM) : -1;
+    if (e->curve && curve_correct(e, idx, S, s)) return -1;
+    auto seg_rest = [&]() -> int {
     if (buf_ensure(e->shared, S * sizeof(uint64_t), s)) return -1;
     e->pend_fused = !e->curve;
     if (e->pend_fused) {
@@ -1108,6 +1170,10 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
     } else {
       *fail = -1;  // single device: the finish kernels read it in place
     }
+    return 0;
+    };
+    // (then the strict filter flag's OR)
+    if (seg_rest()) return ccoll ? coll_fail(e, 1, TNP_COLL_OR) : -1;
   }
   e->pend_dup = S > 0 ? e->h_ctr[CTR_DUP] : 0;
   e->pend_tight = (S > 0 && e->curve) ? (int)e->h_ctr[CTR_TIGHT] : 0;

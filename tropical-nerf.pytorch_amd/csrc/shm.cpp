@@ -25,7 +25,7 @@
 #include "common.h"
 
 namespace {
-constexpr int SHM_WORDS = 8;
+constexpr int SHM_WORDS = 16;  // (the curve branch: 8 convergence words + the failure word)
 struct Hdr {
   std::atomic<uint64_t> arrive;
   char pad[56];

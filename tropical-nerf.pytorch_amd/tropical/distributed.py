@@ -57,7 +57,7 @@ from torch import Tensor
 class ShmCollective:
     """The per-step agreements (run_steps' ``allreduce(vec, op)``) between
     the ranks of ONE node through host shared memory (csrc/shm.cpp,
-    tnp_shm_*): every rank writes its <= 8 words and spins on one atomic
+    tnp_shm_*): every rank writes its <= 16 words and spins on one atomic
     counter -- no library collective, no device copies.  Same results as an
     all_gather + host reduction: "max" (int64), "or" / "and" (64-bit masks),
     "sum"."""
@@ -84,8 +84,8 @@ class ShmCollective:
         if rank == 0:
             self._lib.tnp_shm_unlink(self.name)  # the mappings stay; nothing left in /dev/shm
         self.h = h
-        self._in = np.zeros(8, dtype=np.int64)
-        self._out = np.zeros(8, dtype=np.int64)
+        self._in = np.zeros(16, dtype=np.int64)  # csrc/shm.cpp SHM_WORDS
+        self._out = np.zeros(16, dtype=np.int64)
 
     def __call__(self, vec, op: str):
         from . import _hip
