@@ -35,7 +35,10 @@ typedef struct tnp_net {
   int32_t n_levels;   /* L  (2..8 are instantiated) */
   int32_t n_features; /* F  (must be 2) */
   int32_t num_layers; /* with num_hidden, one of the instantiated shapes */
-  int32_t num_hidden; /* (layers, hidden): (2..4, 8) (2..4, 16) (2, 32) -- K <= 63 planes */
+  int32_t num_hidden; /* (layers, hidden): (2..4, 8) (2..4, 16) (2, 32) -- K <= 63 planes, every
+                         operation; (5, 16) (3, 32) (4, 32) -- K = 65 / 97, two-word sign keys:
+                         forward, region, sdf, skeleton and the flat single-device steps and
+                         faces (no curve branch, sharding, training or autograd kernels) */
   int32_t n_marks;    /* len(TropicalHashGrid.marks) */
   float eps;          /* Net.eps (model.py:20) */
   float scales[TNP_MAX_LEVELS];    /* fp32 exp2(l*log2 b)*N_min - 1 */

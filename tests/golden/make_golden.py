@@ -121,6 +121,13 @@ CASES = {
     "h32_rand_curve": ("curve", dict(SMALL, num_layers=2, num_hidden=32), ("rand", 43, 0.05), None),
     "synth24_l4h8": ("lattice", None, ("rand", 31, 0.1), (24, 19, dict(num_layers=4, num_hidden=8))),
     "synth20_h32": ("lattice", None, ("rand", 37, 0.1), (20, 19, dict(num_layers=2, num_hidden=32))),
+    # K > 63 planes (two-word sign keys, csrc/common.h Key<2>): Net(3 layers,
+    # 32 hidden) K = 65, Net(5 layers, 16 hidden) K = 65, Net(4, 32) K = 97 --
+    # the flat path from the skeleton and from lattices
+    "h32l3_rand": ("subpoly", dict(SMALL, num_layers=3, num_hidden=32), ("rand", 47, 0.05), None),
+    "h16l5_sphere": ("subpoly", dict(SMALL, num_layers=5), ("fit", sphere, 61), None),
+    "synth16_h32l3": ("lattice", None, ("rand", 53, 0.1), (16, 19, dict(num_layers=3, num_hidden=32))),
+    "synth8_h32l4": ("lattice", None, ("rand", 59, 0.1), (8, 19, dict(num_layers=4, num_hidden=32))),
     # the curve branch with strict=False (subpoly_(..., strict=False),
     # subpoly.py:198-203): every split stays, no strict_check -- driven step
     # by step through subpoly_ from the skeleton (subpoly() never passes it)

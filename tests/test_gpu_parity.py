@@ -24,9 +24,11 @@ def _rand_points(n, seed=0):
 # levels, 8 levels, and lattices of 4 layers x 8 hidden / 2 layers x 32
 SHAPES = [n for n in ("small4l_sphere", "h32_torus", "h8l3_sphere", "lv8_rand", "synth24_l4h8", "synth20_h32")
           if n in cases()]
+# K > 63 planes (two-word sign keys): 3 x 32 and 5 x 16 (K = 65), 4 x 32 (K = 97)
+WIDE = [n for n in ("h32l3_rand", "h16l5_sphere", "synth16_h32l3", "synth8_h32l4") if n in cases()]
 
 
-@pytest.mark.parametrize("name", ["small_sphere", "synth32", "small_rand"] + SHAPES)
+@pytest.mark.parametrize("name", ["small_sphere", "synth32", "small_rand"] + SHAPES + WIDE)
 def test_forward_bitwise(cuda, name):
     d = load(name)
     net, ref = product_net(d, cuda), oracle_net(d)
@@ -44,7 +46,7 @@ def test_forward_bitwise(cuda, name):
     assert torch.equal(out.cpu(), out_ref)
 
 
-@pytest.mark.parametrize("name", ["small_sphere"] + SHAPES)
+@pytest.mark.parametrize("name", ["small_sphere"] + SHAPES + WIDE)
 @pytest.mark.parametrize("n", [1, 2, 3, 5, 7, 8, 15, 16, 17, 64])
 def test_forward_small_batches_bitwise(cuda, name, n):
     """A call's row count selects the reference's MKL summation schedule
@@ -75,7 +77,7 @@ def test_encoding_bitwise(cuda, name):
     assert torch.equal(got, want)
 
 
-@pytest.mark.parametrize("name", ["small_sphere", "synth24"])
+@pytest.mark.parametrize("name", ["small_sphere", "synth24"] + WIDE[:1])
 def test_region_and_sdf(cuda, name):
     d = load(name)
     net, ref = product_net(d, cuda), oracle_net(d)
@@ -356,3 +358,22 @@ def test_subpoly_step_rewrites_caller_edges(cuda, force):
         assert torch.equal(E2[:E.shape[0]], E)
         assert int(E[changed, 1].min()) >= V.shape[0]
         break
+
+
+@pytest.mark.parametrize("name", WIDE[:1])
+def test_wide_net_refuses_curve_and_shards(cuda, name):
+    """A K > 63 net runs the flat single-device path; the curve branch and
+    sharding refuse it with a message instead of computing on one-word keys."""
+    from tropical._engine import engine_for
+    d = load(name)
+    net = product_net(d, cuda)
+    eng = engine_for(net)
+    eng.skeleton(128, 1.2)
+    v0, e0, _ = eng.export()
+    eng.load(v0, e0, keep_all=True)
+    eng.set_curve(True)
+    try:
+        with pytest.raises(RuntimeError, match="two-word sign keys"):
+            eng.split(0)
+    finally:
+        eng.set_curve(False)

@@ -4,6 +4,11 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Rounding: every square root is sqrtf (hipcc's default lowering is the
+// correctly rounded v_sqrt_f32 + fma-check sequence); HIP's __fsqrt_rn is
+// the bare v_sqrt_f32 (up to 1 ulp off) unless OCML_BASIC_ROUNDED_OPERATIONS
+// is defined, so it never appears in a kernel that must match torch bitwise.
+// __fdiv_rn and plain '/' are the correctly rounded division sequence.
 #define TNP_BLOCK 256
 #define TNP_WAVES (TNP_BLOCK / 64)
 
@@ -306,6 +311,173 @@ __device__ __forceinline__ T ld_agent(const T* p) {
   return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// ---------------------------------------------------------------------------
+// Sign keys of KW 64-bit words (bit p of word p / 64: plane p).  Nets of
+// K <= 63 planes use one word (every kernel's original form), K in 64..127
+// two (the wide shapes, net_device.h TNP_WIDE_SHAPES).  Arrays of keys are
+// word arrays with KW words per vertex; the interleaved (pos, zero) copy pz
+// holds pos words then zero words, 2 KW per vertex.
+// ---------------------------------------------------------------------------
+template <int KW>
+struct Key {
+  uint64_t w[KW];
+};
+template <int KW>
+__host__ __device__ __forceinline__ Key<KW> key_zero() {
+  Key<KW> k;
+#pragma unroll
+  for (int q = 0; q < KW; ++q) k.w[q] = 0;
+  return k;
+}
+// bits [0, n) (n <= 64 KW)
+template <int KW>
+__host__ __device__ __forceinline__ Key<KW> key_below(int n) {
+  Key<KW> k;
+#pragma unroll
+  for (int q = 0; q < KW; ++q) {
+    const int b = n - 64 * q;
+    k.w[q] = b >= 64 ? ~0ull : (b <= 0 ? 0ull : ((1ull << b) - 1ull));
+  }
+  return k;
+}
+template <int KW>
+__host__ __device__ __forceinline__ Key<KW> key_bit(int p) {
+  Key<KW> k;
+#pragma unroll
+  for (int q = 0; q < KW; ++q) k.w[q] = (p >> 6) == q ? (1ull << (p & 63)) : 0ull;
+  return k;
+}
+// bits [lo, hi] (0 <= lo, hi < 64 KW; empty if lo > hi)
+template <int KW>
+__host__ __device__ __forceinline__ Key<KW> key_range(int lo, int hi) {
+  const Key<KW> a = key_below<KW>(hi + 1), b = key_below<KW>(lo);
+  Key<KW> k;
+#pragma unroll
+  for (int q = 0; q < KW; ++q) k.w[q] = a.w[q] & ~b.w[q];
+  return k;
+}
+template <int KW>
+__host__ __device__ __forceinline__ Key<KW> operator&(const Key<KW>& a, const Key<KW>& b) {
+  Key<KW> k;
+#pragma unroll
+  for (int q = 0; q < KW; ++q) k.w[q] = a.w[q] & b.w[q];
+  return k;
+}
+template <int KW>
+__host__ __device__ __forceinline__ Key<KW> operator|(const Key<KW>& a, const Key<KW>& b) {
+  Key<KW> k;
+#pragma unroll
+  for (int q = 0; q < KW; ++q) k.w[q] = a.w[q] | b.w[q];
+  return k;
+}
+template <int KW>
+__host__ __device__ __forceinline__ Key<KW> operator^(const Key<KW>& a, const Key<KW>& b) {
+  Key<KW> k;
+#pragma unroll
+  for (int q = 0; q < KW; ++q) k.w[q] = a.w[q] ^ b.w[q];
+  return k;
+}
+template <int KW>
+__host__ __device__ __forceinline__ Key<KW> operator~(const Key<KW>& a) {
+  Key<KW> k;
+#pragma unroll
+  for (int q = 0; q < KW; ++q) k.w[q] = ~a.w[q];
+  return k;
+}
+template <int KW>
+__host__ __device__ __forceinline__ bool key_any(const Key<KW>& a) {
+  uint64_t o = 0;
+#pragma unroll
+  for (int q = 0; q < KW; ++q) o |= a.w[q];
+  return o != 0;
+}
+template <int KW>
+__device__ __forceinline__ int key_pop(const Key<KW>& a) {
+  int c = 0;
+#pragma unroll
+  for (int q = 0; q < KW; ++q) c += __popcll(a.w[q]);
+  return c;
+}
+template <int KW>
+__host__ __device__ __forceinline__ bool key_test(const Key<KW>& a, int p) {
+  return (a.w[p >> 6] >> (p & 63)) & 1;
+}
+// set bit p to b (bit p clear on entry)
+template <int KW>
+__host__ __device__ __forceinline__ void key_put(Key<KW>& a, int p, bool b) {
+  a.w[p >> 6] |= (uint64_t)b << (p & 63);
+}
+// 1 + the highest set bit (0: none)
+template <int KW>
+__device__ __forceinline__ int key_high(const Key<KW>& a) {
+  int h = 0;
+#pragma unroll
+  for (int q = 0; q < KW; ++q)
+    if (a.w[q]) h = 64 * q + 64 - __clzll(a.w[q]);
+  return h;
+}
+// lowest set bit (-1: none)
+template <int KW>
+__device__ __forceinline__ int key_first(const Key<KW>& a) {
+#pragma unroll
+  for (int q = 0; q < KW; ++q)
+    if (a.w[q]) return 64 * q + __builtin_ctzll(a.w[q]);
+  return -1;
+}
+// key of vertex v of a word array (KW words per vertex)
+template <int KW>
+__device__ __forceinline__ Key<KW> key_load(const uint64_t* a, int64_t v) {
+  Key<KW> k;
+  if constexpr (KW == 2) {
+    const ulonglong2 t = reinterpret_cast<const ulonglong2*>(a)[v];
+    k.w[0] = t.x;
+    k.w[1] = t.y;
+  } else {
+#pragma unroll
+    for (int q = 0; q < KW; ++q) k.w[q] = a[KW * v + q];
+  }
+  return k;
+}
+template <int KW>
+__device__ __forceinline__ void key_store(uint64_t* a, int64_t v, const Key<KW>& k) {
+  if constexpr (KW == 2) {
+    reinterpret_cast<ulonglong2*>(a)[v] = make_ulonglong2(k.w[0], k.w[1]);
+  } else {
+#pragma unroll
+    for (int q = 0; q < KW; ++q) a[KW * v + q] = k.w[q];
+  }
+}
+// the (pos, zero) pair of vertex v from the interleaved copy
+template <int KW>
+__device__ __forceinline__ void pz_load(const uint64_t* pz, int64_t v, Key<KW>& p, Key<KW>& z) {
+  const ulonglong2* t = reinterpret_cast<const ulonglong2*>(pz) + KW * v;
+  if constexpr (KW == 1) {
+    const ulonglong2 a = t[0];
+    p.w[0] = a.x;
+    z.w[0] = a.y;
+  } else {
+    const ulonglong2 a = t[0], b = t[1];
+    p.w[0] = a.x;
+    p.w[1] = a.y;
+    z.w[0] = b.x;
+    z.w[1] = b.y;
+  }
+}
+template <int KW>
+__device__ __forceinline__ void pz_store(uint64_t* pz, int64_t v, const Key<KW>& p, const Key<KW>& z) {
+  ulonglong2* t = reinterpret_cast<ulonglong2*>(pz) + KW * v;
+  if constexpr (KW == 1) {
+    t[0] = make_ulonglong2(p.w[0], z.w[0]);
+  } else {
+    t[0] = make_ulonglong2(p.w[0], p.w[1]);
+    t[1] = make_ulonglong2(z.w[0], z.w[1]);
+  }
+}
+// an active-plane word: bit p for plane p < 63, bit 63 for every plane >= 63
+__host__ __device__ __forceinline__ uint64_t act_bit(int p) { return 1ull << (p < 63 ? p : 63); }
+__host__ __device__ __forceinline__ bool act_test(uint64_t m, int p) { return (m >> (p < 63 ? p : 63)) & 1; }
+
 }  // namespace tnp
 
 using tnp::TnpLB;
+using tnp::Key;

@@ -41,6 +41,23 @@ __device__ __forceinline__ PairTest pair_test(uint64_t below, uint32_t fu, uint6
   return t;
 }
 
+// the same test on KW-word keys (k_connect)
+template <int KW>
+__device__ __forceinline__ PairTest pair_test(const Key<KW>& below, uint32_t fu, const Key<KW>& pu,
+                                              const Key<KW>& zu, uint32_t fv, const Key<KW>& pv,
+                                              const Key<KW>& zv) {
+  PairTest t{false, false, 0};
+  if (((fu | fv) & 7u) != 7u) return t;  // not the canonical cell
+  if (tnp::key_any((pu ^ pv) & ~zu & ~zv & below)) return t;
+  const uint32_t a = fu & fv;
+  const uint32_t sp = a & (a >> 3) & 7u;  // axes where both lie on the same mark plane
+  const Key<KW> zz = zu & zv & below;
+  t.compat = true;
+  t.regions = (int64_t)1 << (__popc(sp) + tnp::key_pop(zz));
+  t.emit = sp != 0 || tnp::key_any(zz);
+  return t;
+}
+
 // where the connect phase counts its appended keys and pair statistics:
 // this workgroup's XCD shard (xs != null: large grids, k_keys_finish folds
 // the shards into ctr) or the counter block itself (small grids: a few

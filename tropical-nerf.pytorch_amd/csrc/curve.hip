@@ -106,7 +106,7 @@ __device__ __forceinline__ float slapy2(float x, float y) {
   float w = fmaxf(x, y), z = fminf(x, y);
   if (z == 0.f || w > 3.4e38f) return w;
   float r = __fdiv_rn(z, w);
-  return __fmul_rn(w, __fsqrt_rn(__fadd_rn(1.f, __fmul_rn(r, r))));
+  return __fmul_rn(w, sqrtf(__fadd_rn(1.f, __fmul_rn(r, r))));
 }
 
 __device__ void slanv2(float a, float b, float c, float d, float wr[2], float wi[2]) {
@@ -127,7 +127,7 @@ __device__ void slanv2(float a, float b, float c, float d, float wr[2], float wi
     float scale = fmaxf(fabsf(p), bcmax);
     float z = __fadd_rn(__fmul_rn(__fdiv_rn(p, scale), p), __fmul_rn(__fdiv_rn(bcmax, scale), bcmis));
     if (z >= 4.f * EPS) {
-      z = __fadd_rn(p, fsign(__fmul_rn(__fsqrt_rn(scale), __fsqrt_rn(z)), p));
+      z = __fadd_rn(p, fsign(__fmul_rn(sqrtf(scale), sqrtf(z)), p));
       a = __fadd_rn(d, z);
       d = __fsub_rn(d, __fmul_rn(__fdiv_rn(bcmax, z), bcmis));
       b = __fsub_rn(b, c);
@@ -135,7 +135,7 @@ __device__ void slanv2(float a, float b, float c, float d, float wr[2], float wi
     } else {
       float sigma = __fadd_rn(b, c);
       float tau = slapy2(sigma, temp);
-      float cs = __fsqrt_rn(__fmul_rn(0.5f, __fadd_rn(1.f, __fdiv_rn(fabsf(sigma), tau))));
+      float cs = sqrtf(__fmul_rn(0.5f, __fadd_rn(1.f, __fdiv_rn(fabsf(sigma), tau))));
       float sn = __fmul_rn(-__fdiv_rn(p, __fmul_rn(tau, cs)), fsign(1.f, sigma));
       float aa = __fadd_rn(__fmul_rn(a, cs), __fmul_rn(b, sn));
       float bb = __fadd_rn(__fmul_rn(-a, sn), __fmul_rn(b, cs));
@@ -150,7 +150,7 @@ __device__ void slanv2(float a, float b, float c, float d, float wr[2], float wi
       if (c != 0.f) {
         if (b != 0.f) {
           if ((b > 0.f) == (c > 0.f)) {
-            float sab = __fsqrt_rn(fabsf(b)), sac = __fsqrt_rn(fabsf(c));
+            float sab = sqrtf(fabsf(b)), sac = sqrtf(fabsf(c));
             p = fsign(__fmul_rn(sab, sac), c);
             a = __fadd_rn(temp, p);
             d = __fsub_rn(temp, p);
@@ -169,7 +169,7 @@ __device__ void slanv2(float a, float b, float c, float d, float wr[2], float wi
   if (c == 0.f) {
     wi[0] = wi[1] = 0.f;
   } else {
-    wi[0] = __fmul_rn(__fsqrt_rn(fabsf(b)), __fsqrt_rn(fabsf(c)));
+    wi[0] = __fmul_rn(sqrtf(fabsf(b)), sqrtf(fabsf(c)));
     wi[1] = -wi[0];
   }
 }
@@ -464,7 +464,7 @@ struct SmallEig {
           h11 = __fdiv_rn(h11, s); h21 = __fdiv_rn(h21, s); h12 = __fdiv_rn(h12, s); h22 = __fdiv_rn(h22, s);
           const float tr = __fdiv_rn(__fadd_rn(h11, h22), 2.f);
           const float det = __fsub_rn(__fmul_rn(__fsub_rn(h11, tr), __fsub_rn(h22, tr)), __fmul_rn(h12, h21));
-          const float rtdisc = __fsqrt_rn(fabsf(det));
+          const float rtdisc = sqrtf(fabsf(det));
           if (det >= 0.f) {
             rt1r = __fmul_rn(tr, s); rt2r = rt1r; rt1i = __fmul_rn(rtdisc, s); rt2i = -rt1i;
           } else {
@@ -853,7 +853,7 @@ int launch_descend(const NetDev& net, int64_t G, const int32_t* glist, const int
                    int idx, float eps, int iters, int record, float* ints, float* d0s, float* d1s,
                    unsigned long long* conv, hipStream_t s) {
   if (G <= 0) return 0;
-  if (!net_supported(net)) { tnp_set_error("unsupported net shape"); return -1; }
+  if (!net_supported_full(net)) { tnp_set_error("the curve descent: net shape not instantiated (the K > 63 shapes run the flat path only)"); return -1; }
   if (iters > 512) { tnp_set_error("descend: at most 512 iterations"); return -1; }
   // TNP_DESCEND_THREAD=1: the one-thread-per-row kernel (tests compare both)
   const char* pt = getenv("TNP_DESCEND_THREAD");

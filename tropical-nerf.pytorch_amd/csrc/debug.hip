@@ -8,7 +8,7 @@ namespace {
 __global__ void k_ops(const float* a, const float* b, const float* c, int64_t n, float* o) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  o[8 * i + 0] = __fsqrt_rn(a[i]);
+  o[8 * i + 0] = sqrtf(a[i]);
   o[8 * i + 1] = __fdiv_rn(a[i], b[i]);
   o[8 * i + 2] = __fmaf_rn(a[i], b[i], c[i]);
   o[8 * i + 3] = __fmul_rn(a[i], b[i]);

@@ -56,7 +56,7 @@ __device__ __forceinline__ float mm_col(const float* x, const float* W, int k, b
 template <int LV, int H, int NL>
 __device__ __forceinline__ void plane_pair_grad(const NetDev& net, const float* w, const float u[3],
                                                 int j0, int j1, int m0, int mh, int mo, bool one_row,
-                                                float& d0, float& d1, float gu[3]) {
+                                                int64_t row, float& d0, float& d1, float gu[3]) {
   constexpr int IN = 2 * LV;
   constexpr int NH = NL - 1;
   float f[IN], a[NH][H], h[H], o[2];
@@ -66,16 +66,17 @@ __device__ __forceinline__ void plane_pair_grad(const NetDev& net, const float* 
 #pragma unroll
   for (int l = 1; l < NH; ++l) Wl[l] = Wl[l - 1] + (l == 1 ? H * IN + H : H * H + H);
   const float* WL = Wl[NH - 1] + (NH == 1 ? H * IN + H : H * H + H);
-  linear_mode<IN, H>(Wl[0], Wl[0] + H * IN, f, a[0], m0);
+  // row: the row's index in the batch (the 32-input FOLD schedule's parity)
+  linear_mode<IN, H>(Wl[0], Wl[0] + H * IN, f, a[0], m0, row);
 #pragma unroll
   for (int j = 0; j < H; ++j) h[j] = fmaxf(a[0][j], 0.f);
 #pragma unroll
   for (int l = 1; l < NH; ++l) {
-    linear_mode<H, H>(Wl[l], Wl[l] + H * H, h, a[l], mh);
+    linear_mode<H, H>(Wl[l], Wl[l] + H * H, h, a[l], mh, row);
 #pragma unroll
     for (int j = 0; j < H; ++j) h[j] = fmaxf(a[l][j], 0.f);
   }
-  linear_mode<H, 2>(WL, WL + 2 * H, h, o, mo);
+  linear_mode<H, 2>(WL, WL + 2 * H, h, o, mo, row);
   float last = __fsub_rn(o[1], o[0]);
   d0 = last;
   d1 = last;
@@ -207,14 +208,14 @@ k_descend(NetDev net, int64_t G, const int32_t* __restrict__ glist,
 #pragma unroll
     for (int d = 0; d < 3; ++d)
       u[d] = __fmul_rn(__fadd_rn(__fadd_rn(e0[d], __fmul_rn(x[d], de[d])), 1.0f), 0.5f);  // x/2 == x*0.5
-    plane_pair_grad<LV, H, NL>(net, w, u, j0, idx, m0, mh, mo, Gs == 1, d0, d1, gu);
+    plane_pair_grad<LV, H, NL>(net, w, u, j0, idx, m0, mh, mo, Gs == 1, g, d0, d1, gu);
     float gx[3], nn = 0.f;
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
       gx[d] = __fmul_rn(__fmul_rn(gu[d], 0.5f), de[d]);
       nn = __fmaf_rn(gx[d], gx[d], nn);
     }
-    float den = fmaxf(__fsqrt_rn(nn), 1e-12f);
+    float den = fmaxf(sqrtf(nn), 1e-12f);
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
       float v = __fsub_rn(x[d], __fmul_rn(1e-2f, __fdiv_rn(gx[d], den)));
@@ -337,16 +338,16 @@ k_descend_wave(NetDev net, int64_t G, const int32_t* __restrict__ glist,
     // forward, neuron nj per lane; a[l]: this lane's neuron of hidden layer l
     float a[NH];
     float hh[H];
-    a[0] = neuron_mode<IN, H>(Wl[0], Wl[0] + H * IN, f, nj, m0);
+    a[0] = neuron_mode<IN, H>(Wl[0], Wl[0] + H * IN, f, nj, m0, g);
 #pragma unroll
     for (int l = 1; l < NH; ++l) {
 #pragma unroll
       for (int j = 0; j < H; ++j) hh[j] = fmaxf(lane_f(a[l - 1], j), 0.f);
-      a[l] = neuron_mode<H, H>(Wl[l], Wl[l] + H * H, hh, nj, mh);
+      a[l] = neuron_mode<H, H>(Wl[l], Wl[l] + H * H, hh, nj, mh, g);
     }
 #pragma unroll
     for (int j = 0; j < H; ++j) hh[j] = fmaxf(lane_f(a[NH - 1], j), 0.f);
-    const float o = neuron_mode<H, 2>(WL, WL + 2 * H, hh, lane & 1, mo);
+    const float o = neuron_mode<H, 2>(WL, WL + 2 * H, hh, lane & 1, mo, g);
     const float last = __fsub_rn(lane_f(o, 1), lane_f(o, 0));
     d0 = last;
     d1 = last;
@@ -417,7 +418,7 @@ k_descend_wave(NetDev net, int64_t G, const int32_t* __restrict__ glist,
       gx[d] = __fmul_rn(__fmul_rn(acc, 0.5f), de[d]);
       nn = __fmaf_rn(gx[d], gx[d], nn);
     }
-    const float den = fmaxf(__fsqrt_rn(nn), 1e-12f);
+    const float den = fmaxf(sqrtf(nn), 1e-12f);
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
       const float vv = __fsub_rn(x[d], __fmul_rn(1e-2f, __fdiv_rn(gx[d], den)));

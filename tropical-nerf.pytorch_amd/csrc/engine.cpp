@@ -141,6 +141,7 @@ struct tnp_engine {
   std::vector<int64_t> kt_n;
   NetDev net{};
   int K = 0;
+  int kw = 1;  // sign-key words per vertex key (net_kw: 2 when K > 63)
   bool has_net = false;
   VSet cur, alt;
   Buf edges, edges_alt;
@@ -338,18 +339,19 @@ static int vset_ensure(tnp_engine* e, VSet& v, int64_t rows, int64_t keep_rows, 
   n.K = e->K;
   if (buf_ensure(n.xyz, nc * 3 * sizeof(float), s)) return -1;
   if (buf_ensure(n.pre, (size_t)nc * e->K * sizeof(float), s)) return -1;
-  if (buf_ensure(n.pos, nc * sizeof(uint64_t), s)) return -1;
-  if (buf_ensure(n.zero, nc * sizeof(uint64_t), s)) return -1;
+  const int64_t kb = 8 * e->kw;  // bytes per key
+  if (buf_ensure(n.pos, nc * kb, s)) return -1;
+  if (buf_ensure(n.zero, nc * kb, s)) return -1;
   if (buf_ensure(n.grid, nc * sizeof(uint64_t), s)) return -1;
-  if (buf_ensure(n.pz, nc * 2 * sizeof(uint64_t), s)) return -1;
+  if (buf_ensure(n.pz, nc * 2 * kb, s)) return -1;
   if (keep_rows > 0 && v.cap > 0) {
     TNP_CHECK(hipMemcpyAsync(n.xyz.p, v.xyz.p, keep_rows * 3 * sizeof(float), hipMemcpyDeviceToDevice, s));
     TNP_CHECK(hipMemcpy2DAsync(n.pre.p, nc * sizeof(float), v.pre.p, v.cap * sizeof(float),
                                keep_rows * sizeof(float), e->K, hipMemcpyDeviceToDevice, s));
-    TNP_CHECK(hipMemcpyAsync(n.pos.p, v.pos.p, keep_rows * 8, hipMemcpyDeviceToDevice, s));
-    TNP_CHECK(hipMemcpyAsync(n.zero.p, v.zero.p, keep_rows * 8, hipMemcpyDeviceToDevice, s));
+    TNP_CHECK(hipMemcpyAsync(n.pos.p, v.pos.p, keep_rows * kb, hipMemcpyDeviceToDevice, s));
+    TNP_CHECK(hipMemcpyAsync(n.zero.p, v.zero.p, keep_rows * kb, hipMemcpyDeviceToDevice, s));
     TNP_CHECK(hipMemcpyAsync(n.grid.p, v.grid.p, keep_rows * 8, hipMemcpyDeviceToDevice, s));
-    TNP_CHECK(hipMemcpyAsync(n.pz.p, v.pz.p, keep_rows * 16, hipMemcpyDeviceToDevice, s));
+    TNP_CHECK(hipMemcpyAsync(n.pz.p, v.pz.p, keep_rows * 2 * kb, hipMemcpyDeviceToDevice, s));
   }
   buf_free(v.xyz, s);
   buf_free(v.pre, s);
@@ -387,6 +389,7 @@ static int reset_live(tnp_engine* e, hipStream_t s, bool edges_changed = true) {
 // the cell grouping runs on spatial buckets (bucket.hip) unless the grid is
 // too fine for them or TNP_RADIX_CELLS=1; *bg: their geometry
 static bool uses_buckets(const tnp_engine* e, BucketGeom* bg) {
+  if (e->kw != 1) return false;  // two-word keys: the radix path's 48-B records
   const int gx0 = e->xs1 >= e->xs0 ? e->xs0 : 0, gx1 = e->xs1 >= e->xs0 ? e->xs1 : e->net.n_marks - 1;
   return !e->radix_cells && bucket_geometry(e->net.n_marks, gx0, gx1, bg) == 0;
 }
@@ -425,10 +428,16 @@ static int compute_masks(tnp_engine* e, int from, int64_t* ctr, hipStream_t s) {
 // [mask_from, idx) still splits some edge (a step the caller skipped) --
 // then they are recomputed from idx.  Returns 1 if recomputed (the OR of
 // the first planes is then in ctr[CTR_ACTIVE], ctr zeroed by the caller).
+// the active-plane word of the planes [lo, hi) (planes >= 63 share bit 63)
+static uint64_t act_range(int lo, int hi) {
+  uint64_t m = 0;
+  for (int p = lo; p < hi && p < 63; ++p) m |= 1ull << p;
+  if (hi > 63 && hi > lo) m |= 1ull << 63;
+  return m;
+}
+
 static int ensure_masks(tnp_engine* e, int idx, hipStream_t s) {
-  const uint64_t below = idx >= 64 ? ~0ull : ((1ull << idx) - 1ull);
-  const uint64_t from = e->mask_from >= 64 ? ~0ull : ((1ull << e->mask_from) - 1ull);
-  if (e->masks_valid && idx >= e->mask_from && (e->act_bits & below & ~from) == 0) return 0;
+  if (e->masks_valid && idx >= e->mask_from && (e->act_bits & act_range(e->mask_from, idx)) == 0) return 0;
   return compute_masks(e, idx, P<int64_t>(e->ctr), s) ? -1 : 1;
 }
 
@@ -588,7 +597,7 @@ static int check_net(const tnp_net* n) {
                   n->num_layers, n->num_hidden);
     return -1;
   }
-  if (net_K(d) > 63) { tnp_set_error("more than 63 planes (edge masks reserve all-ones)"); return -1; }
+  if (net_K(d) > 127) { tnp_set_error("more than 127 planes (two-word sign keys)"); return -1; }
   return 0;
 }
 
@@ -629,6 +638,7 @@ extern "C" int tnp_engine_set_net(tnp_engine* e, const tnp_net* n) {
     e->pend_idx = -1;
   }
   e->K = K;
+  e->kw = net_kw(e->net);
   e->has_net = true;
   return 0;
 }
@@ -1045,6 +1055,11 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
     return -1;
   }
   if (require_valid(e, "split")) return -1;
+  if (e->kw != 1 && (e->curve || e->shards > 1)) {
+    tnp_set_error("a net of %d planes (two-word sign keys) runs the flat single-device path only "
+                  "(no force=False curve branch, no sharding)", e->K);
+    return -1;
+  }
   e->valid = false;  // until this split has completed
   const float eps = e->net.eps_s;  // subpoly_'s eps: hits, split point, failover
   const float* col = P<float>(e->cur.pre) + (int64_t)idx * e->cur.cap;
@@ -1128,7 +1143,7 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
     if (seg_new()) return ccoll ? coll_fail(e, 1, TNP_COLL_SUM) : -1;
     if (e->curve && curve_correct(e, idx, S, s)) return -1;
     auto seg_rest = [&]() -> int {
-    if (buf_ensure(e->shared, S * sizeof(uint64_t), s)) return -1;
+    if (buf_ensure(e->shared, S * sizeof(uint64_t) * e->kw, s)) return -1;
     e->pend_fused = !e->curve;
     if (e->pend_fused) {
       // flat: split points + forward + failover test + keys in one pass,
@@ -1231,7 +1246,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   } else if (e->pend_fused) {
     TIMED("override_new", 8.0 * S,
           launch_override_new(S, override_, P<uint64_t>(e->shared), P<float>(c.pre), c.cap,
-                              e->valid_from, V, pos, zero, ctr, P<uint64_t>(c.pz), s));
+                              e->valid_from, V, pos, zero, ctr, P<uint64_t>(c.pz), e->kw, s));
   } else {
     TIMED("finalize_new", (8.0 + 4.0 * K + 4.0 * (K - e->valid_from) + 16.0) * S,
           launch_finalize_new(S, K, override_, P<uint64_t>(e->shared), P<float>(e->stage), eps,
@@ -1265,7 +1280,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   // buffers take the bound 8 M, so nothing waits for the entry count T
   const int64_t TB = std::max<int64_t>(8 * M, 1);
   const int64_t RC = TB / 2 + 1;  // a pair cell holds >= 2 entries
-  if (buf_ensure(e->ents, TB * sizeof(CellEnt), s)) return -1;
+  if (buf_ensure(e->ents, TB * cell_ent_bytes(e->kw), s)) return -1;
   if (buf_ensure(e->pcell, RC * sizeof(int32_t), s)) return -1;
   if (buf_ensure(e->pent, RC * sizeof(int32_t), s)) return -1;
   if (buf_ensure(e->pcn, RC * sizeof(int32_t), s)) return -1;
@@ -1317,7 +1332,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     if (buf_ensure(e->part, (int64_t)(tnp_grid(M) + 1) * sizeof(int64_t), s)) return -1;
     TIMED("span_count", 28.0 * M,
           launch_span_count(P<int32_t>(e->members), S, M, grid, zero, idx, P<int32_t>(e->spcnt),
-                            P<int64_t>(e->part), ctr, s));
+                            P<int64_t>(e->part), ctr, e->kw, s));
     if (scan_counts(e, P<int32_t>(e->spcnt), P<int64_t>(e->spoff), M, CTR_T, s)) return -1;
     if (buf_ensure(e->ekey_a, TB * sizeof(uint32_t), s)) return -1;
     if (buf_ensure(e->ent_v, TB * sizeof(int32_t), s)) return -1;
@@ -1365,7 +1380,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
       }
     }
     TIMED("entry_keys", 52.0 * T,
-          launch_entry_keys(sval, skey, NC, T, grid, P<uint64_t>(c.pz), P<CellEnt>(e->ents), s));
+          launch_entry_keys(sval, skey, NC, T, grid, P<uint64_t>(c.pz), e->ents.p, e->kw, s));
   }
   // 4. connecting edges: test every in-cell member pair once, append the
   //    emitted ones, radix-sort them (lexicographic c_new, subpoly.py:243-244).
@@ -1430,7 +1445,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     TIMED("connect", 0.0,
           launch_connect(P<int64_t>(e->ptoff), P<int32_t>(e->pcell), P<int32_t>(e->pcn),
                          P<int32_t>(e->pent), NC, e->max_pair_tests, P<int32_t>(e->bcell),
-                         P<CellEnt>(e->ents), idx, nb, cfmask, P<uint64_t>(e->ckeys_a), cap, xs, ctr, s,
+                         e->ents.p, idx, nb, prune ? K - 1 : -1, e->kw, P<uint64_t>(e->ckeys_a), cap, xs, ctr, s,
                          bstat, NG));
     if (shard) {
       if (launch_keys_finish(xs, cap, ctr, s)) return -1;
@@ -1659,7 +1674,7 @@ extern "C" int tnp_engine_run_steps(tnp_engine* e, void* stream, tnp_step_stats*
   if (tnp_engine_active_planes(e, 0, &mask, stream)) return -1;
   const int K = e->K;
   for (int idx = 0; idx < K; ++idx) {
-    if (!((mask >> idx) & 1ull)) continue;
+    if (!tnp::act_test(mask, idx)) continue;
     int64_t S = 0;
     int32_t fail = 0;
     if (tnp_engine_split(e, idx, stream, &S, &fail)) return -1;
@@ -1669,7 +1684,9 @@ extern "C" int tnp_engine_run_steps(tnp_engine* e, void* stream, tnp_step_stats*
     if (tnp_engine_finish(e, idx, prune, fail, stream, &st)) return -1;
     if (*n_steps < max_stats) stats[*n_steps] = st;
     ++*n_steps;
-    if (prune) mask = (mask & ((2ull << idx) - 1ull)) | st.next_active;
+    // (planes >= 63 share bit 63: after such a step only the next-active word counts)
+    if (prune) mask = idx >= 62 ? ((mask & ((1ull << 63) - 1ull)) | st.next_active)
+                                : ((mask & ((2ull << idx) - 1ull)) | st.next_active);
   }
   return 0;
 }
@@ -2013,7 +2030,6 @@ extern "C" int tnp_engine_faces(tnp_engine* e, void* stream, int64_t* n_tri, int
     tnp_set_error("faces: region keys hold n_marks + 2 < 1024 cells per axis");
     return -1;
   }
-  const uint64_t pmask = (K - 1 >= 64) ? ~0ull : ((1ull << (K - 1)) - 1ull);
   int64_t* ctr = P<int64_t>(e->ctr);
   const uint64_t* pos = P<uint64_t>(e->cur.pos);
   const uint64_t* zero = P<uint64_t>(e->cur.zero);
@@ -2024,7 +2040,7 @@ extern "C" int tnp_engine_faces(tnp_engine* e, void* stream, int64_t* n_tri, int
     // outputs, eps), subpoly.py:606): keys of every plane from the cache
     if (e->valid_from != 0) { tnp_set_error("split-eps faces: cached planes were dropped"); return -1; }
     for (int k = 0; k < 3; ++k)
-      if (buf_ensure(e->kse[k], V * sizeof(uint64_t), s)) return -1;
+      if (buf_ensure(e->kse[k], V * sizeof(uint64_t) * (k < 2 ? e->kw : 1), s)) return -1;
     NetDev ns = e->net;
     ns.eps = ns.eps_s;
     if (launch_keys(ns, xyz, P<float>(e->cur.pre), e->cur.cap, V, K, P<uint64_t>(e->kse[0]),
@@ -2036,26 +2052,33 @@ extern "C" int tnp_engine_faces(tnp_engine* e, void* stream, int64_t* n_tri, int
   }
   TNP_CHECK(hipMemsetAsync(ctr, 0, CTR_CLEAR_BYTES, s));
   // F1: augmented-row count and region hash table
-  if (launch_face_count(V, grid, pos, zero, pmask, ctr + CTR_AUX - 1, s)) return -1;
+  if (launch_face_count(V, grid, pos, zero, K, ctr + CTR_AUX - 1, s)) return -1;
   if (read_ctr(e, s)) return -1;
   const int64_t A = e->h_ctr[CTR_AUX - 1];
   if (e->h_ctr[CTR_AUX] > 30) { tnp_set_error("faces: a vertex lies on %lld planes", (long long)e->h_ctr[CTR_AUX]); return -1; }
   int64_t cap = 1024;
   while (cap < 2 * A) cap <<= 1;
-  // region table: cap sign words + cap cell words (faces.hip probe_insert)
-  if (buf_ensure(fs[FS_TABLE], cap * 16, s) || buf_ensure(fs[FS_CNT], cap * 4, s) ||
+  // region table: cap sign words + cap cell words (faces.hip probe_insert);
+  // two-word keys: cap cell words + 2 cap sign words + cap ready words
+  if (buf_ensure(fs[FS_TABLE], cap * 16 * e->kw, s) || buf_ensure(fs[FS_CNT], cap * 4, s) ||
       buf_ensure(fs[FS_KC], cap * 4, s) || buf_ensure(fs[FS_KF], cap * 4, s) ||
       buf_ensure(fs[FS_MEMOFF], cap * 8, s) || buf_ensure(fs[FS_RID], cap * 8, s) ||
       buf_ensure(fs[FS_CUR], cap * 4, s))
     return -1;
-  {  // EMPTY signs, NO_CELL, counts, cursors: one dispatch
+  if (e->kw == 1) {  // EMPTY signs, NO_CELL, counts, cursors: one dispatch
     const FillOp f[4] = {{fs[FS_TABLE].p, (uint64_t)cap * 8, 0xFF},
                          {static_cast<char*>(fs[FS_TABLE].p) + cap * 8, (uint64_t)cap * 8, 0},
                          {fs[FS_CNT].p, (uint64_t)cap * 4, 0},
                          {fs[FS_CUR].p, (uint64_t)cap * 4, 0}};
     if (launch_fill(f, 4, s)) return -1;
+  } else {  // NO_CELL claim words and not-ready words (the sign words are written before use)
+    const FillOp f[4] = {{fs[FS_TABLE].p, (uint64_t)cap * 8, 0},
+                         {static_cast<char*>(fs[FS_TABLE].p) + cap * 24, (uint64_t)cap * 8, 0},
+                         {fs[FS_CNT].p, (uint64_t)cap * 4, 0},
+                         {fs[FS_CUR].p, (uint64_t)cap * 4, 0}};
+    if (launch_fill(f, 4, s)) return -1;
   }
-  if (launch_face_insert(V, grid, pos, zero, pmask, P<uint64_t>(fs[FS_TABLE]), (uint64_t)cap - 1,
+  if (launch_face_insert(V, grid, pos, zero, K, P<uint64_t>(fs[FS_TABLE]), (uint64_t)cap - 1,
                          P<int32_t>(fs[FS_CNT]), s))
     return -1;
   if (launch_keep_counts(P<int32_t>(fs[FS_CNT]), cap, P<int32_t>(fs[FS_KC]), P<int32_t>(fs[FS_KF]), s)) return -1;
@@ -2079,7 +2102,7 @@ extern "C" int tnp_engine_faces(tnp_engine* e, void* stream, int64_t* n_tri, int
   if (buf_ensure(fs[FS_MEM], Mtot * 8, s) || buf_ensure(fs[FS_ROFF], R * 8, s) ||
       buf_ensure(fs[FS_RCNT], R * 4, s))
     return -1;
-  if (launch_face_scatter(V, grid, pos, zero, pmask, P<uint64_t>(fs[FS_TABLE]), (uint64_t)cap - 1,
+  if (launch_face_scatter(V, grid, pos, zero, K, P<uint64_t>(fs[FS_TABLE]), (uint64_t)cap - 1,
                           P<int32_t>(fs[FS_CNT]), P<int64_t>(fs[FS_MEMOFF]), P<int32_t>(fs[FS_CUR]),
                           P<uint64_t>(fs[FS_MEM]), s))
     return -1;

@@ -3,13 +3,15 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// K: the net's planes (the regions' plane columns are planes < K - 1); K > 63:
+// two-word keys, a table of 4 cap words (else 2 cap)
 int launch_face_count(int64_t V, const uint64_t* grid, const uint64_t* pos, const uint64_t* zero,
-                      uint64_t pmask, int64_t* ctr2, hipStream_t s);
+                      int K, int64_t* ctr2, hipStream_t s);
 int launch_face_insert(int64_t V, const uint64_t* grid, const uint64_t* pos, const uint64_t* zero,
-                       uint64_t pmask, uint64_t* table, uint64_t tmask, int32_t* cnt, hipStream_t s);
+                       int K, uint64_t* table, uint64_t tmask, int32_t* cnt, hipStream_t s);
 int launch_keep_counts(const int32_t* cnt, int64_t n, int32_t* kc, int32_t* kf, hipStream_t s);
 int launch_face_scatter(int64_t V, const uint64_t* grid, const uint64_t* pos, const uint64_t* zero,
-                        uint64_t pmask, const uint64_t* table, uint64_t tmask, const int32_t* cnt,
+                        int K, const uint64_t* table, uint64_t tmask, const int32_t* cnt,
                         const int64_t* memoff, int32_t* cur, uint64_t* mem, hipStream_t s);
 int launch_region_finalize(int64_t n, const int32_t* kf, const int64_t* rid, const int32_t* cnt,
                            const int64_t* memoff, uint64_t* mem, int64_t* roff, int32_t* rcnt,

@@ -40,17 +40,19 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
   return x;
 }
 
+template <int KW>
 struct VKey {
   int k;        // zeros among the region columns
   int zc[3];    // grid zero dims
   int nzg;      // number of grid zeros
-  uint64_t pz;  // plane zeros (planes < nplanes)
-  uint64_t ps;  // plane positive signs
+  Key<KW> pz;   // plane zeros (planes < nplanes)
+  Key<KW> ps;   // plane positive signs
   int off[3];
 };
 
-__device__ __forceinline__ VKey vkey(uint64_t g, uint64_t pos, uint64_t zero, uint64_t pmask) {
-  VKey r;
+template <int KW>
+__device__ __forceinline__ VKey<KW> vkey(uint64_t g, const Key<KW>& pos, const Key<KW>& zero, const Key<KW>& pmask) {
+  VKey<KW> r;
   r.nzg = 0;
 #pragma unroll
   for (int d = 0; d < 3; ++d) {
@@ -59,44 +61,55 @@ __device__ __forceinline__ VKey vkey(uint64_t g, uint64_t pos, uint64_t zero, ui
   }
   r.pz = zero & pmask;
   r.ps = pos & pmask;
-  r.k = r.nzg + __popcll(r.pz);
+  r.k = r.nzg + tnp::key_pop(r.pz);
   return r;
+}
+template <int KW>
+__device__ __forceinline__ VKey<KW> vkey_of(int64_t v, const uint64_t* grid, const uint64_t* pos,
+                                            const uint64_t* zero, const Key<KW>& pmask) {
+  return vkey<KW>(grid[v], tnp::key_load<KW>(pos, v), tnp::key_load<KW>(zero, v), pmask);
 }
 
 // a region key: cell word (3 x 10-bit cell coordinates + 2, never 0) and the
-// plane-sign word (bit j: plane j positive; planes < K - 1 <= 62, so never
-// all ones)
+// plane-sign words (bit j: plane j positive).  One-word nets: planes < K - 1
+// <= 62, so the sign word is never all ones (the table's EMPTY claim word)
+template <int KW>
 struct RKey {
-  uint64_t cell, signs;
+  uint64_t cell;
+  Key<KW> signs;
 };
 constexpr uint64_t NO_CELL = 0ull;
 
 // augmented key of pattern p (torch.cartesian_prod order: the first zero
 // column is the most significant pattern bit; 0 -> -1, 1 -> +1)
-__device__ __forceinline__ RKey aug_key(const VKey& v, uint32_t p) {
+template <int KW>
+__device__ __forceinline__ RKey<KW> aug_key(const VKey<KW>& v, uint32_t p) {
   int cell[3] = {v.off[0], v.off[1], v.off[2]};
   int j = 0;
   for (int i = 0; i < v.nzg; ++i, ++j) {
     int b = (p >> (v.k - 1 - j)) & 1;
     cell[v.zc[i]] = b ? v.off[v.zc[i]] : v.off[v.zc[i]] - 1;
   }
-  uint64_t signs = v.ps;
-  for (uint64_t t = v.pz; t; t &= t - 1, ++j) {
-    int pl = __builtin_ctzll(t);
-    int b = (p >> (v.k - 1 - j)) & 1;
-    if (b) signs |= 1ull << pl;
-  }
-  return RKey{((uint64_t)(cell[0] + 2) << 20) | ((uint64_t)(cell[1] + 2) << 10) | (uint64_t)(cell[2] + 2),
-              signs};
+  Key<KW> signs = v.ps;
+#pragma unroll
+  for (int q = 0; q < KW; ++q)
+    for (uint64_t t = v.pz.w[q]; t; t &= t - 1, ++j) {
+      int pl = __builtin_ctzll(t);
+      int b = (p >> (v.k - 1 - j)) & 1;
+      if (b) signs.w[q] |= 1ull << pl;
+    }
+  return RKey<KW>{((uint64_t)(cell[0] + 2) << 20) | ((uint64_t)(cell[1] + 2) << 10) | (uint64_t)(cell[2] + 2),
+                  signs};
 }
 
+template <int KW>
 __global__ void k_face_count(int64_t V, const uint64_t* __restrict__ grid, const uint64_t* __restrict__ pos,
-                             const uint64_t* __restrict__ zero, uint64_t pmask, int64_t* __restrict__ ctr) {
+                             const uint64_t* __restrict__ zero, Key<KW> pmask, int64_t* __restrict__ ctr) {
   int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int64_t a = 0;
   int kmax = 0;
   if (v < V) {
-    VKey k = vkey(grid[v], pos[v], zero[v], pmask);
+    VKey<KW> k = vkey_of<KW>(v, grid, pos, zero, pmask);
     a = 1ll << k.k;
     kmax = k.k;
   }
@@ -109,27 +122,34 @@ __global__ void k_face_count(int64_t V, const uint64_t* __restrict__ grid, const
   }
 }
 
-// table: [cap] sign words (EMPTY: free) then [cap] cell words (NO_CELL: not
-// yet published).  A slot is claimed by CAS on its sign word and the
+// One-word table: [cap] sign words (EMPTY: free) then [cap] cell words
+// (NO_CELL: not yet published).  A slot is claimed by CAS on its sign word and the
 // claiming lane publishes the cell word in the same loop round; a lane that
 // found the same sign word reads the cell word once per round (no inner
 // wait: every lane advances one step per round, so a lane never waits on a
 // store its own wave has not yet issued).
-__device__ __forceinline__ uint64_t rkey_hash(const RKey& k) { return mix64(k.signs ^ mix64(k.cell)); }
+// Two-word table (K > 63: a sign word may be all ones): [cap] cell words
+// (NO_CELL: free, claimed by CAS), [cap] low and [cap] high sign words,
+// [cap] ready words (release-stored by the claimer behind its sign words),
+// the same one-step-per-round loop.
+__device__ __forceinline__ uint64_t rkey_hash(const RKey<1>& k) { return mix64(k.signs.w[0] ^ mix64(k.cell)); }
+__device__ __forceinline__ uint64_t rkey_hash(const RKey<2>& k) {
+  return mix64(k.signs.w[1] ^ mix64(k.signs.w[0] ^ mix64(k.cell)));
+}
 
-__device__ __forceinline__ uint64_t probe_insert(uint64_t* table, uint64_t mask, RKey key) {
+__device__ __forceinline__ uint64_t probe_insert(uint64_t* table, uint64_t mask, const RKey<1>& key) {
   uint64_t* cells = table + mask + 1;
   uint64_t h = rkey_hash(key) & mask;
   bool polling = false;  // slot h holds our signs; its cell word was not published yet
   while (true) {
     if (!polling) {
       const uint64_t prev = atomicCAS((unsigned long long*)&table[h], (unsigned long long)EMPTY,
-                                      (unsigned long long)key.signs);
+                                      (unsigned long long)key.signs.w[0]);
       if (prev == EMPTY) {
         tnp::st_agent(cells + h, key.cell);
         return h;
       }
-      if (prev != key.signs) {
+      if (prev != key.signs.w[0]) {
         h = (h + 1) & mask;
         continue;
       }
@@ -142,21 +162,59 @@ __device__ __forceinline__ uint64_t probe_insert(uint64_t* table, uint64_t mask,
   }
 }
 
-__device__ __forceinline__ uint64_t probe_find(const uint64_t* table, uint64_t mask, RKey key) {
+__device__ __forceinline__ uint64_t probe_insert(uint64_t* table, uint64_t mask, const RKey<2>& key) {
+  const uint64_t cap = mask + 1;
+  uint64_t* s0 = table + cap;
+  uint64_t* s1 = table + 2 * cap;
+  uint64_t* ready = table + 3 * cap;
+  uint64_t h = rkey_hash(key) & mask;
+  bool polling = false;  // slot h holds our cell; its sign words were not published yet
+  while (true) {
+    if (!polling) {
+      const uint64_t prev = atomicCAS((unsigned long long*)&table[h], (unsigned long long)NO_CELL,
+                                      (unsigned long long)key.cell);
+      if (prev == NO_CELL) {
+        tnp::st_agent(s0 + h, key.signs.w[0]);
+        tnp::st_agent(s1 + h, key.signs.w[1]);
+        __hip_atomic_store(ready + h, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        return h;
+      }
+      if (prev != key.cell) {
+        h = (h + 1) & mask;
+        continue;
+      }
+    }
+    const uint64_t r = __hip_atomic_load(ready + h, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    polling = r == 0;
+    if (polling) continue;
+    if (tnp::ld_agent(s0 + h) == key.signs.w[0] && tnp::ld_agent(s1 + h) == key.signs.w[1]) return h;
+    h = (h + 1) & mask;
+  }
+}
+
+__device__ __forceinline__ uint64_t probe_find(const uint64_t* table, uint64_t mask, const RKey<1>& key) {
   const uint64_t* cells = table + mask + 1;
   uint64_t h = rkey_hash(key) & mask;
-  while (table[h] != key.signs || cells[h] != key.cell) h = (h + 1) & mask;
+  while (table[h] != key.signs.w[0] || cells[h] != key.cell) h = (h + 1) & mask;
+  return h;
+}
+__device__ __forceinline__ uint64_t probe_find(const uint64_t* table, uint64_t mask, const RKey<2>& key) {
+  const uint64_t cap = mask + 1;
+  uint64_t h = rkey_hash(key) & mask;
+  while (table[h] != key.cell || table[cap + h] != key.signs.w[0] || table[2 * cap + h] != key.signs.w[1])
+    h = (h + 1) & mask;
   return h;
 }
 
+template <int KW>
 __global__ void k_face_insert(int64_t V, const uint64_t* __restrict__ grid, const uint64_t* __restrict__ pos,
-                              const uint64_t* __restrict__ zero, uint64_t pmask, uint64_t* __restrict__ table,
+                              const uint64_t* __restrict__ zero, Key<KW> pmask, uint64_t* __restrict__ table,
                               uint64_t tmask, int32_t* __restrict__ cnt) {
   int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= V) return;
-  VKey k = vkey(grid[v], pos[v], zero[v], pmask);
+  VKey<KW> k = vkey_of<KW>(v, grid, pos, zero, pmask);
   for (uint32_t p = 0; p < (1u << k.k); ++p) {
-    uint64_t s = probe_insert(table, tmask, aug_key(k, p));
+    uint64_t s = probe_insert(table, tmask, aug_key<KW>(k, p));
     atomicAdd(&cnt[s], 1);
   }
 }
@@ -170,16 +228,17 @@ __global__ void k_keep_counts(const int32_t* __restrict__ cnt, int64_t n, int32_
   kf[i] = c >= 3 ? 1 : 0;
 }
 
+template <int KW>
 __global__ void k_face_scatter(int64_t V, const uint64_t* __restrict__ grid, const uint64_t* __restrict__ pos,
-                               const uint64_t* __restrict__ zero, uint64_t pmask,
+                               const uint64_t* __restrict__ zero, Key<KW> pmask,
                                const uint64_t* __restrict__ table, uint64_t tmask,
                                const int32_t* __restrict__ cnt, const int64_t* __restrict__ memoff,
                                int32_t* __restrict__ cur, uint64_t* __restrict__ mem) {
   int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= V) return;
-  VKey k = vkey(grid[v], pos[v], zero[v], pmask);
+  VKey<KW> k = vkey_of<KW>(v, grid, pos, zero, pmask);
   for (uint32_t p = 0; p < (1u << k.k); ++p) {
-    uint64_t s = probe_find(table, tmask, aug_key(k, p));
+    uint64_t s = probe_find(table, tmask, aug_key<KW>(k, p));
     if (cnt[s] < 3) continue;
     int64_t at = memoff[s] + atomicAdd(&cur[s], 1);
     mem[at] = ((uint64_t)(uint32_t)k.k << 32) | (uint64_t)(uint32_t)v;
@@ -691,17 +750,26 @@ k_fan_emit(int64_t F, const int32_t* __restrict__ frow, const int32_t* __restric
 
 // ----------------------------------------------------------------------------
 int launch_face_count(int64_t V, const uint64_t* grid, const uint64_t* pos, const uint64_t* zero,
-                      uint64_t pmask, int64_t* ctr2, hipStream_t s) {
+                      int K, int64_t* ctr2, hipStream_t s) {
   if (V <= 0) return 0;
-  hipLaunchKernelGGL(k_face_count, dim3(tnp_grid(V)), dim3(TNP_BLOCK), 0, s, V, grid, pos, zero, pmask, ctr2);
+  if (K > 63)
+    hipLaunchKernelGGL(k_face_count<2>, dim3(tnp_grid(V)), dim3(TNP_BLOCK), 0, s, V, grid, pos, zero,
+                       tnp::key_below<2>(K - 1), ctr2);
+  else
+    hipLaunchKernelGGL(k_face_count<1>, dim3(tnp_grid(V)), dim3(TNP_BLOCK), 0, s, V, grid, pos, zero,
+                       tnp::key_below<1>(K - 1), ctr2);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
 int launch_face_insert(int64_t V, const uint64_t* grid, const uint64_t* pos, const uint64_t* zero,
-                       uint64_t pmask, uint64_t* table, uint64_t tmask, int32_t* cnt, hipStream_t s) {
+                       int K, uint64_t* table, uint64_t tmask, int32_t* cnt, hipStream_t s) {
   if (V <= 0) return 0;
-  hipLaunchKernelGGL(k_face_insert, dim3(tnp_grid(V)), dim3(TNP_BLOCK), 0, s, V, grid, pos, zero, pmask,
-                     table, tmask, cnt);
+  if (K > 63)
+    hipLaunchKernelGGL(k_face_insert<2>, dim3(tnp_grid(V)), dim3(TNP_BLOCK), 0, s, V, grid, pos, zero,
+                       tnp::key_below<2>(K - 1), table, tmask, cnt);
+  else
+    hipLaunchKernelGGL(k_face_insert<1>, dim3(tnp_grid(V)), dim3(TNP_BLOCK), 0, s, V, grid, pos, zero,
+                       tnp::key_below<1>(K - 1), table, tmask, cnt);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
@@ -711,11 +779,15 @@ int launch_keep_counts(const int32_t* cnt, int64_t n, int32_t* kc, int32_t* kf, 
   return 0;
 }
 int launch_face_scatter(int64_t V, const uint64_t* grid, const uint64_t* pos, const uint64_t* zero,
-                        uint64_t pmask, const uint64_t* table, uint64_t tmask, const int32_t* cnt,
+                        int K, const uint64_t* table, uint64_t tmask, const int32_t* cnt,
                         const int64_t* memoff, int32_t* cur, uint64_t* mem, hipStream_t s) {
   if (V <= 0) return 0;
-  hipLaunchKernelGGL(k_face_scatter, dim3(tnp_grid(V)), dim3(TNP_BLOCK), 0, s, V, grid, pos, zero, pmask,
-                     table, tmask, cnt, memoff, cur, mem);
+  if (K > 63)
+    hipLaunchKernelGGL(k_face_scatter<2>, dim3(tnp_grid(V)), dim3(TNP_BLOCK), 0, s, V, grid, pos, zero,
+                       tnp::key_below<2>(K - 1), table, tmask, cnt, memoff, cur, mem);
+  else
+    hipLaunchKernelGGL(k_face_scatter<1>, dim3(tnp_grid(V)), dim3(TNP_BLOCK), 0, s, V, grid, pos, zero,
+                       tnp::key_below<1>(K - 1), table, tmask, cnt, memoff, cur, mem);
   TNP_CHECK(hipGetLastError());
   return 0;
 }

@@ -36,7 +36,9 @@ struct NetDev {
 };
 
 static inline int net_K(const NetDev& n) { return (n.num_layers - 1) * n.num_hidden + 1; }
-int net_supported(const NetDev& n);  // 1 if an instantiation exists
+int net_supported(const NetDev& n);       // 1 if forward / keys / the flat steps are instantiated
+int net_supported_full(const NetDev& n);  // ... and the curve descent, training and autograd kernels
+static inline int net_kw(const NetDev& n) { return net_K(n) <= 63 ? 1 : 2; }  // sign-key words
 
 // ---- net_lv.hip: the kernels of one level count (one translation unit per
 // level count 2..8, -DTNP_LV; explicit specializations, dispatched by the
@@ -129,7 +131,7 @@ int launch_forward_new(const NetDev& net, const float* xyz, int64_t n, float* pr
                        uint64_t* shared, int64_t* ctr, uint64_t* pz, const float* col, hipStream_t s);
 int launch_override_new(int64_t n, int override_, const uint64_t* shared, float* pre, int64_t ld,
                         int keep_from, int64_t V, uint64_t* pos, uint64_t* zero,
-                        const int64_t* ctr, uint64_t* pz, hipStream_t s);
+                        const int64_t* ctr, uint64_t* pz, int kw, hipStream_t s);
 int launch_encode(const NetDev& net, const float* x01, int64_t n, float* out, hipStream_t s);
 // pre plane-major; writes int64 m[n][3+K] and off[n][3] (Net.region)
 int launch_region(const NetDev& net, const float* xyz, const float* pre, int64_t ld,

@@ -34,23 +34,26 @@ namespace {
 // the override itself (masked_fill_ of the shared planes, subpoly_debug.py:48)
 // on what k_forward_new wrote; override_ < 0: the single-device predicate is
 // still in ctr[CTR_FAIL]
+template <int KW>
 __global__ void k_override_new(int64_t n, int override_, const uint64_t* __restrict__ shared,
                                float* __restrict__ pre, int64_t ld, int keep_from, int64_t V,
                                uint64_t* __restrict__ pos, uint64_t* __restrict__ zero,
-                               const int64_t* __restrict__ ctr, ulonglong2* __restrict__ pz) {
+                               const int64_t* __restrict__ ctr, uint64_t* __restrict__ pz) {
   const bool ov = override_ < 0 ? ctr[CTR_FAIL] != 0 : override_ != 0;
   if (!ov) return;
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n) return;
-  const uint64_t m = shared[r];
-  for (uint64_t t = m; t; t &= t - 1) {
-    const int p = __builtin_ctzll(t);
-    if (p >= keep_from) pre[(int64_t)p * ld + V + r] = 0.f;
-  }
-  const uint64_t p = pos[V + r] & ~m, z = zero[V + r] | m;
-  pos[V + r] = p;
-  zero[V + r] = z;
-  pz[V + r] = make_ulonglong2(p, z);
+  const Key<KW> m = tnp::key_load<KW>(shared, r);
+#pragma unroll
+  for (int q = 0; q < KW; ++q)
+    for (uint64_t t = m.w[q]; t; t &= t - 1) {
+      const int p = 64 * q + __builtin_ctzll(t);
+      if (p >= keep_from) pre[(int64_t)p * ld + V + r] = 0.f;
+    }
+  const Key<KW> p = tnp::key_load<KW>(pos, V + r) & ~m, z = tnp::key_load<KW>(zero, V + r) | m;
+  tnp::key_store(pos, V + r, p);
+  tnp::key_store(zero, V + r, z);
+  tnp::pz_store(pz, V + r, p, z);
 }
 
 __global__ void k_region(NetDev net, const float* __restrict__ xyz,
@@ -73,29 +76,38 @@ __global__ void k_region(NetDev net, const float* __restrict__ xyz,
   }
 }
 
+template <int KW>
 __global__ void k_keys(NetDev net, const float* __restrict__ xyz, const float* __restrict__ pre,
                        int64_t ld, int64_t n, int K, uint64_t* __restrict__ pos,
                        uint64_t* __restrict__ zero, uint64_t* __restrict__ grid,
-                       ulonglong2* __restrict__ pz) {
+                       uint64_t* __restrict__ pz) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   float x[3];
   load_point(xyz, i, x);
   grid[i] = grid_word(net.marks, net.n_marks, net.eps, x);
-  uint64_t ps = 0, zs = 0;
+  Key<KW> ps = tnp::key_zero<KW>(), zs = tnp::key_zero<KW>();
   for (int p = 0; p < K; ++p) {
     float v = pre[(int64_t)p * ld + i];
-    ps |= (uint64_t)(v > net.eps) << p;  // sign +1 ((output>0)*2-1 with |.|<=eps -> 0)
-    zs |= (uint64_t)(fabsf(v) <= net.eps) << p;
+    tnp::key_put(ps, p, v > net.eps);  // sign +1 ((output>0)*2-1 with |.|<=eps -> 0)
+    tnp::key_put(zs, p, fabsf(v) <= net.eps);
   }
-  pos[i] = ps;
-  zero[i] = zs;
-  if (pz) pz[i] = make_ulonglong2(ps, zs);
+  tnp::key_store(pos, i, ps);
+  tnp::key_store(zero, i, zs);
+  if (pz) tnp::pz_store(pz, i, ps, zs);
 }
 
 }  // namespace
 
 int net_supported(const NetDev& n) {
+  if (n.n_levels < 2 || n.n_levels > 8) return 0;
+#define TNP_SHAPE_OK(H_, NL_) if (n.num_hidden == H_ && n.num_layers == NL_) return 1;
+  TNP_ALL_SHAPES(TNP_SHAPE_OK)
+#undef TNP_SHAPE_OK
+  return 0;
+}
+
+int net_supported_full(const NetDev& n) {
   if (n.n_levels < 2 || n.n_levels > 8) return 0;
 #define TNP_SHAPE_OK(H_, NL_) if (n.num_hidden == H_ && n.num_layers == NL_) return 1;
   TNP_NET_SHAPES(TNP_SHAPE_OK)
@@ -128,10 +140,14 @@ int launch_forward_new(const NetDev& net, const float* xyz, int64_t n, float* pr
 
 int launch_override_new(int64_t n, int override_, const uint64_t* shared, float* pre, int64_t ld,
                         int keep_from, int64_t V, uint64_t* pos, uint64_t* zero,
-                        const int64_t* ctr, uint64_t* pz, hipStream_t s) {
+                        const int64_t* ctr, uint64_t* pz, int kw, hipStream_t s) {
   if (n <= 0 || override_ == 0) return 0;
-  hipLaunchKernelGGL(k_override_new, dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, n, override_, shared,
-                     pre, ld, keep_from, V, pos, zero, ctr, reinterpret_cast<ulonglong2*>(pz));
+  if (kw == 2)
+    hipLaunchKernelGGL(k_override_new<2>, dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, n, override_, shared,
+                       pre, ld, keep_from, V, pos, zero, ctr, pz);
+  else
+    hipLaunchKernelGGL(k_override_new<1>, dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, n, override_, shared,
+                       pre, ld, keep_from, V, pos, zero, ctr, pz);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
@@ -148,8 +164,12 @@ int launch_region(const NetDev& net, const float* xyz, const float* pre, int64_t
 int launch_keys(const NetDev& net, const float* xyz, const float* pre, int64_t ld, int64_t n,
                 int K, uint64_t* pos, uint64_t* zero, uint64_t* grid, hipStream_t s, uint64_t* pz) {
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(k_keys, dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net, xyz, pre, ld, n, K,
-                     pos, zero, grid, reinterpret_cast<ulonglong2*>(pz));
+  if (key_words(K) == 2)
+    hipLaunchKernelGGL(k_keys<2>, dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net, xyz, pre, ld, n, K,
+                       pos, zero, grid, pz);
+  else
+    hipLaunchKernelGGL(k_keys<1>, dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net, xyz, pre, ld, n, K,
+                       pos, zero, grid, pz);
   TNP_CHECK(hipGetLastError());
   return 0;
 }

@@ -307,10 +307,26 @@ __device__ __forceinline__ float neuron_mode(const float* __restrict__ W, const 
   constexpr int WD = next_pow2(IN);
   constexpr int LN = WD < 16 ? WD : 16;
   static_assert(WD <= 32, "layers of at most 32 inputs");
-  // (a 32-input layer with more than 2 outputs -- 32-wide hidden layers --
-  // is compiled but never run: TNP_NET_SHAPES has no such shape, and MKL's
-  // 1-row schedule for it is not verified)
   const float* Wj = W + j * IN;
+  if constexpr (IN == 32 && OUT == 32) {
+    // the 32 -> 32 hidden layer's 1-row call (mode ONE; FOLD never applies):
+    // MKL's tree, probed bitwise (tools/mkl_order_probe.py tree32): inputs
+    // 0..16 as one block, then 17 by fma, then 25, 21 + 29 and
+    // 19/23/27/31 in turn, the even inputs 18..30 as one block, bias last
+    if (mode == LIN_ONE) {
+      auto p = [&](int k) { return __fmul_rn(in[k], Wj[k]); };
+      auto s = [](float u, float v) { return __fadd_rn(u, v); };
+      const float a1 = s(s(__fmaf_rn(in[1], Wj[1], p(0)), p(9)), s(p(5), p(13)));
+      const float a2 = s(s(p(3), p(11)), s(p(7), p(15)));
+      const float bl = s(s(s(p(2), p(10)), s(p(6), p(14))), s(s(p(4), p(12)), s(p(8), p(16))));
+      float t = __fmaf_rn(in[17], Wj[17], s(s(a1, a2), bl));
+      t = s(t, p(25));
+      t = s(t, s(p(21), p(29)));
+      t = s(t, s(s(p(19), p(27)), s(p(23), p(31))));
+      const float ev = s(s(s(p(18), p(26)), s(p(22), p(30))), s(s(p(20), p(28)), p(24)));
+      return s(s(t, ev), b[j]);
+    }
+  }
   float l[LN];
   float r;
   if (mode == LIN_FOLD) {
@@ -371,5 +387,13 @@ struct NetShape {
 // net_lv.hip), (hidden, layers) below -- K = (layers - 1) hidden + 1 <= 63
 // planes fit the 64-bit sign keys
 #define TNP_NET_SHAPES(X) X(8, 2) X(8, 3) X(8, 4) X(16, 2) X(16, 3) X(16, 4) X(32, 2)
+// wide shapes: K = 65 or 97 planes, two-word sign keys (common.h Key<2>).
+// They run the flat subpoly path (forward, keys, steps, faces), Net.forward /
+// sdf / normal and the skeleton; the curve branch, its descent and the
+// training / autograd kernels stay with TNP_NET_SHAPES
+#define TNP_WIDE_SHAPES(X) X(16, 5) X(32, 3) X(32, 4)
+#define TNP_ALL_SHAPES(X) TNP_NET_SHAPES(X) TNP_WIDE_SHAPES(X)
+// sign-key words of a net of K planes
+__host__ __device__ constexpr int key_words(int K) { return K <= 63 ? 1 : 2; }
 
 }  // namespace tnpnet

@@ -41,7 +41,7 @@ template <int LV, int H, int NL, bool GROUPED>
 __global__ void __launch_bounds__(TNP_BLOCK)
 k_forward(NetDev net, const float* __restrict__ xyz, int64_t n, float* __restrict__ pre,
           int64_t ld, float* __restrict__ out2, uint64_t* __restrict__ kpos, uint64_t* __restrict__ kzero,
-          uint64_t* __restrict__ kgrid, ulonglong2* __restrict__ kpz) {
+          uint64_t* __restrict__ kgrid, uint64_t* __restrict__ kpz) {
   constexpr int IN = 2 * LV;
   constexpr int NW = NetShape<LV, H, NL>::NW;
   __shared__ float w[NW];
@@ -61,7 +61,8 @@ k_forward(NetDev net, const float* __restrict__ xyz, int64_t n, float* __restric
   int p = 0;
   const int64_t ns = net.sched_rows > 0 ? net.sched_rows : n;  // the schedule's row count
   const int m0 = lin_mode<IN, H>(ns), mh = lin_mode<H, H>(ns), mo = lin_mode<H, 2>(ns);
-  uint64_t ps = 0, zs = 0;  // packed eps-sign keys (k_keys), when kpos is given
+  constexpr int KW = key_words((NL - 1) * H + 1);
+  Key<KW> ps = tnp::key_zero<KW>(), zs = tnp::key_zero<KW>();  // packed eps-sign keys (k_keys), when kpos is given
 #pragma unroll
   for (int layer = 0; layer < NL - 1; ++layer) {
     if (layer == 0) {
@@ -73,8 +74,8 @@ k_forward(NetDev net, const float* __restrict__ xyz, int64_t n, float* __restric
     }
 #pragma unroll
     for (int j = 0; j < H; ++j) {
-      ps |= (uint64_t)(a[j] > net.eps) << (p + j);
-      zs |= (uint64_t)(fabsf(a[j]) <= net.eps) << (p + j);
+      tnp::key_put(ps, p + j, a[j] > net.eps);
+      tnp::key_put(zs, p + j, fabsf(a[j]) <= net.eps);
       if (live && pre) pre[(int64_t)(p + j) * ld + i] = a[j];
       if (GROUPED) {
         const int base = (threadIdx.x & 63) & ~7;
@@ -97,11 +98,11 @@ k_forward(NetDev net, const float* __restrict__ xyz, int64_t n, float* __restric
     out2[2 * i + 1] = o[1];
   }
   if (!GROUPED && live && kpos) {  // the keys of k_keys, from the values in registers
-    ps |= (uint64_t)(v > net.eps) << p;
-    zs |= (uint64_t)(fabsf(v) <= net.eps) << p;
-    kpos[i] = ps;
-    kzero[i] = zs;
-    kpz[i] = make_ulonglong2(ps, zs);
+    tnp::key_put(ps, p, v > net.eps);
+    tnp::key_put(zs, p, fabsf(v) <= net.eps);
+    tnp::key_store(kpos, i, ps);
+    tnp::key_store(kzero, i, zs);
+    tnp::pz_store(kpz, i, ps, zs);
     kgrid[i] = grid_word(mk, net.n_marks, net.eps, x);
   }
 }
@@ -120,9 +121,10 @@ k_forward_new(NetDev net, const float* xyz, int64_t n, float* __restrict__ pre,
               int64_t ld, int64_t V, int keep_from, const int32_t* __restrict__ sa,
               const int32_t* __restrict__ sb, int idx, int own_lo, int own_hi, uint64_t* pos,
               uint64_t* zero, uint64_t* __restrict__ grid, uint64_t* __restrict__ shared,
-              int64_t* __restrict__ ctr, ulonglong2* __restrict__ pz, const float* __restrict__ scol) {
+              int64_t* __restrict__ ctr, uint64_t* __restrict__ pz, const float* __restrict__ scol) {
   constexpr int IN = 2 * LV;
   constexpr int NW = NetShape<LV, H, NL>::NW;
+  constexpr int KW = key_words((NL - 1) * H + 1);
   __shared__ float w[NW];
   __shared__ float mk[TNP_MAX_MARKS];
   for (int i = threadIdx.x; i < NW; i += blockDim.x) w[i] = net.weights[i];
@@ -135,12 +137,12 @@ k_forward_new(NetDev net, const float* xyz, int64_t n, float* __restrict__ pre,
   const float eps = net.eps;      // Net.region: the keys
   const float eps_s = net.eps_s;  // subpoly_'s eps: split point, failover
   float x[3] = {0.f, 0.f, 0.f};
-  uint64_t m = 0;
+  Key<KW> m = tnp::key_zero<KW>();
   if (live) {
     const int a = sa[i], b = sb[i];
     // every gather the endpoints need, issued before the first store (the
     // coordinate store could alias zero[] for the compiler)
-    const uint64_t za = zero[a], zb = zero[b];
+    const Key<KW> za = tnp::key_load<KW>(zero, a), zb = tnp::key_load<KW>(zero, b);
     if (scol) {
       // the split point itself (k_new_vertices, subpoly.py:113-117, 180), fused:
       // d = d/eps; w = |d0| / |d1 - d0|; v = e0*(1-w) + e1*w
@@ -165,15 +167,14 @@ k_forward_new(NetDev net, const float* xyz, int64_t n, float* __restrict__ pre,
     } else {
       load_point(xyz, i, x);
     }
-    const uint64_t below = (idx >= 64) ? ~0ull : ((1ull << idx) - 1ull);
-    m = (za & zb & below) | (1ull << idx);
+    m = (za & zb & tnp::key_below<KW>(idx)) | tnp::key_bit<KW>(idx);
   }
   float h[H > IN ? H : IN];
   float a[H];
   encode<LV>(net, x, h);
   const float* W = w;
   int p = 0;
-  uint64_t ps = 0, zs = 0;
+  Key<KW> ps = tnp::key_zero<KW>(), zs = tnp::key_zero<KW>();
   bool bad = false;
   const int m0 = lin_mode<IN, H>(n), mh = lin_mode<H, H>(n), mo = lin_mode<H, 2>(n);
   float* col = pre + V + i;
@@ -190,9 +191,9 @@ k_forward_new(NetDev net, const float* xyz, int64_t n, float* __restrict__ pre,
     for (int j = 0; j < H; ++j) {
       const float v = a[j];
       if (live && p + j >= keep_from) col[(int64_t)(p + j) * ld] = v;
-      ps |= (uint64_t)(v > eps) << (p + j);
-      zs |= (uint64_t)(fabsf(v) <= eps) << (p + j);
-      bad |= ((m >> (p + j)) & 1) && fabsf(v) > eps_s;
+      tnp::key_put(ps, p + j, v > eps);
+      tnp::key_put(zs, p + j, fabsf(v) <= eps);
+      bad |= tnp::key_test(m, p + j) && fabsf(v) > eps_s;
       h[j] = fmaxf(v, 0.0f);
     }
     p += H;
@@ -202,13 +203,13 @@ k_forward_new(NetDev net, const float* xyz, int64_t n, float* __restrict__ pre,
   const float v = __fsub_rn(o[1], o[0]);
   if (live) {
     if (p >= keep_from) col[(int64_t)p * ld] = v;
-    ps |= (uint64_t)(v > eps) << p;
-    zs |= (uint64_t)(fabsf(v) <= eps) << p;
-    bad |= ((m >> p) & 1) && fabsf(v) > eps_s;
-    pos[V + i] = ps;
-    zero[V + i] = zs;
-    pz[V + i] = make_ulonglong2(ps, zs);
-    shared[i] = m;
+    tnp::key_put(ps, p, v > eps);
+    tnp::key_put(zs, p, fabsf(v) <= eps);
+    bad |= tnp::key_test(m, p) && fabsf(v) > eps_s;
+    tnp::key_store(pos, V + i, ps);
+    tnp::key_store(zero, V + i, zs);
+    tnp::pz_store(pz, V + i, ps, zs);
+    tnp::key_store(shared, i, m);
   }
   // full lower_bound over the marks in LDS: cheaper than gathering the
   // endpoints' grid words to narrow it (measured at 128^3: 1.02 -> 0.90 ms
@@ -227,218 +228,6 @@ k_forward_new(NetDev net, const float* xyz, int64_t n, float* __restrict__ pre,
     if (halo && tnp::lane() == 0)
       atomicAdd((unsigned long long*)&ctr[CTR_DUP], (unsigned long long)__popcll(halo));
   }
-}
-
-// k_forward_new with TWO splits per thread (rows i and i + blockDim.x of
-// the block's span): both rows' endpoint gathers, then both rows' hash-table
-// gathers are in flight together -- the kernel waits on those two dependent
-// gather rounds (the table lines mostly miss L2), and a second row doubles
-// the loads in flight per wave at the cost of one wave per SIMD.  Every
-// value and store is k_forward_new's (same ops per row, same MKL schedule).
-template <int LV>
-__device__ __forceinline__ void encode_rows2(const NetDev& net, const float x0[3], const float x1[3], float* f0,
-                                             float* f1) {
-  if constexpr (LV % 2 == 0) {
-    if (net.tied) {
-      // level 0's cell, weights and indices serve every level (encode_tied)
-      const float s = net.scales[0];
-      const uint32_t res = (uint32_t)net.res[0];
-      const uint32_t size = net.sizes[0];
-      const bool dense = net.dense[0] != 0;
-      const float4* tab = reinterpret_cast<const float4*>(net.table);
-      const float* xs[2] = {x0, x1};
-      float wc[2][8];
-      float4 v[2][8][LV / 2];
-#pragma unroll
-      for (int r = 0; r < 2; ++r) {
-        float t[3];
-        uint32_t g[3];
-#pragma unroll
-        for (int d = 0; d < 3; ++d) {
-          float pos = __fadd_rn(__fmul_rn(xs[r][d], s), 0.5f);
-          float fl = floorf(pos);
-          t[d] = __fsub_rn(pos, fl);
-          g[d] = (uint32_t)(int)fl;
-        }
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-          float w = 1.0f;
-          uint32_t gc[3];
-#pragma unroll
-          for (int d = 0; d < 3; ++d) {
-            if ((c >> d) & 1) {
-              w = __fmul_rn(w, t[d]);
-              gc[d] = g[d] + 1u;
-            } else {
-              w = __fmul_rn(w, __fsub_rn(1.0f, t[d]));
-              gc[d] = g[d];
-            }
-          }
-          uint32_t idx = dense ? (gc[0] + gc[1] * res + gc[2] * (res * res)) : (gc[0] ^ (gc[1] * P1) ^ (gc[2] * P2));
-          idx = wrap_index(idx, size);
-          wc[r][c] = w;
-#pragma unroll
-          for (int q = 0; q < LV / 2; ++q) v[r][c][q] = tab[(size_t)idx * (LV / 2) + q];
-        }
-      }
-      float* fs[2] = {f0, f1};
-#pragma unroll
-      for (int r = 0; r < 2; ++r) {
-        float acc[2 * LV];
-#pragma unroll
-        for (int q = 0; q < 2 * LV; ++q) acc[q] = 0.f;
-#pragma unroll
-        for (int c = 0; c < 8; ++c)
-#pragma unroll
-          for (int q = 0; q < LV / 2; ++q) {
-            acc[4 * q + 0] = __fadd_rn(acc[4 * q + 0], __fmul_rn(wc[r][c], v[r][c][q].x));
-            acc[4 * q + 1] = __fadd_rn(acc[4 * q + 1], __fmul_rn(wc[r][c], v[r][c][q].y));
-            acc[4 * q + 2] = __fadd_rn(acc[4 * q + 2], __fmul_rn(wc[r][c], v[r][c][q].z));
-            acc[4 * q + 3] = __fadd_rn(acc[4 * q + 3], __fmul_rn(wc[r][c], v[r][c][q].w));
-          }
-#pragma unroll
-        for (int q = 0; q < 2 * LV; ++q) fs[r][q] = acc[q];
-      }
-      return;
-    }
-  }
-  encode<LV>(net, x0, f0);
-  encode<LV>(net, x1, f1);
-}
-
-template <int LV, int H, int NL>
-__global__ void __launch_bounds__(TNP_BLOCK, 3)
-k_forward_new2(NetDev net, const float* xyz, int64_t n, float* __restrict__ pre,
-               int64_t ld, int64_t V, int keep_from, const int32_t* __restrict__ sa,
-               const int32_t* __restrict__ sb, int idx, int own_lo, int own_hi, uint64_t* pos,
-               uint64_t* zero, uint64_t* __restrict__ grid, uint64_t* __restrict__ shared,
-               int64_t* __restrict__ ctr, ulonglong2* __restrict__ pz, const float* __restrict__ scol) {
-  constexpr int IN = 2 * LV;
-  constexpr int NW = NetShape<LV, H, NL>::NW;
-  __shared__ float w[NW];
-  __shared__ float mk[TNP_MAX_MARKS];
-  for (int i = threadIdx.x; i < NW; i += blockDim.x) w[i] = net.weights[i];
-  for (int i = threadIdx.x; i < net.n_marks; i += blockDim.x) mk[i] = net.marks[i];
-  __syncthreads();
-  const int64_t i0 = tnp::xcd_block(blockIdx.x, gridDim.x) * (2 * (int64_t)blockDim.x) + threadIdx.x;
-  const int64_t ir[2] = {i0, i0 + blockDim.x};
-  const float eps = net.eps;      // Net.region: the keys
-  const float eps_s = net.eps_s;  // subpoly_'s eps: split point, failover
-  const uint64_t below = (idx >= 64) ? ~0ull : ((1ull << idx) - 1ull);
-  bool live[2];
-  float x[2][3];
-  uint64_t m[2] = {0, 0};
-  {
-    int a[2], b[2];
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      live[r] = ir[r] < n;
-      a[r] = live[r] ? sa[ir[r]] : 0;
-      b[r] = live[r] ? sb[ir[r]] : 0;
-    }
-    // both rows' endpoint gathers before any store (the coordinate store
-    // could alias zero[] for the compiler)
-    uint64_t za[2], zb[2];
-    float c0[2] = {0.f, 0.f}, c1[2] = {0.f, 0.f}, ea[2][3], eb[2][3];
-    const float* base = xyz - 3 * V;  // xyz points at slot V
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      za[r] = zero[a[r]];
-      zb[r] = zero[b[r]];
-      if (scol) {
-        c0[r] = scol[a[r]];
-        c1[r] = scol[b[r]];
-#pragma unroll
-        for (int d = 0; d < 3; ++d) {
-          ea[r][d] = base[3 * (int64_t)a[r] + d];
-          eb[r][d] = base[3 * (int64_t)b[r] + d];
-        }
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      x[r][0] = x[r][1] = x[r][2] = 0.f;
-      if (!live[r]) continue;
-      if (scol) {
-        // the split point (k_new_vertices, subpoly.py:113-117, 180)
-        const float d0 = __fdiv_rn(c0[r], eps_s), d1 = __fdiv_rn(c1[r], eps_s);
-        const float wt = __fdiv_rn(fabsf(d0), fabsf(__fsub_rn(d1, d0)));
-        const float om = __fsub_rn(1.0f, wt);
-        float* out = const_cast<float*>(xyz) + 3 * ir[r];
-#pragma unroll
-        for (int d = 0; d < 3; ++d) {
-          const float v = __fadd_rn(__fmul_rn(ea[r][d], om), __fmul_rn(eb[r][d], wt));
-          out[d] = v;
-          x[r][d] = __fmul_rn(__fadd_rn(v, 1.0f), 0.5f);  // Net.preprocess (x/2 == x*0.5 exactly)
-        }
-      } else {
-        load_point(xyz, ir[r], x[r]);
-      }
-      m[r] = (za[r] & zb[r] & below) | (1ull << idx);
-    }
-  }
-  float f[2][IN];
-  encode_rows2<LV>(net, x[0], x[1], f[0], f[1]);
-  const int m0 = lin_mode<IN, H>(n), mh = lin_mode<H, H>(n), mo = lin_mode<H, 2>(n);
-  bool bad_any = false;
-  uint64_t halo = 0;
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    const int64_t i = ir[r];
-    float h[H > IN ? H : IN];
-#pragma unroll
-    for (int q = 0; q < IN; ++q) h[q] = f[r][q];
-    float a[H];
-    const float* W = w;
-    int p = 0;
-    uint64_t ps = 0, zs = 0;
-    bool bad = false;
-    float* col = pre + V + i;
-#pragma unroll
-    for (int layer = 0; layer < NL - 1; ++layer) {
-      if (layer == 0) {
-        linear_mode<IN, H>(W, W + H * IN, h, a, m0, i);
-        W += H * IN + H;
-      } else {
-        linear_mode<H, H>(W, W + H * H, h, a, mh, i);
-        W += H * H + H;
-      }
-#pragma unroll
-      for (int j = 0; j < H; ++j) {
-        const float v = a[j];
-        if (live[r] && p + j >= keep_from) col[(int64_t)(p + j) * ld] = v;
-        ps |= (uint64_t)(v > eps) << (p + j);
-        zs |= (uint64_t)(fabsf(v) <= eps) << (p + j);
-        bad |= ((m[r] >> (p + j)) & 1) && fabsf(v) > eps_s;
-        h[j] = fmaxf(v, 0.0f);
-      }
-      p += H;
-    }
-    float o[2];
-    linear_mode<H, 2>(W, W + 2 * H, h, o, mo, i);
-    const float v = __fsub_rn(o[1], o[0]);
-    if (live[r]) {
-      if (p >= keep_from) col[(int64_t)p * ld] = v;
-      ps |= (uint64_t)(v > eps) << p;
-      zs |= (uint64_t)(fabsf(v) <= eps) << p;
-      bad |= ((m[r] >> p) & 1) && fabsf(v) > eps_s;
-      pos[V + i] = ps;
-      zero[V + i] = zs;
-      pz[V + i] = make_ulonglong2(ps, zs);
-      shared[i] = m[r];
-    }
-    const uint64_t g = grid_word(mk, net.n_marks, eps, x[r]);
-    if (live[r]) grid[V + i] = g;
-    bad_any |= live[r] && bad;
-    if (own_lo <= own_hi) {
-      const int c = tnp::grid_off(g, 0);
-      const bool owned = tnp::grid_zero(g, 0) ? ((c > own_lo || (own_lo == 0 && c == 0)) && c <= own_hi)
-                                              : (c >= own_lo && c < own_hi);
-      halo += __popcll(__ballot(live[r] && !owned));
-    }
-  }
-  if (__ballot(bad_any) && tnp::lane() == 0) tnp::or_sticky(&ctr[CTR_FAIL], 1ull);
-  if (halo && tnp::lane() == 0) atomicAdd((unsigned long long*)&ctr[CTR_DUP], (unsigned long long)halo);
 }
 
 // TropicalHashGrid.forward: raw encoding of x already in [0,1]^3 -> [n][2L]
@@ -516,13 +305,17 @@ k_skel_eval(NetDev net, int i0, int j0, int k0, int n0, int n1, int n2,
     TNP_SHAPE_BODY;                                          \
     break;                                                   \
   }
-#define TNP_SHAPE_SWITCH(net)                                                                       \
+#define TNP_SHAPE_SWITCH_OF(net, SHAPES)                                                            \
   switch ((net).num_hidden * 16 + (net).num_layers) {                                              \
-    TNP_NET_SHAPES(TNP_SHAPE_CASE)                                                                   \
+    SHAPES(TNP_SHAPE_CASE)                                                                           \
     default:                                                                                         \
-      tnp_set_error("net shape (hidden=%d, layers=%d) not instantiated", (net).num_hidden, (net).num_layers); \
+      tnp_set_error("net shape (hidden=%d, layers=%d) not instantiated for this operation",         \
+                    (net).num_hidden, (net).num_layers);                                             \
       return -1;                                                                                     \
   }
+// every shape / the K <= 63 shapes (curve descent, training, autograd)
+#define TNP_SHAPE_SWITCH_ALL(net) TNP_SHAPE_SWITCH_OF(net, TNP_ALL_SHAPES)
+#define TNP_SHAPE_SWITCH(net) TNP_SHAPE_SWITCH_OF(net, TNP_NET_SHAPES)
 
 template <>
 int lv_forward<LVC>(const NetDev& net, const float* xyz, int64_t n, float* pre, int64_t ld, int group,
@@ -533,8 +326,8 @@ int lv_forward<LVC>(const NetDev& net, const float* xyz, int64_t n, float* pre, 
                        ld, out2, nullptr, nullptr, nullptr, nullptr);                                           \
   else                                                                                                          \
     hipLaunchKernelGGL((k_forward<LVC, H, NL, false>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net, xyz, n,    \
-                       pre, ld, out2, pos, zero, grid, reinterpret_cast<ulonglong2*>(pz));
-  TNP_SHAPE_SWITCH(net)
+                       pre, ld, out2, pos, zero, grid, pz);
+  TNP_SHAPE_SWITCH_ALL(net)
 #undef TNP_SHAPE_BODY
   TNP_CHECK(hipGetLastError());
   return 0;
@@ -545,21 +338,10 @@ int lv_forward_new<LVC>(const NetDev& net, const float* xyz, int64_t n, float* p
                         int keep_from, const int32_t* sa, const int32_t* sb, int idx, int own_lo, int own_hi,
                         uint64_t* pos, uint64_t* zero, uint64_t* grid, uint64_t* shared, int64_t* ctr, uint64_t* pz,
                         const float* col, hipStream_t s) {
-  static const int s_rows = [] {  // TNP_FN_ROWS=2: two splits per thread (k_forward_new2)
-    const char* v = getenv("TNP_FN_ROWS");
-    return v ? atoi(v) : 1;
-  }();
-  const int64_t g2 = (n + 2 * TNP_BLOCK - 1) / (2 * TNP_BLOCK);
 #define TNP_SHAPE_BODY                                                                                   \
-  if (s_rows == 2)                                                                                       \
-    hipLaunchKernelGGL((k_forward_new2<LVC, H, NL>), dim3(g2), dim3(TNP_BLOCK), 0, s, net, xyz, n, pre, ld, V, \
-                       keep_from, sa, sb, idx, own_lo, own_hi, pos, zero, grid, shared, ctr,                   \
-                       reinterpret_cast<ulonglong2*>(pz), col);                                               \
-  else                                                                                                   \
-    hipLaunchKernelGGL((k_forward_new<LVC, H, NL>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net, xyz, n, pre, \
-                       ld, V, keep_from, sa, sb, idx, own_lo, own_hi, pos, zero, grid, shared, ctr,            \
-                       reinterpret_cast<ulonglong2*>(pz), col);
-  TNP_SHAPE_SWITCH(net)
+  hipLaunchKernelGGL((k_forward_new<LVC, H, NL>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net, xyz, n, pre, ld, \
+                     V, keep_from, sa, sb, idx, own_lo, own_hi, pos, zero, grid, shared, ctr, pz, col);
+  TNP_SHAPE_SWITCH_ALL(net)
 #undef TNP_SHAPE_BODY
   TNP_CHECK(hipGetLastError());
   return 0;
@@ -569,7 +351,7 @@ template <>
 int lv_sdf_grad<LVC>(const NetDev& net, const float* xyz, int64_t n, float* sdf, float* grad, hipStream_t s) {
 #define TNP_SHAPE_BODY \
   hipLaunchKernelGGL((k_sdf_grad<LVC, H, NL>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net, xyz, n, sdf, grad);
-  TNP_SHAPE_SWITCH(net)
+  TNP_SHAPE_SWITCH_ALL(net)
 #undef TNP_SHAPE_BODY
   TNP_CHECK(hipGetLastError());
   return 0;
@@ -582,7 +364,7 @@ int lv_skel_eval<LVC>(const NetDev& net, int i0, int j0, int k0, int n0, int n1,
 #define TNP_SHAPE_BODY                                                                                         \
   hipLaunchKernelGGL((k_skel_eval<LVC, H, NL>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net, i0, j0, k0, n0, \
                      n1, n2, dist, gmax_bits);
-  TNP_SHAPE_SWITCH(net)
+  TNP_SHAPE_SWITCH_ALL(net)
 #undef TNP_SHAPE_BODY
   TNP_CHECK(hipGetLastError());
   return 0;

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "common.h"
+
 // slots of the engine's int64 device counter block (one pinned readback)
 enum {
   CTR_S = 0,        // split count (scan total)
@@ -91,7 +93,7 @@ int launch_count_unowned(const uint64_t* grid, int64_t n, int own_lo, int own_hi
 // the device (no host round trip for the hit count)
 int launch_span_count(const int32_t* members, int64_t S, int64_t M, const uint64_t* grid,
                       const uint64_t* zero, int idx, int32_t* cnt, int64_t* part, int64_t* ctr,
-                      hipStream_t s);
+                      int kw, hipStream_t s);
 int launch_span_emit(const int32_t* members, int64_t S, int64_t M, const uint64_t* grid, int NC,
                      const int64_t* eoff, uint32_t* ekey, int32_t* eval, const int64_t* ctr,
                      hipStream_t s);
@@ -123,6 +125,31 @@ struct alignas(32) CellEnt {
   uint32_t f;
   uint32_t tag, pad;
 };
+// the record of a two-word-key net (K > 63, radix path only): 48 bytes
+struct alignas(16) CellEnt2 {
+  uint64_t p[2], z[2];
+  int32_t v;
+  uint32_t f;
+  uint32_t tag, pad;
+};
+template <int KW> struct CellEntOf { using type = CellEnt; };
+template <> struct CellEntOf<2> { using type = CellEnt2; };
+template <int KW> using CellEntT = typename CellEntOf<KW>::type;
+__host__ __device__ inline size_t cell_ent_bytes(int kw) { return kw == 2 ? sizeof(CellEnt2) : sizeof(CellEnt); }
+__device__ __forceinline__ Key<1> ent_p(const CellEnt& e) { return Key<1>{{e.p}}; }
+__device__ __forceinline__ Key<1> ent_z(const CellEnt& e) { return Key<1>{{e.z}}; }
+__device__ __forceinline__ Key<2> ent_p(const CellEnt2& e) { return Key<2>{{e.p[0], e.p[1]}}; }
+__device__ __forceinline__ Key<2> ent_z(const CellEnt2& e) { return Key<2>{{e.z[0], e.z[1]}}; }
+__device__ __forceinline__ void ent_set_keys(CellEnt& e, const Key<1>& p, const Key<1>& z) {
+  e.p = p.w[0];
+  e.z = z.w[0];
+}
+__device__ __forceinline__ void ent_set_keys(CellEnt2& e, const Key<2>& p, const Key<2>& z) {
+  e.p[0] = p.w[0];
+  e.p[1] = p.w[1];
+  e.z[0] = z.w[0];
+  e.z[1] = z.w[1];
+}
 // cells of at most WCELL members have their pairs tested by the window pass
 // (k_connect_win): a pair (j < i) of such a cell lies in the 64-entry
 // window starting at 32 * floor(j / 32)
@@ -145,9 +172,9 @@ __device__ __forceinline__ uint32_t cell_flags(uint64_t g, int cx, int cy, int c
   }
   return f;
 }
-// pz: the interleaved (pos, zero) copy of the vertex keys
+// pz: the interleaved (pos, zero) copy of the vertex keys; ent: CellEntT<kw> records
 int launch_entry_keys(const int32_t* ent_v, const uint32_t* ekey, int NC, int64_t T,
-                      const uint64_t* grid, const uint64_t* pz, CellEnt* ent, hipStream_t s);
+                      const uint64_t* grid, const uint64_t* pz, void* ent, int kw, hipStream_t s);
 
 // connecting edges over the flattened pair space (pair cells in order, then
 // (i, j<i) inside a cell); the pair count and R are read on the device.
@@ -162,9 +189,11 @@ int64_t connect_chunks(int64_t TT);
 int64_t connect_grid();
 int launch_chunk_cells(const int64_t* ptoff, const int32_t* pn, int64_t rcap, int32_t* bcell,
                        int64_t cap, int64_t* ctr, hipStream_t s);
+// ent: CellEntT<kw> records; filt_last >= 0: the pruning filter is planes
+// [idx, filt_last] (endpoint keys differing there), < 0: every pair kept
 int launch_connect(const int64_t* ptoff, const int32_t* pcell, const int32_t* pn,
                    const int32_t* pent, int NC, int64_t max_tests, const int32_t* bcell,
-                   const CellEnt* ent, int idx, int nb, uint64_t fmask, uint64_t* keys,
+                   const void* ent, int idx, int nb, int filt_last, int kw, uint64_t* keys,
                    int64_t cap, int64_t* xs, int64_t* ctr, hipStream_t s, const int64_t* bstat = nullptr,
                    int nbstat = 0);
 // single-pass pruning over [edges; e_new; c_new] (lb_tiles(E + S + X)

@@ -48,6 +48,24 @@ constexpr uint8_t EDGE_DEAD = 0xFE;
 __device__ __forceinline__ uint8_t first_plane(uint64_t m) {
   return (uint8_t)(m ? __builtin_ctzll(m) : EDGE_NOSPLIT);
 }
+// an edge's high plane byte d and first split plane byte m (planes of amask)
+// from its endpoint keys (pz, KW words per key)
+template <int KW>
+__device__ __forceinline__ void edge_bytes(const uint64_t* __restrict__ pz, int a, int b, const Key<KW>& amask,
+                                           uint32_t& d, uint32_t& m) {
+  Key<KW> pa, za, pb, zb;
+  tnp::pz_load(pz, a, pa, za);
+  tnp::pz_load(pz, b, pb, zb);
+  d = (uint32_t)tnp::key_high((pa ^ pb) | (za ^ zb));
+  const int f = tnp::key_first((pa ^ pb) & ~za & ~zb & amask);
+  m = f < 0 ? EDGE_NOSPLIT : (uint32_t)f;
+}
+// a plane set folded into an active-plane word (common.h act_bit)
+template <int KW>
+__device__ __forceinline__ uint64_t act_word(const Key<KW>& k) {
+  if constexpr (KW == 1) return k.w[0];
+  else return k.w[0] | (k.w[1] ? (1ull << 63) : 0ull);
+}
 constexpr int IPT = 8;                  // items per thread per tile
 constexpr int TILE = TNP_BLOCK * IPT;   // tile of a compaction pass
 // single-pass (look-back) compactions: items per thread of the split / hit
@@ -369,6 +387,7 @@ __device__ __forceinline__ int span_cells(uint64_t g, int lo[3], int n[3]) {
 }
 
 // entries per member; per-block sums of the reference's augmented rows (A)
+template <int KW>
 __global__ void __launch_bounds__(TNP_BLOCK)
 k_span_count(const int32_t* __restrict__ members, int64_t S, int64_t Mcap,
              const uint64_t* __restrict__ grid, const uint64_t* __restrict__ zero, int idx,
@@ -383,8 +402,8 @@ k_span_count(const int32_t* __restrict__ members, int64_t S, int64_t Mcap,
     int v = members[m];
     int lo[3], n[3];
     cnt[m] = span_cells(grid[v], lo, n);
-    uint64_t below = (idx >= 64) ? ~0ull : ((1ull << idx) - 1ull);
-    int kz = __popcll(zero[v] & below) + (n[0] - 1) + (n[1] - 1) + (n[2] - 1);
+    const int kz = tnp::key_pop(tnp::key_load<KW>(zero, v) & tnp::key_below<KW>(idx)) + (n[0] - 1) + (n[1] - 1) +
+                   (n[2] - 1);
     aug = 1ll << kz;
     k0 = kz == 0;
   }
@@ -546,17 +565,20 @@ k_pair_runs_lb(const uint32_t* __restrict__ key, const int32_t* __restrict__ rst
 
 // entry-aligned records of the cell-sorted (cell, member) entries (radix
 // path): the member's keys and its cell flags in that cell
+template <int KW>
 __global__ void k_entry_keys(const int32_t* __restrict__ ent_v, const uint32_t* __restrict__ ekey, int NC,
                              int64_t T, const uint64_t* __restrict__ grid,
-                             const ulonglong2* __restrict__ pz, CellEnt* __restrict__ ent) {
+                             const uint64_t* __restrict__ pz, CellEntT<KW>* __restrict__ ent) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= T) return;
   const int v = ent_v[i];
   const uint32_t c = ekey[i];
-  const ulonglong2 k = pz[v];  // pos and zero in one 16-byte gather
-  CellEnt r;
-  r.p = k.x;
-  r.z = k.y;
+  CellEntT<KW> r;
+  {
+    Key<KW> p, z;
+    tnp::pz_load(pz, v, p, z);  // pos and zero in one 16-byte gather (per word pair)
+    ent_set_keys(r, p, z);
+  }
   r.v = v;
   r.f = cell_flags(grid[v], (int)(c / ((uint32_t)NC * NC)), (int)((c / NC) % NC), (int)(c % NC));
   r.tag = 0x80000000u;  // radix path: every cell goes through k_connect
@@ -635,11 +657,12 @@ __device__ __forceinline__ void pair_row(int q, int& i, int& j) {
 // and read consecutive column entries (coalesced 32-byte records); a wave
 // walks CIPT such steps.  The chunk's pair cells (offset, id, member count,
 // first entry) sit in LDS, so locating a pair is an LDS walk.
+template <int KW>
 __global__ void __launch_bounds__(TNP_BLOCK)
 k_connect(const int64_t* __restrict__ ptoff, const int32_t* __restrict__ pcell,
           const int32_t* __restrict__ pn, const int32_t* __restrict__ pent, int NC,
-          int64_t max_tests, const int32_t* __restrict__ bcell, const CellEnt* __restrict__ ent,
-          int idx, int nb, uint64_t fmask, uint64_t* __restrict__ keys, int64_t cap,
+          int64_t max_tests, const int32_t* __restrict__ bcell, const CellEntT<KW>* __restrict__ ent,
+          int idx, int nb, Key<KW> fmask, uint64_t* __restrict__ keys, int64_t cap,
           int64_t* __restrict__ xs, int64_t* __restrict__ ctr, const int64_t* __restrict__ bstat,
           int nbstat) {
   __shared__ int64_t lds[TNP_WAVES];
@@ -668,7 +691,8 @@ k_connect(const int64_t* __restrict__ ptoff, const int32_t* __restrict__ pcell,
   const int64_t R = pk ? (pk & (PCK_CELLS - 1)) : ctr[CTR_R];
   if (TT > max_tests || ctr[CTR_BOVF] || ctr[CTR_BIG]) return;
   const int64_t nblk = (TT + CCH - 1) / CCH;
-  const uint64_t below = (idx >= 64) ? ~0ull : ((1ull << idx) - 1ull);
+  const Key<KW> below = tnp::key_below<KW>(idx);
+  const bool filt = tnp::key_any(fmask);
   int64_t n_compat = 0, n_reg = 0, n_conn = 0;
   for (int64_t b = blockIdx.x; b < nblk; b += gridDim.x) {
   const int64_t pb = b * (int64_t)CCH;
@@ -706,15 +730,16 @@ k_connect(const int64_t* __restrict__ ptoff, const int32_t* __restrict__ pcell,
       int i, j;
       pair_row(x - s_off[lc], i, j);
       const int64_t base = s_ent[lc];
-      const CellEnt eu = ent[base + i];
-      const CellEnt ev = ent[base + j];
-      PairTest t = pair_test(below, eu.f, eu.p, eu.z, ev.f, ev.p, ev.z);
+      const CellEntT<KW> eu = ent[base + i];
+      const CellEntT<KW> ev = ent[base + j];
+      const Key<KW> pu = ent_p(eu), zu = ent_z(eu), pv = ent_p(ev), zv = ent_z(ev);
+      PairTest t = pair_test(below, eu.f, pu, zu, ev.f, pv, zv);
       if (t.compat) {
         n_compat++;
         n_reg += t.regions;
         n_conn += t.emit;
         // the step's pruning drops it anyway (keep_edge): never appended
-        if (t.emit && (fmask == 0 || (((eu.p ^ ev.p) | (eu.z ^ ev.z)) & fmask) != 0)) {
+        if (t.emit && (!filt || tnp::key_any(((pu ^ pv) | (zu ^ zv)) & fmask))) {
           const uint32_t vu = (uint32_t)eu.v, vv = (uint32_t)ev.v;
           const uint32_t lo = vu < vv ? vu : vv, hi = vu < vv ? vv : vu;
           kk[ne++] = ((uint64_t)lo << nb) | hi;
@@ -744,29 +769,47 @@ k_connect(const int64_t* __restrict__ ptoff, const int32_t* __restrict__ pcell,
       iu[kb] = base + i;
       iv[kb] = base + j;
     }
-    ulonglong2 ua[CONNECT_CB], va[CONNECT_CB];
+    // a record is RW 8-byte words: the KW pos words, the KW zero words, then (v, f)
+    constexpr int RW = sizeof(CellEntT<KW>) / 8;
+    Key<KW> pua[CONNECT_CB], zua[CONNECT_CB], pva[CONNECT_CB], zva[CONNECT_CB];
     uint2 fua[CONNECT_CB], fva[CONNECT_CB];
     const ulonglong2* er = reinterpret_cast<const ulonglong2*>(ent);
     const uint2* ef = reinterpret_cast<const uint2*>(ent);
 #pragma unroll
     for (int kb = 0; kb < CONNECT_CB; ++kb) {
-      ua[kb] = er[2 * (int64_t)iu[kb]];  // (p, z)
-      fua[kb] = ef[4 * (int64_t)iu[kb] + 2];  // (v, f)
-      va[kb] = er[2 * (int64_t)iv[kb]];
-      fva[kb] = ef[4 * (int64_t)iv[kb] + 2];
+      if constexpr (KW == 1) {
+        const ulonglong2 ua = er[2 * (int64_t)iu[kb]], va = er[2 * (int64_t)iv[kb]];  // (p, z)
+        pua[kb].w[0] = ua.x;
+        zua[kb].w[0] = ua.y;
+        pva[kb].w[0] = va.x;
+        zva[kb].w[0] = va.y;
+      } else {
+        const ulonglong2 up = er[(RW / 2) * (int64_t)iu[kb]], uz = er[(RW / 2) * (int64_t)iu[kb] + 1];
+        const ulonglong2 vp = er[(RW / 2) * (int64_t)iv[kb]], vz = er[(RW / 2) * (int64_t)iv[kb] + 1];
+        pua[kb].w[0] = up.x;
+        pua[kb].w[1] = up.y;
+        zua[kb].w[0] = uz.x;
+        zua[kb].w[1] = uz.y;
+        pva[kb].w[0] = vp.x;
+        pva[kb].w[1] = vp.y;
+        zva[kb].w[0] = vz.x;
+        zva[kb].w[1] = vz.y;
+      }
+      fua[kb] = ef[RW * (int64_t)iu[kb] + 2 * KW];  // (v, f)
+      fva[kb] = ef[RW * (int64_t)iv[kb] + 2 * KW];
     }
 #pragma unroll
     for (int kb = 0; kb < CONNECT_CB; ++kb) {
       if (!ok[kb]) continue;
-      const uint64_t pu = ua[kb].x, zu = ua[kb].y;
-      const uint64_t pv = va[kb].x, zv = va[kb].y;
+      const Key<KW> pu = pua[kb], zu = zua[kb];
+      const Key<KW> pv = pva[kb], zv = zva[kb];
       PairTest t = pair_test(below, fua[kb].y, pu, zu, fva[kb].y, pv, zv);
       if (t.compat) {
         n_compat++;
         n_reg += t.regions;
         n_conn += t.emit;
         // the step's pruning drops it anyway (keep_edge): never appended
-        if (t.emit && (fmask == 0 || (((pu ^ pv) | (zu ^ zv)) & fmask) != 0)) {
+        if (t.emit && (!filt || tnp::key_any(((pu ^ pv) | (zu ^ zv)) & fmask))) {
           const uint32_t vu = fua[kb].x, vv = fva[kb].x;
           const uint32_t lo = vu < vv ? vu : vv, hi = vu < vv ? vv : vu;
           kk[ne++] = ((uint64_t)lo << nb) | hi;
@@ -871,17 +914,20 @@ __device__ __forceinline__ void fetch_edge(const EdgeSrc& s, int64_t i, int& a, 
   }
 }
 
-__device__ __forceinline__ bool keep_edge(int a, int b, uint64_t fmask, const uint64_t* pos,
+template <int KW>
+__device__ __forceinline__ bool keep_edge(int a, int b, const Key<KW>& fmask, const uint64_t* pos,
                                           const uint64_t* zero) {
-  return ((pos[a] ^ pos[b]) & fmask) != 0 || ((zero[a] ^ zero[b]) & fmask) != 0;
+  return tnp::key_any(((tnp::key_load<KW>(pos, a) ^ tnp::key_load<KW>(pos, b)) |
+                       (tnp::key_load<KW>(zero, a) ^ tnp::key_load<KW>(zero, b))) & fmask);
 }
 
 
 // emits kept edges in order, flags used vertices and ORs the next-active
 // plane mask: planes > idx on which a kept edge has non-zero opposite signs
 // (exactly the split test of that future step, subpoly.py:104-105).
+template <int KW>
 __global__ void __launch_bounds__(TNP_BLOCK)
-k_prune_emit(EdgeSrc src, int64_t N, uint64_t fmask, uint64_t amask,
+k_prune_emit(EdgeSrc src, int64_t N, Key<KW> fmask, Key<KW> amask,
              const uint64_t* __restrict__ pos, const uint64_t* __restrict__ zero,
              const int64_t* __restrict__ blkoff, int prune, int32_t* __restrict__ out,
              int32_t* __restrict__ used, int64_t* __restrict__ ctr) {
@@ -895,7 +941,7 @@ k_prune_emit(EdgeSrc src, int64_t N, uint64_t fmask, uint64_t amask,
     bool f = false;
     if (i < N) {
       fetch_edge(src, i, a, b);
-      f = !prune || keep_edge(a, b, fmask, pos, zero);
+      f = !prune || keep_edge<KW>(a, b, fmask, pos, zero);
     }
     if (prune) {
       int tot;
@@ -914,8 +960,8 @@ k_prune_emit(EdgeSrc src, int64_t N, uint64_t fmask, uint64_t amask,
         used[a] = 1;
         used[b] = 1;
       }
-      uint64_t za = zero[a], zb = zero[b];
-      act |= (pos[a] ^ pos[b]) & ~za & ~zb & amask;
+      const Key<KW> za = tnp::key_load<KW>(zero, a), zb = tnp::key_load<KW>(zero, b);
+      act |= act_word((tnp::key_load<KW>(pos, a) ^ tnp::key_load<KW>(pos, b)) & ~za & ~zb & amask);
     }
   }
   act = tnp::wave_or(act);
@@ -935,9 +981,10 @@ k_prune_emit(EdgeSrc src, int64_t N, uint64_t fmask, uint64_t amask,
 // creation, so an edge's masks change only when the edge does: the prune
 // reads them coalesced for the old edges and gathers the endpoint keys only
 // for rewired (dm == EDGE_STALE), e_new and c_new edges.
+template <int KW>
 __global__ void __launch_bounds__(TNP_BLOCK, 4)
-k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, int idx, uint64_t amask,
-           const ulonglong2* __restrict__ pz, const uint8_t* __restrict__ dm,
+k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, int idx, Key<KW> amask,
+           const uint64_t* __restrict__ pz, const uint8_t* __restrict__ dm,
            const uint8_t* __restrict__ ef, int32_t* __restrict__ out, uint8_t* __restrict__ odm,
            uint8_t* __restrict__ oef, uint8_t* __restrict__ used, int count_live,
            int64_t* __restrict__ ctr, TnpLB lb) {
@@ -999,11 +1046,8 @@ k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, int idx, uint64_t amask,
   }
 #pragma unroll
   for (int k = 0; k < LIPT; ++k) {
-    if (d[k] == EDGE_STALE) {  // new or rewired edge: masks from the endpoint keys
-      const ulonglong2 ka = pz[a[k]], kb = pz[b[k]];
-      d[k] = high_plane((ka.x ^ kb.x) | (ka.y ^ kb.y));
-      m[k] = first_plane((ka.x ^ kb.x) & ~ka.y & ~kb.y & amask);
-    }
+    if (d[k] == EDGE_STALE)  // new or rewired edge: masks from the endpoint keys
+      edge_bytes<KW>(pz, a[k], b[k], amask, d[k], m[k]);
   }
   uint64_t bal[LIPT];
   uint64_t act = 0;
@@ -1012,7 +1056,7 @@ k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, int idx, uint64_t amask,
     const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
     const bool f = (i <= last) && ((int)d[k] > idx) && d[k] != EDGE_DEAD;
     // (an old edge's first split plane is above idx: else it would have split)
-    if (f && m[k] != EDGE_NOSPLIT) act |= 1ull << m[k];
+    if (f && m[k] != EDGE_NOSPLIT) act |= tnp::act_bit((int)m[k]);
     bal[k] = __ballot(f);
     if (tnp::lane() == 0) cnt[k][tnp::wave()] = __popcll(bal[k]);
   }
@@ -1031,8 +1075,8 @@ k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, int idx, uint64_t amask,
       if (dd == EDGE_STALE) {
         int ea, eb;
         fetch_edge(src, i, ea, eb);
-        const ulonglong2 ka = pz[ea], kb = pz[eb];
-        dd = high_plane((ka.x ^ kb.x) | (ka.y ^ kb.y));
+        uint32_t mm;
+        edge_bytes<KW>(pz, ea, eb, amask, dd, mm);
       }
       c += (int)dd > idx && dd != EDGE_DEAD;
     }
@@ -1099,8 +1143,9 @@ k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, int idx, uint64_t amask,
 // reads (live flags).  Kept count per workgroup -> part[blockIdx.x] (folded
 // by the counting pass, launch_count_flags), next-active mask -> ctr.
 constexpr int LZ_IPT = 4;
+template <int KW>
 __global__ void __launch_bounds__(TNP_BLOCK)
-k_prune_lazy(EdgeSrc src, int64_t N, int idx, uint64_t amask, const ulonglong2* __restrict__ pz,
+k_prune_lazy(EdgeSrc src, int64_t N, int idx, Key<KW> amask, const uint64_t* __restrict__ pz,
              int32_t* __restrict__ edges, uint8_t* __restrict__ dm, uint8_t* __restrict__ ef,
              uint8_t* __restrict__ used, int64_t* __restrict__ part, int64_t* __restrict__ ctr) {
   __shared__ int64_t lds[TNP_WAVES];
@@ -1145,11 +1190,8 @@ k_prune_lazy(EdgeSrc src, int64_t N, int idx, uint64_t amask, const ulonglong2* 
       const int64_t i = t0 + (int64_t)k * TNP_BLOCK + threadIdx.x;
       if (i >= N) continue;
       const bool stale = d[k] == EDGE_STALE;
-      if (stale) {  // rewired or new: bytes from the endpoint keys
-        const ulonglong2 ka = pz[a[k]], kb = pz[b[k]];
-        d[k] = high_plane((ka.x ^ kb.x) | (ka.y ^ kb.y));
-        m[k] = first_plane((ka.x ^ kb.x) & ~ka.y & ~kb.y & amask);
-      }
+      if (stale)  // rewired or new: bytes from the endpoint keys
+        edge_bytes<KW>(pz, a[k], b[k], amask, d[k], m[k]);
       const bool keep = need[k] && (int)d[k] > idx;
       if (i >= src.E) e2[i] = make_int2(a[k], b[k]);
       if (i >= src.E || stale || (!keep && d[k] != EDGE_DEAD)) {
@@ -1160,7 +1202,7 @@ k_prune_lazy(EdgeSrc src, int64_t N, int idx, uint64_t amask, const ulonglong2* 
         used[a[k]] = 1;
         used[b[k]] = 1;
         ++kept;
-        if (m[k] != EDGE_NOSPLIT) act |= 1ull << m[k];
+        if (m[k] != EDGE_NOSPLIT) act |= tnp::act_bit((int)m[k]);
       }
     }
   }
@@ -1223,9 +1265,10 @@ k_ef_cache(const int32_t* __restrict__ edges, int64_t E, const uint8_t* __restri
 // masks of every edge from the endpoint keys (after a load, or when the
 // curve path rewired edges); OR of the split masks on planes of amask into
 // ctr[CTR_ACTIVE] when ctr != null
+template <int KW>
 __global__ void __launch_bounds__(TNP_BLOCK)
-k_edge_masks(const int32_t* __restrict__ edges, int64_t E, const ulonglong2* __restrict__ pz,
-             uint8_t* __restrict__ dm, uint8_t* __restrict__ ef, uint64_t amask,
+k_edge_masks(const int32_t* __restrict__ edges, int64_t E, const uint64_t* __restrict__ pz,
+             uint8_t* __restrict__ dm, uint8_t* __restrict__ ef, Key<KW> amask,
              int keep_dead, int64_t* __restrict__ ctr) {
   __shared__ uint64_t lds[TNP_WAVES];
   uint64_t act = 0;
@@ -1233,11 +1276,11 @@ k_edge_masks(const int32_t* __restrict__ edges, int64_t E, const ulonglong2* __r
        i += (int64_t)gridDim.x * blockDim.x) {
     if (keep_dead && dm[i] == EDGE_DEAD) continue;  // stays deleted
     const int2 ab = reinterpret_cast<const int2*>(edges)[i];
-    const ulonglong2 ka = pz[ab.x], kb = pz[ab.y];
-    const uint8_t f = first_plane((ka.x ^ kb.x) & ~ka.y & ~kb.y & amask);
-    dm[i] = high_plane((ka.x ^ kb.x) | (ka.y ^ kb.y));
-    ef[i] = f;
-    if (f != EDGE_NOSPLIT) act |= 1ull << f;
+    uint32_t d, f;
+    edge_bytes<KW>(pz, ab.x, ab.y, amask, d, f);
+    dm[i] = (uint8_t)d;
+    ef[i] = (uint8_t)f;
+    if (f != EDGE_NOSPLIT) act |= tnp::act_bit((int)f);
   }
   if (!ctr) return;
   act = tnp::wave_or(act);
@@ -1298,6 +1341,7 @@ __global__ void k_widen_flags(const uint8_t* __restrict__ f, int64_t n, int32_t*
   if (i < n) out[i] = f[i];
 }
 
+template <int KW>
 __global__ void k_gather_vertices(const int32_t* __restrict__ used, const int64_t* __restrict__ nid,
                                   int64_t NV, int K, int keep_from,
                                   const float* __restrict__ xyz, const float* __restrict__ pre,
@@ -1305,17 +1349,17 @@ __global__ void k_gather_vertices(const int32_t* __restrict__ used, const int64_
                                   const uint64_t* __restrict__ zero, const uint64_t* __restrict__ grid,
                                   float* __restrict__ xyz2, float* __restrict__ pre2, int64_t ld2,
                                   uint64_t* __restrict__ pos2, uint64_t* __restrict__ zero2,
-                                  uint64_t* __restrict__ grid2, ulonglong2* __restrict__ pz2) {
+                                  uint64_t* __restrict__ grid2, uint64_t* __restrict__ pz2) {
   int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= NV || !used[v]) return;
   int64_t n = nid[v];
 #pragma unroll
   for (int d = 0; d < 3; ++d) xyz2[3 * n + d] = xyz[3 * v + d];
   for (int p = keep_from; p < K; ++p) pre2[(int64_t)p * ld2 + n] = pre[(int64_t)p * ld + v];
-  const uint64_t p = pos[v], z = zero[v];
-  pos2[n] = p;
-  zero2[n] = z;
-  pz2[n] = make_ulonglong2(p, z);
+  const Key<KW> p = tnp::key_load<KW>(pos, v), z = tnp::key_load<KW>(zero, v);
+  tnp::key_store(pos2, n, p);
+  tnp::key_store(zero2, n, z);
+  tnp::pz_store(pz2, n, p, z);
   grid2[n] = grid[v];
 }
 
@@ -1419,10 +1463,14 @@ int launch_new_members(int32_t* members, int64_t S, int64_t V, hipStream_t s) {
 }
 int launch_span_count(const int32_t* members, int64_t S, int64_t M, const uint64_t* grid,
                       const uint64_t* zero, int idx, int32_t* cnt, int64_t* part, int64_t* ctr,
-                      hipStream_t s) {
+                      int kw, hipStream_t s) {
   if (M <= 0) return 0;
-  hipLaunchKernelGGL(k_span_count, dim3(tnp_grid(M)), dim3(TNP_BLOCK), 0, s, members, S, M, grid,
-                     zero, idx, cnt, part, ctr);
+  if (kw == 2)
+    hipLaunchKernelGGL(k_span_count<2>, dim3(tnp_grid(M)), dim3(TNP_BLOCK), 0, s, members, S, M, grid,
+                       zero, idx, cnt, part, ctr);
+  else
+    hipLaunchKernelGGL(k_span_count<1>, dim3(tnp_grid(M)), dim3(TNP_BLOCK), 0, s, members, S, M, grid,
+                       zero, idx, cnt, part, ctr);
   hipLaunchKernelGGL(k_sum_parts, dim3(1), dim3(TNP_BLOCK), 0, s, part, (int64_t)tnp_grid(M), ctr,
                      (int)CTR_A);
   TNP_CHECK(hipGetLastError());
@@ -1457,10 +1505,14 @@ int launch_pair_runs(const uint32_t* key, const int32_t* rstart, int64_t T, int3
   return 0;
 }
 int launch_entry_keys(const int32_t* ent_v, const uint32_t* ekey, int NC, int64_t T,
-                      const uint64_t* grid, const uint64_t* pz, CellEnt* ent, hipStream_t s) {
+                      const uint64_t* grid, const uint64_t* pz, void* ent, int kw, hipStream_t s) {
   if (T <= 0) return 0;
-  hipLaunchKernelGGL(k_entry_keys, dim3(tnp_grid(T)), dim3(TNP_BLOCK), 0, s, ent_v, ekey, NC, T, grid,
-                     reinterpret_cast<const ulonglong2*>(pz), ent);
+  if (kw == 2)
+    hipLaunchKernelGGL(k_entry_keys<2>, dim3(tnp_grid(T)), dim3(TNP_BLOCK), 0, s, ent_v, ekey, NC, T, grid, pz,
+                       static_cast<CellEntT<2>*>(ent));
+  else
+    hipLaunchKernelGGL(k_entry_keys<1>, dim3(tnp_grid(T)), dim3(TNP_BLOCK), 0, s, ent_v, ekey, NC, T, grid, pz,
+                       static_cast<CellEnt*>(ent));
   TNP_CHECK(hipGetLastError());
   return 0;
 }
@@ -1485,7 +1537,7 @@ static int resident_grid(K kernel, int slot) {
   return g;
 }
 static int connect_grid_size() {
-  return std::max(resident_grid(k_connect, 0), resident_grid(k_connect_win, 1));
+  return std::max(resident_grid(k_connect<1>, 0), resident_grid(k_connect_win, 1));
 }
 int64_t connect_chunks(int64_t TT) { return (TT + CCH - 1) / CCH; }
 int64_t connect_chunk_pairs() { return CCH; }
@@ -1498,12 +1550,21 @@ int launch_chunk_cells(const int64_t* ptoff, const int32_t* pn, int64_t rcap, in
 }
 int launch_connect(const int64_t* ptoff, const int32_t* pcell, const int32_t* pn,
                    const int32_t* pent, int NC, int64_t max_tests, const int32_t* bcell,
-                   const CellEnt* ent, int idx, int nb, uint64_t fmask, uint64_t* keys,
+                   const void* ent, int idx, int nb, int filt_last, int kw, uint64_t* keys,
                    int64_t cap, int64_t* xs, int64_t* ctr, hipStream_t s, const int64_t* bstat, int nbstat) {
   static_assert(CONNECT_CELLS >= CCH + 2, "chunk cell window");
   const int grid = connect_grid_size();
-  hipLaunchKernelGGL(k_connect, dim3(grid), dim3(TNP_BLOCK), 0, s, ptoff, pcell, pn,
-                     pent, NC, max_tests, bcell, ent, idx, nb, fmask, keys, cap, xs, ctr, bstat, nbstat);
+  // the pruning filter: planes [idx, filt_last] (filt_last < 0: none)
+  if (kw == 2)
+    hipLaunchKernelGGL(k_connect<2>, dim3(grid), dim3(TNP_BLOCK), 0, s, ptoff, pcell, pn, pent, NC, max_tests, bcell,
+                       static_cast<const CellEntT<2>*>(ent), idx, nb,
+                       filt_last >= 0 ? tnp::key_range<2>(idx, filt_last) : tnp::key_zero<2>(), keys, cap, xs, ctr,
+                       bstat, nbstat);
+  else
+    hipLaunchKernelGGL(k_connect<1>, dim3(grid), dim3(TNP_BLOCK), 0, s, ptoff, pcell, pn, pent, NC, max_tests, bcell,
+                       static_cast<const CellEnt*>(ent), idx, nb,
+                       filt_last >= 0 ? tnp::key_range<1>(idx, filt_last) : tnp::key_zero<1>(), keys, cap, xs, ctr,
+                       bstat, nbstat);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
@@ -1533,6 +1594,13 @@ uint64_t prune_mask(int idx, int last_plane) {
   if (last_plane < 63) fmask &= (1ull << (last_plane + 1)) - 1ull;
   return fmask;
 }
+// the planes [lo, last_plane] (lo clamped at 0) as a KW-word key
+template <int KW>
+static Key<KW> plane_mask(int lo, int last_plane) {
+  return tnp::key_range<KW>(lo < 0 ? 0 : lo, last_plane);
+}
+// the key words of a net whose last plane is last_plane
+static int kw_of(int last_plane) { return last_plane + 1 <= 63 ? 1 : 2; }
 int launch_prune(bool emit, const int32_t* edges, int64_t E, const int32_t* sb, int64_t S,
                  int64_t V, const uint64_t* ckeys, int nb, int64_t X, int idx,
                  int prune, int last_plane, const uint64_t* pos, const uint64_t* zero,
@@ -1541,13 +1609,16 @@ int launch_prune(bool emit, const int32_t* edges, int64_t E, const int32_t* sb, 
   EdgeSrc src{edges, E, sb, S, V, ckeys, nb, X};
   int64_t N = E + S + X;
   if (N <= 0) return 0;
-  uint64_t fmask = prune_mask(idx, last_plane);
-  uint64_t amask = (idx + 1 >= 64) ? 0ull : (~0ull << (idx + 1));
-  if (last_plane < 63) amask &= (1ull << (last_plane + 1)) - 1ull;
   (void)emit;
   (void)blk;
-  hipLaunchKernelGGL(k_prune_emit, dim3((unsigned)step_tiles(N)), dim3(TNP_BLOCK), 0, s, src, N,
-                     fmask, amask, pos, zero, blkoff, prune, out, used, ctr);
+  if (kw_of(last_plane) == 2)
+    hipLaunchKernelGGL(k_prune_emit<2>, dim3((unsigned)step_tiles(N)), dim3(TNP_BLOCK), 0, s, src, N,
+                       plane_mask<2>(idx, last_plane), plane_mask<2>(idx + 1, last_plane), pos, zero, blkoff, prune,
+                       out, used, ctr);
+  else
+    hipLaunchKernelGGL(k_prune_emit<1>, dim3((unsigned)step_tiles(N)), dim3(TNP_BLOCK), 0, s, src, N,
+                       plane_mask<1>(idx, last_plane), plane_mask<1>(idx + 1, last_plane), pos, zero, blkoff, prune,
+                       out, used, ctr);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
@@ -1562,14 +1633,15 @@ int launch_prune_lb(const int32_t* edges, int64_t E, const int32_t* sb, int64_t 
     TNP_CHECK(hipMemsetAsync(ctr + CTR_E, 0, sizeof(int64_t), s));
     return 0;
   }
-  uint64_t fmask = prune_mask(idx, last_plane);
-  uint64_t amask = (idx + 1 >= 64) ? 0ull : (~0ull << (idx + 1));
-  if (last_plane < 63) amask &= (1ull << (last_plane + 1)) - 1ull;
   const int64_t tiles = lb_tiles(N);
-  (void)fmask;
-  hipLaunchKernelGGL(k_prune_lb, dim3((unsigned)tiles), dim3(TNP_BLOCK), 0, s, src, N, tiles, idx,
-                     amask, reinterpret_cast<const ulonglong2*>(pz), dm, ef, out, odm, oef, used,
-                     count_live ? 1 : 0, ctr, lb);
+  if (kw_of(last_plane) == 2)
+    hipLaunchKernelGGL(k_prune_lb<2>, dim3((unsigned)tiles), dim3(TNP_BLOCK), 0, s, src, N, tiles, idx,
+                       plane_mask<2>(idx + 1, last_plane), pz, dm, ef, out, odm, oef, used, count_live ? 1 : 0, ctr,
+                       lb);
+  else
+    hipLaunchKernelGGL(k_prune_lb<1>, dim3((unsigned)tiles), dim3(TNP_BLOCK), 0, s, src, N, tiles, idx,
+                       plane_mask<1>(idx + 1, last_plane), pz, dm, ef, out, odm, oef, used, count_live ? 1 : 0, ctr,
+                       lb);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
@@ -1586,11 +1658,13 @@ int launch_prune_lazy(int32_t* edges, int64_t E, const int32_t* sb, int64_t S, i
                       uint8_t* used, int64_t* part, int64_t* ctr, hipStream_t s) {
   EdgeSrc src{edges, E, sb, S, V, ckeys, nb, X};
   const int64_t N = E + S + X;
-  uint64_t amask = (idx + 1 >= 64) ? 0ull : (~0ull << (idx + 1));
-  if (last_plane < 63) amask &= (1ull << (last_plane + 1)) - 1ull;
   const int g = prune_lazy_blocks(N);
-  hipLaunchKernelGGL(k_prune_lazy, dim3(g), dim3(TNP_BLOCK), 0, s, src, N, idx, amask,
-                     reinterpret_cast<const ulonglong2*>(pz), edges, dm, ef, used, part, ctr);
+  if (kw_of(last_plane) == 2)
+    hipLaunchKernelGGL(k_prune_lazy<2>, dim3(g), dim3(TNP_BLOCK), 0, s, src, N, idx,
+                       plane_mask<2>(idx + 1, last_plane), pz, edges, dm, ef, used, part, ctr);
+  else
+    hipLaunchKernelGGL(k_prune_lazy<1>, dim3(g), dim3(TNP_BLOCK), 0, s, src, N, idx,
+                       plane_mask<1>(idx + 1, last_plane), pz, edges, dm, ef, used, part, ctr);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
@@ -1628,11 +1702,13 @@ int launch_count_flags(const uint8_t* f, int64_t n, int64_t* ctr, int slot, hipS
 int launch_edge_masks(const int32_t* edges, int64_t E, const uint64_t* pz, uint8_t* dm,
                       uint8_t* sm, int from, int last_plane, bool keep_dead, int64_t* ctr, hipStream_t s) {
   if (E <= 0) return 0;
-  uint64_t amask = (from >= 64) ? 0ull : (~0ull << from);
-  if (last_plane < 63) amask &= (1ull << (last_plane + 1)) - 1ull;
   const unsigned g = (unsigned)std::min<int64_t>(4096, tnp_grid(E));
-  hipLaunchKernelGGL(k_edge_masks, dim3(g), dim3(TNP_BLOCK), 0, s, edges, E,
-                     reinterpret_cast<const ulonglong2*>(pz), dm, sm, amask, keep_dead ? 1 : 0, ctr);
+  if (kw_of(last_plane) == 2)
+    hipLaunchKernelGGL(k_edge_masks<2>, dim3(g), dim3(TNP_BLOCK), 0, s, edges, E, pz, dm, sm,
+                       plane_mask<2>(from, last_plane), keep_dead ? 1 : 0, ctr);
+  else
+    hipLaunchKernelGGL(k_edge_masks<1>, dim3(g), dim3(TNP_BLOCK), 0, s, edges, E, pz, dm, sm,
+                       plane_mask<1>(from, last_plane), keep_dead ? 1 : 0, ctr);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
@@ -1642,9 +1718,12 @@ int launch_gather_vertices(const int32_t* used, const int64_t* nid, int64_t NV, 
                            float* xyz2, float* pre2, int64_t ld2, uint64_t* pos2, uint64_t* zero2,
                            uint64_t* grid2, uint64_t* pz2, hipStream_t s) {
   if (NV <= 0) return 0;
-  hipLaunchKernelGGL(k_gather_vertices, dim3(tnp_grid(NV)), dim3(TNP_BLOCK), 0, s, used, nid, NV,
-                     K, keep_from, xyz, pre, ld, pos, zero, grid, xyz2, pre2, ld2, pos2, zero2,
-                     grid2, reinterpret_cast<ulonglong2*>(pz2));
+  if (kw_of(K - 1) == 2)
+    hipLaunchKernelGGL(k_gather_vertices<2>, dim3(tnp_grid(NV)), dim3(TNP_BLOCK), 0, s, used, nid, NV,
+                       K, keep_from, xyz, pre, ld, pos, zero, grid, xyz2, pre2, ld2, pos2, zero2, grid2, pz2);
+  else
+    hipLaunchKernelGGL(k_gather_vertices<1>, dim3(tnp_grid(NV)), dim3(TNP_BLOCK), 0, s, used, nid, NV,
+                       K, keep_from, xyz, pre, ld, pos, zero, grid, xyz2, pre2, ld2, pos2, zero2, grid2, pz2);
   TNP_CHECK(hipGetLastError());
   return 0;
 }

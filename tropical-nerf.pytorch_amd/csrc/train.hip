@@ -155,7 +155,7 @@ __global__ void k_fill_u32(uint32_t* __restrict__ p, int64_t n, uint32_t v) {
 }  // namespace
 
 static int train_net_ok(const NetDev& net, const char* what) {
-  if (!net_supported(net) || net.tied) {
+  if (!net_supported_full(net) || net.tied) {
     tnp_set_error("%s: net shape (levels=%d, layers=%d, hidden=%d) not instantiated", what, net.n_levels,
                   net.num_layers, net.num_hidden);
     return -1;
