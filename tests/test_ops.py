@@ -92,7 +92,8 @@ def test_subpoly_step_op_reproduces_reference_steps(cuda):
     args = ops.net_args(net)
     V = torch.from_numpy(lattice_vertices(d["marks"])).to(cuda)
     E = torch.from_numpy(lattice_edges(int(d["lattice_n"]))).to(cuda)
-    o = torch.cat(net(V, gather=True)[1], -1)
+    with torch.no_grad():  # (Net.forward is differentiable: no graph for the cache)
+        o = torch.cat(net(V, gather=True)[1], -1)
     for step, idx in enumerate(d["step_idx"][:12]):
         E_in = E.clone()
         V2, E2, o2 = torch.ops.tropical_hip.subpoly_step(V, E, o, *args, int(idx), True, True)
