@@ -377,3 +377,30 @@ def test_wide_net_refuses_curve_and_shards(cuda, name):
             eng.split(0)
     finally:
         eng.set_curve(False)
+
+
+@pytest.mark.parametrize("name", ["small_sphere", "synth32"])
+def test_row_order_fast_path_is_the_full_sort(cuda, name, monkeypatch):
+    """Faces F4: rows without an exact key tie are ordered in registers
+    (faces.hip k_row_fast); TNP_ROW_SORT_FULL=1 runs the padded introsort on
+    every row.  Both give the same triangles and float faces, bitwise."""
+    from tropical._engine import engine_for
+    d = load(name)
+    net = product_net(d, cuda)
+    eng = engine_for(net)
+    outs = []
+    for full in ("0", "1"):
+        monkeypatch.setenv("TNP_ROW_SORT_FULL", full)
+        if d["kind"] == "lattice":
+            eng.lattice(keep_all=True)
+        else:
+            eng.skeleton(128, 1.2)
+            v0, e0, _ = eng.export()
+            eng.load(v0, e0, keep_all=True)
+        engine_steps(eng, record=False)
+        eng.surface()
+        tri, fc = eng.faces()
+        outs.append((tri.cpu().numpy(), fc.cpu().numpy()))
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])
+    assert sha(outs[0][0]) == str(d["sha_tri"]) and sha(outs[0][1]) == str(d["sha_faces"])

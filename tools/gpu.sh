@@ -18,6 +18,9 @@
 #   prof[:G]           rocprofv3 --kernel-trace --stats of a short bench
 #   proffinish         rocprofv3 --kernel-trace --stats of tools/finish64.py
 #   pmc:<counters>     one rocprofv3 --pmc pass (counters comma-separated) of a short bench
+#   pmcsession         tools/pmc_session.sh (kernel trace + the four counter passes -> pmc_table.json)
+#   rehearsal[:N]      bench at 161^3 on one rank, then N (default 2) gloo ranks sharing the GPU
+#   diag:<cases>       tools/descend_diag.py on descend fixtures (comma-separated)
 #   env:<VAR=val>      export a variable for the following steps
 # Logs: gpurun_out/<tag>_<n>_<step>.log, summary gpurun_out/<tag>_session.log
 # (tag = $TNP_TAG, default "s").
@@ -62,6 +65,12 @@ for step in "$@"; do
             -- python bench.py --marks "${a1:-128}" --steps 2 --warmup 1 --no-cpu ;;
     pmc) run 120 0 rocprofv3 --pmc ${a1//,/ } -d "gpurun_out/${tag}_pmc_${a1//,/_}" -o run --output-format csv \
             -- python bench.py --marks "${a2:-128}" --steps 1 --warmup 1 --no-cpu ;;
+    pmcsession) run 900 0 bash tools/pmc_session.sh ;;
+    rehearsal) run 300 0 python -u bench.py --marks 161 --steps 2 --warmup 1 --no-cpu &&
+               run 400 0 env TNP_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 \
+                 --nproc-per-node "${a1:-2}" --master-addr 127.0.0.1 --master-port 29517 bench.py \
+                 --gpus "${a1:-2}" --steps 2 --warmup 1 --no-cpu ;;
+    diag) run 240 0 python -u tools/descend_diag.py ${a1//,/ } ;;
     env) export "$a1"; echo "== env $a1" >> "$sess" ;;
     *) echo "unknown step $step" >> "$sess"; exit 2 ;;
   esac

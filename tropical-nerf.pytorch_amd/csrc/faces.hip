@@ -26,6 +26,7 @@
 #include "faces.h"
 #include "kernels.h"
 #include <algorithm>
+#include <cstdlib>
 
 namespace {
 
@@ -463,9 +464,9 @@ __global__ void k_row_score(int64_t F, const int32_t* __restrict__ frow, const u
                             const int64_t* __restrict__ roff, const int32_t* __restrict__ rcnt, int M,
                             const float* __restrict__ xyz, const float* __restrict__ nrm, int quirk3,
                             float* __restrict__ skey, int32_t* __restrict__ sidx, int32_t* __restrict__ cnt_all,
-                            int32_t* __restrict__ cnt_nz) {
+                            int32_t* __restrict__ cnt_nz, const int32_t* __restrict__ slow) {
   int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= F) return;
+  if (f >= F || (slow && !slow[f])) return;
   const int r = frow[f];
   const int c = rcnt[r];
   const int64_t off = roff[r];
@@ -527,6 +528,81 @@ __global__ void k_row_score(int64_t F, const int32_t* __restrict__ frow, const u
     key[i] = __fadd_rn(__fmul_rn(cs, dd >= 0.f ? 1.f : -1.f), dd < 0.f ? 2.f : 0.f);
     idx[i] = i;
   }
+  cnt_all[f] = c;
+  cnt_nz[f] = nz;
+}
+
+// F4 fast path.  The pads of a padded row are all the zero point, so they
+// share one key; the sort is unstable, but when no two of the c member keys
+// and the pad key are equal (and none is NaN), every member's place is its
+// rank in descending key order whatever the introsort does with the pads --
+// so such a row is ordered in registers, without the padded M-entry sort.
+// Rows with an exact tie (or more than FAST_MAX members, or the 3-row cross
+// quirk) are flagged for k_row_score + k_row_sort.  Same keys as k_row_score.
+constexpr int FAST_MAX = 16;
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_row_fast(int64_t F, const int32_t* __restrict__ frow, const uint64_t* __restrict__ mem,
+           const int64_t* __restrict__ roff, const int32_t* __restrict__ rcnt, int M,
+           const float* __restrict__ xyz, const float* __restrict__ nrm, int32_t* __restrict__ ordv,
+           int32_t* __restrict__ cnt_all, int32_t* __restrict__ cnt_nz, int32_t* __restrict__ slow) {
+  int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= F) return;
+  const int r = frow[f];
+  const int c = rcnt[r];
+  const int64_t off = roff[r];
+  if (c > FAST_MAX) {
+    slow[f] = 1;
+    return;
+  }
+  float cen[3];
+  row_centroid(mem, off, c, M, xyz, cen);
+  const int v0 = row_v(mem, off, 0);
+  float u0[3];
+#pragma unroll
+  for (int d = 0; d < 3; ++d) u0[d] = __fsub_rn(xyz[3 * (int64_t)v0 + d], cen[d]);
+  const float n[3] = {nrm[3 * f], nrm[3 * f + 1], nrm[3 * f + 2]};
+  auto score = [&](const float p[3]) {
+    const float u[3] = {__fsub_rn(p[0], cen[0]), __fsub_rn(p[1], cen[1]), __fsub_rn(p[2], cen[2])};
+    float cr[3];
+    cross3(u0, u, cr);
+    const float dd = dot3_bmm(cr, n);
+    const float cs = cosine(u0, u);
+    return __fadd_rn(__fmul_rn(cs, dd >= 0.f ? 1.f : -1.f), dd < 0.f ? 2.f : 0.f);
+  };
+  float key[FAST_MAX];
+  int id[FAST_MAX];
+  int nz = 0;
+  bool tie = false;
+  for (int i = 0; i < c; ++i) {
+    const int v = row_v(mem, off, i);
+    const float p[3] = {xyz[3 * (int64_t)v], xyz[3 * (int64_t)v + 1], xyz[3 * (int64_t)v + 2]};
+    nz += nonzero3(p);
+    key[i] = score(p);
+    id[i] = v;
+    tie |= isnan(key[i]);
+  }
+  if (c < M) {
+    const float z[3] = {0.f, 0.f, 0.f};
+    const float kp = score(z);
+    tie |= isnan(kp);
+    for (int i = 0; i < c; ++i) tie |= key[i] == kp;
+  }
+  for (int i = 1; i < c && !tie; ++i) {  // insertion sort, descending; an equal key is a tie
+    const float k = key[i];
+    const int v = id[i];
+    int j = i - 1;
+    while (j >= 0 && key[j] < k) {
+      key[j + 1] = key[j];
+      id[j + 1] = id[j];
+      --j;
+    }
+    tie |= j >= 0 && key[j] == k;
+    key[j + 1] = k;
+    id[j + 1] = v;
+  }
+  slow[f] = tie ? 1 : 0;
+  if (tie) return;
+  for (int i = 0; i < c; ++i) ordv[off + i] = id[i];
   cnt_all[f] = c;
   cnt_nz[f] = nz;
 }
@@ -671,12 +747,13 @@ __device__ void std_sort(KV* first, KV* last) {
 }
 
 // F4b: sort each padded row and write the members' ids in sorted order
+// (slow != null: only the rows k_row_fast left to this path)
 __global__ void k_row_sort(int64_t F, const int32_t* __restrict__ frow, const uint64_t* __restrict__ mem,
                            const int64_t* __restrict__ roff, const int32_t* __restrict__ rcnt, int M,
                            KV* __restrict__ kv, const float* __restrict__ skey, const int32_t* __restrict__ sidx,
-                           int32_t* __restrict__ ordv) {
+                           int32_t* __restrict__ ordv, const int32_t* __restrict__ slow) {
   int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= F) return;
+  if (f >= F || (slow && !slow[f])) return;
   const int r = frow[f];
   const int c = rcnt[r];
   const int64_t off = roff[r];
@@ -828,7 +905,7 @@ int launch_row_mean(int64_t F, const int32_t* frow, const uint64_t* mem, const i
   TNP_CHECK(hipGetLastError());
   return 0;
 }
-size_t row_order_scratch(int64_t F, int M) { return (size_t)F * M * (sizeof(float) + 4 + sizeof(KV)); }
+size_t row_order_scratch(int64_t F, int M) { return (size_t)F * M * (sizeof(float) + 4 + sizeof(KV)) + F * 4; }
 
 int launch_row_order(int64_t F, const int32_t* frow, const uint64_t* mem, const int64_t* roff,
                      const int32_t* rcnt, int M, const float* xyz, const float* nrm, int quirk3, void* scratch,
@@ -837,10 +914,17 @@ int launch_row_order(int64_t F, const int32_t* frow, const uint64_t* mem, const 
   float* skey = static_cast<float*>(scratch);
   int32_t* sidx = reinterpret_cast<int32_t*>(skey + F * (int64_t)M);
   KV* kv = reinterpret_cast<KV*>(sidx + F * (int64_t)M);
+  // the 3-row quirk (and TNP_ROW_SORT_FULL=1, tests) sorts every padded row
+  const char* full = getenv("TNP_ROW_SORT_FULL");
+  const bool s_full = full && full[0] == '1';
+  int32_t* slow = (quirk3 || s_full) ? nullptr : reinterpret_cast<int32_t*>(kv + F * (int64_t)M);
+  if (slow)
+    hipLaunchKernelGGL(k_row_fast, dim3(tnp_grid(F)), dim3(TNP_BLOCK), 0, s, F, frow, mem, roff, rcnt, M, xyz, nrm,
+                       ordv, cnt_all, cnt_nz, slow);
   hipLaunchKernelGGL(k_row_score, dim3(tnp_grid(F)), dim3(TNP_BLOCK), 0, s, F, frow, mem, roff, rcnt, M, xyz,
-                     nrm, quirk3, skey, sidx, cnt_all, cnt_nz);
+                     nrm, quirk3, skey, sidx, cnt_all, cnt_nz, slow);
   hipLaunchKernelGGL(k_row_sort, dim3(tnp_grid(F)), dim3(TNP_BLOCK), 0, s, F, frow, mem, roff, rcnt, M, kv, skey,
-                     sidx, ordv);
+                     sidx, ordv, slow);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
