@@ -200,6 +200,20 @@ def cpu_baseline(G: int, seed: int, threads: int):
     return S / dt, S, dt
 
 
+def halo_stats(G: int, world: int, halo: int) -> dict:
+    """Per-rank redundancy of the x-slab decomposition: the cells a rank
+    extracts beyond the ones it owns (its halo), as a fraction of its slab."""
+    if world <= 1:
+        return {}
+    from tropical.distributed import slab_cuts, slab_marks
+    cuts = slab_cuts(G, world)
+    fr = []
+    for r in range(world):
+        x0, x1 = slab_marks(cuts, r, halo)
+        fr.append(1.0 - (cuts[r + 1] - cuts[r]) / max(x1 - x0, 1))
+    return {"redundant_cell_frac_max": round(max(fr), 4), "redundant_cell_frac_mean": round(sum(fr) / world, 4)}
+
+
 def gpu_same_workload(G: int, seed: int, dev, reps: int = 5):
     """The engine on the CPU baseline's workload (the whole G^3 lattice of
     the same net): splits per pass and the median pass time."""
@@ -658,7 +672,7 @@ def main():
                                    f"{net.K} hyperplane steps", "marks_per_axis": G,
                        "lattice_vertices": G ** 3, "edges_subdivided_per_pass": int(per_pass),
                        "seed": args.seed, "table_amp": 0.1, "parallelism": f"xslab{world}",
-                       "halo_cells": halo},
+                       "halo_cells": halo, **halo_stats(G, world, halo)},
             "roofline": roof,
             "loop_model_bytes_per_pass": int(bytes_tot / args.steps),
             "loop_model_gbs": round(loop_gbs, 1),

@@ -765,17 +765,34 @@ __global__ void k_row_sort(int64_t F, const int32_t* __restrict__ frow, const ui
     if (a[i].v < c) ordv[off + j++] = row_v(mem, off, a[i].v);
 }
 
+// the largest v over the block (every thread calls it; two barriers)
+__device__ __forceinline__ int block_max(int v, int* lds) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+  if (tnp::lane() == 0) lds[tnp::wave()] = v;
+  __syncthreads();
+  int m = lds[0];
+#pragma unroll
+  for (int w = 1; w < TNP_WAVES; ++w) m = max(m, lds[w]);
+  __syncthreads();
+  return m;
+}
+
 // F5: per block of rows, how many rows have c >= t+3, t-major layout
 __global__ void __launch_bounds__(TNP_BLOCK)
 k_fan_hist(int64_t F, const int32_t* __restrict__ cnt, int T, int64_t nb, int32_t* __restrict__ hist) {
   __shared__ int lds[TNP_WAVES];
   int64_t f = (int64_t)blockIdx.x * TNP_BLOCK + threadIdx.x;
   int c = f < F ? cnt[f] : 0;
-  for (int t = 0; t < T; ++t) {
+  // fan positions past this block's largest row hold none of its rows (T is
+  // the largest row over all rows): ranked only up to the block's own
+  const int tb = min(T, block_max(c, lds) - 2);
+  for (int t = 0; t < tb; ++t) {
     int tot;
     (void)tnp::block_rank(c >= t + 3, lds, tot);
     if (threadIdx.x == 0) hist[(int64_t)t * nb + blockIdx.x] = tot;
   }
+  for (int t = max(tb, 0) + threadIdx.x; t < T; t += TNP_BLOCK) hist[(int64_t)t * nb + blockIdx.x] = 0;
 }
 
 // i-th ordered member with a non-zero position (the float faces' mask m)
@@ -803,7 +820,8 @@ k_fan_emit(int64_t F, const int32_t* __restrict__ frow, const int32_t* __restric
     rc = rcnt[r];
     a = ordv + roff[r];
   }
-  for (int t = 0; t < T; ++t) {
+  const int tb = min(T, block_max(c, lds) - 2);  // (as k_fan_hist)
+  for (int t = 0; t < tb; ++t) {
     bool on = c >= t + 3;
     int tot;
     int rk = tnp::block_rank(on, lds, tot);
