@@ -821,6 +821,10 @@ k_fan_emit(int64_t F, const int32_t* __restrict__ frow, const int32_t* __restric
     a = ordv + roff[r];
   }
   const int tb = min(T, block_max(c, lds) - 2);  // (as k_fan_hist)
+  // floats: c counts the row's members off the origin; a row with none at
+  // the origin (c == rc, all but a vertex exactly at 0) takes its i-th
+  // member directly instead of scanning the row for it per triangle
+  const bool clean = c == rc;
   for (int t = 0; t < tb; ++t) {
     bool on = c >= t + 3;
     int tot;
@@ -834,7 +838,7 @@ k_fan_emit(int64_t F, const int32_t* __restrict__ frow, const int32_t* __restric
     } else {
       const int ids[3] = {0, t + 1, t + 2};
       for (int q = 0; q < 3; ++q) {
-        int v = nz_member(a, rc, ids[q], xyz);
+        int v = clean ? a[ids[q]] : nz_member(a, rc, ids[q], xyz);
         for (int d = 0; d < 3; ++d) fc[9 * at + 3 * q + d] = xyz[3 * (int64_t)v + d];
       }
     }
