@@ -200,18 +200,30 @@ def cpu_baseline(G: int, seed: int, threads: int):
     return S / dt, S, dt
 
 
-def halo_stats(G: int, world: int, halo: int) -> dict:
-    """Per-rank redundancy of the x-slab decomposition: the cells a rank
-    extracts beyond the ones it owns (its halo), as a fraction of its slab."""
-    if world <= 1:
+def parallelism(part) -> str:
+    if part is None:
+        return "single"
+    if part.dims[1] == part.dims[2] == 1:
+        return f"xslab{part.world}"
+    return "blocks" + "x".join(str(p) for p in part.dims)
+
+
+def shard_text(part) -> str:
+    if part is None:
+        return "one GPU"
+    if part.dims[1] == part.dims[2] == 1:
+        return "x-slab per GPU"
+    return "{}x{}x{} blocks, one per GPU".format(*part.dims)
+
+
+def halo_stats(part, halo: int) -> dict:
+    """Per-rank redundancy of the decomposition (tropical.distributed.Blocks):
+    the cells a rank extracts beyond the ones it owns (its halo), as a
+    fraction of the cells it extracts."""
+    if part is None or part.world <= 1:
         return {}
-    from tropical.distributed import slab_cuts, slab_marks
-    cuts = slab_cuts(G, world)
-    fr = []
-    for r in range(world):
-        x0, x1 = slab_marks(cuts, r, halo)
-        fr.append(1.0 - (cuts[r + 1] - cuts[r]) / max(x1 - x0, 1))
-    return {"redundant_cell_frac_max": round(max(fr), 4), "redundant_cell_frac_mean": round(sum(fr) / world, 4)}
+    fr = [part.redundant_frac(r, halo) for r in range(part.world)]
+    return {"redundant_cell_frac_max": round(max(fr), 4), "redundant_cell_frac_mean": round(sum(fr) / part.world, 4)}
 
 
 def gpu_same_workload(G: int, seed: int, dev, reps: int = 5):
@@ -511,29 +523,35 @@ def main():
     from tropical._engine import engine_for
     G = args.marks if world == 1 else int(round(args.marks * world ** (1.0 / 3.0)))
     net = make_net(G, dev, args.seed)
-    from tropical.distributed import HALOS, halo_check, slab_cuts, slab_marks
-    cuts = slab_cuts(G, world)
+    from tropical.distributed import HALOS, Blocks, block_dims, halo_check, slab_cuts
+    # N > 1: one block of the lattice per rank (2 x 2 x 2 at N = 8; x-slabs
+    # with TNP_SHARD=xslab) -- blocks have the smallest cut faces, so the
+    # smallest halo
+    part = None
+    if world > 1:
+        part = (Blocks.xslabs(slab_cuts(G, world)) if os.environ.get("TNP_SHARD") == "xslab"
+                else Blocks(G, block_dims(world)))
     eng = engine_for(net)
     if world > 1:
-        eng.set_owned(cuts[rank], cuts[rank + 1])  # halo splits -> S_dup
+        eng.set_owned_box(*part.owned(rank))  # halo splits -> S_dup
     eng.set_shards(world)
-    slab = [0, G - 1]
+    box = [[0, 0, 0], [G - 1, G - 1, G - 1]]
 
     def one_pass():
         stats = []
-        eng.lattice(*slab)
+        eng.lattice_box(*box)
         eng.run_steps(stats, coll)
         return stats
 
     halo = 0
     if world > 1:
-        # this rank's cells + a halo each side, as wide as halo_check needs
-        # (untimed: one pass per width tried)
+        # this rank's cells + a halo beyond every cut face, as wide as
+        # halo_check needs (untimed: one pass per width tried)
         for k, halo in enumerate(HALOS):
-            slab[:] = slab_marks(cuts, rank, halo)
+            box[:] = part.box(rank, halo)
             one_pass()
             Vl, El, _ = eng.export()
-            ok = halo_check(Vl.to(comm_dev), El.to(comm_dev), net.enc.marks, cuts,
+            ok = halo_check(Vl.to(comm_dev), El.to(comm_dev), net.enc.marks, part,
                             raise_=k == len(HALOS) - 1)
             if ok is not None:
                 break
@@ -583,8 +601,8 @@ def main():
         # RCCL all_gathers), untimed
         from tropical.distributed import stitch
         Vl, El, _ = eng.export()
-        halo_check(Vl.to(comm_dev), El.to(comm_dev), net.enc.marks, cuts)
-        owned, first, gE, own, keep = stitch(Vl.to(comm_dev), El.to(comm_dev), net.enc.marks, cuts,
+        halo_check(Vl.to(comm_dev), El.to(comm_dev), net.enc.marks, part)
+        owned, first, gE, own, keep = stitch(Vl.to(comm_dev), El.to(comm_dev), net.enc.marks, part,
                                              masks=True)
         hv, he = complex_hash(Vl.to(comm_dev), El.to(comm_dev), own, keep)
         tot = torch.tensor([owned.shape[0], gE.shape[0], hv, he], device=comm_dev, dtype=torch.int64)
@@ -668,11 +686,11 @@ def main():
             "ms_per_step": round(dt_max / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": f"synthetic random-weight trilinear net, {G}^3 initial lattice "
-                                   f"({'x-slab per GPU' if world > 1 else 'one GPU'}), flat path, all "
+                                   f"({shard_text(part)}), flat path, all "
                                    f"{net.K} hyperplane steps", "marks_per_axis": G,
                        "lattice_vertices": G ** 3, "edges_subdivided_per_pass": int(per_pass),
-                       "seed": args.seed, "table_amp": 0.1, "parallelism": f"xslab{world}",
-                       "halo_cells": halo, **halo_stats(G, world, halo)},
+                       "seed": args.seed, "table_amp": 0.1, "parallelism": parallelism(part),
+                       "halo_cells": halo, **halo_stats(part, halo)},
             "roofline": roof,
             "loop_model_bytes_per_pass": int(bytes_tot / args.steps),
             "loop_model_gbs": round(loop_gbs, 1),

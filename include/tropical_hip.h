@@ -140,6 +140,12 @@ int tnp_engine_skeleton_mode(tnp_engine* eng, int unit, float size, int mode, vo
  * (tropical.py:103-109) with vertex ids (i-x0)*N^2 + j*N + k. */
 int tnp_engine_lattice(tnp_engine* eng, int x0, int x1, int keep_all_planes,
                        void* stream, int64_t* V, int64_t* E);
+/* The same lattice restricted to the box of mark indices [lo[d], hi[d]] per
+ * axis (a block of a sharded lattice): vertex ids
+ * (i-lo0)*ny*nz + (j-lo1)*nz + (k-lo2), edges in the same x / y / z order;
+ * sets the span (tnp_engine_set_span) to the box. */
+int tnp_engine_lattice_box(tnp_engine* eng, const int32_t* lo, const int32_t* hi, int keep_all_planes,
+                           void* stream, int64_t* V, int64_t* E);
 
 /* Bit p (p >= from) set iff some edge has endpoints with non-zero opposite
  * eps-signs on plane p, i.e. subpoly_ at idx=p would split (subpoly.py:104-110). */
@@ -240,6 +246,11 @@ int tnp_engine_set_strict(tnp_engine* eng, int on);
  * counted in tnp_step_stats.S_dup so the global split count counts each
  * split once.  lo > hi (default) = everything owned.  Flat path only. */
 int tnp_engine_set_owned(tnp_engine* eng, int lo, int hi);
+/* The same for a block of the mark grid (shards cut along several axes):
+ * along axis d the shard owns the planes (lo[d], hi[d]] (plane 0 by the
+ * shard with lo[d] == 0) and the cells between them; lo[d] > hi[d]: the
+ * axis is not cut.  A vertex is owned iff it is owned along every cut axis. */
+int tnp_engine_set_owned_box(tnp_engine* eng, const int32_t* lo, const int32_t* hi);
 
 /* subpoly(net, d, size, eps) / subpoly_(..., eps, ...) with eps != Net.eps
  * (subpoly.py:24, 90): the following steps take the sign test, split point,
@@ -259,6 +270,10 @@ int tnp_engine_set_eps(tnp_engine* eng, float eps);
  * Performance only: the results do not depend on it.  No reference
  * counterpart (multi-GPU sharding). */
 int tnp_engine_set_xspan(tnp_engine* eng, int x0, int x1);
+/* Per axis: the complex lies between the mark planes lo[d] and hi[d]
+ * (hi[d] < lo[d]: anywhere along d) -- a block with its halo; x-slabs are
+ * tnp_engine_set_xspan. */
+int tnp_engine_set_span(tnp_engine* eng, const int32_t* lo, const int32_t* hi);
 
 /* world > 1: this engine holds one x-slab of a complex sharded over `world`
  * devices.  A step the other shards split may leave this one without any

@@ -39,27 +39,28 @@ def _free_port():
     return port
 
 
-def _sharded_lattice(net, rank, world, coll, stats):
-    """This rank's x-slab of the net's full lattice, with the narrowest halo
-    of HALOS that halo_check accepts (bench.py's N > 1 path)."""
+def _sharded_lattice(net, rank, world, coll, stats, blocks=False):
+    """This rank's x-slab (blocks: its block of the most cubic split,
+    bench.py's N > 1 path) of the net's full lattice, with the narrowest halo
+    of HALOS that halo_check accepts."""
     from tropical import distributed as D
     from tropical._engine import engine_for
     n = int(net.enc.marks.shape[0])
-    cuts = D.slab_cuts(n, world)
+    part = D.Blocks(n, D.block_dims(world)) if blocks else D.Blocks.xslabs(D.slab_cuts(n, world))
     eng = engine_for(net)
-    eng.set_owned(cuts[rank], cuts[rank + 1])
+    eng.set_owned_box(*part.owned(rank))
     eng.set_shards(world)
     marks = net.enc.marks.cpu()
     for k, h in enumerate(D.HALOS):
         st = []
-        eng.lattice(*D.slab_marks(cuts, rank, h))
+        eng.lattice_box(*part.box(rank, h))
         eng.run_steps(st, coll)
         Vl, El, _ = eng.export()
         Vl, El = Vl.cpu(), El.cpu()
-        if D.halo_check(Vl, El, marks, cuts, raise_=k == len(D.HALOS) - 1) is not None:
+        if D.halo_check(Vl, El, marks, part, raise_=k == len(D.HALOS) - 1) is not None:
             break
     stats.extend(st)
-    return cuts, Vl, El
+    return part, Vl, El, h
 
 
 def _worker(rank, world, port, outdir, case, mode):
@@ -74,34 +75,33 @@ def _worker(rank, world, port, outdir, case, mode):
         torch.cuda.set_device(dev)
         coll = bench.Collective(torch.device("cpu"))
         stats = []
-        if mode == "bench":  # the synthetic bench net of `case` = (marks, seed)
+        blocks = mode.endswith("_blocks")
+        if mode.startswith("bench"):  # the synthetic bench net of `case` = (marks, seed)
             G, seed = case
             net = bench.make_net(G, dev, seed)
-            cuts, Vl, El = _sharded_lattice(net, rank, world, coll, stats)
-            own = D.owner_of(Vl, net.enc.marks.cpu(), cuts) == rank
-            owner = D.owner_of(Vl, net.enc.marks.cpu(), cuts)
-            keep = torch.maximum(owner[El[:, 0]], owner[El[:, 1]]) == rank
+            part, Vl, El, halo = _sharded_lattice(net, rank, world, coll, stats, blocks)
+            own, keep = D.owned_masks(Vl, El, net.enc.marks.cpu(), part, rank)
             hv, he = D.complex_hash(Vl, El, own, keep)
             splits = sum(s["S"] - s["S_dup"] for s in stats)
             tot = torch.tensor([int(own.sum()), int(keep.sum()), hv, he, splits], dtype=torch.int64)
             dist.all_reduce(tot)
             if rank == 0:
-                np.savez(os.path.join(outdir, "out.npz"), tot=tot.numpy(), cuts=np.array(cuts))
+                np.savez(os.path.join(outdir, "out.npz"), tot=tot.numpy(), dims=np.array(part.dims),
+                         halo=np.array(halo), redundant=np.array(part.redundant_frac(rank, halo)))
             return
         d = load(case)
         net = product_net(d, dev)
-        if mode == "lattice":
-            cuts, Vl, El = _sharded_lattice(net, rank, world, coll, stats)
-            owned, first, gE, own, keep = D.stitch(Vl, El, net.enc.marks.cpu(), cuts, masks=True)
+        if mode.startswith("lattice"):
+            part, Vl, El, _ = _sharded_lattice(net, rank, world, coll, stats, blocks)
+            cuts = part.cuts[0]
+            owned, first, gE, own, keep = D.stitch(Vl, El, net.enc.marks.cpu(), part, masks=True)
         else:  # "skeleton" (flat) or "curve" (force=False: the curve branch's decisions go
             # through the engine's collective callback)
             eng, owned, first, gE, cuts = D.subpoly_sharded(net, 1.2, allreduce=coll, stats=stats,
                                                             force=mode != "curve")
             Vl, El, _ = eng.export()
             Vl, El = Vl.cpu(), El.cpu()
-            own = D.owner_of(Vl, net.enc.marks.cpu(), cuts) == rank
-            keep = torch.maximum(D.owner_of(Vl, net.enc.marks.cpu(), cuts)[El[:, 0]],
-                                 D.owner_of(Vl, net.enc.marks.cpu(), cuts)[El[:, 1]]) == rank
+            own, keep = D.owned_masks(Vl, El, net.enc.marks.cpu(), cuts, rank)
         hv, he = D.complex_hash(Vl, El, own, keep)
         splits = sum(s["S"] - s["S_dup"] for s in stats)
         tot = torch.tensor([owned.shape[0], gE.shape[0], hv, he, splits], dtype=torch.int64)
@@ -115,7 +115,7 @@ def _worker(rank, world, port, outdir, case, mode):
         from golden_io import sha
         import tropical.subpoly as sp
         single_ok = torch.tensor([1])
-        if mode != "lattice":  # (the lattice goldens hold the full-lattice surface, not subpoly's)
+        if not mode.startswith("lattice"):  # (the lattice goldens hold the full-lattice surface, not subpoly's)
             with contextlib.redirect_stdout(io.StringIO()):
                 _, verts, fwi = sp.subpoly(net, 3, 1.2, force=mode != "curve")
             single_ok[0] = int(verts.shape[0] == int(d["n_surf"][0]) and
@@ -155,12 +155,17 @@ def _unsharded(cuda, case, mode):
     return d, V, E, (V.shape[0], E.shape[0], hv, he, sum(s["S"] for s in stats))
 
 
-@pytest.mark.parametrize("case,world", [("synth32h", 2), ("synth32h", 3), ("synth64h", 2), ("synth64h", 8)])
-def test_sharded_lattice_engine(cuda, tmp_path, case, world):
+@pytest.mark.parametrize("case,world,mode", [("synth32h", 2, "lattice"), ("synth32h", 3, "lattice"),
+                                             ("synth64h", 2, "lattice"), ("synth64h", 8, "lattice"),
+                                             ("synth32h", 4, "lattice_blocks"), ("synth64h", 8, "lattice_blocks")])
+def test_sharded_lattice_engine(cuda, tmp_path, case, world, mode):
+    """x-slabs, and blocks (2 x 2 x 1, 2 x 2 x 2: the box lattice, owned box
+    and span of the engine, halo_check over every cut face, the stitch's
+    cell-owner edge rule with vertices shared by up to 8 blocks)."""
     d, V, E, want = _unsharded(cuda, case, "lattice")
     assert (want[0], want[1]) == tuple(int(x) for x in d["pre_VE"])
     assert (want[2], want[3]) == tuple(int(x) for x in d["complex_hash"])  # the reference's
-    z = _run(tmp_path, case, "lattice", world)
+    z = _run(tmp_path, case, mode, world)
     assert tuple(int(x) for x in z["tot"]) == want
     # the gathered complex has one global numbering: every edge resolves
     assert z["V"].shape[0] == want[0] and z["E"].shape[0] == want[1]
@@ -196,12 +201,15 @@ def test_sharded_curve_branch(cuda, tmp_path, case, world):
 
 
 @pytest.mark.timeout(600)
-def test_lattice256_eight_slabs_stitch_to_the_unsharded_complex(cuda, tmp_path):
+@pytest.mark.parametrize("mode", ["bench", "bench_blocks"])
+def test_lattice256_eight_slabs_stitch_to_the_unsharded_complex(cuda, tmp_path, mode):
     """BASELINE config 5 at its full size (the 8-GPU weak-scaling lattice of
-    bench.py --gpus 8): the 256^3 seed-6 synthetic lattice cut into 8 x-slabs
-    (8 gloo ranks sharing this GPU, halo search as bench.py) must hold exactly
-    the complex the unsharded engine extracts on one GPU -- same vertex and
-    edge counts, same order-free fingerprints -- and count every split once."""
+    bench.py --gpus 8): the 256^3 seed-6 synthetic lattice cut into 8 x-slabs,
+    or the 2 x 2 x 2 blocks bench.py uses (8 gloo ranks sharing this GPU,
+    halo search as bench.py), must hold exactly the complex the unsharded
+    engine extracts on one GPU -- same vertex and edge counts, same
+    order-free fingerprints -- and count every split once; the blocks' halo
+    must leave at most 7 % of a rank's cells redundant."""
     import bench
     from tropical.distributed import complex_hash
     from tropical._engine import engine_for
@@ -217,9 +225,11 @@ def test_lattice256_eight_slabs_stitch_to_the_unsharded_complex(cuda, tmp_path):
     want = (V.shape[0], E.shape[0], hv, he, sum(s["S"] for s in stats))
     del V, E
     torch.cuda.empty_cache()
-    z = _run(tmp_path, (256, 6), "bench", 8)
+    z = _run(tmp_path, (256, 6), mode, 8)
     assert tuple(int(x) for x in z["tot"]) == want
-    assert len(z["cuts"]) == 9
+    if mode == "bench_blocks":
+        assert z["dims"].tolist() == [2, 2, 2]
+        assert float(z["redundant"]) <= 0.07, (int(z["halo"]), float(z["redundant"]))
 
 
 def test_slab_buckets_do_not_change_the_result(cuda):
@@ -244,8 +254,22 @@ def test_slab_buckets_do_not_change_the_result(cuda):
         V, E, _ = eng.export()
         got.append((V.shape[0], E.shape[0]) + complex_hash(V, E))
     assert got[0] == got[1]
+    # a block: buckets over its box along all three axes
+    got = []
+    for narrow in (True, False):
+        eng.lattice_box([20, 10, 5], [41, 40, 30])
+        if not narrow:
+            eng.set_span([0, 0, 0], [-1, -1, -1])
+        eng.run_steps([])
+        V, E, _ = eng.export()
+        got.append((V.shape[0], E.shape[0]) + complex_hash(V, E))
+    assert got[0] == got[1]
+    eng.lattice_box([20, 10, 5], [41, 40, 30])
+    eng.set_span([20, 10, 5], [41, 25, 30])
+    with pytest.raises(RuntimeError, match="outside the mark planes"):
+        eng.run_steps([])
     eng.lattice(20, 41)
     eng.set_xspan(30, 41)
-    with pytest.raises(RuntimeError, match="outside the x mark planes"):
+    with pytest.raises(RuntimeError, match="outside the mark planes"):
         eng.run_steps([])
     eng.set_shards(1)

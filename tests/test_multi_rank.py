@@ -44,21 +44,26 @@ def _canon(V, E):
 
 
 def _slab_worker(rank, world, port, outdir, cuts):
+    """cuts: x-slab cuts, or ("blocks", dims) for a block split."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         import bench
         import oracle.subdivide as od
-        from tropical.synthetic import slab_lattice
-        torch.set_num_threads(2)
+        from tropical.synthetic import block_lattice, slab_lattice
+        torch.set_num_threads(2 if world <= 4 else 1)
         d = load(CASE)
         net = oracle_net(d)
         n = int(d["lattice_n"])
-        from tropical.distributed import gather_complex, slab_marks, stitch
-        assert cuts[-1] == n - 1
-        x0, x1 = slab_marks(cuts, rank)
-        V, E = slab_lattice(d["marks"], x0, x1)
+        from tropical.distributed import HALO, Blocks, gather_complex, slab_marks, stitch
+        if cuts[0] == "blocks":
+            cuts = Blocks(n, cuts[1])
+            V, E = block_lattice(d["marks"], *cuts.box(rank, HALO))
+        else:
+            assert cuts[-1] == n - 1
+            x0, x1 = slab_marks(cuts, rank)
+            V, E = slab_lattice(d["marks"], x0, x1)
         coll = bench.Collective(torch.device("cpu"))
 
         def sync(kind, value):
@@ -99,6 +104,45 @@ def test_slab_cuts_cover_the_lattice():
             assert x0 == max(cuts[r] - 2, 0) and x1 == min(cuts[r + 1] + 2, G - 1)
 
 
+def test_block_split():
+    """block_dims is the most cubic factorisation; every cell of the grid has
+    exactly one owning block; the 256^3 / 8-rank split at a 3-cell halo
+    extracts 6.7-6.8 % redundant cells per rank (x-slabs: 15.8 %)."""
+    from tropical.distributed import Blocks, block_dims, slab_cuts
+    assert [block_dims(w) for w in (1, 2, 3, 4, 6, 8, 12, 16)] == [
+        (1, 1, 1), (2, 1, 1), (3, 1, 1), (2, 2, 1), (3, 2, 1), (2, 2, 2), (3, 2, 2), (4, 2, 2)]
+    B = Blocks(256, (2, 2, 2))
+    assert [B.rank_of(B.index(r)) for r in range(8)] == list(range(8))
+    cells = np.zeros((255, 255, 255), dtype=np.int32)
+    for r in range(8):
+        lo, hi = B.owned(r)
+        cells[lo[0]:hi[0], lo[1]:hi[1], lo[2]:hi[2]] += 1
+    assert (cells == 1).all()
+    assert abs(B.redundant_frac(0, 3) - 0.0672) < 1e-3
+    assert abs(Blocks.xslabs(slab_cuts(256, 8)).redundant_frac(1, 3) - 0.158) < 1e-3
+
+
+def test_block_owner_and_edge_rules():
+    """Per axis the x-slab owner rule; an edge belongs to the block of the
+    highest cell whose closure holds both endpoints."""
+    from tropical.distributed import Blocks, edge_owner, owner_of
+    marks = torch.linspace(0, 1, 11)
+    B = Blocks(11, (2, 2, 1), [[0, 4, 10], [0, 6, 10], [0, 10]])
+    p = lambda i: float(marks[i]) * 2 - 1  # on mark plane i
+    c = lambda i: (float(marks[i]) + 0.05) * 2 - 1  # inside cell i
+    V = torch.tensor([[p(4), p(6), 0.0],    # planes x4, y6 -> block (0, 0)
+                      [c(4), p(6), 0.0],    # cell x4, plane y6 -> (1, 0)
+                      [c(4), c(6), 0.0],    # (1, 1)
+                      [p(4), c(6), 0.0],    # (0, 1)
+                      [p(0), p(0), 0.0],    # (0, 0)
+                      [p(10), p(10), 0.0]])  # (1, 1)
+    assert owner_of(V, marks, B).tolist() == [0, 2, 3, 1, 0, 3]
+    E = torch.tensor([[0, 1], [0, 2], [0, 3], [1, 2], [3, 2], [5, 5]])
+    # each edge lies in cell (x4, y6) (per axis the lower endpoint offset),
+    # block (1, 1) = rank 3; the last one on the grid's far corner line
+    assert edge_owner(V, E, marks, B).tolist() == [3, 3, 3, 3, 3, 3]
+
+
 def test_owner_rule_matches_cells_and_planes():
     import torch
     from tropical.distributed import owner_of
@@ -111,9 +155,17 @@ def test_owner_rule_matches_cells_and_planes():
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, "blocks4", "blocks8"])
 def test_gloo_ranks_reproduce_the_unsharded_complex(tmp_path, world, whole):
-    mp.spawn(_slab_worker, args=(world, _free_port(), str(tmp_path), CUTS[world]), nprocs=world,
+    """x-slabs (2, 3 ranks) and blocks (2 x 2 x 1, 2 x 2 x 2 ranks: cut faces
+    along two and three axes, edges and corners where 4 and 8 blocks meet)."""
+    if isinstance(world, str):
+        from tropical.distributed import block_dims
+        world = int(world[len("blocks"):])
+        part = ("blocks", block_dims(world))
+    else:
+        part = CUTS[world]
+    mp.spawn(_slab_worker, args=(world, _free_port(), str(tmp_path), part), nprocs=world,
              join=True)
     d = load(CASE)
     V, E = whole

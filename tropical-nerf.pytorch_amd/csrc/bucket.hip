@@ -141,18 +141,20 @@ __device__ __forceinline__ void span_of(uint64_t g, int lo[3], int n[3]) {
 }
 
 __device__ __forceinline__ int bucket_of(const BGeom& G, int cx, int cy, int cz) {
-  return (((cx - G.xorg) >> G.sh) * G.NBd + (cy >> G.sh)) * G.NBd + (cz >> G.sh);
+  return (((cx - G.xorg) >> G.sh) * G.NBy + ((cy - G.yorg) >> G.sh)) * G.NBz + ((cz - G.zorg) >> G.sh);
 }
 
 __device__ __forceinline__ int local_of(const BGeom& G, int cx, int cy, int cz) {
   const int m = (1 << G.sh) - 1;
-  return (((cx - G.xorg) & m) << (2 * G.sh)) | ((cy & m) << G.sh) | (cz & m);
+  return (((cx - G.xorg) & m) << (2 * G.sh)) | (((cy - G.yorg) & m) << G.sh) | ((cz - G.zorg) & m);
 }
 
-// every cell of the span inside the buckets' x range (else the member is
-// skipped and flagged: the complex left the slab the engine was told of)
+// every cell of the span inside the buckets' box (else the member is
+// skipped and flagged: the complex left the span the engine was told of)
 __device__ __forceinline__ bool span_inside(const BGeom& G, const int lo[3], const int n[3]) {
-  return (unsigned)(lo[0] - G.xorg) <= (unsigned)(G.xn - n[0]);
+  return ((unsigned)(lo[0] - G.xorg) <= (unsigned)(G.xn - n[0])) &
+         ((unsigned)(lo[1] - G.yorg) <= (unsigned)(G.yn - n[1])) &
+         ((unsigned)(lo[2] - G.zorg) <= (unsigned)(G.zn - n[2]));
 }
 
 // exclusive scan of n counts another workgroup of this launch handed over
@@ -687,10 +689,10 @@ __device__ __forceinline__ void put_pair_cell(int64_t o, int64_t lo, int32_t cel
 // or (sub geometries) octant b & 7 of member-pass bucket b >> 3
 __device__ __forceinline__ void group_origin(const BGeom& G, int b, int& ox, int& oy, int& oz) {
   const int B = G.sub ? b >> 3 : b;
-  const int bz = B % G.NBd, by = (B / G.NBd) % G.NBd, bx = B / (G.NBd * G.NBd);
+  const int bz = B % G.NBz, by = (B / G.NBz) % G.NBy, bx = B / (G.NBy * G.NBz);
   ox = G.xorg + (bx << G.sh);
-  oy = by << G.sh;
-  oz = bz << G.sh;
+  oy = G.yorg + (by << G.sh);
+  oz = G.zorg + (bz << G.sh);
   if (G.sub) {
     ox += ((b >> 2) & 1) << 3;
     oy += ((b >> 1) & 1) << 3;
@@ -1329,12 +1331,16 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
 
 }  // namespace
 
-int bucket_geometry(int n_marks, int x0, int x1, BucketGeom* g) {
+int bucket_geometry(int n_marks, const int lo[3], const int hi[3], BucketGeom* g) {
   const int NC = n_marks + 2;
-  // cells of a complex inside the x mark planes [x0, x1]: offsets x0 - 1
-  // (a vertex within eps of plane x0 spans the cell below) to x1, i.e. cell
-  // coordinates x0 + 1 .. x1 + 2; one more on each side
-  const int xlo = std::max(0, x0), xhi = std::min(NC - 1, x1 + 3);
+  // cells of a complex inside the mark planes [lo, hi] of an axis: offsets
+  // lo - 1 (a vertex within eps of plane lo spans the cell below) to hi,
+  // i.e. cell coordinates lo + 1 .. hi + 2; one more on each side
+  int clo[3], cn[3];
+  for (int d = 0; d < 3; ++d) {
+    clo[d] = std::max(0, lo[d]);
+    cn[d] = std::min(NC - 1, hi[d] + 3) - clo[d] + 1;
+  }
   static const int s_env = [] {  // TNP_BUCKET_SH=3|4: force the bucket edge (experiments)
     const char* v = getenv("TNP_BUCKET_SH");
     return v ? atoi(v) : 0;
@@ -1344,14 +1350,16 @@ int bucket_geometry(int n_marks, int x0, int x1, BucketGeom* g) {
     return v ? atoi(v) : -1;
   }();
   for (int s = (s_env == 4 || s_sub == 1 ? 4 : 3); s <= 4; ++s) {
-    const int nbd = (NC + (1 << s) - 1) >> s;
-    const int nbx = (xhi - xlo + 1 + (1 << s) - 1) >> s;
-    const int64_t nb = (int64_t)nbx * nbd * nbd;
+    int nbs[3];
+    for (int d = 0; d < 3; ++d) nbs[d] = (cn[d] + (1 << s) - 1) >> s;
+    const int64_t nb = (int64_t)nbs[0] * nbs[1] * nbs[2];
     if (nb > BUCKET_MAX) continue;
     // 16^3-cell member buckets are refined into 8^3-cell group buckets
     // unless TNP_BUCKET_SH=4 asks for the 16^3-cell grouping kernel
     const int sub = s == 4 && s_env != 4 && s_sub != 0;
-    *g = BucketGeom{NC, s, nbd, nbx, xlo, nbx << s, (int)nb, sub, sub ? 8 * (int)nb : (int)nb};
+    *g = BucketGeom{NC,          s,           nbs[0],      nbs[1],   nbs[2],   clo[0],
+                    clo[1],      clo[2],      nbs[0] << s, nbs[1] << s, nbs[2] << s, (int)nb,
+                    sub,         sub ? 8 * (int)nb : (int)nb};
     return 0;
   }
   return -1;

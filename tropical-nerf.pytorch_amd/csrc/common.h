@@ -285,6 +285,27 @@ __device__ __forceinline__ bool grid_zero(uint64_t g, int d) {
   return (g >> (48 + d)) & 1;
 }
 
+// A shard's owned box of the mark grid: along axis d, the cells lo[d] <= c <
+// hi[d] and the mark planes lo[d] < p <= hi[d] (plane 0 by the shard with
+// lo[d] == 0); lo[d] > hi[d]: the axis is not cut.  x-slabs cut x only.
+struct OwnBox {
+  int lo[3], hi[3];
+};
+__host__ __device__ __forceinline__ bool own_any(const OwnBox& o) {
+  return o.lo[0] <= o.hi[0] || o.lo[1] <= o.hi[1] || o.lo[2] <= o.hi[2];
+}
+// a vertex (grid word g) lies in the box in the grid-region sense
+__device__ __forceinline__ bool owned_by(const OwnBox& o, uint64_t g) {
+  bool in = true;
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    const int lo = o.lo[d], hi = o.hi[d], c = grid_off(g, d);
+    const bool ok = grid_zero(g, d) ? ((c > lo || (lo == 0 && c == 0)) && c <= hi) : (c >= lo && c < hi);
+    in &= lo > hi || ok;
+  }
+  return in;
+}
+
 // True in every thread of the workgroup that finishes a launch last, so it
 // can finish the launch's reduction without another launch.  Hand-off
 // (MI355X_MICROARCH.md, inter-workgroup visibility, first row): the values
@@ -481,3 +502,4 @@ __host__ __device__ __forceinline__ bool act_test(uint64_t m, int p) { return (m
 
 using tnp::TnpLB;
 using tnp::Key;
+using tnp::OwnBox;

@@ -121,10 +121,10 @@ enum {
 
 struct tnp_engine {
   int device = 0;
-  int own_lo = 1, own_hi = 0;  // owned mark planes (lo, hi]; lo > hi: all
-  // x mark planes the complex lies within (the spatial buckets cover only
-  // those cells); xs1 < xs0: all
-  int xs0 = 0, xs1 = -1;
+  OwnBox own{{1, 1, 1}, {0, 0, 0}};  // owned box of a shard (common.h); uncut axes: all
+  // mark planes the complex lies within, per axis (the spatial buckets cover
+  // only those cells); sp_hi[d] < sp_lo[d]: the whole axis
+  int sp_lo[3] = {0, 0, 0}, sp_hi[3] = {-1, -1, -1};
   int curve = 0;          // 1: subpoly_(force=False) semantics
   int strict = 1;         // curve path: subpoly_(strict=...) -- 0 keeps every split (subpoly.py:198-202)
   int shards = 1;         // >1: one x-slab of a sharded complex
@@ -388,10 +388,22 @@ static int reset_live(tnp_engine* e, hipStream_t s, bool edges_changed = true) {
 
 // the cell grouping runs on spatial buckets (bucket.hip) unless the grid is
 // too fine for them or TNP_RADIX_CELLS=1; *bg: their geometry
+static void span_all(tnp_engine* e) {
+  for (int d = 0; d < 3; ++d) e->sp_lo[d] = 0, e->sp_hi[d] = -1;
+}
+// the span's mark planes along each axis (the whole axis where not narrowed)
+static void span_of(const tnp_engine* e, int lo[3], int hi[3]) {
+  for (int d = 0; d < 3; ++d) {
+    const bool set = e->sp_hi[d] >= e->sp_lo[d];
+    lo[d] = set ? e->sp_lo[d] : 0;
+    hi[d] = set ? e->sp_hi[d] : e->net.n_marks - 1;
+  }
+}
 static bool uses_buckets(const tnp_engine* e, BucketGeom* bg) {
   if (e->kw != 1) return false;  // two-word keys: the radix path's 48-B records
-  const int gx0 = e->xs1 >= e->xs0 ? e->xs0 : 0, gx1 = e->xs1 >= e->xs0 ? e->xs1 : e->net.n_marks - 1;
-  return !e->radix_cells && bucket_geometry(e->net.n_marks, gx0, gx1, bg) == 0;
+  int lo[3], hi[3];
+  span_of(e, lo, hi);
+  return !e->radix_cells && bucket_geometry(e->net.n_marks, lo, hi, bg) == 0;
 }
 
 // split-eps mode: subpoly's eps argument differs from Net.eps (tnp_engine_set_eps)
@@ -725,8 +737,7 @@ extern "C" int tnp_engine_load(tnp_engine* e, const float* d_xyz, int64_t V, con
   hipStream_t s = (hipStream_t)stream;
   if (!e->has_net) { tnp_set_error("engine has no net"); return -1; }
   TNP_CHECK(hipSetDevice(e->device));
-  e->xs0 = 0;  // anywhere (tnp_engine_set_xspan narrows it)
-  e->xs1 = -1;
+  span_all(e);  // anywhere (tnp_engine_set_span narrows it)
   if (buf_ensure(e->ctr, CTR_CLEAR_BYTES, s)) return -1;
   if (vset_ensure(e, e->cur, std::max<int64_t>(V, 1), 0, s)) return -1;
   if (V > 0)
@@ -1158,7 +1169,7 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
                 table_bytes(e->net),
             launch_forward_new(e->net, P<float>(e->cur.xyz) + 3 * e->V, S, P<float>(e->cur.pre),
                                e->cur.cap, e->V, e->valid_from, P<int32_t>(e->sa), P<int32_t>(e->sb),
-                               idx, e->own_lo, e->own_hi, P<uint64_t>(e->cur.pos),
+                               idx, e->own, P<uint64_t>(e->cur.pos),
                                P<uint64_t>(e->cur.zero), P<uint64_t>(e->cur.grid),
                                P<uint64_t>(e->shared), P<int64_t>(e->ctr), P<uint64_t>(e->cur.pz),
                                col, s));
@@ -1224,7 +1235,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     // the kept splits another shard owns (read back with the connect
     // counters; the split's CTR_DUP count is the flat path's)
     TNP_CHECK(hipMemsetAsync(P<int64_t>(e->ctr) + CTR_DUP, 0, sizeof(int64_t), s));
-    if (launch_count_unowned(P<uint64_t>(e->cur.grid) + e->V, S_kept, e->own_lo, e->own_hi, P<int64_t>(e->ctr), s))
+    if (launch_count_unowned(P<uint64_t>(e->cur.grid) + e->V, S_kept, e->own, P<int64_t>(e->ctr), s))
       return -1;
   }
   const int64_t V = e->V, E = e->E, S = S_kept;
@@ -1237,7 +1248,8 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   uint64_t* grid = P<uint64_t>(c.grid);
 
   BucketGeom bg{};
-  const int gx0 = e->xs1 >= e->xs0 ? e->xs0 : 0, gx1 = e->xs1 >= e->xs0 ? e->xs1 : e->net.n_marks - 1;
+  int sp0[3], sp1[3];
+  span_of(e, sp0, sp1);
   const bool buckets = uses_buckets(e, &bg);
   const int NB = buckets ? bg.NB : 0;
   // 1. override + keys of the new vertices (flat bucket path: the override
@@ -1457,8 +1469,8 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
       e->h_ctr[CTR_R] = e->h_ctr[CTR_PCK] & (PCK_CELLS - 1);
       e->h_ctr[CTR_TESTS] = e->h_ctr[CTR_PCK] >> 24;
       if (e->h_ctr[CTR_K0] & 2) {
-        tnp_set_error("plane %d: a vertex outside the x mark planes [%d, %d] the engine was given "
-                      "(tnp_engine_set_xspan)", idx, gx0, gx1);
+        tnp_set_error("plane %d: a vertex outside the mark planes [%d, %d] x [%d, %d] x [%d, %d] the engine "
+                      "was given (tnp_engine_set_span)", idx, sp0[0], sp1[0], sp0[1], sp1[1], sp0[2], sp1[2]);
         return -1;
       }
       if (e->h_ctr[CTR_K0]) {
@@ -1776,40 +1788,42 @@ extern "C" int tnp_engine_surface(tnp_engine* e, void* stream, int64_t* V_out, i
 }
 
 // ---------------------------------------------------------------------------
-// full lattice over the marks, x-slab [x0, x1] (tropical.py:103-109 layout:
-// x-edges, then y, then z, each (hi, lo), meshgrid-ij order)
+// full lattice over the marks, box [lo, hi] of mark indices per axis
+// (tropical.py:103-109 layout: x-edges, then y, then z, each (hi, lo),
+// meshgrid-ij order; the whole grid is the reference's lattice, an x-slab or
+// a block of a sharded one keeps the same order within the box)
 // ---------------------------------------------------------------------------
 namespace {
-__global__ void k_lattice_vertices(const float* __restrict__ marks, int N, int x0, int nx,
-                                   float* __restrict__ xyz) {
+__global__ void k_lattice_vertices(const float* __restrict__ marks, int x0, int y0, int z0, int nx, int ny,
+                                   int nz, float* __restrict__ xyz) {
   int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  int64_t nv = (int64_t)nx * N * N;
+  int64_t nv = (int64_t)nx * ny * nz;
   if (v >= nv) return;
-  int k = (int)(v % N), j = (int)((v / N) % N), i = (int)(v / ((int64_t)N * N)) + x0;
+  int k = (int)(v % nz) + z0, j = (int)((v / nz) % ny) + y0, i = (int)(v / ((int64_t)ny * nz)) + x0;
   // preprocess_inverse: x * 2 - 1 (model.py:81-82)
   xyz[3 * v + 0] = __fsub_rn(__fmul_rn(marks[i], 2.0f), 1.0f);
   xyz[3 * v + 1] = __fsub_rn(__fmul_rn(marks[j], 2.0f), 1.0f);
   xyz[3 * v + 2] = __fsub_rn(__fmul_rn(marks[k], 2.0f), 1.0f);
 }
-__global__ void k_lattice_edges(int N, int nx, int32_t* __restrict__ edges) {
-  const int64_t NN = (int64_t)N * N;
+__global__ void k_lattice_edges(int nx, int ny, int nz, int32_t* __restrict__ edges) {
+  const int64_t NN = (int64_t)ny * nz;
   const int64_t ex = (int64_t)(nx - 1) * NN;
-  const int64_t ey = (int64_t)nx * (N - 1) * N;
-  const int64_t ez = (int64_t)nx * N * (N - 1);
+  const int64_t ey = (int64_t)nx * (ny - 1) * nz;
+  const int64_t ez = (int64_t)nx * ny * (nz - 1);
   int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int64_t lo, hi;
   if (e < ex) {
     lo = e;
     hi = e + NN;
   } else if (e < ex + ey) {
-    int64_t r = e - ex;  // shape (nx, N-1, N)
-    int64_t k = r % N, j = (r / N) % (N - 1), i = r / ((int64_t)(N - 1) * N);
-    lo = i * NN + j * N + k;
-    hi = lo + N;
+    int64_t r = e - ex;  // shape (nx, ny-1, nz)
+    int64_t k = r % nz, j = (r / nz) % (ny - 1), i = r / ((int64_t)(ny - 1) * nz);
+    lo = i * NN + j * nz + k;
+    hi = lo + nz;
   } else if (e < ex + ey + ez) {
-    int64_t r = e - ex - ey;  // shape (nx, N, N-1)
-    int64_t k = r % (N - 1), j = (r / (N - 1)) % N, i = r / ((int64_t)N * (N - 1));
-    lo = i * NN + j * N + k;
+    int64_t r = e - ex - ey;  // shape (nx, ny, nz-1)
+    int64_t k = r % (nz - 1), j = (r / (nz - 1)) % ny, i = r / ((int64_t)ny * (nz - 1));
+    lo = i * NN + j * nz + k;
     hi = lo + 1;
   } else {
     return;
@@ -1819,25 +1833,32 @@ __global__ void k_lattice_edges(int N, int nx, int32_t* __restrict__ edges) {
 }
 }  // namespace
 
-extern "C" int tnp_engine_lattice(tnp_engine* e, int x0, int x1, int keep_all, void* stream,
-                                  int64_t* V_out, int64_t* E_out) {
+extern "C" int tnp_engine_lattice_box(tnp_engine* e, const int32_t* lo3, const int32_t* hi3, int keep_all,
+                                      void* stream, int64_t* V_out, int64_t* E_out) {
   hipStream_t s = (hipStream_t)stream;
   if (!e->has_net) { tnp_set_error("engine has no net"); return -1; }
   TNP_CHECK(hipSetDevice(e->device));
   const int N = e->net.n_marks;
-  if (x0 < 0 || x1 >= N || x1 < x0) { tnp_set_error("bad slab [%d, %d] of %d marks", x0, x1, N); return -1; }
-  const int nx = x1 - x0 + 1;
-  e->xs0 = x0;
-  e->xs1 = x1;
-  const int64_t V = (int64_t)nx * N * N;
-  const int64_t E = (int64_t)(nx - 1) * N * N + 2LL * nx * (N - 1) * N;
+  int n[3];
+  for (int d = 0; d < 3; ++d) {
+    if (lo3[d] < 0 || hi3[d] >= N || hi3[d] < lo3[d]) {
+      tnp_set_error("bad lattice box: axis %d marks [%d, %d] of %d", d, lo3[d], hi3[d], N);
+      return -1;
+    }
+    n[d] = hi3[d] - lo3[d] + 1;
+    e->sp_lo[d] = lo3[d];
+    e->sp_hi[d] = hi3[d];
+  }
+  const int64_t V = (int64_t)n[0] * n[1] * n[2];
+  const int64_t E = (int64_t)(n[0] - 1) * n[1] * n[2] + (int64_t)n[0] * (n[1] - 1) * n[2] +
+                    (int64_t)n[0] * n[1] * (n[2] - 1);
   if (V >= (1LL << 31) || E >= (1LL << 31)) { tnp_set_error("lattice too large for int32 ids"); return -1; }
   if (buf_ensure(e->ctr, CTR_CLEAR_BYTES, s)) return -1;
   if (vset_ensure(e, e->cur, V, 0, s)) return -1;
   if (buf_ensure(e->edges, std::max<int64_t>(E, 1) * 2 * sizeof(int32_t), s)) return -1;
-  hipLaunchKernelGGL(k_lattice_vertices, dim3(tnp_grid(V)), dim3(TNP_BLOCK), 0, s, e->net.marks, N,
-                     x0, nx, P<float>(e->cur.xyz));
-  hipLaunchKernelGGL(k_lattice_edges, dim3(tnp_grid(E)), dim3(TNP_BLOCK), 0, s, N, nx,
+  hipLaunchKernelGGL(k_lattice_vertices, dim3(tnp_grid(V)), dim3(TNP_BLOCK), 0, s, e->net.marks, lo3[0], lo3[1],
+                     lo3[2], n[0], n[1], n[2], P<float>(e->cur.xyz));
+  hipLaunchKernelGGL(k_lattice_edges, dim3(tnp_grid(E)), dim3(TNP_BLOCK), 0, s, n[0], n[1], n[2],
                      P<int32_t>(e->edges));
   TNP_CHECK(hipGetLastError());
   // the lattice's full forward (12 B coordinates in; K planes, 40 B of keys out)
@@ -1854,6 +1875,15 @@ extern "C" int tnp_engine_lattice(tnp_engine* e, int x0, int x1, int keep_all, v
   *V_out = V;
   *E_out = E;
   return reset_live(e, s);
+}
+
+extern "C" int tnp_engine_lattice(tnp_engine* e, int x0, int x1, int keep_all, void* stream,
+                                  int64_t* V_out, int64_t* E_out) {
+  if (!e->has_net) { tnp_set_error("engine has no net"); return -1; }
+  const int N = e->net.n_marks;
+  if (x0 < 0 || x1 >= N || x1 < x0) { tnp_set_error("bad slab [%d, %d] of %d marks", x0, x1, N); return -1; }
+  const int32_t lo[3] = {x0, 0, 0}, hi[3] = {x1, N - 1, N - 1};
+  return tnp_engine_lattice_box(e, lo, hi, keep_all, stream, V_out, E_out);
 }
 
 // ---------------------------------------------------------------------------
@@ -1905,8 +1935,7 @@ extern "C" int tnp_engine_skeleton_mode(tnp_engine* e, int unit, float size, int
   if (!e->has_net) { tnp_set_error("engine has no net"); return -1; }
   if (unit < 2) { tnp_set_error("unit must be >= 2"); return -1; }
   TNP_CHECK(hipSetDevice(e->device));
-  e->xs0 = 0;  // the whole grid
-  e->xs1 = -1;
+  span_all(e);  // the whole grid
   const int L = e->net.n_marks;
   if ((int64_t)L * L * L >= (1LL << 31)) { tnp_set_error("too many marks for int32 ids"); return -1; }
   std::vector<float> mk(L);
@@ -2202,8 +2231,12 @@ extern "C" int tnp_engine_faces_export(tnp_engine* e, int64_t* d_tri, float* d_f
 // slab boundary + kernel timer controls
 // ---------------------------------------------------------------------------
 extern "C" int tnp_engine_set_owned(tnp_engine* e, int lo, int hi) {
-  e->own_lo = lo;
-  e->own_hi = hi;
+  e->own = OwnBox{{lo, 1, 1}, {hi, 0, 0}};
+  return 0;
+}
+
+extern "C" int tnp_engine_set_owned_box(tnp_engine* e, const int32_t* lo3, const int32_t* hi3) {
+  for (int d = 0; d < 3; ++d) e->own.lo[d] = lo3[d], e->own.hi[d] = hi3[d];
   return 0;
 }
 
@@ -2217,14 +2250,19 @@ extern "C" int tnp_engine_set_eps(tnp_engine* e, float eps) {
   return 0;
 }
 
-extern "C" int tnp_engine_set_xspan(tnp_engine* e, int x0, int x1) {
-  if (x1 >= x0 && (x0 < 0 || (e->has_net && x1 >= e->net.n_marks))) {
-    tnp_set_error("bad x span [%d, %d]", x0, x1);
-    return -1;
-  }
-  e->xs0 = x0;
-  e->xs1 = x1;
+extern "C" int tnp_engine_set_span(tnp_engine* e, const int32_t* lo3, const int32_t* hi3) {
+  for (int d = 0; d < 3; ++d)
+    if (hi3[d] >= lo3[d] && (lo3[d] < 0 || (e->has_net && hi3[d] >= e->net.n_marks))) {
+      tnp_set_error("bad span: axis %d marks [%d, %d]", d, lo3[d], hi3[d]);
+      return -1;
+    }
+  for (int d = 0; d < 3; ++d) e->sp_lo[d] = lo3[d], e->sp_hi[d] = hi3[d];
   return 0;
+}
+
+extern "C" int tnp_engine_set_xspan(tnp_engine* e, int x0, int x1) {
+  const int32_t lo[3] = {x0, 0, 0}, hi[3] = {x1, -1, -1};
+  return tnp_engine_set_span(e, lo, hi);
 }
 
 extern "C" int tnp_engine_kernel_timer(tnp_engine* e, int on, void* stream, int32_t* n_kernels) {

@@ -48,7 +48,7 @@ int lv_forward(const NetDev& net, const float* xyz, int64_t n, float* pre, int64
                float* out2, uint64_t* pos, uint64_t* zero, uint64_t* grid, uint64_t* pz);
 template <int LV>
 int lv_forward_new(const NetDev& net, const float* xyz, int64_t n, float* pre, int64_t ld, int64_t V,
-                   int keep_from, const int32_t* sa, const int32_t* sb, int idx, int own_lo, int own_hi,
+                   int keep_from, const int32_t* sa, const int32_t* sb, int idx, const OwnBox& own,
                    uint64_t* pos, uint64_t* zero, uint64_t* grid, uint64_t* shared, int64_t* ctr, uint64_t* pz,
                    const float* col, hipStream_t s);
 template <int LV>
@@ -77,7 +77,7 @@ int lv_descend(const NetDev& net, int64_t G, const int32_t* glist, const int32_t
   template <> int lv_forward<L>(const NetDev&, const float*, int64_t, float*, int64_t, int, hipStream_t, float*, \
                                 uint64_t*, uint64_t*, uint64_t*, uint64_t*);                                  \
   template <> int lv_forward_new<L>(const NetDev&, const float*, int64_t, float*, int64_t, int64_t, int,        \
-                                    const int32_t*, const int32_t*, int, int, int, uint64_t*, uint64_t*,      \
+                                    const int32_t*, const int32_t*, int, const OwnBox&, uint64_t*, uint64_t*, \
                                     uint64_t*, uint64_t*, int64_t*, uint64_t*, const float*, hipStream_t);    \
   template <> int lv_sdf_grad<L>(const NetDev&, const float*, int64_t, float*, float*, hipStream_t);           \
   template <> int lv_skel_eval<L>(const NetDev&, int, int, int, int, int, int, float*, unsigned int*,         \
@@ -124,10 +124,10 @@ int launch_forward(const NetDev& net, const float* xyz, int64_t n, float* pre,
 // the plane column (xyz = slot V: written); cache planes >= keep_from at
 // slots V.., keys, shared
 // planes, failover predicate -> ctr[CTR_FAIL], new vertices outside the
-// owned slab (own_lo, own_hi] -> ctr[CTR_DUP]; then the override itself
+// owned box (common.h OwnBox) -> ctr[CTR_DUP]; then the override itself
 int launch_forward_new(const NetDev& net, const float* xyz, int64_t n, float* pre, int64_t ld,
                        int64_t V, int keep_from, const int32_t* sa, const int32_t* sb, int idx,
-                       int own_lo, int own_hi, uint64_t* pos, uint64_t* zero, uint64_t* grid,
+                       const OwnBox& own, uint64_t* pos, uint64_t* zero, uint64_t* grid,
                        uint64_t* shared, int64_t* ctr, uint64_t* pz, const float* col, hipStream_t s);
 int launch_override_new(int64_t n, int override_, const uint64_t* shared, float* pre, int64_t ld,
                         int keep_from, int64_t V, uint64_t* pos, uint64_t* zero,

@@ -119,7 +119,7 @@ template <int LV, int H, int NL>
 __global__ void __launch_bounds__(TNP_BLOCK, 4)
 k_forward_new(NetDev net, const float* xyz, int64_t n, float* __restrict__ pre,
               int64_t ld, int64_t V, int keep_from, const int32_t* __restrict__ sa,
-              const int32_t* __restrict__ sb, int idx, int own_lo, int own_hi, uint64_t* pos,
+              const int32_t* __restrict__ sb, int idx, OwnBox own, uint64_t* pos,
               uint64_t* zero, uint64_t* __restrict__ grid, uint64_t* __restrict__ shared,
               int64_t* __restrict__ ctr, uint64_t* __restrict__ pz, const float* __restrict__ scol) {
   constexpr int IN = 2 * LV;
@@ -217,13 +217,9 @@ k_forward_new(NetDev net, const float* xyz, int64_t n, float* __restrict__ pre,
   const uint64_t g = grid_word(mk, net.n_marks, eps, x);
   if (live) grid[V + i] = g;
   if (__ballot(live && bad) && tnp::lane() == 0) tnp::or_sticky(&ctr[CTR_FAIL], 1ull);
-  if (own_lo <= own_hi) {
-    // x-slab ownership of the new vertex: on mark plane p -> owned iff
-    // own_lo < p <= own_hi (plane 0 by the first shard); in the cell above
-    // mark c -> owned iff own_lo <= c < own_hi
-    const int c = tnp::grid_off(g, 0);
-    const bool owned = tnp::grid_zero(g, 0) ? ((c > own_lo || (own_lo == 0 && c == 0)) && c <= own_hi)
-                                            : (c >= own_lo && c < own_hi);
+  if (tnp::own_any(own)) {
+    // the shard's ownership of the new vertex (common.h OwnBox)
+    const bool owned = tnp::owned_by(own, g);
     const uint64_t halo = __ballot(live && !owned);
     if (halo && tnp::lane() == 0)
       atomicAdd((unsigned long long*)&ctr[CTR_DUP], (unsigned long long)__popcll(halo));
@@ -335,12 +331,12 @@ int lv_forward<LVC>(const NetDev& net, const float* xyz, int64_t n, float* pre, 
 
 template <>
 int lv_forward_new<LVC>(const NetDev& net, const float* xyz, int64_t n, float* pre, int64_t ld, int64_t V,
-                        int keep_from, const int32_t* sa, const int32_t* sb, int idx, int own_lo, int own_hi,
+                        int keep_from, const int32_t* sa, const int32_t* sb, int idx, const OwnBox& own,
                         uint64_t* pos, uint64_t* zero, uint64_t* grid, uint64_t* shared, int64_t* ctr, uint64_t* pz,
                         const float* col, hipStream_t s) {
 #define TNP_SHAPE_BODY                                                                                   \
   hipLaunchKernelGGL((k_forward_new<LVC, H, NL>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net, xyz, n, pre, ld, \
-                     V, keep_from, sa, sb, idx, own_lo, own_hi, pos, zero, grid, shared, ctr, pz, col);
+                     V, keep_from, sa, sb, idx, own, pos, zero, grid, shared, ctr, pz, col);
   TNP_SHAPE_SWITCH_ALL(net)
 #undef TNP_SHAPE_BODY
   TNP_CHECK(hipGetLastError());

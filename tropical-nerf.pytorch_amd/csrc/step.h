@@ -86,7 +86,7 @@ int launch_hits(const float* col, const uint8_t* alive, int64_t V, float eps, in
                 int64_t S, int64_t* ctr, hipStream_t s);
 int launch_new_members(int32_t* members, int64_t S, int64_t V, hipStream_t s);
 // new vertices (grid words) outside the owned x range (lo, hi] -> ctr[CTR_DUP] (lo > hi: nothing)
-int launch_count_unowned(const uint64_t* grid, int64_t n, int own_lo, int own_hi, int64_t* ctr, hipStream_t s);
+int launch_count_unowned(const uint64_t* grid, int64_t n, const OwnBox& own, int64_t* ctr, hipStream_t s);
 // sort-based cell bucketing: span counts (+ A), (cell, member) entries,
 // segment bounds of the cell-sorted entries, per-cell counts, key copies
 // M = capacity (S + V); the live member count S + ctr[CTR_H] is read on
@@ -235,18 +235,18 @@ uint64_t prune_mask(int idx, int last_plane);
 // ---- bucket.hip: members grouped by grid cell in spatial buckets ----------
 constexpr int BUCKET_MAX = 6144;        // member-pass buckets (17^3 lattice; 5 x 33 x 33 slab)
 constexpr int BUCKET_LOCAL_MAX = 4096;  // cells per bucket (16^3)
-// The buckets cover the cells (+2 coordinates) [0, NC) along y and z and
-// [xorg, xorg + xn) along x: an x-slab of a sharded complex buckets only its
-// own cells (an 8-rank 256^3 slab: 5 x 33 x 33 buckets of 8^3 cells instead
-// of 17^3 buckets of 16^3, 82 % of them empty)
+// The buckets cover the cells (+2 coordinates) [xorg, xorg + xn) along x,
+// and the same along y and z: a slab or block of a sharded complex buckets
+// only its own cells (an 8-rank 256^3 x-slab: 5 x 33 x 33 buckets of 8^3
+// cells instead of 17^3 buckets of 16^3, 82 % of them empty; a 2 x 2 x 2
+// block: 17^3 buckets of 8^3 cells, the 128^3 lattice's geometry)
 struct BucketGeom {
   int NC;    // cell coordinates per axis (n_marks + 2)
   int sh;    // log2 of the bucket edge in cells (the member passes' buckets)
-  int NBd;   // buckets along y and z
-  int NBx;   // buckets along x
-  int xorg;  // first cell coordinate along x
-  int xn;    // cells along x the buckets cover (NBx << sh)
-  int NB;    // NBx * NBd * NBd
+  int NBx, NBy, NBz;     // buckets along x, y, z
+  int xorg, yorg, zorg;  // first cell coordinate along each axis
+  int xn, yn, zn;        // cells along each axis the buckets cover (NB. << sh)
+  int NB;    // NBx * NBy * NBz
   // 1: two-level buckets.  The member passes bucket by 16^3 cells (sh = 4,
   // NB <= BUCKET_MAX bins in their LDS histograms); launch_bucket_refine
   // splits every bucket into its 8 octants of 8^3 cells, and the grouping
@@ -256,11 +256,11 @@ struct BucketGeom {
   int sub;
   int NG;  // group buckets: NB, or 8 NB when sub
 };
-// the bucket geometry for a complex inside the x mark planes [x0, x1]:
+// the bucket geometry for a complex inside the mark planes [lo[d], hi[d]]:
 // 8^3-cell buckets when their count fits BUCKET_MAX, else 16^3-cell member
 // buckets refined into 8^3-cell group buckets (sub); -1: the grid is too
 // fine for the bucket path (the radix-sort path takes it)
-int bucket_geometry(int n_marks, int x0, int x1, BucketGeom* g);
+int bucket_geometry(int n_marks, const int lo[3], const int hi[3], BucketGeom* g);
 // sub geometries: every 16^3-cell bucket's entries (bbase / ekv, the member
 // passes' output) regrouped by octant into ekv2, bases of the 8 NB group
 // buckets -> bbase2 [8 NB + 1]; entries keep their cell flags and vertex,

@@ -335,20 +335,13 @@ k_hit_append(const float* __restrict__ col, const uint8_t* __restrict__ alive, i
   hit_body(blockIdx.x, gridDim.x, col, alive, V, eps, members + S, ctr);
 }
 
-// new vertices outside this shard's owned x range (the flat path counts
+// new vertices outside this shard's owned box (the flat path counts
 // them in k_forward_new) -> ctr[CTR_DUP]: a kept curve-branch split on a
 // halo cell or on the shared boundary plane is another shard's
-__global__ void k_count_unowned(const uint64_t* __restrict__ grid, int64_t n, int own_lo, int own_hi,
+__global__ void k_count_unowned(const uint64_t* __restrict__ grid, int64_t n, OwnBox own,
                                 int64_t* __restrict__ ctr) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  bool halo = false;
-  if (i < n) {
-    const uint64_t g = grid[i];
-    const int c = tnp::grid_off(g, 0);
-    const bool owned = tnp::grid_zero(g, 0) ? ((c > own_lo || (own_lo == 0 && c == 0)) && c <= own_hi)
-                                            : (c >= own_lo && c < own_hi);
-    halo = !owned;
-  }
+  const bool halo = i < n && !tnp::owned_by(own, grid[i]);
   const uint64_t hb = __ballot(halo);
   if (hb && tnp::lane() == 0) atomicAdd((unsigned long long*)&ctr[CTR_DUP], (unsigned long long)__popcll(hb));
 }
@@ -1449,9 +1442,9 @@ int launch_hits(const float* col, const uint8_t* alive, int64_t V, float eps, in
   TNP_CHECK(hipGetLastError());
   return 0;
 }
-int launch_count_unowned(const uint64_t* grid, int64_t n, int own_lo, int own_hi, int64_t* ctr, hipStream_t s) {
-  if (n <= 0 || own_lo > own_hi) return 0;
-  hipLaunchKernelGGL(k_count_unowned, dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, grid, n, own_lo, own_hi, ctr);
+int launch_count_unowned(const uint64_t* grid, int64_t n, const OwnBox& own, int64_t* ctr, hipStream_t s) {
+  if (n <= 0 || !tnp::own_any(own)) return 0;
+  hipLaunchKernelGGL(k_count_unowned, dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, grid, n, own, ctr);
   TNP_CHECK(hipGetLastError());
   return 0;
 }

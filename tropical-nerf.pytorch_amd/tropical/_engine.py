@@ -91,6 +91,20 @@ class Engine:
                                                  C.byref(V), C.byref(E)), "tnp_engine_lattice")
         return V.value, E.value
 
+    @staticmethod
+    def _i3(v):
+        a = (C.c_int32 * 3)(*[int(x) for x in v])
+        return a
+
+    def lattice_box(self, lo, hi, keep_all: bool = False):
+        """The lattice over the marks restricted to the box of mark indices
+        [lo[d], hi[d]] per axis (a block of a sharded lattice; the whole grid
+        is lattice())."""
+        V, E = C.c_int64(), C.c_int64()
+        _hip.check(_hip.lib().tnp_engine_lattice_box(self.h, self._i3(lo), self._i3(hi), int(keep_all), self._s,
+                                                     C.byref(V), C.byref(E)), "tnp_engine_lattice_box")
+        return V.value, E.value
+
     SKELETON_MODES = {"distance": 0, "sign": 1}
 
     def skeleton(self, unit: int = 128, size: float = None, mode: str = "distance"):
@@ -142,6 +156,12 @@ class Engine:
         (lo > hi: everything); splits outside are reported as S_dup."""
         _hip.check(_hip.lib().tnp_engine_set_owned(self.h, int(lo), int(hi)), "tnp_engine_set_owned")
 
+    def set_owned_box(self, lo, hi):
+        """Along axis d this shard owns mark planes (lo[d], hi[d]] and the
+        cells between (lo[d] > hi[d]: the axis is not cut)."""
+        _hip.check(_hip.lib().tnp_engine_set_owned_box(self.h, self._i3(lo), self._i3(hi)),
+                   "tnp_engine_set_owned_box")
+
     def set_eps(self, eps: float = None):
         """subpoly's eps argument (None: Net.eps): the steps' sign test, split
         point, hits and failover, the surface and the faces take it; the
@@ -155,6 +175,12 @@ class Engine:
         with its halo; x1 < x0: anywhere): the step's spatial buckets cover
         only those cells.  lattice() sets it, load()/skeleton() reset it."""
         _hip.check(_hip.lib().tnp_engine_set_xspan(self.h, int(x0), int(x1)), "tnp_engine_set_xspan")
+        return self
+
+    def set_span(self, lo, hi):
+        """Per axis, the loaded complex lies between mark planes lo[d] and
+        hi[d] (hi[d] < lo[d]: anywhere along d)."""
+        _hip.check(_hip.lib().tnp_engine_set_span(self.h, self._i3(lo), self._i3(hi)), "tnp_engine_set_span")
         return self
 
     def kernel_timer(self, on: bool):

@@ -74,6 +74,7 @@ SIGNATURES = {
     "tnp_shm_allreduce": (C.c_int, [_VP, _VP, C.c_int, C.c_int, _VP]),
     "tnp_engine_skeleton_mode": (C.c_int, [_VP, C.c_int, _F, C.c_int, _VP, _P64, _P64]),
     "tnp_engine_lattice": (C.c_int, [_VP, C.c_int, C.c_int, C.c_int, _VP, _P64, _P64]),
+    "tnp_engine_lattice_box": (C.c_int, [_VP, _P32, _P32, C.c_int, _VP, _P64, _P64]),
     "tnp_engine_active_planes": (C.c_int, [_VP, C.c_int, _PU64, _VP]),
     "tnp_engine_split": (C.c_int, [_VP, C.c_int, _VP, _P64, _P32]),
     "tnp_engine_finish": (C.c_int, [_VP, C.c_int, C.c_int, C.c_int, _VP, C.POINTER(TnpStepStats)]),
@@ -85,6 +86,8 @@ SIGNATURES = {
     "tnp_engine_faces_export": (C.c_int, [_VP, _VP, _VP, _VP]),
     "tnp_engine_set_owned": (C.c_int, [_VP, C.c_int, C.c_int]),
     "tnp_engine_set_xspan": (C.c_int, [_VP, C.c_int, C.c_int]),
+    "tnp_engine_set_owned_box": (C.c_int, [_VP, _P32, _P32]),
+    "tnp_engine_set_span": (C.c_int, [_VP, _P32, _P32]),
     "tnp_engine_set_eps": (C.c_int, [_VP, C.c_float]),
     "tnp_engine_run_steps": (C.c_int, [_VP, _VP, C.POINTER(TnpStepStats), C.c_int, _P32]),
     "tnp_engine_set_curve": (C.c_int, [_VP, C.c_int]),

@@ -1,9 +1,13 @@
-"""Multi-GPU x-slab sharding of the extraction.
+"""Multi-GPU sharding of the extraction: x-slabs or blocks.
 
 One process per GPU.  The cells between mark planes cuts[r] and cuts[r+1]
 of the x axis belong to rank r, which also owns the mark planes
-(cuts[r], cuts[r+1]] (rank 0 also plane 0).  Each rank extracts the lattice
-of its cells plus a HALO of HALO cell columns on either side (slab_marks),
+(cuts[r], cuts[r+1]] (rank 0 also plane 0).  Blocks (class Blocks) apply
+the same rule along every cut axis: a px x py x pz split of the lattice,
+whose cut faces -- and so halos -- are smallest (bench.py's N > 1 path:
+2 x 2 x 2 blocks of the 256^3 lattice at N = 8, 6.7 % redundant cells per
+rank at a 3-cell halo, against 15.8 % for 8 x-slabs).  Each rank extracts
+the lattice of its cells plus a HALO of HALO cell columns on either side (slab_marks),
 with the reference's two whole-complex decisions made global (``allreduce``
 of run_steps: "does anything split", subpoly.py:110, and the failover
 override, subpoly_debug.py:43-49).
@@ -23,11 +27,12 @@ the widths of HALOS in turn until halo_check (below) passes.
 
 Stitching (one pair of all_gathers, RCCL over xGMI / gloo on CPU):
 * vertex owner = the rank owning its cell or plane (grid sense, eps rule);
-* edge owner = the larger owner of its endpoints; a rank keeps its edges;
+* edge owner = the owner of the cell the edge lies in (edge_owner); a rank
+  keeps its edges;
 * owned vertices get global ids by an exclusive scan of the owned counts;
-* a rank's kept edges can reference vertices of the lower neighbour only on
-  the shared plane: the lower rank's owned upper-plane records (coordinate
-  bits + global id) are matched bitwise on the device.
+* a rank's kept edges can reference other ranks' vertices only on its lower
+  faces: the owners' records on their upper faces (coordinate bits + global
+  id) are matched bitwise on the device.
 
 Regions are (grid cell x sign pattern), so pairs, connecting edges and faces
 never span cells: the stitched complex equals the unsharded one up to the
@@ -123,6 +128,92 @@ def slab_marks(cuts: list, rank: int, halo: int = HALO):
     return max(cuts[rank] - halo, cuts[0]), min(cuts[rank + 1] + halo, cuts[-1])
 
 
+def block_dims(world: int) -> tuple:
+    """(px, py, pz), px * py * pz == world: the most cubic split of the ranks
+    into blocks (px >= py >= pz; 8 -> 2 x 2 x 2, 4 -> 2 x 2 x 1, 2 -> 2 x 1 x 1)."""
+    best = None
+    for px in range(1, world + 1):
+        if world % px:
+            continue
+        for py in range(1, px + 1):
+            if (world // px) % py:
+                continue
+            pz = world // px // py
+            if pz > py:
+                continue
+            key = (px - pz, -px)
+            if best is None or key < best[0]:
+                best = (key, (px, py, pz))
+    return best[1]
+
+
+class Blocks:
+    """A split of the mark grid into px x py x pz blocks, one per rank.
+
+    Along axis d block i OWNS the cells cuts[d][i] <= c < cuts[d][i+1] and
+    the mark planes cuts[d][i] < p <= cuts[d][i+1] (block 0 also plane 0) --
+    x-slabs are the (world, 1, 1) case (``Blocks.xslabs``).  rank =
+    (ix * py + iy) * pz + iz.  Why blocks: a shard extracts its block plus a
+    halo of cells beyond every cut face, and a block of a 256^3 lattice on 8
+    ranks has three such faces of 128^2 cells where an x-slab has two of
+    256^2 -- 6 % redundant cells at a 3-cell halo instead of 16 %."""
+
+    def __init__(self, n_marks: int, dims, cuts=None):
+        self.n_marks = int(n_marks)
+        self.dims = tuple(int(p) for p in dims)
+        self.cuts = [list(c) for c in cuts] if cuts is not None else [slab_cuts(n_marks, p) for p in self.dims]
+        self.world = self.dims[0] * self.dims[1] * self.dims[2]
+
+    @classmethod
+    def xslabs(cls, cuts: list):
+        n = cuts[-1] + 1
+        return cls(n, (len(cuts) - 1, 1, 1), [list(cuts), [0, n - 1], [0, n - 1]])
+
+    def index(self, rank: int) -> tuple:
+        _, py, pz = self.dims
+        return rank // (py * pz), (rank // pz) % py, rank % pz
+
+    def rank_of(self, idx) -> int:
+        _, py, pz = self.dims
+        return (idx[0] * py + idx[1]) * pz + idx[2]
+
+    def owned(self, rank: int):
+        """(lo, hi) of tnp_engine_set_owned_box: per axis the owned planes
+        (lo, hi]; lo > hi on an axis that is not cut."""
+        idx = self.index(rank)
+        lo, hi = [1, 1, 1], [0, 0, 0]
+        for d in range(3):
+            if self.dims[d] > 1:
+                lo[d], hi[d] = self.cuts[d][idx[d]], self.cuts[d][idx[d] + 1]
+        return lo, hi
+
+    def box(self, rank: int, halo: int):
+        """Mark indices [lo[d], hi[d]] the rank extracts: its block plus
+        `halo` cells beyond every cut face."""
+        idx = self.index(rank)
+        lo, hi = [0, 0, 0], [0, 0, 0]
+        for d in range(3):
+            c = self.cuts[d]
+            lo[d] = max(c[idx[d]] - halo, c[0])
+            hi[d] = min(c[idx[d] + 1] + halo, c[-1])
+        return lo, hi
+
+    def redundant_frac(self, rank: int, halo: int) -> float:
+        """Share of the rank's extracted cells that another rank owns."""
+        lo, hi = self.box(rank, halo)
+        idx = self.index(rank)
+        mine = tot = 1
+        for d in range(3):
+            mine *= self.cuts[d][idx[d] + 1] - self.cuts[d][idx[d]]
+            tot *= hi[d] - lo[d]
+        return 1.0 - mine / tot
+
+
+def as_blocks(part) -> Blocks:
+    """x-slab cuts (a list) or a Blocks split."""
+    return part if isinstance(part, Blocks) else Blocks.xslabs(part)
+
+
 def balanced_cuts(cell_load: Tensor, world: int) -> list:
     """Cut the x cells 0..n-1 (n = n_marks - 1) into `world` slabs of about
     equal load (e.g. skeleton edges per x cell); every slab gets >= 1 cell."""
@@ -139,27 +230,73 @@ def balanced_cuts(cell_load: Tensor, world: int) -> list:
     return cuts
 
 
-def x_grid(vertices: Tensor, marks: Tensor, eps: float = 1e-4):
-    """(offset, on_mark) of the x coordinate in the grid-region sense of
+def axis_grid(vertices: Tensor, marks: Tensor, eps: float = 1e-4, d: int = 0):
+    """(offset, on_mark) of coordinate d in the grid-region sense of
     TropicalHashGrid.region (tropical.py:227-236) on x01 = (x + 1) / 2
     (Net.preprocess, model.py:78-79) -- the engine's grid word, bit for bit."""
-    x01 = (vertices[:, 0] + 1.0) / 2.0
+    x01 = (vertices[:, d] + 1.0) / 2.0
     off = torch.searchsorted(marks, x01 + eps) - 1
     mk = marks[torch.where(off < 0, off + marks.shape[0], off)]
     return off, ~((mk - x01).abs() > eps)
 
 
-def owner_of(vertices: Tensor, marks: Tensor, cuts: list, eps: float = 1e-4) -> Tensor:
-    """Owning rank of each vertex: plane p -> rank r with cuts[r] < p <=
-    cuts[r+1] (plane cuts[0] -> rank 0); cell c -> rank r with cuts[r] <= c
-    < cuts[r+1] (the engine's tnp_engine_set_owned rule)."""
-    off, on = x_grid(vertices, marks, eps)
-    c = torch.tensor(cuts, dtype=torch.int64, device=vertices.device)
-    # planes: count of cuts strictly below p, minus one; cells: cuts <= c, minus one
-    r_plane = torch.searchsorted(c, off, right=False) - 1
+def x_grid(vertices: Tensor, marks: Tensor, eps: float = 1e-4):
+    return axis_grid(vertices, marks, eps, 0)
+
+
+def _axis_index(off: Tensor, on: Tensor, cuts: list, plane: bool = True) -> Tensor:
+    """Block index along one axis: plane p -> i with cuts[i] < p <= cuts[i+1]
+    (plane cuts[0] -> 0), cell c -> i with cuts[i] <= c < cuts[i+1]."""
+    c = torch.tensor(cuts, dtype=torch.int64, device=off.device)
     r_cell = torch.searchsorted(c, off, right=True) - 1
-    r = torch.where(on, r_plane, r_cell)
+    if plane:
+        r = torch.where(on, torch.searchsorted(c, off, right=False) - 1, r_cell)
+    else:
+        r = r_cell
     return r.clamp(0, len(cuts) - 2)
+
+
+def owner_of(vertices: Tensor, marks: Tensor, cuts, eps: float = 1e-4) -> Tensor:
+    """Owning rank of each vertex: along every cut axis, plane p -> block i
+    with cuts[i] < p <= cuts[i+1] (plane cuts[0] -> block 0), cell c -> block
+    i with cuts[i] <= c < cuts[i+1] (the engine's tnp_engine_set_owned_box
+    rule).  cuts: x-slab cuts (a list) or Blocks."""
+    B = as_blocks(cuts)
+    idx = []
+    for d in range(3):
+        if B.dims[d] == 1:
+            idx.append(torch.zeros(vertices.shape[0], dtype=torch.int64, device=vertices.device))
+            continue
+        off, on = axis_grid(vertices, marks, eps, d)
+        idx.append(_axis_index(off, on, B.cuts[d]))
+    return B.rank_of(idx)
+
+
+def edge_owner(vertices: Tensor, edges: Tensor, marks: Tensor, cuts, eps: float = 1e-4) -> Tensor:
+    """Owning rank of each edge: the owner of the cell it lies in, taken as
+    the highest cell whose closure holds both endpoints (per axis the lower
+    of the endpoints' offsets) -- a cell of the owner's block, so the edge is
+    one of its own cells' and both endpoints lie in that block or on its
+    lower faces."""
+    B = as_blocks(cuts)
+    e = edges.to(vertices.device)
+    idx = []
+    for d in range(3):
+        if B.dims[d] == 1:
+            idx.append(torch.zeros(e.shape[0], dtype=torch.int64, device=vertices.device))
+            continue
+        off, _ = axis_grid(vertices, marks, eps, d)
+        cell = torch.minimum(off[e[:, 0]], off[e[:, 1]])
+        idx.append(_axis_index(cell, None, B.cuts[d], plane=False))
+    return B.rank_of(idx)
+
+
+def owned_masks(vertices: Tensor, edges: Tensor, marks: Tensor, cuts, rank: int, eps: float = 1e-4):
+    """(owned vertex mask, kept edge mask) of `rank` over its local arrays:
+    the share stitch() contributes to the global complex."""
+    marks = marks.to(vertices.device)
+    return (owner_of(vertices, marks, cuts, eps) == rank,
+            edge_owner(vertices, edges, marks, cuts, eps) == rank)
 
 
 def slab_restrict(vertices: Tensor, edges: Tensor, marks: Tensor, x0: int, x1: int,
@@ -223,61 +360,105 @@ def complex_hash(vertices: Tensor, edges: Tensor, vmask: Tensor = None, emask: T
     return int(hv.sum().item()), int(he.sum().item())
 
 
-def cut_fingerprint(vertices: Tensor, edges: Tensor, marks: Tensor, cut: int, eps: float = 1e-4):
+def cut_fingerprint(vertices: Tensor, edges: Tensor, marks: Tensor, cut: int, eps: float = 1e-4,
+                    axis: int = 0, across=None):
     """(#vertices, #edges, vertex-set hash, edge-set hash) of the complex
-    strictly between mark planes cut-1 and cut+1: cells cut-1 and cut and
-    the cut plane, edges with both endpoints there."""
-    off, on = x_grid(vertices, marks.to(vertices.device), eps)
+    strictly between mark planes cut-1 and cut+1 of `axis`: cells cut-1 and
+    cut and the cut plane, edges with both endpoints there.  across: {axis b:
+    (lo, hi)} further restricts the region along the other cut axes of a
+    block split to the two blocks' common range plus one cell beyond each
+    of its faces (cells lo-1 .. hi, planes lo .. hi)."""
+    marks = marks.to(vertices.device)
+    off, on = axis_grid(vertices, marks, eps, axis)
     sel = torch.where(on, off == cut, (off == cut - 1) | (off == cut))
+    for b, (lo, hi) in (across or {}).items():
+        ob, nb = axis_grid(vertices, marks, eps, b)
+        sel &= torch.where(nb, (ob >= lo) & (ob <= hi), (ob >= lo - 1) & (ob <= hi))
     e = edges.to(vertices.device)
     emask = sel[e[:, 0]] & sel[e[:, 1]]
     hv, he = complex_hash(vertices, e, sel, emask)
     return [int(sel.sum().item()), int(emask.sum().item()), hv, he]
 
 
-def halo_check(vertices: Tensor, edges: Tensor, marks: Tensor, cuts: list, eps: float = 1e-4,
+def halo_check(vertices: Tensor, edges: Tensor, marks: Tensor, cuts, eps: float = 1e-4,
                group=None, raise_: bool = True):
-    """Compare, across every cut, the two neighbours' complexes next to the
-    cut (cut_fingerprint); raise RuntimeError on any difference (raise_=False:
-    return None instead, on every rank).  Returns the per-cut fingerprints
-    (rank 0's view) for logging."""
+    """Compare, across every cut face, the two neighbouring blocks'
+    complexes next to the face (cut_fingerprint over the face's range);
+    raise RuntimeError on any difference (raise_=False: return None instead,
+    on every rank).  Returns the per-face fingerprints (rank 0's view) for
+    logging.  cuts: x-slab cuts (a list) or Blocks.
+
+    A block's own errors start at its outer halo boundary; to reach a cell it
+    owns they must cross one of its faces, where the neighbour across that
+    face -- for which those cells are interior along that axis -- computed
+    them from a different boundary (an error from a corner of the halo
+    differs from at least one of the two or three neighbours whose faces
+    meet there)."""
+    B = as_blocks(cuts)
     rank, world = dist.get_rank(group), dist.get_world_size(group)
-    mine = torch.zeros(2, 4, dtype=torch.int64, device=comm_device(group, vertices.device))
-    if rank > 0:
-        mine[0] = torch.tensor(cut_fingerprint(vertices, edges, marks, cuts[rank], eps))
-    if rank < world - 1:
-        mine[1] = torch.tensor(cut_fingerprint(vertices, edges, marks, cuts[rank + 1], eps))
+    if world != B.world:
+        raise ValueError(f"halo_check: {world} ranks for a split into {B.world} blocks")
+    idx = B.index(rank)
+    mine = torch.zeros(3, 2, 4, dtype=torch.int64, device=comm_device(group, vertices.device))
+
+    def across(i):
+        return {b: (B.cuts[b][i[b]], B.cuts[b][i[b] + 1]) for b in range(3) if B.dims[b] > 1 and b != a}
+
+    for a in range(3):
+        if B.dims[a] == 1:
+            continue
+        if idx[a] > 0:
+            mine[a, 0] = torch.tensor(cut_fingerprint(vertices, edges, marks, B.cuts[a][idx[a]], eps, a, across(idx)))
+        if idx[a] < B.dims[a] - 1:
+            mine[a, 1] = torch.tensor(cut_fingerprint(vertices, edges, marks, B.cuts[a][idx[a] + 1], eps, a,
+                                                      across(idx)))
     allv = [torch.zeros_like(mine) for _ in range(world)]
     dist.all_gather(allv, mine, group=group)
-    bad = []
-    for r in range(world - 1):
-        lo, hi = allv[r][1].tolist(), allv[r + 1][0].tolist()
-        if lo != hi:
-            bad.append(f"cut {cuts[r + 1]}: rank {r} sees {lo[:2]} (hash {lo[2]:x}/{lo[3]:x}), "
-                       f"rank {r + 1} sees {hi[:2]} (hash {hi[2]:x}/{hi[3]:x})")
+    bad, seen = [], []
+    for r in range(world):
+        ir = B.index(r)
+        for a in range(3):
+            if B.dims[a] == 1 or ir[a] == B.dims[a] - 1:
+                continue
+            up = list(ir)
+            up[a] += 1
+            q = B.rank_of(up)
+            lo, hi = allv[r][a, 1].tolist(), allv[q][a, 0].tolist()
+            seen.append(lo)
+            if lo != hi:
+                bad.append(f"cut {B.cuts[a][ir[a] + 1]} of axis {'xyz'[a]}: rank {r} sees {lo[:2]} "
+                           f"(hash {lo[2]:x}/{lo[3]:x}), rank {q} sees {hi[:2]} (hash {hi[2]:x}/{hi[3]:x})")
     if bad:
         if not raise_:
             return None
         raise RuntimeError("halo_check: the shards disagree next to a cut (halo too narrow): "
                            + "; ".join(bad))
-    return [allv[r][1].tolist() for r in range(world - 1)]
+    return seen
 
 
-def stitch(vertices: Tensor, edges: Tensor, marks: Tensor, cuts: list, eps: float = 1e-4,
+def stitch(vertices: Tensor, edges: Tensor, marks: Tensor, cuts, eps: float = 1e-4,
            group=None, masks: bool = False):
-    """Stitch this rank's (halo) slab complex into the global one.
+    """Stitch this rank's (halo) slab or block complex into the global one.
 
     vertices [V, 3] fp32, edges [E, 2] int64 (local ids), marks [M] fp32
-    (net.enc.marks), cuts from slab_cuts.  Returns (owned_vertices [V', 3],
-    first_global_id, global_edges [E', 2] int64): the owned vertices carry
-    global ids first_global_id + arange(V'); global_edges are this rank's
-    share of the global edge list.  masks=True appends the (owned vertex,
-    kept edge) masks over the local arrays."""
+    (net.enc.marks), cuts: x-slab cuts from slab_cuts, or Blocks.  Returns
+    (owned_vertices [V', 3], first_global_id, global_edges [E', 2] int64):
+    the owned vertices carry global ids first_global_id + arange(V');
+    global_edges are this rank's share of the global edge list (edge_owner:
+    the edges of its own cells).  masks=True appends the (owned vertex, kept
+    edge) masks over the local arrays.
+
+    A kept edge lies in one of the rank's cells, so an endpoint it does not
+    own lies on one of its LOWER faces, owned by the block below along that
+    axis (or diagonally below): every rank publishes its owned vertices on
+    its upper faces (coordinate bits + global id) and looks the others up
+    there, bitwise, on the device."""
+    B = as_blocks(cuts)
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     dev = vertices.device
     marks = marks.to(dev)
     nv = vertices.shape[0]
-    owner = owner_of(vertices, marks, cuts, eps)
+    owner = owner_of(vertices, marks, B, eps)
     own = owner == rank
     n_own = int(own.sum().item())
     cnt = torch.tensor([n_own], dtype=torch.int64, device=dev)
@@ -287,34 +468,37 @@ def stitch(vertices: Tensor, edges: Tensor, marks: Tensor, cuts: list, eps: floa
     gid = torch.full((nv,), -1, dtype=torch.int64, device=dev)
     gid[own] = first + torch.arange(n_own, dtype=torch.int64, device=dev)
 
-    # owned records on the upper cut plane, for the upper neighbour
+    # owned records on an upper cut face, for the blocks above
     bits = vertices.contiguous().view(torch.int32).to(torch.int64)
-    if rank < world - 1:
-        off, on = x_grid(vertices, marks, eps)
-        up = own & on & (off == cuts[rank + 1])
-    else:
-        up = torch.zeros(nv, dtype=torch.bool, device=dev)
+    idx = B.index(rank)
+    up = torch.zeros(nv, dtype=torch.bool, device=dev)
+    for d in range(3):
+        if idx[d] < B.dims[d] - 1:
+            off, on = axis_grid(vertices, marks, eps, d)
+            up |= on & (off == B.cuts[d][idx[d] + 1])
+    up &= own
     recs = _all_gather_padded(torch.cat([bits[up], gid[up, None]], dim=1), group)
 
     e_all = edges.to(dev)
-    keep = torch.maximum(owner[e_all[:, 0]], owner[e_all[:, 1]]) == rank
+    keep = edge_owner(vertices, e_all, marks, B, eps) == rank
     e = e_all[keep]
     used = torch.zeros(nv, dtype=torch.bool, device=dev)
     used[e.reshape(-1)] = True
     need = used & ~own
     if bool(need.any()):
-        if rank == 0 or bool((owner[need] != rank - 1).any()):
-            raise RuntimeError("stitch: a kept edge references a vertex beyond the lower cut plane")
-        prev = recs[rank - 1]
         ni = torch.nonzero(need).squeeze(1)
+        below = [r for r in range(world) if r != rank and all(a <= b for a, b in zip(B.index(r), idx))]
+        if not below:
+            raise RuntimeError("stitch: a kept edge references a vertex beyond the block's lower faces")
+        prev = torch.cat([recs[r] for r in below], dim=0)
         keys = torch.cat([prev[:, :3], bits[ni]], dim=0)
         uniq, inv = torch.unique(keys, dim=0, return_inverse=True)
         table = torch.full((uniq.shape[0],), -1, dtype=torch.int64, device=dev)
         table[inv[: prev.shape[0]]] = prev[:, 3]
         got = table[inv[prev.shape[0]:]]
         if bool((got < 0).any()):
-            raise RuntimeError(f"stitch: {int((got < 0).sum())} vertices on cut plane "
-                               f"{cuts[rank]} have no counterpart on rank {rank - 1}")
+            raise RuntimeError(f"stitch: {int((got < 0).sum())} vertices on the lower faces of rank "
+                               f"{rank} have no counterpart on the ranks below")
         gid[ni] = got
     if masks:
         return vertices[own], first, gid[e], own, keep

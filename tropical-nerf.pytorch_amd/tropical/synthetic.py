@@ -84,12 +84,20 @@ def slab_lattice(marks: np.ndarray, x0: int, x1: int):
     x-edges, then y, then z, each (hi, lo) -- an order-preserving subsequence
     of lattice_edges(N) restricted to the slab, so shards number and orient
     every shared element exactly as the unsharded run does."""
+    n = np.asarray(marks).shape[0]
+    return block_lattice(marks, (x0, 0, 0), (x1, n - 1, n - 1))
+
+
+def block_lattice(marks: np.ndarray, lo, hi):
+    """The box of mark indices [lo[d], hi[d]] of the full lattice, laid out
+    as tnp_engine_lattice_box does: vertex (i, j, k) -> id (i - lo0) ny nz +
+    (j - lo1) nz + (k - lo2); x-edges, then y, then z, each (hi, lo)."""
     m = np.asarray(marks, dtype=np.float32)
-    n = m.shape[0]
-    nx = x1 - x0 + 1
-    g = np.stack(np.meshgrid(m[x0:x1 + 1], m, m, indexing="ij"), -1).reshape(-1, 3)
+    n = [hi[d] - lo[d] + 1 for d in range(3)]
+    g = np.stack(np.meshgrid(m[lo[0]:hi[0] + 1], m[lo[1]:hi[1] + 1], m[lo[2]:hi[2] + 1], indexing="ij"),
+                 -1).reshape(-1, 3)
     verts = (g * np.float32(2) - np.float32(1)).astype(np.float32)
-    ids = np.arange(nx * n * n, dtype=np.int64).reshape(nx, n, n)
+    ids = np.arange(n[0] * n[1] * n[2], dtype=np.int64).reshape(*n)
     ex = np.stack([ids[1:, :, :].reshape(-1), ids[:-1, :, :].reshape(-1)], -1)
     ey = np.stack([ids[:, 1:, :].reshape(-1), ids[:, :-1, :].reshape(-1)], -1)
     ez = np.stack([ids[:, :, 1:].reshape(-1), ids[:, :, :-1].reshape(-1)], -1)
