@@ -98,7 +98,7 @@ def _worker(rank, world, port, outdir, case, mode):
         else:  # "skeleton" (flat) or "curve" (force=False: the curve branch's decisions go
             # through the engine's collective callback)
             eng, owned, first, gE, cuts = D.subpoly_sharded(net, 1.2, allreduce=coll, stats=stats,
-                                                            force=mode != "curve")
+                                                            force=mode != "curve", blocks=blocks)
             Vl, El, _ = eng.export()
             Vl, El = Vl.cpu(), El.cpu()
             own, keep = D.owned_masks(Vl, El, net.enc.marks.cpu(), cuts, rank)
@@ -123,7 +123,8 @@ def _worker(rank, world, port, outdir, case, mode):
         dist.all_reduce(single_ok, op=dist.ReduceOp.MIN)
         if rank == 0:
             np.savez(os.path.join(outdir, "out.npz"), tot=tot.numpy(), V=SV.numpy(), E=SE.numpy(),
-                     cuts=np.array(cuts), single_ok=single_ok.numpy())
+                     cuts=np.array(cuts.cuts[0] if isinstance(cuts, D.Blocks) else cuts),
+                     single_ok=single_ok.numpy())
     finally:
         dist.destroy_process_group()
 
@@ -172,14 +173,18 @@ def test_sharded_lattice_engine(cuda, tmp_path, case, world, mode):
     assert z["E"].min() >= 0 and z["E"].max() < want[0]
 
 
-@pytest.mark.parametrize("case,world", [("large_sphere", 2), ("large_sphere", 3), ("large_sphere", 8),
-                                        ("small_sphere", 2)])
-def test_sharded_stanford_net(cuda, tmp_path, case, world):
+@pytest.mark.parametrize("case,world,mode", [("large_sphere", 2, "skeleton"), ("large_sphere", 3, "skeleton"),
+                                             ("large_sphere", 8, "skeleton"), ("small_sphere", 2, "skeleton"),
+                                             ("large_sphere", 8, "skeleton_blocks")])
+def test_sharded_stanford_net(cuda, tmp_path, case, world, mode):
+    """x-slabs of equal skeleton-edge load, and (skeleton_blocks) 2 x 2 x 2
+    blocks cut at equal marginal load per axis."""
     d, V, E, want = _unsharded(cuda, case, "skeleton")
-    z = _run(tmp_path, case, "skeleton", world)
+    z = _run(tmp_path, case, mode, world)
     assert tuple(int(x) for x in z["tot"]) == want
     cuts = z["cuts"].tolist()
-    assert cuts[0] == 0 and cuts[-1] == len(d["marks"]) - 1 and len(cuts) == world + 1
+    assert cuts[0] == 0 and cuts[-1] == len(d["marks"]) - 1
+    assert len(cuts) == (world + 1 if mode == "skeleton" else 3)
 
 
 @pytest.mark.parametrize("case,world", [("small_sphere_curve", 2), ("small_sphere_curve", 3),

@@ -247,6 +247,14 @@ def test_slab_restrict_matches_slab_lattice():
         # the lattice slab orders x-edges, then y, then z: the same subsequence
         assert sorted(map(tuple, e.tolist())) == sorted(map(tuple, se.tolist()))
         assert e.shape[0] == se.shape[0]
+    # boxes (blocks with their halo) likewise
+    from tropical.distributed import box_restrict
+    from tropical.synthetic import block_lattice
+    for lo, hi in (((0, 3, 5), (9, 14, 20)), ((12, 0, 0), (n - 1, 11, n - 1))):
+        v, e = box_restrict(V, E, torch.from_numpy(d["marks"]), lo, hi)
+        sv, se = block_lattice(d["marks"], lo, hi)
+        assert torch.equal(v, torch.from_numpy(sv))
+        assert sorted(map(tuple, e.tolist())) == sorted(map(tuple, se.tolist()))
 
 
 def _shm_worker(rank, world, port, outdir):

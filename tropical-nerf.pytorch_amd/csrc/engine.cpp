@@ -2185,8 +2185,8 @@ extern "C" int tnp_engine_faces(tnp_engine* e, void* stream, int64_t* n_tri, int
     const FillOp f{ctr + CTR_TRI, 2 * sizeof(int64_t), 0};
     if (launch_fill(&f, 1, s)) return -1;
   }
-  if (launch_max_i32(P<int32_t>(fs[FS_CALL]), F, ctr + CTR_TRI, s)) return -1;
-  if (launch_max_i32(P<int32_t>(fs[FS_CNZ]), F, ctr + CTR_FACES, s)) return -1;
+  if (launch_max_i32(P<int32_t>(fs[FS_CALL]), F, ctr + CTR_TRI, s, P<int32_t>(fs[FS_CNZ]), ctr + CTR_FACES))
+    return -1;
   if (read_ctr(e, s)) return -1;
   // F5: fan triangles, fan-position-major
   const int64_t nb = fan_blocks(F);

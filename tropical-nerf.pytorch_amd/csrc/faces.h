@@ -32,4 +32,6 @@ int launch_fan_hist(int64_t F, const int32_t* cnt, int T, int32_t* hist, hipStre
 int launch_fan_emit(int64_t F, const int32_t* frow, const int32_t* ordv, const int64_t* roff,
                     const int32_t* rcnt, const int32_t* cnt, int T, const int64_t* base, int floats,
                     const float* xyz, int64_t* tri, float* fc, hipStream_t s);
-int launch_max_i32(const int32_t* a, int64_t n, int64_t* out, hipStream_t s);
+// max of a (and of b, if given) over [0, n) -> *out (*out_b), zeroed by the caller
+int launch_max_i32(const int32_t* a, int64_t n, int64_t* out, hipStream_t s, const int32_t* b = nullptr,
+                   int64_t* out_b = nullptr);

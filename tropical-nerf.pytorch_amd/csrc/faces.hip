@@ -970,20 +970,44 @@ int launch_fan_emit(int64_t F, const int32_t* frow, const int32_t* ordv, const i
 }
 
 namespace {
-__global__ void k_max_i32(const int32_t* __restrict__ a, int64_t n, int64_t* __restrict__ out) {
-  int m = 0;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+// max of a[0..n) -> *out and (b != null) of b[0..n) -> *out_b: the waves
+// reduce in LDS, one atomic per workgroup and array on a grid of at most 256
+// (one per wave on one word serialised ~4,000 atomics: ~50 us per call)
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_max_i32(const int32_t* __restrict__ a, const int32_t* __restrict__ b, int64_t n, int64_t* __restrict__ out,
+          int64_t* __restrict__ out_b) {
+  __shared__ int lds[2][TNP_WAVES];
+  int m = 0, mb = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     m = max(m, a[i]);
+    if (b) mb = max(mb, b[i]);
+  }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
-  if (tnp::lane() == 0) atomicMax((unsigned long long*)out, (unsigned long long)m);
+  for (int o = 32; o > 0; o >>= 1) {
+    m = max(m, __shfl_xor(m, o, 64));
+    mb = max(mb, __shfl_xor(mb, o, 64));
+  }
+  if (tnp::lane() == 0) {
+    lds[0][tnp::wave()] = m;
+    lds[1][tnp::wave()] = mb;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int w = 1; w < TNP_WAVES; ++w) {
+      m = max(m, lds[0][w]);
+      mb = max(mb, lds[1][w]);
+    }
+    atomicMax((unsigned long long*)out, (unsigned long long)m);
+    if (b) atomicMax((unsigned long long*)out_b, (unsigned long long)mb);
+  }
 }
 }  // namespace
 
-int launch_max_i32(const int32_t* a, int64_t n, int64_t* out, hipStream_t s) {
+int launch_max_i32(const int32_t* a, int64_t n, int64_t* out, hipStream_t s, const int32_t* b, int64_t* out_b) {
   if (n <= 0) return 0;
-  unsigned g = (unsigned)std::min<int64_t>(tnp_grid(n), 1024);
-  hipLaunchKernelGGL(k_max_i32, dim3(g), dim3(TNP_BLOCK), 0, s, a, n, out);
+  unsigned g = (unsigned)std::min<int64_t>(tnp_grid(n), 256);
+  hipLaunchKernelGGL(k_max_i32, dim3(g), dim3(TNP_BLOCK), 0, s, a, b, n, out, out_b);
   TNP_CHECK(hipGetLastError());
   return 0;
 }

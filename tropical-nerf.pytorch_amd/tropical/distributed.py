@@ -315,6 +315,23 @@ def slab_restrict(vertices: Tensor, edges: Tensor, marks: Tensor, x0: int, x1: i
     return vertices[keep], nid[e[ke]]
 
 
+def box_restrict(vertices: Tensor, edges: Tensor, marks: Tensor, lo, hi, eps: float = 1e-4):
+    """slab_restrict for a box of mark planes [lo[d], hi[d]] per axis (a
+    block with its halo): vertices of a mark-plane complex kept in order,
+    edges with both endpoints kept, in order."""
+    marks = marks.to(vertices.device)
+    keep = torch.ones(vertices.shape[0], dtype=torch.bool, device=vertices.device)
+    for d in range(3):
+        off, on = axis_grid(vertices, marks, eps, d)
+        if not bool(on.all()):
+            raise ValueError("box_restrict: vertices off the mark planes")
+        keep &= (off >= lo[d]) & (off <= hi[d])
+    nid = torch.cumsum(keep.to(torch.int64), 0) - 1
+    e = edges.to(vertices.device)
+    ke = keep[e[:, 0]] & keep[e[:, 1]]
+    return vertices[keep], nid[e[ke]]
+
+
 def comm_device(group, device) -> torch.device:
     """Where a collective's tensors must live: the GPU for RCCL ("nccl"),
     host memory for gloo (multi-rank rehearsals sharing one GPU)."""
@@ -517,7 +534,7 @@ def gather_complex(owned: Tensor, first: int, gedges: Tensor, dst: int = 0, grou
 
 
 def subpoly_sharded(net, size: float = 1.2, group=None, allreduce=None, stats: list = None,
-                    halo: int = None, force: bool = True, eps: float = 1e-4):
+                    halo: int = None, force: bool = True, eps: float = 1e-4, blocks: bool = False):
     """The hot loop of subpoly() (subpoly.py:45-69) sharded over the ranks of
     `group` (one GPU each): the skeleton (tropical.py:158-225, computed whole
     on every rank -- a few lattice passes), x-slabs of equal skeleton-edge
@@ -528,7 +545,9 @@ def subpoly_sharded(net, size: float = 1.2, group=None, allreduce=None, stats: l
     halo).  Returns (engine, owned vertices, first global id, global edges,
     cuts): the engine still holds this rank's slab complex.  force=False:
     the curve branch, its in-step decisions through the same allreduce.
-    eps: subpoly's eps argument (None: Net.eps), as in subpoly()."""
+    eps: subpoly's eps argument (None: Net.eps), as in subpoly().
+    blocks=True: the most cubic block split instead of x-slabs, each axis
+    cut at equal marginal skeleton-edge load; `cuts` is then the Blocks."""
     from ._engine import engine_for
     from .subpoly import _eps
     rank, world = dist.get_rank(group), dist.get_world_size(group)
@@ -544,18 +563,29 @@ def subpoly_sharded(net, size: float = 1.2, group=None, allreduce=None, stats: l
         raise NotImplementedError("subpoly_sharded: the skeleton fell back to get_hypercube "
                                   "(subpoly.py:51-52); nothing to shard")
     n_cells = marks.shape[0] - 1
-    # an edge's x cell: the lower of its endpoints' x planes (x-edges span one
-    # cell; y/z edges lie in a plane, charged to the cell on its right)
-    ex = torch.minimum(off[e[:, 0]], off[e[:, 1]]).clamp(0, n_cells - 1)
-    load = torch.bincount(ex, minlength=n_cells)
-    cuts = balanced_cuts(load, world)
+
+    def axis_cuts(d, parts):
+        # an edge's cell along d: the lower of its endpoints' planes (edges
+        # along d span one cell; the others lie in a plane, charged to the
+        # cell on its right)
+        o, _ = axis_grid(v, marks, net.eps, d)
+        ed = torch.minimum(o[e[:, 0]], o[e[:, 1]]).clamp(0, n_cells - 1)
+        return balanced_cuts(torch.bincount(ed, minlength=n_cells), parts)
+
+    if blocks:
+        dims = block_dims(world)
+        part = Blocks(n_cells + 1, dims, [axis_cuts(d, dims[d]) if dims[d] > 1 else [0, n_cells]
+                                          for d in range(3)])
+    else:
+        part = Blocks.xslabs(axis_cuts(0, world))
+    cuts = part.cuts[0] if not blocks else part
     widths = HALOS if halo is None else (halo,)
     for k, h in enumerate(widths):
-        x0, x1 = slab_marks(cuts, rank, h)
-        vs, es = slab_restrict(v, e, marks, x0, x1, net.eps)
+        lo, hi = part.box(rank, h)
+        vs, es = box_restrict(v, e, marks, lo, hi, net.eps)
         eng.load(vs, es)
-        eng.set_xspan(x0, x1)
-        eng.set_owned(cuts[rank], cuts[rank + 1])
+        eng.set_span(lo, hi)
+        eng.set_owned_box(*part.owned(rank))
         st = []
         eng.run_steps(st, allreduce)
         Vl, El, _ = eng.export()
