@@ -296,6 +296,13 @@ k_descend_wave(NetDev net, int64_t G, const int32_t* __restrict__ glist,
   const float* WL = Wl[NH - 1] + (NH == 1 ? H * IN + H : H * H + H);
   uint64_t word = 0;  // convergence bits of iterations [64 k, 64 k + 64)
   float d0 = 1.f, d1 = 1.f;
+  // this lane's table entry of the last iteration: the point moves by ~1e-2
+  // of its edge per iteration, so its corners mostly stay those of the
+  // iteration before -- a lane gathers only when its corner id changes, and
+  // a wave whose lanes all hit skips the iteration's one dependent memory
+  // round trip (same values: the table is constant over the descent)
+  uint32_t cid = 0xFFFFFFFFu;  // (wrap_index < size <= 2^31: never an id)
+  float2 cv = make_float2(0.f, 0.f);
   for (int it = 0; it < iters; ++it) {
     float u[3];
 #pragma unroll
@@ -321,7 +328,11 @@ k_descend_wave(NetDev net, int64_t G, const int32_t* __restrict__ glist,
     }
     uint32_t id = dense ? (gc[0] + gc[1] * res + gc[2] * (res * res)) : (gc[0] ^ (gc[1] * P1) ^ (gc[2] * P2));
     id = wrap_index(id, size);
-    const float2 v = table_entry(net, lc, id);
+    if (id != cid) {
+      cv = table_entry(net, lc, id);
+      cid = id;
+    }
+    const float2 v = cv;
     const float px = __fmul_rn(wc, v.x), py = __fmul_rn(wc, v.y);
     float f[IN];
 #pragma unroll
