@@ -120,6 +120,8 @@ def test_block_split():
     assert (cells == 1).all()
     assert abs(B.redundant_frac(0, 3) - 0.0672) < 1e-3
     assert abs(Blocks.xslabs(slab_cuts(256, 8)).redundant_frac(1, 3) - 0.158) < 1e-3
+    with pytest.raises(ValueError, match="non-empty"):
+        Blocks(3, (4, 1, 1))  # more blocks than cells along x
 
 
 def test_block_owner_and_edge_rules():

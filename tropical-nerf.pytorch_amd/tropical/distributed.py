@@ -163,6 +163,11 @@ class Blocks:
         self.dims = tuple(int(p) for p in dims)
         self.cuts = [list(c) for c in cuts] if cuts is not None else [slab_cuts(n_marks, p) for p in self.dims]
         self.world = self.dims[0] * self.dims[1] * self.dims[2]
+        for d in range(3):
+            c = self.cuts[d]
+            if len(c) != self.dims[d] + 1 or any(b <= a for a, b in zip(c, c[1:])):
+                raise ValueError(f"Blocks: axis {'xyz'[d]} cuts {c} do not give {self.dims[d]} non-empty "
+                                 f"blocks of the {self.n_marks - 1} cells")
 
     @classmethod
     def xslabs(cls, cuts: list):
