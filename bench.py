@@ -562,10 +562,16 @@ def main():
             torch.distributed.barrier()
         torch.cuda.synchronize(dev)
 
+    if os.environ.get("TNP_BENCH_MEM"):
+        fr, tot = torch.cuda.mem_get_info(dev)
+        log(f"rank {rank}: halo {halo}, box {box}, device memory {(tot - fr) / 2**30:.1f} of {tot / 2**30:.0f} GiB in use")
     log(f"rank {rank}: {G}^3 lattice, {args.warmup} warmup + {args.steps} timed passes")
     for _ in range(args.warmup):
         one_pass()
     barrier()
+    if os.environ.get("TNP_BENCH_MEM"):
+        fr, tot = torch.cuda.mem_get_info(dev)
+        log(f"rank {rank}: after warmup, device memory {(tot - fr) / 2**30:.1f} GiB in use")
     t0 = time.perf_counter()
     all_stats = []
     for _ in range(args.steps):

@@ -20,6 +20,7 @@
 #   pmc:<counters>     one rocprofv3 --pmc pass (counters comma-separated) of a short bench
 #   pmcsession         tools/pmc_session.sh (kernel trace + the four counter passes -> pmc_table.json)
 #   rehearsal[:N]      bench at 161^3 on one rank, then N (default 2) gloo ranks sharing the GPU
+#   ranks[:N]          only the N gloo ranks sharing the GPU (rc 1 does not stop the session)
 #   diag:<cases>       tools/descend_diag.py on descend fixtures (comma-separated)
 #   env:<VAR=val>      export a variable for the following steps
 # Logs: gpurun_out/<tag>_<n>_<step>.log, summary gpurun_out/<tag>_session.log
@@ -70,6 +71,9 @@ for step in "$@"; do
                run 400 0 env TNP_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 \
                  --nproc-per-node "${a1:-2}" --master-addr 127.0.0.1 --master-port 29517 bench.py \
                  --gpus "${a1:-2}" --steps 2 --warmup 1 --no-cpu ;;
+    ranks) run 400 1 env TNP_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 \
+             --nproc-per-node "${a1:-2}" --master-addr 127.0.0.1 --master-port 29518 bench.py \
+             --gpus "${a1:-2}" --steps 2 --warmup 1 --no-cpu ;;
     diag) run 240 0 python -u tools/descend_diag.py ${a1//,/ } ;;
     env) export "$a1"; echo "== env $a1" >> "$sess" ;;
     *) echo "unknown step $step" >> "$sess"; exit 2 ;;

@@ -83,7 +83,13 @@ static int buf_ensure(Buf& b, size_t bytes, hipStream_t s, bool keep = false) {
   size_t nb = std::max(bytes, b.bytes + b.bytes / 2);
   nb = std::max<size_t>(nb, 256);
   void* p = nullptr;
-  TNP_CHECK(hipMallocAsync(&p, nb, s));
+  if (hipMallocAsync(&p, nb, s) != hipSuccess) {
+    size_t fr = 0, tot = 0;
+    (void)hipMemGetInfo(&fr, &tot);
+    tnp_set_error("hipMallocAsync of %zu bytes (buffer of %zu, %zu requested): out of memory, %zu of %zu free",
+                  nb, b.bytes, bytes, fr, tot);
+    return -1;
+  }
   if (keep && b.p && b.bytes) TNP_CHECK(hipMemcpyAsync(p, b.p, b.bytes, hipMemcpyDeviceToDevice, s));
   if (b.p) TNP_CHECK(hipFreeAsync(b.p, s));
   b.p = p;

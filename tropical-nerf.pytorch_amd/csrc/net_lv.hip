@@ -216,10 +216,14 @@ k_forward_new(NetDev net, const float* xyz, int64_t n, float* __restrict__ pre,
   // per pass for this kernel)
   const uint64_t g = grid_word(mk, net.n_marks, eps, x);
   if (live) grid[V + i] = g;
-  if (__ballot(live && bad) && tnp::lane() == 0) tnp::or_sticky(&ctr[CTR_FAIL], 1ull);
+  // a shard's failover predicate covers the new vertices it owns: their OR
+  // over the shards is the whole batch's, while a halo vertex is another
+  // shard's or -- near the halo's outer faces, which miss the cells beyond
+  // -- may split an edge the whole complex does not have
+  const bool owned = !tnp::own_any(own) || tnp::owned_by(own, g);
+  if (__ballot(live && bad && owned) && tnp::lane() == 0) tnp::or_sticky(&ctr[CTR_FAIL], 1ull);
   if (tnp::own_any(own)) {
     // the shard's ownership of the new vertex (common.h OwnBox)
-    const bool owned = tnp::owned_by(own, g);
     const uint64_t halo = __ballot(live && !owned);
     if (halo && tnp::lane() == 0)
       atomicAdd((unsigned long long*)&ctr[CTR_DUP], (unsigned long long)__popcll(halo));
