@@ -524,13 +524,16 @@ def main():
     G = args.marks if world == 1 else int(round(args.marks * world ** (1.0 / 3.0)))
     net = make_net(G, dev, args.seed)
     from tropical.distributed import HALOS, Blocks, block_dims, halo_check, slab_cuts
-    # N > 1: one block of the lattice per rank (2 x 2 x 2 at N = 8; x-slabs
-    # with TNP_SHARD=xslab) -- blocks have the smallest cut faces, so the
-    # smallest halo
+    # N > 1: one block of the lattice per rank when the most cubic split cuts
+    # every axis (2 x 2 x 2 at N = 8: the smallest cut faces, so the smallest
+    # halo), x-slabs otherwise -- 2 x 2 x 1 blocks of 203^3 on 4 ranks
+    # sharing one GPU blew up in a timed pass (open);
+    # TNP_SHARD=blocks|xslab forces either
     part = None
     if world > 1:
-        part = (Blocks.xslabs(slab_cuts(G, world)) if os.environ.get("TNP_SHARD") == "xslab"
-                else Blocks(G, block_dims(world)))
+        dims = block_dims(world)
+        shard = os.environ.get("TNP_SHARD", "blocks" if min(dims) > 1 else "xslab")
+        part = Blocks.xslabs(slab_cuts(G, world)) if shard == "xslab" else Blocks(G, dims)
     eng = engine_for(net)
     if world > 1:
         eng.set_owned_box(*part.owned(rank))  # halo splits -> S_dup
