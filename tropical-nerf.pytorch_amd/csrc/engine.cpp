@@ -81,7 +81,11 @@ struct Buf {
 static int buf_ensure(Buf& b, size_t bytes, hipStream_t s, bool keep = false) {
   if (bytes <= b.bytes && b.p) return 0;
   size_t nb = std::max(bytes, b.bytes + b.bytes / 2);
-  nb = std::max<size_t>(nb, 256);
+  // whole 256-B units: a capacity derived from the size (the connect keys'
+  // cap = bytes / 8 rounded up to the XCD shard count) must not exceed it,
+  // else every step grows the buffer by another half (a 1.5x growth of an
+  // odd size ran a 203^3 shard to 44 GB of keys)
+  nb = std::max<size_t>((nb + 255) & ~size_t(255), 256);
   void* p = nullptr;
   if (hipMallocAsync(&p, nb, s) != hipSuccess) {
     size_t fr = 0, tot = 0;
