@@ -526,9 +526,9 @@ def main():
     from tropical.distributed import HALOS, Blocks, block_dims, halo_check, slab_cuts
     # N > 1: one block of the lattice per rank when the most cubic split cuts
     # every axis (2 x 2 x 2 at N = 8: the smallest cut faces, so the smallest
-    # halo), x-slabs otherwise -- 2 x 2 x 1 blocks of 203^3 on 4 ranks
-    # sharing one GPU blew up in a timed pass (open);
-    # TNP_SHARD=blocks|xslab forces either
+    # halo), x-slabs otherwise until the 2 x 2 x 1 split is re-run on the GPU
+    # (its 4-rank rehearsal hit the key-buffer regrowth fixed in buf_ensure,
+    # DESIGN §6); TNP_SHARD=blocks|xslab forces either
     part = None
     if world > 1:
         dims = block_dims(world)
