@@ -524,15 +524,15 @@ def main():
     G = args.marks if world == 1 else int(round(args.marks * world ** (1.0 / 3.0)))
     net = make_net(G, dev, args.seed)
     from tropical.distributed import HALOS, Blocks, block_dims, halo_check, slab_cuts
-    # N > 1: one block of the lattice per rank when the most cubic split cuts
-    # every axis (2 x 2 x 2 at N = 8: the smallest cut faces, so the smallest
-    # halo), x-slabs otherwise until the 2 x 2 x 1 split is re-run on the GPU
-    # (its 4-rank rehearsal hit the key-buffer regrowth fixed in buf_ensure,
-    # DESIGN §6); TNP_SHARD=blocks|xslab forces either
+    # N > 1: one block of the lattice per rank from N = 4 (2 x 2 x 1, 2 x 2 x 2:
+    # the smallest cut faces, so the fewest redundant halo cells); N = 2 is
+    # one cut either way (x-slabs).  TNP_SHARD=blocks|xslab forces either.
     part = None
     if world > 1:
         dims = block_dims(world)
-        shard = os.environ.get("TNP_SHARD", "blocks" if min(dims) > 1 else "xslab")
+        shard = os.environ.get("TNP_SHARD", "blocks" if world >= 4 else "xslab")
+        if shard not in ("blocks", "xslab"):
+            raise SystemExit(f"TNP_SHARD={shard!r}: 'blocks' or 'xslab'")
         part = Blocks.xslabs(slab_cuts(G, world)) if shard == "xslab" else Blocks(G, dims)
     eng = engine_for(net)
     if world > 1:
@@ -547,17 +547,21 @@ def main():
         return stats
 
     halo = 0
+    search = {"halo_search_passes": 0, "halo_search_ms": 0.0}
     if world > 1:
         # this rank's cells + a halo beyond every cut face, as wide as
-        # halo_check needs (untimed: one pass per width tried)
+        # halo_check needs (untimed: one pass per width tried, reported)
+        t_s = time.perf_counter()
         for k, halo in enumerate(HALOS):
             box[:] = part.box(rank, halo)
             one_pass()
+            search["halo_search_passes"] += 1
             Vl, El, _ = eng.export()
             ok = halo_check(Vl.to(comm_dev), El.to(comm_dev), net.enc.marks, part,
                             raise_=k == len(HALOS) - 1)
             if ok is not None:
                 break
+        search["halo_search_ms"] = round((time.perf_counter() - t_s) * 1e3, 1)
 
     def barrier():
         torch.cuda.synchronize(dev)
@@ -699,7 +703,7 @@ def main():
                                    f"{net.K} hyperplane steps", "marks_per_axis": G,
                        "lattice_vertices": G ** 3, "edges_subdivided_per_pass": int(per_pass),
                        "seed": args.seed, "table_amp": 0.1, "parallelism": parallelism(part),
-                       "halo_cells": halo, **halo_stats(part, halo)},
+                       "halo_cells": halo, **halo_stats(part, halo), **search},
             "roofline": roof,
             "loop_model_bytes_per_pass": int(bytes_tot / args.steps),
             "loop_model_gbs": round(loop_gbs, 1),

@@ -111,6 +111,13 @@ typedef struct tnp_engine tnp_engine;
 int tnp_engine_create(tnp_engine** out, int device);
 void tnp_engine_destroy(tnp_engine* eng);
 int tnp_engine_set_net(tnp_engine* eng, const tnp_net* net);
+/* Device memory the engine holds: *bytes = the sum of every scratch and
+ * complex buffer (they grow geometrically and are reused across steps and
+ * passes, so a repeated workload holds this constant after its first pass);
+ * *buffers = buffers allocated; *key_bytes = the connect phase's key buffer
+ * (the one round 4's growth bug inflated).  buffers / key_bytes may be null.
+ * No reference counterpart (PyTorch's caching allocator there). */
+int tnp_engine_scratch_bytes(tnp_engine* eng, int64_t* bytes, int64_t* buffers, int64_t* key_bytes);
 
 /* Load a complex: vertices V x 3 fp32, edges E x 2 int64 (device).  d_pre:
  * optional cached outputs_ (V x K fp32, row-major as the reference keeps

@@ -38,6 +38,16 @@ int tnp_engine_debug_lb_recomputes(tnp_engine* eng, int64_t* n, int reset, void*
  * it off): on = 0 sends every bucket's records through memory, as before. */
 int tnp_engine_debug_set_lds_records(tnp_engine* eng, int on);
 
+/* Debug: the engine's capacity arithmetic, host only (csrc/engine.cpp
+ * buf_grow_bytes, connect_key_cap).  grown_bytes: the size a buffer of
+ * have_bytes grows to for a request of request_bytes; key_cap: the connect
+ * phase's key capacity (keys, a multiple of xs_n) for a step of `members`
+ * bucket members when the key buffer holds have_bytes.  A steady workload
+ * must never ask for more than the buffer holds: key_cap * 8 <= have_bytes
+ * whenever have_bytes already covers the floor. */
+int tnp_debug_buf_growth(int64_t have_bytes, int64_t request_bytes, int64_t members, int xs_n,
+                         int64_t* grown_bytes, int64_t* key_cap);
+
 /* Debug: the curve branch's gradient-descent fallback (descend.h, the
  * engine's launch) on n arbitrary rows: row r descends along the edge
  * d_ends[r] (e0 xyz, e1 xyz) from the box parameters d_x[r] (in/out) on

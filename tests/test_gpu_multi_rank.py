@@ -76,10 +76,26 @@ def _worker(rank, world, port, outdir, case, mode):
         coll = bench.Collective(torch.device("cpu"))
         stats = []
         blocks = mode.endswith("_blocks")
-        if mode.startswith("bench"):  # the synthetic bench net of `case` = (marks, seed)
-            G, seed = case
+        if mode.startswith("bench"):  # the synthetic bench net of `case` = (marks, seed[, passes])
+            G, seed = case[:2]
             net = bench.make_net(G, dev, seed)
             part, Vl, El, halo = _sharded_lattice(net, rank, world, coll, stats, blocks)
+            # further passes of the accepted halo on the same engine (bench.py's
+            # timed loop): the engine's device footprint must stay what the
+            # first pass left (round 4's 4-block run grew a buffer by half per
+            # step until hipMallocAsync failed)
+            from tropical._engine import engine_for
+            eng = engine_for(net)
+            foot = [eng.scratch_bytes()]
+            for _ in range(case[2] if len(case) > 2 else 0):
+                eng.lattice_box(*part.box(rank, halo))
+                eng.run_steps([], coll)
+                foot.append(eng.scratch_bytes())
+            if len(foot) > 1:
+                Vl, El, _ = eng.export()
+                Vl, El = Vl.cpu(), El.cpu()
+            steady = torch.tensor([int(all(f == foot[1] for f in foot[1:]))])
+            dist.all_reduce(steady, op=dist.ReduceOp.MIN)
             own, keep = D.owned_masks(Vl, El, net.enc.marks.cpu(), part, rank)
             hv, he = D.complex_hash(Vl, El, own, keep)
             splits = sum(s["S"] - s["S_dup"] for s in stats)
@@ -87,7 +103,8 @@ def _worker(rank, world, port, outdir, case, mode):
             dist.all_reduce(tot)
             if rank == 0:
                 np.savez(os.path.join(outdir, "out.npz"), tot=tot.numpy(), dims=np.array(part.dims),
-                         halo=np.array(halo), redundant=np.array(part.redundant_frac(rank, halo)))
+                         halo=np.array(halo), redundant=np.array(part.redundant_frac(rank, halo)),
+                         steady=steady.numpy(), foot=np.array([f["bytes"] for f in foot]))
             return
         d = load(case)
         net = product_net(d, dev)
@@ -97,8 +114,9 @@ def _worker(rank, world, port, outdir, case, mode):
             owned, first, gE, own, keep = D.stitch(Vl, El, net.enc.marks.cpu(), part, masks=True)
         else:  # "skeleton" (flat) or "curve" (force=False: the curve branch's decisions go
             # through the engine's collective callback)
+            curve = mode.startswith("curve")
             eng, owned, first, gE, cuts = D.subpoly_sharded(net, 1.2, allreduce=coll, stats=stats,
-                                                            force=mode != "curve", blocks=blocks)
+                                                            force=not curve, blocks=blocks)
             Vl, El, _ = eng.export()
             Vl, El = Vl.cpu(), El.cpu()
             own, keep = D.owned_masks(Vl, El, net.enc.marks.cpu(), cuts, rank)
@@ -117,7 +135,7 @@ def _worker(rank, world, port, outdir, case, mode):
         single_ok = torch.tensor([1])
         if not mode.startswith("lattice"):  # (the lattice goldens hold the full-lattice surface, not subpoly's)
             with contextlib.redirect_stdout(io.StringIO()):
-                _, verts, fwi = sp.subpoly(net, 3, 1.2, force=mode != "curve")
+                _, verts, fwi = sp.subpoly(net, 3, 1.2, force=not curve)
             single_ok[0] = int(verts.shape[0] == int(d["n_surf"][0]) and
                                sha(np.asarray(fwi, dtype=np.int64)) == str(d["sha_tri"]))
         dist.all_reduce(single_ok, op=dist.ReduceOp.MIN)
@@ -187,18 +205,22 @@ def test_sharded_stanford_net(cuda, tmp_path, case, world, mode):
     assert len(cuts) == (world + 1 if mode == "skeleton" else 3)
 
 
-@pytest.mark.parametrize("case,world", [("small_sphere_curve", 2), ("small_sphere_curve", 3),
-                                        ("small_torus_curve", 2)])
-def test_sharded_curve_branch(cuda, tmp_path, case, world):
+@pytest.mark.parametrize("case,world,mode", [("small_sphere_curve", 2, "curve"), ("small_sphere_curve", 3, "curve"),
+                                             ("small_torus_curve", 2, "curve"),
+                                             ("small_sphere_curve", 4, "curve_blocks"),
+                                             ("small_torus_curve", 8, "curve_blocks")])
+def test_sharded_curve_branch(cuda, tmp_path, case, world, mode):
     """The curve branch (force=False) on x-slabs: the per-step decisions the
     reference takes over the whole batch -- the curve rows' and descent rows'
     counts (MKL's row-count schedules), the descent's stop iteration (an AND
     of the shards' convergence words, subpoly_debug.py:141) and the strict
     filter's flag (subpoly_debug.py:253-257) -- go through the engine's
     collective callback (tnp_engine_set_collective); the stitched complex must
-    equal the unsharded curve run's."""
+    equal the unsharded curve run's.  curve_blocks: 2 x 2 x 1 and 2 x 2 x 2
+    blocks, where the failover test counts only each shard's owned new
+    vertices (k_fail_check)."""
     d, V, E, want = _unsharded(cuda, case, "curve")
-    z = _run(tmp_path, case, "curve", world)
+    z = _run(tmp_path, case, mode, world)
     assert tuple(int(x) for x in z["tot"]) == want
     assert z["V"].shape[0] == want[0] and z["E"].shape[0] == want[1]
     # a single-device subpoly(force=False) after the sharded run, same process
@@ -235,6 +257,41 @@ def test_lattice256_eight_slabs_stitch_to_the_unsharded_complex(cuda, tmp_path, 
     if mode == "bench_blocks":
         assert z["dims"].tolist() == [2, 2, 2]
         assert float(z["redundant"]) <= 0.07, (int(z["halo"]), float(z["redundant"]))
+
+
+def _unsharded_bench(cuda, G, seed):
+    import bench
+    from tropical.distributed import complex_hash
+    from tropical._engine import engine_for
+    net = bench.make_net(G, cuda, seed)
+    eng = engine_for(net)
+    eng.set_owned()
+    eng.set_shards(1)
+    eng.lattice()
+    stats = []
+    eng.run_steps(stats)
+    V, E, _ = eng.export()
+    hv, he = complex_hash(V, E)
+    want = (V.shape[0], E.shape[0], hv, he, sum(s["S"] for s in stats))
+    del V, E
+    torch.cuda.empty_cache()
+    return want
+
+
+@pytest.mark.timeout(600)
+def test_four_blocks_203_steady_footprint(cuda, tmp_path):
+    """The run that blew up in round 4 (bench.py --gpus 4: 2 x 2 x 1 blocks of
+    the 203^3 seed-6 lattice, gpurun_out/rs.log: hipMallocAsync of 66 GB after
+    the connect key buffer grew by half per step): 4 gloo ranks sharing this
+    GPU run the halo search and then 5 more passes each on the same engine;
+    every rank's device footprint (tnp_engine_scratch_bytes) must stay what
+    its first timed pass left, and the stitched complex must equal the
+    unsharded one."""
+    want = _unsharded_bench(cuda, 203, 6)
+    z = _run(tmp_path, (203, 6, 5), "bench_blocks", 4)
+    assert z["dims"].tolist() == [2, 2, 1]
+    assert int(z["steady"][0]) == 1, z["foot"].tolist()
+    assert tuple(int(x) for x in z["tot"]) == want
 
 
 def test_slab_buckets_do_not_change_the_result(cuda):

@@ -404,3 +404,30 @@ def test_row_order_fast_path_is_the_full_sort(cuda, name, monkeypatch):
     np.testing.assert_array_equal(outs[0][0], outs[1][0])
     np.testing.assert_array_equal(outs[0][1], outs[1][1])
     assert sha(outs[0][0]) == str(d["sha_tri"]) and sha(outs[0][1]) == str(d["sha_faces"])
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("G", [128, 203])
+def test_engine_footprint_is_steady_across_passes(cuda, G):
+    """bench.py's loop on one engine (the 128^3 headline lattice and the 203^3
+    one round 4's 4-block run blew up on): 8 passes of the same workload;
+    after the first, the engine's device footprint (every buffer,
+    tnp_engine_scratch_bytes) and its connect key buffer do not change, and
+    every pass extracts the same complex."""
+    import bench
+    from tropical.distributed import complex_hash
+    from tropical._engine import engine_for
+    net = bench.make_net(G, cuda, 6)
+    eng = engine_for(net)
+    eng.set_owned()
+    eng.set_shards(1)
+    foot, got = [], []
+    for _ in range(8):
+        eng.lattice()
+        eng.run_steps([])
+        foot.append(eng.scratch_bytes())
+        V, E = eng.sizes()
+        got.append((V, E))
+    assert all(f == foot[1] for f in foot[1:]), [f["bytes"] for f in foot]
+    assert len(set(got)) == 1
+    assert foot[0]["key_bytes"] > 0 and foot[0]["buffers"] > 10

@@ -1,6 +1,6 @@
 """CPU, world_size 2 over gloo: the N>1 path of bench.py.
 
-Each rank extracts its x-slab of the synthetic lattice with a two-cell halo (the default HALO)
+Each rank extracts its x-slab of the synthetic lattice with the default HALO (three cells)
 (tropical/distributed.py::slab_marks; tropical/synthetic.py::slab_lattice ==
 tnp_engine_lattice's layout) and takes the reference's two whole-complex
 decisions per step -- "does anything split" (subpoly.py:110) and the
@@ -95,13 +95,14 @@ def whole():
 
 
 def test_slab_cuts_cover_the_lattice():
-    from tropical.distributed import slab_cuts, slab_marks
+    from tropical.distributed import HALO, HALOS, slab_cuts, slab_marks
+    assert HALOS[0] == HALO and list(HALOS) == sorted(set(HALOS))
     for G, world in ((128, 1), (161, 2), (203, 4), (256, 8)):
         cuts = slab_cuts(G, world)
         assert cuts[0] == 0 and cuts[-1] == G - 1 and cuts == sorted(set(cuts))
         for r in range(world):
             x0, x1 = slab_marks(cuts, r)
-            assert x0 == max(cuts[r] - 2, 0) and x1 == min(cuts[r + 1] + 2, G - 1)
+            assert x0 == max(cuts[r] - HALO, 0) and x1 == min(cuts[r + 1] + HALO, G - 1)
 
 
 def test_block_split():

@@ -92,12 +92,15 @@ def test_subpoly_step_op_reproduces_reference_steps(cuda):
     args = ops.net_args(net)
     V = torch.from_numpy(lattice_vertices(d["marks"])).to(cuda)
     E = torch.from_numpy(lattice_edges(int(d["lattice_n"]))).to(cuda)
-    with torch.no_grad():  # (Net.forward is differentiable: no graph for the cache)
-        o = torch.cat(net(V, gather=True)[1], -1)
+    # the cache as the reference hands it over: Net.forward's output, with a
+    # graph (subpoly.py:93) -- the op detaches it; its outputs carry none
+    o = torch.cat(net(V, gather=True)[1], -1)
+    assert o.requires_grad
     for step, idx in enumerate(d["step_idx"][:12]):
         E_in = E.clone()
         V2, E2, o2 = torch.ops.tropical_hip.subpoly_step(V, E, o, *args, int(idx), True, True)
         assert torch.equal(E, E_in)
+        assert not (V2.requires_grad or E2.requires_grad or o2.requires_grad)
         assert sha(V2.cpu().numpy(), E2.cpu().numpy(), o2.cpu().numpy()) == str(d["step_sha"][step])
         V, E, o = V2, E2, o2
 

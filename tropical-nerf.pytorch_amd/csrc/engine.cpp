@@ -78,14 +78,27 @@ struct Buf {
   size_t bytes = 0;
 };
 
+// the capacity buf_ensure grows a buffer of `have` bytes to for a request of
+// `bytes`: geometric (x1.5), in whole 256-B units
+static size_t buf_grow_bytes(size_t have, size_t bytes) {
+  const size_t nb = std::max(bytes, have + have / 2);
+  return std::max<size_t>((nb + 255) & ~size_t(255), 256);
+}
+
+// the connect phase's key capacity (keys) for a step of M members, given the
+// key buffer's current size: XS_N equal per-XCD regions.  The capacity the
+// buffer already holds is rounded DOWN to the regions (so it never asks for
+// more than the buffer has -- round 4's 1.5x-per-step growth to 44 GB came
+// from rounding it up); only the floor of 4 M + 1024 keys is rounded up.
+static int64_t connect_key_cap(size_t have_bytes, int64_t M, int xs_n) {
+  const int64_t have = (int64_t)(have_bytes / sizeof(uint64_t)) / xs_n * xs_n;
+  const int64_t floor = (4 * M + 1024 + xs_n - 1) / xs_n * xs_n;
+  return std::max(have, floor);
+}
+
 static int buf_ensure(Buf& b, size_t bytes, hipStream_t s, bool keep = false) {
   if (bytes <= b.bytes && b.p) return 0;
-  size_t nb = std::max(bytes, b.bytes + b.bytes / 2);
-  // whole 256-B units: a capacity derived from the size (the connect keys'
-  // cap = bytes / 8 rounded up to the XCD shard count) must not exceed it,
-  // else every step grows the buffer by another half (a 1.5x growth of an
-  // odd size ran a 203^3 shard to 44 GB of keys)
-  nb = std::max<size_t>((nb + 255) & ~size_t(255), 256);
+  const size_t nb = buf_grow_bytes(b.bytes, bytes);
   void* p = nullptr;
   if (hipMallocAsync(&p, nb, s) != hipSuccess) {
     size_t fr = 0, tot = 0;
@@ -558,35 +571,56 @@ extern "C" int tnp_engine_create(tnp_engine** out, int device) {
   return 0;
 }
 
-extern "C" void tnp_engine_destroy(tnp_engine* e) {
-  if (!e) return;
-  (void)hipSetDevice(e->device);
-  (void)hipDeviceSynchronize();
-  hipStream_t s = 0;
-  VSet* sets[2] = {&e->cur, &e->alt};
-  for (VSet* v : sets) {
-    buf_free(v->xyz, s); buf_free(v->pre, s); buf_free(v->pos, s); buf_free(v->zero, s); buf_free(v->grid, s);
-    buf_free(v->pz, s);
-  }
+// every device buffer the engine owns (destroy, tnp_engine_scratch_bytes)
+template <typename F>
+static void for_each_buf(tnp_engine* e, F&& f) {
+  for (VSet* v : {&e->cur, &e->alt})
+    for (Buf* b : {&v->xyz, &v->pre, &v->pos, &v->zero, &v->grid, &v->pz}) f(*b);
   Buf* bufs[] = {&e->edges, &e->edges_alt, &e->blk, &e->blkoff, &e->scan_scr, &e->sa, &e->sb,
                  &e->stage, &e->shared, &e->members, &e->pcn, &e->pent, &e->rstart,
                  &e->ent_v, &e->ents, &e->pcell, &e->ptoff, &e->bcell,
                  &e->ckeys_a, &e->ckeys_b, &e->sort_scr, &e->flags, &e->used, &e->nid,
                  &e->ctr, &e->tri, &e->faces, &e->lb[0], &e->lb[1], &e->edm, &e->eef,
-                 &e->edm_alt, &e->eef_alt, &e->live, &e->tied_table, &e->xs, &e->lbrc, &e->lzpart, &e->kse[0], &e->kse[1], &e->kse[2]};
-  for (Buf* b : bufs) buf_free(*b, s);
-  for (Buf& b : e->fscr) buf_free(b, s);
-  for (Buf& b : e->fscr2) buf_free(b, s);
-  for (Buf& b : e->bk) buf_free(b, s);
-  buf_free(e->sents, s);
-  buf_free(e->sents2, s);
-  for (Buf& b : e->cv) buf_free(b, s);
-  for (Buf* b : {&e->spcnt, &e->spoff, &e->part, &e->ekey_a, &e->ekey_b, &e->eval_b,
-                 &e->sort_scr2})
-    buf_free(*b, s);
+                 &e->edm_alt, &e->eef_alt, &e->live, &e->tied_table, &e->xs, &e->lbrc, &e->lzpart,
+                 &e->kse[0], &e->kse[1], &e->kse[2], &e->sents, &e->sents2,
+                 &e->spcnt, &e->spoff, &e->part, &e->ekey_a, &e->ekey_b, &e->eval_b, &e->sort_scr2};
+  for (Buf* b : bufs) f(*b);
+  for (Buf& b : e->fscr) f(b);
+  for (Buf& b : e->fscr2) f(b);
+  for (Buf& b : e->bk) f(b);
+  for (Buf& b : e->cv) f(b);
+}
+
+extern "C" void tnp_engine_destroy(tnp_engine* e) {
+  if (!e) return;
+  (void)hipSetDevice(e->device);
+  (void)hipDeviceSynchronize();
+  hipStream_t s = 0;
+  for_each_buf(e, [&](Buf& b) { buf_free(b, s); });
   (void)hipDeviceSynchronize();
   if (e->h_ctr) (void)hipHostFree(e->h_ctr);
   delete e;
+}
+
+extern "C" int tnp_engine_scratch_bytes(tnp_engine* e, int64_t* bytes, int64_t* buffers, int64_t* key_bytes) {
+  if (!e || !bytes) { tnp_set_error("tnp_engine_scratch_bytes: null argument"); return -1; }
+  int64_t tot = 0, n = 0;
+  for_each_buf(e, [&](Buf& b) { tot += (int64_t)b.bytes; n += b.p != nullptr; });
+  *bytes = tot;
+  if (buffers) *buffers = n;
+  if (key_bytes) *key_bytes = (int64_t)e->ckeys_a.bytes;
+  return 0;
+}
+
+extern "C" int tnp_debug_buf_growth(int64_t have_bytes, int64_t request_bytes, int64_t members, int xs_n,
+                                    int64_t* grown_bytes, int64_t* key_cap) {
+  if (have_bytes < 0 || request_bytes < 0 || members < 0 || xs_n < 1 || xs_n > 63) {
+    tnp_set_error("tnp_debug_buf_growth: bad argument");
+    return -1;
+  }
+  if (grown_bytes) *grown_bytes = (int64_t)buf_grow_bytes((size_t)have_bytes, (size_t)request_bytes);
+  if (key_cap) *key_cap = connect_key_cap((size_t)have_bytes, members, xs_n);
+  return 0;
 }
 
 static NetDev to_dev(const tnp_net* n) {
@@ -1189,14 +1223,16 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
       if (ccoll) nf.sched_rows = Sg;
       TIMED("forward", (12.0 + 4.0 * e->K) * S,
             launch_forward(nf, P<float>(e->cur.xyz) + 3 * e->V, S, P<float>(e->stage), S, 1, s));
-      TIMED("fail_check", 40.0 * S,
-            launch_fail_check(P<int32_t>(e->sa), P<int32_t>(e->sb), S, idx, P<uint64_t>(e->cur.zero),
-                              P<float>(e->stage), eps, P<uint64_t>(e->shared), P<int64_t>(e->ctr), s));
-      // grid words of the new vertices (coordinates are final)
+      // grid words of the new vertices (coordinates are final; the failover
+      // test of a shard reads them: only owned vertices vote)
       if (launch_keys(e->net, P<float>(e->cur.xyz) + 3 * e->V, P<float>(e->stage), S, S, 0,
                       P<uint64_t>(e->cur.pos) + e->V, P<uint64_t>(e->cur.zero) + e->V,
                       P<uint64_t>(e->cur.grid) + e->V, s))
         return -1;
+      TIMED("fail_check", 48.0 * S,
+            launch_fail_check(P<int32_t>(e->sa), P<int32_t>(e->sb), S, idx, P<uint64_t>(e->cur.zero),
+                              P<float>(e->stage), eps, P<uint64_t>(e->shared), P<int64_t>(e->ctr),
+                              P<uint64_t>(e->cur.grid) + e->V, e->own, s));
     }
     if (e->curve || e->shards > 1) {
       // the host takes the global override decision (all-reduce) / the curve
@@ -1423,8 +1459,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   // connect kernel sums, instead of counter-block atomics from every bucket
   if (buckets && !shard && buf_ensure(e->bk[3], (int64_t)NG * 4 * sizeof(int64_t), s)) return -1;
   int64_t* const bstat = (buckets && !shard) ? P<int64_t>(e->bk[3]) : nullptr;
-  int64_t cap = std::max<int64_t>(e->ckeys_a.bytes / sizeof(uint64_t), 4 * M + 1024);
-  cap = (cap + XS_N - 1) / XS_N * XS_N;
+  int64_t cap = connect_key_cap(e->ckeys_a.bytes, M, XS_N);
   int64_t X = 0, TT = 0;
   bool chunks_ok = false;  // (radix path) the chunk table matches the pair cells
   for (int attempt = 0; attempt < 3; ++attempt) {
@@ -1521,7 +1556,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     }
     chunks_ok = true;
     if (X <= cap) break;
-    cap = X;  // appended beyond the buffer: grow to the exact count and redo
+    cap = (X + XS_N - 1) / XS_N * XS_N;  // appended beyond the buffer: grow and redo
   }
   if (e->h_ctr[CTR_BOVF] || X > cap) { tnp_set_error("connect: capacity retry failed"); return -1; }
   if (e->h_ctr[CTR_COMPAT] == 0 && e->shards <= 1) {

@@ -74,7 +74,7 @@ int launch_new_vertices(const int32_t* sa, const int32_t* sb, int64_t S, const f
                         float eps, float* xyz, int64_t V, hipStream_t s);
 int launch_fail_check(const int32_t* sa, const int32_t* sb, int64_t S, int idx,
                       const uint64_t* zero, const float* stage, float eps, uint64_t* shared,
-                      int64_t* ctr, hipStream_t s);
+                      int64_t* ctr, const uint64_t* grid_new, const OwnBox& own, hipStream_t s);
 int launch_finalize_new(int64_t S, int K, int override_, const uint64_t* shared, float* stage,
                         float eps, float* pre, int64_t ld, int keep_from, int64_t V, uint64_t* pos,
                         uint64_t* zero, const int64_t* ctr, uint64_t* pz, hipStream_t s);

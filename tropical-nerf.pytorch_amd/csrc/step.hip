@@ -223,11 +223,15 @@ __global__ void k_new_vertices(const int32_t* __restrict__ sa, const int32_t* __
 
 // shared planes (subpoly_debug.py:35-42): planes j < idx where both
 // endpoints are eps-zero, plus the current plane idx.  Any new vertex off one
-// of its shared planes by more than eps -> global override flag.
+// of its shared planes by more than eps -> global override flag.  On a shard
+// (own_any(own)) only the new vertices it owns vote (grid_new: their grid
+// words), as k_forward_new on the flat path: a halo vertex near the halo's
+// outer faces may belong to an edge the whole complex does not have.
 __global__ void k_fail_check(const int32_t* __restrict__ sa, const int32_t* __restrict__ sb,
                              int64_t S, int idx, const uint64_t* __restrict__ zero,
                              const float* __restrict__ stage, float eps,
-                             uint64_t* __restrict__ shared, int64_t* __restrict__ ctr) {
+                             uint64_t* __restrict__ shared, int64_t* __restrict__ ctr,
+                             const uint64_t* __restrict__ grid_new, OwnBox own) {
   int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   bool bad = false;
   if (r < S) {
@@ -238,6 +242,7 @@ __global__ void k_fail_check(const int32_t* __restrict__ sa, const int32_t* __re
       int p = __builtin_ctzll(t);
       bad |= fabsf(stage[(int64_t)p * S + r]) > eps;
     }
+    if (tnp::own_any(own)) bad &= tnp::owned_by(own, grid_new[r]);
   }
   if (__ballot(bad) && tnp::lane() == 0) tnp::or_sticky(&ctr[CTR_FAIL], 1ull);
 }
@@ -1416,10 +1421,10 @@ int launch_new_vertices(const int32_t* sa, const int32_t* sb, int64_t S, const f
 }
 int launch_fail_check(const int32_t* sa, const int32_t* sb, int64_t S, int idx,
                       const uint64_t* zero, const float* stage, float eps, uint64_t* shared,
-                      int64_t* ctr, hipStream_t s) {
+                      int64_t* ctr, const uint64_t* grid_new, const OwnBox& own, hipStream_t s) {
   if (S <= 0) return 0;
   hipLaunchKernelGGL(k_fail_check, dim3(tnp_grid(S)), dim3(TNP_BLOCK), 0, s, sa, sb, S, idx, zero,
-                     stage, eps, shared, ctr);
+                     stage, eps, shared, ctr, grid_new, own);
   TNP_CHECK(hipGetLastError());
   return 0;
 }

@@ -123,6 +123,14 @@ class Engine:
         _hip.check(_hip.lib().tnp_engine_sizes(self.h, C.byref(V), C.byref(E)), "tnp_engine_sizes")
         return V.value, E.value
 
+    def scratch_bytes(self) -> dict:
+        """Device memory the engine holds (tnp_engine_scratch_bytes): the sum
+        over its buffers, how many are allocated, the connect key buffer."""
+        b, n, k = C.c_int64(), C.c_int64(), C.c_int64()
+        _hip.check(_hip.lib().tnp_engine_scratch_bytes(self.h, C.byref(b), C.byref(n), C.byref(k)),
+                   "tnp_engine_scratch_bytes")
+        return {"bytes": b.value, "buffers": n.value, "key_bytes": k.value}
+
     def export(self, pre: bool = False, edges: bool = True):
         """(vertices [V, 3], edges [E, 2] int64 or None when edges=False,
         cache [V, K] when pre) of the compacted complex."""

@@ -66,6 +66,7 @@ SIGNATURES = {
     "tnp_engine_create": (C.c_int, [C.POINTER(_VP), C.c_int]),
     "tnp_engine_destroy": (None, [_VP]),
     "tnp_engine_set_net": (C.c_int, [_VP, _NETP]),
+    "tnp_engine_scratch_bytes": (C.c_int, [_VP, _P64, _P64, _P64]),
     "tnp_engine_load": (C.c_int, [_VP, _VP, _I64, _VP, _I64, _VP, C.c_int, _VP]),
     "tnp_engine_skeleton": (C.c_int, [_VP, C.c_int, _F, _VP, _P64, _P64]),
     "tnp_shm_open": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int, C.POINTER(_VP)]),
@@ -99,6 +100,7 @@ SIGNATURES = {
                                     C.c_int, _VP]),
     "tnp_engine_faces_debug": (C.c_int, [_VP, _VP, C.c_int64, _P64, _P64, _VP]),
     "tnp_engine_debug_set_lb_spin": (C.c_int, [_VP, C.c_int]),
+    "tnp_debug_buf_growth": (C.c_int, [C.c_int64, C.c_int64, C.c_int64, C.c_int, _P64, _P64]),
     "tnp_engine_debug_set_lds_records": (C.c_int, [_VP, C.c_int]),
     "tnp_engine_debug_lb_recomputes": (C.c_int, [_VP, _P64, C.c_int, _VP]),
     "tnp_engine_kernel_timer": (C.c_int, [_VP, C.c_int, _VP, _P32]),

@@ -115,12 +115,17 @@ def slab_cuts(n_marks: int, world: int) -> list:
     return [round(r * (n_marks - 1) / world) for r in range(world + 1)]
 
 
-HALO = 2  # first halo tried: cell columns extracted beyond each cut plane
+HALO = 3  # first halo tried: cell columns extracted beyond each cut plane
 # the widths tried in turn while halo_check still sees a difference (the
 # error front of a slab's outer boundary moves inward by at most one cell per
 # active step, and only through eps coincidences: how far it gets depends on
-# the net and the lattice, so the width is found, then checked again)
-HALOS = (2, 3, 4, 6, 8, 12, 16, 24, 33)
+# the net and the lattice, so the width is found, then checked again).  The
+# search starts at 3, the widest any measured workload needed (161^3: 2;
+# 203^3, 256^3: 3 -- a 2-cell halo left 1-2 vertices different at 203^3), so
+# none of them pays a rejected extraction; at 161^3 / 2 slabs the extra
+# column costs 1.2 % more redundant cells, at 256^3 / 8 blocks 3 is the
+# minimum anyway (6.7 % redundant)
+HALOS = (3, 4, 6, 8, 12, 16, 24, 33)
 
 
 def slab_marks(cuts: list, rank: int, halo: int = HALO):
@@ -513,14 +518,25 @@ def stitch(vertices: Tensor, edges: Tensor, marks: Tensor, cuts, eps: float = 1e
         if not below:
             raise RuntimeError("stitch: a kept edge references a vertex beyond the block's lower faces")
         prev = torch.cat([recs[r] for r in below], dim=0)
+        src = torch.cat([torch.full((recs[r].shape[0],), r, dtype=torch.int64, device=dev) for r in below])
         keys = torch.cat([prev[:, :3], bits[ni]], dim=0)
         uniq, inv = torch.unique(keys, dim=0, return_inverse=True)
         table = torch.full((uniq.shape[0],), -1, dtype=torch.int64, device=dev)
         table[inv[: prev.shape[0]]] = prev[:, 3]
-        got = table[inv[prev.shape[0]:]]
+        tsrc = torch.full((uniq.shape[0],), -1, dtype=torch.int64, device=dev)
+        tsrc[inv[: prev.shape[0]]] = src
+        q = inv[prev.shape[0]:]
+        got = table[q]
         if bool((got < 0).any()):
             raise RuntimeError(f"stitch: {int((got < 0).sum())} vertices on the lower faces of rank "
                                f"{rank} have no counterpart on the ranks below")
+        # each needed vertex must come from the rank owner_of names: a record
+        # is published only by its owner, so another source means the ranks
+        # disagree on ownership (a bitwise match against the wrong block)
+        wrong = tsrc[q] != owner[ni]
+        if bool(wrong.any()):
+            raise RuntimeError(f"stitch: {int(wrong.sum())} vertices on the lower faces of rank {rank} "
+                               f"matched a record of a rank other than their owner")
         gid[ni] = got
     if masks:
         return vertices[own], first, gid[e], own, keep

@@ -234,6 +234,20 @@ def subpoly_step(vertices: Tensor, edges: Tensor, cache: Tensor, table: Tensor, 
     return v, e, o
 
 
+def _no_graph(ctx, inputs, output):
+    # the reference's subpoly_ takes outputs_ as the net's forward left it --
+    # a graph-carrying tensor (subpoly.py:93) -- and nothing it returns is
+    # differentiated: the step's outputs carry no graph whatever the inputs
+    ctx.mark_non_differentiable(*output)
+
+
+def _no_grads(ctx, *grads):
+    return (None,) * 14
+
+
+subpoly_step.register_autograd(_no_grads, setup_context=_no_graph)
+
+
 @subpoly_step.register_fake
 def _(vertices, edges, cache, table, level_meta, scales, weights, marks, eps, num_layers,
       num_hidden, idx, prune, force):
