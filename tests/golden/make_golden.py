@@ -128,6 +128,11 @@ CASES = {
     "h16l5_sphere": ("subpoly", dict(SMALL, num_layers=5), ("fit", sphere, 61), None),
     "synth16_h32l3": ("lattice", None, ("rand", 53, 0.1), (16, 19, dict(num_layers=3, num_hidden=32))),
     "synth8_h32l4": ("lattice", None, ("rand", 59, 0.1), (8, 19, dict(num_layers=4, num_hidden=32))),
+    # the curve branch (force=False) on K = 65 nets: two-word sign keys through
+    # the corner forward, the failover shared planes and the 32- / 16-wide
+    # descent
+    "h32l3_rand_curve": ("curve", dict(SMALL, num_layers=3, num_hidden=32), ("same", "h32l3_rand"), None),
+    "h16l5_sphere_curve": ("curve", dict(SMALL, num_layers=5), ("same", "h16l5_sphere"), None),
     # the curve branch with strict=False (subpoly_(..., strict=False),
     # subpoly.py:198-203): every split stays, no strict_check -- driven step
     # by step through subpoly_ from the skeleton (subpoly() never passes it)

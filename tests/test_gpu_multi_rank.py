@@ -176,7 +176,10 @@ def _unsharded(cuda, case, mode):
 
 @pytest.mark.parametrize("case,world,mode", [("synth32h", 2, "lattice"), ("synth32h", 3, "lattice"),
                                              ("synth64h", 2, "lattice"), ("synth64h", 8, "lattice"),
-                                             ("synth32h", 4, "lattice_blocks"), ("synth64h", 8, "lattice_blocks")])
+                                             ("synth32h", 4, "lattice_blocks"), ("synth64h", 8, "lattice_blocks"),
+                                             # K = 65 (two-word sign keys) on shards
+                                             ("synth16_h32l3", 2, "lattice"),
+                                             ("synth16_h32l3", 4, "lattice_blocks")])
 def test_sharded_lattice_engine(cuda, tmp_path, case, world, mode):
     """x-slabs, and blocks (2 x 2 x 1, 2 x 2 x 2: the box lattice, owned box
     and span of the engine, halo_check over every cut face, the stitch's
@@ -208,7 +211,9 @@ def test_sharded_stanford_net(cuda, tmp_path, case, world, mode):
 @pytest.mark.parametrize("case,world,mode", [("small_sphere_curve", 2, "curve"), ("small_sphere_curve", 3, "curve"),
                                              ("small_torus_curve", 2, "curve"),
                                              ("small_sphere_curve", 4, "curve_blocks"),
-                                             ("small_torus_curve", 8, "curve_blocks")])
+                                             ("small_torus_curve", 8, "curve_blocks"),
+                                             # K = 65: two-word keys through the curve branch's shards
+                                             ("h16l5_sphere_curve", 2, "curve")])
 def test_sharded_curve_branch(cuda, tmp_path, case, world, mode):
     """The curve branch (force=False) on x-slabs: the per-step decisions the
     reference takes over the whole batch -- the curve rows' and descent rows'

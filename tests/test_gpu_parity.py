@@ -360,25 +360,6 @@ def test_subpoly_step_rewrites_caller_edges(cuda, force):
         break
 
 
-@pytest.mark.parametrize("name", WIDE[:1])
-def test_wide_net_refuses_curve_and_shards(cuda, name):
-    """A K > 63 net runs the flat single-device path; the curve branch and
-    sharding refuse it with a message instead of computing on one-word keys."""
-    from tropical._engine import engine_for
-    d = load(name)
-    net = product_net(d, cuda)
-    eng = engine_for(net)
-    eng.skeleton(128, 1.2)
-    v0, e0, _ = eng.export()
-    eng.load(v0, e0, keep_all=True)
-    eng.set_curve(True)
-    try:
-        with pytest.raises(RuntimeError, match="two-word sign keys"):
-            eng.split(0)
-    finally:
-        eng.set_curve(False)
-
-
 @pytest.mark.parametrize("name", ["small_sphere", "synth32"])
 def test_row_order_fast_path_is_the_full_sort(cuda, name, monkeypatch):
     """Faces F4: rows without an exact key tie are ordered in registers

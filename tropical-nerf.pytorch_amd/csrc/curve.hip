@@ -56,6 +56,7 @@ __global__ void k_curve_rows(const int32_t* __restrict__ cflag, const int64_t* _
   if (r < S && cflag[r]) crow[coff[r]] = (int32_t)r;
 }
 
+template <int KW>
 __global__ void k_curve_corners(const int32_t* __restrict__ crow, int64_t B,
                                 const int32_t* __restrict__ sa, const int32_t* __restrict__ sb,
                                 const float* __restrict__ xyz, const uint64_t* __restrict__ zero,
@@ -74,16 +75,17 @@ __global__ void k_curve_corners(const int32_t* __restrict__ crow, int64_t B,
   if (n == 0) {
     // last plane j < idx both endpoints are eps-zero on (nonzero_last,
     // torch_ext.py:18-29); none -> the reference exit()s (subpoly.py:141-148)
-    uint64_t below = (idx >= 64) ? ~0ull : ((1ull << idx) - 1ull);
-    uint64_t m = zero[e[0]] & zero[e[1]] & below;
-    plane[b] = m ? 63 - __builtin_clzll(m) : 0;
-    if (!m) atomicOr((unsigned long long*)&ctr[CTR_NOPLANE], 1ull);
+    const Key<KW> zz = tnp::key_load<KW>(zero, e[0]) & tnp::key_load<KW>(zero, e[1]);
+    const Key<KW> m = zz & tnp::key_below<KW>(idx);
+    const int hi = tnp::key_high(m);
+    plane[b] = hi ? hi - 1 : 0;
+    if (!hi) atomicOr((unsigned long long*)&ctr[CTR_NOPLANE], 1ull);
     // check_new_vertices_on_two_planes (subpoly.py:134-135, subpoly_debug.py:
     // 96-104): the endpoints share fewer than two zero columns (every plane,
     // plus grid axes with both on the same mark) -> the reference's
     // diagnostic print fails (AttributeError: Tensor.astype)
     const uint64_t ga = grid[e[0]], gb = grid[e[1]];
-    int shared = __popcll(zero[e[0]] & zero[e[1]]);
+    int shared = tnp::key_pop(zz);
 #pragma unroll
     for (int d = 0; d < 3; ++d)
       shared += tnp::grid_zero(ga, d) && tnp::grid_zero(gb, d) && tnp::grid_off(ga, d) == tnp::grid_off(gb, d);
@@ -759,6 +761,7 @@ __global__ void k_curve_apply(int64_t B, const int32_t* __restrict__ crow,
 }
 
 // strict_check (subpoly_debug.py:234-271) after the override
+template <int KW>
 __global__ void k_strict_keep(int64_t S, const int32_t* __restrict__ cinfo,
                               const float* __restrict__ stage, int idx, int override_,
                               const uint64_t* __restrict__ shared, float eps, int tight, int strict,
@@ -766,7 +769,7 @@ __global__ void k_strict_keep(int64_t S, const int32_t* __restrict__ cinfo,
   int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= S) return;
   float chk = stage[(int64_t)idx * S + r];
-  if (override_ && ((shared[r] >> idx) & 1)) chk = 0.f;
+  if (override_ && tnp::key_test(tnp::key_load<KW>(shared, r), idx)) chk = 0.f;
   bool k = fabsf(chk) < eps;
   int ci = cinfo[r];
   if (ci & 1) k = k && !(ci & 2) && (!tight || (ci & 4));
@@ -775,6 +778,7 @@ __global__ void k_strict_keep(int64_t S, const int32_t* __restrict__ cinfo,
 
 // surviving splits -> consecutive new ids in edge order; the split edge's
 // second endpoint becomes the new vertex (masked_scatter_, subpoly.py:211)
+template <int KW>
 __global__ void k_compact_splits(int64_t S, int K, const int32_t* __restrict__ keep,
                                  const int64_t* __restrict__ nid, const int32_t* __restrict__ eidx,
                                  int64_t V, const int32_t* __restrict__ sa,
@@ -790,7 +794,7 @@ __global__ void k_compact_splits(int64_t S, int K, const int32_t* __restrict__ k
   int64_t n = nid[r];
   sa2[n] = sa[r];
   sb2[n] = sb[r];
-  shared2[n] = shared[r];
+  tnp::key_store(shared2, n, tnp::key_load<KW>(shared, r));
   for (int p = 0; p < K; ++p) stage2[(int64_t)p * S2 + n] = stage[(int64_t)p * S + r];
 #pragma unroll
   for (int d = 0; d < 3; ++d) xyz2[3 * n + d] = xyz[3 * (V + r) + d];
@@ -817,10 +821,14 @@ int launch_curve_rows(const int32_t* cflag, const int64_t* coff, int64_t S, int3
 }
 int launch_curve_corners(const int32_t* crow, int64_t B, const int32_t* sa, const int32_t* sb,
                          const float* xyz, const uint64_t* zero, const uint64_t* grid, int idx, float* corners,
-                         int32_t* plane, int64_t* ctr, hipStream_t s) {
+                         int32_t* plane, int64_t* ctr, int kw, hipStream_t s) {
   if (B <= 0) return 0;
-  hipLaunchKernelGGL(k_curve_corners, dim3(tnp_grid(8 * B)), dim3(TNP_BLOCK), 0, s, crow, B, sa, sb,
-                     xyz, zero, grid, idx, corners, plane, ctr);
+  if (kw == 2)
+    hipLaunchKernelGGL(k_curve_corners<2>, dim3(tnp_grid(8 * B)), dim3(TNP_BLOCK), 0, s, crow, B, sa, sb,
+                       xyz, zero, grid, idx, corners, plane, ctr);
+  else
+    hipLaunchKernelGGL(k_curve_corners<1>, dim3(tnp_grid(8 * B)), dim3(TNP_BLOCK), 0, s, crow, B, sa, sb,
+                       xyz, zero, grid, idx, corners, plane, ctr);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
@@ -853,7 +861,7 @@ int launch_descend(const NetDev& net, int64_t G, const int32_t* glist, const int
                    int idx, float eps, int iters, int record, float* ints, float* d0s, float* d1s,
                    unsigned long long* conv, hipStream_t s) {
   if (G <= 0) return 0;
-  if (!net_supported_full(net)) { tnp_set_error("the curve descent: net shape not instantiated (the K > 63 shapes run the flat path only)"); return -1; }
+  if (!net_supported(net)) { tnp_set_error("the curve descent: net shape not instantiated"); return -1; }
   if (iters > 512) { tnp_set_error("descend: at most 512 iterations"); return -1; }
   // TNP_DESCEND_THREAD=1: the one-thread-per-row kernel (tests compare both)
   const char* pt = getenv("TNP_DESCEND_THREAD");
@@ -872,10 +880,15 @@ int launch_curve_apply(int64_t B, const int32_t* crow, const int32_t* sa, const 
   return 0;
 }
 int launch_strict_keep(int64_t S, const int32_t* cinfo, const float* stage, int idx, int override_,
-                       const uint64_t* shared, float eps, int tight, int strict, int32_t* keep, hipStream_t s) {
+                       const uint64_t* shared, float eps, int tight, int strict, int32_t* keep, int kw,
+                       hipStream_t s) {
   if (S <= 0) return 0;
-  hipLaunchKernelGGL(k_strict_keep, dim3(tnp_grid(S)), dim3(TNP_BLOCK), 0, s, S, cinfo, stage, idx,
-                     override_, shared, eps, tight, strict, keep);
+  if (kw == 2)
+    hipLaunchKernelGGL(k_strict_keep<2>, dim3(tnp_grid(S)), dim3(TNP_BLOCK), 0, s, S, cinfo, stage, idx,
+                       override_, shared, eps, tight, strict, keep);
+  else
+    hipLaunchKernelGGL(k_strict_keep<1>, dim3(tnp_grid(S)), dim3(TNP_BLOCK), 0, s, S, cinfo, stage, idx,
+                       override_, shared, eps, tight, strict, keep);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
@@ -884,11 +897,16 @@ int launch_compact_splits(int64_t S, int K, const int32_t* keep, const int64_t* 
                           const uint64_t* shared, const float* stage, const float* xyz,
                           const uint64_t* grid, int64_t S2, int32_t* sa2, int32_t* sb2,
                           uint64_t* shared2, float* stage2, float* xyz2, uint64_t* grid2,
-                          int32_t* edges, hipStream_t s) {
+                          int32_t* edges, int kw, hipStream_t s) {
   if (S <= 0) return 0;
-  hipLaunchKernelGGL(k_compact_splits, dim3(tnp_grid(S)), dim3(TNP_BLOCK), 0, s, S, K, keep, nid,
-                     eidx, V, sa, sb, shared, stage, xyz, grid, S2, sa2, sb2, shared2, stage2, xyz2,
-                     grid2, edges);
+  if (kw == 2)
+    hipLaunchKernelGGL(k_compact_splits<2>, dim3(tnp_grid(S)), dim3(TNP_BLOCK), 0, s, S, K, keep, nid,
+                       eidx, V, sa, sb, shared, stage, xyz, grid, S2, sa2, sb2, shared2, stage2, xyz2,
+                       grid2, edges);
+  else
+    hipLaunchKernelGGL(k_compact_splits<1>, dim3(tnp_grid(S)), dim3(TNP_BLOCK), 0, s, S, K, keep, nid,
+                       eidx, V, sa, sb, shared, stage, xyz, grid, S2, sa2, sb2, shared2, stage2, xyz2,
+                       grid2, edges);
   TNP_CHECK(hipGetLastError());
   return 0;
 }

@@ -3,7 +3,7 @@
 // forward at the row's point on its edge, the gradient of d0^2 + d1^2 by
 // torch autograd's CPU schedules, a normalised step.  Included by net_lv.hip
 // (one translation unit per level count, every hidden/layer shape of
-// TNP_NET_SHAPES: lv_descend), launched by curve.hip launch_descend.
+// TNP_ALL_SHAPES: lv_descend), launched by curve.hip launch_descend.
 #pragma once
 #include "common.h"
 #include "kernels.h"

@@ -186,6 +186,7 @@ struct tnp_engine {
   int64_t E_live = 0;
   int keep_all = 0;
   int valid_from = 0;  // pre planes [valid_from, K) are valid for every vertex
+  int pend_keep = 0;   // the pending flat step's new vertices get planes [pend_keep, K) (new_keep_from)
   // Lazy compaction: during the hot loop vertex ids are SLOTS (V = slots in
   // use); pruned vertices stay in place, flagged dead in `used` (the live
   // flags).  Slot order == the reference's compacted id order (compaction
@@ -388,8 +389,8 @@ static int vset_ensure(tnp_engine* e, VSet& v, int64_t rows, int64_t keep_rows, 
 
 static int keys_for(tnp_engine* e, VSet& v, int64_t from, int64_t n, hipStream_t s) {
   return launch_keys(e->net, P<float>(v.xyz) + 3 * from, P<float>(v.pre) + from, v.cap, n, e->K,
-                     P<uint64_t>(v.pos) + from, P<uint64_t>(v.zero) + from,
-                     P<uint64_t>(v.grid) + from, s, P<uint64_t>(v.pz) + 2 * from);
+                     P<uint64_t>(v.pos) + from * e->kw, P<uint64_t>(v.zero) + from * e->kw,
+                     P<uint64_t>(v.grid) + from, s, P<uint64_t>(v.pz) + 2 * e->kw * from);
 }
 
 // live flags of slots [from, from + n) := 1 (kept capacity: earlier flags stay)
@@ -431,6 +432,17 @@ static bool uses_buckets(const tnp_engine* e, BucketGeom* bg) {
 
 // split-eps mode: subpoly's eps argument differs from Net.eps (tnp_engine_set_eps)
 static bool eps2(const tnp_engine* e) { return e->net.eps_s != e->net.eps; }
+
+// the cache planes a flat step at plane idx stores for its new vertices:
+// those a later step, the surface (plane K - 1) or an export can read.  In the
+// hot loop that is planes > idx (the step's pruning moves valid_from to
+// idx + 1; the last plane always) -- not [valid_from, idx], dead the moment
+// the step ends (up to 15 of 33 planes a split at 128^3).  A caller that
+// hands outputs_ back (keep_all) or the split-eps mode keeps every plane.
+static int new_keep_from(const tnp_engine* e, int idx) {
+  if (e->keep_all || eps2(e)) return e->valid_from;
+  return std::max(e->valid_from, std::min(idx + 1, e->K - 1));
+}
 
 // per-edge high plane and first split plane (>= from) from the endpoint
 // keys; ctr != null: the OR of the first split planes -> ctr[CTR_ACTIVE]
@@ -938,7 +950,7 @@ static int curve_correct(tnp_engine* e, int idx, int64_t S, hipStream_t s) {
   if (launch_curve_rows(P<int32_t>(cv[CV_CFLAG]), P<int64_t>(cv[CV_COFF]), S, crow, s)) return -1;
   TIMED("curve_corners", 8.0 * B * 12 + 24.0 * B,
         launch_curve_corners(crow, B, sa, sb, xyz, P<uint64_t>(e->cur.zero), P<uint64_t>(e->cur.grid), idx,
-                             P<float>(cv[CV_CORNERS]), plane, ctr, s));
+                             P<float>(cv[CV_CORNERS]), plane, ctr, e->kw, s));
   if (sh) ns.sched_rows = 8 * Bg;
   TIMED("curve_forward", 8.0 * B * (12 + 4.0 * K),
         launch_forward(ns, P<float>(cv[CV_CORNERS]), 8 * B, P<float>(cv[CV_STAGE_C]), 8 * B, 8, s));
@@ -1034,7 +1046,8 @@ static int curve_filter(tnp_engine* e, int idx, int override_, hipStream_t s, in
   if (buf_ensure(cv[CV_KEEP], S * sizeof(int32_t), s)) return -1;
   if (buf_ensure(cv[CV_NID], S * sizeof(int64_t), s)) return -1;
   if (launch_strict_keep(S, P<int32_t>(cv[CV_CINFO]), P<float>(e->stage), idx, override_,
-                         P<uint64_t>(e->shared), e->net.eps_s, e->pend_tight, e->strict, P<int32_t>(cv[CV_KEEP]), s))
+                         P<uint64_t>(e->shared), e->net.eps_s, e->pend_tight, e->strict, P<int32_t>(cv[CV_KEEP]),
+                         e->kw, s))
     return -1;
   if (scan_counts(e, P<int32_t>(cv[CV_KEEP]), P<int64_t>(cv[CV_NID]), S, CTR_KEEP, s)) return -1;
   if (read_ctr(e, s)) return -1;
@@ -1042,7 +1055,7 @@ static int curve_filter(tnp_engine* e, int idx, int override_, hipStream_t s, in
   const int64_t n = std::max<int64_t>(S2, 1);
   if (buf_ensure(cv[CV_SA2], n * sizeof(int32_t), s)) return -1;
   if (buf_ensure(cv[CV_SB2], n * sizeof(int32_t), s)) return -1;
-  if (buf_ensure(cv[CV_SHARED2], n * sizeof(uint64_t), s)) return -1;
+  if (buf_ensure(cv[CV_SHARED2], n * sizeof(uint64_t) * e->kw, s)) return -1;
   if (buf_ensure(cv[CV_STAGE2], (size_t)n * K * sizeof(float), s)) return -1;
   if (buf_ensure(cv[CV_XYZ2], 3 * n * sizeof(float), s)) return -1;
   if (buf_ensure(cv[CV_GRID2], n * sizeof(uint64_t), s)) return -1;
@@ -1053,7 +1066,7 @@ static int curve_filter(tnp_engine* e, int idx, int override_, hipStream_t s, in
                               P<uint64_t>(e->cur.grid), S2, P<int32_t>(cv[CV_SA2]),
                               P<int32_t>(cv[CV_SB2]), P<uint64_t>(cv[CV_SHARED2]),
                               P<float>(cv[CV_STAGE2]), P<float>(cv[CV_XYZ2]),
-                              P<uint64_t>(cv[CV_GRID2]), P<int32_t>(e->edges), s));
+                              P<uint64_t>(cv[CV_GRID2]), P<int32_t>(e->edges), e->kw, s));
   if (S2 > 0) {
     TNP_CHECK(hipMemcpyAsync(P<float>(e->cur.xyz) + 3 * V, cv[CV_XYZ2].p, 3 * S2 * sizeof(float),
                              hipMemcpyDeviceToDevice, s));
@@ -1110,11 +1123,6 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
     return -1;
   }
   if (require_valid(e, "split")) return -1;
-  if (e->kw != 1 && (e->curve || e->shards > 1)) {
-    tnp_set_error("a net of %d planes (two-word sign keys) runs the flat single-device path only "
-                  "(no force=False curve branch, no sharding)", e->K);
-    return -1;
-  }
   e->valid = false;  // until this split has completed
   const float eps = e->net.eps_s;  // subpoly_'s eps: hits, split point, failover
   const float* col = P<float>(e->cur.pre) + (int64_t)idx * e->cur.cap;
@@ -1208,11 +1216,12 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
       // writes 12 B coordinates, the cache planes >= valid_from, 48 B keys
       // (pos, zero, pz, grid, shared); plus the encoding tables once per
       // launch (the 8 corners x L levels gathers are cache traffic)
+      e->pend_keep = new_keep_from(e, idx);
       TIMED("forward_new",
-            (8.0 + 24.0 + 8.0 + 16.0 + 12.0 + 4.0 * (e->K - e->valid_from) + 48.0) * S +
+            (8.0 + 24.0 + 8.0 + 16.0 + 12.0 + 4.0 * (e->K - e->pend_keep) + 48.0) * S +
                 table_bytes(e->net),
             launch_forward_new(e->net, P<float>(e->cur.xyz) + 3 * e->V, S, P<float>(e->cur.pre),
-                               e->cur.cap, e->V, e->valid_from, P<int32_t>(e->sa), P<int32_t>(e->sb),
+                               e->cur.cap, e->V, e->pend_keep, P<int32_t>(e->sa), P<int32_t>(e->sb),
                                idx, e->own, P<uint64_t>(e->cur.pos),
                                P<uint64_t>(e->cur.zero), P<uint64_t>(e->cur.grid),
                                P<uint64_t>(e->shared), P<int64_t>(e->ctr), P<uint64_t>(e->cur.pz),
@@ -1226,13 +1235,13 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
       // grid words of the new vertices (coordinates are final; the failover
       // test of a shard reads them: only owned vertices vote)
       if (launch_keys(e->net, P<float>(e->cur.xyz) + 3 * e->V, P<float>(e->stage), S, S, 0,
-                      P<uint64_t>(e->cur.pos) + e->V, P<uint64_t>(e->cur.zero) + e->V,
+                      P<uint64_t>(e->cur.pos) + e->V * e->kw, P<uint64_t>(e->cur.zero) + e->V * e->kw,
                       P<uint64_t>(e->cur.grid) + e->V, s))
         return -1;
       TIMED("fail_check", 48.0 * S,
             launch_fail_check(P<int32_t>(e->sa), P<int32_t>(e->sb), S, idx, P<uint64_t>(e->cur.zero),
                               P<float>(e->stage), eps, P<uint64_t>(e->shared), P<int64_t>(e->ctr),
-                              P<uint64_t>(e->cur.grid) + e->V, e->own, s));
+                              P<uint64_t>(e->cur.grid) + e->V, e->own, e->kw, s));
     }
     if (e->curve || e->shards > 1) {
       // the host takes the global override decision (all-reduce) / the curve
@@ -1304,12 +1313,12 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   } else if (e->pend_fused) {
     TIMED("override_new", 8.0 * S,
           launch_override_new(S, override_, P<uint64_t>(e->shared), P<float>(c.pre), c.cap,
-                              e->valid_from, V, pos, zero, ctr, P<uint64_t>(c.pz), e->kw, s));
+                              e->pend_keep, V, pos, zero, ctr, P<uint64_t>(c.pz), e->kw, s));
   } else {
     TIMED("finalize_new", (8.0 + 4.0 * K + 4.0 * (K - e->valid_from) + 16.0) * S,
           launch_finalize_new(S, K, override_, P<uint64_t>(e->shared), P<float>(e->stage), eps,
                               P<float>(c.pre), c.cap, e->valid_from, V, pos, zero, ctr,
-                              P<uint64_t>(c.pz), s));
+                              P<uint64_t>(c.pz), e->kw, s));
   }
 
   // 2. members = new vertices ++ live hit vertices (any order); the bucket
@@ -1364,7 +1373,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     // a pruning step recomputes the live flags: zeroed by the bucket count
     // (after the hit pass read them), re-marked by the prune
     if (prune && buf_ensure(e->live, std::max<int64_t>(NV + 4, 16), s)) return -1;
-    NewOverride nov{override_, P<uint64_t>(e->shared), P<float>(c.pre), c.cap, e->valid_from, pos, zero,
+    NewOverride nov{override_, P<uint64_t>(e->shared), P<float>(c.pre), c.cap, e->pend_keep, pos, zero,
                     P<uint64_t>(c.pz)};
     TIMED("bucket_entries", 16.0 * M,  // + 8 B per entry, set once T is known
           // (member m >= S is members[m]: the hits sit at hoff >= S when the split found them)
@@ -1690,6 +1699,9 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     if (read_ctr(e, s)) return -1;
   }
   if (swap_edges) std::swap(e->edges, e->edges_alt);
+  // the new vertices hold planes >= pend_keep only: valid_from never claims
+  // the planes below (a step order that could read them needs keep_all)
+  if (e->pend_fused) next_valid = std::max(next_valid, e->pend_keep);
   const int64_t V_in_live = e->V_live;
   e->V = NV;  // slots
   e->V_live = V2;

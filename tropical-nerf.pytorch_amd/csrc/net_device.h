@@ -386,12 +386,17 @@ struct NetShape {
 // the net shapes with kernels: levels 2..8 (one translation unit each,
 // net_lv.hip), (hidden, layers) below -- K = (layers - 1) hidden + 1 <= 63
 // planes fit the 64-bit sign keys
+#ifdef TNP_SHAPES_BENCH_ONLY  // experiment builds (tools/): the bench net's shape only, fast to compile
+#define TNP_NET_SHAPES(X) X(16, 3)
+#define TNP_WIDE_SHAPES(X)
+#else
 #define TNP_NET_SHAPES(X) X(8, 2) X(8, 3) X(8, 4) X(16, 2) X(16, 3) X(16, 4) X(32, 2)
 // wide shapes: K = 65 or 97 planes, two-word sign keys (common.h Key<2>).
 // They run the flat subpoly path (forward, keys, steps, faces), Net.forward /
 // sdf / normal and the skeleton; the curve branch, its descent and the
 // training / autograd kernels stay with TNP_NET_SHAPES
 #define TNP_WIDE_SHAPES(X) X(16, 5) X(32, 3) X(32, 4)
+#endif
 #define TNP_ALL_SHAPES(X) TNP_NET_SHAPES(X) TNP_WIDE_SHAPES(X)
 // sign-key words of a net of K planes
 __host__ __device__ constexpr int key_words(int K) { return K <= 63 ? 1 : 2; }

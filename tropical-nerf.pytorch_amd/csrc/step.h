@@ -74,10 +74,10 @@ int launch_new_vertices(const int32_t* sa, const int32_t* sb, int64_t S, const f
                         float eps, float* xyz, int64_t V, hipStream_t s);
 int launch_fail_check(const int32_t* sa, const int32_t* sb, int64_t S, int idx,
                       const uint64_t* zero, const float* stage, float eps, uint64_t* shared,
-                      int64_t* ctr, const uint64_t* grid_new, const OwnBox& own, hipStream_t s);
+                      int64_t* ctr, const uint64_t* grid_new, const OwnBox& own, int kw, hipStream_t s);
 int launch_finalize_new(int64_t S, int K, int override_, const uint64_t* shared, float* stage,
                         float eps, float* pre, int64_t ld, int keep_from, int64_t V, uint64_t* pos,
-                        uint64_t* zero, const int64_t* ctr, uint64_t* pz, hipStream_t s);
+                        uint64_t* zero, const int64_t* ctr, uint64_t* pz, int kw, hipStream_t s);
 // members = [V, V + S) ++ live vertices v < V with |col[v]| < eps (in no
 // particular order: atomic appends); count -> ctr[CTR_H] (zero on entry).
 // S < 0: the hits only, placed after ctr[CTR_S] members (launched behind
@@ -398,7 +398,7 @@ int launch_curve_rows(const int32_t* cflag, const int64_t* coff, int64_t S, int3
                       hipStream_t s);
 int launch_curve_corners(const int32_t* crow, int64_t B, const int32_t* sa, const int32_t* sb,
                          const float* xyz, const uint64_t* zero, const uint64_t* grid, int idx, float* corners,
-                         int32_t* plane, int64_t* ctr, hipStream_t s);
+                         int32_t* plane, int64_t* ctr, int kw, hipStream_t s);
 int launch_curve_solve(int64_t B, const float* stage_c, int64_t ldc, const int32_t* plane, int idx,
                        const int32_t* crow, const int32_t* sa, const int32_t* sb, const float* xyz,
                        float* ints, float* pts, hipStream_t s);
@@ -415,10 +415,10 @@ int launch_curve_apply(int64_t B, const int32_t* crow, const int32_t* sa, const 
                        float* xyz, int64_t V, const float* ints, const float* d0s, const int32_t* gg,
                        float eps, int32_t* cinfo, int64_t* ctr, hipStream_t s);
 int launch_strict_keep(int64_t S, const int32_t* cinfo, const float* stage, int idx, int override_,
-                       const uint64_t* shared, float eps, int tight, int strict, int32_t* keep, hipStream_t s);
+                       const uint64_t* shared, float eps, int tight, int strict, int32_t* keep, int kw, hipStream_t s);
 int launch_compact_splits(int64_t S, int K, const int32_t* keep, const int64_t* nid,
                           const int32_t* eidx, int64_t V, const int32_t* sa, const int32_t* sb,
                           const uint64_t* shared, const float* stage, const float* xyz,
                           const uint64_t* grid, int64_t S2, int32_t* sa2, int32_t* sb2,
                           uint64_t* shared2, float* stage2, float* xyz2, uint64_t* grid2,
-                          int32_t* edges, hipStream_t s);
+                          int32_t* edges, int kw, hipStream_t s);

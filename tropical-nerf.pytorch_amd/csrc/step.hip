@@ -227,6 +227,7 @@ __global__ void k_new_vertices(const int32_t* __restrict__ sa, const int32_t* __
 // (own_any(own)) only the new vertices it owns vote (grid_new: their grid
 // words), as k_forward_new on the flat path: a halo vertex near the halo's
 // outer faces may belong to an edge the whole complex does not have.
+template <int KW>
 __global__ void k_fail_check(const int32_t* __restrict__ sa, const int32_t* __restrict__ sb,
                              int64_t S, int idx, const uint64_t* __restrict__ zero,
                              const float* __restrict__ stage, float eps,
@@ -235,13 +236,15 @@ __global__ void k_fail_check(const int32_t* __restrict__ sa, const int32_t* __re
   int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   bool bad = false;
   if (r < S) {
-    uint64_t below = (idx >= 64) ? ~0ull : ((1ull << idx) - 1ull);
-    uint64_t m = (zero[sa[r]] & zero[sb[r]] & below) | (1ull << idx);
-    shared[r] = m;
-    for (uint64_t t = m; t; t &= t - 1) {
-      int p = __builtin_ctzll(t);
-      bad |= fabsf(stage[(int64_t)p * S + r]) > eps;
-    }
+    const Key<KW> m = (tnp::key_load<KW>(zero, sa[r]) & tnp::key_load<KW>(zero, sb[r]) & tnp::key_below<KW>(idx)) |
+                      tnp::key_bit<KW>(idx);
+    tnp::key_store(shared, r, m);
+#pragma unroll
+    for (int q = 0; q < KW; ++q)
+      for (uint64_t t = m.w[q]; t; t &= t - 1) {
+        const int p = 64 * q + __builtin_ctzll(t);
+        bad |= fabsf(stage[(int64_t)p * S + r]) > eps;
+      }
     if (tnp::own_any(own)) bad &= tnp::owned_by(own, grid_new[r]);
   }
   if (__ballot(bad) && tnp::lane() == 0) tnp::or_sticky(&ctr[CTR_FAIL], 1ull);
@@ -250,26 +253,27 @@ __global__ void k_fail_check(const int32_t* __restrict__ sa, const int32_t* __re
 // override (masked_fill_ on the shared planes, subpoly_debug.py:48), packed
 // keys of the final pre-activations, live planes copied into the cache.
 // override_ < 0: the (single-device) predicate is still in ctr[CTR_FAIL]
+template <int KW>
 __global__ void k_finalize_new(int64_t S, int K, int override_, const uint64_t* __restrict__ shared,
                                float* __restrict__ stage, float eps, float* __restrict__ pre,
                                int64_t ld, int keep_from, int64_t V, uint64_t* __restrict__ pos,
                                uint64_t* __restrict__ zero, const int64_t* __restrict__ ctr,
-                               ulonglong2* __restrict__ pz) {
+                               uint64_t* __restrict__ pz) {
   int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= S) return;
   const bool ov = override_ < 0 ? ctr[CTR_FAIL] != 0 : override_ != 0;
-  uint64_t m = ov ? shared[r] : 0ull;
-  uint64_t ps = 0, zs = 0;
+  const Key<KW> m = ov ? tnp::key_load<KW>(shared, r) : tnp::key_zero<KW>();
+  Key<KW> ps = tnp::key_zero<KW>(), zs = tnp::key_zero<KW>();
   for (int p = 0; p < K; ++p) {
     float v = stage[(int64_t)p * S + r];
-    if ((m >> p) & 1) v = 0.f;
-    ps |= (uint64_t)(v > eps) << p;   // sign +1  (pos & zero == 0)
-    zs |= (uint64_t)(fabsf(v) <= eps) << p;
+    if (tnp::key_test(m, p)) v = 0.f;
+    tnp::key_put(ps, p, v > eps);  // sign +1  (pos & zero == 0)
+    tnp::key_put(zs, p, fabsf(v) <= eps);
     if (p >= keep_from) pre[(int64_t)p * ld + V + r] = v;
   }
-  pos[V + r] = ps;
-  zero[V + r] = zs;
-  pz[V + r] = make_ulonglong2(ps, zs);
+  tnp::key_store(pos, V + r, ps);
+  tnp::key_store(zero, V + r, zs);
+  tnp::pz_store(pz, V + r, ps, zs);
 }
 
 // ---------------------------------------------------------------------------
@@ -1421,19 +1425,27 @@ int launch_new_vertices(const int32_t* sa, const int32_t* sb, int64_t S, const f
 }
 int launch_fail_check(const int32_t* sa, const int32_t* sb, int64_t S, int idx,
                       const uint64_t* zero, const float* stage, float eps, uint64_t* shared,
-                      int64_t* ctr, const uint64_t* grid_new, const OwnBox& own, hipStream_t s) {
+                      int64_t* ctr, const uint64_t* grid_new, const OwnBox& own, int kw, hipStream_t s) {
   if (S <= 0) return 0;
-  hipLaunchKernelGGL(k_fail_check, dim3(tnp_grid(S)), dim3(TNP_BLOCK), 0, s, sa, sb, S, idx, zero,
-                     stage, eps, shared, ctr, grid_new, own);
+  if (kw == 2)
+    hipLaunchKernelGGL(k_fail_check<2>, dim3(tnp_grid(S)), dim3(TNP_BLOCK), 0, s, sa, sb, S, idx, zero,
+                       stage, eps, shared, ctr, grid_new, own);
+  else
+    hipLaunchKernelGGL(k_fail_check<1>, dim3(tnp_grid(S)), dim3(TNP_BLOCK), 0, s, sa, sb, S, idx, zero,
+                       stage, eps, shared, ctr, grid_new, own);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
 int launch_finalize_new(int64_t S, int K, int override_, const uint64_t* shared, float* stage,
                         float eps, float* pre, int64_t ld, int keep_from, int64_t V, uint64_t* pos,
-                        uint64_t* zero, const int64_t* ctr, uint64_t* pz, hipStream_t s) {
+                        uint64_t* zero, const int64_t* ctr, uint64_t* pz, int kw, hipStream_t s) {
   if (S <= 0) return 0;
-  hipLaunchKernelGGL(k_finalize_new, dim3(tnp_grid(S)), dim3(TNP_BLOCK), 0, s, S, K, override_,
-                     shared, stage, eps, pre, ld, keep_from, V, pos, zero, ctr, reinterpret_cast<ulonglong2*>(pz));
+  if (kw == 2)
+    hipLaunchKernelGGL(k_finalize_new<2>, dim3(tnp_grid(S)), dim3(TNP_BLOCK), 0, s, S, K, override_,
+                       shared, stage, eps, pre, ld, keep_from, V, pos, zero, ctr, pz);
+  else
+    hipLaunchKernelGGL(k_finalize_new<1>, dim3(tnp_grid(S)), dim3(TNP_BLOCK), 0, s, S, K, override_,
+                       shared, stage, eps, pre, ld, keep_from, V, pos, zero, ctr, pz);
   TNP_CHECK(hipGetLastError());
   return 0;
 }

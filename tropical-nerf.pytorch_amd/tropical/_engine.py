@@ -303,7 +303,9 @@ class Engine:
         if allreduce is not None:
             mask = int(allreduce(np.array([mask], dtype=np.uint64), "or")[0])
         for idx in range(K):
-            if not (mask >> idx) & 1:
+            # active-plane words keep planes 0..62 and fold 63.. into bit 63
+            # (common.h act_bit): a wide net's planes >= 63 are never skipped
+            if not (mask >> min(idx, 63)) & 1:
                 continue
             S, fail = self.split(idx)
             if allreduce is not None:
@@ -321,7 +323,8 @@ class Engine:
                 m2 = st["next_active"]
                 if allreduce is not None:
                     m2 = int(allreduce(np.array([m2], dtype=np.uint64), "or")[0])
-                mask = (mask & ((1 << (idx + 1)) - 1)) | m2
+                keep = (1 << 63) - 1 if idx >= 62 else (1 << (idx + 1)) - 1
+                mask = (mask & keep) | m2
         return stats
 
 
