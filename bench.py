@@ -479,11 +479,11 @@ def main():
     # 12 contain regions of 1e5-1e7 vertices (seed 8: 5.5e13 in-region pairs)
     # that the reference's CPU path could not materialise (tools/seed_scan.py)
     ap.add_argument("--seed", type=int, default=6)
-    # the CPU baseline's sample: the whole lattice of this many
-    # marks per axis, same seed (48: ~8 s of CPU work on the GPU box's 16-core
-    # share, so the default run finishes in a few minutes; 64 took over three
-    # minutes there; 128 is the benchmarked workload itself, ~18 min)
-    ap.add_argument("--cpu-marks", type=int, default=int(os.environ.get("TNP_CPU_MARKS", 48)))
+    # the CPU baseline's sample (BASELINE.md §3's budget fallback, N = 64): the
+    # whole 64^3 lattice of the same net and seed (48^3 took 7.9 s on the GPU
+    # box's 16-core share in round 4; 64^3 holds ~2.4x its vertices; 128 is the
+    # benchmarked workload itself, ~18 min of the reference's CPU path)
+    ap.add_argument("--cpu-marks", type=int, default=int(os.environ.get("TNP_CPU_MARKS", 64)))
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
 

@@ -60,6 +60,7 @@ def _sharded_lattice(net, rank, world, coll, stats, blocks=False):
         if D.halo_check(Vl, El, marks, part, raise_=k == len(D.HALOS) - 1) is not None:
             break
     stats.extend(st)
+    _sharded_lattice.attempts = k + 1  # extractions the halo search ran
     return part, Vl, El, h
 
 
@@ -104,6 +105,7 @@ def _worker(rank, world, port, outdir, case, mode):
             if rank == 0:
                 np.savez(os.path.join(outdir, "out.npz"), tot=tot.numpy(), dims=np.array(part.dims),
                          halo=np.array(halo), redundant=np.array(part.redundant_frac(rank, halo)),
+                         attempts=np.array(_sharded_lattice.attempts),
                          steady=steady.numpy(), foot=np.array([f["bytes"] for f in foot]))
             return
         d = load(case)
@@ -115,8 +117,9 @@ def _worker(rank, world, port, outdir, case, mode):
         else:  # "skeleton" (flat) or "curve" (force=False: the curve branch's decisions go
             # through the engine's collective callback)
             curve = mode.startswith("curve")
+            info = {}
             eng, owned, first, gE, cuts = D.subpoly_sharded(net, 1.2, allreduce=coll, stats=stats,
-                                                            force=not curve, blocks=blocks)
+                                                            force=not curve, blocks=blocks, info=info)
             Vl, El, _ = eng.export()
             Vl, El = Vl.cpu(), El.cpu()
             own, keep = D.owned_masks(Vl, El, net.enc.marks.cpu(), cuts, rank)
@@ -139,10 +142,11 @@ def _worker(rank, world, port, outdir, case, mode):
             single_ok[0] = int(verts.shape[0] == int(d["n_surf"][0]) and
                                sha(np.asarray(fwi, dtype=np.int64)) == str(d["sha_tri"]))
         dist.all_reduce(single_ok, op=dist.ReduceOp.MIN)
+        attempts = _sharded_lattice.attempts if mode.startswith("lattice") else info["halo_attempts"]
         if rank == 0:
             np.savez(os.path.join(outdir, "out.npz"), tot=tot.numpy(), V=SV.numpy(), E=SE.numpy(),
                      cuts=np.array(cuts.cuts[0] if isinstance(cuts, D.Blocks) else cuts),
-                     single_ok=single_ok.numpy())
+                     single_ok=single_ok.numpy(), attempts=np.array(attempts))
     finally:
         dist.destroy_process_group()
 
@@ -203,6 +207,8 @@ def test_sharded_stanford_net(cuda, tmp_path, case, world, mode):
     d, V, E, want = _unsharded(cuda, case, "skeleton")
     z = _run(tmp_path, case, mode, world)
     assert tuple(int(x) for x in z["tot"]) == want
+    if mode == "skeleton_blocks":  # the halo search accepts its first width: one extraction
+        assert int(z["attempts"]) == 1
     cuts = z["cuts"].tolist()
     assert cuts[0] == 0 and cuts[-1] == len(d["marks"]) - 1
     assert len(cuts) == (world + 1 if mode == "skeleton" else 3)
@@ -262,6 +268,7 @@ def test_lattice256_eight_slabs_stitch_to_the_unsharded_complex(cuda, tmp_path, 
     if mode == "bench_blocks":
         assert z["dims"].tolist() == [2, 2, 2]
         assert float(z["redundant"]) <= 0.07, (int(z["halo"]), float(z["redundant"]))
+        assert int(z["attempts"]) == 1  # no rejected extraction in the halo search
 
 
 def _unsharded_bench(cuda, G, seed):

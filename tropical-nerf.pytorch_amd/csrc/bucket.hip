@@ -1312,6 +1312,7 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
                     wa.xs, ctr, W, a);
       }
       BG_PH(6);
+      fold_wave_counts(a);
       window_flush(wa.keys, wa.cap, wa.xs, ctr, W, a);
       int64_t tc, tr, tx;
       tnp::block_scan_excl(a.n_compat, lds, tc);

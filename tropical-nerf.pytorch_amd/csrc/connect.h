@@ -117,7 +117,21 @@ struct WinLds {
 struct WinAcc {
   int kn = 0;  // wave-uniform fill of this wave's key buffer
   int64_t n_compat = 0, n_reg = 0, n_conn = 0;
+  // (packed path) wave-uniform counts from the tests' ballots, scalar
+  // registers instead of a per-lane 64-bit add per test; folded into lane 0's
+  // n_compat / n_conn by fold_wave_counts before the block sums
+  int64_t w_compat = 0, w_conn = 0;
 };
+__device__ __forceinline__ void fold_wave_counts(WinAcc& a) {
+  if (tnp::lane() == 0) {
+    a.n_compat += a.w_compat;
+    a.n_conn += a.w_conn;
+  }
+  a.w_compat = a.w_conn = 0;
+}
+// a value every lane holds alike, as a scalar (wave-uniform branches and loop
+// bounds instead of exec-mask juggling)
+__device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // this wave's buffered keys -> its XCD shard's key region (xs != null) or
 // the one key array, counted there
@@ -188,7 +202,7 @@ __device__ __forceinline__ void window_pass_packed(const CellEnt* __restrict__ e
                                                    WinLds& W, WinAcc& a) {
   const int wv = tnp::wave(), L = tnp::lane();
   for (int w = w0; w < nwin; w += dw) {
-    const uint32_t se = wl[w];
+    const uint32_t se = (uint32_t)uniform((int)wl[w]);
     const int s = (int)(se & 0xFFFFu), n = (int)(se >> 16) - s;
     const bool valid = L < n;
     CellEnt r;
@@ -221,7 +235,7 @@ __device__ __forceinline__ void window_pass_lds(const CellEnt* rec, int p0, int 
                                                 WinLds& W, WinAcc& a) {
   const int L = tnp::lane();
   for (; *k < nwin; *k += dw) {
-    const uint32_t se = wl[*k];
+    const uint32_t se = (uint32_t)uniform((int)wl[*k]);
     const int s = (int)(se & 0xFFFFu), n = (int)(se >> 16) - s;
     if (s >= p_end) break;
     const CellEnt* st = rec + (s - p0);
@@ -273,7 +287,7 @@ __device__ __forceinline__ void window_tests_packed(const PackedRecs& R, int s, 
                                                     int64_t* __restrict__ ctr, WinLds& W, WinAcc& a) {
   const int wv = tnp::wave(), L = tnp::lane();
   const int incl = tnp::wave_scan_incl(rounds);
-  const int total = __shfl(incl, 63, 64);
+  const int total = uniform(__shfl(incl, 63, 64));
   const bool table = total <= WOWN;
   W.exc[wv][L] = incl - rounds;
   if (table)
@@ -311,9 +325,9 @@ __device__ __forceinline__ void window_tests_packed(const PackedRecs& R, int s, 
     const uint32_t zz = below & ~(hu | hv);
     const bool compat = live & canon & (d == 0u);
     const bool emit = compat & ((sp | zz) != 0u);
-    a.n_compat += compat;
+    a.w_compat += __popcll(__ballot(compat));
     a.n_reg += compat ? ((int64_t)1 << (__popc(sp) + __popc(zz))) : 0;
-    a.n_conn += emit;
+    a.w_conn += __popcll(__ballot(emit));
     key = ((uint64_t)min(vu, vq) << nb) | max(vu, vq);
     // the step's pruning drops it anyway (keep_edge): never appended
     return emit & ((amask == 0) | (((au ^ av) & amask) != 0));
@@ -359,7 +373,7 @@ __device__ __forceinline__ void window_pass_packed_lds(const PackedRecs& R, int 
                                                        WinLds& W, WinAcc& a) {
   const int L = tnp::lane();
   for (; *k < nwin; *k += dw) {
-    const uint32_t se = wl[*k];
+    const uint32_t se = (uint32_t)uniform((int)wl[*k]);
     const int s = (int)(se & 0xFFFFu), n = (int)(se >> 16) - s;
     if (s >= p_end) break;
     const bool valid = L < n;
@@ -379,7 +393,7 @@ __device__ __forceinline__ void window_tests(const CellEnt* st, int rounds, uint
     // flatten the window's (initiator, partner) tests over the lanes: test t
     // belongs to the last initiator j with exc[j] <= t, partner j + 1 + t - exc[j]
     const int incl = tnp::wave_scan_incl(rounds);
-    const int total = __shfl(incl, 63, 64);
+    const int total = uniform(__shfl(incl, 63, 64));
     const bool table = total <= WOWN;
     W.exc[wv][L] = incl - rounds;
     if (table)  // each initiator lists its own tests (a few, mostly)

@@ -555,7 +555,8 @@ def gather_complex(owned: Tensor, first: int, gedges: Tensor, dst: int = 0, grou
 
 
 def subpoly_sharded(net, size: float = 1.2, group=None, allreduce=None, stats: list = None,
-                    halo: int = None, force: bool = True, eps: float = 1e-4, blocks: bool = False):
+                    halo: int = None, force: bool = True, eps: float = 1e-4, blocks: bool = False,
+                    info: dict = None):
     """The hot loop of subpoly() (subpoly.py:45-69) sharded over the ranks of
     `group` (one GPU each): the skeleton (tropical.py:158-225, computed whole
     on every rank -- a few lattice passes), x-slabs of equal skeleton-edge
@@ -568,7 +569,10 @@ def subpoly_sharded(net, size: float = 1.2, group=None, allreduce=None, stats: l
     the curve branch, its in-step decisions through the same allreduce.
     eps: subpoly's eps argument (None: Net.eps), as in subpoly().
     blocks=True: the most cubic block split instead of x-slabs, each axis
-    cut at equal marginal skeleton-edge load; `cuts` is then the Blocks."""
+    cut at equal marginal skeleton-edge load; `cuts` is then the Blocks.
+    info (a dict): filled with the accepted halo, the extractions the halo
+    search ran (halo_attempts: 1 unless a width was rejected) and their
+    wall time (halo_ms)."""
     from ._engine import engine_for
     from .subpoly import _eps
     rank, world = dist.get_rank(group), dist.get_world_size(group)
@@ -601,6 +605,8 @@ def subpoly_sharded(net, size: float = 1.2, group=None, allreduce=None, stats: l
         part = Blocks.xslabs(axis_cuts(0, world))
     cuts = part.cuts[0] if not blocks else part
     widths = HALOS if halo is None else (halo,)
+    import time
+    t0 = time.perf_counter()
     for k, h in enumerate(widths):
         lo, hi = part.box(rank, h)
         vs, es = box_restrict(v, e, marks, lo, hi, net.eps)
@@ -614,6 +620,8 @@ def subpoly_sharded(net, size: float = 1.2, group=None, allreduce=None, stats: l
         Vl, El = Vl.to(cd), El.to(cd)
         if halo_check(Vl, El, marks, cuts, net.eps, group, raise_=k == len(widths) - 1) is not None:
             break
+    if info is not None:
+        info.update(halo=h, halo_attempts=k + 1, halo_ms=(time.perf_counter() - t0) * 1e3)
     if stats is not None:
         stats.extend(st)
     owned, first, gE = stitch(Vl, El, marks, cuts, net.eps, group)
