@@ -140,6 +140,25 @@ int tnp_engine_skeleton(tnp_engine* eng, int unit, float size, void* stream,
 enum { TNP_SKELETON_DISTANCE = 0, TNP_SKELETON_SIGN = 1 };
 int tnp_engine_skeleton_mode(tnp_engine* eng, int unit, float size, int mode, void* stream,
                              int64_t* n_vertices, int64_t* n_edges);
+/* The distance-mode skeleton split over the ranks of a sharded extraction
+ * (no reference counterpart: the reference runs one device).
+ * skeleton_gmax: the tiles t of the reference's tile grid (tropical.py:
+ * 176-181) with t % world == rank are evaluated whole; h_gmax[t] = the bits
+ * of their max |grad sdf| (0 for the other tiles; the ranks' MAX is every
+ * tile's), h_load[3][n_marks] (may be null) += per axis and mark plane the
+ * points under the tile's edge threshold (the cuts' load balance; SUM over
+ * the ranks).  *n_tiles = the tile count (<= cap).
+ * skeleton_box: loads the part of the skeleton inside the mark box
+ * [lo[d], hi[d]] -- exactly the whole skeleton with the vertices outside
+ * the box and the edges leaving it dropped, order kept -- evaluating only
+ * tile & box, with every tile's max |grad sdf| from h_gmax[n_tiles].  A box
+ * the skeleton misses holds an empty complex (the whole skeleton's
+ * emptiness, the hypercube fallback, is the caller's test). */
+int tnp_engine_skeleton_gmax(tnp_engine* eng, int unit, int rank, int world, uint32_t* h_gmax,
+                             int64_t* h_load, int cap, int* n_tiles, void* stream);
+int tnp_engine_skeleton_box(tnp_engine* eng, int unit, const int32_t* lo, const int32_t* hi,
+                            const uint32_t* h_gmax, int n_tiles, void* stream, int64_t* n_vertices,
+                            int64_t* n_edges);
 
 /* Load the full lattice over the marks restricted to the x-slab of mark
  * indices [x0, x1] (x0=0, x1=n_marks-1: the whole N^3 lattice) in the

@@ -412,3 +412,35 @@ def test_engine_footprint_is_steady_across_passes(cuda, G):
     assert all(f == foot[1] for f in foot[1:]), [f["bytes"] for f in foot]
     assert len(set(got)) == 1
     assert foot[0]["key_bytes"] > 0 and foot[0]["buffers"] > 10
+
+
+@pytest.mark.parametrize("name", ["large_sphere", "small_sphere"])
+def test_skeleton_box_is_the_restricted_skeleton(cuda, name):
+    """The sharded skeleton (tnp_engine_skeleton_gmax / _box): the tiles' max
+    |grad sdf| computed on 3 'ranks' (every third tile each) and MAX-reduced
+    equal the one-rank values, and the skeleton built on a box -- tile & box
+    only, with those maxima -- is exactly box_restrict of the whole skeleton
+    (vertices bitwise, edges in order, tile-overlap duplicates included), on
+    boxes that cut the tiles and one that misses the surface."""
+    from tropical.distributed import box_restrict
+    from tropical._engine import engine_for
+    d = load(name)
+    net = product_net(d, cuda)
+    eng = engine_for(net)
+    g1, l1 = eng.skeleton_gmax(128, 0, 1)
+    parts = [eng.skeleton_gmax(128, r, 3) for r in range(3)]
+    gm = np.maximum.reduce([g for g, _ in parts])
+    assert np.array_equal(gm, g1) and (g1 > 0).all()
+    assert np.array_equal(sum(ld for _, ld in parts), l1) and l1.sum() > 0
+    eng.skeleton(128, 1.2)
+    v, e, _ = eng.export()
+    marks = net.enc.marks
+    L = int(marks.shape[0])
+    boxes = [([0, 0, 0], [L - 1, L - 1, L - 1]), ([L // 3, 2, L // 2 - 3], [L - 4, L // 2 + 7, L - 1]),
+             ([L // 2 - 3, L // 2 - 3, L // 2 - 3], [L // 2 + 3, L // 2 + 3, L // 2 + 3]), ([0, 0, 0], [2, 2, 2])]
+    for lo, hi in boxes:
+        vw, ew = box_restrict(v, e, marks, lo, hi, net.eps)
+        V, E = eng.skeleton_box(lo, hi, g1)
+        vb, eb, _ = eng.export()
+        assert (V, E) == (vw.shape[0], ew.shape[0]), (lo, hi)
+        assert torch.equal(vb, vw) and torch.equal(eb, ew), (lo, hi)

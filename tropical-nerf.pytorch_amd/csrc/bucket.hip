@@ -1108,6 +1108,9 @@ __device__ __forceinline__ int build_windows_par(int* cnt, const int* cur, uint1
 // chunk's end) are gathered into LDS (over the window stage and behind it)
 // and the windows starting in the chunk are tested there.  Only the cells
 // above WCELL members (k_connect's) get records in memory.
+#ifndef TNP_BG_WAVEWIN  // 1: per-wave windows (no workgroup barriers in the pass); 0: shared chunks
+#define TNP_BG_WAVEWIN 1
+#endif
 #ifndef TNP_LREC_CH
 #define TNP_LREC_CH 192  // (256 records: the window stage's own LDS, occupancy unchanged)
 #endif
@@ -1196,7 +1199,84 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
         }
         __syncthreads();
         BG_PH(5);
-        if (in_lds) {
+        if (in_lds && SW && TNP_BG_WAVEWIN) {
+          // each wave walks its own windows (kw, kw + TNP_WAVES, ...) through a
+          // private 64-record stage in LDS, no workgroup barrier: a window's
+          // records are built from the bucket's entry words in cell order and
+          // the member keys, software-pipelined (the keys of the next window
+          // and the words of the one after are in flight while a window is
+          // tested), so a wave never waits on the slowest window of a shared
+          // chunk (round 4's chunk pipeline)
+          const uint64_t* sw = static_cast<const uint64_t*>(order);
+          const int L = tnp::lane(), wv = tnp::wave(), nw = nwin_s;
+          const uint32_t* wl = reinterpret_cast<const uint32_t*>(cnt);
+          auto span = [&](int k, int& s, int& m) {
+            if (k >= nw) { s = 0; m = 0; return; }
+            const uint32_t se = (uint32_t)uniform((int)wl[k]);
+            s = (int)(se & 0xFFFFu);
+            m = (int)(se >> 16) - s;
+          };
+          int s0, m0, s1, m1;
+          span(wv, s0, m0);
+          span(wv + TNP_WAVES, s1, m1);
+          uint64_t w0 = L < m0 ? sw[s0 + L] : 0ull;
+          uint64_t w1 = L < m1 ? sw[s1 + L] : 0ull;
+          ulonglong2 k0 = L < m0 ? pz[(uint32_t)w0] : make_ulonglong2(0ull, 0ull);
+          // this wave's packed stage (64 records), laid over its W.st slots
+          uint64_t* const ptw = reinterpret_cast<uint64_t*>(&W.st[wv][0]);
+          uint64_t* const paw = ptw + 64;
+          uint32_t* const pvv = reinterpret_cast<uint32_t*>(paw + 64);
+          uint16_t* const ptg = reinterpret_cast<uint16_t*>(pvv + 64);
+          static_assert(64 * (8 + 8 + 4 + 2) <= sizeof(W.st[0]), "a wave's packed stage fits its record slots");
+          const PackedRecs PR{ptw, paw, pvv, ptg};
+          uint64_t amask = 0;
+          if (PK && wa.fmask) {
+            const uint64_t lo = (uint32_t)(wa.fmask >> wa.idx);
+            amask = lo | (lo << 32);
+          }
+          for (int k = wv; k < nw; k += TNP_WAVES) {
+            // in flight behind this window: the keys of the next, the words of the one after
+            int s2, m2;
+            span(k + 2 * TNP_WAVES, s2, m2);
+            const ulonglong2 k1 = L < m1 ? pz[(uint32_t)w1] : make_ulonglong2(0ull, 0ull);
+            const uint64_t w2 = L < m2 ? sw[s2 + L] : 0ull;
+            const bool valid = L < m0;
+            uint32_t tag;
+            if constexpr (PK) {
+              if (valid) {
+                ptw[L] = packed_test_word(k0.x, k0.y, (uint32_t)(w0 >> 32) & 63u, below);
+                paw[L] = packed_above_word(k0.x, k0.y, wa.idx);
+                pvv[L] = (uint32_t)w0;
+              }
+              tag = valid ? (uint32_t)(w0 >> 40) : 0xFFFFFFFFu;
+            } else {
+              CellEnt e;
+              e.p = k0.x;
+              e.z = k0.y;
+              e.v = (int32_t)(uint32_t)w0;
+              e.f = (uint32_t)(w0 >> 32) & 63u;
+              e.tag = valid ? (uint32_t)b * (uint32_t)LC + (uint32_t)(w0 >> 40) : 0xFFFFFFFFu;
+              e.pad = 0;
+              if (valid) W.st[wv][L] = e;
+              tag = e.tag;
+            }
+            lds_fence();
+            // last lane of my cell in the window (the window holds whole cells)
+            const uint32_t nxt = __shfl_down(tag, 1, 64);
+            const uint64_t bm = __ballot(L >= m0 - 1 || nxt != tag);
+            const int last = L + __builtin_ctzll(bm >> L);
+            const int rounds = valid ? last - L : 0;
+            if constexpr (PK)
+              window_tests_packed(PR, 0, rounds, (uint32_t)below, wa.nb, amask, wa.keys, wa.cap, wa.xs, ctr, W, a);
+            else
+              window_tests(W.st[wv], rounds, below, wa.nb, wa.fmask, wa.keys, wa.cap, wa.xs, ctr, W, a);
+            w0 = w1;
+            k0 = k1;
+            m0 = m1;
+            w1 = w2;
+            m1 = m2;
+          }
+        } else if (in_lds) {
           // chunks of TNP_LREC_CH record positions gathered into LDS, then the
           // windows that start there tested.  Software-pipelined: SW (the
           // bucket's entry words written in cell order by the grouping): the

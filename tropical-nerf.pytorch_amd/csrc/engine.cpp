@@ -1986,20 +1986,50 @@ extern "C" int tnp_engine_skeleton(tnp_engine* e, int unit, float size, void* st
   return tnp_engine_skeleton_mode(e, unit, size, TNP_SKELETON_DISTANCE, stream, V_out, E_out);
 }
 
-extern "C" int tnp_engine_skeleton_mode(tnp_engine* e, int unit, float size, int mode, void* stream,
-                                        int64_t* V_out, int64_t* E_out) {
-  hipStream_t s = (hipStream_t)stream;
+// torch.diff(marks).max().item() (the skeleton's edge-length bound)
+static int marks_dmax(tnp_engine* e, hipStream_t s, float* dmax) {
+  const int L = e->net.n_marks;
+  std::vector<float> mk(L);
+  TNP_CHECK(hipMemcpyAsync(mk.data(), e->net.marks, L * sizeof(float), hipMemcpyDeviceToHost, s));
+  TNP_CHECK(hipStreamSynchronize(s));
+  float d = -INFINITY;
+  for (int i = 0; i + 1 < L; ++i) d = std::max(d, mk[i + 1] - mk[i]);
+  *dmax = d;
+  return 0;
+}
+
+// the reference's skeleton tiles (tropical.py:176-181): starts range(0, L,
+// unit - 1) per axis, unit marks each (1-mark overlap), x-major order
+struct SkelTile {
+  int o[3], n[3];
+};
+static std::vector<SkelTile> skeleton_tiles(int L, int unit) {
+  std::vector<SkelTile> t;
+  for (int i0 = 0; i0 < L; i0 += unit - 1)
+    for (int j0 = 0; j0 < L; j0 += unit - 1)
+      for (int k0 = 0; k0 < L; k0 += unit - 1)
+        t.push_back(SkelTile{{i0, j0, k0},
+                             {std::min(L, i0 + unit) - i0, std::min(L, j0 + unit) - j0, std::min(L, k0 + unit) - k0}});
+  return t;
+}
+
+// TropicalHashGrid.skeleton on the device.  box_lo / box_hi (distance mode
+// only): the part of the skeleton inside the mark box [lo, hi] -- every tile
+// meeting the box evaluated on tile & box only, with its max |grad sdf| from
+// tile_gmax (device, one word per tile: the whole tile's, tnp_engine_
+// skeleton_gmax); the edges (both endpoints in the box) come out in the
+// whole skeleton's order, so the result is box_restrict of the whole one.
+static int skeleton_build(tnp_engine* e, int unit, float size, int mode, const int32_t* box_lo,
+                          const int32_t* box_hi, const unsigned int* tile_gmax, hipStream_t s, int64_t* V_out,
+                          int64_t* E_out) {
   if (!e->has_net) { tnp_set_error("engine has no net"); return -1; }
   if (unit < 2) { tnp_set_error("unit must be >= 2"); return -1; }
   TNP_CHECK(hipSetDevice(e->device));
   span_all(e);  // the whole grid
   const int L = e->net.n_marks;
   if ((int64_t)L * L * L >= (1LL << 31)) { tnp_set_error("too many marks for int32 ids"); return -1; }
-  std::vector<float> mk(L);
-  TNP_CHECK(hipMemcpyAsync(mk.data(), e->net.marks, L * sizeof(float), hipMemcpyDeviceToHost, s));
-  TNP_CHECK(hipStreamSynchronize(s));
-  float dmax = -INFINITY;  // torch.diff(marks).max().item()
-  for (int i = 0; i + 1 < L; ++i) dmax = std::max(dmax, mk[i + 1] - mk[i]);
+  float dmax;
+  if (marks_dmax(e, s, &dmax)) return -1;
   if (buf_ensure(e->ctr, CTR_CLEAR_BYTES, s)) return -1;
   const int64_t LLL = (int64_t)L * L * L;
   if (buf_ensure(e->used, LLL * sizeof(int32_t), s)) return -1;
@@ -2011,6 +2041,11 @@ extern "C" int tnp_engine_skeleton_mode(tnp_engine* e, int unit, float size, int
     return -1;
   }
   const bool sign = mode == TNP_SKELETON_SIGN;
+  const bool box = box_lo != nullptr;
+  if (box && (sign || !tile_gmax)) {
+    tnp_set_error("skeleton box: distance mode with the tiles' max |grad sdf| only");
+    return -1;
+  }
   int64_t tile_pts = (int64_t)std::min(unit, L) * std::min(unit, L) * std::min(unit, L);
   if (buf_ensure(e->stage, tile_pts * sizeof(float) * (sign ? e->K : 1), s)) return -1;
   // sign mode: the tile's points, their forward and packed keys (pos, zero,
@@ -2023,60 +2058,76 @@ extern "C" int tnp_engine_skeleton_mode(tnp_engine* e, int unit, float size, int
   }
   if (buf_ensure(e->shared, 16, s)) return -1;
   unsigned int* gmax = P<unsigned int>(e->shared);
+  const std::vector<SkelTile> tiles = skeleton_tiles(L, unit);
   int64_t total = 0;
-  for (int i0 = 0; i0 < L; i0 += unit - 1)
-    for (int j0 = 0; j0 < L; j0 += unit - 1)
-      for (int k0 = 0; k0 < L; k0 += unit - 1) {
-        int n0 = std::min(L, i0 + unit) - i0, n1 = std::min(L, j0 + unit) - j0,
-            n2 = std::min(L, k0 + unit) - k0;
-        const uint64_t* keys = nullptr;
-        if (sign) {
-          // Net.region on the tile's vertices (tropical.py:199-201): the
-          // forward of every point with its eps-sign keys
-          const int64_t np_ = (int64_t)n0 * n1 * n2;
-          if (launch_skel_points(i0, j0, k0, n0, n1, n2, e->net.marks, P<float>(sk[CV_CORNERS]), s)) return -1;
-          if (launch_forward(e->net, P<float>(sk[CV_CORNERS]), np_, P<float>(e->stage), np_, 1, s, nullptr,
-                             P<uint64_t>(sk[CV_D0]), P<uint64_t>(sk[CV_D1]), P<uint64_t>(sk[CV_GG]),
-                             P<uint64_t>(sk[CV_STAGE_C])))
-            return -1;
-          keys = P<uint64_t>(sk[CV_STAGE_C]);
-        } else {
-          TNP_CHECK(hipMemsetAsync(gmax, 0, sizeof(unsigned int), s));
-          if (launch_skel_eval(e->net, i0, j0, k0, n0, n1, n2, P<float>(e->stage), gmax, s)) return -1;
-        }
-        int64_t N = skel_candidates(n0, n1, n2);
-        int64_t nt = skel_tiles(N);
-        if (buf_ensure(e->blk, (nt + 1) * sizeof(int32_t), s)) return -1;
-        if (buf_ensure(e->blkoff, (nt + 1) * sizeof(int64_t), s)) return -1;
-        if (launch_skel_edges(false, i0, j0, k0, n0, n1, n2, L, P<float>(e->stage), keys, dmax, gmax,
-                              P<int32_t>(e->blk), nullptr, 0, nullptr, nullptr, s))
-          return -1;
-        if (scan_counts(e, P<int32_t>(e->blk), P<int64_t>(e->blkoff), nt, CTR_AUX, s)) return -1;
-        if (read_ctr(e, s)) return -1;
-        int64_t cnt = e->h_ctr[CTR_AUX];
-        if (cnt > 0) {
-          if (buf_ensure(e->edges_alt, (total + cnt) * 2 * sizeof(int32_t), s, true)) return -1;
-          if (launch_skel_edges(true, i0, j0, k0, n0, n1, n2, L, P<float>(e->stage), keys, dmax, gmax,
-                                nullptr, P<int64_t>(e->blkoff), total, P<int32_t>(e->edges_alt),
-                                P<int32_t>(e->used), s))
-            return -1;
-        }
-        total += cnt;
+  for (size_t t = 0; t < tiles.size(); ++t) {
+    int o[3], n[3];
+    bool empty = false;
+    for (int d = 0; d < 3; ++d) {
+      o[d] = tiles[t].o[d];
+      n[d] = tiles[t].n[d];
+      if (box) {  // tile & box
+        const int a = std::max(o[d], box_lo[d]), b = std::min(o[d] + n[d] - 1, box_hi[d]);
+        empty |= b < a;
+        o[d] = a;
+        n[d] = b - a + 1;
       }
+    }
+    if (empty) continue;
+    const int i0 = o[0], j0 = o[1], k0 = o[2], n0 = n[0], n1 = n[1], n2 = n[2];
+    const uint64_t* keys = nullptr;
+    const unsigned int* gm = box ? tile_gmax + t : gmax;
+    if (sign) {
+      // Net.region on the tile's vertices (tropical.py:199-201): the
+      // forward of every point with its eps-sign keys
+      const int64_t np_ = (int64_t)n0 * n1 * n2;
+      if (launch_skel_points(i0, j0, k0, n0, n1, n2, e->net.marks, P<float>(sk[CV_CORNERS]), s)) return -1;
+      if (launch_forward(e->net, P<float>(sk[CV_CORNERS]), np_, P<float>(e->stage), np_, 1, s, nullptr,
+                         P<uint64_t>(sk[CV_D0]), P<uint64_t>(sk[CV_D1]), P<uint64_t>(sk[CV_GG]),
+                         P<uint64_t>(sk[CV_STAGE_C])))
+        return -1;
+      keys = P<uint64_t>(sk[CV_STAGE_C]);
+    } else {
+      // (box: the sub-tile's |sdf|; its own gradient maximum is not used)
+      TNP_CHECK(hipMemsetAsync(gmax, 0, sizeof(unsigned int), s));
+      if (launch_skel_eval(e->net, i0, j0, k0, n0, n1, n2, P<float>(e->stage), gmax, s)) return -1;
+    }
+    int64_t N = skel_candidates(n0, n1, n2);
+    int64_t nt = skel_tiles(N);
+    if (nt == 0) continue;
+    if (buf_ensure(e->blk, (nt + 1) * sizeof(int32_t), s)) return -1;
+    if (buf_ensure(e->blkoff, (nt + 1) * sizeof(int64_t), s)) return -1;
+    if (launch_skel_edges(false, i0, j0, k0, n0, n1, n2, L, P<float>(e->stage), keys, dmax, gm,
+                          P<int32_t>(e->blk), nullptr, 0, nullptr, nullptr, s))
+      return -1;
+    if (scan_counts(e, P<int32_t>(e->blk), P<int64_t>(e->blkoff), nt, CTR_AUX, s)) return -1;
+    if (read_ctr(e, s)) return -1;
+    int64_t cnt = e->h_ctr[CTR_AUX];
+    if (cnt > 0) {
+      if (buf_ensure(e->edges_alt, (total + cnt) * 2 * sizeof(int32_t), s, true)) return -1;
+      if (launch_skel_edges(true, i0, j0, k0, n0, n1, n2, L, P<float>(e->stage), keys, dmax, gm,
+                            nullptr, P<int64_t>(e->blkoff), total, P<int32_t>(e->edges_alt),
+                            P<int32_t>(e->used), s))
+        return -1;
+    }
+    total += cnt;
+  }
   e->pend_idx = -1;
   e->valid_from = 0;
-  if (total == 0) {
+  if (total == 0 && !box) {
     if (load_hypercube(e, size, s)) return -1;
   } else {
+    // (box: a box without skeleton edges holds an empty complex -- the whole
+    // skeleton's emptiness, the hypercube fallback, is the caller's check)
     if (scan_counts(e, P<int32_t>(e->used), P<int64_t>(e->nid), LLL, CTR_V, s)) return -1;
     if (read_ctr(e, s)) return -1;
     int64_t V = e->h_ctr[CTR_V];
-    if (vset_ensure(e, e->cur, V, 0, s)) return -1;
+    if (vset_ensure(e, e->cur, std::max<int64_t>(V, 1), 0, s)) return -1;
     if (launch_skel_vertices(P<int32_t>(e->used), P<int64_t>(e->nid), LLL, L, e->net.marks,
                              P<float>(e->cur.xyz), s))
       return -1;
     if (launch_remap_i32(P<int32_t>(e->edges_alt), 2 * total, P<int64_t>(e->nid), s)) return -1;
-    std::swap(e->edges, e->edges_alt);
+    if (total > 0) std::swap(e->edges, e->edges_alt);
     e->V = V;
     e->E = total;
     e->E_live = total;
@@ -2089,6 +2140,73 @@ extern "C" int tnp_engine_skeleton_mode(tnp_engine* e, int unit, float size, int
   *V_out = e->V;
   *E_out = e->E;
   return reset_live(e, s);
+}
+
+extern "C" int tnp_engine_skeleton_mode(tnp_engine* e, int unit, float size, int mode, void* stream,
+                                        int64_t* V_out, int64_t* E_out) {
+  return skeleton_build(e, unit, size, mode, nullptr, nullptr, nullptr, (hipStream_t)stream, V_out, E_out);
+}
+
+extern "C" int tnp_engine_skeleton_gmax(tnp_engine* e, int unit, int rank, int world, uint32_t* h_gmax,
+                                        int64_t* h_load, int cap, int* n_tiles, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (!e->has_net) { tnp_set_error("engine has no net"); return -1; }
+  if (unit < 2 || world < 1 || rank < 0 || rank >= world) {
+    tnp_set_error("skeleton_gmax: unit %d, rank %d of %d", unit, rank, world);
+    return -1;
+  }
+  TNP_CHECK(hipSetDevice(e->device));
+  const int L = e->net.n_marks;
+  const std::vector<SkelTile> tiles = skeleton_tiles(L, unit);
+  *n_tiles = (int)tiles.size();
+  if ((int)tiles.size() > cap) {
+    tnp_set_error("skeleton_gmax: %d tiles, room for %d", (int)tiles.size(), cap);
+    return -1;
+  }
+  float dmax;
+  if (marks_dmax(e, s, &dmax)) return -1;
+  const int64_t T = (int64_t)tiles.size();
+  int64_t tile_pts = (int64_t)std::min(unit, L) * std::min(unit, L) * std::min(unit, L);
+  if (buf_ensure(e->stage, tile_pts * sizeof(float), s)) return -1;
+  // [T] gmax words, then [3][L] int64 load counts
+  const size_t gbytes = (size_t)((T + 1) / 2 * 2) * sizeof(uint32_t);
+  if (buf_ensure(e->fscr[0], gbytes + 3 * (size_t)L * sizeof(int64_t), s)) return -1;
+  unsigned int* gm = P<unsigned int>(e->fscr[0]);
+  int64_t* load = reinterpret_cast<int64_t*>(static_cast<char*>(e->fscr[0].p) + gbytes);
+  TNP_CHECK(hipMemsetAsync(e->fscr[0].p, 0, gbytes + 3 * (size_t)L * sizeof(int64_t), s));
+  for (int64_t t = rank; t < T; t += world) {
+    const SkelTile& q = tiles[t];
+    if (launch_skel_eval(e->net, q.o[0], q.o[1], q.o[2], q.n[0], q.n[1], q.n[2], P<float>(e->stage), gm + t, s))
+      return -1;
+    if (launch_skel_load(q.o[0], q.o[1], q.o[2], q.n[0], q.n[1], q.n[2], L, P<float>(e->stage), dmax, gm + t,
+                         load, s))
+      return -1;
+  }
+  TNP_CHECK(hipMemcpyAsync(h_gmax, gm, T * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  if (h_load) TNP_CHECK(hipMemcpyAsync(h_load, load, 3 * (size_t)L * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  TNP_CHECK(hipStreamSynchronize(s));
+  return 0;
+}
+
+extern "C" int tnp_engine_skeleton_box(tnp_engine* e, int unit, const int32_t* lo, const int32_t* hi,
+                                       const uint32_t* h_gmax, int n_tiles, void* stream, int64_t* V_out,
+                                       int64_t* E_out) {
+  hipStream_t s = (hipStream_t)stream;
+  if (!e->has_net) { tnp_set_error("engine has no net"); return -1; }
+  TNP_CHECK(hipSetDevice(e->device));
+  const int L = e->net.n_marks;
+  if ((int)skeleton_tiles(L, unit).size() != n_tiles) {
+    tnp_set_error("skeleton_box: %d tile maxima for %d tiles", n_tiles, (int)skeleton_tiles(L, unit).size());
+    return -1;
+  }
+  for (int d = 0; d < 3; ++d)
+    if (lo[d] < 0 || hi[d] >= L || lo[d] > hi[d]) {
+      tnp_set_error("skeleton_box: axis %d box [%d, %d] outside the %d marks", d, lo[d], hi[d], L);
+      return -1;
+    }
+  if (buf_ensure(e->fscr[1], (size_t)std::max(n_tiles, 1) * sizeof(uint32_t), s)) return -1;
+  TNP_CHECK(hipMemcpyAsync(e->fscr[1].p, h_gmax, n_tiles * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+  return skeleton_build(e, unit, 0.f, TNP_SKELETON_DISTANCE, lo, hi, P<unsigned int>(e->fscr[1]), s, V_out, E_out);
 }
 
 // ---------------------------------------------------------------------------

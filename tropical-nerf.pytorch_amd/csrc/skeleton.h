@@ -17,6 +17,10 @@ int launch_skel_edges(bool emit, int i0, int j0, int k0, int n0, int n1, int n2,
                       const float* dist, const uint64_t* keys, float dmax, const unsigned int* gmax_bits,
                       int32_t* blk, const int64_t* blkoff, int64_t out_base, int32_t* out, int32_t* used,
                       hipStream_t s);
+// per-axis, per-mark-plane counts of the tile's points under its edge
+// threshold (the sharded skeleton's load balance), added into load[3][L]
+int launch_skel_load(int i0, int j0, int k0, int n0, int n1, int n2, int L, const float* dist, float dmax,
+                     const unsigned int* gmax_bits, int64_t* load, hipStream_t s);
 int launch_skel_vertices(const int32_t* used, const int64_t* nid, int64_t n, int L,
                          const float* marks, float* xyz, hipStream_t s);
 int launch_remap_i32(int32_t* e, int64_t n, const int64_t* nid, hipStream_t s);

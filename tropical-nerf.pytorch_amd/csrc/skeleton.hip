@@ -14,6 +14,8 @@
 // then squeeze: used global ids p2v(i,j,k) -> dense ranks (sorted unique),
 // vertices = marks[v2p(id)]*2-1 with the reference's float32 v2p division.
 // Duplicate edges on tile overlaps are kept, as in the reference.
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 #include "net_device.h"
@@ -126,6 +128,30 @@ k_skel_emit(TileGeom g, const float* __restrict__ dist, const ulonglong2* __rest
   }
 }
 
+// the skeleton's load per mark plane (sharded subpoly: the cuts' balance):
+// per axis d, load[d * L + m] += the tile's points on plane m of axis d with
+// |sdf| under the tile's edge threshold (the candidates of its edges)
+__global__ void __launch_bounds__(TNP_BLOCK)
+k_skel_load(TileGeom g, const float* __restrict__ dist, float dmax, const unsigned int* __restrict__ gmax_bits,
+            unsigned long long* __restrict__ load) {
+  extern __shared__ unsigned int hist[];  // [3][L]
+  const int L = g.L;
+  for (int i = threadIdx.x; i < 3 * L; i += blockDim.x) hist[i] = 0;
+  __syncthreads();
+  const float thr = skel_threshold(dmax, gmax_bits);
+  const int64_t n = (int64_t)g.n0 * g.n1 * g.n2;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x) {
+    if (!(dist[t] <= thr)) continue;
+    const int k = (int)(t % g.n2), j = (int)((t / g.n2) % g.n1), i = (int)(t / ((int64_t)g.n1 * g.n2));
+    atomicAdd(&hist[g.i0 + i], 1u);
+    atomicAdd(&hist[L + g.j0 + j], 1u);
+    atomicAdd(&hist[2 * L + g.k0 + k], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 3 * L; i += blockDim.x)
+    if (hist[i]) atomicAdd(&load[i], (unsigned long long)hist[i]);
+}
+
 __global__ void k_skel_vertices(const int32_t* __restrict__ used, const int64_t* __restrict__ nid,
                                 int64_t n, int L, const float* __restrict__ marks,
                                 float* __restrict__ xyz) {
@@ -199,6 +225,19 @@ int launch_skel_edges(bool emit, int i0, int j0, int k0, int n0, int n1, int n2,
   else
     hipLaunchKernelGGL(k_skel_count, dim3((unsigned)skel_tiles(N)), dim3(TNP_BLOCK), 0, s, g, dist, k2,
                        dmax, gmax_bits, blk);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int launch_skel_load(int i0, int j0, int k0, int n0, int n1, int n2, int L, const float* dist, float dmax,
+                     const unsigned int* gmax_bits, int64_t* load, hipStream_t s) {
+  const int64_t n = (int64_t)n0 * n1 * n2;
+  if (n <= 0) return 0;
+  if (L > 4096) { tnp_set_error("skeleton load: more than 4096 marks"); return -1; }
+  TileGeom g = geom(i0, j0, k0, n0, n1, n2, L);
+  const unsigned grid = (unsigned)std::min<int64_t>((n + TNP_BLOCK * 16 - 1) / (TNP_BLOCK * 16), 1024);
+  hipLaunchKernelGGL(k_skel_load, dim3(grid), dim3(TNP_BLOCK), 3 * L * sizeof(unsigned int), s, g, dist, dmax,
+                     gmax_bits, reinterpret_cast<unsigned long long*>(load));
   TNP_CHECK(hipGetLastError());
   return 0;
 }

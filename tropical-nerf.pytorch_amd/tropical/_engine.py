@@ -118,6 +118,30 @@ class Engine:
                    "tnp_engine_skeleton_mode")
         return V.value, E.value
 
+    def skeleton_gmax(self, unit: int = 128, rank: int = 0, world: int = 1):
+        """The tiles t % world == rank of the distance-mode skeleton evaluated
+        whole (tnp_engine_skeleton_gmax): (uint32 max |grad sdf| bits per tile,
+        0 for the others; int64 [3, n_marks] per-plane load of those tiles)."""
+        n_marks = int(self._keep[0].n_marks)
+        cap = 4096
+        gmax = np.zeros(cap, dtype=np.uint32)
+        load = np.zeros((3, n_marks), dtype=np.int64)
+        nt = C.c_int()
+        _hip.check(_hip.lib().tnp_engine_skeleton_gmax(self.h, unit, rank, world, gmax.ctypes.data,
+                                                       load.ctypes.data, cap, C.byref(nt), self._s),
+                   "tnp_engine_skeleton_gmax")
+        return gmax[: nt.value].copy(), load
+
+    def skeleton_box(self, lo, hi, gmax, unit: int = 128):
+        """The skeleton inside the mark box [lo, hi] (tnp_engine_skeleton_box),
+        every tile's max |grad sdf| bits in gmax: (V, E) loaded."""
+        g = np.ascontiguousarray(np.asarray(gmax, dtype=np.uint32))
+        V, E = C.c_int64(), C.c_int64()
+        _hip.check(_hip.lib().tnp_engine_skeleton_box(self.h, unit, self._i3(lo), self._i3(hi), g.ctypes.data,
+                                                      int(g.shape[0]), self._s, C.byref(V), C.byref(E)),
+                   "tnp_engine_skeleton_box")
+        return V.value, E.value
+
     def sizes(self):
         V, E = C.c_int64(), C.c_int64()
         _hip.check(_hip.lib().tnp_engine_sizes(self.h, C.byref(V), C.byref(E)), "tnp_engine_sizes")

@@ -67,6 +67,9 @@ SIGNATURES = {
     "tnp_engine_destroy": (None, [_VP]),
     "tnp_engine_set_net": (C.c_int, [_VP, _NETP]),
     "tnp_engine_scratch_bytes": (C.c_int, [_VP, _P64, _P64, _P64]),
+    "tnp_engine_skeleton_gmax": (C.c_int, [_VP, C.c_int, C.c_int, C.c_int, _VP, _VP, C.c_int,
+                                           C.POINTER(C.c_int), _VP]),
+    "tnp_engine_skeleton_box": (C.c_int, [_VP, C.c_int, _P32, _P32, _VP, C.c_int, _VP, _P64, _P64]),
     "tnp_engine_load": (C.c_int, [_VP, _VP, _I64, _VP, _I64, _VP, C.c_int, _VP]),
     "tnp_engine_skeleton": (C.c_int, [_VP, C.c_int, _F, _VP, _P64, _P64]),
     "tnp_shm_open": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int, C.POINTER(_VP)]),

@@ -46,10 +46,12 @@ start at its outer halo boundary; to reach anything a rank keeps they must
 cross those two cells, where the neighbour -- for which they are interior --
 computed them from a different boundary.
 
-Stanford nets (BASELINE config 4): every rank computes the reference's
-skeleton on its 128-mark tiles (tropical.py:176-181, per-tile max_grad),
-cuts the x axis into slabs of equal skeleton-edge count (balanced_cuts) and
-keeps its slab plus halo (slab_restrict) -- subpoly_sharded().
+Stanford nets (BASELINE config 4): the reference's skeleton on its
+128-mark tiles (tropical.py:176-181, per-tile max_grad) is split over the
+ranks -- each evaluates every world-th tile whole for its max |grad sdf| and
+per-plane load, the ranks agree on both, cut the grid at equal load
+(balanced_cuts) and each builds only the part of the skeleton inside its
+block plus halo (tnp_engine_skeleton_box) -- subpoly_sharded().
 """
 from __future__ import annotations
 
@@ -556,23 +558,31 @@ def gather_complex(owned: Tensor, first: int, gedges: Tensor, dst: int = 0, grou
 
 def subpoly_sharded(net, size: float = 1.2, group=None, allreduce=None, stats: list = None,
                     halo: int = None, force: bool = True, eps: float = 1e-4, blocks: bool = False,
-                    info: dict = None):
+                    info: dict = None, box_skeleton: bool = True):
     """The hot loop of subpoly() (subpoly.py:45-69) sharded over the ranks of
-    `group` (one GPU each): the skeleton (tropical.py:158-225, computed whole
-    on every rank -- a few lattice passes), x-slabs of equal skeleton-edge
-    load, each rank's slab + halo through every hyperplane step with the
-    reference's global decisions made by `allreduce(vec, op)`, then
-    halo_check and stitch; while halo_check sees a difference, the slabs are
-    redone with the next width of HALOS (halo=None), or it raises (a fixed
+    `group` (one GPU each): the skeleton (tropical.py:158-225), x-slabs of
+    equal skeleton load, each rank's slab + halo through every hyperplane
+    step with the reference's global decisions made by `allreduce(vec, op)`,
+    then halo_check and stitch; while halo_check sees a difference, the slabs
+    are redone with the next width of HALOS (halo=None), or it raises (a fixed
     halo).  Returns (engine, owned vertices, first global id, global edges,
     cuts): the engine still holds this rank's slab complex.  force=False:
     the curve branch, its in-step decisions through the same allreduce.
     eps: subpoly's eps argument (None: Net.eps), as in subpoly().
     blocks=True: the most cubic block split instead of x-slabs, each axis
-    cut at equal marginal skeleton-edge load; `cuts` is then the Blocks.
+    cut at equal marginal load; `cuts` is then the Blocks.
+    box_skeleton (default): the skeleton is split over the ranks too -- each
+    rank evaluates every world-th reference tile whole (its max |grad sdf|
+    and its per-plane load), the ranks agree on the tiles' maxima (MAX) and
+    the loads (SUM), cut the grid at equal load, and each rank then builds
+    only the part of the skeleton inside its box (tnp_engine_skeleton_box:
+    tile & box, the whole skeleton restricted, order kept).  False: every
+    rank computes the whole skeleton and restricts it (box_restrict), cuts at
+    equal skeleton-edge load.
     info (a dict): filled with the accepted halo, the extractions the halo
     search ran (halo_attempts: 1 unless a width was rejected) and their
     wall time (halo_ms)."""
+    import time
     from ._engine import engine_for
     from .subpoly import _eps
     rank, world = dist.get_rank(group), dist.get_world_size(group)
@@ -580,22 +590,40 @@ def subpoly_sharded(net, size: float = 1.2, group=None, allreduce=None, stats: l
     eng.set_shards(world)
     eng.set_curve(not force)
     eng.set_eps(_eps(net, eps))
-    V0, E0 = eng.skeleton(unit=128, size=size)
-    v, e, _ = eng.export()
-    marks = net.enc.marks.to(v.device)
-    off, on = x_grid(v, marks, net.eps)
-    if not bool(on.all()):
-        raise NotImplementedError("subpoly_sharded: the skeleton fell back to get_hypercube "
-                                  "(subpoly.py:51-52); nothing to shard")
+    marks = net.enc.marks
     n_cells = marks.shape[0] - 1
 
-    def axis_cuts(d, parts):
-        # an edge's cell along d: the lower of its endpoints' planes (edges
-        # along d span one cell; the others lie in a plane, charged to the
-        # cell on its right)
-        o, _ = axis_grid(v, marks, net.eps, d)
-        ed = torch.minimum(o[e[:, 0]], o[e[:, 1]]).clamp(0, n_cells - 1)
-        return balanced_cuts(torch.bincount(ed, minlength=n_cells), parts)
+    def reduce(vec: np.ndarray, op: str) -> np.ndarray:
+        if allreduce is not None:
+            return np.asarray(allreduce(vec, op))
+        t = torch.from_numpy(np.ascontiguousarray(vec)).to(comm_device(group, marks.device))
+        dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM, group=group)
+        return t.cpu().numpy()
+
+    if box_skeleton:
+        gmax, load = eng.skeleton_gmax(128, rank, world)
+        gmax = reduce(gmax.astype(np.int64), "max").astype(np.uint32)
+        load = reduce(load.reshape(-1), "sum").reshape(3, -1)
+
+        def axis_cuts(d, parts):
+            # plane m's load charged to cell m (the cell on its right)
+            return balanced_cuts(torch.from_numpy(load[d][:n_cells].copy()), parts)
+    else:
+        V0, E0 = eng.skeleton(unit=128, size=size)
+        v, e, _ = eng.export()
+        mk = marks.to(v.device)
+        off, on = x_grid(v, mk, net.eps)
+        if not bool(on.all()):
+            raise NotImplementedError("subpoly_sharded: the skeleton fell back to get_hypercube "
+                                      "(subpoly.py:51-52); nothing to shard")
+
+        def axis_cuts(d, parts):
+            # an edge's cell along d: the lower of its endpoints' planes (edges
+            # along d span one cell; the others lie in a plane, charged to the
+            # cell on its right)
+            o, _ = axis_grid(v, mk, net.eps, d)
+            ed = torch.minimum(o[e[:, 0]], o[e[:, 1]]).clamp(0, n_cells - 1)
+            return balanced_cuts(torch.bincount(ed, minlength=n_cells), parts)
 
     if blocks:
         dims = block_dims(world)
@@ -605,12 +633,18 @@ def subpoly_sharded(net, size: float = 1.2, group=None, allreduce=None, stats: l
         part = Blocks.xslabs(axis_cuts(0, world))
     cuts = part.cuts[0] if not blocks else part
     widths = HALOS if halo is None else (halo,)
-    import time
     t0 = time.perf_counter()
     for k, h in enumerate(widths):
         lo, hi = part.box(rank, h)
-        vs, es = box_restrict(v, e, marks, lo, hi, net.eps)
-        eng.load(vs, es)
+        if box_skeleton:
+            Vb, Eb = eng.skeleton_box(lo, hi, gmax)
+            if k == 0 and int(reduce(np.array([Eb], dtype=np.int64), "sum")[0]) == 0:
+                # the boxes cover the grid: no edge in any is no skeleton at all
+                raise NotImplementedError("subpoly_sharded: the skeleton fell back to get_hypercube "
+                                          "(subpoly.py:51-52); nothing to shard")
+        else:
+            vs, es = box_restrict(v, e, mk, lo, hi, net.eps)
+            eng.load(vs, es)
         eng.set_span(lo, hi)
         eng.set_owned_box(*part.owned(rank))
         st = []
