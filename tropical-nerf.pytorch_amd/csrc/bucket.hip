@@ -1111,6 +1111,9 @@ __device__ __forceinline__ int build_windows_par(int* cnt, const int* cur, uint1
 #ifndef TNP_BG_WAVEWIN  // 1: per-wave windows (no workgroup barriers in the pass); 0: shared chunks
 #define TNP_BG_WAVEWIN 1
 #endif
+#ifndef TNP_BG_LDS_MIN  // buckets above this many entries skip the records in memory
+#define TNP_BG_LDS_MIN LREC_N
+#endif
 #ifndef TNP_LREC_CH
 #define TNP_LREC_CH 192  // (256 records: the window stage's own LDS, occupancy unchanged)
 #endif
@@ -1167,7 +1170,7 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
     unsigned long long tph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     BG_PH(0);
     // (a bucket of one chunk gains nothing from it: bunny-scale buckets)
-    const bool in_lds = LREC && wa.keys && pl.perm && n > LREC_N && n < 65536;
+    const bool in_lds = LREC && wa.keys && pl.perm && n > TNP_BG_LDS_MIN && n < 65536;
     void* const order = !in_lds ? nullptr
                                 : SW ? static_cast<void*>(reinterpret_cast<uint64_t*>(pl.perm) + base)
                                      : static_cast<void*>(pl.perm + base);
