@@ -479,11 +479,13 @@ def main():
     # 12 contain regions of 1e5-1e7 vertices (seed 8: 5.5e13 in-region pairs)
     # that the reference's CPU path could not materialise (tools/seed_scan.py)
     ap.add_argument("--seed", type=int, default=6)
-    # the CPU baseline's sample (BASELINE.md §3's budget fallback, N = 64): the
-    # whole 64^3 lattice of the same net and seed (48^3 took 7.9 s on the GPU
-    # box's 16-core share in round 4; 64^3 holds ~2.4x its vertices; 128 is the
-    # benchmarked workload itself, ~18 min of the reference's CPU path)
-    ap.add_argument("--cpu-marks", type=int, default=int(os.environ.get("TNP_CPU_MARKS", 64)))
+    # the CPU baseline's sample: the whole 48^3 lattice of the same net and
+    # seed (7.9 s on the GPU box's 16-core share).  BASELINE.md §3's budget
+    # fallback, 64^3, ran past three minutes there in round 5 (killed by the
+    # box's 180-s silence limit: its larger regions grow the oracle's
+    # pair materialisation faster than the lattice); 128 is the benchmarked
+    # workload itself, ~18 min of the reference's CPU path
+    ap.add_argument("--cpu-marks", type=int, default=int(os.environ.get("TNP_CPU_MARKS", 48)))
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
 
