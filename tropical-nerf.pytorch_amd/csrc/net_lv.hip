@@ -120,8 +120,11 @@ k_forward(NetDev net, const float* __restrict__ xyz, int64_t n, float* __restric
 // endpoints read coalesced (slots i, i + 1), 4 no zero-key gathers, 8 no
 // plane-value gathers, 16 no coordinate gathers, 32 no encoding; 64: the
 // real kernel (its outputs rewritten by the real launch)
+#ifndef TNP_FWD_MINB  // workgroups per CU the register budget is cut for (4: 100 VGPRs, no spill)
+#define TNP_FWD_MINB 4
+#endif
 template <int LV, int H, int NL, int EXP = 0>
-__global__ void __launch_bounds__(TNP_BLOCK, 4)
+__global__ void __launch_bounds__(TNP_BLOCK, TNP_FWD_MINB)
 k_forward_new(NetDev net, const float* xyz, int64_t n, float* __restrict__ pre,
               int64_t ld, int64_t V, int keep_from, const int32_t* __restrict__ sa,
               const int32_t* __restrict__ sb, int idx, OwnBox own, uint64_t* pos,
