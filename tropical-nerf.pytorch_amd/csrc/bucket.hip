@@ -914,6 +914,68 @@ __device__ __forceinline__ int build_windows(int* cnt, const int* cur) {
   return nwin;
 }
 
+// build_windows over the cells [c_lo, c_hi) only (one wave's share of the
+// bucket, bucket_group's per-wave path): the list goes to cnt[c_lo ...]
+// (still written only after every count it could overwrite was read).
+// Returns the window count (every lane).
+__device__ __forceinline__ int build_windows_range(int* cnt, const int* cur, int c_lo, int c_hi) {
+  const int L = tnp::lane();
+  int nwin = 0;
+  int so = -1;  // start offset of the open window (-1: none)
+  for (int c0 = c_lo; c0 < c_hi; c0 += 64) {
+    const int c = c0 + L;
+    const bool in = c < c_hi;
+    const int len = in ? cnt[c] : 0, end = in ? cur[c] : 0;
+    const int start = end - len;
+    const bool big = len > WCELL;
+    __builtin_amdgcn_wave_barrier();
+    int lo = 0;  // first lane of this chunk not yet placed in a window
+    while (lo < 64) {
+      const uint64_t rest = ~0ull << lo;
+      if (so < 0) {
+        const uint64_t cand = __ballot(len > 0 && !big) & rest;
+        if (!cand) break;
+        const int f = __builtin_ctzll(cand);
+        so = __shfl(start, f, 64);
+        lo = f;
+        continue;
+      }
+      const uint64_t stop = __ballot((len > 0) && (big || end > so + 64)) & rest;
+      if (!stop) break;
+      const int f = __builtin_ctzll(stop);
+      const int eo = __shfl(start, f, 64);
+      if (eo > so) {
+        if (L == 0) cnt[c_lo + nwin] = so | (eo << 16);
+        ++nwin;
+      }
+      so = -1;
+      lo = __shfl(big ? 1 : 0, f, 64) ? f + 1 : f;
+    }
+  }
+  if (so >= 0 && c_hi > c_lo) {
+    const int eo = cur[c_hi - 1];
+    if (eo > so) {
+      if (L == 0) cnt[c_lo + nwin] = so | (eo << 16);
+      ++nwin;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  return nwin;
+}
+
+// the first cell whose records start at or after offset `target` (cells in
+// local order; starts non-decreasing): a wave's share of the bucket
+template <int LC>
+__device__ __forceinline__ int first_cell_from(const int* cnt, const int* cur, int target) {
+  int lo = 0, hi = LC;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (cur[mid] - cnt[mid] >= target) hi = mid;
+    else lo = mid + 1;
+  }
+  return lo;
+}
+
 // A small bucket (2..64 entries, the bunny-scale nets' buckets hold tens):
 // ONE wave groups it and tests all its pairs in a single window, with no
 // barrier and no trip of the records through memory.  The wave ranks its
@@ -1182,7 +1244,96 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
       __syncthreads();
       WinAcc a;
       const uint64_t below = (wa.idx >= 64) ? ~0ull : ((1ull << wa.idx) - 1ull);
-      if (TNP_PACKED_WIN && n < 65536) {
+      const bool wave_lists = in_lds && SW && TNP_BG_WAVEWIN;
+      if (wave_lists) {
+        // each wave takes the cells whose records start in its quarter of the
+        // bucket, packs them into windows of whole cells itself (the serial
+        // walk of build_windows over a quarter of the cells) and walks its
+        // windows through a private 64-record stage in LDS: no workgroup
+        // barrier from the grouping to the statistics.  A window's records
+        // are built from the bucket's entry words in cell order and the
+        // member keys, software-pipelined (the keys of the next window and the
+        // words of the one after are in flight while a window is tested).
+        // Round 4 built one list for the bucket (the whole workgroup,
+        // pointer doubling) and tested it in shared chunks, each waiting for
+        // its slowest window.
+        const uint64_t* sw = static_cast<const uint64_t*>(order);
+        const int L = tnp::lane(), wv = tnp::wave();
+        const int nn = (int)n;
+        const int c_lo = wv == 0 ? 0 : first_cell_from<LC>(cnt, cur, (int)((int64_t)nn * wv / TNP_WAVES));
+        const int c_hi = wv == TNP_WAVES - 1 ? LC
+                                             : first_cell_from<LC>(cnt, cur, (int)((int64_t)nn * (wv + 1) / TNP_WAVES));
+        // (every wave has read the cells it bounds by before any list is written)
+        __syncthreads();
+        const int nw = uniform(build_windows_range(cnt, cur, c_lo, c_hi));
+        BG_PH(5);
+        const uint32_t* wl = reinterpret_cast<const uint32_t*>(cnt) + c_lo;
+        auto span = [&](int k, int& s, int& m) {
+          if (k >= nw) { s = 0; m = 0; return; }
+          const uint32_t se = (uint32_t)uniform((int)wl[k]);
+          s = (int)(se & 0xFFFFu);
+          m = (int)(se >> 16) - s;
+        };
+        int s0, m0, s1, m1;
+        span(0, s0, m0);
+        span(1, s1, m1);
+        uint64_t w0 = L < m0 ? sw[s0 + L] : 0ull;
+        uint64_t w1 = L < m1 ? sw[s1 + L] : 0ull;
+        ulonglong2 k0 = L < m0 ? pz[(uint32_t)w0] : make_ulonglong2(0ull, 0ull);
+        // this wave's packed stage (64 records), laid over its W.st slots
+        uint64_t* const ptw = reinterpret_cast<uint64_t*>(&W.st[wv][0]);
+        uint64_t* const paw = ptw + 64;
+        uint32_t* const pvv = reinterpret_cast<uint32_t*>(paw + 64);
+        static_assert(64 * (8 + 8 + 4) <= sizeof(W.st[0]), "a wave's packed stage fits its record slots");
+        const PackedRecs PR{ptw, paw, pvv, nullptr};
+        uint64_t amask = 0;
+        if (PK && wa.fmask) {
+          const uint64_t lo = (uint32_t)(wa.fmask >> wa.idx);
+          amask = lo | (lo << 32);
+        }
+        for (int k = 0; k < nw; ++k) {
+          // in flight behind this window: the keys of the next, the words of the one after
+          int s2, m2;
+          span(k + 2, s2, m2);
+          const ulonglong2 k1 = L < m1 ? pz[(uint32_t)w1] : make_ulonglong2(0ull, 0ull);
+          const uint64_t w2 = L < m2 ? sw[s2 + L] : 0ull;
+          const bool valid = L < m0;
+          uint32_t tag;
+          if constexpr (PK) {
+            if (valid) {
+              ptw[L] = packed_test_word(k0.x, k0.y, (uint32_t)(w0 >> 32) & 63u, below);
+              paw[L] = packed_above_word(k0.x, k0.y, wa.idx);
+              pvv[L] = (uint32_t)w0;
+            }
+            tag = valid ? (uint32_t)(w0 >> 40) : 0xFFFFFFFFu;
+          } else {
+            CellEnt e;
+            e.p = k0.x;
+            e.z = k0.y;
+            e.v = (int32_t)(uint32_t)w0;
+            e.f = (uint32_t)(w0 >> 32) & 63u;
+            e.tag = valid ? (uint32_t)b * (uint32_t)LC + (uint32_t)(w0 >> 40) : 0xFFFFFFFFu;
+            e.pad = 0;
+            if (valid) W.st[wv][L] = e;
+            tag = e.tag;
+          }
+          lds_fence();
+          // last lane of my cell in the window (the window holds whole cells)
+          const uint32_t nxt = __shfl_down(tag, 1, 64);
+          const uint64_t bm = __ballot(L >= m0 - 1 || nxt != tag);
+          const int last = L + __builtin_ctzll(bm >> L);
+          const int rounds = valid ? last - L : 0;
+          if constexpr (PK)
+            window_tests_packed(PR, 0, rounds, (uint32_t)below, wa.nb, amask, wa.keys, wa.cap, wa.xs, ctr, W, a);
+          else
+            window_tests(W.st[wv], rounds, below, wa.nb, wa.fmask, wa.keys, wa.cap, wa.xs, ctr, W, a);
+          w0 = w1;
+          k0 = k1;
+          m0 = m1;
+          w1 = w2;
+          m1 = m2;
+        }
+      } else if (TNP_PACKED_WIN && n < 65536) {
         // packed windows of whole cells (the list overwrites cnt[]): built by
         // the whole workgroup for 8^3-cell buckets (their scratch fits the
         // window pass's LDS, unused until the pass), by wave 0 for 16^3
@@ -1202,84 +1353,7 @@ k_bucket_group(BGeom G, const int64_t* __restrict__ bbase, const uint64_t* __res
         }
         __syncthreads();
         BG_PH(5);
-        if (in_lds && SW && TNP_BG_WAVEWIN) {
-          // each wave walks its own windows (kw, kw + TNP_WAVES, ...) through a
-          // private 64-record stage in LDS, no workgroup barrier: a window's
-          // records are built from the bucket's entry words in cell order and
-          // the member keys, software-pipelined (the keys of the next window
-          // and the words of the one after are in flight while a window is
-          // tested), so a wave never waits on the slowest window of a shared
-          // chunk (round 4's chunk pipeline)
-          const uint64_t* sw = static_cast<const uint64_t*>(order);
-          const int L = tnp::lane(), wv = tnp::wave(), nw = nwin_s;
-          const uint32_t* wl = reinterpret_cast<const uint32_t*>(cnt);
-          auto span = [&](int k, int& s, int& m) {
-            if (k >= nw) { s = 0; m = 0; return; }
-            const uint32_t se = (uint32_t)uniform((int)wl[k]);
-            s = (int)(se & 0xFFFFu);
-            m = (int)(se >> 16) - s;
-          };
-          int s0, m0, s1, m1;
-          span(wv, s0, m0);
-          span(wv + TNP_WAVES, s1, m1);
-          uint64_t w0 = L < m0 ? sw[s0 + L] : 0ull;
-          uint64_t w1 = L < m1 ? sw[s1 + L] : 0ull;
-          ulonglong2 k0 = L < m0 ? pz[(uint32_t)w0] : make_ulonglong2(0ull, 0ull);
-          // this wave's packed stage (64 records), laid over its W.st slots
-          uint64_t* const ptw = reinterpret_cast<uint64_t*>(&W.st[wv][0]);
-          uint64_t* const paw = ptw + 64;
-          uint32_t* const pvv = reinterpret_cast<uint32_t*>(paw + 64);
-          uint16_t* const ptg = reinterpret_cast<uint16_t*>(pvv + 64);
-          static_assert(64 * (8 + 8 + 4 + 2) <= sizeof(W.st[0]), "a wave's packed stage fits its record slots");
-          const PackedRecs PR{ptw, paw, pvv, ptg};
-          uint64_t amask = 0;
-          if (PK && wa.fmask) {
-            const uint64_t lo = (uint32_t)(wa.fmask >> wa.idx);
-            amask = lo | (lo << 32);
-          }
-          for (int k = wv; k < nw; k += TNP_WAVES) {
-            // in flight behind this window: the keys of the next, the words of the one after
-            int s2, m2;
-            span(k + 2 * TNP_WAVES, s2, m2);
-            const ulonglong2 k1 = L < m1 ? pz[(uint32_t)w1] : make_ulonglong2(0ull, 0ull);
-            const uint64_t w2 = L < m2 ? sw[s2 + L] : 0ull;
-            const bool valid = L < m0;
-            uint32_t tag;
-            if constexpr (PK) {
-              if (valid) {
-                ptw[L] = packed_test_word(k0.x, k0.y, (uint32_t)(w0 >> 32) & 63u, below);
-                paw[L] = packed_above_word(k0.x, k0.y, wa.idx);
-                pvv[L] = (uint32_t)w0;
-              }
-              tag = valid ? (uint32_t)(w0 >> 40) : 0xFFFFFFFFu;
-            } else {
-              CellEnt e;
-              e.p = k0.x;
-              e.z = k0.y;
-              e.v = (int32_t)(uint32_t)w0;
-              e.f = (uint32_t)(w0 >> 32) & 63u;
-              e.tag = valid ? (uint32_t)b * (uint32_t)LC + (uint32_t)(w0 >> 40) : 0xFFFFFFFFu;
-              e.pad = 0;
-              if (valid) W.st[wv][L] = e;
-              tag = e.tag;
-            }
-            lds_fence();
-            // last lane of my cell in the window (the window holds whole cells)
-            const uint32_t nxt = __shfl_down(tag, 1, 64);
-            const uint64_t bm = __ballot(L >= m0 - 1 || nxt != tag);
-            const int last = L + __builtin_ctzll(bm >> L);
-            const int rounds = valid ? last - L : 0;
-            if constexpr (PK)
-              window_tests_packed(PR, 0, rounds, (uint32_t)below, wa.nb, amask, wa.keys, wa.cap, wa.xs, ctr, W, a);
-            else
-              window_tests(W.st[wv], rounds, below, wa.nb, wa.fmask, wa.keys, wa.cap, wa.xs, ctr, W, a);
-            w0 = w1;
-            k0 = k1;
-            m0 = m1;
-            w1 = w2;
-            m1 = m2;
-          }
-        } else if (in_lds) {
+        if (in_lds) {
           // chunks of TNP_LREC_CH record positions gathered into LDS, then the
           // windows that start there tested.  Software-pipelined: SW (the
           // bucket's entry words written in cell order by the grouping): the
