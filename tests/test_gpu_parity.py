@@ -414,6 +414,36 @@ def test_engine_footprint_is_steady_across_passes(cuda, G):
     assert foot[0]["key_bytes"] > 0 and foot[0]["buffers"] > 10
 
 
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("G", [48, 128])
+def test_run_steps_deferred_counts_match_host_loop(cuda, G):
+    """tnp_engine_run_steps leaves a pruning step's live counts to the next
+    split's hit workers (engine.cpp resolve_counts): its per-step stats (V_out,
+    E_out included) and the extracted complex equal the host loop's, which
+    counts them in the finish (split / finish through the same entry points)."""
+    import bench
+    from tropical._engine import engine_for
+    net = bench.make_net(G, cuda, 6)
+    eng = engine_for(net)
+    eng.set_owned()
+    eng.set_shards(1)
+    outs = []
+    for host in (False, True):
+        eng.lattice()
+        st = []
+        if host:
+            eng._run_steps_host(st, lambda v, op: v)
+        else:
+            eng.run_steps(st)
+        v, e, _ = eng.export()
+        outs.append((st, eng.sizes(), v.cpu().numpy(), e.cpu().numpy()))
+    assert outs[0][0] == outs[1][0]
+    assert outs[0][1] == outs[1][1]
+    np.testing.assert_array_equal(outs[0][2], outs[1][2])
+    np.testing.assert_array_equal(outs[0][3], outs[1][3])
+    assert any(s["E_out"] < s["E_in"] + s["X"] for s in outs[0][0])
+
+
 @pytest.mark.parametrize("name", ["large_sphere", "small_sphere"])
 def test_skeleton_box_is_the_restricted_skeleton(cuda, name):
     """The sharded skeleton (tnp_engine_skeleton_gmax / _box): the tiles' max

@@ -200,6 +200,16 @@ struct tnp_engine {
   bool valid = false;
   int64_t V_live = 0;
   Buf live;  // live-slot flags (uint8) of the lazily compacted vertex set
+  // deferred live counts (tnp_engine_run_steps): a pruning step leaves
+  // V_live (and, lazy prune, E_live) to the next split, whose hit workers read
+  // every live flag anyway (HitArgs::hpart) and whose readback sums them
+  // with the lazy prune's per-workgroup kept counts -- no count_live launch
+  bool defer_counts = false;  // set by the run loop only
+  bool cnt_pending = false;
+  bool defer_ok = true;               // TNP_DEFER_COUNTS=0: count in the finish (A/B)
+  int64_t pend_lz_n = 0;              // lzpart entries holding E_live (0: E_live is known)
+  tnp_step_stats* pend_st = nullptr;  // the step whose V_out / E_out wait for them
+  Buf hpart;                          // the hit workers' live counts
   // step scratch
   Buf spcnt, spoff, part, ekey_a, ekey_b, eval_b, sort_scr2;
   // (pcell/ptoff: compacted pair cells and their first pair; ents: CellEnt
@@ -251,9 +261,14 @@ static_assert(CTR_N <= 32, "counter block");
 // the host spins on its sequence word (measured on MI355X: 9.9 us per round
 // trip against 15.7 us for a copy + stream synchronise); after 2 ms of
 // spinning (long kernels) it blocks in the stream synchronise instead
-static int read_ctr(tnp_engine* e, hipStream_t s) {
+// vpart != null: the published CTR_V (and CTR_E when ne > 0) are the sums of
+// vpart[nv] / epart[ne] (the deferred live counts), not the device words
+static int read_ctr(tnp_engine* e, hipStream_t s, const int64_t* vpart = nullptr, int nv = 0,
+                    const int64_t* epart = nullptr, int ne = 0) {
   const int64_t seq = ++e->pub_seq;
-  if (launch_publish(P<int64_t>(e->ctr), e->h_map_dev, seq, s)) return -1;
+  if (vpart ? launch_publish_sums(P<int64_t>(e->ctr), e->h_map_dev, seq, vpart, nv, epart, ne, s)
+            : launch_publish(P<int64_t>(e->ctr), e->h_map_dev, seq, s))
+    return -1;
   volatile int64_t* flag = e->h_map + 31;
   const auto t0 = std::chrono::steady_clock::now();
   int n = 0;
@@ -267,6 +282,33 @@ static int read_ctr(tnp_engine* e, hipStream_t s) {
   }
   std::atomic_thread_fence(std::memory_order_acquire);
   memcpy(e->h_ctr, (const void*)e->h_map, CTR_N * sizeof(int64_t));
+  return 0;
+}
+
+// the deferred live counts arrived (V_live, E_live; E_live < 0: unchanged)
+static void apply_counts(tnp_engine* e, int64_t V_live, int64_t E_live) {
+  e->V_live = V_live;
+  if (e->pend_lz_n > 0) e->E_live = E_live;
+  if (e->pend_st) {
+    e->pend_st->V_out = e->V_live;
+    e->pend_st->E_out = e->E_live;
+  }
+  e->cnt_pending = false;
+  e->pend_lz_n = 0;
+  e->pend_st = nullptr;
+}
+
+// the deferred counts now, by the counting pass (a split without hit
+// workers, the end of the run loop, any other caller); the counter words
+// CTR_V / CTR_E are still zero from the last split's reset
+static int resolve_counts(tnp_engine* e, hipStream_t s) {
+  if (!e->cnt_pending) return 0;
+  int64_t* ctr = P<int64_t>(e->ctr);
+  if (launch_count_flags(P<uint8_t>(e->live), e->V, ctr, CTR_V, s, e->pend_lz_n ? P<int64_t>(e->lzpart) : nullptr,
+                         (int)e->pend_lz_n, CTR_E))
+    return -1;
+  if (read_ctr(e, s)) return -1;
+  apply_counts(e, e->h_ctr[CTR_V], e->h_ctr[CTR_E]);
   return 0;
 }
 
@@ -452,7 +494,7 @@ static int compute_masks(tnp_engine* e, int from, int64_t* ctr, hipStream_t s) {
   if (buf_ensure(e->eef, E1 * sizeof(uint8_t), s)) return -1;
   TIMED("edge_masks", 42.0 * e->E,
         launch_edge_masks(P<int32_t>(e->edges), e->E, P<uint64_t>(e->cur.pz), P<uint8_t>(e->edm),
-                          P<uint8_t>(e->eef), from, e->K - 1, e->E != e->E_live, ctr, s));
+                          P<uint8_t>(e->eef), from, e->K - 1, e->cnt_pending || e->E != e->E_live, ctr, s));
   if (eps2(e)) {
     // first split planes at subpoly's eps from the cached planes (the mode
     // keeps them all): they replace the Net.eps ones and their OR
@@ -568,6 +610,7 @@ extern "C" int tnp_engine_create(tnp_engine** out, int device) {
   if (const char* lr = getenv("TNP_LDS_RECORDS")) e->lds_records = atoi(lr) != 0;
   if (const char* pr = getenv("TNP_PACKED_RECORDS")) e->packed_records = atoi(pr) != 0;
   if (const char* sp = getenv("TNP_LB_SPIN")) e->lb_spin = atoi(sp);
+  if (const char* dc = getenv("TNP_DEFER_COUNTS")) e->defer_ok = atoi(dc) != 0;
   if (hipHostMalloc((void**)&e->h_ctr, CTR_N * sizeof(int64_t), hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc((void**)&e->h_map, 32 * sizeof(int64_t), hipHostMallocMapped | hipHostMallocCoherent) !=
           hipSuccess ||
@@ -595,7 +638,8 @@ static void for_each_buf(tnp_engine* e, F&& f) {
                  &e->ctr, &e->tri, &e->faces, &e->lb[0], &e->lb[1], &e->edm, &e->eef,
                  &e->edm_alt, &e->eef_alt, &e->live, &e->tied_table, &e->xs, &e->lbrc, &e->lzpart,
                  &e->kse[0], &e->kse[1], &e->kse[2], &e->sents, &e->sents2,
-                 &e->spcnt, &e->spoff, &e->part, &e->ekey_a, &e->ekey_b, &e->eval_b, &e->sort_scr2};
+                 &e->spcnt, &e->spoff, &e->part, &e->ekey_a, &e->ekey_b, &e->eval_b, &e->sort_scr2,
+                 &e->hpart};
   for (Buf* b : bufs) f(*b);
   for (Buf& b : e->fscr) f(b);
   for (Buf& b : e->fscr2) f(b);
@@ -1135,6 +1179,12 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
   int64_t S = 0;
   e->pend_hits = false;
   auto seg_split = [&]() -> int {
+  // the last step's deferred live counts ride in this split's hit workers
+  // (the flat bucket path); otherwise they are counted now, before the reset
+  BucketGeom bgs{};
+  const bool fused_hits = !e->curve && e->V > 0 && e->E > 0 && uses_buckets(e, &bgs);
+  if (e->cnt_pending && !fused_hits && resolve_counts(e, s)) return -1;
+  const bool take_counts = e->cnt_pending;
   TNP_CHECK(hipMemsetAsync(e->ctr.p, 0, CTR_CLEAR_BYTES, s));
   if (e->E > 0) {
     // single pass; the id buffers hold the upper bound E (capacity is kept)
@@ -1151,11 +1201,11 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
     // (S <= E) and they ride in the split's own dispatch; the radix path
     // wants them after the S new members (members[S, S + H)): launched
     // behind the split, which writes S
-    BucketGeom bgs{};
     const bool flat_hits = !e->curve && e->V > 0;
-    const bool fused_hits = flat_hits && uses_buckets(e, &bgs);
     if (flat_hits && buf_ensure(e->members, (e->E + e->V) * sizeof(int32_t), s)) return -1;
-    const HitArgs ha{col, P<uint8_t>(e->live), e->V, eps, P<int32_t>(e->members) + e->E};
+    if (take_counts && buf_ensure(e->hpart, HIT_WORKERS_MAX * sizeof(int64_t), s)) return -1;
+    const HitArgs ha{col, P<uint8_t>(e->live), e->V, eps, P<int32_t>(e->members) + e->E,
+                     take_counts ? P<int64_t>(e->hpart) : nullptr};
     // algorithmic bytes: 1 B first split plane per edge (+ 5 B per vertex
     // slot for fused hits); per split 8 B endpoints, 4 B rewired id, 1 B
     // stale mask (set once S is known)
@@ -1169,7 +1219,14 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
                         P<int64_t>(e->ctr), s));
     e->pend_hits = flat_hits;
     e->pend_hoff = fused_hits ? e->E : -1;
-    if (read_ctr(e, s)) return -1;
+    if (take_counts) {
+      if (read_ctr(e, s, P<int64_t>(e->hpart), split_hit_workers(e->V), e->pend_lz_n ? P<int64_t>(e->lzpart) : nullptr,
+                   (int)e->pend_lz_n))
+        return -1;
+      apply_counts(e, e->h_ctr[CTR_V], e->h_ctr[CTR_E]);
+    } else if (read_ctr(e, s)) {
+      return -1;
+    }
     S = e->h_ctr[CTR_S];
     if (fresh) e->act_bits = (uint64_t)e->h_ctr[CTR_ACTIVE];
     if (e->h_ctr[CTR_MISSED]) {  // ensure_masks keeps this from happening
@@ -1276,6 +1333,10 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   TNP_CHECK(hipSetDevice(e->device));
   if (e->pend_idx != idx) { tnp_set_error("finish(%d) without split(%d)", idx, idx); return -1; }
   if (require_valid(e, "finish")) return -1;
+  if (e->cnt_pending) {  // (the split resolves them; a finish never sees them pending)
+    tnp_set_error("finish(%d): live counts of the last step still pending", idx);
+    return -1;
+  }
   e->pend_idx = -1;
   e->valid = false;  // until this step has completed
   const bool hits_done = e->pend_hits;
@@ -1598,6 +1659,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   // ctr[CTR_ACTIVE] and ctr[CTR_V] are still zero from the split's reset
   const int32_t* eg = P<int32_t>(e->edges);
   int64_t V2 = NV, E2 = N, E2_live = N;
+  bool defer = false;  // the live counts left to the next split (tnp_engine_run_steps)
   int next_valid = e->valid_from;
   // lazy edge deletion (k_prune_lazy) unless the list is mostly dead edges
   // already: then the compacting prune drops them (and this step's)
@@ -1613,6 +1675,10 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     // (word-atomic live counting inside the prune measured slower than the
     // counting pass even at bunny scale: 0.25 vs 0.13 + 0.07 ms per subpoly)
     const bool count_in_prune = false;
+    // the run loop leaves the live counts to the next split's hit workers
+    // (not in the kernel-timer pass: the prune's modelled bytes want them)
+    BucketGeom bgd{};
+    defer = e->defer_counts && !e->kt_on && !e->curve && !eps2(e) && uses_buckets(e, &bgd);
     // (curve path: recomputed after the rewiring, first split planes above idx)
     if (!e->masks_valid && compute_masks(e, idx + 1, nullptr, s)) return -1;
     const int64_t N1 = std::max<int64_t>(N, 1);
@@ -1634,9 +1700,12 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
               launch_ef_cache(P<int32_t>(e->edges), N, P<uint8_t>(e->edm), P<uint8_t>(e->eef), P<float>(c.pre),
                               c.cap, idx + 1, K, e->net.eps_s, ctr, s));
       }
-      TIMED("count_live", 1.0 * NV,
-            launch_count_flags(P<uint8_t>(e->live), NV, ctr, CTR_V, s, P<int64_t>(e->lzpart),
-                               prune_lazy_blocks(N), CTR_E));
+      if (defer)
+        e->pend_lz_n = prune_lazy_blocks(N);
+      else
+        TIMED("count_live", 1.0 * NV,
+              launch_count_flags(P<uint8_t>(e->live), NV, ctr, CTR_V, s, P<int64_t>(e->lzpart),
+                                 prune_lazy_blocks(N), CTR_E));
       swap_edges = false;
     } else {
       if (buf_ensure(e->edges_alt, N1 * 2 * sizeof(int32_t), s)) return -1;
@@ -1653,12 +1722,14 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
                             P<uint8_t>(e->live), count_in_prune, ctr, lb, s));
       std::swap(e->edm, e->edm_alt);
       std::swap(e->eef, e->eef_alt);
-      if (!count_in_prune)
+      if (defer)
+        e->pend_lz_n = 0;  // (E_live: the compacting prune's own count, read back below)
+      else if (!count_in_prune)
         TIMED("count_live", 1.0 * NV, launch_count_flags(P<uint8_t>(e->live), NV, ctr, CTR_V, s));
     }
     next_valid = (e->keep_all || eps2(e)) ? 0 : std::min(idx + 1, K - 1);
     if (read_ctr(e, s)) return -1;
-    E2_live = e->h_ctr[CTR_E];
+    E2_live = (defer && lazy) ? E_live_in : e->h_ctr[CTR_E];  // (deferred: set by apply_counts)
     E2 = lazy ? N : E2_live;
     ktimer_set_bytes(e, "prune", lazy ? 1.0 * E + 36.0 * S + 40.0 * X + 9.0 * E2_live
                                       : 10.0 * E + 36.0 * S + 40.0 * X + 12.0 * E2_live);
@@ -1708,6 +1779,10 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   e->E = E2;
   e->E_live = E2_live;
   e->valid_from = next_valid;
+  if (defer) {  // V_live (and the lazy prune's E_live) arrive with the next split
+    e->cnt_pending = true;
+    e->pend_st = st;
+  }
   if (st) {
     st->idx = idx;
     st->V_in = V_in_live;
@@ -1742,22 +1817,32 @@ extern "C" int tnp_engine_run_steps(tnp_engine* e, void* stream, tnp_step_stats*
   uint64_t mask = 0;
   if (tnp_engine_active_planes(e, 0, &mask, stream)) return -1;
   const int K = e->K;
+  // a pruning step's live counts are taken by the next split (deferred);
+  // every exit path below resolves the last ones
+  tnp_step_stats spare{};
+  auto done = [&](int rc) -> int {
+    e->defer_counts = false;
+    if (resolve_counts(e, (hipStream_t)stream)) rc = -1;
+    e->pend_st = nullptr;
+    return rc;
+  };
+  e->defer_counts = e->defer_ok;
   for (int idx = 0; idx < K; ++idx) {
     if (!tnp::act_test(mask, idx)) continue;
     int64_t S = 0;
     int32_t fail = 0;
-    if (tnp_engine_split(e, idx, stream, &S, &fail)) return -1;
+    if (tnp_engine_split(e, idx, stream, &S, &fail)) return done(-1);
     if (S == 0) continue;
     const int prune = idx < K - 1;  // the last plane never prunes
-    tnp_step_stats st{};
-    if (tnp_engine_finish(e, idx, prune, fail, stream, &st)) return -1;
-    if (*n_steps < max_stats) stats[*n_steps] = st;
+    tnp_step_stats* st = *n_steps < max_stats ? &stats[*n_steps] : &spare;
+    *st = tnp_step_stats{};
+    if (tnp_engine_finish(e, idx, prune, fail, stream, st)) return done(-1);
     ++*n_steps;
     // (planes >= 63 share bit 63: after such a step only the next-active word counts)
-    if (prune) mask = idx >= 62 ? ((mask & ((1ull << 63) - 1ull)) | st.next_active)
-                                : ((mask & ((2ull << idx) - 1ull)) | st.next_active);
+    if (prune) mask = idx >= 62 ? ((mask & ((1ull << 63) - 1ull)) | st->next_active)
+                                : ((mask & ((2ull << idx) - 1ull)) | st->next_active);
   }
-  return 0;
+  return done(0);
 }
 
 extern "C" int tnp_engine_export(tnp_engine* e, float* d_xyz, int64_t* d_edges, float* d_pre,

@@ -44,6 +44,7 @@ enum {
 int64_t step_tiles(int64_t n);
 int64_t lb_tiles(int64_t n);     // tiles of the single-pass prune
 int64_t split_tiles(int64_t n);  // tiles of the single-pass split and hit passes
+int split_hit_workers(int64_t V);  // hit workers a split over V vertex slots runs (HitArgs::hpart entries)
 int64_t run_tiles(int64_t n);    // tiles of the radix path's run-start pass
 // single-pass split over split_tiles(E) look-back tiles (E > 0) from the
 // edges' first split planes (ef == idx): S -> ctr[CTR_S]; an edge whose
@@ -60,7 +61,12 @@ struct HitArgs {
   int64_t V;
   float eps;
   int32_t* out;
+  // != null: every hit worker also counts the live slots it reads -> hpart[w]
+  // (the previous step's live vertex count, summed by launch_publish_sums:
+  // the engine's run loop defers count_live into the next split)
+  int64_t* hpart;
 };
+constexpr int HIT_WORKERS_MAX = 512;  // hit workers of one split (hpart entries)
 int launch_split_lb(int32_t* edges, int64_t E, const uint8_t* ef, uint8_t* dm, int idx, int64_t V,
                     int32_t* sa, int32_t* sb, int64_t* ctr, int32_t* eidx, const TnpLB& lb,
                     hipStream_t s, const HitArgs* hits = nullptr);
@@ -229,6 +235,11 @@ int launch_prune_lazy(int32_t* edges, int64_t E, const int32_t* sb, int64_t S, i
 // the counter block -> a host-mapped mirror, then the sequence word at [31]
 // (the host spins on it instead of a copy + stream synchronise)
 int launch_publish(const int64_t* ctr, int64_t* host, int64_t seq, hipStream_t s);
+// the same, publishing host[CTR_V] = sum(vpart[0..nv)) and (ne > 0)
+// host[CTR_E] = sum(epart[0..ne)) instead of the device words (the deferred
+// live counts of the previous step; the device words stay untouched)
+int launch_publish_sums(const int64_t* ctr, int64_t* host, int64_t seq, const int64_t* vpart, int nv,
+                        const int64_t* epart, int ne, hipStream_t s);
 int launch_widen_flags(const uint8_t* f, int64_t n, int32_t* out, hipStream_t s);
 // planes the pruning of step idx compares (idx .. last_plane)
 uint64_t prune_mask(int idx, int last_plane);

@@ -96,11 +96,12 @@ constexpr int LTILE = TNP_BLOCK * LIPT;
 constexpr int HIPT = 16;                    // slots per thread per chunk
 constexpr int HCHUNK = TNP_BLOCK * HIPT;    // slots per chunk
 constexpr int HBUF = 2 * HCHUNK;            // LDS hit buffer (a chunk always fits after a flush)
-constexpr int HIT_GRID = 512;
+constexpr int HIT_GRID = HIT_WORKERS_MAX;
 
 __device__ __forceinline__ void hit_body(int64_t bid, int64_t nblk, const float* __restrict__ col,
                                          const uint8_t* __restrict__ alive, int64_t V, float eps,
-                                         int32_t* __restrict__ out, int64_t* __restrict__ ctr);
+                                         int32_t* __restrict__ out, int64_t* __restrict__ ctr,
+                                         int64_t* __restrict__ hpart);
 // ---------------------------------------------------------------------------
 // split test: subpoly.py:102-105
 // ---------------------------------------------------------------------------
@@ -126,7 +127,7 @@ k_split_lb(int32_t* __restrict__ edges, int64_t E, int64_t ntiles, const uint8_t
     // the plane's hit vertices (k_hit_append's work) in the same dispatch:
     // workgroups past the split tiles (they wait on nothing)
     hit_body((int64_t)blockIdx.x - ntiles, (int64_t)gridDim.x - ntiles, ha.col, ha.alive, ha.V, ha.eps, ha.out,
-             ctr);
+             ctr, ha.hpart);
     return;
   }
   __shared__ int cnt[SI][TNP_WAVES];
@@ -291,10 +292,13 @@ __global__ void k_finalize_new(int64_t S, int K, int override_, const uint64_t* 
 // one hit worker (block bid of nblk): hits appended to out[ctr[CTR_H]++]
 __device__ __forceinline__ void hit_body(int64_t bid, int64_t nblk, const float* __restrict__ col,
                                          const uint8_t* __restrict__ alive, int64_t V, float eps,
-                                         int32_t* __restrict__ out, int64_t* __restrict__ ctr) {
+                                         int32_t* __restrict__ out, int64_t* __restrict__ ctr,
+                                         int64_t* __restrict__ hpart) {
   __shared__ int32_t hb[HBUF];
   __shared__ int hn;
   __shared__ int64_t hbase;
+  __shared__ int64_t lcnt[TNP_WAVES];
+  int64_t nlive = 0;  // (hpart) live slots this thread read
   if (threadIdx.x == 0) hn = 0;
   __syncthreads();
   auto flush = [&]() {
@@ -320,6 +324,7 @@ __device__ __forceinline__ void hit_body(int64_t bid, int64_t nblk, const float*
 #pragma unroll
     for (int k = 0; k < HIPT; ++k) {
       const int64_t i = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
+      nlive += (i < V) && al[k];
       const bool h = (i < V) && (fabsf(c[k]) < eps) && al[k];
       const uint64_t b = __ballot(h);
       if (b) {
@@ -334,6 +339,16 @@ __device__ __forceinline__ void hit_body(int64_t bid, int64_t nblk, const float*
   }
   __syncthreads();
   flush();
+  if (hpart) {
+    nlive = tnp::wave_sum(nlive);
+    if (tnp::lane() == 0) lcnt[tnp::wave()] = nlive;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int64_t t = 0;
+      for (int w = 0; w < TNP_WAVES; ++w) t += lcnt[w];
+      hpart[bid] = t;
+    }
+  }
 }
 
 __global__ void __launch_bounds__(TNP_BLOCK)
@@ -341,7 +356,7 @@ k_hit_append(const float* __restrict__ col, const uint8_t* __restrict__ alive, i
              int32_t* __restrict__ members, int64_t S_arg, int64_t* __restrict__ ctr) {
   // S_arg < 0: launched right behind the split, whose count is on the device
   const int64_t S = S_arg < 0 ? ctr[CTR_S] : S_arg;
-  hit_body(blockIdx.x, gridDim.x, col, alive, V, eps, members + S, ctr);
+  hit_body(blockIdx.x, gridDim.x, col, alive, V, eps, members + S, ctr, nullptr);
 }
 
 // new vertices outside this shard's owned box (the flat path counts
@@ -1381,6 +1396,21 @@ __global__ void k_publish(const int64_t* __restrict__ ctr, volatile int64_t* hos
   __syncthreads();
   if (t == 31) host[t] = seq;
 }
+// k_publish with the deferred live counts summed in (one wave)
+__global__ void k_publish_sums(const int64_t* __restrict__ ctr, volatile int64_t* host, int64_t seq,
+                               const int64_t* __restrict__ vpart, int nv, const int64_t* __restrict__ epart,
+                               int ne) {
+  const int t = threadIdx.x;
+  int64_t v = 0, e = 0;
+  for (int i = t; i < nv; i += 64) v += vpart[i];
+  for (int i = t; i < ne; i += 64) e += epart[i];
+  v = tnp::wave_sum(v);
+  e = tnp::wave_sum(e);
+  if (t < CTR_N) host[t] = t == CTR_V ? v : (t == CTR_E && ne > 0) ? e : ctr[t];
+  __threadfence_system();
+  __syncthreads();
+  if (t == 31) host[t] = seq;
+}
 
 }  // namespace
 
@@ -1389,6 +1419,9 @@ __global__ void k_publish(const int64_t* __restrict__ ctr, volatile int64_t* hos
 // ----------------------------------------------------------------------------
 int64_t step_tiles(int64_t n) { return (n + TILE - 1) / TILE; }
 int64_t lb_tiles(int64_t n) { return (n + LTILE - 1) / LTILE; }
+int split_hit_workers(int64_t V) {
+  return V > 0 ? (int)std::min<int64_t>(HIT_GRID, (V + HCHUNK - 1) / HCHUNK) : 0;
+}
 int64_t split_tiles(int64_t n) {
   const int64_t t = (int64_t)TNP_BLOCK * split_ipt(n);
   return (n + t - 1) / t;
@@ -1399,11 +1432,11 @@ int launch_split_lb(int32_t* edges, int64_t E, const uint8_t* sm, uint8_t* dm, i
                     int32_t* sa, int32_t* sb, int64_t* ctr, int32_t* eidx, const TnpLB& lb,
                     hipStream_t s, const HitArgs* hits) {
   const int64_t tiles = split_tiles(E);
-  HitArgs ha{nullptr, nullptr, 0, 0.f, nullptr};
+  HitArgs ha{nullptr, nullptr, 0, 0.f, nullptr, nullptr};
   int64_t hg = 0;
   if (hits && hits->V > 0) {
     ha = *hits;
-    hg = std::min<int64_t>(HIT_GRID, (hits->V + HCHUNK - 1) / HCHUNK);
+    hg = split_hit_workers(hits->V);
   }
   const unsigned grid = (unsigned)(tiles + hg);
   if (split_ipt(E) == SIPT_BIG)
@@ -1694,6 +1727,12 @@ int launch_widen_flags(const uint8_t* f, int64_t n, int32_t* out, hipStream_t s)
 }
 int launch_publish(const int64_t* ctr, int64_t* host, int64_t seq, hipStream_t s) {
   hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, s, ctr, host, seq);
+  TNP_CHECK(hipGetLastError());
+  return 0;
+}
+int launch_publish_sums(const int64_t* ctr, int64_t* host, int64_t seq, const int64_t* vpart, int nv,
+                        const int64_t* epart, int ne, hipStream_t s) {
+  hipLaunchKernelGGL(k_publish_sums, dim3(1), dim3(64), 0, s, ctr, host, seq, vpart, nv, epart, ne);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
