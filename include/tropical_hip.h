@@ -224,7 +224,9 @@ int tnp_engine_surface(tnp_engine* eng, void* stream, int64_t* V, int64_t* E);
  * (surface) complex: n_tri = rows of faces_with_indices, n_faces = rows of
  * the float faces (they differ only when a vertex sits exactly at the
  * origin, which the reference's norm>0 mask drops).  Read both with
- * tnp_engine_faces_export (d_tri n_tri x 3 int64, d_faces n_faces x 3 x 3). */
+ * tnp_engine_faces_export (d_tri n_tri x 3 int64, d_faces n_faces x 3 x 3;
+ * device memory or pinned host memory -- the copies are asynchronous on
+ * `stream`: synchronise it before reading host destinations). */
 int tnp_engine_faces(tnp_engine* eng, void* stream, int64_t* n_tri, int64_t* n_faces);
 int tnp_engine_faces_export(tnp_engine* eng, int64_t* d_tri, float* d_faces,
                             void* stream);

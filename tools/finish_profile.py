@@ -46,7 +46,7 @@ def main():
             eng.export()
             torch.cuda.synchronize(dev)
             t.append(time.perf_counter())
-            tri, fc = eng.faces()
+            tri, fc = eng.faces(host=True)
             torch.cuda.synchronize(dev)
             t.append(time.perf_counter())
             sp._faces_to_numpy(tri, fc)

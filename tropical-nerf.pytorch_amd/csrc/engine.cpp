@@ -2481,9 +2481,9 @@ extern "C" int tnp_engine_faces_export(tnp_engine* e, int64_t* d_tri, float* d_f
   hipStream_t s = (hipStream_t)stream;
   TNP_CHECK(hipSetDevice(e->device));
   if (d_tri && e->n_tri > 0)
-    TNP_CHECK(hipMemcpyAsync(d_tri, e->tri.p, e->n_tri * 3 * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
-  if (d_faces && e->n_faces > 0)
-    TNP_CHECK(hipMemcpyAsync(d_faces, e->faces.p, e->n_faces * 9 * sizeof(float), hipMemcpyDeviceToDevice, s));
+    TNP_CHECK(hipMemcpyAsync(d_tri, e->tri.p, e->n_tri * 3 * sizeof(int64_t), hipMemcpyDefault, s));
+  if (d_faces && e->n_faces > 0)  // (device or pinned host destinations: one DMA each)
+    TNP_CHECK(hipMemcpyAsync(d_faces, e->faces.p, e->n_faces * 9 * sizeof(float), hipMemcpyDefault, s));
   return 0;
 }
 

@@ -283,14 +283,21 @@ class Engine:
                    "tnp_engine_surface")
         return V.value, E.value
 
-    def faces(self):
+    def faces(self, host: bool = False):
+        """(faces_with_indices [F, 3] int64, faces [F', 3, 3] float); host=True:
+        in pinned host memory, copied by DMA straight from the engine's
+        buffers (what subpoly() returns as numpy arrays)."""
         nt, nf = C.c_int64(), C.c_int64()
-        _hip.check(_hip.lib().tnp_engine_faces(self.h, self._s, C.byref(nt), C.byref(nf)),
+        s = self._s
+        _hip.check(_hip.lib().tnp_engine_faces(self.h, s, C.byref(nt), C.byref(nf)),
                    "tnp_engine_faces")
-        tri = torch.empty(nt.value, 3, dtype=torch.int64, device=self.device)
-        fc = torch.empty(nf.value, 3, 3, device=self.device)
-        _hip.check(_hip.lib().tnp_engine_faces_export(self.h, _hip.ptr(tri), _hip.ptr(fc), self._s),
+        where = dict(device="cpu", pin_memory=True) if host else dict(device=self.device)
+        tri = torch.empty(nt.value, 3, dtype=torch.int64, **where)
+        fc = torch.empty(nf.value, 3, 3, **where)
+        _hip.check(_hip.lib().tnp_engine_faces_export(self.h, _hip.ptr(tri), _hip.ptr(fc), s),
                    "tnp_engine_faces_export")
+        if host:
+            torch.cuda.current_stream(self.device).synchronize()  # (the stream of self._s)
         return tri, fc
 
     # -- the hot loop (subpoly.py:58-69) -------------------------------------

@@ -31,7 +31,7 @@ def _eps(net, eps):
 def _faces_to_numpy(tri: Tensor, faces: Tensor):
     if tri.shape[0] == 0:
         return [], []
-    return faces.cpu().numpy(), tri.cpu().numpy()
+    return faces.numpy(), tri.numpy()  # (host tensors: faces(host=True))
 
 
 @torch.no_grad()
@@ -60,7 +60,7 @@ def _finish(eng, net):
         print("0 faces", end=", ")
         return [], torch.zeros(0, dtype=torch.int64, device=eng.device), []
     verts, _, _ = eng.export(edges=False)  # (the faces need no edge list)
-    tri, fc = eng.faces()
+    tri, fc = eng.faces(host=True)
     faces, fwi = _faces_to_numpy(tri, fc)
     print(f"{len(faces)} faces", end=", ")
     return faces, verts, fwi
@@ -131,7 +131,7 @@ def extract_faces(vertices, edges, net, outputs=None, eps=None):
         return [], []
     eng = engine_for(net).set_eps(_eps(net, eps))
     eng.load(vertices, edges, outputs, keep_all=True)
-    tri, fc = eng.faces()
+    tri, fc = eng.faces(host=True)
     return _faces_to_numpy(tri, fc)
 
 
