@@ -207,6 +207,7 @@ struct tnp_engine {
   bool defer_counts = false;  // set by the run loop only
   bool cnt_pending = false;
   bool defer_ok = true;               // TNP_DEFER_COUNTS=0: count in the finish (A/B)
+  bool early_forward = true;          // TNP_EARLY_FWD=0: k_forward_new after S is read back (A/B)
   int64_t pend_lz_n = 0;              // lzpart entries holding E_live (0: E_live is known)
   tnp_step_stats* pend_st = nullptr;  // the step whose V_out / E_out wait for them
   Buf hpart;                          // the hit workers' live counts
@@ -263,12 +264,18 @@ static_assert(CTR_N <= 32, "counter block");
 // spinning (long kernels) it blocks in the stream synchronise instead
 // vpart != null: the published CTR_V (and CTR_E when ne > 0) are the sums of
 // vpart[nv] / epart[ne] (the deferred live counts), not the device words
-static int read_ctr(tnp_engine* e, hipStream_t s, const int64_t* vpart = nullptr, int nv = 0,
+// (post_ctr enqueues the publish, wait_ctr takes it: work enqueued between
+// the two runs on the GPU while the counters travel to the host)
+static int post_ctr(tnp_engine* e, hipStream_t s, int64_t* seq_out, const int64_t* vpart = nullptr, int nv = 0,
                     const int64_t* epart = nullptr, int ne = 0) {
   const int64_t seq = ++e->pub_seq;
   if (vpart ? launch_publish_sums(P<int64_t>(e->ctr), e->h_map_dev, seq, vpart, nv, epart, ne, s)
             : launch_publish(P<int64_t>(e->ctr), e->h_map_dev, seq, s))
     return -1;
+  *seq_out = seq;
+  return 0;
+}
+static int wait_ctr(tnp_engine* e, hipStream_t s, int64_t seq) {
   volatile int64_t* flag = e->h_map + 31;
   const auto t0 = std::chrono::steady_clock::now();
   int n = 0;
@@ -283,6 +290,11 @@ static int read_ctr(tnp_engine* e, hipStream_t s, const int64_t* vpart = nullptr
   std::atomic_thread_fence(std::memory_order_acquire);
   memcpy(e->h_ctr, (const void*)e->h_map, CTR_N * sizeof(int64_t));
   return 0;
+}
+static int read_ctr(tnp_engine* e, hipStream_t s, const int64_t* vpart = nullptr, int nv = 0,
+                    const int64_t* epart = nullptr, int ne = 0) {
+  int64_t seq = 0;
+  return post_ctr(e, s, &seq, vpart, nv, epart, ne) || wait_ctr(e, s, seq) ? -1 : 0;
 }
 
 // the deferred live counts arrived (V_live, E_live; E_live < 0: unchanged)
@@ -611,6 +623,7 @@ extern "C" int tnp_engine_create(tnp_engine** out, int device) {
   if (const char* pr = getenv("TNP_PACKED_RECORDS")) e->packed_records = atoi(pr) != 0;
   if (const char* sp = getenv("TNP_LB_SPIN")) e->lb_spin = atoi(sp);
   if (const char* dc = getenv("TNP_DEFER_COUNTS")) e->defer_ok = atoi(dc) != 0;
+  if (const char* ef = getenv("TNP_EARLY_FWD")) e->early_forward = atoi(ef) != 0;
   if (hipHostMalloc((void**)&e->h_ctr, CTR_N * sizeof(int64_t), hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc((void**)&e->h_map, 32 * sizeof(int64_t), hipHostMallocMapped | hipHostMallocCoherent) !=
           hipSuccess ||
@@ -1159,6 +1172,32 @@ extern "C" int tnp_engine_set_collective(tnp_engine* e, tnp_collective_fn fn, vo
   return 0;
 }
 
+// the flat step's new vertices: split points + forward + failover test +
+// keys in one pass, straight into the cache (k_forward_new).  n < 0: S is
+// still on the device (launched right behind the split, before the host
+// reads S back: the readback's round trip overlaps this kernel), -n bounds
+// it and sizes the vertex set and the shared-plane words.
+static int flat_forward_new(tnp_engine* e, int idx, int64_t n, hipStream_t s) {
+  const int64_t bound = n >= 0 ? n : -n;
+  if (vset_ensure(e, e->cur, e->V + bound, e->V, s)) return -1;
+  if (buf_ensure(e->shared, bound * sizeof(uint64_t) * e->kw, s)) return -1;
+  const float* col = P<float>(e->cur.pre) + (int64_t)idx * e->cur.cap;  // (after any move)
+  e->pend_keep = new_keep_from(e, idx);
+  // compulsory bytes per split: reads 8 B endpoint ids, 24 B endpoint
+  // coordinates, 8 B endpoint plane values, 16 B endpoint zero keys; writes
+  // 12 B coordinates, the cache planes >= keep_from, 48 B keys (pos, zero,
+  // pz, grid, shared); plus the encoding tables once per launch (the 8
+  // corners x L levels gathers are cache traffic).  (n < 0: set once S is known)
+  TIMED("forward_new",
+        (8.0 + 24.0 + 8.0 + 16.0 + 12.0 + 4.0 * (e->K - e->pend_keep) + 48.0) * std::max<int64_t>(n, 0) +
+            table_bytes(e->net),
+        launch_forward_new(e->net, P<float>(e->cur.xyz) + 3 * e->V, n, P<float>(e->cur.pre), e->cur.cap, e->V,
+                           e->pend_keep, P<int32_t>(e->sa), P<int32_t>(e->sb), idx, e->own,
+                           P<uint64_t>(e->cur.pos), P<uint64_t>(e->cur.zero), P<uint64_t>(e->cur.grid),
+                           P<uint64_t>(e->shared), P<int64_t>(e->ctr), P<uint64_t>(e->cur.pz), col, s));
+  return 0;
+}
+
 extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S_out, int32_t* fail) {
   hipStream_t s = (hipStream_t)stream;
   TNP_CHECK(hipSetDevice(e->device));
@@ -1177,6 +1216,7 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
   // with its failure flag (coll_fail)
   const bool ccoll = e->curve && e->shards > 1;
   int64_t S = 0;
+  bool early_fwd = false;  // k_forward_new already launched (device S)
   e->pend_hits = false;
   auto seg_split = [&]() -> int {
   // the last step's deferred live counts ride in this split's hit workers
@@ -1219,14 +1259,17 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
                         P<int64_t>(e->ctr), s));
     e->pend_hits = flat_hits;
     e->pend_hoff = fused_hits ? e->E : -1;
-    if (take_counts) {
-      if (read_ctr(e, s, P<int64_t>(e->hpart), split_hit_workers(e->V), e->pend_lz_n ? P<int64_t>(e->lzpart) : nullptr,
-                   (int)e->pend_lz_n))
-        return -1;
-      apply_counts(e, e->h_ctr[CTR_V], e->h_ctr[CTR_E]);
-    } else if (read_ctr(e, s)) {
+    // flat path: the new vertices' forward goes behind the split now, sized
+    // by the bound S <= E, so the GPU runs it while S travels to the host
+    early_fwd = !e->curve && e->early_forward;
+    int64_t seq = 0;
+    if (take_counts ? post_ctr(e, s, &seq, P<int64_t>(e->hpart), split_hit_workers(e->V),
+                               e->pend_lz_n ? P<int64_t>(e->lzpart) : nullptr, (int)e->pend_lz_n)
+                    : post_ctr(e, s, &seq))
       return -1;
-    }
+    if (early_fwd && flat_forward_new(e, idx, -e->E, s)) return -1;
+    if (wait_ctr(e, s, seq)) return -1;
+    if (take_counts) apply_counts(e, e->h_ctr[CTR_V], e->h_ctr[CTR_E]);
     S = e->h_ctr[CTR_S];
     if (fresh) e->act_bits = (uint64_t)e->h_ctr[CTR_ACTIVE];
     if (e->h_ctr[CTR_MISSED]) {  // ensure_masks keeps this from happening
@@ -1263,27 +1306,16 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
     if (seg_new()) return ccoll ? coll_fail(e, 1, TNP_COLL_SUM) : -1;
     if (e->curve && curve_correct(e, idx, S, s)) return -1;
     auto seg_rest = [&]() -> int {
-    if (buf_ensure(e->shared, S * sizeof(uint64_t) * e->kw, s)) return -1;
     e->pend_fused = !e->curve;
     if (e->pend_fused) {
-      // flat: split points + forward + failover test + keys in one pass,
-      // straight into the cache
-      // compulsory bytes per split: reads 8 B endpoint ids, 24 B endpoint
-      // coordinates, 8 B endpoint plane values, 16 B endpoint zero keys;
-      // writes 12 B coordinates, the cache planes >= valid_from, 48 B keys
-      // (pos, zero, pz, grid, shared); plus the encoding tables once per
-      // launch (the 8 corners x L levels gathers are cache traffic)
-      e->pend_keep = new_keep_from(e, idx);
-      TIMED("forward_new",
-            (8.0 + 24.0 + 8.0 + 16.0 + 12.0 + 4.0 * (e->K - e->pend_keep) + 48.0) * S +
-                table_bytes(e->net),
-            launch_forward_new(e->net, P<float>(e->cur.xyz) + 3 * e->V, S, P<float>(e->cur.pre),
-                               e->cur.cap, e->V, e->pend_keep, P<int32_t>(e->sa), P<int32_t>(e->sb),
-                               idx, e->own, P<uint64_t>(e->cur.pos),
-                               P<uint64_t>(e->cur.zero), P<uint64_t>(e->cur.grid),
-                               P<uint64_t>(e->shared), P<int64_t>(e->ctr), P<uint64_t>(e->cur.pz),
-                               col, s));
+      if (early_fwd)  // (launched behind the split; its modelled bytes now)
+        ktimer_set_bytes(e, "forward_new",
+                         (8.0 + 24.0 + 8.0 + 16.0 + 12.0 + 4.0 * (e->K - e->pend_keep) + 48.0) * S +
+                             table_bytes(e->net));
+      else if (flat_forward_new(e, idx, S, s))
+        return -1;
     } else {
+      if (buf_ensure(e->shared, S * sizeof(uint64_t) * e->kw, s)) return -1;
       if (buf_ensure(e->stage, (size_t)S * e->K * sizeof(float), s)) return -1;
       NetDev nf = e->net;
       if (ccoll) nf.sched_rows = Sg;

@@ -124,7 +124,10 @@ int launch_forward(const NetDev& net, const float* xyz, int64_t n, float* pre,
 // the plane column (xyz = slot V: written); cache planes >= keep_from at
 // slots V.., keys, shared
 // planes, failover predicate -> ctr[CTR_FAIL], new vertices outside the
-// owned box (common.h OwnBox) -> ctr[CTR_DUP]; then the override itself
+// owned box (common.h OwnBox) -> ctr[CTR_DUP]; then the override itself.
+// n < 0: the split count is read from ctr[CTR_S] on the device (-n bounds
+// it; buffers sized for the bound): launched behind the split, ahead of the
+// host's readback of S
 int launch_forward_new(const NetDev& net, const float* xyz, int64_t n, float* pre, int64_t ld,
                        int64_t V, int keep_from, const int32_t* sa, const int32_t* sb, int idx,
                        const OwnBox& own, uint64_t* pos, uint64_t* zero, uint64_t* grid,

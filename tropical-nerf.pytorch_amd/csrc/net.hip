@@ -130,7 +130,7 @@ int launch_forward_new(const NetDev& net, const float* xyz, int64_t n, float* pr
                        int64_t V, int keep_from, const int32_t* sa, const int32_t* sb, int idx,
                        const OwnBox& own, uint64_t* pos, uint64_t* zero, uint64_t* grid,
                        uint64_t* shared, int64_t* ctr, uint64_t* pz, const float* col, hipStream_t s) {
-  if (n <= 0) return 0;
+  if (n == 0) return 0;  // (n < 0: the count on the device, -n a bound)
   if (!net_supported(net)) { tnp_set_error("unsupported net shape"); return -1; }
   if (net.n_marks > TNP_MAX_MARKS) { tnp_set_error("more than %d marks per axis", TNP_MAX_MARKS); return -1; }
   TNP_LV_SWITCH(net.n_levels, return lv_forward_new<L_>(net, xyz, n, pre, ld, V, keep_from, sa, sb, idx, own, pos, zero, grid, shared, ctr, pz, col, s));

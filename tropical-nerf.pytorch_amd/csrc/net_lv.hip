@@ -120,12 +120,15 @@ k_forward(NetDev net, const float* __restrict__ xyz, int64_t n, float* __restric
 // endpoints read coalesced (slots i, i + 1), 4 no zero-key gathers, 8 no
 // plane-value gathers, 16 no coordinate gathers, 32 no encoding; 64: the
 // real kernel (its outputs rewritten by the real launch)
+// k_forward_new's grid: one workgroup per 256 splits (n < 0: the count on
+// the device, -n its bound)
+inline unsigned fwd_new_grid(int64_t n) { return tnp_grid(n >= 0 ? n : -n); }
 #ifndef TNP_FWD_MINB  // workgroups per CU the register budget is cut for (4: 100 VGPRs, no spill)
 #define TNP_FWD_MINB 4
 #endif
 template <int LV, int H, int NL, int EXP = 0>
 __global__ void __launch_bounds__(TNP_BLOCK, TNP_FWD_MINB)
-k_forward_new(NetDev net, const float* xyz, int64_t n, float* __restrict__ pre,
+k_forward_new(NetDev net, const float* xyz, int64_t n_arg, float* __restrict__ pre,
               int64_t ld, int64_t V, int keep_from, const int32_t* __restrict__ sa,
               const int32_t* __restrict__ sb, int idx, OwnBox own, uint64_t* pos,
               uint64_t* zero, uint64_t* __restrict__ grid, uint64_t* __restrict__ shared,
@@ -136,14 +139,22 @@ k_forward_new(NetDev net, const float* xyz, int64_t n, float* __restrict__ pre,
   constexpr int IN = 2 * LV;
   constexpr int NW = NetShape<LV, H, NL>::NW;
   constexpr int KW = key_words((NL - 1) * H + 1);
+  // n_arg < 0: the split count is on the device (ctr[CTR_S], the split just
+  // launched ahead on the stream), the grid sized by a bound (launch_forward_new)
+  const int64_t n = n_arg >= 0 ? n_arg : ctr[CTR_S];
+  // XCD-contiguous chunks of the (edge-ordered, spatially coherent) splits:
+  // the hash-table lines one XCD's splits touch then mostly fit its L2.  One
+  // tile per workgroup (a loop over tiles spills this kernel's registers):
+  // with a device count the grid covers the bound, the workgroups past the
+  // count leave before any barrier
+  const int64_t ntl = (n + TNP_BLOCK - 1) / TNP_BLOCK;
+  if ((int64_t)blockIdx.x >= ntl) return;
   __shared__ float w[NW];
   __shared__ float mk[TNP_MAX_MARKS];
   for (int i = threadIdx.x; i < NW; i += blockDim.x) w[i] = net.weights[i];
   for (int i = threadIdx.x; i < net.n_marks; i += blockDim.x) mk[i] = net.marks[i];
   __syncthreads();
-  // XCD-contiguous chunks of the (edge-ordered, spatially coherent) splits:
-  // the hash-table lines one XCD's splits touch then mostly fit its L2
-  const int64_t i = tnp::xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+  const int64_t i = tnp::xcd_block(blockIdx.x, ntl) * TNP_BLOCK + threadIdx.x;
   const bool live = i < n;
   const float eps = net.eps;      // Net.region: the keys
   const float eps_s = net.eps_s;  // subpoly_'s eps: split point, failover
@@ -397,7 +408,7 @@ int lv_forward_new<LVC>(const NetDev& net, const float* xyz, int64_t n, float* p
   if (shadow) (void)hipEventRecord(ev[0], s);
 #define TNP_SHADOW(M)                                                                                          \
   case M:                                                                                                      \
-    hipLaunchKernelGGL((k_forward_new<LVC, H, NL, M>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net, xyz, n, pre, \
+    hipLaunchKernelGGL((k_forward_new<LVC, H, NL, M>), dim3(fwd_new_grid(n)), dim3(TNP_BLOCK), 0, s, net, xyz, n, pre, \
                        ld, V, keep_from, sa, sb, idx, own, pos, zero, grid, shared, ctr, pz, col, sink);       \
     break;
 #define TNP_SHADOW_LAUNCH                                                                                      \
@@ -414,7 +425,7 @@ int lv_forward_new<LVC>(const NetDev& net, const float* xyz, int64_t n, float* p
 #endif
 #define TNP_SHAPE_BODY                                                                                   \
   TNP_SHADOW_LAUNCH                                                                                      \
-  hipLaunchKernelGGL((k_forward_new<LVC, H, NL>), dim3(tnp_grid(n)), dim3(TNP_BLOCK), 0, s, net, xyz, n, pre, ld, \
+  hipLaunchKernelGGL((k_forward_new<LVC, H, NL>), dim3(fwd_new_grid(n)), dim3(TNP_BLOCK), 0, s, net, xyz, n, pre, ld, \
                      V, keep_from, sa, sb, idx, own, pos, zero, grid, shared, ctr, pz, col);
   TNP_SHAPE_SWITCH_ALL(net)
 #undef TNP_SHAPE_BODY
