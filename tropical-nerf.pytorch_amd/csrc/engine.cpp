@@ -1564,6 +1564,17 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   int64_t cap = connect_key_cap(e->ckeys_a.bytes, M, XS_N);
   int64_t X = 0, TT = 0;
   bool chunks_ok = false;  // (radix path) the chunk table matches the pair cells
+  // lazy edge deletion (k_prune_lazy) unless the list is mostly dead edges
+  // already: then the compacting prune drops them (and this step's)
+  // (split-eps mode: always lazy -- its first split planes are recomputed
+  // over the edge slots in place, k_ef_cache)
+  const int64_t E_live_in = e->E_live;
+  const bool lazy = prune && (eps2(e) || (e->lazy_edges && (E - E_live_in) <= E_live_in));
+  // the lazy prune's old edges and e_new need no connecting edge: they are
+  // pruned while the connect counts travel to the host (slots [0, E + S)),
+  // c_new after the sort (part A's workgroup parts first in lzpart)
+  const bool early_prune = lazy && buckets && e->early_forward && !eps2(e) && !e->curve && e->masks_valid;
+  int part_a = 0;
   for (int attempt = 0; attempt < 3; ++attempt) {
     if (buf_ensure(e->ckeys_a, std::max<int64_t>(cap, 1) * sizeof(uint64_t), s)) return -1;
     if (attempt > 0) {  // the split zeroed the whole counter block
@@ -1610,7 +1621,22 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
       if (launch_keys_finish(xs, cap, ctr, s)) return -1;
       e->xs_clean = true;
     }
-    if (read_ctr(e, s)) return -1;
+    int64_t seq = 0;
+    if (post_ctr(e, s, &seq)) return -1;
+    if (early_prune && attempt == 0) {  // (a redone connect leaves part A as it is)
+      const int64_t ES = E + S;
+      if (buf_ensure(e->live, std::max<int64_t>(NV + 4, 16), s)) return -1;  // (+4: word atomics)
+      if (buf_ensure(e->edges, std::max<int64_t>(ES, 1) * 2 * sizeof(int32_t), s, true)) return -1;
+      if (buf_ensure(e->edm, std::max<int64_t>(ES, 1) * sizeof(uint8_t), s, true)) return -1;
+      if (buf_ensure(e->eef, std::max<int64_t>(ES, 1) * sizeof(uint8_t), s, true)) return -1;
+      part_a = prune_lazy_blocks(ES);
+      if (buf_ensure(e->lzpart, part_a * sizeof(int64_t), s)) return -1;
+      TIMED("prune", 1.0 * E + 36.0 * S,
+            launch_prune_lazy(P<int32_t>(e->edges), E, P<int32_t>(e->sb), S, V, nullptr, nb, 0, idx, K - 1,
+                              P<uint64_t>(c.pz), P<uint8_t>(e->edm), P<uint8_t>(e->eef), P<uint8_t>(e->live),
+                              P<int64_t>(e->lzpart), ctr, s, 0, ES));
+    }
+    if (wait_ctr(e, s, seq)) return -1;
     if (buckets) {
       // the atomically allocated pair-cell list: cells | pairs << 24
       e->h_ctr[CTR_R] = e->h_ctr[CTR_PCK] & (PCK_CELLS - 1);
@@ -1684,7 +1710,6 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
 
   // 5. pruning over [edges; e_new; c_new] + vertex compaction
   const int64_t N = E + S + X;
-  const int64_t E_live_in = e->E_live;
   int64_t nt = step_tiles(N);
   if (buf_ensure(e->blk, (nt + 1) * sizeof(int32_t), s)) return -1;
   if (buf_ensure(e->blkoff, (nt + 1) * sizeof(int64_t), s)) return -1;
@@ -1693,11 +1718,6 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   int64_t V2 = NV, E2 = N, E2_live = N;
   bool defer = false;  // the live counts left to the next split (tnp_engine_run_steps)
   int next_valid = e->valid_from;
-  // lazy edge deletion (k_prune_lazy) unless the list is mostly dead edges
-  // already: then the compacting prune drops them (and this step's)
-  // (split-eps mode: always lazy -- its first split planes are recomputed
-  // over the edge slots in place, k_ef_cache)
-  const bool lazy = prune && (eps2(e) || (e->lazy_edges && (E - E_live_in) <= E_live_in));
   bool swap_edges = true;
   if (prune) {
     // live flags recomputed from the kept edges; no vertex moves (lazy
@@ -1719,13 +1739,16 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
       if (buf_ensure(e->edges, N1 * 2 * sizeof(int32_t), s, true)) return -1;
       if (buf_ensure(e->edm, N1 * sizeof(uint8_t), s, true)) return -1;
       if (buf_ensure(e->eef, N1 * sizeof(uint8_t), s, true)) return -1;
-      if (buf_ensure(e->lzpart, prune_lazy_blocks(N) * sizeof(int64_t), s)) return -1;
       // old edges: 1 B high plane (+ 1 B first split plane, 8 B ids when
       // kept); e_new / c_new: 4 / 8 B ids + 32 B endpoint keys, 10 B written
-      TIMED("prune", 1.0 * E + 36.0 * S + 40.0 * X,
+      // (part_a > 0: the old edges and e_new were pruned behind the connect)
+      const int64_t i0 = part_a ? E + S : 0;
+      const int nparts = part_a + prune_lazy_blocks(N - i0);
+      if (buf_ensure(e->lzpart, nparts * sizeof(int64_t), s, part_a > 0)) return -1;
+      TIMED("prune", part_a ? 40.0 * X : 1.0 * E + 36.0 * S + 40.0 * X,
             launch_prune_lazy(P<int32_t>(e->edges), E, P<int32_t>(e->sb), S, V, e->ckeys, nb, X, idx, K - 1,
                               P<uint64_t>(c.pz), P<uint8_t>(e->edm), P<uint8_t>(e->eef), P<uint8_t>(e->live),
-                              P<int64_t>(e->lzpart), ctr, s));
+                              P<int64_t>(e->lzpart) + part_a, ctr, s, i0, N));
       if (eps2(e)) {  // the first split planes at subpoly's eps, and their OR
         TNP_CHECK(hipMemsetAsync(ctr + CTR_ACTIVE, 0, sizeof(int64_t), s));
         TIMED("edge_masks", 8.0 * N,
@@ -1733,11 +1756,10 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
                               c.cap, idx + 1, K, e->net.eps_s, ctr, s));
       }
       if (defer)
-        e->pend_lz_n = prune_lazy_blocks(N);
+        e->pend_lz_n = nparts;
       else
         TIMED("count_live", 1.0 * NV,
-              launch_count_flags(P<uint8_t>(e->live), NV, ctr, CTR_V, s, P<int64_t>(e->lzpart),
-                                 prune_lazy_blocks(N), CTR_E));
+              launch_count_flags(P<uint8_t>(e->live), NV, ctr, CTR_V, s, P<int64_t>(e->lzpart), nparts, CTR_E));
       swap_edges = false;
     } else {
       if (buf_ensure(e->edges_alt, N1 * 2 * sizeof(int32_t), s)) return -1;

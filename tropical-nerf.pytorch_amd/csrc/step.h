@@ -229,9 +229,12 @@ int launch_ef_cache(const int32_t* edges, int64_t E, const uint8_t* dm, uint8_t*
                     int from, int K, float eps_s, int64_t* ctr, hipStream_t s);
 constexpr int PRUNE_LAZY_MAX_BLOCKS = 1024;
 int prune_lazy_blocks(int64_t N);
+// [i0, i1): the slots of [edges; e_new; c_new] this launch takes (the
+// old edges and e_new need no c_new: the engine runs them while the connect
+// counts travel to the host); prune_lazy_blocks(i1 - i0) parts
 int launch_prune_lazy(int32_t* edges, int64_t E, const int32_t* sb, int64_t S, int64_t V, const uint64_t* ckeys,
                       int nb, int64_t X, int idx, int last_plane, const uint64_t* pz, uint8_t* dm, uint8_t* ef,
-                      uint8_t* used, int64_t* part, int64_t* ctr, hipStream_t s);
+                      uint8_t* used, int64_t* part, int64_t* ctr, hipStream_t s, int64_t i0, int64_t i1);
 // the counter block -> a host-mapped mirror, then the sequence word at [31]
 // (the host spins on it instead of a copy + stream synchronise)
 int launch_publish(const int64_t* ctr, int64_t* host, int64_t seq, hipStream_t s);

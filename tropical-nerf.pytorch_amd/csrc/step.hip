@@ -1162,7 +1162,7 @@ k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, int idx, Key<KW> amask,
 constexpr int LZ_IPT = 4;
 template <int KW>
 __global__ void __launch_bounds__(TNP_BLOCK)
-k_prune_lazy(EdgeSrc src, int64_t N, int idx, Key<KW> amask, const uint64_t* __restrict__ pz,
+k_prune_lazy(EdgeSrc src, int64_t i0, int64_t N, int idx, Key<KW> amask, const uint64_t* __restrict__ pz,
              int32_t* __restrict__ edges, uint8_t* __restrict__ dm, uint8_t* __restrict__ ef,
              uint8_t* __restrict__ used, int64_t* __restrict__ part, int64_t* __restrict__ ctr) {
   __shared__ int64_t lds[TNP_WAVES];
@@ -1172,7 +1172,7 @@ k_prune_lazy(EdgeSrc src, int64_t N, int idx, Key<KW> amask, const uint64_t* __r
   const int64_t ES = src.E + src.S;
   int64_t kept = 0;
   uint64_t act = 0;
-  for (int64_t t0 = (int64_t)blockIdx.x * TNP_BLOCK * LZ_IPT; t0 < N;
+  for (int64_t t0 = i0 + (int64_t)blockIdx.x * TNP_BLOCK * LZ_IPT; t0 < N;
        t0 += (int64_t)gridDim.x * TNP_BLOCK * LZ_IPT) {
     uint32_t d[LZ_IPT], m[LZ_IPT];
     int a[LZ_IPT], b[LZ_IPT];
@@ -1698,15 +1698,19 @@ int prune_lazy_blocks(int64_t N) {
 }
 int launch_prune_lazy(int32_t* edges, int64_t E, const int32_t* sb, int64_t S, int64_t V, const uint64_t* ckeys,
                       int nb, int64_t X, int idx, int last_plane, const uint64_t* pz, uint8_t* dm, uint8_t* ef,
-                      uint8_t* used, int64_t* part, int64_t* ctr, hipStream_t s) {
+                      uint8_t* used, int64_t* part, int64_t* ctr, hipStream_t s, int64_t i0, int64_t i1) {
   EdgeSrc src{edges, E, sb, S, V, ckeys, nb, X};
-  const int64_t N = E + S + X;
-  const int g = prune_lazy_blocks(N);
+  if (i0 < 0 || i1 < i0 || i1 > E + S + X) {
+    tnp_set_error("prune range [%lld, %lld) outside the %lld slots", (long long)i0, (long long)i1,
+                  (long long)(E + S + X));
+    return -1;
+  }
+  const int g = prune_lazy_blocks(i1 - i0);
   if (kw_of(last_plane) == 2)
-    hipLaunchKernelGGL(k_prune_lazy<2>, dim3(g), dim3(TNP_BLOCK), 0, s, src, N, idx,
+    hipLaunchKernelGGL(k_prune_lazy<2>, dim3(g), dim3(TNP_BLOCK), 0, s, src, i0, i1, idx,
                        plane_mask<2>(idx + 1, last_plane), pz, edges, dm, ef, used, part, ctr);
   else
-    hipLaunchKernelGGL(k_prune_lazy<1>, dim3(g), dim3(TNP_BLOCK), 0, s, src, N, idx,
+    hipLaunchKernelGGL(k_prune_lazy<1>, dim3(g), dim3(TNP_BLOCK), 0, s, src, i0, i1, idx,
                        plane_mask<1>(idx + 1, last_plane), pz, edges, dm, ef, used, part, ctr);
   TNP_CHECK(hipGetLastError());
   return 0;
