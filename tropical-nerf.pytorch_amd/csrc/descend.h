@@ -235,6 +235,20 @@ __device__ __forceinline__ float lane_f(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 
+// every lane's v -> out[0..N) in every lane, through LDS (one wave per
+// workgroup: its LDS accesses complete in program order, so no barrier; the
+// slot array's aliasing keeps the compiler's order).  Replaces N v_readlane
+// round trips (each with its SGPR hazard wait, and the SGPRs they fill
+// spilled to VGPR lanes) by one store and N/4 broadcast loads.
+template <int N>
+__device__ __forceinline__ void wave_bcast(float v, float (&out)[N], float* slot) {
+  slot[threadIdx.x] = v;
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int j = 0; j < N; ++j) out[j] = slot[j];
+  __builtin_amdgcn_wave_barrier();
+}
+
 // The same descent with ONE WAVE PER ROW: the 500 iterations are strictly
 // sequential, so a row's latency per iteration is the whole cost (one thread
 // per row left a lone wave issuing ~4k dependent instructions per
@@ -242,8 +256,8 @@ __device__ __forceinline__ float lane_f(float v, int l) {
 // table entry is gathered once per iteration and reused by the backward
 // pass) and lane j < H neuron j of each layer; every sum keeps the
 // single-thread order above -- corner sums, sequential fma chains, the
-// 1-row 16 x 16 tree -- over operands broadcast with v_readlane, so the
-// result is bitwise that of k_descend.
+// 1-row 16 x 16 tree -- over operands broadcast through LDS (wave_bcast), so
+// the result is bitwise that of k_descend.
 template <int LV, int H, int NL>
 __global__ void __launch_bounds__(64)
 k_descend_wave(NetDev net, int64_t G, const int32_t* __restrict__ glist,
@@ -294,6 +308,10 @@ k_descend_wave(NetDev net, int64_t G, const int32_t* __restrict__ glist,
 #pragma unroll
   for (int l = 1; l < NH; ++l) Wl[l] = Wl[l - 1] + (l == 1 ? H * IN + H : H * H + H);
   const float* WL = Wl[NH - 1] + (NH == 1 ? H * IN + H : H * H + H);
+  // broadcast slots (wave_bcast): rows 0..2 the corner / gradient sums, rows
+  // 3..3+NH-1 the hidden layers' pre-activations (read again for d0 / d1),
+  // row 3+NH the two outputs
+  __shared__ __attribute__((aligned(16))) float bc[4 + NH][64];
   uint64_t word = 0;  // convergence bits of iterations [64 k, 64 k + 64)
   float d0 = 1.f, d1 = 1.f;
   // this lane's table entry of the last iteration: the point moves by ~1e-2
@@ -335,38 +353,46 @@ k_descend_wave(NetDev net, int64_t G, const int32_t* __restrict__ glist,
     const float2 v = cv;
     const float px = __fmul_rn(wc, v.x), py = __fmul_rn(wc, v.y);
     float f[IN];
+    {
+      float cx[8 * LV], cy[8 * LV];
+      wave_bcast<8 * LV>(px, cx, bc[0]);
+      wave_bcast<8 * LV>(py, cy, bc[1]);
 #pragma unroll
-    for (int l = 0; l < LV; ++l) {
-      float a0 = 0.f, a1 = 0.f;
+      for (int l = 0; l < LV; ++l) {
+        float a0 = 0.f, a1 = 0.f;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        a0 = __fadd_rn(a0, lane_f(px, 8 * l + k));
-        a1 = __fadd_rn(a1, lane_f(py, 8 * l + k));
+        for (int k = 0; k < 8; ++k) {
+          a0 = __fadd_rn(a0, cx[8 * l + k]);
+          a1 = __fadd_rn(a1, cy[8 * l + k]);
+        }
+        f[2 * l] = a0;
+        f[2 * l + 1] = a1;
       }
-      f[2 * l] = a0;
-      f[2 * l + 1] = a1;
     }
     // forward, neuron nj per lane; a[l]: this lane's neuron of hidden layer l
+    // (ab[l]: layer l's H pre-activations, in every lane)
     float a[NH];
+    float ab[NH][H];
     float hh[H];
     a[0] = neuron_mode<IN, H>(Wl[0], Wl[0] + H * IN, f, nj, m0, g);
 #pragma unroll
     for (int l = 1; l < NH; ++l) {
+      wave_bcast<H>(a[l - 1], ab[l - 1], bc[3 + l - 1]);
 #pragma unroll
-      for (int j = 0; j < H; ++j) hh[j] = fmaxf(lane_f(a[l - 1], j), 0.f);
+      for (int j = 0; j < H; ++j) hh[j] = fmaxf(ab[l - 1][j], 0.f);
       a[l] = neuron_mode<H, H>(Wl[l], Wl[l] + H * H, hh, nj, mh, g);
     }
+    wave_bcast<H>(a[NH - 1], ab[NH - 1], bc[3 + NH - 1]);
 #pragma unroll
-    for (int j = 0; j < H; ++j) hh[j] = fmaxf(lane_f(a[NH - 1], j), 0.f);
+    for (int j = 0; j < H; ++j) hh[j] = fmaxf(ab[NH - 1][j], 0.f);
     const float o = neuron_mode<H, 2>(WL, WL + 2 * H, hh, lane & 1, mo, g);
-    const float last = __fsub_rn(lane_f(o, 1), lane_f(o, 0));
-    d0 = last;
-    d1 = last;
-#pragma unroll
-    for (int l = 0; l < NH; ++l) {
-      if (j0 >= l * H && j0 < (l + 1) * H) d0 = lane_f(a[l], j0 - l * H);
-      if (idx >= l * H && idx < (l + 1) * H) d1 = lane_f(a[l], idx - l * H);
-    }
+    float ob[2];
+    wave_bcast<2>(o, ob, bc[3 + NH]);
+    const float last = __fsub_rn(ob[1], ob[0]);
+    // the two planes' values: a hidden pre-activation (row 3 + layer, slot
+    // neuron; uniform indices) or the output
+    d0 = j0 < NH * H ? bc[3 + j0 / H][j0 % H] : last;
+    d1 = idx < NH * H ? bc[3 + idx / H][idx % H] : last;
     // backward: seeds of d0^2 + d1^2, neuron nj per lane
     float gl[NH], go = 0.f;
 #pragma unroll
@@ -388,27 +414,22 @@ k_descend_wave(NetDev net, int64_t G, const int32_t* __restrict__ glist,
 #pragma unroll
     for (int l = NH - 1; l >= 1; --l) {
       float gu_[H];
-#pragma unroll
-      for (int j = 0; j < H; ++j) gu_[j] = lane_f(gl[l], j);
+      wave_bcast<H>(gl[l], gu_, bc[0]);
       const float v2 = mm_col<H, H>(gu_, Wl[l], nj, one_row);
       gl[l - 1] = a[l - 1] > 0.f ? __fadd_rn(gl[l - 1], v2) : gl[l - 1];
     }
     float ga1u[H];
-#pragma unroll
-    for (int k = 0; k < H; ++k) ga1u[k] = lane_f(gl[0], k);
+    wave_bcast<H>(gl[0], ga1u, bc[2]);  // (rows 0 / 2 alternate: a row is rewritten only after its reads)
     const float* W0 = Wl[0];
     const int m = lane % IN;
     const float dfm = mm_col<H, IN>(ga1u, W0, m, one_row);
     // encoding input gradient, this lane's corner; sums in (level, corner) order
-    float dfa = 0.f, dfb = 0.f;
-#pragma unroll
-    for (int l = 0; l < LV; ++l) {
-      const float pa = lane_f(dfm, 2 * l), pb = lane_f(dfm, 2 * l + 1);
-      if (l == lc) {
-        dfa = pa;
-        dfb = pb;
-      }
-    }
+    float dfa, dfb;
+    bc[1][lane] = dfm;  // (this lane's level lc: its two input gradients)
+    __builtin_amdgcn_wave_barrier();
+    dfa = bc[1][2 * lc];
+    dfb = bc[1][2 * lc + 1];
+    __builtin_amdgcn_wave_barrier();
     const float dv = __fadd_rn(__fmul_rn(v.x, dfa), __fmul_rn(v.y, dfb));
     float fc[3];
 #pragma unroll
@@ -423,9 +444,11 @@ k_descend_wave(NetDev net, int64_t G, const int32_t* __restrict__ glist,
     float gx[3], nn = 0.f;
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
+      float tq[8 * LV];
+      wave_bcast<8 * LV>(term[d], tq, bc[d]);
       float acc = 0.f;
 #pragma unroll
-      for (int q = 0; q < 8 * LV; ++q) acc = __fadd_rn(acc, lane_f(term[d], q));
+      for (int q = 0; q < 8 * LV; ++q) acc = __fadd_rn(acc, tq[q]);
       gx[d] = __fmul_rn(__fmul_rn(acc, 0.5f), de[d]);
       nn = __fmaf_rn(gx[d], gx[d], nn);
     }
