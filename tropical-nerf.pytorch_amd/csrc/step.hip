@@ -1115,7 +1115,9 @@ k_prune_lb(EdgeSrc src, int64_t N, int64_t ntiles, int idx, Key<KW> amask,
     }
     if ((bal[k] >> tnp::lane()) & 1) {
       const int64_t o = off + tnp::mbcnt(bal[k]);
-      reinterpret_cast<int2*>(out)[o] = make_int2(a[k], b[k]);
+      // (the kept list is read again a whole step later: streamed out)
+      __builtin_nontemporal_store((uint64_t)(uint32_t)a[k] | ((uint64_t)(uint32_t)b[k] << 32),
+                                  reinterpret_cast<uint64_t*>(out) + o);  // (int2 {a, b})
       odm[o] = (uint8_t)d[k];
       oef[o] = (uint8_t)m[k];
       if (count_live) {
@@ -1210,7 +1212,9 @@ k_prune_lazy(EdgeSrc src, int64_t i0, int64_t N, int idx, Key<KW> amask, const u
       if (stale)  // rewired or new: bytes from the endpoint keys
         edge_bytes<KW>(pz, a[k], b[k], amask, d[k], m[k]);
       const bool keep = need[k] && (int)d[k] > idx;
-      if (i >= src.E) e2[i] = make_int2(a[k], b[k]);
+      if (i >= src.E)  // (int2 {a, b}, streamed: read again a step later)
+        __builtin_nontemporal_store((uint64_t)(uint32_t)a[k] | ((uint64_t)(uint32_t)b[k] << 32),
+                                    reinterpret_cast<uint64_t*>(edges) + i);
       if (i >= src.E || stale || (!keep && d[k] != EDGE_DEAD)) {
         dm[i] = keep ? (uint8_t)d[k] : EDGE_DEAD;
         ef[i] = keep ? (uint8_t)m[k] : EDGE_NOSPLIT;
