@@ -13,8 +13,15 @@
 #ifndef TNP_SORT_MERGE_LIMIT
 #define TNP_SORT_MERGE_LIMIT (256 * 1024)
 #endif
-using KeySortCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
-                                              rocprim::default_config, TNP_SORT_MERGE_LIMIT>;
+// onesweep in 1024-thread blocks of 8 keys per thread: 0.43 -> 0.40 ms per
+// 128^3 pass against rocPRIM's gfx950 default (512 x 12); 1024 x 6 measured
+// the same, 1024 x 12 and 768 x 8 slower (tools/sort_cfg_bench.hip, A/B in
+// the engine)
+using KeySortCfg = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 8>, rocprim::kernel_config<1024, 8>, 8,
+                                        rocprim::block_radix_rank_algorithm::match>,
+    TNP_SORT_MERGE_LIMIT>;
 
 size_t sort_scratch_bytes(int64_t n, int bits) {
   size_t bytes = 0;
