@@ -192,9 +192,18 @@ def cpu_baseline(G: int, seed: int, threads: int):
     V, E = slab_lattice(ref.enc.marks.numpy(), 0, G - 1)
     V, E = torch.from_numpy(V), torch.from_numpy(E)
     stats = {}
+    done = [0]
+
+    def progress(V, E, cache):
+        # one stderr line per step: the GPU box ends a command that prints
+        # nothing for 3 minutes (round 5's 64^3 sample was killed that way)
+        done[0] += 1
+        log(f"CPU baseline: step {done[0]}: {V.shape[0]} vertices, {E.shape[0]} edges, "
+            f"{time.perf_counter() - t0:.1f} s")
+
     t0 = time.perf_counter()
     with torch.no_grad():
-        od.run_steps(V, E, ref, 1e-4, None, stats)
+        od.run_steps(V, E, ref, 1e-4, None, stats, on_step=progress)
     dt = time.perf_counter() - t0
     S = sum(s["S"] for s in stats["steps"])
     return S / dt, S, dt

@@ -38,6 +38,12 @@ int tnp_engine_debug_lb_recomputes(tnp_engine* eng, int64_t* n, int reset, void*
  * it off): on = 0 sends every bucket's records through memory, as before. */
 int tnp_engine_debug_set_lds_records(tnp_engine* eng, int on);
 
+/* Debug: the vertex set's row capacity (the cache, coordinates and keys are
+ * sized by it) and how often the early k_forward_new's row bound (the
+ * largest split count seen, csrc/engine.cpp early_bound) was below a step's
+ * split count, so that the forward ran again once the count was known. */
+int tnp_engine_debug_vertex_capacity(tnp_engine* eng, int64_t* rows, int64_t* early_redo);
+
 /* Debug: the engine's capacity arithmetic, host only (csrc/engine.cpp
  * buf_grow_bytes, connect_key_cap).  grown_bytes: the size a buffer of
  * have_bytes grows to for a request of request_bytes; key_cap: the connect

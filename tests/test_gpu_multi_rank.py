@@ -110,6 +110,23 @@ def _worker(rank, world, port, outdir, case, mode):
             return
         d = load(case)
         net = product_net(d, dev)
+        if mode == "empty":
+            # a net whose SDF never crosses zero (o1 - o0 = 5 everywhere): its
+            # skeleton is empty, subpoly falls back to get_hypercube
+            # (subpoly.py:51-52), and the sharded driver must say so
+            with torch.no_grad():
+                net.fc[-1].weight.zero_()
+                net.fc[-1].bias.copy_(torch.tensor([0.0, 5.0]))
+            raised = []
+            for box in (True, False):
+                try:
+                    D.subpoly_sharded(net, 1.2, allreduce=coll, box_skeleton=box)
+                    raised.append(0)
+                except NotImplementedError:
+                    raised.append(1)
+            if rank == 0:
+                np.savez(os.path.join(outdir, "out.npz"), raised=np.array(raised))
+            return
         if mode.startswith("lattice"):
             part, Vl, El, _ = _sharded_lattice(net, rank, world, coll, stats, blocks)
             cuts = part.cuts[0]
@@ -119,7 +136,8 @@ def _worker(rank, world, port, outdir, case, mode):
             curve = mode.startswith("curve")
             info = {}
             eng, owned, first, gE, cuts = D.subpoly_sharded(net, 1.2, allreduce=coll, stats=stats,
-                                                            force=not curve, blocks=blocks, info=info)
+                                                            force=not curve, blocks=blocks, info=info,
+                                                            box_skeleton=not mode.endswith("_whole"))
             Vl, El, _ = eng.export()
             Vl, El = Vl.cpu(), El.cpu()
             own, keep = D.owned_masks(Vl, El, net.enc.marks.cpu(), cuts, rank)
@@ -200,10 +218,17 @@ def test_sharded_lattice_engine(cuda, tmp_path, case, world, mode):
 
 @pytest.mark.parametrize("case,world,mode", [("large_sphere", 2, "skeleton"), ("large_sphere", 3, "skeleton"),
                                              ("large_sphere", 8, "skeleton"), ("small_sphere", 2, "skeleton"),
-                                             ("large_sphere", 8, "skeleton_blocks")])
+                                             ("large_sphere", 8, "skeleton_blocks"),
+                                             # the whole skeleton on every rank, cuts at equal edge load
+                                             ("large_sphere", 3, "skeleton_whole"),
+                                             ("small_sphere", 2, "skeleton_whole")])
 def test_sharded_stanford_net(cuda, tmp_path, case, world, mode):
-    """x-slabs of equal skeleton-edge load, and (skeleton_blocks) 2 x 2 x 2
-    blocks cut at equal marginal load per axis."""
+    """x-slabs of equal skeleton load, and (skeleton_blocks) 2 x 2 x 2
+    blocks cut at equal marginal load per axis.  The default splits the
+    skeleton itself over the ranks (box_skeleton: per-plane point loads);
+    skeleton_whole computes it whole on every rank and cuts at equal
+    skeleton-edge load -- both stitch to the unsharded complex, so they
+    stitch to the same one."""
     d, V, E, want = _unsharded(cuda, case, "skeleton")
     z = _run(tmp_path, case, mode, world)
     assert tuple(int(x) for x in z["tot"]) == want
@@ -211,7 +236,16 @@ def test_sharded_stanford_net(cuda, tmp_path, case, world, mode):
         assert int(z["attempts"]) == 1
     cuts = z["cuts"].tolist()
     assert cuts[0] == 0 and cuts[-1] == len(d["marks"]) - 1
-    assert len(cuts) == (world + 1 if mode == "skeleton" else 3)
+    assert len(cuts) == (3 if mode == "skeleton_blocks" else world + 1)
+
+
+def test_sharded_empty_skeleton_raises(cuda, tmp_path):
+    """A net whose skeleton is empty: subpoly() falls back to get_hypercube
+    (subpoly.py:51-52), which subpoly_sharded does not shard -- it raises
+    NotImplementedError on every rank, with the skeleton split over the ranks
+    (box_skeleton, the default: no box holds an edge) and whole."""
+    z = _run(tmp_path, "small_sphere", "empty", 2)
+    assert z["raised"].tolist() == [1, 1]
 
 
 @pytest.mark.parametrize("case,world,mode", [("small_sphere_curve", 2, "curve"), ("small_sphere_curve", 3, "curve"),
@@ -347,3 +381,112 @@ def test_slab_buckets_do_not_change_the_result(cuda):
     with pytest.raises(RuntimeError, match="outside the mark planes"):
         eng.run_steps([])
     eng.set_shards(1)
+
+
+def _nccl_worker(rank, world, port, outdir):
+    """ONE process on the one GPU, world size 1, backend nccl (RCCL): every
+    collective call site of the sharded path -- bench.Collective's
+    all_gather_into_tensor on device tensors, the engine's in-step
+    collective callback (curve branch), halo_check's and stitch's
+    all_gathers, the final all_reduce -- runs through RCCL on device tensors,
+    as on the 8-GPU node (the gloo tests put them on host copies)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    try:
+        import bench
+        from helpers import product_net
+        from tropical import distributed as D
+        from tropical._engine import engine_for
+        coll = bench.Collective(dev, shm=False)
+        assert coll.shm is None and D.comm_device(None, dev).type == "cuda"
+        # the collective itself: OR / AND / SUM / MAX of one rank's words
+        v = np.array([5, 1 << 62, 3], dtype=np.uint64)
+        out = {op: coll(v, op) for op in ("or", "and")}
+        w = np.array([7, -2, 40], dtype=np.int64)
+        out.update({op: coll(w, op) for op in ("sum", "max")})
+        ok = all(np.array_equal(out[o], v) for o in ("or", "and")) and \
+            all(np.array_equal(out[o], w) for o in ("sum", "max"))
+        # the synthetic lattice through the host loop with the RCCL collective
+        net = bench.make_net(24, dev, 6)
+        part = D.Blocks(24, D.block_dims(1))
+        eng = engine_for(net)
+        eng.set_owned_box(*part.owned(0))
+        eng.set_shards(1)
+        eng.lattice_box(*part.box(0, 3))
+        st = []
+        eng.run_steps(st, coll)
+        Vl, El, _ = eng.export()
+        marks = net.enc.marks
+        seen = D.halo_check(Vl, El, marks, part)  # device tensors: RCCL all_gather
+        owned, first, gE, own, keep = D.stitch(Vl, El, marks, part, masks=True)
+        hv, he = D.complex_hash(Vl, El, own, keep)
+        tot = torch.tensor([owned.shape[0], gE.shape[0], hv, he, sum(s["S"] for s in st)], device=dev,
+                           dtype=torch.int64)
+        dist.all_reduce(tot)
+        SV, SE = D.gather_complex(owned, first, gE)
+        # the curve branch's in-step decisions through the engine's collective
+        # callback, then the skeleton split, all on RCCL
+        d = load("small_sphere_curve")
+        cnet = product_net(d, dev)
+        cst = []
+        ceng, cown, cfirst, cgE, ccuts = D.subpoly_sharded(cnet, 1.2, allreduce=coll, stats=cst, force=False)
+        CV, CE, _ = ceng.export()
+        ch = D.complex_hash(CV, CE)
+        # the engine calls the collective back from inside a curve step only
+        # on shards: the same extraction as 2 "shards" of which this rank is
+        # the only one (its totals are the batch's), every in-step decision
+        # (curve rows, descent rows, convergence AND, strict OR) over RCCL
+        ceng.set_owned()
+        ceng.set_span([0, 0, 0], [-1, -1, -1])
+        ceng.set_shards(2)
+        ceng.set_curve(True)
+        ceng.skeleton(128, 1.2)
+        cst2 = []
+        ceng.run_steps(cst2, coll)
+        CV2, CE2, _ = ceng.export()
+        ch2 = D.complex_hash(CV2, CE2)
+        ceng.set_shards(1)
+        ceng.set_curve(False)
+        np.savez(os.path.join(outdir, "out.npz"), ok=np.array(int(ok)), tot=tot.cpu().numpy(),
+                 seen=np.array(seen is not None), first=np.array(first),
+                 nV=np.array(SV.shape[0]), nE=np.array(SE.shape[0]), dev=np.array(str(SV.device)),
+                 curve=np.array([CV.shape[0], CE.shape[0], ch[0], ch[1], sum(s["S"] for s in cst)],
+                                dtype=np.int64),
+                 curve2=np.array([CV2.shape[0], CE2.shape[0], ch2[0], ch2[1], sum(s["S"] for s in cst2)],
+                                 dtype=np.int64),
+                 cown=np.array(cown.shape[0]), cgE=np.array(cgE.shape[0]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_world_size_one_runs_every_collective_call_site(cuda, tmp_path):
+    """the RCCL branch of every collective (bench.Collective
+    without shared memory, halo_check, stitch, gather_complex, the curve
+    branch's engine callback) on device tensors, in one nccl process group of
+    world size 1 on the one GPU; the results equal the unsharded engine's."""
+    mp.spawn(_nccl_worker, args=(1, _free_port(), str(tmp_path)), nprocs=1, join=True)
+    z = np.load(tmp_path / "out.npz")
+    assert int(z["ok"]) == 1
+    assert bool(z["seen"])
+    assert str(z["dev"]).startswith("cuda")
+    import bench
+    from tropical.distributed import complex_hash
+    from tropical._engine import engine_for
+    net = bench.make_net(24, cuda, 6)
+    eng = engine_for(net)
+    eng.set_owned()
+    eng.set_shards(1)
+    eng.lattice()
+    st = []
+    eng.run_steps(st)
+    V, E, _ = eng.export()
+    ref = [V.shape[0], E.shape[0], *complex_hash(V, E), sum(s["S"] for s in st)]
+    assert z["tot"].tolist() == ref
+    assert int(z["first"]) == 0 and int(z["nV"]) == V.shape[0] and int(z["nE"]) == E.shape[0]
+    d, Vc, Ec, cref = _unsharded(cuda, "small_sphere_curve", "curve")
+    assert z["curve"].tolist() == list(cref)
+    assert z["curve2"].tolist() == list(cref)
+    assert int(z["cown"]) == Vc.shape[0] and int(z["cgE"]) == Ec.shape[0]

@@ -474,3 +474,40 @@ def test_skeleton_box_is_the_restricted_skeleton(cuda, name):
         vb, eb, _ = eng.export()
         assert (V, E) == (vw.shape[0], ew.shape[0]), (lo, hi)
         assert torch.equal(vb, vw) and torch.equal(eb, ew), (lo, hi)
+
+
+@pytest.mark.timeout(300)
+def test_early_forward_bound_keeps_the_vertex_set_small(cuda, monkeypatch):
+    """the early k_forward_new (launched before the
+    split count reaches the host) sized the vertex set by the edge-SLOT count
+    E, lazily deleted slots included, so the cache kept ~V + E rows.  Its
+    bound is now the largest split count seen (+25 %); a step above it runs
+    the forward again once S is known.  On fresh engines over the 128^3
+    headline lattice: the complex is the reference's (bench128 fingerprint),
+    the redo happens only while the engine learns the split counts (never in
+    a later pass), and the vertex set holds no more rows than with the
+    edge-slot bound (TNP_EARLY_BOUND=0, round 5's sizing).  (At 128^3 both
+    end at the last step's V + S -- 12,957,696 rows on the box: the bound
+    matters where the dead edge slots outnumber the splits.)"""
+    import bench
+    from tropical._engine import Engine
+    from tropical.distributed import complex_hash
+    net = bench.make_net(128, cuda, 6)
+    ref = bench.reference_fingerprint(128, 6)
+    rows = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("TNP_EARLY_BOUND", mode)
+        eng = Engine(cuda)
+        eng.set_net(net)
+        redo = []
+        for _ in range(3):
+            eng.lattice()
+            eng.run_steps([])
+            redo.append(eng.vertex_capacity()["early_redo"])
+        V, E, _ = eng.export()
+        assert (V.shape[0], E.shape[0]) + complex_hash(V, E) == ref
+        rows[mode] = eng.vertex_capacity()["rows"]
+        if mode == "1":
+            assert redo[1] == redo[0] and redo[2] == redo[0], redo  # steady after the first pass
+        del eng
+    assert rows["1"] <= rows["0"], rows

@@ -125,8 +125,8 @@ struct Override {
   float* pre;
   int64_t ld;
   int keep_from;
-  uint64_t* pos;
-  uint64_t* zero;
+  const uint64_t* pos;  // (pos / zero: views of pz, common.h vkey_load)
+  const uint64_t* zero;
   ulonglong2* pz;
 };
 
@@ -200,7 +200,7 @@ __device__ __forceinline__ int64_t scan_handed(const T* cnt, int n, int64_t* out
 __global__ void __launch_bounds__(TNP_BLOCK)
 k_bucket_count(const int32_t* __restrict__ members, int64_t S, int64_t V, int64_t M,
                const uint64_t* __restrict__ grid,
-               const uint64_t* __restrict__ zero, int idx, BGeom G, int NB,
+               const uint64_t* zero, int idx, BGeom G, int NB,
                int32_t* __restrict__ bcount, int64_t* __restrict__ part, int64_t* __restrict__ bbase,
                uint8_t* __restrict__ live, int64_t nlive, int fuse, Override ov,
                int64_t* __restrict__ ctr) {
@@ -237,7 +237,7 @@ k_bucket_count(const int32_t* __restrict__ members, int64_t S, int64_t V, int64_
   for (int k = 0; k < BK_IPT; ++k) {
     const int v = vv[k] >= 0 ? vv[k] : 0;
     gg[k] = grid[v];
-    zz[k] = zero[v];
+    zz[k] = zero[2 * (int64_t)v];  // (a view of pz: 2 words per vertex)
   }
   // the failover override of the new vertices (masked_fill_ of their shared
   // planes, subpoly_debug.py:48), fused here: new members are slots V + m
@@ -248,7 +248,7 @@ k_bucket_count(const int32_t* __restrict__ members, int64_t S, int64_t V, int64_
       const int64_t m = base + (int64_t)k * TNP_BLOCK + threadIdx.x;
       const int64_t mc = m < S ? m : 0;
       sh[k] = ov.shared[mc];
-      ps[k] = ov.pos[V + mc];
+      ps[k] = ov.pos[2 * (V + mc)];
     }
 #pragma unroll
     for (int k = 0; k < BK_IPT; ++k) {
@@ -259,8 +259,6 @@ k_bucket_count(const int32_t* __restrict__ members, int64_t S, int64_t V, int64_
         if (p >= ov.keep_from) ov.pre[(int64_t)p * ov.ld + V + m] = 0.f;
       }
       const uint64_t pp = ps[k] & ~sh[k], z = zz[k] | sh[k];
-      ov.pos[V + m] = pp;
-      ov.zero[V + m] = z;
       ov.pz[V + m] = make_ulonglong2(pp, z);
       zz[k] = z;
     }
@@ -334,7 +332,7 @@ __device__ __forceinline__ int64_t sb_scan_excl(int64_t v, int64_t* lds, int64_t
 
 __global__ void __launch_bounds__(SB_THREADS)
 k_bucket_small(const int32_t* __restrict__ members, int64_t S, int64_t V, int64_t M,
-               const uint64_t* __restrict__ grid, const uint64_t* __restrict__ zero, int idx, BGeom G, int NB,
+               const uint64_t* __restrict__ grid, const uint64_t* zero, int idx, BGeom G, int NB,
                int64_t* __restrict__ bbase, uint64_t* __restrict__ ekv, uint8_t* __restrict__ live,
                int64_t nlive, Override ov, int64_t* __restrict__ ctr) {
   extern __shared__ int hist[];  // NB bins
@@ -359,7 +357,7 @@ k_bucket_small(const int32_t* __restrict__ members, int64_t S, int64_t V, int64_
   for (int k = 0; k < SB_IPT; ++k) {
     const int v = vv[k] >= 0 ? vv[k] : 0;
     gg[k] = grid[v];
-    zz[k] = zero[v];
+    zz[k] = zero[2 * (int64_t)v];  // (a view of pz: 2 words per vertex)
   }
   if (ov.shared && (ov.flag < 0 ? ctr[CTR_FAIL] != 0 : ov.flag != 0)) {
     // the new vertices' failover override (as k_bucket_count)
@@ -369,7 +367,7 @@ k_bucket_small(const int32_t* __restrict__ members, int64_t S, int64_t V, int64_
       const int64_t m = (int64_t)k * SB_THREADS + t;
       const int64_t mc = m < S ? m : 0;
       sh[k] = ov.shared[mc];
-      ps[k] = ov.pos[V + mc];
+      ps[k] = ov.pos[2 * (V + mc)];
     }
 #pragma unroll
     for (int k = 0; k < SB_IPT; ++k) {
@@ -380,8 +378,6 @@ k_bucket_small(const int32_t* __restrict__ members, int64_t S, int64_t V, int64_
         if (p >= ov.keep_from) ov.pre[(int64_t)p * ov.ld + V + m] = 0.f;
       }
       const uint64_t pp = ps[k] & ~sh[k], z = zz[k] | sh[k];
-      ov.pos[V + m] = pp;
-      ov.zero[V + m] = z;
       ov.pz[V + m] = make_ulonglong2(pp, z);
       zz[k] = z;
     }

@@ -336,8 +336,9 @@ __device__ __forceinline__ T ld_agent(const T* p) {
 // Sign keys of KW 64-bit words (bit p of word p / 64: plane p).  Nets of
 // K <= 63 planes use one word (every kernel's original form), K in 64..127
 // two (the wide shapes, net_device.h TNP_WIDE_SHAPES).  Arrays of keys are
-// word arrays with KW words per vertex; the interleaved (pos, zero) copy pz
-// holds pos words then zero words, 2 KW per vertex.
+// word arrays with KW words per entry (key_load / key_store); the vertex
+// keys are ONE interleaved array pz, pos words then zero words, 2 KW per
+// vertex (vkey_load, pz_load, pz_store).
 // ---------------------------------------------------------------------------
 template <int KW>
 struct Key {
@@ -467,6 +468,23 @@ __device__ __forceinline__ void key_store(uint64_t* a, int64_t v, const Key<KW>&
 #pragma unroll
     for (int q = 0; q < KW; ++q) a[KW * v + q] = k.w[q];
   }
+}
+// Vertex keys live ONLY in the interleaved array pz (2 KW words per vertex:
+// pos words, then zero words).  A kernel's `pos` / `zero` vertex-key
+// pointers are views of it -- pos = pz, zero = pz + KW (engine.cpp VP / VZ)
+// -- read with vkey_load; writers store the pair with pz_store.  (Round 5
+// kept separate pos and zero arrays besides pz: 16 B more per new vertex.)
+template <int KW>
+__device__ __forceinline__ Key<KW> vkey_load(const uint64_t* a, int64_t v) {
+  Key<KW> k;
+  if constexpr (KW == 2) {
+    const ulonglong2 t = *reinterpret_cast<const ulonglong2*>(a + 4 * v);
+    k.w[0] = t.x;
+    k.w[1] = t.y;
+  } else {
+    k.w[0] = a[2 * v];
+  }
+  return k;
 }
 // the (pos, zero) pair of vertex v from the interleaved copy
 template <int KW>

@@ -75,7 +75,7 @@ __global__ void k_curve_corners(const int32_t* __restrict__ crow, int64_t B,
   if (n == 0) {
     // last plane j < idx both endpoints are eps-zero on (nonzero_last,
     // torch_ext.py:18-29); none -> the reference exit()s (subpoly.py:141-148)
-    const Key<KW> zz = tnp::key_load<KW>(zero, e[0]) & tnp::key_load<KW>(zero, e[1]);
+    const Key<KW> zz = tnp::vkey_load<KW>(zero, e[0]) & tnp::vkey_load<KW>(zero, e[1]);
     const Key<KW> m = zz & tnp::key_below<KW>(idx);
     const int hi = tnp::key_high(m);
     plane[b] = hi ? hi - 1 : 0;

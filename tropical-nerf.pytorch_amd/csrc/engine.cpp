@@ -123,11 +123,17 @@ template <typename T>
 static T* P(Buf& b) { return static_cast<T*>(b.p); }
 
 struct VSet {
-  Buf xyz, pre, pos, zero, grid;
-  Buf pz;  // (pos, zero) interleaved, 16 B per vertex: one gather for both
+  Buf xyz, pre, grid;
+  // the vertex keys, (pos, zero) interleaved: 2 kw words per vertex, one
+  // gather for both; the kernels' pos / zero arrays are views of it (VP / VZ,
+  // common.h vkey_load)
+  Buf pz;
   int64_t cap = 0;  // rows; pre leading dimension == cap
   int K = 0;        // planes the pre buffer holds (the engine is reused across nets)
 };
+// the pos / zero key views of a vertex set from vertex `from` on
+static uint64_t* VP(VSet& v, int kw, int64_t from = 0) { return static_cast<uint64_t*>(v.pz.p) + 2 * kw * from; }
+static uint64_t* VZ(VSet& v, int kw, int64_t from = 0) { return VP(v, kw, from) + kw; }
 
 struct KRec {
   const char* name;
@@ -208,6 +214,13 @@ struct tnp_engine {
   bool cnt_pending = false;
   bool defer_ok = true;               // TNP_DEFER_COUNTS=0: count in the finish (A/B)
   bool early_forward = true;          // TNP_EARLY_FWD=0: k_forward_new after S is read back (A/B)
+  // the early k_forward_new's row bound (early_bound): the largest split
+  // count this engine has seen, not the edge-slot count E -- E counts the
+  // lazily deleted slots too (up to ~2x the live edges), and the vertex set
+  // and the shared-plane words keep whatever capacity the bound asks for
+  int64_t max_split_seen = 0;
+  int64_t n_early_redo = 0;  // steps whose S exceeded the early bound (forward run again)
+  bool early_bound_splits = true;  // TNP_EARLY_BOUND=0 at creation: the edge-slot bound E (round 5, A/B)
   int64_t pend_lz_n = 0;              // lzpart entries holding E_live (0: E_live is known)
   tnp_step_stats* pend_st = nullptr;  // the step whose V_out / E_out wait for them
   Buf hpart;                          // the hit workers' live counts
@@ -418,23 +431,17 @@ static int vset_ensure(tnp_engine* e, VSet& v, int64_t rows, int64_t keep_rows, 
   if (buf_ensure(n.xyz, nc * 3 * sizeof(float), s)) return -1;
   if (buf_ensure(n.pre, (size_t)nc * e->K * sizeof(float), s)) return -1;
   const int64_t kb = 8 * e->kw;  // bytes per key
-  if (buf_ensure(n.pos, nc * kb, s)) return -1;
-  if (buf_ensure(n.zero, nc * kb, s)) return -1;
   if (buf_ensure(n.grid, nc * sizeof(uint64_t), s)) return -1;
   if (buf_ensure(n.pz, nc * 2 * kb, s)) return -1;
   if (keep_rows > 0 && v.cap > 0) {
     TNP_CHECK(hipMemcpyAsync(n.xyz.p, v.xyz.p, keep_rows * 3 * sizeof(float), hipMemcpyDeviceToDevice, s));
     TNP_CHECK(hipMemcpy2DAsync(n.pre.p, nc * sizeof(float), v.pre.p, v.cap * sizeof(float),
                                keep_rows * sizeof(float), e->K, hipMemcpyDeviceToDevice, s));
-    TNP_CHECK(hipMemcpyAsync(n.pos.p, v.pos.p, keep_rows * kb, hipMemcpyDeviceToDevice, s));
-    TNP_CHECK(hipMemcpyAsync(n.zero.p, v.zero.p, keep_rows * kb, hipMemcpyDeviceToDevice, s));
     TNP_CHECK(hipMemcpyAsync(n.grid.p, v.grid.p, keep_rows * 8, hipMemcpyDeviceToDevice, s));
     TNP_CHECK(hipMemcpyAsync(n.pz.p, v.pz.p, keep_rows * 2 * kb, hipMemcpyDeviceToDevice, s));
   }
   buf_free(v.xyz, s);
   buf_free(v.pre, s);
-  buf_free(v.pos, s);
-  buf_free(v.zero, s);
   buf_free(v.grid, s);
   buf_free(v.pz, s);
   v = n;
@@ -443,8 +450,8 @@ static int vset_ensure(tnp_engine* e, VSet& v, int64_t rows, int64_t keep_rows, 
 
 static int keys_for(tnp_engine* e, VSet& v, int64_t from, int64_t n, hipStream_t s) {
   return launch_keys(e->net, P<float>(v.xyz) + 3 * from, P<float>(v.pre) + from, v.cap, n, e->K,
-                     P<uint64_t>(v.pos) + from * e->kw, P<uint64_t>(v.zero) + from * e->kw,
-                     P<uint64_t>(v.grid) + from, s, P<uint64_t>(v.pz) + 2 * e->kw * from);
+                     VP(v, e->kw, from), VZ(v, e->kw, from), P<uint64_t>(v.grid) + from, s,
+                     VP(v, e->kw, from));
 }
 
 // live flags of slots [from, from + n) := 1 (kept capacity: earlier flags stay)
@@ -574,6 +581,10 @@ static int compact_edges(tnp_engine* e, hipStream_t s) {
 // subpoly.py:266-277, done once): scan of the live flags, gather of the
 // vertex rows (planes >= valid_from), edge remap
 static int compact_now(tnp_engine* e, hipStream_t s) {
+  if (e->cnt_pending) {  // (run_steps resolves them on every exit; V_live / E_live would read stale)
+    tnp_set_error("compaction with the live counts of the last step still pending");
+    return -1;
+  }
   if (compact_edges(e, s)) return -1;
   if (!e->dirty) return 0;
   const int64_t NV = e->V;
@@ -586,9 +597,9 @@ static int compact_now(tnp_engine* e, hipStream_t s) {
   VSet& a = e->alt;
   TIMED("gather_vertices", 4.0 * NV + 2.0 * (12 + 4.0 * (e->K - e->valid_from) + 24) * e->V_live,
         launch_gather_vertices(P<int32_t>(e->used), P<int64_t>(e->nid), NV, e->K, e->valid_from,
-                               P<float>(c.xyz), P<float>(c.pre), c.cap, P<uint64_t>(c.pos),
-                               P<uint64_t>(c.zero), P<uint64_t>(c.grid), P<float>(a.xyz),
-                               P<float>(a.pre), a.cap, P<uint64_t>(a.pos), P<uint64_t>(a.zero),
+                               P<float>(c.xyz), P<float>(c.pre), c.cap, VP(c, e->kw),
+                               VZ(c, e->kw), P<uint64_t>(c.grid), P<float>(a.xyz),
+                               P<float>(a.pre), a.cap, VP(a, e->kw), VZ(a, e->kw),
                                P<uint64_t>(a.grid), P<uint64_t>(a.pz), s));
   TIMED("remap_edges", 32.0 * e->E, launch_remap_edges(P<int32_t>(e->edges), e->E, P<int64_t>(e->nid), s));
   if (read_ctr(e, s)) return -1;
@@ -624,6 +635,7 @@ extern "C" int tnp_engine_create(tnp_engine** out, int device) {
   if (const char* sp = getenv("TNP_LB_SPIN")) e->lb_spin = atoi(sp);
   if (const char* dc = getenv("TNP_DEFER_COUNTS")) e->defer_ok = atoi(dc) != 0;
   if (const char* ef = getenv("TNP_EARLY_FWD")) e->early_forward = atoi(ef) != 0;
+  if (const char* eb = getenv("TNP_EARLY_BOUND")) e->early_bound_splits = atoi(eb) != 0;
   if (hipHostMalloc((void**)&e->h_ctr, CTR_N * sizeof(int64_t), hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc((void**)&e->h_map, 32 * sizeof(int64_t), hipHostMallocMapped | hipHostMallocCoherent) !=
           hipSuccess ||
@@ -643,7 +655,7 @@ extern "C" int tnp_engine_create(tnp_engine** out, int device) {
 template <typename F>
 static void for_each_buf(tnp_engine* e, F&& f) {
   for (VSet* v : {&e->cur, &e->alt})
-    for (Buf* b : {&v->xyz, &v->pre, &v->pos, &v->zero, &v->grid, &v->pz}) f(*b);
+    for (Buf* b : {&v->xyz, &v->pre, &v->grid, &v->pz}) f(*b);
   Buf* bufs[] = {&e->edges, &e->edges_alt, &e->blk, &e->blkoff, &e->scan_scr, &e->sa, &e->sb,
                  &e->stage, &e->shared, &e->members, &e->pcn, &e->pent, &e->rstart,
                  &e->ent_v, &e->ents, &e->pcell, &e->ptoff, &e->bcell,
@@ -678,6 +690,13 @@ extern "C" int tnp_engine_scratch_bytes(tnp_engine* e, int64_t* bytes, int64_t* 
   *bytes = tot;
   if (buffers) *buffers = n;
   if (key_bytes) *key_bytes = (int64_t)e->ckeys_a.bytes;
+  return 0;
+}
+
+extern "C" int tnp_engine_debug_vertex_capacity(tnp_engine* e, int64_t* rows, int64_t* early_redo) {
+  if (!e || !rows || !early_redo) { tnp_set_error("tnp_engine_debug_vertex_capacity: null argument"); return -1; }
+  *rows = e->cur.cap;
+  *early_redo = e->n_early_redo;
   return 0;
 }
 
@@ -863,7 +882,7 @@ extern "C" int tnp_engine_load(tnp_engine* e, const float* d_xyz, int64_t V, con
     TNP_CHECK(hipGetLastError());
   } else {
     if (launch_forward(e->net, P<float>(e->cur.xyz), V, P<float>(e->cur.pre), e->cur.cap, 1, s, nullptr,
-                       P<uint64_t>(e->cur.pos), P<uint64_t>(e->cur.zero), P<uint64_t>(e->cur.grid),
+                       VP(e->cur, e->kw), VZ(e->cur, e->kw), P<uint64_t>(e->cur.grid),
                        P<uint64_t>(e->cur.pz)))
       return -1;
   }
@@ -876,6 +895,10 @@ extern "C" int tnp_engine_load(tnp_engine* e, const float* d_xyz, int64_t V, con
 }
 
 extern "C" int tnp_engine_sizes(tnp_engine* e, int64_t* V, int64_t* E) {
+  if (e->cnt_pending) {  // (never a silent 0 from a deferred count)
+    tnp_set_error("tnp_engine_sizes: the live counts of the last step are still pending");
+    return -1;
+  }
   *V = e->V_live;
   *E = e->E_live;
   return 0;
@@ -949,6 +972,23 @@ static int coll_fail(tnp_engine* e, int n, int op) {
 // and descent rows' totals (MKL's row-count schedules of the corner, point
 // and descent launches follow the whole batch) and the descent's stop (the
 // AND of the shards' per-iteration convergence words).
+// A sharded curve step whose batch -- the shards' total rows of one of its
+// forwards -- is 2..15 rows on a 32-wide net: MKL's 32-input FOLD schedule
+// of the 2-output layer depends on each row's parity in the WHOLE batch
+// (net_device.h neuron_mode), the shards number their rows locally, and the
+// batch's row order across shards is not defined.  Refused instead of left
+// to halo_check; every shard sees the same total after the
+// same collective, so every shard refuses at the same point.
+static int fold32_sharded(const tnp_engine* e, int64_t rows, const char* what, int idx) {
+  if (e->shards > 1 && e->net.num_hidden == 32 && rows >= 2 && rows <= 15) {
+    tnp_set_error("plane %d: a sharded curve step of %lld %s on a 32-wide net (MKL's 2..15-row FOLD schedule "
+                  "depends on each row's parity in the whole batch, which the shards do not share); run it "
+                  "unsharded", idx, (long long)rows, what);
+    return -1;
+  }
+  return 0;
+}
+
 static int curve_correct(tnp_engine* e, int idx, int64_t S, hipStream_t s) {
   const float eps = e->net.eps_s;  // subpoly_'s eps (subpoly.py:120-177)
   const int K = e->K;
@@ -980,6 +1020,7 @@ static int curve_correct(tnp_engine* e, int idx, int64_t S, hipStream_t s) {
   int64_t Bg = B;  // the batch's curve rows (r_edges, subpoly.py:120)
   if (coll(e, &Bg, 1, TNP_COLL_SUM)) return -1;
   if (Bg == 0) return 0;
+  if (fold32_sharded(e, Bg, "curve rows", idx)) return -1;
   NetDev ns = e->net;  // sharded: the schedules of the whole batch
   int64_t G = 0;
   int32_t* crow = nullptr;
@@ -1006,7 +1047,7 @@ static int curve_correct(tnp_engine* e, int idx, int64_t S, hipStream_t s) {
   d1s = P<float>(cv[CV_D1]);
   if (launch_curve_rows(P<int32_t>(cv[CV_CFLAG]), P<int64_t>(cv[CV_COFF]), S, crow, s)) return -1;
   TIMED("curve_corners", 8.0 * B * 12 + 24.0 * B,
-        launch_curve_corners(crow, B, sa, sb, xyz, P<uint64_t>(e->cur.zero), P<uint64_t>(e->cur.grid), idx,
+        launch_curve_corners(crow, B, sa, sb, xyz, VZ(e->cur, e->kw), P<uint64_t>(e->cur.grid), idx,
                              P<float>(cv[CV_CORNERS]), plane, ctr, e->kw, s));
   if (sh) ns.sched_rows = 8 * Bg;
   TIMED("curve_forward", 8.0 * B * (12 + 4.0 * K),
@@ -1039,6 +1080,7 @@ static int curve_correct(tnp_engine* e, int idx, int64_t S, hipStream_t s) {
   if (seg_rows()) return coll_fail(e, 1, TNP_COLL_SUM);
   int64_t Gg = G;  // the batch's descent rows
   if (coll(e, &Gg, 1, TNP_COLL_SUM)) return -1;
+  if (fold32_sharded(e, Gg, "descent rows", idx)) return -1;
   if (Gg > 0) {
     if (sh) ns.sched_rows = Gg;
     uint64_t h_conv[8] = {~0ull, ~0ull, ~0ull, ~0ull, ~0ull, ~0ull, ~0ull, ~0ull};  // (no rows: converged)
@@ -1177,6 +1219,11 @@ extern "C" int tnp_engine_set_collective(tnp_engine* e, tnp_collective_fn fn, vo
 // still on the device (launched right behind the split, before the host
 // reads S back: the readback's round trip overlaps this kernel), -n bounds
 // it and sizes the vertex set and the shared-plane words.
+static int64_t early_bound(const tnp_engine* e) {
+  if (!e->early_bound_splits) return e->E;
+  return std::min<int64_t>(e->E, e->max_split_seen + e->max_split_seen / 4 + 4096);
+}
+
 static int flat_forward_new(tnp_engine* e, int idx, int64_t n, hipStream_t s) {
   const int64_t bound = n >= 0 ? n : -n;
   if (vset_ensure(e, e->cur, e->V + bound, e->V, s)) return -1;
@@ -1193,7 +1240,7 @@ static int flat_forward_new(tnp_engine* e, int idx, int64_t n, hipStream_t s) {
             table_bytes(e->net),
         launch_forward_new(e->net, P<float>(e->cur.xyz) + 3 * e->V, n, P<float>(e->cur.pre), e->cur.cap, e->V,
                            e->pend_keep, P<int32_t>(e->sa), P<int32_t>(e->sb), idx, e->own,
-                           P<uint64_t>(e->cur.pos), P<uint64_t>(e->cur.zero), P<uint64_t>(e->cur.grid),
+                           VP(e->cur, e->kw), VZ(e->cur, e->kw), P<uint64_t>(e->cur.grid),
                            P<uint64_t>(e->shared), P<int64_t>(e->ctr), P<uint64_t>(e->cur.pz), col, s));
   return 0;
 }
@@ -1262,15 +1309,25 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
     // flat path: the new vertices' forward goes behind the split now, sized
     // by the bound S <= E, so the GPU runs it while S travels to the host
     early_fwd = !e->curve && e->early_forward;
+    const int64_t eb = early_fwd ? early_bound(e) : 0;
     int64_t seq = 0;
     if (take_counts ? post_ctr(e, s, &seq, P<int64_t>(e->hpart), split_hit_workers(e->V),
                                e->pend_lz_n ? P<int64_t>(e->lzpart) : nullptr, (int)e->pend_lz_n)
                     : post_ctr(e, s, &seq))
       return -1;
-    if (early_fwd && flat_forward_new(e, idx, -e->E, s)) return -1;
+    if (early_fwd && flat_forward_new(e, idx, -eb, s)) return -1;
     if (wait_ctr(e, s, seq)) return -1;
     if (take_counts) apply_counts(e, e->h_ctr[CTR_V], e->h_ctr[CTR_E]);
     S = e->h_ctr[CTR_S];
+    e->max_split_seen = std::max(e->max_split_seen, S);
+    if (early_fwd && S > eb) {
+      // more splits than the early launch's bound: it processed rows [0, eb)
+      // only; the whole forward runs again once S is known (the same values;
+      // the failover OR is idempotent, the halo count is recounted)
+      early_fwd = false;
+      e->n_early_redo++;
+      TNP_CHECK(hipMemsetAsync(P<int64_t>(e->ctr) + CTR_DUP, 0, sizeof(int64_t), s));
+    }
     if (fresh) e->act_bits = (uint64_t)e->h_ctr[CTR_ACTIVE];
     if (e->h_ctr[CTR_MISSED]) {  // ensure_masks keeps this from happening
       tnp_set_error("plane %d: an edge's first split plane lies below the step (stale edge masks)", idx);
@@ -1291,6 +1348,7 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
   *fail = 0;
   int64_t Sg = S;
   if (ccoll && coll(e, &Sg, 1, TNP_COLL_SUM)) return -1;
+  if (ccoll && fold32_sharded(e, Sg, "splits", idx)) return -1;
   if (ccoll && S == 0 && Sg > 0 && curve_correct(e, idx, 0, s)) return -1;
   if (S > 0) {
     auto seg_new = [&]() -> int {
@@ -1324,11 +1382,11 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
       // grid words of the new vertices (coordinates are final; the failover
       // test of a shard reads them: only owned vertices vote)
       if (launch_keys(e->net, P<float>(e->cur.xyz) + 3 * e->V, P<float>(e->stage), S, S, 0,
-                      P<uint64_t>(e->cur.pos) + e->V * e->kw, P<uint64_t>(e->cur.zero) + e->V * e->kw,
-                      P<uint64_t>(e->cur.grid) + e->V, s))
+                      VP(e->cur, e->kw, e->V), VZ(e->cur, e->kw, e->V), P<uint64_t>(e->cur.grid) + e->V, s,
+                      VP(e->cur, e->kw, e->V)))
         return -1;
       TIMED("fail_check", 48.0 * S,
-            launch_fail_check(P<int32_t>(e->sa), P<int32_t>(e->sb), S, idx, P<uint64_t>(e->cur.zero),
+            launch_fail_check(P<int32_t>(e->sa), P<int32_t>(e->sb), S, idx, VZ(e->cur, e->kw),
                               P<float>(e->stage), eps, P<uint64_t>(e->shared), P<int64_t>(e->ctr),
                               P<uint64_t>(e->cur.grid) + e->V, e->own, e->kw, s));
     }
@@ -1391,8 +1449,8 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   VSet& c = e->cur;
   const float* col = P<float>(c.pre) + (int64_t)idx * c.cap;
   int64_t* ctr = P<int64_t>(e->ctr);
-  uint64_t* pos = P<uint64_t>(c.pos);
-  uint64_t* zero = P<uint64_t>(c.zero);
+  uint64_t* pos = VP(c, e->kw);
+  uint64_t* zero = VZ(c, e->kw);
   uint64_t* grid = P<uint64_t>(c.grid);
 
   BucketGeom bg{};
@@ -1965,9 +2023,9 @@ extern "C" int tnp_engine_surface(tnp_engine* e, void* stream, int64_t* V_out, i
   VSet& a = e->alt;
   int keep_from = e->valid_from;
   if (launch_gather_vertices(P<int32_t>(e->used), P<int64_t>(e->nid), V, e->K, keep_from,
-                             P<float>(c.xyz), P<float>(c.pre), c.cap, P<uint64_t>(c.pos),
-                             P<uint64_t>(c.zero), P<uint64_t>(c.grid), P<float>(a.xyz),
-                             P<float>(a.pre), a.cap, P<uint64_t>(a.pos), P<uint64_t>(a.zero),
+                             P<float>(c.xyz), P<float>(c.pre), c.cap, VP(c, e->kw),
+                             VZ(c, e->kw), P<uint64_t>(c.grid), P<float>(a.xyz),
+                             P<float>(a.pre), a.cap, VP(a, e->kw), VZ(a, e->kw),
                              P<uint64_t>(a.grid), P<uint64_t>(a.pz), s))
     return -1;
   if (read_ctr(e, s)) return -1;
@@ -2060,7 +2118,7 @@ extern "C" int tnp_engine_lattice_box(tnp_engine* e, const int32_t* lo3, const i
   // the lattice's full forward (12 B coordinates in; K planes, 40 B of keys out)
   TIMED("forward", (12.0 + 4.0 * e->K + 40.0) * V + table_bytes(e->net),
         launch_forward(e->net, P<float>(e->cur.xyz), V, P<float>(e->cur.pre), e->cur.cap, 1, s, nullptr,
-                       P<uint64_t>(e->cur.pos), P<uint64_t>(e->cur.zero), P<uint64_t>(e->cur.grid),
+                       VP(e->cur, e->kw), VZ(e->cur, e->kw), P<uint64_t>(e->cur.grid),
                        P<uint64_t>(e->cur.pz)));
   e->V = V;
   e->E = E;
@@ -2187,13 +2245,14 @@ static int skeleton_build(tnp_engine* e, int unit, float size, int mode, const i
   }
   int64_t tile_pts = (int64_t)std::min(unit, L) * std::min(unit, L) * std::min(unit, L);
   if (buf_ensure(e->stage, tile_pts * sizeof(float) * (sign ? e->K : 1), s)) return -1;
-  // sign mode: the tile's points, their forward and packed keys (pos, zero,
-  // grid, pz) in the curve path's scratch slots
+  // sign mode: the tile's points, their forward and packed keys (grid words;
+  // pz: (pos, zero) interleaved, 2 kw words a point) in the curve path's
+  // scratch slots
   Buf* sk = e->cv;
   if (sign) {
     if (buf_ensure(sk[CV_CORNERS], tile_pts * 3 * sizeof(float), s)) return -1;
-    for (int k : {CV_D0, CV_D1, CV_GG}) if (buf_ensure(sk[k], tile_pts * sizeof(uint64_t), s)) return -1;
-    if (buf_ensure(sk[CV_STAGE_C], tile_pts * 2 * sizeof(uint64_t), s)) return -1;
+    if (buf_ensure(sk[CV_GG], tile_pts * sizeof(uint64_t), s)) return -1;
+    if (buf_ensure(sk[CV_STAGE_C], tile_pts * 2 * e->kw * sizeof(uint64_t), s)) return -1;
   }
   if (buf_ensure(e->shared, 16, s)) return -1;
   unsigned int* gmax = P<unsigned int>(e->shared);
@@ -2222,8 +2281,8 @@ static int skeleton_build(tnp_engine* e, int unit, float size, int mode, const i
       const int64_t np_ = (int64_t)n0 * n1 * n2;
       if (launch_skel_points(i0, j0, k0, n0, n1, n2, e->net.marks, P<float>(sk[CV_CORNERS]), s)) return -1;
       if (launch_forward(e->net, P<float>(sk[CV_CORNERS]), np_, P<float>(e->stage), np_, 1, s, nullptr,
-                         P<uint64_t>(sk[CV_D0]), P<uint64_t>(sk[CV_D1]), P<uint64_t>(sk[CV_GG]),
-                         P<uint64_t>(sk[CV_STAGE_C])))
+                         P<uint64_t>(sk[CV_STAGE_C]), P<uint64_t>(sk[CV_STAGE_C]) + e->kw,
+                         P<uint64_t>(sk[CV_GG]), P<uint64_t>(sk[CV_STAGE_C])))
         return -1;
       keys = P<uint64_t>(sk[CV_STAGE_C]);
     } else {
@@ -2237,7 +2296,7 @@ static int skeleton_build(tnp_engine* e, int unit, float size, int mode, const i
     if (buf_ensure(e->blk, (nt + 1) * sizeof(int32_t), s)) return -1;
     if (buf_ensure(e->blkoff, (nt + 1) * sizeof(int64_t), s)) return -1;
     if (launch_skel_edges(false, i0, j0, k0, n0, n1, n2, L, P<float>(e->stage), keys, dmax, gm,
-                          P<int32_t>(e->blk), nullptr, 0, nullptr, nullptr, s))
+                          P<int32_t>(e->blk), nullptr, 0, nullptr, nullptr, s, e->kw))
       return -1;
     if (scan_counts(e, P<int32_t>(e->blk), P<int64_t>(e->blkoff), nt, CTR_AUX, s)) return -1;
     if (read_ctr(e, s)) return -1;
@@ -2246,7 +2305,7 @@ static int skeleton_build(tnp_engine* e, int unit, float size, int mode, const i
       if (buf_ensure(e->edges_alt, (total + cnt) * 2 * sizeof(int32_t), s, true)) return -1;
       if (launch_skel_edges(true, i0, j0, k0, n0, n1, n2, L, P<float>(e->stage), keys, dmax, gm,
                             nullptr, P<int64_t>(e->blkoff), total, P<int32_t>(e->edges_alt),
-                            P<int32_t>(e->used), s))
+                            P<int32_t>(e->used), s, e->kw))
         return -1;
     }
     total += cnt;
@@ -2272,7 +2331,7 @@ static int skeleton_build(tnp_engine* e, int unit, float size, int mode, const i
     e->E_live = total;
   }
   if (launch_forward(e->net, P<float>(e->cur.xyz), e->V, P<float>(e->cur.pre), e->cur.cap, 1, s, nullptr,
-                     P<uint64_t>(e->cur.pos), P<uint64_t>(e->cur.zero), P<uint64_t>(e->cur.grid),
+                     VP(e->cur, e->kw), VZ(e->cur, e->kw), P<uint64_t>(e->cur.grid),
                      P<uint64_t>(e->cur.pz)))
     return -1;
   e->keep_all = 0;
@@ -2374,23 +2433,24 @@ extern "C" int tnp_engine_faces(tnp_engine* e, void* stream, int64_t* n_tri, int
     return -1;
   }
   int64_t* ctr = P<int64_t>(e->ctr);
-  const uint64_t* pos = P<uint64_t>(e->cur.pos);
-  const uint64_t* zero = P<uint64_t>(e->cur.zero);
+  const uint64_t* pos = VP(e->cur, e->kw);
+  const uint64_t* zero = VZ(e->cur, e->kw);
   const uint64_t* grid = P<uint64_t>(e->cur.grid);
   const float* xyz = P<float>(e->cur.xyz);
   if (eps2(e)) {
     // extract_faces takes the regions at subpoly's eps (net.region(vertices,
     // outputs, eps), subpoly.py:606): keys of every plane from the cache
     if (e->valid_from != 0) { tnp_set_error("split-eps faces: cached planes were dropped"); return -1; }
-    for (int k = 0; k < 3; ++k)
-      if (buf_ensure(e->kse[k], V * sizeof(uint64_t) * (k < 2 ? e->kw : 1), s)) return -1;
+    // kse[0]: the keys at subpoly's eps, (pos, zero) interleaved as pz; kse[2]: grid words
+    for (int k = 0; k < 3; k += 2)
+      if (buf_ensure(e->kse[k], V * sizeof(uint64_t) * (k == 0 ? 2 * e->kw : 1), s)) return -1;
     NetDev ns = e->net;
     ns.eps = ns.eps_s;
     if (launch_keys(ns, xyz, P<float>(e->cur.pre), e->cur.cap, V, K, P<uint64_t>(e->kse[0]),
-                    P<uint64_t>(e->kse[1]), P<uint64_t>(e->kse[2]), s))
+                    P<uint64_t>(e->kse[0]) + e->kw, P<uint64_t>(e->kse[2]), s, P<uint64_t>(e->kse[0])))
       return -1;
     pos = P<uint64_t>(e->kse[0]);
-    zero = P<uint64_t>(e->kse[1]);
+    zero = P<uint64_t>(e->kse[0]) + e->kw;
     grid = P<uint64_t>(e->kse[2]);
   }
   TNP_CHECK(hipMemsetAsync(ctr, 0, CTR_CLEAR_BYTES, s));

@@ -68,7 +68,7 @@ __device__ __forceinline__ VKey<KW> vkey(uint64_t g, const Key<KW>& pos, const K
 template <int KW>
 __device__ __forceinline__ VKey<KW> vkey_of(int64_t v, const uint64_t* grid, const uint64_t* pos,
                                             const uint64_t* zero, const Key<KW>& pmask) {
-  return vkey<KW>(grid[v], tnp::key_load<KW>(pos, v), tnp::key_load<KW>(zero, v), pmask);
+  return vkey<KW>(grid[v], tnp::vkey_load<KW>(pos, v), tnp::vkey_load<KW>(zero, v), pmask);
 }
 
 // a region key: cell word (3 x 10-bit cell coordinates + 2, never 0) and the

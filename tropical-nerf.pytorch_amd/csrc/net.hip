@@ -37,8 +37,8 @@ namespace {
 template <int KW>
 __global__ void k_override_new(int64_t n, int override_, const uint64_t* __restrict__ shared,
                                float* __restrict__ pre, int64_t ld, int keep_from, int64_t V,
-                               uint64_t* __restrict__ pos, uint64_t* __restrict__ zero,
-                               const int64_t* __restrict__ ctr, uint64_t* __restrict__ pz) {
+                               const uint64_t* pos, const uint64_t* zero,
+                               const int64_t* __restrict__ ctr, uint64_t* pz) {
   const bool ov = override_ < 0 ? ctr[CTR_FAIL] != 0 : override_ != 0;
   if (!ov) return;
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -50,10 +50,8 @@ __global__ void k_override_new(int64_t n, int override_, const uint64_t* __restr
       const int p = 64 * q + __builtin_ctzll(t);
       if (p >= keep_from) pre[(int64_t)p * ld + V + r] = 0.f;
     }
-  const Key<KW> p = tnp::key_load<KW>(pos, V + r) & ~m, z = tnp::key_load<KW>(zero, V + r) | m;
-  tnp::key_store(pos, V + r, p);
-  tnp::key_store(zero, V + r, z);
-  tnp::pz_store(pz, V + r, p, z);
+  const Key<KW> p = tnp::vkey_load<KW>(pos, V + r) & ~m, z = tnp::vkey_load<KW>(zero, V + r) | m;
+  tnp::pz_store(pz, V + r, p, z);  // (pos / zero: views of pz)
 }
 
 __global__ void k_region(NetDev net, const float* __restrict__ xyz,
@@ -92,9 +90,7 @@ __global__ void k_keys(NetDev net, const float* __restrict__ xyz, const float* _
     tnp::key_put(ps, p, v > net.eps);  // sign +1 ((output>0)*2-1 with |.|<=eps -> 0)
     tnp::key_put(zs, p, fabsf(v) <= net.eps);
   }
-  tnp::key_store(pos, i, ps);
-  tnp::key_store(zero, i, zs);
-  if (pz) tnp::pz_store(pz, i, ps, zs);
+  tnp::pz_store(pz, i, ps, zs);  // (pos / zero: views of pz)
 }
 
 }  // namespace

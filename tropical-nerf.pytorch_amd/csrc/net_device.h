@@ -377,6 +377,64 @@ __host__ __device__ __forceinline__ int lin_mode(int64_t n) {
   return LIN_SEQ;
 }
 
+// ---------------------------------------------------------------------------
+// The SEQ schedule on the matrix cores.  On gfx950 v_mfma_f32_16x16x4_f32 is
+// bit for bit the k-ordered fp32 fma chain D = fma(a_k3, b_k3, ... fma(a_k0,
+// b_k0, C)), one rounding per product (cdna_hip_programming.md "FP32-input
+// MFMA"; tools/mfma_probe.hip checks it on the box: 41 M outputs, zeros,
+// negative zeros and denormals included, 0 mismatches).  So a 16-output
+// slice of an IN -> H layer over 16 rows, K-blocks of 4 chained in ascending
+// order from C = 0 and the bias added after, IS acc = fma(x_k, W_jk, acc),
+// + b_j -- the LIN_SEQ schedule of every call of >= 16 rows.
+//
+// The layer is computed transposed, D = W' . X^T (16 neurons x 16 rows), so
+// a wave's 64 rows are 4 row blocks b of 16 and lane (q = lane >> 4, r =
+// lane & 15) holds, in accumulator register g of block b, the neuron
+// 4g + q (+ 16 G for output group G) of row 16 b + r: the A operand's row i
+// is neuron perm(i) = 4 (i & 3) + (i >> 2).  That is exactly the B operand
+// layout of the next layer's K-block s = 4 G + g (input 4 s + q of row r),
+// so activations never leave the registers between layers.  An input count
+// that is not a multiple of 4 is padded with weight -0 and activation 0:
+// fma(-0, 0, acc) = acc for every acc, so the chain is unchanged.
+// ---------------------------------------------------------------------------
+typedef float mf4 __attribute__((ext_vector_type(4)));
+constexpr int MST = 80;  // LDS stage: floats per plane (64 rows + 16: conflict-free transposes)
+
+// LDS hand-over between lanes of ONE wave: every DS op of the wave retires
+// in order, so a wait on this wave's own DS ops (and no compiler motion of
+// memory ops across it) suffices -- no workgroup barrier
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// acc[G][b] = D of output group G, row block b; act[b][s]: K-block s of row
+// block b (B operand); Wl: the layer's weights [16 NG][KI] (row-major, LDS)
+template <int KI, int NG, int SMAX>
+__device__ __forceinline__ void mfma_layer(const float* Wl, const float (&act)[4][SMAX], mf4 (&acc)[NG][4],
+                                           int q, int r) {
+  constexpr int S = (KI + 3) / 4;
+  static_assert(S <= SMAX, "K-blocks");
+#pragma unroll
+  for (int G = 0; G < NG; ++G) {
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[G][b] = mf4{0.f, 0.f, 0.f, 0.f};
+    const int j = 16 * G + 4 * (r & 3) + (r >> 2);
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int k = 4 * s + q;
+      const float a = (KI % 4 == 0 || k < KI) ? Wl[j * KI + k] : -0.0f;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[G][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, act[b][s], acc[G][b], 0, 0, 0);
+    }
+  }
+}
+
+// the layers of an NL-layer net that run on MFMA: hidden widths of 16 or 32
+// (TNP_FWD_MFMA=0: variant builds for A/B, every layer on VALU as round 5)
+#ifndef TNP_FWD_MFMA
+#define TNP_FWD_MFMA 1
+#endif
+template <int H>
+__host__ __device__ constexpr bool mfma_shape() { return TNP_FWD_MFMA && H % 16 == 0; }
+
 template <int LV, int H, int NL>
 struct NetShape {
   static constexpr int IN = 2 * LV;
@@ -392,9 +450,10 @@ struct NetShape {
 #else
 #define TNP_NET_SHAPES(X) X(8, 2) X(8, 3) X(8, 4) X(16, 2) X(16, 3) X(16, 4) X(32, 2)
 // wide shapes: K = 65 or 97 planes, two-word sign keys (common.h Key<2>).
-// They run the flat subpoly path (forward, keys, steps, faces), Net.forward /
-// sdf / normal and the skeleton; the curve branch, its descent and the
-// training / autograd kernels stay with TNP_NET_SHAPES
+// They run everything the K <= 63 shapes run -- the flat and curve subpoly
+// paths (the descent included), sharding, faces, Net.forward / sdf / normal
+// and the skeleton -- except the training / autograd kernels, which stay
+// with TNP_NET_SHAPES
 #define TNP_WIDE_SHAPES(X) X(16, 5) X(32, 3) X(32, 4)
 #endif
 #define TNP_ALL_SHAPES(X) TNP_NET_SHAPES(X) TNP_WIDE_SHAPES(X)

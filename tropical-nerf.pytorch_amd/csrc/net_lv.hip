@@ -100,9 +100,7 @@ k_forward(NetDev net, const float* __restrict__ xyz, int64_t n, float* __restric
   if (!GROUPED && live && kpos) {  // the keys of k_keys, from the values in registers
     tnp::key_put(ps, p, v > net.eps);
     tnp::key_put(zs, p, fabsf(v) <= net.eps);
-    tnp::key_store(kpos, i, ps);
-    tnp::key_store(kzero, i, zs);
-    tnp::pz_store(kpz, i, ps, zs);
+    tnp::pz_store(kpz, i, ps, zs);  // (kpos / kzero: views of kpz)
     kgrid[i] = grid_word(mk, net.n_marks, net.eps, x);
   }
 }
@@ -125,11 +123,11 @@ k_forward(NetDev net, const float* __restrict__ xyz, int64_t n, float* __restric
 inline unsigned fwd_new_grid(int64_t n) { return tnp_grid(n >= 0 ? n : -n); }
 // Streaming stores of k_forward_new: what no later kernel of the step reads
 // -- the cache planes (later steps' split tests), the coordinates (later
-// steps' split points, the finish), the positive-sign keys and the shared
-// planes (the failover override, rare) -- go out non-temporal, keeping the
-// L2 for the encoding tables and the endpoint gathers; the zero keys, the
-// (pos, zero) pairs and the grid words are read by this step's grouping and
-// stay cached.  128^3: 0.89 -> 0.84 ms per pass for this kernel.
+// steps' split points, the finish) and the shared planes (the failover
+// override) -- go out non-temporal, keeping the L2 for the encoding tables
+// and the endpoint gathers; the (pos, zero) keys (pz, the only copy since
+// round 6) and the grid words are read by this step's grouping and stay
+// cached.  128^3: 0.89 -> 0.84 ms per pass for this kernel.
 template <typename T>
 __device__ __forceinline__ void st_stream(T& dst, T v) {
   __builtin_nontemporal_store(v, &dst);
@@ -148,7 +146,7 @@ k_forward_new(NetDev net, const float* xyz, int64_t n_arg, float* __restrict__ p
               int64_t ld, int64_t V, int keep_from, const int32_t* __restrict__ sa,
               const int32_t* __restrict__ sb, int idx, OwnBox own, uint64_t* pos,
               uint64_t* zero, uint64_t* __restrict__ grid, uint64_t* __restrict__ shared,
-              int64_t* __restrict__ ctr, uint64_t* __restrict__ pz, const float* __restrict__ scol,
+              int64_t* __restrict__ ctr, uint64_t* pz, const float* __restrict__ scol,
               uint32_t* __restrict__ sink = nullptr) {
   constexpr bool NOST = (EXP & 1) != 0;
   uint32_t chk = 0;
@@ -157,21 +155,29 @@ k_forward_new(NetDev net, const float* xyz, int64_t n_arg, float* __restrict__ p
   constexpr int KW = key_words((NL - 1) * H + 1);
   // n_arg < 0: the split count is on the device (ctr[CTR_S], the split just
   // launched ahead on the stream), the grid sized by a bound (launch_forward_new)
-  const int64_t n = n_arg >= 0 ? n_arg : ctr[CTR_S];
+  const int64_t n = n_arg >= 0 ? n_arg : ctr[CTR_S];  // the batch: its MKL schedule
+  // the rows this launch computes: a device count is capped by the host's
+  // bound -n_arg, which sized the grid, the vertex set and the shared words
+  // (engine.cpp early_bound: the largest split count seen, possibly below
+  // this step's S -- the host then runs the whole forward again once S is
+  // known; rows past the bound are never touched here)
+  const int64_t nr = n_arg >= 0 ? n_arg : (n < -n_arg ? n : -n_arg);
   // XCD-contiguous chunks of the (edge-ordered, spatially coherent) splits:
   // the hash-table lines one XCD's splits touch then mostly fit its L2.  One
   // tile per workgroup (a loop over tiles spills this kernel's registers):
   // with a device count the grid covers the bound, the workgroups past the
   // count leave before any barrier
-  const int64_t ntl = (n + TNP_BLOCK - 1) / TNP_BLOCK;
+  const int64_t ntl = (nr + TNP_BLOCK - 1) / TNP_BLOCK;
   if ((int64_t)blockIdx.x >= ntl) return;
   __shared__ float w[NW];
   __shared__ float mk[TNP_MAX_MARKS];
+  // MFMA path: each wave's LDS stage for the row <-> lane-layout transposes
+  __shared__ float stg[(EXP == 0 && mfma_shape<H>()) ? TNP_WAVES * 16 * MST : 1];
   for (int i = threadIdx.x; i < NW; i += blockDim.x) w[i] = net.weights[i];
   for (int i = threadIdx.x; i < net.n_marks; i += blockDim.x) mk[i] = net.marks[i];
   __syncthreads();
   const int64_t i = tnp::xcd_block(blockIdx.x, ntl) * TNP_BLOCK + threadIdx.x;
-  const bool live = i < n;
+  const bool live = i < nr;
   const float eps = net.eps;      // Net.region: the keys
   const float eps_s = net.eps_s;  // subpoly_'s eps: split point, failover
   float x[3] = {0.f, 0.f, 0.f};
@@ -184,8 +190,8 @@ k_forward_new(NetDev net, const float* xyz, int64_t n_arg, float* __restrict__ p
     }
     // every gather the endpoints need, issued before the first store (the
     // coordinate store could alias zero[] for the compiler)
-    const Key<KW> za = (EXP & 4) ? tnp::key_zero<KW>() : tnp::key_load<KW>(zero, a);
-    const Key<KW> zb = (EXP & 4) ? tnp::key_zero<KW>() : tnp::key_load<KW>(zero, b);
+    const Key<KW> za = (EXP & 4) ? tnp::key_zero<KW>() : tnp::vkey_load<KW>(zero, a);
+    const Key<KW> zb = (EXP & 4) ? tnp::key_zero<KW>() : tnp::vkey_load<KW>(zero, b);
     if (scol) {
       // the split point itself (k_new_vertices, subpoly.py:113-117, 180), fused:
       // d = d/eps; w = |d0| / |d1 - d0|; v = e0*(1-w) + e1*w
@@ -227,27 +233,98 @@ k_forward_new(NetDev net, const float* xyz, int64_t n_arg, float* __restrict__ p
   bool bad = false;
   const int m0 = lin_mode<IN, H>(n), mh = lin_mode<H, H>(n), mo = lin_mode<H, 2>(n);
   float* col = pre + V + i;
+  // one plane value of this row: the cache store, the keys, the failover test
+  auto plane = [&](int pp, float v) {
+    if (live && pp >= keep_from) st_stream(col[(int64_t)pp * ld], v);
+    tnp::key_put(ps, pp, v > eps);
+    tnp::key_put(zs, pp, fabsf(v) <= eps);
+    bad |= tnp::key_test(m, pp) && fabsf(v) > eps_s;
+  };
+  bool on_mfma = false;
+  if constexpr (EXP == 0 && mfma_shape<H>()) {
+    // >= 16 rows: every hidden layer is the SEQ schedule (lin_mode) -> MFMA
+    // (net_device.h mfma_layer); the wave's rows go through LDS twice per 16
+    // planes: features in, pre-activations back out to one row per lane
+    if (n >= 16) {
+      on_mfma = true;
+      constexpr int NG = H / 16;
+      constexpr int S0 = (IN + 3) / 4, SH = H / 4;
+      constexpr int SM = S0 > SH ? S0 : SH;
+      const int lane = threadIdx.x & 63, q = lane >> 4, r = lane & 15;
+      float* st = stg + (threadIdx.x >> 6) * (16 * MST);
 #pragma unroll
-  for (int layer = 0; layer < NL - 1; ++layer) {
-    if (layer == 0) {
-      linear_mode<IN, H>(W, W + H * IN, h, a, m0, i);
-      W += H * IN + H;
-    } else {
-      linear_mode<H, H>(W, W + H * H, h, a, mh, i);
-      W += H * H + H;
-    }
+      for (int k = 0; k < IN; ++k) st[k * MST + lane] = h[k];
+      wave_lds_sync();
+      float act[4][SM];
 #pragma unroll
-    for (int j = 0; j < H; ++j) {
-      const float v = a[j];
-      if constexpr (NOST) chk ^= __float_as_uint(v);
-      else if (live && p + j >= keep_from) st_stream(col[(int64_t)(p + j) * ld], v);
-      tnp::key_put(ps, p + j, v > eps);
-      tnp::key_put(zs, p + j, fabsf(v) <= eps);
-      bad |= tnp::key_test(m, p + j) && fabsf(v) > eps_s;
-      h[j] = fmaxf(v, 0.0f);
+      for (int b = 0; b < 4; ++b) {
+#pragma unroll
+        for (int s = 0; s < S0; ++s) {
+          const int k = 4 * s + q;
+          act[b][s] = (IN % 4 == 0 || k < IN) ? st[k * MST + 16 * b + r] : 0.f;
+        }
+      }
+      wave_lds_sync();
+#pragma unroll
+      for (int layer = 0; layer < NL - 1; ++layer) {
+        mf4 acc[NG][4];
+        if (layer == 0) mfma_layer<IN, NG, SM>(W, act, acc, q, r);
+        else mfma_layer<H, NG, SM>(W, act, acc, q, r);
+        const float* B = W + H * (layer == 0 ? IN : H);
+        W = B + H;
+#pragma unroll
+        for (int G = 0; G < NG; ++G) {
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const float bj = B[16 * G + 4 * g + q];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+              const float v = __fadd_rn(acc[G][b][g], bj);
+              st[(4 * g + q) * MST + 16 * b + r] = v;
+              act[b][4 * G + g] = fmaxf(v, 0.0f);
+            }
+          }
+          wave_lds_sync();
+#pragma unroll
+          for (int j = 0; j < 16; ++j) {
+            const float v = st[j * MST + lane];
+            plane(p + 16 * G + j, v);
+            h[16 * G + j] = fmaxf(v, 0.0f);
+          }
+          wave_lds_sync();
+        }
+        p += H;
+      }
     }
-    p += H;
   }
+  if (!on_mfma) {
+    // VALU: the small-batch schedules (ONE / FOLD, < 16 rows), 8-wide nets
+#pragma unroll
+    for (int layer = 0; layer < NL - 1; ++layer) {
+      if (layer == 0) {
+        linear_mode<IN, H>(W, W + H * IN, h, a, m0, i);
+        W += H * IN + H;
+      } else {
+        linear_mode<H, H>(W, W + H * H, h, a, mh, i);
+        W += H * H + H;
+      }
+#pragma unroll
+      for (int j = 0; j < H; ++j) {
+        const float v = a[j];
+        if constexpr (NOST) chk ^= __float_as_uint(v);
+        else plane(p + j, v);
+        if constexpr (NOST) {
+          tnp::key_put(ps, p + j, v > eps);
+          tnp::key_put(zs, p + j, fabsf(v) <= eps);
+          bad |= tnp::key_test(m, p + j) && fabsf(v) > eps_s;
+        }
+        h[j] = fmaxf(v, 0.0f);
+      }
+      p += H;
+    }
+  }
+  p = (NL - 1) * H;
+  W = w + (NW - 2 * H - 2);  // the output layer
   float o[2];
   linear_mode<H, 2>(W, W + 2 * H, h, o, mo, i);
   const float v = __fsub_rn(o[1], o[0]);
@@ -266,9 +343,7 @@ k_forward_new(NetDev net, const float* xyz, int64_t n_arg, float* __restrict__ p
     tnp::key_put(ps, p, v > eps);
     tnp::key_put(zs, p, fabsf(v) <= eps);
     bad |= tnp::key_test(m, p) && fabsf(v) > eps_s;
-    key_store_stream<KW>(pos, V + i, ps);
-    tnp::key_store(zero, V + i, zs);
-    tnp::pz_store(pz, V + i, ps, zs);
+    tnp::pz_store(pz, V + i, ps, zs);  // (pos / zero: views of pz)
     key_store_stream<KW>(shared, i, m);
   }
   // full lower_bound over the marks in LDS: cheaper than gathering the

@@ -12,11 +12,11 @@ int64_t skel_tiles(int64_t n);
 // the tile's lattice points as vertices (sign mode's forward input)
 int launch_skel_points(int i0, int j0, int k0, int n0, int n1, int n2, const float* marks, float* xyz,
                        hipStream_t s);
-// keys != null (2 x u64 per tile point, (pos, zero)): sign mode, else distance
+// keys != null (2 kw x u64 per tile point, (pos, zero) as pz): sign mode, else distance
 int launch_skel_edges(bool emit, int i0, int j0, int k0, int n0, int n1, int n2, int L,
                       const float* dist, const uint64_t* keys, float dmax, const unsigned int* gmax_bits,
                       int32_t* blk, const int64_t* blkoff, int64_t out_base, int32_t* out, int32_t* used,
-                      hipStream_t s);
+                      hipStream_t s, int kw = 1);
 // per-axis, per-mark-plane counts of the tile's points under its edge
 // threshold (the sharded skeleton's load balance), added into load[3][L]
 int launch_skel_load(int i0, int j0, int k0, int n0, int n1, int n2, int L, const float* dist, float dmax,

@@ -33,6 +33,7 @@ constexpr int TILE = TNP_BLOCK * IPT;
 struct TileGeom {
   int i0, j0, k0, n0, n1, n2, L;
   int64_t nx, ny, nz;
+  int kw;  // sign mode: sign-key words (the keys are (pos, zero) pairs of kw words each)
 };
 
 // the tile's lattice points as vertices (marks * 2 - 1, preprocess_inverse)
@@ -67,8 +68,12 @@ __device__ __forceinline__ bool skel_edge(const TileGeom& g, const float* dist, 
   lo = (int)((g.i0 + a0) * LL + (int64_t)(g.j0 + a1) * g.L + (g.k0 + a2));
   hi = (int)((g.i0 + b0) * LL + (int64_t)(g.j0 + b1) * g.L + (g.k0 + b2));
   if (keys) {
-    const ulonglong2 ka = keys[ia], kb = keys[ib];
-    return ka.x != kb.x || ka.y != kb.y;
+    bool d = false;
+    for (int q = 0; q < g.kw; ++q) {  // the point's kw (pos, zero) word pairs (common.h pz_store)
+      const ulonglong2 ka = keys[g.kw * ia + q], kb = keys[g.kw * ib + q];
+      d |= ka.x != kb.x || ka.y != kb.y;
+    }
+    return d;
   }
   return (dist[ib] <= thr) && (dist[ia] <= thr);
 }
@@ -197,7 +202,7 @@ int64_t skel_tiles(int64_t n) { return (n + TILE - 1) / TILE; }
 
 static TileGeom geom(int i0, int j0, int k0, int n0, int n1, int n2, int L) {
   TileGeom g{i0, j0, k0, n0, n1, n2, L, (int64_t)(n0 - 1) * n1 * n2,
-             (int64_t)n0 * (n1 - 1) * n2, (int64_t)n0 * n1 * (n2 - 1)};
+             (int64_t)n0 * (n1 - 1) * n2, (int64_t)n0 * n1 * (n2 - 1), 1};
   return g;
 }
 
@@ -214,8 +219,9 @@ int launch_skel_points(int i0, int j0, int k0, int n0, int n1, int n2, const flo
 int launch_skel_edges(bool emit, int i0, int j0, int k0, int n0, int n1, int n2, int L,
                       const float* dist, const uint64_t* keys, float dmax, const unsigned int* gmax_bits,
                       int32_t* blk, const int64_t* blkoff, int64_t out_base, int32_t* out, int32_t* used,
-                      hipStream_t s) {
+                      hipStream_t s, int kw) {
   TileGeom g = geom(i0, j0, k0, n0, n1, n2, L);
+  g.kw = kw;
   int64_t N = g.nx + g.ny + g.nz;
   if (N <= 0) return 0;
   const ulonglong2* k2 = reinterpret_cast<const ulonglong2*>(keys);

@@ -237,7 +237,7 @@ __global__ void k_fail_check(const int32_t* __restrict__ sa, const int32_t* __re
   int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   bool bad = false;
   if (r < S) {
-    const Key<KW> m = (tnp::key_load<KW>(zero, sa[r]) & tnp::key_load<KW>(zero, sb[r]) & tnp::key_below<KW>(idx)) |
+    const Key<KW> m = (tnp::vkey_load<KW>(zero, sa[r]) & tnp::vkey_load<KW>(zero, sb[r]) & tnp::key_below<KW>(idx)) |
                       tnp::key_bit<KW>(idx);
     tnp::key_store(shared, r, m);
 #pragma unroll
@@ -272,9 +272,7 @@ __global__ void k_finalize_new(int64_t S, int K, int override_, const uint64_t* 
     tnp::key_put(zs, p, fabsf(v) <= eps);
     if (p >= keep_from) pre[(int64_t)p * ld + V + r] = v;
   }
-  tnp::key_store(pos, V + r, ps);
-  tnp::key_store(zero, V + r, zs);
-  tnp::pz_store(pz, V + r, ps, zs);
+  tnp::pz_store(pz, V + r, ps, zs);  // (pos / zero: views of pz)
 }
 
 // ---------------------------------------------------------------------------
@@ -419,7 +417,7 @@ k_span_count(const int32_t* __restrict__ members, int64_t S, int64_t Mcap,
     int v = members[m];
     int lo[3], n[3];
     cnt[m] = span_cells(grid[v], lo, n);
-    const int kz = tnp::key_pop(tnp::key_load<KW>(zero, v) & tnp::key_below<KW>(idx)) + (n[0] - 1) + (n[1] - 1) +
+    const int kz = tnp::key_pop(tnp::vkey_load<KW>(zero, v) & tnp::key_below<KW>(idx)) + (n[0] - 1) + (n[1] - 1) +
                    (n[2] - 1);
     aug = 1ll << kz;
     k0 = kz == 0;
@@ -934,8 +932,8 @@ __device__ __forceinline__ void fetch_edge(const EdgeSrc& s, int64_t i, int& a, 
 template <int KW>
 __device__ __forceinline__ bool keep_edge(int a, int b, const Key<KW>& fmask, const uint64_t* pos,
                                           const uint64_t* zero) {
-  return tnp::key_any(((tnp::key_load<KW>(pos, a) ^ tnp::key_load<KW>(pos, b)) |
-                       (tnp::key_load<KW>(zero, a) ^ tnp::key_load<KW>(zero, b))) & fmask);
+  return tnp::key_any(((tnp::vkey_load<KW>(pos, a) ^ tnp::vkey_load<KW>(pos, b)) |
+                       (tnp::vkey_load<KW>(zero, a) ^ tnp::vkey_load<KW>(zero, b))) & fmask);
 }
 
 
@@ -977,8 +975,8 @@ k_prune_emit(EdgeSrc src, int64_t N, Key<KW> fmask, Key<KW> amask,
         used[a] = 1;
         used[b] = 1;
       }
-      const Key<KW> za = tnp::key_load<KW>(zero, a), zb = tnp::key_load<KW>(zero, b);
-      act |= act_word((tnp::key_load<KW>(pos, a) ^ tnp::key_load<KW>(pos, b)) & ~za & ~zb & amask);
+      const Key<KW> za = tnp::vkey_load<KW>(zero, a), zb = tnp::vkey_load<KW>(zero, b);
+      act |= act_word((tnp::vkey_load<KW>(pos, a) ^ tnp::vkey_load<KW>(pos, b)) & ~za & ~zb & amask);
     }
   }
   act = tnp::wave_or(act);
@@ -1377,10 +1375,8 @@ __global__ void k_gather_vertices(const int32_t* __restrict__ used, const int64_
 #pragma unroll
   for (int d = 0; d < 3; ++d) xyz2[3 * n + d] = xyz[3 * v + d];
   for (int p = keep_from; p < K; ++p) pre2[(int64_t)p * ld2 + n] = pre[(int64_t)p * ld + v];
-  const Key<KW> p = tnp::key_load<KW>(pos, v), z = tnp::key_load<KW>(zero, v);
-  tnp::key_store(pos2, n, p);
-  tnp::key_store(zero2, n, z);
-  tnp::pz_store(pz2, n, p, z);
+  const Key<KW> p = tnp::vkey_load<KW>(pos, v), z = tnp::vkey_load<KW>(zero, v);
+  tnp::pz_store(pz2, n, p, z);  // (pos2 / zero2: views of pz2)
   grid2[n] = grid[v];
 }
 

@@ -155,6 +155,14 @@ class Engine:
                    "tnp_engine_scratch_bytes")
         return {"bytes": b.value, "buffers": n.value, "key_bytes": k.value}
 
+    def vertex_capacity(self) -> dict:
+        """(debug) the vertex set's row capacity and the steps whose split
+        count exceeded the early forward's row bound (forward run again)."""
+        r, x = C.c_int64(), C.c_int64()
+        _hip.check(_hip.lib().tnp_engine_debug_vertex_capacity(self.h, C.byref(r), C.byref(x)),
+                   "tnp_engine_debug_vertex_capacity")
+        return {"rows": r.value, "early_redo": x.value}
+
     def export(self, pre: bool = False, edges: bool = True):
         """(vertices [V, 3], edges [E, 2] int64 or None when edges=False,
         cache [V, K] when pre) of the compacted complex."""

@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import sys
 
 import torch  # noqa: F401  (must load before the HIP library)
 
@@ -105,6 +106,7 @@ SIGNATURES = {
     "tnp_engine_debug_set_lb_spin": (C.c_int, [_VP, C.c_int]),
     "tnp_debug_buf_growth": (C.c_int, [C.c_int64, C.c_int64, C.c_int64, C.c_int, _P64, _P64]),
     "tnp_engine_debug_set_lds_records": (C.c_int, [_VP, C.c_int]),
+    "tnp_engine_debug_vertex_capacity": (C.c_int, [_VP, _P64, _P64]),
     "tnp_engine_debug_lb_recomputes": (C.c_int, [_VP, _P64, C.c_int, _VP]),
     "tnp_engine_kernel_timer": (C.c_int, [_VP, C.c_int, _VP, _P32]),
     "tnp_mc_count": (C.c_int, [_VP, C.c_int, C.c_int, C.c_int, _F, _VP, _VP, _VP, _P64, _P64, _VP]),
@@ -136,6 +138,13 @@ def lib():
         # points left unbound.  Never the default: the product loads only a
         # library built from this tree's sources.
         any_build = os.environ.get("TNP_LIB_ANY_BUILD") == "1" and "TNP_LIB" in os.environ
+        if any_build:
+            import warnings
+            warnings.warn(f"TNP_LIB_ANY_BUILD=1: loading {_LIB_PATH} without the build-id check "
+                          "(timing experiments only; missing entry points stay unbound)", RuntimeWarning,
+                          stacklevel=2)
+            print(f"[tropical] TNP_LIB_ANY_BUILD=1: {os.path.basename(_LIB_PATH)} loaded without the "
+                  "build-id check", file=sys.stderr, flush=True)
         for name, (res, args) in SIGNATURES.items():
             if any_build and not hasattr(L, name):
                 continue
