@@ -201,9 +201,24 @@ def cpu_baseline(G: int, seed: int, threads: int):
         log(f"CPU baseline: step {done[0]}: {V.shape[0]} vertices, {E.shape[0]} edges, "
             f"{time.perf_counter() - t0:.1f} s")
 
+    # and a heartbeat inside a long step (64^3: one oracle step runs for
+    # minutes on the box's 16-core share)
+    import threading
+    stop = threading.Event()
+
+    def heartbeat():
+        while not stop.wait(30.0):
+            log(f"CPU baseline: step {done[0] + 1} running, {time.perf_counter() - t0:.0f} s")
+
     t0 = time.perf_counter()
-    with torch.no_grad():
-        od.run_steps(V, E, ref, 1e-4, None, stats, on_step=progress)
+    hb = threading.Thread(target=heartbeat, daemon=True)
+    hb.start()
+    try:
+        with torch.no_grad():
+            od.run_steps(V, E, ref, 1e-4, None, stats, on_step=progress)
+    finally:
+        stop.set()
+        hb.join()
     dt = time.perf_counter() - t0
     S = sum(s["S"] for s in stats["steps"])
     return S / dt, S, dt
@@ -344,10 +359,17 @@ def small_net_check(dev, force: bool = True):
     kt = eng.kernel_timer(False)
     nl = int(sum(x["launches"] for x in kt.values()))
     kms = float(sum(x["ms"] for x in kt.values()))
+    # the hyperplane loop alone (the finish -- surface, export, and since
+    # round 6 the faces kernels, on the timer too -- counted apart)
+    fin = ("faces_", "surface", "gather_vertices", "remap_edges", "scan", "skel")
+    loop = {k: v for k, v in kt.items() if not k.startswith(fin)}
+    nll = int(sum(x["launches"] for x in loop.values()))
     out.update({"active_steps": len(stats), "timed_launches": nl,
+                "loop_launches_per_step": round(nll / max(len(stats), 1), 1),
                 "launches_per_step": round(nl / max(len(stats), 1), 1),
                 "us_per_launch": round(kms * 1e3 / max(nl, 1), 2),
-                "kernel_ms_total": round(kms, 3)})
+                "kernel_ms_total": round(kms, 3),
+                "loop_kernel_ms": round(float(sum(x["ms"] for x in loop.values())), 3)})
     v = verts.cpu().numpy()
     out["chamfer_l2_vs_ref"] = chamfer(v, rv)
     out["faces_bit_exact"] = bool(np.array_equal(np.asarray(tri), np.asarray(rtri)))

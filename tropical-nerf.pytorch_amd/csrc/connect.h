@@ -95,7 +95,7 @@ __device__ __forceinline__ void add_pair_stats(int64_t a, int64_t r, int64_t x, 
 // buffer, one global append per WKEYS.
 // ---------------------------------------------------------------------------
 #ifndef TNP_WKEYS
-#define TNP_WKEYS 384
+#define TNP_WKEYS 256  // (round 6: 384 -> 256, its LDS to the 1,024-test table; bucket_group -1 %)
 #endif
 constexpr int WKEYS = TNP_WKEYS;
 
@@ -104,7 +104,10 @@ __device__ __forceinline__ void lds_fence() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
-constexpr int WOWN = 512;  // tests of one window resolved by table (more: binary search)
+#ifndef TNP_WOWN
+#define TNP_WOWN 1024  // >= the most tests a window of cells <= WCELL members holds: no search
+#endif
+constexpr int WOWN = TNP_WOWN;  // tests of one window resolved by table (more: binary search)
 
 // st last: the grouping kernel's LDS-record path lays its record chunk over
 // st and the space behind it (bucket.hip k_bucket_group)

@@ -220,6 +220,19 @@ struct tnp_engine {
   // and the shared-plane words keep whatever capacity the bound asks for
   int64_t max_split_seen = 0;
   int64_t n_early_redo = 0;  // steps whose S exceeded the early bound (forward run again)
+  // side stream: the lazy prune of the old edges and e_new runs there, beside
+  // the grouping kernel and the connect on the caller's stream (finish);
+  // ev_s2[0]: the caller's stream reached the prune's inputs, ev_s2[1]: the
+  // prune is done (the caller's stream waits on it before anything touches
+  // the edge slots again: side_join)
+  hipStream_t s2 = nullptr;
+  hipEvent_t ev_s2[2] = {nullptr, nullptr};
+  bool s2_pending = false;
+  // TNP_SIDE_PRUNE=1 at creation: part A on the side stream.  Off: measured
+  // no faster (profiles/r06_ab_side_prune.jsonl: 3.71-3.75 ms per 128^3 pass
+  // either way -- the two kernels slow each other down as much as they
+  // overlap: bucket_group 0.80 -> 1.08 ms, the prune 0.63 -> 1.03 ms)
+  bool side_prune = false;
   bool early_bound_splits = true;  // TNP_EARLY_BOUND=0 at creation: the edge-slot bound E (round 5, A/B)
   int64_t pend_lz_n = 0;              // lzpart entries holding E_live (0: E_live is known)
   tnp_step_stats* pend_st = nullptr;  // the step whose V_out / E_out wait for them
@@ -636,6 +649,7 @@ extern "C" int tnp_engine_create(tnp_engine** out, int device) {
   if (const char* dc = getenv("TNP_DEFER_COUNTS")) e->defer_ok = atoi(dc) != 0;
   if (const char* ef = getenv("TNP_EARLY_FWD")) e->early_forward = atoi(ef) != 0;
   if (const char* eb = getenv("TNP_EARLY_BOUND")) e->early_bound_splits = atoi(eb) != 0;
+  if (const char* sp = getenv("TNP_SIDE_PRUNE")) e->side_prune = atoi(sp) != 0;
   if (hipHostMalloc((void**)&e->h_ctr, CTR_N * sizeof(int64_t), hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc((void**)&e->h_map, 32 * sizeof(int64_t), hipHostMallocMapped | hipHostMallocCoherent) !=
           hipSuccess ||
@@ -676,6 +690,9 @@ extern "C" void tnp_engine_destroy(tnp_engine* e) {
   if (!e) return;
   (void)hipSetDevice(e->device);
   (void)hipDeviceSynchronize();
+  if (e->s2) (void)hipStreamDestroy(e->s2);
+  for (hipEvent_t ev : e->ev_s2)
+    if (ev) (void)hipEventDestroy(ev);
   hipStream_t s = 0;
   for_each_buf(e, [&](Buf& b) { buf_free(b, s); });
   (void)hipDeviceSynchronize();
@@ -1232,11 +1249,12 @@ static int flat_forward_new(tnp_engine* e, int idx, int64_t n, hipStream_t s) {
   e->pend_keep = new_keep_from(e, idx);
   // compulsory bytes per split: reads 8 B endpoint ids, 24 B endpoint
   // coordinates, 8 B endpoint plane values, 16 B endpoint zero keys; writes
-  // 12 B coordinates, the cache planes >= keep_from, 48 B keys (pos, zero,
-  // pz, grid, shared); plus the encoding tables once per launch (the 8
+  // 12 B coordinates, the cache planes >= keep_from, 32 B keys (pz: pos and
+  // zero, the only copy since round 6; grid; shared); plus the encoding
+  // tables once per launch (the 8
   // corners x L levels gathers are cache traffic).  (n < 0: set once S is known)
   TIMED("forward_new",
-        (8.0 + 24.0 + 8.0 + 16.0 + 12.0 + 4.0 * (e->K - e->pend_keep) + 48.0) * std::max<int64_t>(n, 0) +
+        (8.0 + 24.0 + 8.0 + 16.0 + 12.0 + 4.0 * (e->K - e->pend_keep) + 32.0) * std::max<int64_t>(n, 0) +
             table_bytes(e->net),
         launch_forward_new(e->net, P<float>(e->cur.xyz) + 3 * e->V, n, P<float>(e->cur.pre), e->cur.cap, e->V,
                            e->pend_keep, P<int32_t>(e->sa), P<int32_t>(e->sb), idx, e->own,
@@ -1368,7 +1386,7 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
     if (e->pend_fused) {
       if (early_fwd)  // (launched behind the split; its modelled bytes now)
         ktimer_set_bytes(e, "forward_new",
-                         (8.0 + 24.0 + 8.0 + 16.0 + 12.0 + 4.0 * (e->K - e->pend_keep) + 48.0) * S +
+                         (8.0 + 24.0 + 8.0 + 16.0 + 12.0 + 4.0 * (e->K - e->pend_keep) + 32.0) * S +
                              table_bytes(e->net));
       else if (flat_forward_new(e, idx, S, s))
         return -1;
@@ -1417,6 +1435,27 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
   return 0;
 }
 
+// the side stream (created on first use, non-blocking: no implicit sync
+// with the caller's stream) and its two events
+static int side_stream(tnp_engine* e) {
+  if (e->s2) return 0;
+  TNP_CHECK(hipStreamCreateWithFlags(&e->s2, hipStreamNonBlocking));
+  for (hipEvent_t& ev : e->ev_s2) TNP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  return 0;
+}
+// the caller's stream waits for the side stream's prune (every exit of a
+// finish that launched one, errors included)
+static void side_join(tnp_engine* e, hipStream_t s) {
+  if (!e->s2_pending) return;
+  (void)hipStreamWaitEvent(s, e->ev_s2[1], 0);
+  e->s2_pending = false;
+}
+struct SideJoin {
+  tnp_engine* e;
+  hipStream_t s;
+  ~SideJoin() { side_join(e, s); }
+};
+
 extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override_, void* stream,
                                  tnp_step_stats* st) {
   hipStream_t s = (hipStream_t)stream;
@@ -1429,6 +1468,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   }
   e->pend_idx = -1;
   e->valid = false;  // until this step has completed
+  const SideJoin side_guard{e, s};
   const bool hits_done = e->pend_hits;
   const int64_t hoff = hits_done ? e->pend_hoff : -1;
   e->pend_hits = false;
@@ -1633,6 +1673,36 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
   // c_new after the sort (part A's workgroup parts first in lzpart)
   const bool early_prune = lazy && buckets && e->early_forward && !eps2(e) && !e->curve && e->masks_valid;
   int part_a = 0;
+  const int64_t ES = E + S;
+  // part A (slots [0, E + S)) reads the edge slots, their bytes, the keys of
+  // the new vertices (forward_new; their override came with the bucket
+  // count) and writes the slots' bytes, e_new and the live flags the bucket
+  // count zeroed -- nothing the grouping, the connect, the key sort or their
+  // counters touch.  So it runs on the side stream from here, beside them
+  // (the grouping kernel issue-bound, the prune memory-bound), and the
+  // caller's stream waits for it before the pruning of c_new (side_join)
+  const bool side = early_prune && e->side_prune;
+  if (early_prune) {
+    if (buf_ensure(e->live, std::max<int64_t>(NV + 4, 16), s)) return -1;  // (+4: word atomics)
+    if (buf_ensure(e->edges, std::max<int64_t>(ES, 1) * 2 * sizeof(int32_t), s, true)) return -1;
+    if (buf_ensure(e->edm, std::max<int64_t>(ES, 1) * sizeof(uint8_t), s, true)) return -1;
+    if (buf_ensure(e->eef, std::max<int64_t>(ES, 1) * sizeof(uint8_t), s, true)) return -1;
+    part_a = prune_lazy_blocks(ES);
+    if (buf_ensure(e->lzpart, part_a * sizeof(int64_t), s)) return -1;
+  }
+  if (side) {
+    if (side_stream(e)) return -1;
+    TNP_CHECK(hipEventRecord(e->ev_s2[0], s));
+    TNP_CHECK(hipStreamWaitEvent(e->s2, e->ev_s2[0], 0));
+    const int t = ktimer_begin(e, "prune", 1.0 * E + 36.0 * S, e->s2);
+    if (launch_prune_lazy(P<int32_t>(e->edges), E, P<int32_t>(e->sb), S, V, nullptr, nb, 0, idx, K - 1,
+                          P<uint64_t>(c.pz), P<uint8_t>(e->edm), P<uint8_t>(e->eef), P<uint8_t>(e->live),
+                          P<int64_t>(e->lzpart), ctr, e->s2, 0, ES))
+      return -1;
+    ktimer_end(e, t, e->s2);
+    TNP_CHECK(hipEventRecord(e->ev_s2[1], e->s2));
+    e->s2_pending = true;
+  }
   for (int attempt = 0; attempt < 3; ++attempt) {
     if (buf_ensure(e->ckeys_a, std::max<int64_t>(cap, 1) * sizeof(uint64_t), s)) return -1;
     if (attempt > 0) {  // the split zeroed the whole counter block
@@ -1681,14 +1751,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     }
     int64_t seq = 0;
     if (post_ctr(e, s, &seq)) return -1;
-    if (early_prune && attempt == 0) {  // (a redone connect leaves part A as it is)
-      const int64_t ES = E + S;
-      if (buf_ensure(e->live, std::max<int64_t>(NV + 4, 16), s)) return -1;  // (+4: word atomics)
-      if (buf_ensure(e->edges, std::max<int64_t>(ES, 1) * 2 * sizeof(int32_t), s, true)) return -1;
-      if (buf_ensure(e->edm, std::max<int64_t>(ES, 1) * sizeof(uint8_t), s, true)) return -1;
-      if (buf_ensure(e->eef, std::max<int64_t>(ES, 1) * sizeof(uint8_t), s, true)) return -1;
-      part_a = prune_lazy_blocks(ES);
-      if (buf_ensure(e->lzpart, part_a * sizeof(int64_t), s)) return -1;
+    if (early_prune && attempt == 0 && !side) {  // (a redone connect leaves part A as it is)
       TIMED("prune", 1.0 * E + 36.0 * S,
             launch_prune_lazy(P<int32_t>(e->edges), E, P<int32_t>(e->sb), S, V, nullptr, nb, 0, idx, K - 1,
                               P<uint64_t>(c.pz), P<uint8_t>(e->edm), P<uint8_t>(e->eef), P<uint8_t>(e->live),
@@ -1766,7 +1829,9 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
           sort_keys_u64(kin, kalt, X, 2 * nb, e->sort_scr.p, e->sort_scr.bytes, &e->ckeys, s));
   }
 
-  // 5. pruning over [edges; e_new; c_new] + vertex compaction
+  // 5. pruning over [edges; e_new; c_new] + vertex compaction (after the side
+  // stream's part A: everything below may move or read the edge slots)
+  side_join(e, s);
   const int64_t N = E + S + X;
   int64_t nt = step_tiles(N);
   if (buf_ensure(e->blk, (nt + 1) * sizeof(int32_t), s)) return -1;
@@ -2455,7 +2520,8 @@ extern "C" int tnp_engine_faces(tnp_engine* e, void* stream, int64_t* n_tri, int
   }
   TNP_CHECK(hipMemsetAsync(ctr, 0, CTR_CLEAR_BYTES, s));
   // F1: augmented-row count and region hash table
-  if (launch_face_count(V, grid, pos, zero, K, ctr + CTR_AUX - 1, s)) return -1;
+  TIMED("faces_count", 24.0 * V,
+        launch_face_count(V, grid, pos, zero, K, ctr + CTR_AUX - 1, s));
   if (read_ctr(e, s)) return -1;
   const int64_t A = e->h_ctr[CTR_AUX - 1];
   if (e->h_ctr[CTR_AUX] > 30) { tnp_set_error("faces: a vertex lies on %lld planes", (long long)e->h_ctr[CTR_AUX]); return -1; }
@@ -2481,16 +2547,18 @@ extern "C" int tnp_engine_faces(tnp_engine* e, void* stream, int64_t* n_tri, int
                          {fs[FS_CUR].p, (uint64_t)cap * 4, 0}};
     if (launch_fill(f, 4, s)) return -1;
   }
-  if (launch_face_insert(V, grid, pos, zero, K, P<uint64_t>(fs[FS_TABLE]), (uint64_t)cap - 1,
-                         P<int32_t>(fs[FS_CNT]), s))
-    return -1;
-  if (launch_keep_counts(P<int32_t>(fs[FS_CNT]), cap, P<int32_t>(fs[FS_KC]), P<int32_t>(fs[FS_KF]), s)) return -1;
+  TIMED("faces_insert", 24.0 * V + 16.0 * cap,
+        launch_face_insert(V, grid, pos, zero, K, P<uint64_t>(fs[FS_TABLE]), (uint64_t)cap - 1,
+                         P<int32_t>(fs[FS_CNT]), s));
+  TIMED("faces_keep_counts", 12.0 * cap,
+        launch_keep_counts(P<int32_t>(fs[FS_CNT]), cap, P<int32_t>(fs[FS_KC]), P<int32_t>(fs[FS_KF]), s));
   // padded width of r_idx_as_tensor = the largest region over ALL regions
   {
     const FillOp f{ctr + CTR_COMPAT, sizeof(int64_t), 0};
     if (launch_fill(&f, 1, s)) return -1;
   }
-  if (launch_max_i32(P<int32_t>(fs[FS_CNT]), cap, ctr + CTR_COMPAT, s)) return -1;
+  TIMED("faces_width", 4.0 * cap,
+        launch_max_i32(P<int32_t>(fs[FS_CNT]), cap, ctr + CTR_COMPAT, s));
   if (scan_counts(e, P<int32_t>(fs[FS_KC]), P<int64_t>(fs[FS_MEMOFF]), cap, CTR_T, s)) return -1;
   if (scan_counts(e, P<int32_t>(fs[FS_KF]), P<int64_t>(fs[FS_RID]), cap, CTR_X, s)) return -1;
   if (read_ctr(e, s)) return -1;
@@ -2505,14 +2573,14 @@ extern "C" int tnp_engine_faces(tnp_engine* e, void* stream, int64_t* n_tri, int
   if (buf_ensure(fs[FS_MEM], Mtot * 8, s) || buf_ensure(fs[FS_ROFF], R * 8, s) ||
       buf_ensure(fs[FS_RCNT], R * 4, s))
     return -1;
-  if (launch_face_scatter(V, grid, pos, zero, K, P<uint64_t>(fs[FS_TABLE]), (uint64_t)cap - 1,
+  TIMED("faces_scatter", 24.0 * V + 8.0 * Mtot,
+        launch_face_scatter(V, grid, pos, zero, K, P<uint64_t>(fs[FS_TABLE]), (uint64_t)cap - 1,
                           P<int32_t>(fs[FS_CNT]), P<int64_t>(fs[FS_MEMOFF]), P<int32_t>(fs[FS_CUR]),
-                          P<uint64_t>(fs[FS_MEM]), s))
-    return -1;
-  if (launch_region_finalize(cap, P<int32_t>(fs[FS_KF]), P<int64_t>(fs[FS_RID]), P<int32_t>(fs[FS_CNT]),
+                          P<uint64_t>(fs[FS_MEM]), s));
+  TIMED("faces_regions", 16.0 * cap + 12.0 * R,
+        launch_region_finalize(cap, P<int32_t>(fs[FS_KF]), P<int64_t>(fs[FS_RID]), P<int32_t>(fs[FS_CNT]),
                              P<int64_t>(fs[FS_MEMOFF]), P<uint64_t>(fs[FS_MEM]), P<int64_t>(fs[FS_ROFF]),
-                             P<int32_t>(fs[FS_RCNT]), s))
-    return -1;
+                             P<int32_t>(fs[FS_RCNT]), s));
   // F3: lexicographic row order + unique
   if (buf_ensure(fs[FS_BCNT], V * 4, s) || buf_ensure(fs[FS_BOFF], V * 8, s) ||
       buf_ensure(fs[FS_BCUR], V * 4, s) || buf_ensure(fs[FS_ROWS], R * 4, s) ||
@@ -2525,15 +2593,15 @@ extern "C" int tnp_engine_faces(tnp_engine* e, void* stream, int64_t* n_tri, int
   const uint64_t* mem = P<uint64_t>(fs[FS_MEM]);
   const int64_t* roff = P<int64_t>(fs[FS_ROFF]);
   const int32_t* rcnt = P<int32_t>(fs[FS_RCNT]);
-  if (launch_row_buckets(R, V, mem, roff, rcnt, P<int32_t>(fs[FS_BCNT]), nullptr, nullptr, nullptr, nullptr, 0, s))
-    return -1;
+  TIMED("faces_row_count", 8.0 * Mtot + 12.0 * R,
+        launch_row_buckets(R, V, mem, roff, rcnt, P<int32_t>(fs[FS_BCNT]), nullptr, nullptr, nullptr, nullptr, 0, s));
   if (scan_counts(e, P<int32_t>(fs[FS_BCNT]), P<int64_t>(fs[FS_BOFF]), V, CTR_AUX, s)) return -1;
-  if (launch_row_buckets(R, V, mem, roff, rcnt, nullptr, P<int64_t>(fs[FS_BOFF]), P<int32_t>(fs[FS_BCUR]),
-                         P<int32_t>(fs[FS_ROWS]), nullptr, 1, s))
-    return -1;
-  if (launch_row_buckets(R, V, mem, roff, rcnt, P<int32_t>(fs[FS_BCNT]), P<int64_t>(fs[FS_BOFF]), nullptr,
-                         P<int32_t>(fs[FS_ROWS]), P<int32_t>(fs[FS_KEEP]), 2, s))
-    return -1;
+  TIMED("faces_row_place", 8.0 * Mtot + 16.0 * R,
+        launch_row_buckets(R, V, mem, roff, rcnt, nullptr, P<int64_t>(fs[FS_BOFF]), P<int32_t>(fs[FS_BCUR]),
+                         P<int32_t>(fs[FS_ROWS]), nullptr, 1, s));
+  TIMED("faces_row_unique", 8.0 * Mtot + 16.0 * R,
+        launch_row_buckets(R, V, mem, roff, rcnt, P<int32_t>(fs[FS_BCNT]), P<int64_t>(fs[FS_BOFF]), nullptr,
+                         P<int32_t>(fs[FS_ROWS]), P<int32_t>(fs[FS_KEEP]), 2, s));
   if (scan_counts(e, P<int32_t>(fs[FS_KEEP]), P<int64_t>(fs[FS_KOFF]), R, CTR_E, s)) return -1;
   if (read_ctr(e, s)) return -1;
   const int64_t F = e->h_ctr[CTR_E];
@@ -2542,25 +2610,27 @@ extern "C" int tnp_engine_faces(tnp_engine* e, void* stream, int64_t* n_tri, int
       buf_ensure(fs[FS_KEY], row_order_scratch(F, width), s) || buf_ensure(fs[FS_ORDV], Mtot * 4, s) ||
       buf_ensure(fs[FS_CALL], F * 4, s) || buf_ensure(fs[FS_CNZ], F * 4, s))
     return -1;
-  if (launch_compact_rows(R, P<int32_t>(fs[FS_KEEP]), P<int64_t>(fs[FS_KOFF]), P<int32_t>(fs[FS_ROWS]),
-                          P<int32_t>(fs[FS_FROW]), s))
-    return -1;
+  TIMED("faces_compact_rows", 16.0 * R,
+        launch_compact_rows(R, P<int32_t>(fs[FS_KEEP]), P<int64_t>(fs[FS_KOFF]), P<int32_t>(fs[FS_ROWS]),
+                          P<int32_t>(fs[FS_FROW]), s));
   const int32_t* frow = P<int32_t>(fs[FS_FROW]);
   e->dbg_F = F;
   e->dbg_W = width;
   // F4: normals at the row means, angular order
-  if (launch_row_mean(F, frow, mem, roff, rcnt, width, xyz, P<float>(fs[FS_MEAN]), s)) return -1;
-  if (launch_sdf_grad(e->net, P<float>(fs[FS_MEAN]), F, P<float>(fs[FS_SDF]), P<float>(fs[FS_NRM]), s)) return -1;
-  if (launch_row_order(F, frow, mem, roff, rcnt, width, xyz, P<float>(fs[FS_NRM]), F == 3 ? 1 : 0,
+  TIMED("faces_row_mean", 20.0 * Mtot + 12.0 * F,
+        launch_row_mean(F, frow, mem, roff, rcnt, width, xyz, P<float>(fs[FS_MEAN]), s));
+  TIMED("faces_normals", 28.0 * F,
+        launch_sdf_grad(e->net, P<float>(fs[FS_MEAN]), F, P<float>(fs[FS_SDF]), P<float>(fs[FS_NRM]), s));
+  TIMED("faces_row_order", 20.0 * Mtot + 12.0 * F,
+        launch_row_order(F, frow, mem, roff, rcnt, width, xyz, P<float>(fs[FS_NRM]), F == 3 ? 1 : 0,
                        fs[FS_KEY].p, P<int32_t>(fs[FS_ORDV]), P<int32_t>(fs[FS_CALL]),
-                       P<int32_t>(fs[FS_CNZ]), s))
-    return -1;
+                       P<int32_t>(fs[FS_CNZ]), s));
   {
     const FillOp f{ctr + CTR_TRI, 2 * sizeof(int64_t), 0};
     if (launch_fill(&f, 1, s)) return -1;
   }
-  if (launch_max_i32(P<int32_t>(fs[FS_CALL]), F, ctr + CTR_TRI, s, P<int32_t>(fs[FS_CNZ]), ctr + CTR_FACES))
-    return -1;
+  TIMED("faces_fan_width", 8.0 * F,
+        launch_max_i32(P<int32_t>(fs[FS_CALL]), F, ctr + CTR_TRI, s, P<int32_t>(fs[FS_CNZ]), ctr + CTR_FACES));
   if (read_ctr(e, s)) return -1;
   // F5: fan triangles, fan-position-major
   const int64_t nb = fan_blocks(F);
@@ -2570,7 +2640,8 @@ extern "C" int tnp_engine_faces(tnp_engine* e, void* stream, int64_t* n_tri, int
     if (T <= 0) continue;
     if (buf_ensure(fs[FS_HIST], (int64_t)T * nb * 4, s) || buf_ensure(fs[FS_BASE], (int64_t)T * nb * 8, s))
       return -1;
-    if (launch_fan_hist(F, cnt, T, P<int32_t>(fs[FS_HIST]), s)) return -1;
+    TIMED("faces_fan_hist", 4.0 * F,
+        launch_fan_hist(F, cnt, T, P<int32_t>(fs[FS_HIST]), s));
     if (scan_counts(e, P<int32_t>(fs[FS_HIST]), P<int64_t>(fs[FS_BASE]), (int64_t)T * nb, CTR_AUX, s)) return -1;
     if (read_ctr(e, s)) return -1;
     int64_t n = e->h_ctr[CTR_AUX];
@@ -2581,9 +2652,9 @@ extern "C" int tnp_engine_faces(tnp_engine* e, void* stream, int64_t* n_tri, int
       if (buf_ensure(e->tri, std::max<int64_t>(n, 1) * 3 * sizeof(int64_t), s)) return -1;
       e->n_tri = n;
     }
-    if (launch_fan_emit(F, frow, P<int32_t>(fs[FS_ORDV]), roff, rcnt, cnt, T, P<int64_t>(fs[FS_BASE]), floats,
-                        xyz, P<int64_t>(e->tri), P<float>(e->faces), s))
-      return -1;
+    TIMED("faces_fan_emit", (floats ? 36.0 : 24.0) * n + 8.0 * F,
+        launch_fan_emit(F, frow, P<int32_t>(fs[FS_ORDV]), roff, rcnt, cnt, T, P<int64_t>(fs[FS_BASE]), floats,
+                        xyz, P<int64_t>(e->tri), P<float>(e->faces), s));
   }
   TNP_CHECK(hipStreamSynchronize(s));
   *n_tri = e->n_tri;

@@ -19,9 +19,10 @@
 //
 // Roofline: one new vertex costs ~200 B of table gathers (L2/MALL resident:
 // 70 kB-5 MB tables) + 12 B coords in + 4K B pre-activations out and
-// ~2 kflop -- bandwidth-bound on the K*4 B store.  The MLP (8->16->16->2) is
-// too narrow for MFMA tiles and its sequential-fma order is part of the
-// parity contract, so it runs on VALU with weights broadcast from LDS.
+// ~2 kflop -- latency-bound on its dependent gathers.  k_forward_new runs the
+// hidden layers of every >= 16-row call on v_mfma_f32_16x16x4_f32, which on
+// gfx950 is bit for bit the sequential fma chain above (net_device.h
+// mfma_layer); the small-batch schedules and the 2-output layer stay on VALU.
 #include "common.h"
 #include "kernels.h"
 #include "net_device.h"
