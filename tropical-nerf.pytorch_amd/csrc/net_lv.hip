@@ -117,7 +117,8 @@ k_forward(NetDev net, const float* __restrict__ xyz, int64_t n, float* __restric
 // before the real one, tools/fwd_shadow.py): 1 no stores (a checksum), 2
 // endpoints read coalesced (slots i, i + 1), 4 no zero-key gathers, 8 no
 // plane-value gathers, 16 no coordinate gathers, 32 no encoding; 64: the
-// real kernel (its outputs rewritten by the real launch)
+// real kernel (its outputs rewritten by the real launch); 128 the grid word
+// without the marks search (an arithmetic stand-in)
 // k_forward_new's grid: one workgroup per 256 splits (n < 0: the count on
 // the device, -n its bound)
 inline unsigned fwd_new_grid(int64_t n) { return tnp_grid(n >= 0 ? n : -n); }
@@ -349,7 +350,10 @@ k_forward_new(NetDev net, const float* xyz, int64_t n_arg, float* __restrict__ p
   // full lower_bound over the marks in LDS: cheaper than gathering the
   // endpoints' grid words to narrow it (measured at 128^3: 1.02 -> 0.90 ms
   // per pass for this kernel)
-  const uint64_t g = grid_word(mk, net.n_marks, eps, x);
+  // (EXP & 128: timing experiment -- an arithmetic stand-in for the marks search)
+  const uint64_t g = (EXP & 128) ? (uint64_t)(uint32_t)(int)(x[0] * 127.f) | ((uint64_t)(uint32_t)(int)(x[1] * 127.f) << 16) |
+                                       ((uint64_t)(uint32_t)(int)(x[2] * 127.f) << 32)
+                                 : grid_word(mk, net.n_marks, eps, x);
   if (live) grid[V + i] = g;
   // a shard's failover predicate covers the new vertices it owns: their OR
   // over the shards is the whole batch's, while a halo vertex is another
@@ -505,7 +509,7 @@ int lv_forward_new<LVC>(const NetDev& net, const float* xyz, int64_t n, float* p
 #define TNP_SHADOW_LAUNCH                                                                                      \
   switch (shadow) {                                                                                            \
     TNP_SHADOW(1) TNP_SHADOW(3) TNP_SHADOW(5) TNP_SHADOW(9) TNP_SHADOW(17) TNP_SHADOW(33) TNP_SHADOW(29)       \
-    TNP_SHADOW(61) TNP_SHADOW(64) default: break;                                                              \
+    TNP_SHADOW(61) TNP_SHADOW(64) TNP_SHADOW(192) default: break;                                              \
   }                                                                                                            \
   if (shadow) {                                                                                                \
     (void)hipEventRecord(ev[1], s);                                                                            \
