@@ -41,7 +41,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # per-kernel HBM bytes per launch from the committed rocprofv3 --pmc passes of
 # this workload (tools/pmc_session.sh + tools/pmc_table.py: 2*FETCH_SIZE +
 # WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md "HBM")
-PMC_TABLE = os.path.join(ROOT, "profiles", "r05_bench128_seed6_pmc.json")
+PMC_TABLE = os.path.join(ROOT, "profiles", "r06_bench128_seed6_pmc.json")
 # engine timer name -> device kernel symbol (profiles' short names)
 KERNEL_SYMBOL = {"forward_new": "k_forward_new", "prune": "k_prune_lb", "connect_win": "k_connect_win",
                  "bucket_group": "k_bucket_group", "split": "k_split_lb", "hits": "k_hit_lb",

@@ -298,7 +298,10 @@ k_forward_new(NetDev net, const float* xyz, int64_t n_arg, float* __restrict__ p
       }
     }
   }
-  if (!on_mfma) {
+#ifndef TNP_FWD_VALU_PATH  // 0: timing experiments only (tools/build_lv_variant.sh): no VALU layers
+#define TNP_FWD_VALU_PATH 1  // on MFMA shapes, so < 16-row batches compute nothing
+#endif
+  if (!on_mfma && (TNP_FWD_VALU_PATH || !mfma_shape<H>() || EXP != 0)) {
     // VALU: the small-batch schedules (ONE / FOLD, < 16 rows), 8-wide nets
 #pragma unroll
     for (int layer = 0; layer < NL - 1; ++layer) {
