@@ -511,3 +511,35 @@ def test_early_forward_bound_keeps_the_vertex_set_small(cuda, monkeypatch):
             assert redo[1] == redo[0] and redo[2] == redo[0], redo  # steady after the first pass
         del eng
     assert rows["1"] <= rows["0"], rows
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("run", ["2", "32"])
+def test_two_stage_key_sort_keeps_the_reference_complex(cuda, monkeypatch, run):
+    """VERDICT r05 #4 (pair_sort): the connecting-edge keys lo << nb | hi
+    sorted as the lo half (onesweep on bits [nb, 2nb)) plus one pass that
+    orders each run of equal lo by hi (sort.hip sort_keys_lex,
+    TNP_SORT_RUN=R: runs of <= R keys in the pass, longer ones one workgroup
+    each).  R = 2 sends most runs through the long-run kernel.  The order
+    must be c_new.sort(-1).unique(dim=0)'s (subpoly.py:243-244): the 128^3
+    headline complex equals the reference's bench128 fingerprint, and every
+    step's record equals the one-stage sort's."""
+    import bench
+    from tropical._engine import Engine
+    from tropical.distributed import complex_hash
+    net = bench.make_net(128, cuda, 6)
+    ref = bench.reference_fingerprint(128, 6)
+    stats = {}
+    for mode in ("0", run):
+        monkeypatch.setenv("TNP_SORT_RUN", mode)
+        eng = Engine(cuda)
+        eng.set_net(net)
+        for _ in range(2):
+            st = []
+            eng.lattice()
+            eng.run_steps(st)
+        V, E, _ = eng.export()
+        assert (V.shape[0], E.shape[0]) + complex_hash(V, E) == ref, mode
+        stats[mode] = st
+        del eng
+    assert stats["0"] == stats[run]

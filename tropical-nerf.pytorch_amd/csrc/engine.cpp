@@ -234,6 +234,9 @@ struct tnp_engine {
   // overlap: bucket_group 0.80 -> 1.08 ms, the prune 0.63 -> 1.03 ms)
   bool side_prune = false;
   bool early_bound_splits = true;  // TNP_EARLY_BOUND=0 at creation: the edge-slot bound E (round 5, A/B)
+  // the connecting-edge sort: lo half + run pass for runs of <= sort_run keys
+  // (sort.hip sort_keys_lex); 0: all 2 nb bits by onesweep.  TNP_SORT_RUN at creation
+  int sort_run = 64;
   int64_t pend_lz_n = 0;              // lzpart entries holding E_live (0: E_live is known)
   tnp_step_stats* pend_st = nullptr;  // the step whose V_out / E_out wait for them
   Buf hpart;                          // the hit workers' live counts
@@ -649,6 +652,7 @@ extern "C" int tnp_engine_create(tnp_engine** out, int device) {
   if (const char* dc = getenv("TNP_DEFER_COUNTS")) e->defer_ok = atoi(dc) != 0;
   if (const char* ef = getenv("TNP_EARLY_FWD")) e->early_forward = atoi(ef) != 0;
   if (const char* eb = getenv("TNP_EARLY_BOUND")) e->early_bound_splits = atoi(eb) != 0;
+  if (const char* sr = getenv("TNP_SORT_RUN")) e->sort_run = atoi(sr);
   if (const char* sp = getenv("TNP_SIDE_PRUNE")) e->side_prune = atoi(sp) != 0;
   if (hipHostMalloc((void**)&e->h_ctr, CTR_N * sizeof(int64_t), hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc((void**)&e->h_map, 32 * sizeof(int64_t), hipHostMallocMapped | hipHostMallocCoherent) !=
@@ -1823,10 +1827,10 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
     std::swap(kin, kalt);
   }
   {
-    size_t need = sort_scratch_bytes(X, 2 * nb);
+    size_t need = sort_lex_scratch_bytes(X, nb, e->sort_run);
     if (buf_ensure(e->sort_scr, std::max<size_t>(need, 16), s)) return -1;
     TIMED("pair_sort", 16.0 * X * ((2 * nb + 7) / 8),
-          sort_keys_u64(kin, kalt, X, 2 * nb, e->sort_scr.p, e->sort_scr.bytes, &e->ckeys, s));
+          sort_keys_lex(kin, kalt, X, nb, e->sort_run, e->sort_scr.p, e->sort_scr.bytes, &e->ckeys, s));
   }
 
   // 5. pruning over [edges; e_new; c_new] + vertex compaction (after the side

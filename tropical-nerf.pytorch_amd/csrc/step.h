@@ -383,6 +383,13 @@ int sort_pairs_u32(uint32_t* ka, uint32_t* kb, int32_t* va, int32_t* vb, int64_t
                    void* scratch, size_t scratch_bytes, uint32_t** ko, int32_t** vo, hipStream_t s);
 int sort_keys_u64(uint64_t* a, uint64_t* b, int64_t n, int bits, void* scratch, size_t scratch_bytes,
                   uint64_t** out, hipStream_t s);
+// connecting-edge keys lo << nb | hi in lexicographic order: the lo half
+// radix-sorted, then each run of equal lo ordered by hi (runs of <= R keys
+// in one pass, longer ones one workgroup each); R <= 0 or n within the merge
+// sort's range: sort_keys_u64 on all 2 nb bits
+size_t sort_lex_scratch_bytes(int64_t n, int nb, int R);
+int sort_keys_lex(uint64_t* a, uint64_t* b, int64_t n, int nb, int R, void* scratch, size_t scratch_bytes,
+                  uint64_t** out, hipStream_t s);
 // the final (non-pruning) step's edge list [edges; e_new; c_new] with
 // prune = 0 (emit must be true; the pruning steps use launch_prune_lb)
 int launch_prune(bool emit, const int32_t* edges, int64_t E, const int32_t* sb, int64_t S,
