@@ -12,6 +12,7 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout
   > gpurun_out/r6y_tests.log 2>&1 || { echo tests failed; tail -30 gpurun_out/r6y_tests.log; exit 1; }
 tail -1 gpurun_out/r6y_tests.log
 bash tools/pmc_session.sh || { echo pmc failed; exit 1; }
+cp gpurun_out/pmc_table.json profiles/r06_bench128_seed6_pmc.json  # the bench line's traffic figures from this build
 echo pmc done
 bash tools/ab_session.sh 3 r06=libtropical_hip.so r06h=libtropical_hip_r06h.so || exit 1
 timeout -k 10 600 python -u bench.py > gpurun_out/r6y_bench.json 2> gpurun_out/r6y_bench.err || { echo bench failed; tail -20 gpurun_out/r6y_bench.err; exit 1; }
