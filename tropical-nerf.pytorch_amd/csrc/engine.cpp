@@ -252,6 +252,14 @@ struct tnp_engine {
   int64_t* h_map = nullptr;  // host-mapped mirror written by k_publish ([31]: sequence)
   int64_t* h_map_dev = nullptr;
   int64_t pub_seq = 0;
+  // tnp_engine_run_steps: a step's last readback zeroes the counter words
+  // (k_publish clear), and the next split skips its memset -- one host API
+  // call less per step (hipMemsetAsync costs the host ~5-9 us, the
+  // bunny-scale loop is launch-bound, profiles/r06_small_hip_trace.txt).
+  // ctr_zero: the words are zero since the last publish; any other
+  // publish, launch into the words or engine call in between clears it
+  bool in_run = false;
+  bool ctr_zero = false;
   // pending split
   int pend_idx = -1;
   int64_t pend_S = 0, pend_dup = 0;
@@ -296,11 +304,12 @@ static_assert(CTR_N <= 32, "counter block");
 // (post_ctr enqueues the publish, wait_ctr takes it: work enqueued between
 // the two runs on the GPU while the counters travel to the host)
 static int post_ctr(tnp_engine* e, hipStream_t s, int64_t* seq_out, const int64_t* vpart = nullptr, int nv = 0,
-                    const int64_t* epart = nullptr, int ne = 0) {
+                    const int64_t* epart = nullptr, int ne = 0, bool clear = false) {
   const int64_t seq = ++e->pub_seq;
   if (vpart ? launch_publish_sums(P<int64_t>(e->ctr), e->h_map_dev, seq, vpart, nv, epart, ne, s)
-            : launch_publish(P<int64_t>(e->ctr), e->h_map_dev, seq, s))
+            : launch_publish(P<int64_t>(e->ctr), e->h_map_dev, seq, s, clear))
     return -1;
+  e->ctr_zero = clear && !vpart;
   *seq_out = seq;
   return 0;
 }
@@ -321,9 +330,9 @@ static int wait_ctr(tnp_engine* e, hipStream_t s, int64_t seq) {
   return 0;
 }
 static int read_ctr(tnp_engine* e, hipStream_t s, const int64_t* vpart = nullptr, int nv = 0,
-                    const int64_t* epart = nullptr, int ne = 0) {
+                    const int64_t* epart = nullptr, int ne = 0, bool clear = false) {
   int64_t seq = 0;
-  return post_ctr(e, s, &seq, vpart, nv, epart, ne) || wait_ctr(e, s, seq) ? -1 : 0;
+  return post_ctr(e, s, &seq, vpart, nv, epart, ne, clear) || wait_ctr(e, s, seq) ? -1 : 0;
 }
 
 // the deferred live counts arrived (V_live, E_live; E_live < 0: unchanged)
@@ -1294,7 +1303,8 @@ extern "C" int tnp_engine_split(tnp_engine* e, int idx, void* stream, int64_t* S
   const bool fused_hits = !e->curve && e->V > 0 && e->E > 0 && uses_buckets(e, &bgs);
   if (e->cnt_pending && !fused_hits && resolve_counts(e, s)) return -1;
   const bool take_counts = e->cnt_pending;
-  TNP_CHECK(hipMemsetAsync(e->ctr.p, 0, CTR_CLEAR_BYTES, s));
+  if (!(e->in_run && e->ctr_zero)) TNP_CHECK(hipMemsetAsync(e->ctr.p, 0, CTR_CLEAR_BYTES, s));
+  e->ctr_zero = false;
   if (e->E > 0) {
     // single pass; the id buffers hold the upper bound E (capacity is kept)
     if (buf_ensure(e->sa, e->E * sizeof(int32_t), s)) return -1;
@@ -1909,7 +1919,7 @@ extern "C" int tnp_engine_finish(tnp_engine* e, int idx, int prune, int override
         TIMED("count_live", 1.0 * NV, launch_count_flags(P<uint8_t>(e->live), NV, ctr, CTR_V, s));
     }
     next_valid = (e->keep_all || eps2(e)) ? 0 : std::min(idx + 1, K - 1);
-    if (read_ctr(e, s)) return -1;
+    if (read_ctr(e, s, nullptr, 0, nullptr, 0, e->in_run)) return -1;
     E2_live = (defer && lazy) ? E_live_in : e->h_ctr[CTR_E];  // (deferred: set by apply_counts)
     E2 = lazy ? N : E2_live;
     ktimer_set_bytes(e, "prune", lazy ? 1.0 * E + 36.0 * S + 40.0 * X + 9.0 * E2_live
@@ -2002,12 +2012,16 @@ extern "C" int tnp_engine_run_steps(tnp_engine* e, void* stream, tnp_step_stats*
   // every exit path below resolves the last ones
   tnp_step_stats spare{};
   auto done = [&](int rc) -> int {
+    e->in_run = false;
+    e->ctr_zero = false;
     e->defer_counts = false;
     if (resolve_counts(e, (hipStream_t)stream)) rc = -1;
     e->pend_st = nullptr;
     return rc;
   };
   e->defer_counts = e->defer_ok;
+  e->in_run = true;
+  e->ctr_zero = false;
   for (int idx = 0; idx < K; ++idx) {
     if (!tnp::act_test(mask, idx)) continue;
     int64_t S = 0;

@@ -237,7 +237,9 @@ int launch_prune_lazy(int32_t* edges, int64_t E, const int32_t* sb, int64_t S, i
                       uint8_t* used, int64_t* part, int64_t* ctr, hipStream_t s, int64_t i0, int64_t i1);
 // the counter block -> a host-mapped mirror, then the sequence word at [31]
 // (the host spins on it instead of a copy + stream synchronise)
-int launch_publish(const int64_t* ctr, int64_t* host, int64_t seq, hipStream_t s);
+// clear: the counter words are zeroed once read (the next split's reset,
+// without its memset: the run loop's last readback of a step)
+int launch_publish(int64_t* ctr, int64_t* host, int64_t seq, hipStream_t s, bool clear = false);
 // the same, publishing host[CTR_V] = sum(vpart[0..nv)) and (ne > 0)
 // host[CTR_E] = sum(epart[0..ne)) instead of the device words (the deferred
 // live counts of the previous step; the device words stay untouched)

@@ -1389,9 +1389,11 @@ __global__ void k_remap_edges(int32_t* __restrict__ edges, int64_t E, const int6
 
 // per-step counter readback: every lane stores its own word (the block is
 // tiny), the sequence word last, after a system-scope fence
-__global__ void k_publish(const int64_t* __restrict__ ctr, volatile int64_t* host, int64_t seq) {
+__global__ void k_publish(int64_t* __restrict__ ctr, volatile int64_t* host, int64_t seq, int clear) {
   const int t = threadIdx.x;
-  if (t < CTR_N) host[t] = ctr[t];
+  const int64_t v = t < 32 ? ctr[t] : 0;
+  if (t < CTR_N) host[t] = v;
+  if (clear && t < 32) ctr[t] = 0;  // (the word this lane read: program order)
   __threadfence_system();
   __syncthreads();
   if (t == 31) host[t] = seq;
@@ -1758,8 +1760,8 @@ int launch_widen_flags(const uint8_t* f, int64_t n, int32_t* out, hipStream_t s)
   TNP_CHECK(hipGetLastError());
   return 0;
 }
-int launch_publish(const int64_t* ctr, int64_t* host, int64_t seq, hipStream_t s) {
-  hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, s, ctr, host, seq);
+int launch_publish(int64_t* ctr, int64_t* host, int64_t seq, hipStream_t s, bool clear) {
+  hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, s, ctr, host, seq, clear ? 1 : 0);
   TNP_CHECK(hipGetLastError());
   return 0;
 }
