@@ -543,3 +543,32 @@ def test_two_stage_key_sort_keeps_the_reference_complex(cuda, monkeypatch, run):
         stats[mode] = st
         del eng
     assert stats["0"] == stats[run]
+
+
+@pytest.mark.timeout(300)
+def test_early_forward_footprint(cuda, monkeypatch):
+    """ADVICE r05 (medium), the footprint half: the device memory the engine
+    holds after two 128^3 passes with the early k_forward_new
+    (TNP_EARLY_FWD=1, the default, sized by the largest split count seen)
+    against the late launch (0, sized by the split count read back).  On
+    the box: 6.75 vs 6.46 GB, 15.95 M vs 14.40 M vertex rows (the bound's
+    25 % margin meets the set's 1.5x growth one step earlier;
+    profiles/r06_early_forward_footprint.log).  Pinned at <= 10 % more bytes
+    and <= 15 % more rows (round 5's edge-slot bound held ~V + E rows)."""
+    import json
+    import bench
+    from tropical._engine import Engine
+    net = bench.make_net(128, cuda, 6)
+    got = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("TNP_EARLY_FWD", mode)
+        eng = Engine(cuda)
+        eng.set_net(net)
+        for _ in range(2):
+            eng.lattice()
+            eng.run_steps([])
+        got[mode] = dict(eng.scratch_bytes(), rows=eng.vertex_capacity()["rows"])
+        del eng
+    print("footprint", json.dumps(got))
+    assert got["1"]["rows"] <= got["0"]["rows"] * 1.15, got
+    assert got["1"]["bytes"] <= got["0"]["bytes"] * 1.10, got
